@@ -1,0 +1,119 @@
+"""ctypes binding to the CPU oracle (oracle/sbr_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py — never by the product package.  See the header
+of sbr_oracle.c for what is restated and how parity is pinned.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+_HERE = Path(__file__).resolve().parent
+LIB_PATH = _HERE / "_build" / "libsbr_oracle.so"
+
+_D = ctypes.c_double
+_I64 = ctypes.c_int64
+_I32 = ctypes.c_int32
+_P = ctypes.c_void_p
+
+
+def build(force: bool = False) -> Path:
+    if force or not LIB_PATH.exists():
+        subprocess.run(["make", "-C", str(_HERE)], check=True, stdout=subprocess.DEVNULL)
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            build()
+        L = ctypes.CDLL(str(LIB_PATH))
+        L.sbro_learn_logistic.restype = _I64
+        L.sbro_learn_logistic.argtypes = [_D, _D, _D, _D, _D, _D, _I64, _P, _P, _I64, _P]
+        L.sbro_equilibrium.restype = None
+        L.sbro_equilibrium.argtypes = [_P, _P, _I64, _D, _D, _D, _D, _D, _D, _D, _I32, _P, _P, _P, _P, _P, _P, _P]
+        L.sbro_sweep_baseline.restype = ctypes.c_int
+        L.sbro_sweep_baseline.argtypes = [_P, _P, _P, _D, _P, _I64, _I64, _D, _D, _D, _I32, _I32] + [_P] * 8
+        L.sbro_apply_early_exit.restype = None
+        L.sbro_apply_early_exit.argtypes = [_I64, _I64, _I32, _P, _P, _P, _P]
+        for name in ("sbro_sweep_hetero", "sbro_solve_social"):
+            if hasattr(L, name):
+                getattr(L, name).restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+def _ptr(a: np.ndarray | None):
+    return None if a is None else a.ctypes.data_as(_P)
+
+
+EPS = float(np.finfo(np.float64).eps)
+
+
+def learn_logistic(beta, t_end, x0=1e-4, t0=0.0, rtol=EPS, atol=EPS, maxiters=100_000, cap=1 << 16):
+    t = np.empty(cap)
+    G = np.empty(cap)
+    stats = np.zeros(4, np.int64)
+    n = lib().sbro_learn_logistic(beta, t0, t_end, x0, rtol, atol, maxiters, _ptr(t), _ptr(G), cap, _ptr(stats))
+    if n < 0:
+        raise RuntimeError(f"oracle knot buffer too small ({-n} needed)")
+    return t[:n].copy(), G[:n].copy(), dict(naccept=int(stats[0]), nreject=int(stats[1]), status=int(stats[2]))
+
+
+def equilibrium(t, G, beta, eta, t_end, u, p, kappa, lam, max_iters=100, paths=False):
+    t = np.ascontiguousarray(t, np.float64)
+    G = np.ascontiguousarray(G, np.float64)
+    n = len(t)
+    res = np.zeros(5)
+    st = np.zeros(1, np.uint32)
+    it = np.zeros(1, np.int32)
+    hr_tau = np.zeros(n + 1) if paths else None
+    hr_v = np.zeros(n + 1) if paths else None
+    aw = np.zeros(n + 1) if paths else None
+    nhr = np.zeros(1, np.int64)
+    lib().sbro_equilibrium(_ptr(t), _ptr(G), n, beta, eta, t_end, u, p, kappa, lam, max_iters, _ptr(res),
+                           _ptr(st), _ptr(it), _ptr(hr_tau), _ptr(hr_v), _ptr(aw), _ptr(nhr))
+    out = dict(xi=res[0], tau_in_unc=res[1], tau_out_unc=res[2], aw_max=res[3], tol=res[4], status=int(st[0]),
+               iters=int(it[0]), n_hr=int(nhr[0]))
+    if paths:
+        k = int(nhr[0])
+        out.update(hr_tau=hr_tau[:k], hr=hr_v[:k], aw=aw[:k])
+    return out
+
+
+def sweep_baseline(beta, eta, t_end, u, p, kappa, lam, x0=1e-4, max_iters=100, nthreads=0):
+    beta = np.ascontiguousarray(beta, np.float64)
+    eta = np.ascontiguousarray(np.broadcast_to(eta, beta.shape), np.float64)
+    t_end = np.ascontiguousarray(np.broadcast_to(t_end, beta.shape), np.float64)
+    u = np.ascontiguousarray(u, np.float64)
+    nb, nu = len(beta), len(u)
+    o = {k: np.empty(nb * nu) for k in ("xi", "tau_in_unc", "tau_out_unc", "aw_max", "tol")}
+    o["status"] = np.empty(nb * nu, np.uint32)
+    o["iters"] = np.empty(nb * nu, np.int32)
+    nk = np.empty(nb, np.int64)
+    rc = lib().sbro_sweep_baseline(_ptr(beta), _ptr(eta), _ptr(t_end), x0, _ptr(u), nb, nu, p, kappa, lam,
+                                   max_iters, nthreads, _ptr(o["xi"]), _ptr(o["tau_in_unc"]),
+                                   _ptr(o["tau_out_unc"]), _ptr(o["aw_max"]), _ptr(o["tol"]), _ptr(o["status"]),
+                                   _ptr(o["iters"]), _ptr(nk))
+    if rc != 0:
+        raise RuntimeError("oracle sweep failed")
+    out = {k: v.reshape(nb, nu) for k, v in o.items()}
+    out["n_knots"] = nk
+    return out
+
+
+def apply_early_exit(res: dict, threshold: int = 5) -> dict:
+    r = {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in res.items()}
+    nb, nu = r["xi"].shape
+    lib().sbro_apply_early_exit(nb, nu, threshold, _ptr(r["xi"]), _ptr(r["aw_max"]), _ptr(r["tol"]),
+                                _ptr(r["status"]))
+    return r

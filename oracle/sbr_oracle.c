@@ -1,0 +1,611 @@
+/*
+ * sbr_oracle.c — CPU restatement of the reference's hot path.
+ *
+ * *** TEST INFRASTRUCTURE ONLY. ***  Only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may load this library.  The product path
+ * (libsbr.so + HIP kernels) never links, loads or calls it.
+ *
+ * What it restates (file:line are into the Julia reference):
+ *   learning   src/baseline/learning.jl:41-54 (solve_SIhomogeneous),
+ *              :161-173 (compute_pdf_symbolic_baseline)
+ *   ODE solver OrdinaryDiffEq 6.102.1 AutoTsit5(Rosenbrock23()) (Manifest.toml
+ *              :1493-1497, Tsit5 1.5.0 :1679-1683) — NOT vendored in the
+ *              reference; restated from the published Tsit5 method
+ *              (Tsitouras 2011 tableau), OrdinaryDiffEq's PI controller
+ *              defaults (beta1=7/50, beta2=2/25, qmin=1/5, qmax=10,
+ *              gamma=9/10, qoldinit=1e-4), its Hairer-style initial dt and its
+ *              save_everystep knot semantics.  The AutoSwitch stiffness test
+ *              is evaluated and reported (SBR_STIFF_SWITCH) but Rosenbrock23 is
+ *              not restated: on every configured grid the test never fires.
+ *   hazard     src/baseline/solver.jl:153-185
+ *   buffers    src/baseline/solver.jl:211-264
+ *   bisection  src/baseline/solver.jl:308-376
+ *   equilibrium src/baseline/solver.jl:413-462 (+ SolvedModel :79-95)
+ *   AW path    src/baseline/solver.jl:495-532, AW_max :565
+ *   sweeps     scripts/1_baseline.jl:151-192 (Fig 4), :224-267 (Fig 5),
+ *              early-exit rule :236-244
+ *   hetero     src/extensions/heterogeneity/heterogeneity_learning.jl:49-134,
+ *              heterogeneity_solver.jl:48-144,175-210,241-293,316-375
+ *   social     src/extensions/social_learning/social_learning_dynamics.jl:58-114,
+ *              social_learning_solver.jl:63-263
+ *
+ * Parity pinning: the reference is Julia and cannot run in this container or
+ * on the GPU box.  This restatement is pinned by the
+ * known answers extracted from the reference's committed figures
+ * (tests/golden/, made by tools/extract_golden.py): Fig 3 ξ / τ_IN / AW
+ * curves, the exact Fig 4 run boundary (2718 points), the exact Fig 5 run
+ * masks at 500² and 5000², the social-learning figure.  Arithmetic below the
+ * figure precision (~1e-5) — knot positions, ulp-level rounding — is
+ * "parity unpinned" against Julia; the GPU engine is required to match this
+ * file bit for bit.
+ *
+ * Arithmetic contract shared with the HIP kernels: IEEE binary64, compiled
+ * with -ffp-contract=off; fma() appears exactly where OrdinaryDiffEq's
+ * @muladd would put a muladd; exp/log/pow come from include/sbr_detmath.h.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#include "../include/sbr_detmath.h"
+#include "../include/sbr_status.h"
+
+/* ------------------------------------------------------------------------ */
+/* Tsit5 tableau (Tsitouras 2011), as in OrdinaryDiffEqTsit5's constant cache */
+/* ------------------------------------------------------------------------ */
+static const double C1 = 0.161, C2 = 0.327, C3 = 0.9, C4 = 0.9800255409045097;
+static const double A21 = 0.161;
+static const double A31 = -0.008480655492356989, A32 = 0.335480655492357;
+static const double A41 = 2.897153057105493, A42 = -6.359448489975075, A43 = 4.3622954328695815;
+static const double A51 = 5.325864828439257, A52 = -11.748883564062828, A53 = 7.4955393428898365,
+                    A54 = -0.09249506636175525;
+static const double A61 = 5.86145544294642, A62 = -12.92096931784711, A63 = 8.159367898576159,
+                    A64 = -0.071584973281401, A65 = -0.028269050394068383;
+static const double A71 = 0.09646076681806523, A72 = 0.01, A73 = 0.4798896504144996,
+                    A74 = 1.379008574103742, A75 = -3.290069515436081, A76 = 2.324710524099774;
+static const double BT1 = -0.00178001105222577714, BT2 = -0.0008164344596567469,
+                    BT3 = 0.007880878010261995, BT4 = -0.1447110071732629,
+                    BT5 = 0.5823571654525552, BT6 = -0.45808210592918697,
+                    BT7 = 0.015151515151515152;
+static const double TSIT5_STABILITY = 3.5068469938049235;
+
+/* OrdinaryDiffEq PI-controller defaults for a 5th-order method */
+#define CTL_BETA1 0.14   /* 7//50 */
+#define CTL_BETA2 0.08   /* 2//25 */
+#define CTL_INV_QMIN 5.0 /* qmin = 1//5 */
+#define CTL_INV_QMAX 0.1 /* qmax = 10 */
+#define CTL_GAMMA 0.9
+#define CTL_QOLDMIN 1e-4
+#define AUTOSWITCH_TOL 0.9
+#define AUTOSWITCH_MAXSTIFF 10
+
+static inline double dmin(double a, double b) { return a < b ? a : b; }
+static inline double dmax(double a, double b) { return a > b ? a : b; }
+
+/* ------------------------------------------------------------------------ */
+/* growable knot arrays                                                      */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+    double* t;
+    double* x; /* n * K values, row-major [knot][group] */
+    int64_t n, cap;
+    int K;
+} knots_t;
+
+static int knots_push(knots_t* kn, double t, const double* x)
+{
+    if (kn->n == kn->cap) {
+        int64_t nc = kn->cap ? kn->cap * 2 : 1024;
+        double* nt = (double*)realloc(kn->t, (size_t)nc * sizeof(double));
+        if (!nt) return -1;
+        kn->t = nt;
+        double* nx = (double*)realloc(kn->x, (size_t)nc * kn->K * sizeof(double));
+        if (!nx) return -1;
+        kn->x = nx;
+        kn->cap = nc;
+    }
+    kn->t[kn->n] = t;
+    memcpy(kn->x + kn->n * kn->K, x, (size_t)kn->K * sizeof(double));
+    kn->n++;
+    return 0;
+}
+
+static void knots_free(knots_t* kn)
+{
+    free(kn->t);
+    free(kn->x);
+    memset(kn, 0, sizeof(*kn));
+}
+
+/* ------------------------------------------------------------------------ */
+/* Interpolations.jl 0.15.1 gridded Linear, Throw() extrapolation            */
+/* ------------------------------------------------------------------------ */
+/* searchsortedlast over t[0..n): count of elements <= x, minus 1 (−1 if none) */
+static inline int64_t ssl(const double* t, int64_t n, double x)
+{
+    int64_t lo = 0, hi = n; /* first index with t > x */
+    while (lo < hi) {
+        int64_t mid = (lo + hi) >> 1;
+        if (t[mid] <= x) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo - 1;
+}
+
+/* value at x of the piecewise-linear interpolant through (t[i], v[i*stride]).
+ * Out of [t0, t_{n-1}] (or NaN) -> sets *oob and returns NaN (BoundsError). */
+static inline double interp_s(const double* t, const double* v, int64_t stride, int64_t n, double x,
+                              int* oob)
+{
+    if (!(x >= t[0] && x <= t[n - 1])) {
+        *oob = 1;
+        return NAN;
+    }
+    int64_t j = ssl(t, n, x);
+    if (j > n - 2) j = n - 2;
+    if (j < 0) j = 0;
+    double d = (x - t[j]) / (t[j + 1] - t[j]);
+    return v[j * stride] * (1.0 - d) + v[(j + 1) * stride] * d;
+}
+#define INTERP(t, v, n, x, oob) interp_s((t), (v), 1, (n), (x), (oob))
+
+/* ------------------------------------------------------------------------ */
+/* AutoSwitch stiffness bookkeeping (OrdinaryDiffEqCore composite)           */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+    int count;
+    int switched;
+} autoswitch_t;
+
+static inline void autoswitch_update(autoswitch_t* as, double eigen_est, double dt)
+{
+    double stiffness = fabs(eigen_est * dt / TSIT5_STABILITY);
+    int is_stiff = stiffness > AUTOSWITCH_TOL; /* NaN -> false */
+    if (is_stiff) as->count = as->count < 0 ? 1 : as->count + 1;
+    else as->count = as->count > 0 ? -1 : as->count - 1;
+    if (as->count > AUTOSWITCH_MAXSTIFF) as->switched = 1;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Generic Tsit5 on an m-vector ODE with RMS error norm.                     */
+/* rhs(ctx, t, x[m], dx[m], &oob)                                            */
+/* ------------------------------------------------------------------------ */
+typedef void (*rhs_fn)(void* ctx, double t, const double* x, double* dx, int* oob);
+
+typedef struct {
+    int64_t naccept, nreject;
+    uint32_t status;
+} ode_stats_t;
+
+#define MAXK 64
+
+/* RMS norm over m components (DiffEqBase ODE_DEFAULT_NORM); |x| when m == 1 */
+static inline double rms_norm(const double* v, int m)
+{
+    if (m == 1) return fabs(v[0]);
+    double s = 0.0;
+    for (int i = 0; i < m; i++) s = s + v[i] * v[i];
+    return sqrt(s / (double)m);
+}
+
+static int tsit5_solve(rhs_fn f, void* ctx, int m, double t0, double t1, const double* x0, double rtol,
+                       double atol, int64_t maxiters, knots_t* kn, ode_stats_t* st)
+{
+    double x[MAXK], k1[MAXK], k2[MAXK], k3[MAXK], k4[MAXK], k5[MAXK], k6[MAXK], k7[MAXK];
+    double tmp[MAXK], tmp6[MAXK], u[MAXK], sk[MAXK], buf[MAXK], f1[MAXK];
+    int oob = 0;
+    memset(st, 0, sizeof(*st));
+    kn->K = m;
+    const double dtmax = t1 - t0;
+    const double dtmin = sbr_jl_eps(dmax(fabs(t0), fabs(t1)));
+
+    /* ---- ode_determine_initdt (OrdinaryDiffEqCore initdt.jl) ---- */
+    for (int i = 0; i < m; i++) { x[i] = x0[i]; sk[i] = fma(fabs(x0[i]), rtol, atol); }
+    for (int i = 0; i < m; i++) buf[i] = x0[i] / sk[i];
+    double d0 = rms_norm(buf, m);
+    f(ctx, t0, x, k1, &oob);
+    for (int i = 0; i < m; i++) buf[i] = k1[i] / sk[i];
+    double d1 = rms_norm(buf, m);
+    double dt0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * (d0 / d1);
+    dt0 = dmin(dt0, dtmax);
+    double dt;
+    if (dt0 < 10.0 * 2.220446049250313e-16) {
+        dt = dmax(1e-6, dtmin);
+    } else {
+        for (int i = 0; i < m; i++) u[i] = fma(dt0, k1[i], x0[i]);
+        f(ctx, t0 + dt0, u, f1, &oob);
+        int same = 1;
+        for (int i = 0; i < m; i++) same &= (k1[i] == f1[i]);
+        if (same) {
+            dt = dmax(dtmin, 100.0 * dt0);
+        } else {
+            for (int i = 0; i < m; i++) buf[i] = (f1[i] - k1[i]) / sk[i];
+            double d2 = rms_norm(buf, m) / dt0;
+            double md = dmax(d1, d2);
+            double dt1 = (md <= 1e-15) ? dmax(1e-6, dt0 * 1e-3) : sbr_pow_pos(0.01 / md, 1.0 / 6.0);
+            dt = dmax(dtmin, dmin(dmin(100.0 * dt0, dt1), dtmax));
+        }
+    }
+
+    /* ---- main loop (solve! / loopheader! / loopfooter!) ---- */
+    double t = t0, qold = CTL_QOLDMIN, q11 = 1.0;
+    autoswitch_t as = {0, 0};
+    if (knots_push(kn, t0, x)) return -1;
+    int64_t iter = 0;
+    while (t < t1) {
+        if (++iter > maxiters) { st->status |= SBR_ODE_MAXITERS; break; }
+        dt = dmin(dtmax, dt);
+        dt = dmax(dt, dtmin);
+        dt = dmin(dt, t1 - t); /* modify_dt_for_tstops! */
+
+        double a = dt * A21;
+        for (int i = 0; i < m; i++) tmp[i] = fma(a, k1[i], x[i]);
+        f(ctx, fma(C1, dt, t), tmp, k2, &oob);
+        for (int i = 0; i < m; i++) tmp[i] = fma(dt, fma(A31, k1[i], A32 * k2[i]), x[i]);
+        f(ctx, fma(C2, dt, t), tmp, k3, &oob);
+        for (int i = 0; i < m; i++)
+            tmp[i] = fma(dt, fma(A41, k1[i], fma(A42, k2[i], A43 * k3[i])), x[i]);
+        f(ctx, fma(C3, dt, t), tmp, k4, &oob);
+        for (int i = 0; i < m; i++)
+            tmp[i] = fma(dt, fma(A51, k1[i], fma(A52, k2[i], fma(A53, k3[i], A54 * k4[i]))), x[i]);
+        f(ctx, fma(C4, dt, t), tmp, k5, &oob);
+        for (int i = 0; i < m; i++)
+            tmp6[i] = fma(dt, fma(A61, k1[i], fma(A62, k2[i], fma(A63, k3[i], fma(A64, k4[i], A65 * k5[i])))),
+                          x[i]);
+        f(ctx, t + dt, tmp6, k6, &oob);
+        for (int i = 0; i < m; i++)
+            u[i] = fma(dt,
+                       fma(A71, k1[i],
+                           fma(A72, k2[i], fma(A73, k3[i], fma(A74, k4[i], fma(A75, k5[i], A76 * k6[i]))))),
+                       x[i]);
+        f(ctx, t + dt, u, k7, &oob);
+        /* eigenvalue estimate for AutoSwitch: Inf-norm of |(k7-k6)/(u-tmp6)| */
+        double eig = 0.0;
+        int eig_nan = 0;
+        for (int i = 0; i < m; i++) {
+            double r = fabs((k7[i] - k6[i]) / (u[i] - tmp6[i]));
+            if (r != r) eig_nan = 1;
+            else if (r > eig) eig = r;
+        }
+        if (eig_nan) eig = NAN;
+        /* error estimate */
+        for (int i = 0; i < m; i++) {
+            double ut = dt * fma(BT1, k1[i],
+                                 fma(BT2, k2[i],
+                                     fma(BT3, k3[i], fma(BT4, k4[i], fma(BT5, k5[i], fma(BT6, k6[i], BT7 * k7[i]))))));
+            buf[i] = ut / fma(dmax(fabs(x[i]), fabs(u[i])), rtol, atol);
+        }
+        double EEst = rms_norm(buf, m);
+        /* stepsize_controller!(PIController) */
+        double q;
+        if (EEst == 0.0) {
+            q = CTL_INV_QMAX;
+        } else {
+            q11 = sbr_pow_pos(EEst, CTL_BETA1);
+            q = q11 / sbr_pow_pos(qold, CTL_BETA2);
+            q = dmax(CTL_INV_QMAX, dmin(CTL_INV_QMIN, q / CTL_GAMMA));
+        }
+        if (EEst <= 1.0) { /* accept */
+            st->naccept++;
+            double dtnew = dt / q;
+            qold = dmax(EEst, CTL_QOLDMIN);
+            double tn = t + dt;
+            if (fabs(tn - t1) < 100.0 * sbr_jl_eps(dmax(t, t1))) tn = t1;
+            t = tn;
+            for (int i = 0; i < m; i++) { x[i] = u[i]; k1[i] = k7[i]; }
+            dt = dmax(dmin(dtmax, dtnew), dtmin); /* calc_dt_propose! */
+            if (knots_push(kn, t, x)) return -1;
+        } else { /* reject */
+            st->nreject++;
+            dt = dt / dmin(CTL_INV_QMIN, q11 / CTL_GAMMA);
+        }
+        if (!(dt > 0.0) || !isfinite(dt)) { st->status |= SBR_ODE_FAILED; break; }
+        autoswitch_update(&as, eig, dt);
+    }
+    if (as.switched) st->status |= SBR_STIFF_SWITCH;
+    if (oob) st->status |= SBR_OOB;
+    return 0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Baseline learning: dx/dt = β x (1 − x)  (learning.jl:45-48)              */
+/* ------------------------------------------------------------------------ */
+static void rhs_logistic(void* ctx, double t, const double* x, double* dx, int* oob)
+{
+    (void)t; (void)oob;
+    double beta = *(const double*)ctx;
+    dx[0] = (beta * x[0]) * (1.0 - x[0]);
+}
+
+int64_t sbro_learn_logistic(double beta, double t0, double t1, double x0, double rtol, double atol,
+                            int64_t maxiters, double* t_out, double* G_out, int64_t cap, int64_t* stats)
+{
+    knots_t kn = {0};
+    ode_stats_t st;
+    if (tsit5_solve(rhs_logistic, &beta, 1, t0, t1, &x0, rtol, atol, maxiters, &kn, &st)) {
+        knots_free(&kn);
+        return -1;
+    }
+    int64_t n = kn.n;
+    if (stats) { stats[0] = st.naccept; stats[1] = st.nreject; stats[2] = st.status; stats[3] = n; }
+    if (n > cap) n = -n; /* caller buffer too small: return -needed */
+    else {
+        memcpy(t_out, kn.t, (size_t)kn.n * sizeof(double));
+        memcpy(G_out, kn.x, (size_t)kn.n * sizeof(double));
+    }
+    knots_free(&kn);
+    return n;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Hazard rate on the τ̄ grid (solver.jl:153-185)                           */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+    double* tau; /* N_eta knots: t_i <= eta, then eta appended if not last */
+    double* hr;
+    int64_t n;
+    int oob;
+} hazard_t;
+
+static void hazard_free(hazard_t* h) { free(h->tau); free(h->hr); memset(h, 0, sizeof(*h)); }
+
+/* pdf given at the ODE knots (g[i]); explicit_grid=1 reproduces the `grid=`
+ * branch (solver.jl:163-164: always append η) used by the hetero solver. */
+static int hazard_rate(const double* t, const double* g, int64_t n, double p, double a, double eta,
+                       int explicit_grid, hazard_t* h)
+{
+    memset(h, 0, sizeof(*h));
+    int64_t m = 0;
+    while (m < n && t[m] <= eta) m++; /* knots are sorted: the .<= η mask is a prefix */
+    int push = explicit_grid ? 1 : (m == 0 || t[m - 1] != eta);
+    int64_t N = m + push;
+    h->tau = (double*)malloc((size_t)(N > 0 ? N : 1) * sizeof(double));
+    h->hr = (double*)malloc((size_t)(N > 0 ? N : 1) * sizeof(double));
+    double* pdf = (double*)malloc((size_t)(N > 0 ? N : 1) * sizeof(double));
+    double* I = (double*)malloc((size_t)(N > 0 ? N : 1) * sizeof(double));
+    if (!h->tau || !h->hr || !pdf || !I) { free(pdf); free(I); return -1; }
+    for (int64_t i = 0; i < m; i++) { h->tau[i] = t[i]; pdf[i] = g[i]; }
+    if (push) {
+        h->tau[m] = eta;
+        pdf[m] = INTERP(t, g, n, eta, &h->oob);
+    }
+    h->n = N;
+    /* cumulative trapezoid of eg(τ) = exp(aτ)·pdf(τ) (solver.jl:168-176) */
+    I[0] = 0.0;
+    double eprev = sbr_exp(a * h->tau[0]) * pdf[0];
+    for (int64_t i = 1; i < N; i++) {
+        double ei = sbr_exp(a * h->tau[i]) * pdf[i];
+        I[i] = I[i - 1] + (0.5 * (eprev + ei)) * (h->tau[i] - h->tau[i - 1]);
+        eprev = ei;
+    }
+    double Ieta = I[N - 1];
+    double omp = 1.0 - p;
+    for (int64_t i = 0; i < N; i++)
+        h->hr[i] = ((p * sbr_exp(a * h->tau[i])) * pdf[i]) / ((p * I[i]) + (omp * Ieta));
+    free(pdf);
+    free(I);
+    return 0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* optimal_buffer (solver.jl:211-264)                                       */
+/* ------------------------------------------------------------------------ */
+static void optimal_buffer(double u, const double* tau, const double* hr, int64_t n, double t_end,
+                           double* tin_out, double* tout_out)
+{
+    int any = 0, all = 1;
+    int64_t first_above = -1, last_above = -1;
+    for (int64_t i = 0; i < n; i++) {
+        int ab = hr[i] > u;
+        any |= ab;
+        all &= ab;
+        if (ab) { if (first_above < 0) first_above = i; last_above = i; }
+    }
+    if (!any) { *tin_out = t_end; *tout_out = t_end; return; }
+    if (all) { *tin_out = tau[0]; *tout_out = tau[n - 1]; return; }
+    double tin = t_end, tout = t_end;
+    for (int64_t i = 0; i + 1 < n; i++) {
+        if (!(hr[i] > u) && (hr[i + 1] > u)) {
+            tin = tau[i] + ((u - hr[i]) * (tau[i + 1] - tau[i])) / (hr[i + 1] - hr[i]);
+            break;
+        }
+    }
+    for (int64_t i = n - 2; i >= 0; i--) {
+        if ((hr[i] > u) && !(hr[i + 1] > u)) {
+            tout = tau[i] + ((u - hr[i]) * (tau[i + 1] - tau[i])) / (hr[i + 1] - hr[i]);
+            break;
+        }
+    }
+    if (tin == t_end) tin = tau[first_above];
+    if (tout == t_end) tout = tau[last_above];
+    *tin_out = tin;
+    *tout_out = tout;
+}
+
+/* ------------------------------------------------------------------------ */
+/* compute_ξ bisection (solver.jl:308-376)                                  */
+/* returns status bits; *xi / *tol set; *iters = loop iterations executed   */
+/* ------------------------------------------------------------------------ */
+static uint32_t compute_xi(double tin, double tout, const double* t, const double* G, int64_t n, double kappa,
+                           int32_t max_iters, double* xi_out, double* tol_out, int32_t* iters)
+{
+    const double tolerance = 10.0 * sbr_jl_eps(kappa);
+    double xnew = (tin + tout) / 2.0, xmin = tin, xmax = tout;
+    int oob = 0;
+    *xi_out = NAN;
+    *tol_out = INFINITY;
+    for (int32_t iter = 1; iter <= max_iters; iter++) {
+        *iters = iter;
+        double d = xmin - xmax;
+        if (fabs(d) < 2.0 * sbr_jl_eps(d)) return SBR_NO_RUN_COLLAPSE;
+        if (iter == max_iters - 1) return SBR_NO_RUN_MAXITER;
+        double xo = xnew;
+        double ic = dmin(tin, xo), oc = dmin(tout, xo);
+        double AW = INTERP(t, G, n, oc, &oob) - INTERP(t, G, n, ic, &oob);
+        int64_t idx = ssl(t, n, xo);
+        if (idx < 0 || idx + 1 >= n) return SBR_OOB;
+        double eps = t[idx + 1] - t[idx];
+        double AWe = INTERP(t, G, n, oc + eps, &oob) - INTERP(t, G, n, ic + eps, &oob);
+        if (oob) return SBR_OOB;
+        double err = AW - kappa;
+        int inc = AWe >= AW;
+        if (fabs(err) <= tolerance) {
+            if (inc) { *xi_out = xo; *tol_out = fabs(err); return SBR_RUN; }
+            return SBR_FALSE_EQ;
+        } else if (err > 0) {
+            xmax = xo;
+            xnew = 0.5 * (xo + xmin);
+        } else {
+            xmin = xo;
+            xnew = 0.5 * (xo + xmax);
+        }
+    }
+    return SBR_NO_RUN_MAXITER;
+}
+
+/* ------------------------------------------------------------------------ */
+/* get_AW on the HR grid + AW_max (solver.jl:495-532, 565)                  */
+/* ------------------------------------------------------------------------ */
+static double get_aw(double xi, double tin, double tout, const double* tau, int64_t n_tau, const double* t,
+                     const double* G, int64_t n, double* aw_path, int* oob)
+{
+    double ic = (tin >= xi) ? xi : tin;
+    double oc = (tout > xi) ? xi : tout;
+    double G0 = INTERP(t, G, n, 0.0, oob);
+    double mx = -INFINITY;
+    for (int64_t i = 0; i < n_tau; i++) {
+        double a = (tau[i] - xi) + ic;
+        double b = (tau[i] - xi) + oc;
+        double gi = INTERP(t, G, n, a > 0 ? a : 0.0, oob);
+        double go = INTERP(t, G, n, b > 0 ? b : 0.0, oob);
+        double awin = a >= 0 ? gi : 0.0;
+        double awout = b >= 0 ? go : 0.0;
+        double v = (awout - awin) + G0;
+        if (aw_path) aw_path[i] = v;
+        if (mx == mx && (v != v || v > mx)) mx = v; /* NaN-propagating max (Julia maximum) */
+    }
+    return mx;
+}
+
+/* ------------------------------------------------------------------------ */
+/* one (β, u) equilibrium given knots + hazard (solve_equilibrium_baseline)  */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+    double xi, tin, tout, aw_max, tol;
+    uint32_t status;
+    int32_t iters;
+} point_t;
+
+static void equilibrium_point(const double* t, const double* G, int64_t n, const hazard_t* h, double t_end,
+                              double u, double kappa, int32_t max_iters, point_t* r, double* aw_path)
+{
+    memset(r, 0, sizeof(*r));
+    r->xi = NAN;
+    r->aw_max = NAN;
+    r->tol = INFINITY;
+    if (h->oob) { r->status = SBR_OOB; r->tin = r->tout = NAN; return; }
+    optimal_buffer(u, h->tau, h->hr, h->n, t_end, &r->tin, &r->tout);
+    if (r->tin == r->tout) {
+        r->status = SBR_NO_RUN_HR_BELOW_U | SBR_CONVERGED;
+        r->tol = 0.0;
+        return;
+    }
+    double xi, tol;
+    uint32_t s = compute_xi(r->tin, r->tout, t, G, n, kappa, max_iters, &xi, &tol, &r->iters);
+    if (s != SBR_RUN) { r->status = s; return; }
+    int oob = 0;
+    double mx = get_aw(xi, r->tin, r->tout, h->tau, h->n, t, G, n, aw_path, &oob);
+    if (oob) { r->status = SBR_OOB; return; }
+    r->xi = xi;
+    r->tol = tol;
+    r->aw_max = mx;
+    r->status = SBR_RUN | SBR_CONVERGED;
+}
+
+/* public single-point API on caller-provided knots (used by tests) */
+void sbro_equilibrium(const double* t, const double* G, int64_t n, double beta, double eta, double t_end,
+                      double u, double p, double kappa, double lambda, int32_t max_iters, double* res,
+                      uint32_t* status, int32_t* iters, double* hr_tau, double* hr_v, double* aw, int64_t* n_hr)
+{
+    double* g = (double*)malloc((size_t)n * sizeof(double));
+    for (int64_t i = 0; i < n; i++) g[i] = (beta * G[i]) * (1.0 - G[i]);
+    hazard_t h;
+    hazard_rate(t, g, n, p, lambda, eta, 0, &h);
+    point_t r;
+    equilibrium_point(t, G, n, &h, t_end, u, kappa, max_iters, &r, aw);
+    res[0] = r.xi; res[1] = r.tin; res[2] = r.tout; res[3] = r.aw_max; res[4] = r.tol;
+    *status = r.status;
+    *iters = r.iters;
+    if (n_hr) *n_hr = h.n;
+    if (hr_tau) memcpy(hr_tau, h.tau, (size_t)h.n * sizeof(double));
+    if (hr_v) memcpy(hr_v, h.hr, (size_t)h.n * sizeof(double));
+    hazard_free(&h);
+    free(g);
+}
+
+/* ------------------------------------------------------------------------ */
+/* Baseline β×u sweep (scripts/1_baseline.jl:224-267 without the early exit) */
+/* learning + hazard once per β column (u-independent), then every u.       */
+/* ------------------------------------------------------------------------ */
+int sbro_sweep_baseline(const double* beta, const double* eta, const double* t_end, double x0, const double* u,
+                        int64_t n_beta, int64_t n_u, double p, double kappa, double lambda, int32_t max_iters,
+                        int32_t nthreads, double* xi, double* tin, double* tout, double* aw_max, double* tol,
+                        uint32_t* status, int32_t* iters, int64_t* nknots)
+{
+    int err = 0;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 1) reduction(| : err)
+#endif
+    for (int64_t b = 0; b < n_beta; b++) {
+        knots_t kn = {0};
+        ode_stats_t st;
+        double x0v = x0;
+        double bb = beta[b];
+        if (tsit5_solve(rhs_logistic, &bb, 1, 0.0, t_end[b], &x0v, 2.220446049250313e-16, 2.220446049250313e-16,
+                        100000, &kn, &st)) { err |= 1; continue; }
+        if (nknots) nknots[b] = kn.n;
+        int64_t n = kn.n;
+        double* g = (double*)malloc((size_t)n * sizeof(double));
+        for (int64_t i = 0; i < n; i++) g[i] = (bb * kn.x[i]) * (1.0 - kn.x[i]);
+        hazard_t h;
+        hazard_rate(kn.t, g, n, p, lambda, eta[b], 0, &h);
+        for (int64_t j = 0; j < n_u; j++) {
+            point_t r;
+            equilibrium_point(kn.t, kn.x, n, &h, t_end[b], u[j], kappa, max_iters, &r, NULL);
+            int64_t o = b * n_u + j;
+            xi[o] = r.xi; tin[o] = r.tin; tout[o] = r.tout; aw_max[o] = r.aw_max; tol[o] = r.tol;
+            status[o] = r.status | (st.status & (SBR_ODE_MAXITERS | SBR_STIFF_SWITCH | SBR_ODE_FAILED));
+            if (iters) iters[o] = r.iters;
+        }
+        hazard_free(&h);
+        free(g);
+        knots_free(&kn);
+    }
+    return err ? -1 : 0;
+}
+
+/* 5-consecutive-no-run early exit applied as a post-pass over u-fastest
+ * columns (scripts/1_baseline.jl:236-244, :147-164).  Skipped points get
+ * aw_max = xi = NaN, tol = Inf and SBR_SKIPPED_EARLY_EXIT. */
+void sbro_apply_early_exit(int64_t n_beta, int64_t n_u, int32_t threshold, double* xi, double* aw_max, double* tol,
+                           uint32_t* status)
+{
+    for (int64_t b = 0; b < n_beta; b++) {
+        int32_t c = 0;
+        for (int64_t j = 0; j < n_u; j++) {
+            int64_t o = b * n_u + j;
+            if (c >= threshold) {
+                xi[o] = NAN; aw_max[o] = NAN; tol[o] = INFINITY;
+                status[o] = SBR_SKIPPED_EARLY_EXIT;
+                continue;
+            }
+            if (status[o] & SBR_RUN) c = 0;
+            else c++;
+        }
+    }
+}
