@@ -1,0 +1,207 @@
+#!/usr/bin/env python3
+"""Benchmark: equilibria solved per second on the β×u grid (FP64), BASELINE.json's metric.
+
+Workload (BASELINE config 3): the Fig 5 grid of scripts/1_baseline.jl:210-212 at
+2048×2048 — ave_meeting_time = range(1e-4, 1, 2048), β = 1/amt, u = range(0.001, 1,
+2048), η = 15 and tspan = (0, 30) for every β (copy-modify carry-over) — 4,194,304
+equilibria per GPU.  One step = one full sweep: learning (Tsit5 + hazard) for every
+β column, then buffers + ξ bisection + AW_max for every (β, u), every point solved
+(no early exit), inputs already resident in HBM, results written to HBM.
+
+N GPUs (torchrun, one process per GPU, RCCL): weak scaling — rank r owns the β
+columns r, r+N, r+2N, … of a 2048·N-column grid (same u axis), so per-GPU work is
+fixed; each step ends with an RCCL gather of the result tensor (AW_max + status) to
+rank 0 over xGMI.  value = all ranks' equilibria × steps / max-over-ranks time.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+REPO = Path(__file__).resolve().parent
+sys.path.insert(0, str(REPO / "replication-social-bank-runs_amd"))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import sbr  # noqa: E402
+
+FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X FP64 vector, AMD spec (256 CU x 128 FLOP/clk x 2.4 GHz)
+
+# FP64 operations per equilibrium-kernel stage as the code executes them
+# (add/sub/mul/div = 1, fma = 2, compares/selects/loads = 0)
+F_LERP = 7
+F_BUFFER = 12          # two crossing interpolations (solver.jl:237,250)
+F_BISECT_ITER = 37     # 4 lerps + ε + shifted args + AW/AWe/err + midpoint (solver.jl:326-372)
+F_AW_PER_KNOT = 20     # 2 shifted args x2, 2 lerps, net (solver.jl:511-524)
+F_EXP, F_LOG = 22, 24  # include/sbr_detmath.h
+F_RK_STEP = 21 + 48 + 3 + 14 + 3 + 2 * (F_EXP + F_LOG + 1) + 2 + 5  # Tsit5 step + PI controller
+F_HAZARD_KNOT = 3 + F_EXP + 1 + 4 + 2 + 3  # g, exp, e, trapezoid, numerator, HR division
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--n", type=int, default=2048, help="β columns per GPU and u rows")
+    ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-stride", type=int, default=8, help="cpu_baseline samples every k-th β column")
+    ap.add_argument("--traffic", default=str(REPO / "profiles" / "traffic_latest.json"))
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    n = a.n
+    amt = sbr.julia_range("0.0001", "1", n * world)
+    cols = np.arange(rank, n * world, world)
+    beta_h = 1.0 / amt[cols]
+    u_h = sbr.julia_range("0.001", "1", n)
+    nb, nu = len(beta_h), len(u_h)
+    p, kappa, lam, x0 = 0.5, 0.6, 0.01, 1e-4
+
+    beta = torch.from_numpy(beta_h).to(dev)
+    eta = torch.full((nb,), 15.0, dtype=torch.float64, device=dev)
+    t_end = torch.full((nb,), 30.0, dtype=torch.float64, device=dev)
+    u = torch.from_numpy(u_h).to(dev)
+    out = {k: torch.empty(nb * nu, dtype=torch.float64, device=dev) for k in sbr.engine.RESULT_FIELDS}
+    out["status"] = torch.empty(nb * nu, dtype=torch.int32, device=dev)
+    out["iters"] = torch.empty(nb * nu, dtype=torch.int32, device=dev)
+    gather = world > 1 and not a.no_gather
+    if gather and rank == 0:
+        g_aw = [torch.empty(nb * nu, dtype=torch.float64, device=dev) for _ in range(world)]
+        g_st = [torch.empty(nb * nu, dtype=torch.int32, device=dev) for _ in range(world)]
+    else:
+        g_aw = g_st = None
+
+    eng = sbr.Engine(local)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def step():
+        eng.sweep_baseline_dev(beta, eta, t_end, u, p, kappa, lam, x0, out, stream=stream)
+        if gather:
+            dist.gather(out["aw_max"], g_aw, dst=0)
+            dist.gather(out["status"], g_st, dst=0)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    eng.timing_read(stream)  # drop anything recorded so far
+    eng.timing_enable(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    learn_ms, eq_ms, ncalls = eng.timing_read(stream)
+    eng.timing_enable(False)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # ---- algorithmic flops of this rank's last step (from the kernels' own outputs) ----
+    ls = eng.learn_stats(nb)
+    iters = out["iters"].cpu().numpy().reshape(nb, nu).astype(np.int64)
+    status = out["status"].cpu().numpy().view(np.uint32).reshape(nb, nu)
+    run = (status & sbr.STATUS["SBR_RUN"]) > 0
+    n_tau = ls["n_tau"].astype(np.int64)
+    f_eq = (F_BUFFER * nb * nu + F_BISECT_ITER * int(iters.sum())
+            + int((run * (F_AW_PER_KNOT * n_tau[:, None] + F_LERP)).sum())
+            + 2 * int(n_tau.sum()) * ((nu + 1023) // 1024))
+    f_learn = F_RK_STEP * int((ls["n_accept"] + ls["n_reject"]).sum()) + F_HAZARD_KNOT * int(n_tau.sum())
+    eq_s = eq_ms / max(ncalls, 1) / 1e3
+    achieved = f_eq / eq_s / 1e12
+
+    total_pts = nb * nu * world
+    value = total_pts * a.steps / elapsed
+    traffic = None
+    tp = Path(a.traffic)
+    if tp.exists():
+        try:
+            tj = json.loads(tp.read_text())
+            if tj.get("workload") == f"fig5_{n}x{n}" and tj.get("kernel", "").startswith("equilibrium_kernel"):
+                traffic = tj.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    res = {
+        "metric": "equilibria solved/sec on β×u grid (FP64)",
+        "value": value,
+        "unit": "equilibria/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": elapsed / a.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (deterministic Fig 5 parameter grid; no RNG in the reference)",
+        "config": {
+            "workload": f"fig5_beta_u_sweep_{n}x{n}_per_gpu (BASELINE config 3)",
+            "n_beta_per_gpu": nb, "n_u": nu, "eta": 15.0, "t_end": 30.0, "p": p, "kappa": kappa,
+            "lambda": lam, "x0": x0, "early_exit": False, "gather": gather,
+            "parallelism": f"beta-column shards x{world}",
+        },
+        "kernel_ms_per_step": {"learn_logistic": learn_ms / max(ncalls, 1), "equilibrium": eq_ms / max(ncalls, 1)},
+        "flops_per_step": {"equilibrium": f_eq, "learn": f_learn},
+        "roofline": {
+            "bound": "valu_fp64",
+            "kernel": "equilibrium_kernel",
+            "achieved": achieved,
+            "peak": FP64_VALU_PEAK_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": achieved / FP64_VALU_PEAK_TFLOPS,
+            "traffic": traffic,
+        },
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(beta_h, u_h, a.cpu_stride, p, kappa, lam, x0)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(beta_h, u_h, stride, p, kappa, lam, x0):
+    """The CPU oracle (C restatement, same algorithm, OpenMP over β columns) on a
+    bounded sample of the same workload: every `stride`-th β column, all u."""
+    sys.path.insert(0, str(REPO / "oracle"))
+    import oracle as O  # noqa: E402  (test infrastructure: cpu_baseline leg only)
+
+    O.build()
+    cores = max(1, min(16, len(os.sched_getaffinity(0))))
+    cols = beta_h[::stride]
+    t0 = time.perf_counter()
+    O.sweep_baseline(cols, 15.0, 30.0, u_h, p, kappa, lam, x0=x0, nthreads=cores)
+    dt = time.perf_counter() - t0
+    pts = len(cols) * len(u_h)
+    return {"value": pts / dt, "unit": "equilibria/s", "cores": cores, "kind": "port",
+            "sample": f"{len(cols)} β columns (every {stride}th of the {len(beta_h)}) x {len(u_h)} u = {pts} "
+                      f"equilibria in {dt:.2f} s"}
+
+
+if __name__ == "__main__":
+    main()

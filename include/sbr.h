@@ -1,0 +1,142 @@
+/*
+ * sbr.h — C ABI of libsbr, the MI355X batched equilibrium engine for
+ * "The Social Determinants of Bank Runs" (Robin-Lenoir/replication-social-bank-runs).
+ *
+ * The reference has no FFI: its "interface" is a set of Julia functions that
+ * the scripts call point by point.  Each entry point below
+ * replaces one of those call patterns with a batched call; a Julia caller
+ * binds them with `ccall` (see INTEGRATION.md for the shim).
+ *
+ * Conventions
+ *  - plain C types only; every array is caller-allocated;
+ *  - result arrays are n_beta*n_u long, u-fastest: element (i, j) — the i-th β
+ *    and the j-th u — is at [i*n_u + j]; this is max_AW_matrix[j, i] of
+ *    scripts/1_baseline.jl:213,254;
+ *  - functions return 0 on success or a negative SBR_E* code;
+ *  - per-point outcomes are status bits (sbr_status.h); xi is NaN and tol is
+ *    Inf whenever SBR_RUN is clear, exactly like SolvedModel
+ *    (src/baseline/solver.jl:429-455);
+ *  - a context is bound to one HIP device; calls on one context are
+ *    serialised by the caller; distinct contexts are independent.
+ *  - The *_dev variants take device pointers and a hipStream_t (as void*) and
+ *    do not synchronise: they are what the multi-GPU host layer and the
+ *    benchmark use (inputs already resident in HBM).
+ */
+#ifndef SBR_H
+#define SBR_H
+
+#include <stdint.h>
+
+#include "sbr_status.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SBR_OK 0
+#define SBR_EARG (-1)    /* ArgumentError of model.jl:31-35,71-76 / heterogeneity_model.jl:33-41 */
+#define SBR_EDEVICE (-2) /* HIP runtime error or no device */
+#define SBR_ENOMEM (-3)  /* device allocation failed */
+
+typedef struct sbr_ctx sbr_ctx;
+
+typedef struct {
+    double ode_reltol;          /* learning.jl:43 reltol = eps() */
+    double ode_abstol;          /* learning.jl:43 abstol = eps() */
+    int64_t ode_maxiters;       /* DiffEq default maxiters = 1e5 */
+    int32_t bisect_max_iters;   /* solver.jl:309 max_iters = 100 */
+    int32_t early_exit_nan_run; /* 1_baseline.jl:147,221: 5; 0 disables */
+    int32_t knot_capacity;      /* engine limit on stored knots per β (0 = default 8192) */
+    int32_t reserved;
+} sbr_opts;
+
+typedef struct {
+    double* xi;          /* SolvedModel.ξ                       */
+    double* tau_in_unc;  /* SolvedModel.τ_bar_IN_UNC            */
+    double* tau_out_unc; /* SolvedModel.τ_bar_OUT_UNC           */
+    double* aw_max;      /* get_AW_functions!(...).AW_max       */
+    double* tol;         /* SolvedModel.tolerance               */
+    uint32_t* status;    /* SBR_* bits                          */
+    int32_t* iters;      /* bisection iterations (may be NULL)  */
+} sbr_result_soa;
+
+/* Fills *o with the reference defaults (eps() tolerances, 1e5, 100, 5, 8192). */
+void sbr_default_opts(sbr_opts* o);
+
+/* Creates a context on HIP device `device` (the caller's rank-local GPU). */
+int sbr_init(int device, sbr_ctx** ctx);
+int sbr_free(sbr_ctx* ctx);
+const char* sbr_last_error(const sbr_ctx* ctx);
+
+/*
+ * Baseline β×u sweep — replaces the Fig 4/Fig 5 loops of
+ * scripts/1_baseline.jl:151-192 and :224-267, i.e. for each β
+ *     lr = solve_learning(LearningParameters(β, (0, t_end[i]), x0))   learning.jl:109
+ * and for each u
+ *     r  = solve_equilibrium_baseline(lr, EconomicParameters(u, p, κ, λ, η_bar, η[i]))  solver.jl:413
+ *     get_AW_functions!(r).AW_max                                         solver.jl:553-576
+ * eta/t_end are per-β so that the copy-modify carry-over of model.jl:189-211
+ * (η = 15, tspan = (0, 30) for every β of Fig 5) is expressed by the caller.
+ * Host pointers; synchronous.
+ */
+int sbr_sweep_baseline(sbr_ctx* ctx, const double* beta, const double* eta, const double* t_end, double x0,
+                       const double* u, int64_t n_beta, int64_t n_u, double p, double kappa, double lambda,
+                       const sbr_opts* opts, sbr_result_soa* out);
+
+/* Same on device pointers (beta/eta/t_end/u and every out field in HBM),
+ * enqueued on `stream` (hipStream_t); no host synchronisation. */
+int sbr_sweep_baseline_dev(sbr_ctx* ctx, void* stream, const double* beta, const double* eta,
+                           const double* t_end, double x0, const double* u, int64_t n_beta, int64_t n_u, double p,
+                           double kappa, double lambda, const sbr_opts* opts, sbr_result_soa* out);
+
+/*
+ * Learning only — solve_learning (learning.jl:109-124) for n_beta β at once.
+ * Writes, per β, the knot grid t and CDF values G of the adaptive ODE
+ * solution (row i at [i*cap .. i*cap + n_knots[i]) ); g = βG(1−G) is implied
+ * (learning.jl:161-173).  When stop_after_eta != 0 the integration stops at
+ * the first knot the equilibrium stage can never read, else
+ * it runs to t_end like the reference.  Host pointers; synchronous.
+ */
+int sbr_learn_baseline(sbr_ctx* ctx, const double* beta, const double* eta, const double* t_end, double x0,
+                       int64_t n_beta, int32_t stop_after_eta, const sbr_opts* opts, double* t_out, double* G_out,
+                       int64_t cap, int32_t* n_knots, uint32_t* status);
+
+/*
+ * Single point with paths — solve_learning + solve_equilibrium_baseline +
+ * get_AW (solver.jl:495-532) for one (β, u), returning the hazard grid τ̄,
+ * HR(τ̄) and AW_cum(τ̄) (arrays of length *n_tau, capacity cap) so that a
+ * caller can rebuild the LinearInterpolation objects the reference's
+ * plotting code consumes.  res = {ξ, τ̄_IN, τ̄_OUT, AW_max, tol}.
+ */
+int sbr_solve_point_paths(sbr_ctx* ctx, double beta, double eta, double t_end, double x0, double u, double p,
+                          double kappa, double lambda, const sbr_opts* opts, double* res, uint32_t* status,
+                          double* tau, double* hr, double* aw_cum, int64_t cap, int64_t* n_tau);
+
+/* 5-consecutive-no-run early exit (1_baseline.jl:236-244) as a post-pass on
+ * host arrays: points after `threshold` consecutive non-runs in a β column get
+ * SBR_SKIPPED_EARLY_EXIT, xi = aw_max = NaN, tol = Inf. */
+void sbr_apply_early_exit(int64_t n_beta, int64_t n_u, int32_t threshold, sbr_result_soa* r);
+
+/* Kernel timing with HIP events recorded on the launch stream around the
+ * learning and equilibrium kernels of every baseline sweep call while
+ * enabled; sbr_timing_read synchronises `stream` (NULL = context stream),
+ * returns the summed milliseconds per kernel and the number of calls, and
+ * resets the accumulators. */
+int sbr_timing_enable(sbr_ctx* ctx, int on);
+int sbr_timing_read(sbr_ctx* ctx, void* stream, double* learn_ms, double* eq_ms, int32_t* n_calls);
+
+/* Per-β learning statistics of the last sweep (knots stored, τ̄-grid length,
+ * accepted / rejected RK steps, learning status bits) for flop accounting. */
+int sbr_learn_stats(sbr_ctx* ctx, int64_t n_beta, int32_t* n_knots, int32_t* n_tau, int32_t* n_accept,
+                    int32_t* n_reject, uint32_t* status);
+
+/* Diagnostics: sbr_exp / sbr_log / sbr_pow_pos (include/sbr_detmath.h)
+ * evaluated on the device, for host/device bit-equality tests. */
+int sbr_selftest_detmath(sbr_ctx* ctx, const double* x, const double* y, int n, double* exp_out, double* log_out,
+                         double* pow_out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SBR_H */

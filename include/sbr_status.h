@@ -28,5 +28,6 @@
 #define SBR_SOCIAL_NOT_CONVERGED 0x1000u /* fixed point hit max_iter / stopped (social :390)   */
 #define SBR_KNOT_OVERFLOW       0x2000u /* engine knot capacity exceeded (engine limit)        */
 #define SBR_ODE_FAILED          0x4000u /* non-finite step size / state                        */
+#define SBR_ENGINE_TRUNC        0x8000u /* engine bug: lookup past a truncated knot grid       */
 
 #endif /* SBR_STATUS_H */

@@ -45,6 +45,8 @@ def lib() -> ctypes.CDLL:
         L.sbro_sweep_baseline.argtypes = [_P, _P, _P, _D, _P, _I64, _I64, _D, _D, _D, _I32, _I32] + [_P] * 8
         L.sbro_apply_early_exit.restype = None
         L.sbro_apply_early_exit.argtypes = [_I64, _I64, _I32, _P, _P, _P, _P]
+        L.sbro_detmath.restype = None
+        L.sbro_detmath.argtypes = [_P, _P, _I64, _P, _P, _P]
         for name in ("sbro_sweep_hetero", "sbro_solve_social"):
             if hasattr(L, name):
                 getattr(L, name).restype = ctypes.c_int
@@ -117,3 +119,12 @@ def apply_early_exit(res: dict, threshold: int = 5) -> dict:
     lib().sbro_apply_early_exit(nb, nu, threshold, _ptr(r["xi"]), _ptr(r["aw_max"]), _ptr(r["tol"]),
                                 _ptr(r["status"]))
     return r
+
+
+def detmath(x, y):
+    x = np.ascontiguousarray(x, np.float64)
+    y = np.ascontiguousarray(y, np.float64)
+    n = len(x)
+    e, l, pw = np.empty(n), np.empty(n), np.empty(n)
+    lib().sbro_detmath(_ptr(x), _ptr(y), n, _ptr(e), _ptr(l), _ptr(pw))
+    return e, l, pw

@@ -609,3 +609,13 @@ void sbro_apply_early_exit(int64_t n_beta, int64_t n_u, int32_t threshold, doubl
         }
     }
 }
+
+/* detmath exports (tests compare them against numpy and against the device) */
+void sbro_detmath(const double* x, const double* y, int64_t n, double* e, double* l, double* pw)
+{
+    for (int64_t i = 0; i < n; i++) {
+        e[i] = sbr_exp(x[i]);
+        l[i] = sbr_log(x[i]);
+        pw[i] = sbr_pow_pos(x[i], y[i]);
+    }
+}

@@ -1,0 +1,424 @@
+// sbr_baseline.hip — gfx950 kernels for the baseline β×u sweep.
+//
+//   learn_logistic_kernel   one lane per β column: FP64 Tsit5 with
+//                           OrdinaryDiffEq's PI step control on
+//                           dx/dt = βx(1−x) (learning.jl:41-54), every
+//                           accepted step a knot (save_everystep), hazard
+//                           numerator / cumulative trapezoid streamed as the
+//                           knots are produced (solver.jl:153-185), HR
+//                           finalised in a second pass.
+//   equilibrium_kernel      one workgroup per (β, u-tile), one lane per grid
+//                           point: knot grid + HR staged once per workgroup
+//                           in LDS, then per lane the crossing scan
+//                           (solver.jl:211-264), the ξ bisection with the
+//                           slope check (solver.jl:308-376) and the AW path
+//                           maximum (solver.jl:495-532, 565).  Results are
+//                           written as coalesced SoA rows.
+//
+// Bit-exact against oracle/sbr_oracle.c (see sbr_device.h).
+#include "sbr_device.h"
+#include "sbr_kernels.h"
+
+namespace sbr {
+
+// ============================================================================
+// Learning kernel
+// ============================================================================
+__global__ __launch_bounds__(64) void learn_logistic_kernel(const double* __restrict__ beta,
+                                                            const double* __restrict__ eta,
+                                                            const double* __restrict__ t_end, LearnArgs a,
+                                                            LearnBufs L)
+{
+    const int b = blockIdx.x * 64 + threadIdx.x;
+    if (b >= a.n_beta) return;
+    const double BETA = beta[b], ETA = eta[b], T1 = t_end[b], T0 = 0.0;
+    const size_t row = (size_t)b * (size_t)L.cap;
+    double* __restrict__ T = L.t + row;
+    double* __restrict__ Gv = L.G + row;
+    double* __restrict__ H = L.hr + row;
+    double* __restrict__ HI = L.hrI + row;
+    uint32_t st = 0;
+    int n = 0, m = 0;
+    bool pushed = false;
+
+    if (!(BETA > 0.0) || !(T1 > T0) || !(ETA > 0.0)) { // LearningParameters / EconomicParameters checks
+        L.status[b] = SBR_ARG_INVALID;
+        L.n_knots[b] = 0; L.n_tau[b] = 0; L.n_le[b] = 0; L.n_accept[b] = 0; L.n_reject[b] = 0;
+        return;
+    }
+    const double x0 = a.x0, rtol = a.rtol, atol = a.atol, p = a.p, lam = a.lam;
+    const double dtmax = T1 - T0;
+    const double dtmin = sbr_jl_eps(dmax(fabs(T0), fabs(T1)));
+
+    // ---- ode_determine_initdt ----
+    const double sk = fma(fabs(x0), rtol, atol);
+    const double d0 = fabs(x0 / sk);
+    double k1 = (BETA * x0) * (1.0 - x0);
+    const double d1 = fabs(k1 / sk);
+    double dt0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * (d0 / d1);
+    dt0 = dmin(dt0, dtmax);
+    double dt;
+    if (dt0 < 10.0 * DBL_EPS) {
+        dt = dmax(1e-6, dtmin);
+    } else {
+        const double u1 = fma(dt0, k1, x0);
+        const double f1 = (BETA * u1) * (1.0 - u1);
+        if (k1 == f1) {
+            dt = dmax(dtmin, 100.0 * dt0);
+        } else {
+            const double d2 = fabs((f1 - k1) / sk) / dt0;
+            const double md = dmax(d1, d2);
+            const double dt1 = (md <= 1e-15) ? dmax(1e-6, dt0 * 1e-3) : sbr_pow_pos(0.01 / md, 1.0 / 6.0);
+            dt = dmax(dtmin, dmin(dmin(100.0 * dt0, dt1), dtmax));
+        }
+    }
+
+    // ---- knot sink: store (t, G) and stream the hazard terms ----
+    double tprev = 0.0, gprev = 0.0, eprev = 0.0, I = 0.0, tlast = 0.0, bound = -INFINITY;
+    bool past = false, done = false;
+    int jstar = -1;
+    auto push = [&](double t, double x) {
+        if (n >= L.cap) { st |= SBR_KNOT_OVERFLOW; done = true; return; }
+        T[n] = t;
+        Gv[n] = x;
+        const double g = (BETA * x) * (1.0 - x); // compute_pdf_symbolic_baseline
+        if (!past) {
+            if (t <= ETA) {
+                const double E = sbr_exp(lam * t);
+                const double e = E * g;
+                I = (m == 0) ? 0.0 : I + (0.5 * (eprev + e)) * (t - tprev);
+                H[m] = (p * E) * g;
+                HI[m] = I;
+                m++;
+                eprev = e; tprev = t; gprev = g;
+            } else {
+                past = true;
+                jstar = n;
+                if (m == 0) {
+                    st |= SBR_OOB; // pdf(η) with η < t0: BoundsError
+                } else if (tprev != ETA) { // append η (solver.jl:159-160), pdf(η) on bracket [n-1, n]
+                    const double d = (ETA - tprev) / (t - tprev);
+                    const double pe = gprev * (1.0 - d) + g * d;
+                    const double E = sbr_exp(lam * ETA);
+                    const double e = E * pe;
+                    I = I + (0.5 * (eprev + e)) * (ETA - tprev);
+                    H[m] = (p * E) * pe;
+                    HI[m] = I;
+                    m++;
+                    pushed = true;
+                }
+            }
+        }
+        // furthest point any lookup of the equilibrium stage can reach
+        if (n >= 1 && (jstar < 0 || n <= jstar)) bound = dmax(bound, t + (t - tlast));
+        tlast = t;
+        n++;
+        if (a.stop_after_eta && past && t >= bound) done = true;
+    };
+
+    double t = T0, x = x0, qold = CTL_QOLDMIN, q11 = 1.0;
+    AutoSwitch as;
+    int naccept = 0, nreject = 0;
+    push(t, x);
+    int64_t iter = 0;
+    while (t < T1 && !done) {
+        if (++iter > a.maxiters) { st |= SBR_ODE_MAXITERS; break; }
+        dt = dmin(dtmax, dt);
+        dt = dmax(dt, dtmin);
+        dt = dmin(dt, T1 - t);
+
+        const double a21 = dt * A21;
+        double tmp = fma(a21, k1, x);
+        const double k2 = (BETA * tmp) * (1.0 - tmp);
+        tmp = fma(dt, fma(A31, k1, A32 * k2), x);
+        const double k3 = (BETA * tmp) * (1.0 - tmp);
+        tmp = fma(dt, fma(A41, k1, fma(A42, k2, A43 * k3)), x);
+        const double k4 = (BETA * tmp) * (1.0 - tmp);
+        tmp = fma(dt, fma(A51, k1, fma(A52, k2, fma(A53, k3, A54 * k4))), x);
+        const double k5 = (BETA * tmp) * (1.0 - tmp);
+        const double tmp6 = fma(dt, fma(A61, k1, fma(A62, k2, fma(A63, k3, fma(A64, k4, A65 * k5)))), x);
+        const double k6 = (BETA * tmp6) * (1.0 - tmp6);
+        const double u =
+            fma(dt, fma(A71, k1, fma(A72, k2, fma(A73, k3, fma(A74, k4, fma(A75, k5, A76 * k6))))), x);
+        const double k7 = (BETA * u) * (1.0 - u);
+        const double eigr = fabs((k7 - k6) / (u - tmp6));
+        const double eig = (eigr != eigr) ? (double)NAN : eigr;
+        const double ut =
+            dt * fma(BT1, k1, fma(BT2, k2, fma(BT3, k3, fma(BT4, k4, fma(BT5, k5, fma(BT6, k6, BT7 * k7))))));
+        const double EEst = fabs(ut / fma(dmax(fabs(x), fabs(u)), rtol, atol));
+        const double q = pi_q(EEst, qold, q11);
+        if (EEst <= 1.0) {
+            naccept++;
+            const double dtnew = dt / q;
+            qold = dmax(EEst, CTL_QOLDMIN);
+            double tn = t + dt;
+            if (fabs(tn - T1) < 100.0 * sbr_jl_eps(dmax(t, T1))) tn = T1;
+            t = tn;
+            x = u;
+            k1 = k7;
+            dt = dmax(dmin(dtmax, dtnew), dtmin);
+            push(t, x);
+        } else {
+            nreject++;
+            dt = dt / dmin(CTL_INV_QMIN, q11 / CTL_GAMMA);
+        }
+        if (!(dt > 0.0) || !isfinite(dt)) { st |= SBR_ODE_FAILED; break; }
+        as.update(eig, dt);
+    }
+    if (as.switched) st |= SBR_STIFF_SWITCH;
+    if (!past && !(st & SBR_KNOT_OVERFLOW)) {
+        // integration ended at t_end without a knot beyond η
+        if (m == 0 || tprev != ETA) st |= SBR_OOB; // pdf(η) beyond the last knot
+    }
+    // ---- HR second pass (solver.jl:180-182) ----
+    if (m > 0 && !(st & SBR_OOB)) {
+        const double Ieta = HI[m - 1], omp = 1.0 - p;
+        for (int i = 0; i < m; i++) H[i] = H[i] / ((p * HI[i]) + (omp * Ieta));
+    }
+    L.n_knots[b] = n;
+    L.n_tau[b] = m;
+    L.n_le[b] = pushed ? m - 1 : m;
+    L.status[b] = st;
+    L.n_accept[b] = naccept;
+    L.n_reject[b] = nreject;
+}
+
+// ============================================================================
+// Equilibrium kernel
+// ============================================================================
+struct PointResult {
+    double xi, tin, tout, aw, tol;
+    uint32_t status;
+    int iters;
+};
+
+// range check of an interpolation argument; returns false (and flags) when
+// Interpolations' Throw() extrapolation would raise.
+__device__ __forceinline__ bool in_range(double x, double tlo, double thi, bool trunc, uint32_t& flag)
+{
+    if (x >= tlo && x <= thi) return true;
+    flag |= (trunc && x > thi) ? SBR_ENGINE_TRUNC : SBR_OOB;
+    return false;
+}
+
+template <class P>
+__device__ __forceinline__ void solve_point(P T, P G, P H, const int n, const int ntau, const int nle,
+                                            const double ETA, const double T1, const bool trunc, const double u,
+                                            const double kappa, const int max_iters, const uint32_t lbits,
+                                            PointResult& r, double* __restrict__ aw_path)
+{
+    r.xi = NAN; r.aw = NAN; r.tol = INFINITY; r.iters = 0; r.status = 0;
+    const double tlo = T[0], thi = T[n - 1];
+
+    // ---------------- optimal_buffer: one pass over the τ̄ grid ----------------
+    bool any = false, all = true, prev = false;
+    int fa = -1, la = -1, cin = -1, cout = -1;
+    for (int i = 0; i < ntau; i++) {
+        const bool ab = H[i] > u;
+        any |= ab;
+        all &= ab;
+        if (ab) { if (fa < 0) fa = i; la = i; }
+        if (i > 0) {
+            if (!prev && ab && cin < 0) cin = i - 1;
+            if (prev && !ab) cout = i - 1;
+        }
+        prev = ab;
+    }
+    auto tau = [&](int i) -> double { return i < nle ? T[i] : ETA; };
+    double tin, tout;
+    if (!any) {
+        tin = T1; tout = T1;
+    } else if (all) {
+        tin = tau(0); tout = tau(ntau - 1);
+    } else {
+        tin = T1; tout = T1;
+        if (cin >= 0) {
+            const double t0 = tau(cin), t1 = tau(cin + 1), h0 = H[cin], h1 = H[cin + 1];
+            tin = t0 + ((u - h0) * (t1 - t0)) / (h1 - h0);
+        }
+        if (cout >= 0) {
+            const double t0 = tau(cout), t1 = tau(cout + 1), h0 = H[cout], h1 = H[cout + 1];
+            tout = t0 + ((u - h0) * (t1 - t0)) / (h1 - h0);
+        }
+        if (tin == T1) tin = tau(fa);
+        if (tout == T1) tout = tau(la);
+    }
+    r.tin = tin;
+    r.tout = tout;
+    if (tin == tout) {
+        r.status = SBR_NO_RUN_HR_BELOW_U | SBR_CONVERGED | lbits;
+        r.tol = 0.0;
+        return;
+    }
+
+    // ---------------- compute_ξ: bisection with bracketed lookups ----------------
+    uint32_t flag = 0;
+    const double tolerance = 10.0 * sbr_jl_eps(kappa);
+    double xnew = (tin + tout) / 2.0, xmin = tin, xmax = tout;
+    const bool okmin = in_range(xmin, tlo, thi, trunc, flag);
+    const bool okmax = in_range(xmax, tlo, thi, trunc, flag);
+    if (!okmin || !okmax) {
+        r.status = flag | lbits;
+        return;
+    }
+    int jlo = ssl_range(T, 0, n - 1, xmin);
+    int jhi = ssl_range(T, 0, n - 1, xmax);
+    const int jtin = jlo;
+    double c_ic_x = NAN, c_ic_v = 0.0, c_ice_x = NAN, c_ice_v = 0.0;
+    uint32_t s = SBR_NO_RUN_MAXITER;
+    double xi = NAN, tolr = INFINITY;
+    for (int iter = 1; iter <= max_iters; iter++) {
+        r.iters = iter;
+        const double dd = xmin - xmax;
+        if (fabs(dd) < 2.0 * sbr_jl_eps(dd)) { s = SBR_NO_RUN_COLLAPSE; break; }
+        if (iter == max_iters - 1) { s = SBR_NO_RUN_MAXITER; break; }
+        const double xo = xnew;
+        const double ic = dmin(tin, xo), oc = dmin(tout, xo);
+        const int j = ssl_range(T, jlo, jhi, xo); // t[jlo] <= ξmin <= xo <= ξmax < t[jhi+1]
+        // G(oc)
+        bool ok = in_range(oc, tlo, thi, trunc, flag);
+        int joc = (oc == xo) ? j : (ok ? ssl_range(T, 0, n - 1, oc) : 0);
+        const double Goc = ok ? lerp_at(T, G, n, joc, oc) : 0.0;
+        // G(ic) — ic == tin for every iterate of a valid bracket; cached by value
+        double Gic = 0.0;
+        int jic = 0;
+        if (in_range(ic, tlo, thi, trunc, flag)) {
+            jic = (ic == tin) ? jtin : (ic == xo ? j : ssl_range(T, 0, n - 1, ic));
+            if (ic == c_ic_x) Gic = c_ic_v;
+            else { Gic = lerp_at(T, G, n, jic, ic); c_ic_x = ic; c_ic_v = Gic; }
+        }
+        // ε = local knot spacing at ξ_old (solver.jl:336-338)
+        if (j + 1 >= n) { flag |= trunc ? SBR_ENGINE_TRUNC : SBR_OOB; break; }
+        const double eps = T[j + 1] - T[j];
+        double Goce = 0.0, Gice = 0.0;
+        const double xoe = oc + eps, xie = ic + eps;
+        if (in_range(xoe, tlo, thi, trunc, flag)) Goce = lerp_at(T, G, n, ssl_gallop(T, n, joc, xoe), xoe);
+        if (in_range(xie, tlo, thi, trunc, flag)) {
+            if (xie == c_ice_x) Gice = c_ice_v;
+            else { Gice = lerp_at(T, G, n, ssl_gallop(T, n, jic, xie), xie); c_ice_x = xie; c_ice_v = Gice; }
+        }
+        if (flag) break;
+        const double AW = Goc - Gic;
+        const double AWe = Goce - Gice;
+        const double err = AW - kappa;
+        const bool inc = AWe >= AW;
+        if (fabs(err) <= tolerance) {
+            if (inc) { s = SBR_RUN; xi = xo; tolr = fabs(err); }
+            else s = SBR_FALSE_EQ;
+            break;
+        } else if (err > 0) {
+            xmax = xo; jhi = j; xnew = 0.5 * (xo + xmin);
+        } else {
+            xmin = xo; jlo = j; xnew = 0.5 * (xo + xmax);
+        }
+    }
+    if (flag) { r.status = flag | lbits; return; }
+    if (s != SBR_RUN) { r.status = s | lbits; return; }
+
+    // ---------------- get_AW on the HR grid + AW_max ----------------
+    const double icc = (tin >= xi) ? xi : tin;
+    const double occ = (tout > xi) ? xi : tout;
+    if (!in_range(0.0, tlo, thi, trunc, flag)) { r.status = flag | lbits; return; }
+    const double G0 = lerp_at(T, G, n, ssl_range(T, 0, n - 1, 0.0), 0.0);
+    double mx = -INFINITY;
+    int ji = 0, jo = 0;
+    for (int i = 0; i < ntau; i++) {
+        const double ti = tau(i);
+        const double av = (ti - xi) + icc;
+        const double bv = (ti - xi) + occ;
+        const double xa = av > 0 ? av : 0.0;
+        const double xb = bv > 0 ? bv : 0.0;
+        if (!(xa <= thi) || !(xb <= thi)) { flag |= trunc ? SBR_ENGINE_TRUNC : SBR_OOB; break; }
+        while (ji + 1 < n && T[ji + 1] <= xa) ji++;
+        while (jo + 1 < n && T[jo + 1] <= xb) jo++;
+        const double gi = lerp_at(T, G, n, ji, xa);
+        const double go = lerp_at(T, G, n, jo, xb);
+        const double awin = av >= 0 ? gi : 0.0;
+        const double awout = bv >= 0 ? go : 0.0;
+        const double v = (awout - awin) + G0;
+        if (aw_path) aw_path[i] = v;
+        if (mx == mx && (v != v || v > mx)) mx = v;
+    }
+    if (flag) { r.status = flag | lbits; return; }
+    r.xi = xi;
+    r.tol = tolr;
+    r.aw = mx;
+    r.status = SBR_RUN | SBR_CONVERGED | lbits;
+}
+
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void equilibrium_kernel(LearnBufs L, const double* __restrict__ eta,
+                                                            const double* __restrict__ t_end,
+                                                            const double* __restrict__ u, EqArgs a, ResultSoA out)
+{
+    extern __shared__ double smem[];
+    const int b = blockIdx.y;
+    const int n = L.n_knots[b], ntau = L.n_tau[b], nle = L.n_le[b];
+    const uint32_t lst = L.status[b];
+    const size_t row = (size_t)b * (size_t)L.cap;
+    const double* __restrict__ gT = L.t + row;
+    const double* __restrict__ gG = L.G + row;
+    const double* __restrict__ gH = L.hr + row;
+    const bool fits = n <= a.lds_cap && ntau <= a.lds_cap;
+    double* sT = smem;
+    double* sG = smem + a.lds_cap;
+    double* sH = smem + 2 * a.lds_cap;
+    if (fits) {
+        for (int i = threadIdx.x; i < n; i += BLOCK) { sT[i] = gT[i]; sG[i] = gG[i]; }
+        for (int i = threadIdx.x; i < ntau; i += BLOCK) sH[i] = gH[i];
+    }
+    __syncthreads();
+    const int j = blockIdx.x * BLOCK + threadIdx.x;
+    if (j >= a.n_u) return;
+    const double uj = u[j];
+    const double ETA = eta[b], T1 = t_end[b];
+    const uint32_t lbits = lst & (SBR_ODE_MAXITERS | SBR_STIFF_SWITCH | SBR_ODE_FAILED | SBR_KNOT_OVERFLOW);
+    PointResult r;
+    if (lst & (SBR_ARG_INVALID | SBR_OOB) || n < 2 || !(uj >= 0.0)) {
+        r.xi = NAN; r.aw = NAN; r.tol = INFINITY; r.iters = 0;
+        r.tin = NAN; r.tout = NAN;
+        r.status = ((lst & SBR_ARG_INVALID) || !(uj >= 0.0)) ? SBR_ARG_INVALID : (SBR_OOB | lbits);
+    } else {
+        const bool trunc = gT[n - 1] < T1;
+        if (fits) solve_point(sT, sG, sH, n, ntau, nle, ETA, T1, trunc, uj, a.kappa, a.max_iters, lbits, r, a.aw_path);
+        else solve_point(gT, gG, gH, n, ntau, nle, ETA, T1, trunc, uj, a.kappa, a.max_iters, lbits, r, a.aw_path);
+    }
+    const size_t o = (size_t)b * (size_t)a.n_u + j;
+    out.xi[o] = r.xi;
+    out.tau_in_unc[o] = r.tin;
+    out.tau_out_unc[o] = r.tout;
+    out.aw_max[o] = r.aw;
+    out.tol[o] = r.tol;
+    out.status[o] = r.status;
+    if (out.iters) out.iters[o] = r.iters;
+}
+
+// ============================================================================
+// launchers
+// ============================================================================
+hipError_t launch_learn_logistic(const double* beta, const double* eta, const double* t_end, const LearnArgs& a,
+                                 const LearnBufs& L, hipStream_t s)
+{
+    dim3 grid((a.n_beta + 63) / 64);
+    hipLaunchKernelGGL(learn_logistic_kernel, grid, dim3(64), 0, s, beta, eta, t_end, a, L);
+    return hipGetLastError();
+}
+
+hipError_t launch_equilibrium(const LearnBufs& L, const double* eta, const double* t_end, const double* u,
+                              const EqArgs& a, const ResultSoA& out, int n_beta, hipStream_t s)
+{
+    const size_t lds = (size_t)3 * a.lds_cap * sizeof(double);
+    if (a.n_u >= 1024) {
+        dim3 grid((a.n_u + 1023) / 1024, n_beta);
+        hipLaunchKernelGGL(equilibrium_kernel<1024>, grid, dim3(1024), lds, s, L, eta, t_end, u, a, out);
+    } else if (a.n_u >= 256) {
+        dim3 grid((a.n_u + 255) / 256, n_beta);
+        hipLaunchKernelGGL(equilibrium_kernel<256>, grid, dim3(256), lds, s, L, eta, t_end, u, a, out);
+    } else {
+        dim3 grid((a.n_u + 63) / 64, n_beta);
+        hipLaunchKernelGGL(equilibrium_kernel<64>, grid, dim3(64), lds, s, L, eta, t_end, u, a, out);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace sbr

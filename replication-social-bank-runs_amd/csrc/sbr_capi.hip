@@ -1,0 +1,433 @@
+// sbr_capi.hip — the extern "C" boundary of libsbr (declared in include/sbr.h).
+//
+// A context owns one HIP device, one stream and a grow-only HBM workspace
+// (knot slabs sized n_beta × knot_capacity).  Host-pointer entry points stage
+// inputs, run the device pipeline and copy results back synchronously;
+// *_dev entry points only enqueue on the caller's stream.
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/sbr.h"
+#include "../../include/sbr_detmath.h"
+#include "sbr_kernels.h"
+
+struct sbr_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    // learning workspace
+    size_t ws_beta = 0, ws_cap = 0;
+    sbr::LearnBufs L{};
+    // host-API staging
+    void* stage = nullptr;
+    size_t stage_bytes = 0;
+    int lds_cap = 0;
+    // kernel timing (HIP events on the launch stream), opt-in via sbr_timing_enable
+    bool timing = false;
+    std::vector<hipEvent_t> ev_pool;
+    size_t ev_used = 0;
+};
+
+namespace {
+
+constexpr int kDefaultCap = 8192;
+
+int fail(sbr_ctx* c, int code, const char* what, hipError_t e = hipSuccess)
+{
+    if (c) {
+        c->err = what;
+        if (e != hipSuccess) { c->err += ": "; c->err += hipGetErrorString(e); }
+    }
+    return code;
+}
+
+#define HIP_TRY(ctx, expr, code)                                  \
+    do {                                                          \
+        hipError_t _e = (expr);                                   \
+        if (_e != hipSuccess) return fail((ctx), (code), #expr, _e); \
+    } while (0)
+
+void free_learn(sbr_ctx* c)
+{
+    void* ps[] = {c->L.t, c->L.G, c->L.hr, c->L.hrI, c->L.n_knots, c->L.n_tau, c->L.n_le, c->L.status,
+                  c->L.n_accept, c->L.n_reject};
+    for (void* p : ps)
+        if (p) (void)hipFree(p);
+    c->L = sbr::LearnBufs{};
+    c->ws_beta = c->ws_cap = 0;
+}
+
+int ensure_learn(sbr_ctx* c, size_t n_beta, size_t cap)
+{
+    if (n_beta <= c->ws_beta && cap == c->ws_cap) return SBR_OK;
+    free_learn(c);
+    const size_t slab = n_beta * cap * sizeof(double);
+    HIP_TRY(c, hipMalloc(&c->L.t, slab), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&c->L.G, slab), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&c->L.hr, slab), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&c->L.hrI, slab), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&c->L.n_knots, n_beta * 4), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&c->L.n_tau, n_beta * 4), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&c->L.n_le, n_beta * 4), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&c->L.status, n_beta * 4), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&c->L.n_accept, n_beta * 4), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&c->L.n_reject, n_beta * 4), SBR_ENOMEM);
+    c->L.cap = (int32_t)cap;
+    c->ws_beta = n_beta;
+    c->ws_cap = cap;
+    return SBR_OK;
+}
+
+int ensure_stage(sbr_ctx* c, size_t bytes)
+{
+    if (bytes <= c->stage_bytes) return SBR_OK;
+    if (c->stage) (void)hipFree(c->stage);
+    c->stage = nullptr;
+    c->stage_bytes = 0;
+    HIP_TRY(c, hipMalloc(&c->stage, bytes), SBR_ENOMEM);
+    c->stage_bytes = bytes;
+    return SBR_OK;
+}
+
+// EconomicParameters / LearningParameters scalar checks (model.jl:31-35, 71-76)
+bool scalars_valid(double x0, double p, double kappa, double lambda)
+{
+    return x0 >= 0.0 && p >= 0.0 && p <= 1.0 && kappa > 0.0 && kappa < 1.0 && lambda > 0.0;
+}
+
+sbr_opts resolve(const sbr_opts* o)
+{
+    sbr_opts r;
+    sbr_default_opts(&r);
+    if (o) {
+        r = *o;
+        if (r.knot_capacity <= 0) r.knot_capacity = kDefaultCap;
+        if (r.ode_maxiters <= 0) r.ode_maxiters = 100000;
+        if (r.bisect_max_iters <= 0) r.bisect_max_iters = 100;
+    }
+    return r;
+}
+
+hipEvent_t next_event(sbr_ctx* c)
+{
+    if (c->ev_used == c->ev_pool.size()) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        c->ev_pool.push_back(e);
+    }
+    return c->ev_pool[c->ev_used++];
+}
+
+void mark(sbr_ctx* c, hipStream_t s)
+{
+    if (!c->timing) return;
+    hipEvent_t e = next_event(c);
+    if (e) (void)hipEventRecord(e, s);
+}
+
+int run_baseline(sbr_ctx* c, hipStream_t s, const double* beta, const double* eta, const double* t_end, double x0,
+                 const double* u, int64_t n_beta, int64_t n_u, double p, double kappa, double lambda,
+                 const sbr_opts& o, const sbr::ResultSoA& out, double* aw_path)
+{
+    int rc = ensure_learn(c, (size_t)n_beta, (size_t)o.knot_capacity);
+    if (rc) return rc;
+    sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, p, lambda, o.ode_maxiters, (int32_t)n_beta, 1};
+    mark(c, s);
+    HIP_TRY(c, sbr::launch_learn_logistic(beta, eta, t_end, la, c->L, s), SBR_EDEVICE);
+    mark(c, s);
+    sbr::EqArgs ea{kappa, (int32_t)n_u, o.bisect_max_iters, c->lds_cap, aw_path};
+    HIP_TRY(c, sbr::launch_equilibrium(c->L, eta, t_end, u, ea, out, (int)n_beta, s), SBR_EDEVICE);
+    mark(c, s);
+    return SBR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+void sbr_default_opts(sbr_opts* o)
+{
+    o->ode_reltol = 2.220446049250313e-16;
+    o->ode_abstol = 2.220446049250313e-16;
+    o->ode_maxiters = 100000;
+    o->bisect_max_iters = 100;
+    o->early_exit_nan_run = 5;
+    o->knot_capacity = kDefaultCap;
+    o->reserved = 0;
+}
+
+int sbr_init(int device, sbr_ctx** out)
+{
+    if (!out) return SBR_EARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0 || device < 0 || device >= n) return SBR_EDEVICE;
+    sbr_ctx* c = new sbr_ctx();
+    c->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return SBR_EDEVICE;
+    }
+    int smem = 0;
+    (void)hipDeviceGetAttribute(&smem, hipDeviceAttributeMaxSharedMemoryPerBlock, device);
+    if (smem <= 0) smem = 65536;
+    // 3 doubles per staged knot (t, G, HR); keep 1 KiB slack
+    c->lds_cap = (smem - 1024) / 24;
+    *out = c;
+    return SBR_OK;
+}
+
+int sbr_free(sbr_ctx* c)
+{
+    if (!c) return SBR_OK;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    free_learn(c);
+    if (c->stage) (void)hipFree(c->stage);
+    for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+    return SBR_OK;
+}
+
+const char* sbr_last_error(const sbr_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int sbr_sweep_baseline_dev(sbr_ctx* c, void* stream, const double* beta, const double* eta, const double* t_end,
+                           double x0, const double* u, int64_t n_beta, int64_t n_u, double p, double kappa,
+                           double lambda, const sbr_opts* opts, sbr_result_soa* out)
+{
+    if (!c || !out) return SBR_EARG;
+    if (n_beta <= 0 || n_u <= 0 || n_beta > (1 << 30) || n_u > (1 << 30)) return fail(c, SBR_EARG, "grid size");
+    if (!scalars_valid(x0, p, kappa, lambda)) return fail(c, SBR_EARG, "ArgumentError: x0/p/kappa/lambda");
+    if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
+    sbr_opts o = resolve(opts);
+    sbr::ResultSoA r{out->xi, out->tau_in_unc, out->tau_out_unc, out->aw_max, out->tol, out->status, out->iters};
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    return run_baseline(c, s, beta, eta, t_end, x0, u, n_beta, n_u, p, kappa, lambda, o, r, nullptr);
+}
+
+int sbr_sweep_baseline(sbr_ctx* c, const double* beta, const double* eta, const double* t_end, double x0,
+                       const double* u, int64_t n_beta, int64_t n_u, double p, double kappa, double lambda,
+                       const sbr_opts* opts, sbr_result_soa* out)
+{
+    if (!c || !out || !beta || !eta || !t_end || !u) return SBR_EARG;
+    if (n_beta <= 0 || n_u <= 0) return fail(c, SBR_EARG, "grid size");
+    if (!scalars_valid(x0, p, kappa, lambda)) return fail(c, SBR_EARG, "ArgumentError: x0/p/kappa/lambda");
+    for (int64_t i = 0; i < n_beta; i++)
+        if (!(beta[i] > 0.0) || !(t_end[i] > 0.0) || !(eta[i] > 0.0))
+            return fail(c, SBR_EARG, "ArgumentError: beta/eta/t_end must be positive");
+    for (int64_t j = 0; j < n_u; j++)
+        if (!(u[j] >= 0.0)) return fail(c, SBR_EARG, "ArgumentError: u must be non-negative");
+    if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
+    sbr_opts o = resolve(opts);
+    const size_t np = (size_t)n_beta * (size_t)n_u;
+    const size_t in_bytes = (3 * (size_t)n_beta + (size_t)n_u) * 8;
+    const size_t out_bytes = np * (5 * 8 + 4 + 4);
+    int rc = ensure_stage(c, in_bytes + out_bytes + 256);
+    if (rc) return rc;
+    char* base = (char*)c->stage;
+    double* dbeta = (double*)base;
+    double* deta = dbeta + n_beta;
+    double* dtend = deta + n_beta;
+    double* du = dtend + n_beta;
+    double* dres = (double*)(base + ((in_bytes + 255) & ~(size_t)255));
+    sbr::ResultSoA r{dres, dres + np, dres + 2 * np, dres + 3 * np, dres + 4 * np, (uint32_t*)(dres + 5 * np),
+                     (int32_t*)((uint32_t*)(dres + 5 * np) + np)};
+    hipStream_t s = c->stream;
+    HIP_TRY(c, hipMemcpyAsync(dbeta, beta, n_beta * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+    HIP_TRY(c, hipMemcpyAsync(deta, eta, n_beta * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+    HIP_TRY(c, hipMemcpyAsync(dtend, t_end, n_beta * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+    HIP_TRY(c, hipMemcpyAsync(du, u, n_u * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+    rc = run_baseline(c, s, dbeta, deta, dtend, x0, du, n_beta, n_u, p, kappa, lambda, o, r, nullptr);
+    if (rc) return rc;
+    double* hs[5] = {out->xi, out->tau_in_unc, out->tau_out_unc, out->aw_max, out->tol};
+    for (int k = 0; k < 5; k++)
+        if (hs[k]) HIP_TRY(c, hipMemcpyAsync(hs[k], dres + k * np, np * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+    if (out->status) HIP_TRY(c, hipMemcpyAsync(out->status, r.status, np * 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+    if (out->iters) HIP_TRY(c, hipMemcpyAsync(out->iters, r.iters, np * 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+    HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
+    if (o.early_exit_nan_run > 0 && out->status && out->xi && out->aw_max && out->tol)
+        sbr_apply_early_exit(n_beta, n_u, o.early_exit_nan_run, out);
+    return SBR_OK;
+}
+
+int sbr_learn_baseline(sbr_ctx* c, const double* beta, const double* eta, const double* t_end, double x0,
+                       int64_t n_beta, int32_t stop_after_eta, const sbr_opts* opts, double* t_out, double* G_out,
+                       int64_t cap, int32_t* n_knots, uint32_t* status)
+{
+    if (!c || !beta || !eta || !t_end || n_beta <= 0 || cap <= 0) return SBR_EARG;
+    if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
+    sbr_opts o = resolve(opts);
+    if (cap < o.knot_capacity) o.knot_capacity = (int32_t)cap;
+    int rc = ensure_learn(c, (size_t)n_beta, (size_t)o.knot_capacity);
+    if (rc) return rc;
+    rc = ensure_stage(c, 3 * (size_t)n_beta * 8);
+    if (rc) return rc;
+    double* dbeta = (double*)c->stage;
+    double* deta = dbeta + n_beta;
+    double* dtend = deta + n_beta;
+    hipStream_t s = c->stream;
+    HIP_TRY(c, hipMemcpyAsync(dbeta, beta, n_beta * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+    HIP_TRY(c, hipMemcpyAsync(deta, eta, n_beta * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+    HIP_TRY(c, hipMemcpyAsync(dtend, t_end, n_beta * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+    sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, 0.5, 1.0, o.ode_maxiters, (int32_t)n_beta, stop_after_eta};
+    HIP_TRY(c, sbr::launch_learn_logistic(dbeta, deta, dtend, la, c->L, s), SBR_EDEVICE);
+    const size_t w = (size_t)o.knot_capacity;
+    if (t_out)
+        HIP_TRY(c, hipMemcpy2DAsync(t_out, cap * 8, c->L.t, w * 8, w * 8, n_beta, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+    if (G_out)
+        HIP_TRY(c, hipMemcpy2DAsync(G_out, cap * 8, c->L.G, w * 8, w * 8, n_beta, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+    if (n_knots) HIP_TRY(c, hipMemcpyAsync(n_knots, c->L.n_knots, n_beta * 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+    if (status) HIP_TRY(c, hipMemcpyAsync(status, c->L.status, n_beta * 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+    HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
+    return SBR_OK;
+}
+
+int sbr_solve_point_paths(sbr_ctx* c, double beta, double eta, double t_end, double x0, double u, double p,
+                          double kappa, double lambda, const sbr_opts* opts, double* res, uint32_t* status,
+                          double* tau, double* hr, double* aw_cum, int64_t cap, int64_t* n_tau)
+{
+    if (!c || !res || !status) return SBR_EARG;
+    if (!scalars_valid(x0, p, kappa, lambda) || !(beta > 0) || !(eta > 0) || !(t_end > 0) || !(u >= 0))
+        return fail(c, SBR_EARG, "ArgumentError");
+    if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
+    sbr_opts o = resolve(opts);
+    const size_t kc = (size_t)o.knot_capacity;
+    int rc = ensure_stage(c, 4 * 8 + 5 * 8 + 8 + kc * 8 + 256);
+    if (rc) return rc;
+    double* d = (double*)c->stage;
+    double hin[4] = {beta, eta, t_end, u};
+    hipStream_t s = c->stream;
+    HIP_TRY(c, hipMemcpyAsync(d, hin, 32, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+    double* dres = d + 4;
+    uint32_t* dst = (uint32_t*)(dres + 5);
+    double* dpath = dres + 6 + 1;
+    sbr::ResultSoA r{dres, dres + 1, dres + 2, dres + 3, dres + 4, dst, nullptr};
+    rc = run_baseline(c, s, d, d + 1, d + 2, x0, d + 3, 1, 1, p, kappa, lambda, o, r, dpath);
+    if (rc) return rc;
+    HIP_TRY(c, hipMemcpyAsync(res, dres, 40, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+    HIP_TRY(c, hipMemcpyAsync(status, dst, 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+    int32_t nt = 0, nle = 0, nk = 0;
+    HIP_TRY(c, hipMemcpyAsync(&nt, c->L.n_tau, 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+    HIP_TRY(c, hipMemcpyAsync(&nle, c->L.n_le, 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+    HIP_TRY(c, hipMemcpyAsync(&nk, c->L.n_knots, 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+    HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
+    if (n_tau) *n_tau = nt;
+    if (nt > cap) return fail(c, SBR_EARG, "path capacity too small");
+    if (tau) {
+        HIP_TRY(c, hipMemcpy(tau, c->L.t, (size_t)nle * 8, hipMemcpyDeviceToHost), SBR_EDEVICE);
+        if (nt > nle) tau[nle] = eta;
+    }
+    if (hr) HIP_TRY(c, hipMemcpy(hr, c->L.hr, (size_t)nt * 8, hipMemcpyDeviceToHost), SBR_EDEVICE);
+    if (aw_cum) {
+        if (*status & SBR_RUN) HIP_TRY(c, hipMemcpy(aw_cum, dpath, (size_t)nt * 8, hipMemcpyDeviceToHost), SBR_EDEVICE);
+        else for (int i = 0; i < nt; i++) aw_cum[i] = NAN;
+    }
+    (void)nk;
+    return SBR_OK;
+}
+
+int sbr_timing_enable(sbr_ctx* c, int on)
+{
+    if (!c) return SBR_EARG;
+    c->timing = on != 0;
+    c->ev_used = 0;
+    return SBR_OK;
+}
+
+int sbr_timing_read(sbr_ctx* c, void* stream, double* learn_ms, double* eq_ms, int32_t* n_calls)
+{
+    if (!c) return SBR_EARG;
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
+    double a = 0.0, b = 0.0;
+    int32_t n = 0;
+    for (size_t i = 0; i + 3 <= c->ev_used; i += 3) {
+        float t1 = 0.f, t2 = 0.f;
+        HIP_TRY(c, hipEventElapsedTime(&t1, c->ev_pool[i], c->ev_pool[i + 1]), SBR_EDEVICE);
+        HIP_TRY(c, hipEventElapsedTime(&t2, c->ev_pool[i + 1], c->ev_pool[i + 2]), SBR_EDEVICE);
+        a += t1;
+        b += t2;
+        n++;
+    }
+    if (learn_ms) *learn_ms = a;
+    if (eq_ms) *eq_ms = b;
+    if (n_calls) *n_calls = n;
+    c->ev_used = 0;
+    return SBR_OK;
+}
+
+int sbr_learn_stats(sbr_ctx* c, int64_t n_beta, int32_t* n_knots, int32_t* n_tau, int32_t* n_accept,
+                    int32_t* n_reject, uint32_t* status)
+{
+    if (!c || n_beta <= 0 || (size_t)n_beta > c->ws_beta) return SBR_EARG;
+    if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
+    HIP_TRY(c, hipDeviceSynchronize(), SBR_EDEVICE);
+    struct { int32_t* h; void* d; } cp[] = {{n_knots, c->L.n_knots}, {n_tau, c->L.n_tau}, {n_accept, c->L.n_accept},
+                                           {n_reject, c->L.n_reject}, {(int32_t*)status, c->L.status}};
+    for (auto& x : cp)
+        if (x.h) HIP_TRY(c, hipMemcpy(x.h, x.d, (size_t)n_beta * 4, hipMemcpyDeviceToHost), SBR_EDEVICE);
+    return SBR_OK;
+}
+
+void sbr_apply_early_exit(int64_t n_beta, int64_t n_u, int32_t threshold, sbr_result_soa* r)
+{
+    for (int64_t b = 0; b < n_beta; b++) {
+        int32_t cnt = 0;
+        for (int64_t j = 0; j < n_u; j++) {
+            const int64_t o = b * n_u + j;
+            if (cnt >= threshold) {
+                r->xi[o] = NAN;
+                r->aw_max[o] = NAN;
+                r->tol[o] = INFINITY;
+                r->status[o] = SBR_SKIPPED_EARLY_EXIT;
+                continue;
+            }
+            if (r->status[o] & SBR_RUN) cnt = 0;
+            else cnt++;
+        }
+    }
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Diagnostics: evaluate the shared deterministic math on the device so tests
+// can check host/device bit equality of sbr_exp / sbr_log / sbr_pow_pos.
+// ---------------------------------------------------------------------------
+namespace {
+__global__ void detmath_kernel(const double* x, const double* y, int n, double* e, double* l, double* pw)
+{
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    e[i] = sbr_exp(x[i]);
+    l[i] = sbr_log(x[i]);
+    pw[i] = sbr_pow_pos(x[i], y[i]);
+}
+}  // namespace
+
+extern "C" int sbr_selftest_detmath(sbr_ctx* c, const double* x, const double* y, int n, double* e, double* l,
+                                    double* pw)
+{
+    if (!c || n <= 0) return SBR_EARG;
+    if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
+    int rc = ensure_stage(c, (size_t)n * 5 * 8);
+    if (rc) return rc;
+    double* d = (double*)c->stage;
+    hipStream_t s = c->stream;
+    HIP_TRY(c, hipMemcpyAsync(d, x, n * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+    HIP_TRY(c, hipMemcpyAsync(d + n, y, n * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+    hipLaunchKernelGGL(detmath_kernel, dim3((n + 255) / 256), dim3(256), 0, s, d, d + n, n, d + 2 * n, d + 3 * n,
+                       d + 4 * n);
+    HIP_TRY(c, hipGetLastError(), SBR_EDEVICE);
+    HIP_TRY(c, hipMemcpyAsync(e, d + 2 * n, n * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+    HIP_TRY(c, hipMemcpyAsync(l, d + 3 * n, n * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+    HIP_TRY(c, hipMemcpyAsync(pw, d + 4 * n, n * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+    HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
+    return SBR_OK;
+}

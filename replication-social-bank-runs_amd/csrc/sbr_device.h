@@ -1,0 +1,107 @@
+// sbr_device.h — device-side building blocks shared by the gfx950 kernels:
+// the Tsit5 tableau, OrdinaryDiffEq's PI controller, and exact knot-grid
+// lookups (searchsortedlast + Interpolations.jl gridded-linear evaluation).
+//
+// Every formula here is written to reproduce oracle/sbr_oracle.c bit for bit
+// (both sides compile with -ffp-contract=off; fma() only where the oracle has
+// it).  The lookups are *faster* than the oracle's — bracketed and galloping
+// searches instead of full binary searches — but always return the same
+// bracket index, so the interpolated value is identical.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/sbr_detmath.h"
+#include "../../include/sbr_status.h"
+
+namespace sbr {
+
+// ---- Tsit5 (Tsitouras 2011) as in OrdinaryDiffEqTsit5 --------------------
+constexpr double C1 = 0.161, C2 = 0.327, C3 = 0.9, C4 = 0.9800255409045097;
+constexpr double A21 = 0.161;
+constexpr double A31 = -0.008480655492356989, A32 = 0.335480655492357;
+constexpr double A41 = 2.897153057105493, A42 = -6.359448489975075, A43 = 4.3622954328695815;
+constexpr double A51 = 5.325864828439257, A52 = -11.748883564062828, A53 = 7.4955393428898365,
+                 A54 = -0.09249506636175525;
+constexpr double A61 = 5.86145544294642, A62 = -12.92096931784711, A63 = 8.159367898576159,
+                 A64 = -0.071584973281401, A65 = -0.028269050394068383;
+constexpr double A71 = 0.09646076681806523, A72 = 0.01, A73 = 0.4798896504144996, A74 = 1.379008574103742,
+                 A75 = -3.290069515436081, A76 = 2.324710524099774;
+constexpr double BT1 = -0.00178001105222577714, BT2 = -0.0008164344596567469, BT3 = 0.007880878010261995,
+                 BT4 = -0.1447110071732629, BT5 = 0.5823571654525552, BT6 = -0.45808210592918697,
+                 BT7 = 0.015151515151515152;
+constexpr double TSIT5_STABILITY = 3.5068469938049235;
+
+// ---- PI controller defaults (OrdinaryDiffEqCore, 5th-order method) -------
+constexpr double CTL_BETA1 = 0.14, CTL_BETA2 = 0.08, CTL_INV_QMIN = 5.0, CTL_INV_QMAX = 0.1, CTL_GAMMA = 0.9,
+                 CTL_QOLDMIN = 1e-4;
+constexpr double AUTOSWITCH_TOL = 0.9;
+constexpr int AUTOSWITCH_MAXSTIFF = 10;
+constexpr double DBL_EPS = 2.220446049250313e-16;
+
+__device__ __forceinline__ double dmin(double a, double b) { return a < b ? a : b; }
+__device__ __forceinline__ double dmax(double a, double b) { return a > b ? a : b; }
+
+// stepsize_controller!(::PIController): returns q, updates q11
+__device__ __forceinline__ double pi_q(double EEst, double qold, double& q11)
+{
+    if (EEst == 0.0) return CTL_INV_QMAX;
+    q11 = sbr_pow_pos(EEst, CTL_BETA1);
+    double q = q11 / sbr_pow_pos(qold, CTL_BETA2);
+    return dmax(CTL_INV_QMAX, dmin(CTL_INV_QMIN, q / CTL_GAMMA));
+}
+
+struct AutoSwitch {
+    int count = 0;
+    bool switched = false;
+    __device__ __forceinline__ void update(double eig, double dt)
+    {
+        double stiffness = fabs(eig * dt / TSIT5_STABILITY);
+        bool st = stiffness > AUTOSWITCH_TOL;
+        if (st) count = count < 0 ? 1 : count + 1;
+        else count = count > 0 ? -1 : count - 1;
+        if (count > AUTOSWITCH_MAXSTIFF) switched = true;
+    }
+};
+
+// ---- knot-grid lookups ----------------------------------------------------
+// searchsortedlast restricted to [lo, hi]; requires t[lo] <= x and that the
+// true answer is <= hi.  Returns the largest j in [lo, hi] with t[j] <= x.
+template <class P>
+__device__ __forceinline__ int ssl_range(P t, int lo, int hi, double x)
+{
+    while (lo < hi) {
+        int mid = (lo + hi + 1) >> 1;
+        if (t[mid] <= x) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+// searchsortedlast from a hint j0 with t[j0] <= x (exponential gallop forward).
+template <class P>
+__device__ __forceinline__ int ssl_gallop(P t, int n, int j0, double x)
+{
+    int lo = j0, step = 1;
+    while (lo + step < n && t[lo + step] <= x) {
+        lo += step;
+        step <<= 1;
+    }
+    int hi = lo + step - 1;
+    if (hi > n - 1) hi = n - 1;
+    return ssl_range(t, lo, hi, x);
+}
+
+// Interpolations.jl gridded Linear on bracket j (clamped to [0, n-2]):
+// v[j]*(1-δ) + v[j+1]*δ with δ = (x - t[j]) / (t[j+1] - t[j]).
+template <class P, class Q>
+__device__ __forceinline__ double lerp_at(P t, Q v, int n, int j, double x)
+{
+    if (j > n - 2) j = n - 2;
+    if (j < 0) j = 0;
+    double d = (x - t[j]) / (t[j + 1] - t[j]);
+    return v[j] * (1.0 - d) + v[j + 1] * d;
+}
+
+}  // namespace sbr

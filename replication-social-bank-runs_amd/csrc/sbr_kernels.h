@@ -1,0 +1,50 @@
+// sbr_kernels.h — argument blocks and launchers of the gfx950 kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sbr {
+
+// Per-β learning output, row-major [n_beta][cap] in HBM.
+struct LearnBufs {
+    double* t;          // knot times (sol.t)
+    double* G;          // CDF at knots (sol.u)
+    double* hr;         // hazard rate on the τ̄ grid (solver.jl:180-182)
+    double* hrI;        // cumulative trapezoid ∫_0^τ̄ e^{λs} g(s) ds on the τ̄ grid
+    int32_t* n_knots;   // stored knots
+    int32_t* n_tau;     // length of the τ̄ grid
+    int32_t* n_le;      // knots with t <= η (τ̄[i] = t[i] for i < n_le, τ̄[n_le] = η)
+    uint32_t* status;   // learning-level SBR_* bits
+    int32_t* n_accept;  // accepted RK steps (flop accounting)
+    int32_t* n_reject;  // rejected RK steps
+    int32_t cap;
+};
+
+struct LearnArgs {
+    double x0, rtol, atol, p, lam;
+    int64_t maxiters;
+    int32_t n_beta;
+    int32_t stop_after_eta;
+};
+
+struct EqArgs {
+    double kappa;
+    int32_t n_u;
+    int32_t max_iters;
+    int32_t lds_cap;    // knots staged in LDS per workgroup (3 doubles each)
+    double* aw_path;    // optional AW_cum(τ̄) output for single-point mode (n_u == 1)
+};
+
+struct ResultSoA {
+    double *xi, *tau_in_unc, *tau_out_unc, *aw_max, *tol;
+    uint32_t* status;
+    int32_t* iters;
+};
+
+hipError_t launch_learn_logistic(const double* beta, const double* eta, const double* t_end, const LearnArgs& a,
+                                 const LearnBufs& L, hipStream_t s);
+hipError_t launch_equilibrium(const LearnBufs& L, const double* eta, const double* t_end, const double* u,
+                              const EqArgs& a, const ResultSoA& out, int n_beta, hipStream_t s);
+
+}  // namespace sbr

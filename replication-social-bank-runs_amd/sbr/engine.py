@@ -1,0 +1,263 @@
+"""Host-side mirror of the reference's learning/solver call surface, backed by
+libsbr's gfx950 kernels.
+
+Reference call surface → here:
+  solve_learning(::LearningParameters)              learning.jl:109   → solve_learning(lp)
+  solve_equilibrium_baseline(lr, econ)              solver.jl:413     → solve_equilibrium_baseline(lr, econ)
+  get_AW_functions!(result)                         solver.jl:553     → get_AW_functions(result)
+  the Fig 4 / Fig 5 double loops                    1_baseline.jl:151-192, 224-267
+                                                                      → Engine.sweep_baseline(grid)
+There is no CPU fallback: without libsbr.so or a GPU every call raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib
+from ._lib import SBRNativeError, check
+from .grids import BaselineGrid
+from .model import EconomicParameters, LearningParameters
+
+_P = ctypes.c_void_p
+
+RESULT_FIELDS = ("xi", "tau_in_unc", "tau_out_unc", "aw_max", "tol")
+
+
+def _ptr(a: np.ndarray | None):
+    return None if a is None else a.ctypes.data_as(_P)
+
+
+class Engine:
+    """One libsbr context on one HIP device."""
+
+    def __init__(self, device: int | None = None):
+        if device is None:
+            device = int(os.environ.get("LOCAL_RANK", "0"))
+        self.device = device
+        L = _lib.load()
+        ctx = _P()
+        rc = L.sbr_init(device, ctypes.byref(ctx))
+        if rc != 0:
+            raise SBRNativeError(f"sbr_init(device={device}) failed ({rc}): no usable HIP device")
+        self._ctx = ctx
+        self._L = L
+
+    def close(self):
+        if getattr(self, "_ctx", None):
+            self._L.sbr_free(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ sweeps
+    def sweep_baseline(self, grid: BaselineGrid, early_exit: int = 0, max_iters: int = 100,
+                       knot_capacity: int = 8192, with_iters: bool = True) -> dict:
+        """Every (β, u) of ``grid`` through learning → HR → buffers → bisection
+        → AW_max.  Returns [n_beta, n_u] arrays (row i = β_i).  ``early_exit=5``
+        applies the reference's 5-consecutive-no-run rule as a post-pass."""
+        nb, nu = grid.shape
+        out = {k: np.empty(nb * nu) for k in RESULT_FIELDS}
+        out["status"] = np.empty(nb * nu, np.uint32)
+        out["iters"] = np.empty(nb * nu, np.int32) if with_iters else None
+        soa = _lib.ResultSoA(*[_ptr(out[k]) for k in (*RESULT_FIELDS, "status", "iters")])
+        opts = _lib.default_opts(early_exit_nan_run=early_exit, bisect_max_iters=max_iters,
+                                 knot_capacity=knot_capacity)
+        rc = self._L.sbr_sweep_baseline(self._ctx, _ptr(grid.beta), _ptr(grid.eta), _ptr(grid.t_end), grid.x0,
+                                        _ptr(grid.u), nb, nu, grid.p, grid.kappa, grid.lam, ctypes.byref(opts),
+                                        ctypes.byref(soa))
+        check(rc, self._ctx, "sbr_sweep_baseline")
+        return {k: (v.reshape(nb, nu) if v is not None else None) for k, v in out.items()}
+
+    def sweep_baseline_dev(self, beta, eta, t_end, u, p, kappa, lam, x0, out: dict, stream: int | None = None,
+                           max_iters: int = 100, knot_capacity: int = 8192):
+        """Device-pointer variant on torch tensors (float64 cuda) — no host sync.
+        ``out`` holds preallocated tensors xi/tau_in_unc/tau_out_unc/aw_max/tol
+        (float64), status (int32 viewed as uint32) and optional iters (int32)."""
+        nb, nu = beta.numel(), u.numel()
+        soa = _lib.ResultSoA(*[(out[k].data_ptr() if out.get(k) is not None else None)
+                               for k in (*RESULT_FIELDS, "status", "iters")])
+        opts = _lib.default_opts(early_exit_nan_run=0, bisect_max_iters=max_iters, knot_capacity=knot_capacity)
+        rc = self._L.sbr_sweep_baseline_dev(self._ctx, stream, beta.data_ptr(), eta.data_ptr(), t_end.data_ptr(),
+                                            x0, u.data_ptr(), nb, nu, p, kappa, lam, ctypes.byref(opts),
+                                            ctypes.byref(soa))
+        check(rc, self._ctx, "sbr_sweep_baseline_dev")
+
+    def learn_baseline(self, beta, eta, t_end, x0=1e-4, stop_after_eta=False, cap=8192):
+        beta = np.ascontiguousarray(beta, np.float64)
+        nb = len(beta)
+        eta = np.ascontiguousarray(np.broadcast_to(eta, beta.shape), np.float64)
+        t_end = np.ascontiguousarray(np.broadcast_to(t_end, beta.shape), np.float64)
+        T = np.zeros((nb, cap))
+        G = np.zeros((nb, cap))
+        nk = np.zeros(nb, np.int32)
+        st = np.zeros(nb, np.uint32)
+        opts = _lib.default_opts(knot_capacity=cap)
+        rc = self._L.sbr_learn_baseline(self._ctx, _ptr(beta), _ptr(eta), _ptr(t_end), x0, nb, int(stop_after_eta),
+                                        ctypes.byref(opts), _ptr(T), _ptr(G), cap, _ptr(nk), _ptr(st))
+        check(rc, self._ctx, "sbr_learn_baseline")
+        return [(T[i, : nk[i]].copy(), G[i, : nk[i]].copy(), int(st[i])) for i in range(nb)]
+
+    def solve_point_paths(self, beta, eta, t_end, u, p, kappa, lam, x0=1e-4, cap=8192):
+        res = np.zeros(5)
+        st = np.zeros(1, np.uint32)
+        tau = np.zeros(cap)
+        hr = np.zeros(cap)
+        aw = np.zeros(cap)
+        nt = np.zeros(1, np.int64)
+        opts = _lib.default_opts(knot_capacity=cap)
+        rc = self._L.sbr_solve_point_paths(self._ctx, beta, eta, t_end, x0, u, p, kappa, lam, ctypes.byref(opts),
+                                           _ptr(res), _ptr(st), _ptr(tau), _ptr(hr), _ptr(aw), cap, _ptr(nt))
+        check(rc, self._ctx, "sbr_solve_point_paths")
+        k = int(nt[0])
+        return dict(xi=res[0], tau_in_unc=res[1], tau_out_unc=res[2], aw_max=res[3], tol=res[4],
+                    status=int(st[0]), tau=tau[:k].copy(), hr=hr[:k].copy(), aw_cum=aw[:k].copy())
+
+    def timing_enable(self, on: bool = True):
+        check(self._L.sbr_timing_enable(self._ctx, int(on)), self._ctx, "sbr_timing_enable")
+
+    def timing_read(self, stream: int | None = None):
+        """(learn_ms_total, equilibrium_ms_total, n_calls) since the last read."""
+        a, b, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int32()
+        check(self._L.sbr_timing_read(self._ctx, stream, ctypes.byref(a), ctypes.byref(b), ctypes.byref(n)),
+              self._ctx, "sbr_timing_read")
+        return a.value, b.value, n.value
+
+    def learn_stats(self, n_beta: int) -> dict:
+        out = {k: np.zeros(n_beta, np.int32) for k in ("n_knots", "n_tau", "n_accept", "n_reject")}
+        out["status"] = np.zeros(n_beta, np.uint32)
+        check(self._L.sbr_learn_stats(self._ctx, n_beta, *[_ptr(out[k]) for k in
+                                                         ("n_knots", "n_tau", "n_accept", "n_reject", "status")]),
+              self._ctx, "sbr_learn_stats")
+        return out
+
+    def selftest_detmath(self, x, y):
+        x = np.ascontiguousarray(x, np.float64)
+        y = np.ascontiguousarray(y, np.float64)
+        n = len(x)
+        e, l, pw = np.empty(n), np.empty(n), np.empty(n)
+        rc = self._L.sbr_selftest_detmath(self._ctx, _ptr(x), _ptr(y), n, _ptr(e), _ptr(l), _ptr(pw))
+        check(rc, self._ctx, "sbr_selftest_detmath")
+        return e, l, pw
+
+
+_default: Engine | None = None
+
+
+def default_engine() -> Engine:
+    global _default
+    if _default is None:
+        _default = Engine()
+    return _default
+
+
+# ---------------------------------------------------------------------------
+# Interpolations.jl-like gridded linear interpolant (host side, for the
+# plotting drop-in; the hot path never uses it).
+# ---------------------------------------------------------------------------
+class LinearInterpolation:
+    """Gridded Linear with Throw() extrapolation: exact at knots, BoundsError
+    (IndexError here) outside [knots[0], knots[-1]]."""
+
+    def __init__(self, knots, values):
+        self.knots = np.asarray(knots, np.float64)
+        self.coefs = np.asarray(values, np.float64)
+
+    def __call__(self, x):
+        x = np.asarray(x, np.float64)
+        if np.any(~((x >= self.knots[0]) & (x <= self.knots[-1]))):
+            raise IndexError("BoundsError: interpolation outside the knot range")
+        n = len(self.knots)
+        j = np.clip(np.searchsorted(self.knots, x, side="right") - 1, 0, n - 2)
+        t0, t1 = self.knots[j], self.knots[j + 1]
+        d = (x - t0) / (t1 - t0)
+        v = self.coefs[j] * (1.0 - d) + self.coefs[j + 1] * d
+        return v if v.ndim else float(v)
+
+
+@dataclass
+class LearningResults:
+    """learning.jl:74-81 (grid = knots of the adaptive ODE solution)."""
+
+    params: LearningParameters
+    learning_cdf: LinearInterpolation
+    learning_pdf: LinearInterpolation
+    grid: np.ndarray
+    status: int = 0
+
+
+@dataclass
+class SolvedModel:
+    """solver.jl:55-109 (fields + derived τ_IN/τ_OUT; HR as an interpolant)."""
+
+    xi: float
+    tau_bar_IN_UNC: float
+    tau_bar_OUT_UNC: float
+    HR: LinearInterpolation
+    bankrun: bool
+    model_params: tuple
+    learning_results: LearningResults
+    converged: bool
+    tolerance: float
+    status: int
+    aw_cum: np.ndarray = field(repr=False, default=None)
+    aw: dict | None = field(repr=False, default=None)
+
+    @property
+    def tau_IN(self):
+        return max(self.xi - self.tau_bar_IN_UNC, 0.0) if self.xi == self.xi else float("nan")
+
+    @property
+    def tau_OUT(self):
+        return max(self.xi - self.tau_bar_OUT_UNC, 0.0) if self.xi == self.xi else float("nan")
+
+
+def solve_learning(lp: LearningParameters, engine: Engine | None = None) -> LearningResults:
+    """learning.jl:109-124 on the GPU (full tspan, like the reference)."""
+    if lp.tspan[0] != 0.0:
+        raise _lib.ArgumentError("the engine integrates from t = 0 (every reference call site does)")
+    eng = engine or default_engine()
+    (t, G, st), = eng.learn_baseline([lp.beta], [lp.tspan[1]], [lp.tspan[1]], lp.x0, stop_after_eta=False)
+    g = (lp.beta * G) * (1.0 - G)
+    return LearningResults(lp, LinearInterpolation(t, G), LinearInterpolation(t, g), t, st)
+
+
+def solve_equilibrium_baseline(lr: LearningResults, econ: EconomicParameters,
+                               engine: Engine | None = None) -> SolvedModel:
+    """solver.jl:413-462 for one point, with the HR and AW paths (GPU)."""
+    eng = engine or default_engine()
+    lp = lr.params
+    r = eng.solve_point_paths(lp.beta, econ.eta, lp.tspan[1], econ.u, econ.p, econ.kappa, econ.lam, lp.x0)
+    st = r["status"]
+    bankrun = bool(st & _lib.SBR_RUN)
+    return SolvedModel(r["xi"], r["tau_in_unc"], r["tau_out_unc"], LinearInterpolation(r["tau"], r["hr"]), bankrun,
+                       (lp, econ), lr, bool(st & _lib.SBR_CONVERGED), r["tol"], st, aw_cum=r["aw_cum"])
+
+
+def get_AW_functions(result: SolvedModel):
+    """solver.jl:553-576: AW_cum/AW_OUT/AW_IN interpolants on the HR grid and
+    AW_max, or None when there is no run.  AW_OUT/AW_IN are rebuilt on the host
+    from the GPU's ξ, τ̄ and G (plotting only)."""
+    if result.aw is not None:
+        return result.aw
+    if not result.bankrun:
+        return None
+    tg = result.HR.knots
+    cdf = result.learning_results.learning_cdf
+    xi, tin, tout = result.xi, result.tau_bar_IN_UNC, result.tau_bar_OUT_UNC
+    ic = xi if tin >= xi else tin
+    oc = xi if tout > xi else tout
+    a = (tg - xi) + ic
+    b = (tg - xi) + oc
+    aw_in = np.where(a >= 0, cdf(np.where(a > 0, a, 0.0)), 0.0)
+    aw_out = np.where(b >= 0, cdf(np.where(b > 0, b, 0.0)), 0.0)
+    result.aw = dict(AW_cum=LinearInterpolation(tg, result.aw_cum), AW_OUT=LinearInterpolation(tg, aw_out),
+                     AW_IN=LinearInterpolation(tg, aw_in), AW_max=float(np.max(result.aw_cum)))
+    return result.aw

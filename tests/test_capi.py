@@ -1,0 +1,65 @@
+"""The C ABI: libsbr.so loads in the build container and exports every entry
+point include/sbr.h declares; without a GPU the product path fails loudly
+(no CPU fallback)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import sbr
+from sbr import _lib
+
+
+def test_header_declares_the_boundary():
+    syms = sbr.header_symbols()
+    for s in ("sbr_init", "sbr_free", "sbr_sweep_baseline", "sbr_sweep_baseline_dev", "sbr_learn_baseline",
+              "sbr_solve_point_paths", "sbr_apply_early_exit"):
+        assert s in syms
+
+
+def test_library_exports_every_header_symbol():
+    L = sbr.load()
+    missing = [s for s in sbr.header_symbols() if not hasattr(L, s)]
+    assert not missing
+
+
+def test_default_opts_are_the_reference_defaults():
+    o = _lib.default_opts()
+    assert o.ode_reltol == np.finfo(np.float64).eps == o.ode_abstol  # learning.jl:43
+    assert o.ode_maxiters == 100000
+    assert o.bisect_max_iters == 100  # solver.jl:309
+    assert o.early_exit_nan_run == 5  # 1_baseline.jl:147,221
+
+
+def test_status_bits_are_distinct():
+    vals = list(sbr.STATUS.values())
+    assert len(vals) == len(set(vals))
+    assert all(v & (v - 1) == 0 for v in vals)
+
+
+def test_early_exit_post_pass_matches_oracle(oracle):
+    """sbr_apply_early_exit is host code in libsbr: same result as the oracle's rule."""
+    rng = np.random.default_rng(1)
+    nb, nu = 7, 60
+    st = np.where(rng.random((nb, nu)) < 0.6, sbr.STATUS["SBR_RUN"] | sbr.STATUS["SBR_CONVERGED"],
+                  sbr.STATUS["SBR_NO_RUN_HR_BELOW_U"]).astype(np.uint32)
+    st[:, 40:] = sbr.STATUS["SBR_NO_RUN_HR_BELOW_U"]
+    base = dict(xi=rng.random((nb, nu)), aw_max=rng.random((nb, nu)), tol=rng.random((nb, nu)), status=st)
+    o = oracle.apply_early_exit(base, 5)
+    arrs = {k: np.ascontiguousarray(v.copy()) for k, v in base.items()}
+    P = ctypes.c_void_p
+    soa = _lib.ResultSoA(arrs["xi"].ctypes.data_as(P), None, None, arrs["aw_max"].ctypes.data_as(P),
+                         arrs["tol"].ctypes.data_as(P), arrs["status"].ctypes.data_as(P), None)
+    sbr.load().sbr_apply_early_exit(nb, nu, 5, ctypes.byref(soa))
+    for k in ("xi", "aw_max", "tol", "status"):
+        a, b = arrs[k], o[k]
+        assert np.all((a == b) | (np.isnan(a) & np.isnan(b))), k
+
+
+def test_no_gpu_means_loud_failure():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    with pytest.raises(sbr.SBRNativeError):
+        sbr.Engine(0)

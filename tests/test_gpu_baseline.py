@@ -1,0 +1,155 @@
+"""GPU parity: the gfx950 kernels, called through libsbr's C ABI, against the
+CPU oracle on the same inputs — bit for bit — and against the reference's
+golden figures at full size."""
+import numpy as np
+import pytest
+
+import sbr
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = ("xi", "tau_in_unc", "tau_out_unc", "aw_max", "tol")
+
+
+def assert_bitwise(a, b, name):
+    a = np.asarray(a)
+    b = np.asarray(b)
+    same = (a == b) | (np.isnan(a) & np.isnan(b))
+    if not same.all():
+        idx = np.argwhere(~same)[:5]
+        raise AssertionError(f"{name}: {int((~same).sum())} mismatches, e.g. {[(tuple(i), a[tuple(i)], b[tuple(i)]) for i in idx]}")
+
+
+def test_detmath_host_device_bitwise(engine, oracle):
+    rng = np.random.default_rng(0)
+    x = np.concatenate([rng.uniform(-745, 709, 20000), np.exp(rng.uniform(-700, 700, 20000)),
+                        rng.uniform(1e-300, 1e-290, 100), [0.0, 1.0, 2.0, 0.5]])
+    y = rng.uniform(-1.0, 1.0, len(x))
+    xe = x.copy()
+    e_d, _, _ = engine.selftest_detmath(xe, y)
+    e_h, _, _ = oracle.detmath(xe, y)
+    assert_bitwise(e_d, e_h, "exp")
+    xp = np.abs(x) + 1e-300
+    _, l_d, p_d = engine.selftest_detmath(xp, y)
+    _, l_h, p_h = oracle.detmath(xp, y)
+    assert_bitwise(l_d, l_h, "log")
+    assert_bitwise(p_d, p_h, "pow")
+
+
+@pytest.mark.parametrize("stop", [False, True])
+def test_learning_knots_bitwise(engine, oracle, stop):
+    """Every knot (t, G) of the device integrator equals the oracle's; the
+    truncated mode (stop after the last knot the equilibrium can read) is a
+    prefix of the full solve."""
+    grid = sbr.fig5_grid(500)
+    betas = np.concatenate([grid.beta[::25], [0.5, 1.0, 2.0, 3.0, 61.654026637430945]])
+    res = engine.learn_baseline(betas, 15.0, 30.0, stop_after_eta=stop)
+    for b, (t, G, st) in zip(betas, res):
+        to, Go, sto = oracle.learn_logistic(float(b), 30.0)
+        if stop:
+            assert len(t) <= len(to) and t[-1] > 15.0
+        else:
+            assert len(t) == len(to)
+        assert_bitwise(t, to[: len(t)], f"t β={b}")
+        assert_bitwise(G, Go[: len(t)], f"G β={b}")
+
+
+def _oracle_sweep(oracle, grid):
+    return oracle.sweep_baseline(grid.beta, grid.eta, grid.t_end, grid.u, grid.p, grid.kappa, grid.lam, grid.x0)
+
+
+def test_fig5_500_sweep_bitwise(engine, oracle, golden):
+    """All 250,000 points of the Fig 5 grid: every output field and status bit
+    identical to the oracle; run mask identical to the committed heatmap."""
+    grid = sbr.fig5_grid(500)
+    g = engine.sweep_baseline(grid)
+    o = _oracle_sweep(oracle, grid)
+    for f in FIELDS:
+        assert_bitwise(g[f], o[f], f)
+    assert np.array_equal(g["status"], o["status"])
+    assert np.array_equal(g["iters"], o["iters"])
+    run = (g["status"] & sbr.STATUS["SBR_RUN"]) > 0
+    assert run.sum() == golden("fig5_prefix.json")["n500"]["total"]
+
+
+def test_fig4_sweep_bitwise_and_boundary(engine, oracle, golden):
+    grid = sbr.fig4_grid(5000)
+    g = engine.sweep_baseline(grid, early_exit=5)
+    o = oracle.apply_early_exit(_oracle_sweep(oracle, grid), 5)
+    for f in FIELDS:
+        assert_bitwise(g[f], o[f], f)
+    assert np.array_equal(g["status"], o["status"])
+    run = (g["status"][0] & sbr.STATUS["SBR_RUN"]) > 0
+    n = golden("fig4_u_sweep.json")["n_run_prefix"]
+    assert run[:n].all() and not run[n:].any()
+
+
+@pytest.mark.parametrize("case", ["main", "fast", "low_u"])
+def test_point_paths_bitwise(engine, oracle, golden, case):
+    """Single-point mode (τ̄, HR(τ̄), AW_cum(τ̄)) equals the oracle and hits Fig 3."""
+    P = golden("fig3_equilibria.json")[case]["params"]
+    r = engine.solve_point_paths(P["beta"], P["eta"], P["t_end"], P["u"], P["p"], P["kappa"], P["lam"])
+    t, G, _ = oracle.learn_logistic(P["beta"], P["t_end"])
+    o = oracle.equilibrium(t, G, P["beta"], P["eta"], P["t_end"], P["u"], P["p"], P["kappa"], P["lam"], paths=True)
+    assert r["status"] == o["status"]
+    for f in FIELDS:
+        assert_bitwise(r[f], o[f], f)
+    assert_bitwise(r["tau"], o["hr_tau"], "tau")
+    assert_bitwise(r["hr"], o["hr"], "hr")
+    assert_bitwise(r["aw_cum"], o["aw"], "aw_cum")
+    gx = golden("fig3_equilibria.json")[case]
+    assert abs(r["xi"] - gx["xi"]) <= 1.5 * gx["xi_precision"] + 2e-5
+
+
+def test_reference_call_surface(engine):
+    """solve_learning → solve_equilibrium_baseline → get_AW_functions on the GPU."""
+    m = sbr.ModelParameters.make(beta=1.0, eta_bar=15.0, u=0.1, p=0.5, kappa=0.6, lam=0.01)
+    lr = sbr.solve_learning(m.learning, engine)
+    res = sbr.solve_equilibrium_baseline(lr, m.economic, engine)
+    assert res.bankrun and res.converged
+    aw = sbr.get_AW_functions(res)
+    assert abs(aw["AW_max"] - 0.6182312) < 1e-6
+    assert abs(aw["AW_cum"](0.0) - 2e-4) < 1e-12  # AW_cum(0) = 2 x0 (solver.jl:523-524)
+    assert abs(res.tau_IN - 2.8879) < 2e-4
+
+
+def test_config3_2048_properties_and_columns(engine, oracle):
+    """Benchmark config 3 (2048², 4.19M points): spot columns bitwise against
+    the oracle plus size-independent properties on the whole grid."""
+    grid = sbr.fig5_grid(2048)
+    g = engine.sweep_baseline(grid)
+    st = g["status"]
+    run = (st & sbr.STATUS["SBR_RUN"]) > 0
+    bad = sbr.STATUS["SBR_ENGINE_TRUNC"] | sbr.STATUS["SBR_KNOT_OVERFLOW"] | sbr.STATUS["SBR_OOB"]
+    assert not (st & bad).any()
+    # outcome classes are exclusive and exhaustive
+    cls = (sbr.STATUS["SBR_RUN"] | sbr.STATUS["SBR_NO_RUN_HR_BELOW_U"] | sbr.STATUS["SBR_NO_RUN_COLLAPSE"]
+           | sbr.STATUS["SBR_NO_RUN_MAXITER"] | sbr.STATUS["SBR_FALSE_EQ"])
+    assert ((st & cls) != 0).all()
+    # run ⇔ finite ξ; aw_max ≥ κ − tol on runs (AW reaches κ at ξ); ξ within the buffers
+    assert np.array_equal(run, np.isfinite(g["xi"]))
+    assert (g["aw_max"][run] >= 0.6 - 1e-12).all()
+    assert ((g["xi"][run] >= g["tau_in_unc"][run]) & (g["xi"][run] <= g["tau_out_unc"][run])).all()
+    assert (g["tol"][run] <= 10 * np.spacing(0.6)).all()
+    # run cells form a u-prefix in every β column (what the Fig 5 masks show)
+    for c in range(run.shape[0]):
+        k = np.argmin(run[c]) if not run[c].all() else run.shape[1]
+        assert run[c, :k].all() and not run[c, k:].any()
+    cols = np.random.default_rng(0).choice(2048, 12, replace=False)
+    sub = grid.subset(np.sort(cols))
+    o = _oracle_sweep(oracle, sub)
+    for f in FIELDS:
+        assert_bitwise(g[f][np.sort(cols)], o[f], f)
+    assert np.array_equal(st[np.sort(cols)], o["status"])
+
+
+def test_fig5_5000_run_mask(engine, golden):
+    """Paper resolution (5000², 25M points, scripts/1_baseline.jl:208): the run
+    mask of comp_stat_cross_heatmap_AW_large.pdf column by column (8,736,564 cells)."""
+    grid = sbr.fig5_grid(5000)
+    pref = np.array(golden("fig5_prefix.json")["n5000"]["prefix"])
+    g = engine.sweep_baseline(grid, early_exit=5, with_iters=False)
+    run = (g["status"] & sbr.STATUS["SBR_RUN"]) > 0
+    got = np.array([np.argmin(r) if not r.all() else len(r) for r in run])
+    assert np.array_equal(got, pref), f"{int((got != pref).sum())} columns differ"
+    assert run.sum() == 8736564

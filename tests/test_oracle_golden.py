@@ -1,0 +1,164 @@
+"""Pin the CPU oracle to the reference's own outputs (its committed figures).
+
+The Julia reference cannot run here or on the GPU box; these known answers,
+extracted by tools/extract_golden.py from output/figures/**.pdf, are the only
+reference-generated data there is.  Tolerances are the
+figures' own resolution (0.01 pt of PDF coordinates, stated per fixture) plus
+the knot-grid sensitivity of the restatement.
+"""
+import numpy as np
+import pytest
+
+import sbr
+from golden_util import aw_paths, interp, viridis_level
+
+EPS = np.finfo(np.float64).eps
+
+
+def _point(oracle, beta, eta, t_end, u, p, kappa, lam):
+    t, G, st = oracle.learn_logistic(beta, t_end)
+    r = oracle.equilibrium(t, G, beta, eta, t_end, u, p, kappa, lam, paths=True)
+    return t, G, r
+
+
+@pytest.mark.parametrize("case", ["main", "fast", "low_u"])
+def test_fig3_equilibrium_dynamics(oracle, golden, case):
+    """Fig 3 / 3bis / 3ter (scripts/1_baseline.jl:82-126; plotting.jl:156-210)."""
+    g = golden("fig3_equilibria.json")[case]
+    P = g["params"]
+    t, G, r = _point(oracle, P["beta"], P["eta"], P["t_end"], P["u"], P["p"], P["kappa"], P["lam"])
+    assert r["status"] & sbr.STATUS["SBR_RUN"]
+    xi = r["xi"]
+    tol_x = 1.5 * g["xi_precision"] + 2e-5
+    assert abs(xi - g["xi"]) <= tol_x
+    assert abs((xi - r["tau_in_unc"]) - g["tau_in"]) <= 1.5 * g["tau_in_precision"] + 2e-5
+    # 0:0.1:min(2ξ, η) samples of AW_cum / AW_OUT / AW_IN
+    n = int(np.floor(min(2 * xi, P["eta"]) / 0.1 + 1e-9)) + 1
+    assert n == g["n_samples"]
+    ts = np.arange(n) / 10.0
+    cum, out, inn = aw_paths(xi, r["tau_in_unc"], r["tau_out_unc"], r["hr_tau"], t, G)
+    tol_y = 1.5 * g["aw_precision"] + 1e-5
+    for name, path in (("aw_cum", cum), ("aw_out", out), ("aw_in", inn)):
+        got = interp(r["hr_tau"], path, ts)
+        assert np.max(np.abs(got - np.array(g[name]))) <= tol_y, name
+    # the arrow starts at AW_OUT(0.8 ξ)
+    assert abs(interp(r["hr_tau"], out, 0.8 * xi) - g["arrow_y"]) <= tol_y
+
+
+def test_fig1_learning_curves(oracle, golden):
+    """Fig 1 (1_baseline.jl:56-73): G(t) for β = 0.5, 1, 2 on tspan (0, 20)."""
+    g = golden("fig1_learning.json")
+    ts = sbr.julia_range(0.0, 20.0, 1000)
+    for b, ys in g["curves"].items():
+        t, G, st = oracle.learn_logistic(float(b), 20.0)
+        got = interp(t, G, ts)
+        assert np.max(np.abs(got - np.array(ys))) <= 1.5 * g["precision"]
+
+
+def test_learning_matches_closed_form(oracle):
+    """dx/dt = βx(1−x) at reltol = abstol = eps(): knot values agree with the
+    logistic closed form far below the 1e-6 trajectory tolerance."""
+    for b in (0.5, 1.0, 3.0, 100.0, 1e4):
+        t, G, st = oracle.learn_logistic(b, 30.0)
+        exact = 1.0 / (1.0 + (1.0 / 1e-4 - 1.0) * np.exp(-b * t))
+        assert np.max(np.abs(G - exact) / exact) < 1e-12
+        assert t[0] == 0.0 and t[-1] == 30.0 and np.all(np.diff(t) > 0)
+        assert st["status"] == 0
+
+
+def test_fig2_hazard_rate(oracle, golden):
+    """Fig 2 (plotting.jl:62-132): h(τ) evaluated at clamp(ξ − t) for t ∈ range(0, ξ, 1000)."""
+    g = golden("fig2_hazard.json")
+    t, G, r = _point(oracle, 1.0, 15.0, 30.0, 0.1, 0.5, 0.6, 0.01)
+    xi = r["xi"]
+    tp = np.linspace(0.0, xi, 1000)
+    ev = np.clip(xi - tp, 0.0, 1.3 * xi)
+    h = interp(r["hr_tau"], r["hr"], ev)[::-1]  # plotted y = reversed h values
+    assert np.max(np.abs(np.array(g["tau"]) - ev)) <= 1.5 * g["tau_precision"] + 1e-4
+    assert np.max(np.abs(np.array(g["hr"]) - h)) <= 1.5 * g["hr_precision"] + 1e-5
+
+
+def test_fig4_u_sweep(oracle, golden):
+    """Fig 4 (1_baseline.jl:137-192): exactly 2718 leading runs, AW_max, ξ and
+    return time ξ − τ̄_IN along them."""
+    g = golden("fig4_u_sweep.json")
+    grid = sbr.fig4_grid(5000)
+    r = oracle.sweep_baseline(grid.beta, grid.eta, grid.t_end, grid.u, 0.5, 0.6, 0.01)
+    r = oracle.apply_early_exit(r, 5)
+    run = (r["status"][0] & sbr.STATUS["SBR_RUN"]) > 0
+    n = g["n_run_prefix"]
+    assert run[:n].all() and not run[n:].any()
+    assert np.max(np.abs(r["aw_max"][0, :n] - np.array(g["aw_max"]))) <= 1.5 * g["aw_precision"] + 1e-5
+    assert np.max(np.abs(r["xi"][0, :n] - np.array(g["xi"]))) <= 1.5 * g["time_precision"]
+    ret = r["xi"][0, :n] - r["tau_in_unc"][0, :n]
+    assert np.max(np.abs(ret - np.array(g["return_time"]))) <= 1.5 * g["time_precision"]
+    # the 5 no-run points after the boundary were solved, the rest skipped
+    st = r["status"][0]
+    assert not (st[n:n + 5] & sbr.STATUS["SBR_SKIPPED_EARLY_EXIT"]).any()
+    assert (st[n + 5:] & sbr.STATUS["SBR_SKIPPED_EARLY_EXIT"]).all()
+
+
+@pytest.fixture(scope="module")
+def fig5_500(oracle):
+    grid = sbr.fig5_grid(500)
+    return grid, oracle.sweep_baseline(grid.beta, grid.eta, grid.t_end, grid.u, 0.5, 0.6, 0.01)
+
+
+def test_fig5_run_mask_500(oracle, golden, fig5_500):
+    """Fig 5 at 500² (1_baseline.jl:210-267): the run mask of the committed
+    heatmap, cell for cell, after the 5-consecutive-NaN early exit."""
+    grid, r = fig5_500
+    e = oracle.apply_early_exit(r, 5)
+    run = (e["status"] & sbr.STATUS["SBR_RUN"]) > 0
+    prefix = golden("fig5_prefix.json")["n500"]["prefix"]
+    mask = np.zeros_like(run)
+    for c, k in enumerate(prefix):
+        mask[c, :k] = True
+    assert run.sum() == 87554
+    assert np.array_equal(run, mask)
+    # the skip rule only clips the tail: no run cell exists beyond the prefix
+    raw = (r["status"] & sbr.STATUS["SBR_RUN"]) > 0
+    assert np.array_equal(raw, mask)
+
+
+def test_fig5_colours_500(golden, fig5_500):
+    """Heatmap colours (viridis, GR's continuous palette interpolation) encode
+    AW_max on [min, max] of the run cells: decode them and compare."""
+    grid, r = fig5_500
+    h = golden("fig5_heatmap_500.npz")
+    rgb, alpha, pal = h["rgb"], h["alpha"], h["palette"]
+    img = rgb[::-1].transpose(1, 0, 2)  # [beta][u]
+    run = alpha[::-1].T > 0
+    lvl, dist = viridis_level(img[run], pal)
+    assert np.median(dist) < 2.0
+    aw = r["aw_max"][run]
+    lo, hi = np.nanmin(aw), np.nanmax(aw)
+    pred = (aw - lo) / (hi - lo)
+    err = np.abs(pred - lvl)
+    # 8-bit colour quantisation: 1/255 of the range, plus palette-projection noise
+    assert np.quantile(err, 0.99) < 2.5 / 255
+    assert np.corrcoef(pred, lvl)[0, 1] > 0.9999
+
+
+def test_social_script_baseline_figure(oracle, golden):
+    """scripts/4_social_learning.jl:68-69 runs the baseline at the social
+    parameters (β = 0.9, η = η_bar/β = 33.3, tspan (0, 2η))."""
+    g = golden("social_learning.json")["baseline"]
+    P = g["params"]
+    t, G, r = _point(oracle, P["beta"], P["eta"], P["t_end"], P["u"], P["p"], P["kappa"], P["lam"])
+    xi = r["xi"]
+    assert abs(xi - g["xi"]) <= 1.5 * g["xi_precision"] + 2e-5
+    assert abs((xi - r["tau_in_unc"]) - g["tau_in"]) <= 1.5 * g["tau_in_precision"] + 2e-5
+    n = g["n_samples"]
+    ts = np.arange(n) / 10.0
+    cum, out, inn = aw_paths(xi, r["tau_in_unc"], r["tau_out_unc"], r["hr_tau"], t, G)
+    assert np.max(np.abs(interp(r["hr_tau"], cum, ts) - np.array(g["aw_cum"]))) <= 1.5 * g["aw_precision"] + 1e-5
+
+
+def test_no_autoswitch_on_config_grid(oracle):
+    """The AutoTsit5 stiffness test never fires on the benchmark β range, so
+    Tsit5-only is the reference's algorithm there."""
+    grid = sbr.fig5_grid(2048)
+    for b in grid.beta[::16]:
+        t, G, st = oracle.learn_logistic(float(b), 30.0)
+        assert st["status"] & sbr.STATUS["SBR_STIFF_SWITCH"] == 0
