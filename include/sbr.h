@@ -47,7 +47,7 @@ typedef struct {
     int32_t bisect_max_iters;   /* solver.jl:309 max_iters = 100 */
     int32_t early_exit_nan_run; /* 1_baseline.jl:147,221: 5; 0 disables */
     int32_t knot_capacity;      /* engine limit on stored knots per β (0 = default 8192) */
-    int32_t reserved;
+    int32_t hetero_max_iters;   /* heterogeneity_solver.jl:49 max_iters = 500 */
 } sbr_opts;
 
 typedef struct {
@@ -111,6 +111,26 @@ int sbr_learn_baseline(sbr_ctx* ctx, const double* beta, const double* eta, cons
 int sbr_solve_point_paths(sbr_ctx* ctx, double beta, double eta, double t_end, double x0, double u, double p,
                           double kappa, double lambda, const sbr_opts* opts, double* res, uint32_t* status,
                           double* tau, double* hr, double* aw_cum, int64_t cap, int64_t* n_tau);
+
+/*
+ * Heterogeneity extension sweep — for each column c (group rates
+ * betas[c*K .. c*K+K), η = eta[c], tspan = (0, t_end[c])):
+ *     lr = solve_SInetwork_hetero(LearningParametersHetero(βs, dist, tspan, x0))  heterogeneity_learning.jl:49
+ * and for each u:
+ *     r  = solve_equilibrium_hetero(lr, EconomicParameters(u, p, κ, λ, η_bar, η))  heterogeneity_solver.jl:241
+ *     get_AW_functions_hetero!(r).AW_max                                            heterogeneity_solver.jl:386
+ * K ∈ {1, 2, 3, 4, 8}.  out->tau_in_unc/tau_out_unc are ignored; the per-group
+ * buffers go to tau_in/tau_out ([n_col*n_u][K], may be NULL).  The caller
+ * resolves η = η_bar / Σ dist·βs per column (heterogeneity_model.jl:131-132).
+ */
+int sbr_sweep_hetero(sbr_ctx* ctx, int32_t K, const double* betas, const double* dist, const double* eta,
+                     const double* t_end, double x0, const double* u, int64_t n_col, int64_t n_u, double p,
+                     double kappa, double lambda, const sbr_opts* opts, sbr_result_soa* out, double* tau_in,
+                     double* tau_out);
+int sbr_sweep_hetero_dev(sbr_ctx* ctx, void* stream, int32_t K, const double* betas, const double* dist,
+                         const double* eta, const double* t_end, double x0, const double* u, int64_t n_col,
+                         int64_t n_u, double p, double kappa, double lambda, const sbr_opts* opts,
+                         sbr_result_soa* out, double* tau_in, double* tau_out);
 
 /* 5-consecutive-no-run early exit (1_baseline.jl:236-244) as a post-pass on
  * host arrays: points after `threshold` consecutive non-runs in a β column get

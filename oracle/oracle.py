@@ -128,3 +128,57 @@ def detmath(x, y):
     e, l, pw = np.empty(n), np.empty(n), np.empty(n)
     lib().sbro_detmath(_ptr(x), _ptr(y), n, _ptr(e), _ptr(l), _ptr(pw))
     return e, l, pw
+
+
+def _hetero_sigs(L):
+    L.sbro_sweep_hetero.restype = ctypes.c_int
+    L.sbro_sweep_hetero.argtypes = [_I32, _P, _P, _P, _P, _D, _P, _I64, _I64, _D, _D, _D, _I32, _D, _I32] + [_P] * 8
+    L.sbro_learn_hetero.restype = _I64
+    L.sbro_learn_hetero.argtypes = [_P, _P, _I32, _D, _D, _P, _P, _I64, _P]
+
+
+def learn_hetero(betas, dist, t_end, x0=1e-4, cap=1 << 16):
+    L = lib()
+    _hetero_sigs(L)
+    betas = np.ascontiguousarray(betas, np.float64)
+    dist = np.ascontiguousarray(dist, np.float64)
+    K = len(betas)
+    t = np.empty(cap)
+    G = np.empty(cap * K)
+    stats = np.zeros(5, np.int64)
+    n = L.sbro_learn_hetero(_ptr(betas), _ptr(dist), K, t_end, x0, _ptr(t), _ptr(G), cap, _ptr(stats))
+    if n < 0:
+        raise RuntimeError("oracle hetero learning failed")
+    return t[:n].copy(), G[: n * K].reshape(n, K).copy(), dict(naccept=int(stats[0]), nreject=int(stats[1]),
+                                                                status=int(stats[2]),
+                                                                t_switch=float(stats[4:5].view(np.float64)[0]))
+
+
+def sweep_hetero(betas, dist, eta, t_end, u, p, kappa, lam, x0=1e-4, max_iters=500, tolerance=1e-12, nthreads=0):
+    """betas: [n_col, K] group rates per column; eta/t_end per column."""
+    L = lib()
+    _hetero_sigs(L)
+    betas = np.ascontiguousarray(np.atleast_2d(betas), np.float64)
+    n_col, K = betas.shape
+    dist = np.ascontiguousarray(dist, np.float64)
+    eta = np.ascontiguousarray(np.broadcast_to(eta, (n_col,)), np.float64)
+    t_end = np.ascontiguousarray(np.broadcast_to(t_end, (n_col,)), np.float64)
+    u = np.ascontiguousarray(np.atleast_1d(u), np.float64)
+    nu = len(u)
+    o = {k: np.empty(n_col * nu) for k in ("xi", "aw_max", "tol")}
+    o["status"] = np.empty(n_col * nu, np.uint32)
+    o["iters"] = np.empty(n_col * nu, np.int32)
+    o["tau_in_unc"] = np.empty(n_col * nu * K)
+    o["tau_out_unc"] = np.empty(n_col * nu * K)
+    nk = np.empty(n_col, np.int64)
+    rc = L.sbro_sweep_hetero(K, _ptr(betas), _ptr(dist), _ptr(eta), _ptr(t_end), x0, _ptr(u), n_col, nu, p, kappa, lam,
+                             max_iters, tolerance, nthreads, _ptr(o["xi"]), _ptr(o["aw_max"]), _ptr(o["tol"]),
+                             _ptr(o["status"]), _ptr(o["iters"]), _ptr(o["tau_in_unc"]), _ptr(o["tau_out_unc"]),
+                             _ptr(nk))
+    if rc != 0:
+        raise RuntimeError("oracle hetero sweep failed")
+    out = {k: v.reshape(n_col, nu) for k, v in o.items() if k not in ("tau_in_unc", "tau_out_unc")}
+    out["tau_in_unc"] = o["tau_in_unc"].reshape(n_col, nu, K)
+    out["tau_out_unc"] = o["tau_out_unc"].reshape(n_col, nu, K)
+    out["n_knots"] = nk
+    return out

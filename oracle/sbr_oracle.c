@@ -179,6 +179,7 @@ typedef void (*rhs_fn)(void* ctx, double t, const double* x, double* dx, int* oo
 typedef struct {
     int64_t naccept, nreject;
     uint32_t status;
+    double t_switch; /* time at which AutoSwitch would have switched (NaN if never) */
 } ode_stats_t;
 
 #define MAXK 64
@@ -234,6 +235,7 @@ static int tsit5_solve(rhs_fn f, void* ctx, int m, double t0, double t1, const d
     /* ---- main loop (solve! / loopheader! / loopfooter!) ---- */
     double t = t0, qold = CTL_QOLDMIN, q11 = 1.0;
     autoswitch_t as = {0, 0};
+    st->t_switch = NAN;
     if (knots_push(kn, t0, x)) return -1;
     int64_t iter = 0;
     while (t < t1) {
@@ -305,6 +307,7 @@ static int tsit5_solve(rhs_fn f, void* ctx, int m, double t0, double t1, const d
         }
         if (!(dt > 0.0) || !isfinite(dt)) { st->status |= SBR_ODE_FAILED; break; }
         autoswitch_update(&as, eig, dt);
+        if (as.switched && st->t_switch != st->t_switch) st->t_switch = t;
     }
     if (as.switched) st->status |= SBR_STIFF_SWITCH;
     if (oob) st->status |= SBR_OOB;
@@ -618,4 +621,236 @@ void sbro_detmath(const double* x, const double* y, int64_t n, double* e, double
         l[i] = sbr_log(x[i]);
         pw[i] = sbr_pow_pos(x[i], y[i]);
     }
+}
+
+/* ======================================================================== */
+/* Heterogeneity extension (K coupled groups)                               */
+/* heterogeneity_learning.jl:49-134, heterogeneity_solver.jl:48-375         */
+/* ======================================================================== */
+typedef struct {
+    int K;
+    const double* betas;
+    const double* dist;
+} hetero_ctx;
+
+/* ω = Σ_j dist_j I_j (generator sum: left fold from the first term);
+ * du_k = (1 − I_k) β_k ω   (heterogeneity_learning.jl:57-67) */
+static void rhs_hetero(void* ctx, double t, const double* I, double* du, int* oob)
+{
+    (void)t; (void)oob;
+    const hetero_ctx* h = (const hetero_ctx*)ctx;
+    double w = h->dist[0] * I[0];
+    for (int j = 1; j < h->K; j++) w = w + h->dist[j] * I[j];
+    for (int k = 0; k < h->K; k++) du[k] = ((1.0 - I[k]) * h->betas[k]) * w;
+}
+
+int64_t sbro_learn_hetero(const double* betas, const double* dist, int32_t K, double t1, double x0, double* t_out,
+                          double* G_out, int64_t cap, int64_t* stats)
+{
+    knots_t kn = {0};
+    ode_stats_t st;
+    double x0v[MAXK];
+    for (int k = 0; k < K; k++) x0v[k] = x0;
+    hetero_ctx hc = {K, betas, dist};
+    const double e = 2.220446049250313e-16;
+    if (K < 1 || K > MAXK || tsit5_solve(rhs_hetero, &hc, K, 0.0, t1, x0v, e, e, 100000, &kn, &st)) {
+        knots_free(&kn);
+        return -1;
+    }
+    int64_t n = kn.n;
+    if (stats) {
+        stats[0] = st.naccept; stats[1] = st.nreject; stats[2] = st.status; stats[3] = n;
+        memcpy(&stats[4], &st.t_switch, 8);
+    }
+    if (n > cap) n = -n;
+    else {
+        memcpy(t_out, kn.t, (size_t)kn.n * sizeof(double));
+        memcpy(G_out, kn.x, (size_t)kn.n * K * sizeof(double));
+    }
+    knots_free(&kn);
+    return n;
+}
+
+/* is_valid_equilibrium_hetero (heterogeneity_solver.jl:175-210) */
+static int valid_hetero(double xs, const double* tin, const double* t, const double* G, int64_t n, int K,
+                        double kappa, const double* dist, int* oob)
+{
+    int64_t m = 0;
+    while (m < n && t[m] <= xs) m++;
+    if (m == 0) return 1;
+    int prev = 0;
+    for (int64_t i = 0; i < m; i++) {
+        double aw = 0.0;
+        for (int k = 0; k < K; k++) {
+            double tI = dmax(0.0, xs - tin[k]);
+            double a = interp_s(t, G + k, K, n, t[i], oob);
+            double b = interp_s(t, G + k, K, n, dmax(0.0, t[i] - tI), oob);
+            aw = aw + dist[k] * (a - b);
+        }
+        int above = aw > kappa;
+        /* any i with above[i] && !above[i+1] (the reference scans backwards; same set) */
+        if (i > 0 && prev && !above) return 0;
+        prev = above;
+    }
+    return 1;
+}
+
+/* compute_ξ_hetero (heterogeneity_solver.jl:48-144) */
+static uint32_t compute_xi_hetero(const double* tin, const double* tout, const double* dist, int K, const double* t,
+                                  const double* G, int64_t n, double kappa, int32_t max_iters, double tolerance,
+                                  double* xi_out, double* tol_out, int32_t* iters)
+{
+    int oob = 0;
+    double guess = (dist[0] * (tin[0] + tout[0])) / 2.0;
+    for (int k = 1; k < K; k++) guess = guess + (dist[k] * (tin[k] + tout[k])) / 2.0;
+    double mo = tout[0];
+    for (int k = 1; k < K; k++) mo = dmax(mo, tout[k]);
+    double xmin = 0.0, xmax = mo * 2.0, xnew = guess;
+    *xi_out = NAN;
+    *tol_out = INFINITY;
+    for (int32_t iter = 1; iter <= max_iters; iter++) {
+        *iters = iter;
+        double d = xmin - xmax;
+        if (fabs(d) < 2.0 * sbr_jl_eps(d)) return SBR_NO_RUN_COLLAPSE;
+        if (iter == max_iters - 1) return SBR_NO_RUN_MAXITER;
+        double xo = xnew;
+        int64_t idx = ssl(t, n, xo);
+        if (idx < 0) return SBR_OOB;
+        int64_t i2 = idx + 1 < n - 1 ? idx + 1 : n - 1; /* min(current_idx + 1, length) */
+        double eps = t[i2] - t[idx];
+        double AW = 0.0, AWe = 0.0;
+        for (int k = 0; k < K; k++) {
+            double ic = dmin(tin[k], xo), oc = dmin(tout[k], xo);
+            AW = AW + dist[k] * (interp_s(t, G + k, K, n, oc, &oob) - interp_s(t, G + k, K, n, ic, &oob));
+            AWe = AWe + dist[k] * (interp_s(t, G + k, K, n, oc + eps, &oob) -
+                                   interp_s(t, G + k, K, n, ic + eps, &oob));
+        }
+        if (oob) return SBR_OOB;
+        double err = AW - kappa;
+        int inc = AWe >= AW;
+        if (fabs(err) <= tolerance) {
+            if (inc) {
+                int v = valid_hetero(xo, tin, t, G, n, K, kappa, dist, &oob);
+                if (oob) return SBR_OOB;
+                if (!v) return SBR_HETERO_INVALID;
+                *xi_out = xo;
+                *tol_out = fabs(err);
+                return SBR_RUN;
+            }
+            return SBR_FALSE_EQ;
+        } else if (err > 0) {
+            xmax = xo;
+            xnew = 0.5 * (xo + xmin);
+        } else {
+            xmin = xo;
+            xnew = 0.5 * (xo + xmax);
+        }
+    }
+    return SBR_NO_RUN_MAXITER;
+}
+
+/* get_AW_hetero's AW_max over the whole learning grid (heterogeneity_solver.jl:316-375) */
+static double aw_max_hetero(double xi, const double* tin, const double* tout, const double* dist, int K,
+                            const double* t, const double* G, int64_t n, double* cum, int* oob)
+{
+    for (int64_t i = 0; i < n; i++) cum[i] = 0.0;
+    for (int k = 0; k < K; k++) {
+        double ic = dmin(tin[k], xi), oc = dmin(tout[k], xi);
+        for (int64_t i = 0; i < n; i++) {
+            double a = (t[i] - xi) + ic;
+            double b = (t[i] - xi) + oc;
+            double gi = interp_s(t, G + k, K, n, a > 0 ? a : 0.0, oob);
+            double go = interp_s(t, G + k, K, n, b > 0 ? b : 0.0, oob);
+            double awin = a >= 0 ? gi : 0.0;
+            double awout = b >= 0 ? go : 0.0;
+            cum[i] = cum[i] + dist[k] * (awout - awin);
+        }
+    }
+    double mx = -INFINITY;
+    for (int64_t i = 0; i < n; i++)
+        if (mx == mx && (cum[i] != cum[i] || cum[i] > mx)) mx = cum[i];
+    return mx;
+}
+
+/* Hetero sweep: column c has group rates betas[c*K .. c*K+K), η = eta[c],
+ * tspan = (0, t_end[c]); every u.  Outputs u-fastest; tin/tout are [pt][K]. */
+int sbro_sweep_hetero(int32_t K, const double* betas, const double* dist, const double* eta, const double* t_end,
+                      double x0, const double* u, int64_t n_col, int64_t n_u, double p, double kappa, double lambda,
+                      int32_t max_iters, double tolerance, int32_t nthreads, double* xi, double* aw_max, double* tol,
+                      uint32_t* status, int32_t* iters, double* tin_out, double* tout_out, int64_t* nknots)
+{
+    int err = 0;
+    if (K < 1 || K > MAXK) return -1;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 1) reduction(| : err)
+#endif
+    for (int64_t c = 0; c < n_col; c++) {
+        const double* bk = betas + c * K;
+        knots_t kn = {0};
+        ode_stats_t st;
+        double x0v[MAXK];
+        for (int k = 0; k < K; k++) x0v[k] = x0;
+        hetero_ctx hc = {K, bk, dist};
+        const double e = 2.220446049250313e-16;
+        if (tsit5_solve(rhs_hetero, &hc, K, 0.0, t_end[c], x0v, e, e, 100000, &kn, &st)) { err |= 1; continue; }
+        int64_t n = kn.n;
+        if (nknots) nknots[c] = n;
+        /* compute_pdf_hetero: pdf_k = (1 − I_k) β_k ω at the knots */
+        double* g = (double*)malloc((size_t)n * sizeof(double));
+        double* cum = (double*)malloc((size_t)n * sizeof(double));
+        hazard_t hz[MAXK];
+        int hz_oob = 0;
+        for (int k = 0; k < K; k++) {
+            for (int64_t i = 0; i < n; i++) {
+                const double* I = kn.x + i * K;
+                double w = dist[0] * I[0];
+                for (int j = 1; j < K; j++) w = w + dist[j] * I[j];
+                g[i] = ((1.0 - I[k]) * bk[k]) * w;
+            }
+            hazard_rate(kn.t, g, n, p, lambda, eta[c], 1, &hz[k]);
+            hz_oob |= hz[k].oob;
+        }
+        for (int64_t j = 0; j < n_u; j++) {
+            int64_t o = c * n_u + j;
+            double tin[MAXK], tout[MAXK];
+            uint32_t s = 0;
+            double x = NAN, tl = INFINITY, am = NAN;
+            int32_t it = 0;
+            if (hz_oob) {
+                s = SBR_OOB;
+                for (int k = 0; k < K; k++) tin[k] = tout[k] = NAN;
+            } else {
+                int all_eq = 1;
+                for (int k = 0; k < K; k++) {
+                    optimal_buffer(u[j], hz[k].tau, hz[k].hr, hz[k].n, t_end[c], &tin[k], &tout[k]);
+                    all_eq &= (tin[k] == tout[k]);
+                }
+                if (all_eq) {
+                    s = SBR_NO_RUN_HR_BELOW_U | SBR_CONVERGED;
+                    tl = 0.0;
+                } else {
+                    s = compute_xi_hetero(tin, tout, dist, K, kn.t, kn.x, n, kappa, max_iters, tolerance, &x, &tl, &it);
+                    if (s == SBR_RUN) {
+                        int oob = 0;
+                        am = aw_max_hetero(x, tin, tout, dist, K, kn.t, kn.x, n, cum, &oob);
+                        if (oob) { s = SBR_OOB; x = NAN; tl = INFINITY; am = NAN; }
+                        else s = SBR_RUN | SBR_CONVERGED;
+                    }
+                }
+            }
+            xi[o] = x; tol[o] = tl; aw_max[o] = am;
+            status[o] = s | (st.status & (SBR_ODE_MAXITERS | SBR_STIFF_SWITCH | SBR_ODE_FAILED));
+            if (iters) iters[o] = it;
+            for (int k = 0; k < K; k++) {
+                if (tin_out) tin_out[o * K + k] = tin[k];
+                if (tout_out) tout_out[o * K + k] = tout[k];
+            }
+        }
+        for (int k = 0; k < K; k++) hazard_free(&hz[k]);
+        free(g);
+        free(cum);
+        knots_free(&kn);
+    }
+    return err ? -1 : 0;
 }

@@ -23,6 +23,9 @@ struct sbr_ctx {
     // learning workspace
     size_t ws_beta = 0, ws_cap = 0;
     sbr::LearnBufs L{};
+    // hetero learning workspace
+    size_t hs_col = 0, hs_cap = 0, hs_K = 0;
+    sbr::HeteroBufs H{};
     // host-API staging
     void* stage = nullptr;
     size_t stage_bytes = 0;
@@ -83,6 +86,37 @@ int ensure_learn(sbr_ctx* c, size_t n_beta, size_t cap)
     return SBR_OK;
 }
 
+void free_hetero(sbr_ctx* c)
+{
+    void* ps[] = {c->H.t, c->H.G, c->H.hr, c->H.hrI, c->H.n_knots, c->H.n_tau, c->H.n_le, c->H.status,
+                  c->H.n_accept, c->H.n_reject};
+    for (void* p : ps)
+        if (p) (void)hipFree(p);
+    c->H = sbr::HeteroBufs{};
+    c->hs_col = c->hs_cap = c->hs_K = 0;
+}
+
+int ensure_hetero(sbr_ctx* c, size_t n_col, size_t cap, size_t K)
+{
+    if (n_col <= c->hs_col && cap == c->hs_cap && K == c->hs_K) return SBR_OK;
+    free_hetero(c);
+    HIP_TRY(c, hipMalloc(&c->H.t, n_col * cap * 8), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&c->H.G, n_col * cap * K * 8), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&c->H.hr, n_col * cap * K * 8), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&c->H.hrI, n_col * cap * K * 8), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&c->H.n_knots, n_col * 4), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&c->H.n_tau, n_col * 4), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&c->H.n_le, n_col * 4), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&c->H.status, n_col * 4), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&c->H.n_accept, n_col * 4), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&c->H.n_reject, n_col * 4), SBR_ENOMEM);
+    c->H.cap = (int32_t)cap;
+    c->hs_col = n_col;
+    c->hs_cap = cap;
+    c->hs_K = K;
+    return SBR_OK;
+}
+
 int ensure_stage(sbr_ctx* c, size_t bytes)
 {
     if (bytes <= c->stage_bytes) return SBR_OK;
@@ -109,6 +143,7 @@ sbr_opts resolve(const sbr_opts* o)
         if (r.knot_capacity <= 0) r.knot_capacity = kDefaultCap;
         if (r.ode_maxiters <= 0) r.ode_maxiters = 100000;
         if (r.bisect_max_iters <= 0) r.bisect_max_iters = 100;
+        if (r.hetero_max_iters <= 0) r.hetero_max_iters = 500;
     }
     return r;
 }
@@ -158,7 +193,7 @@ void sbr_default_opts(sbr_opts* o)
     o->bisect_max_iters = 100;
     o->early_exit_nan_run = 5;
     o->knot_capacity = kDefaultCap;
-    o->reserved = 0;
+    o->hetero_max_iters = 500;
 }
 
 int sbr_init(int device, sbr_ctx** out)
@@ -188,6 +223,7 @@ int sbr_free(sbr_ctx* c)
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     free_learn(c);
+    free_hetero(c);
     if (c->stage) (void)hipFree(c->stage);
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(c->stream);
@@ -372,6 +408,87 @@ int sbr_learn_stats(sbr_ctx* c, int64_t n_beta, int32_t* n_knots, int32_t* n_tau
                                            {n_reject, c->L.n_reject}, {(int32_t*)status, c->L.status}};
     for (auto& x : cp)
         if (x.h) HIP_TRY(c, hipMemcpy(x.h, x.d, (size_t)n_beta * 4, hipMemcpyDeviceToHost), SBR_EDEVICE);
+    return SBR_OK;
+}
+
+int sbr_sweep_hetero_dev(sbr_ctx* c, void* stream, int32_t K, const double* betas, const double* dist,
+                         const double* eta, const double* t_end, double x0, const double* u, int64_t n_col,
+                         int64_t n_u, double p, double kappa, double lambda, const sbr_opts* opts,
+                         sbr_result_soa* out, double* tau_in, double* tau_out)
+{
+    if (!c || !out || !out->xi || !out->aw_max || !out->tol || !out->status) return SBR_EARG;
+    if (K != 1 && K != 2 && K != 3 && K != 4 && K != 8) return fail(c, SBR_EARG, "K must be 1, 2, 3, 4 or 8");
+    if (n_col <= 0 || n_u <= 0 || n_col > (1 << 30) || n_u > (1 << 30)) return fail(c, SBR_EARG, "grid size");
+    if (!scalars_valid(x0, p, kappa, lambda)) return fail(c, SBR_EARG, "ArgumentError: x0/p/kappa/lambda");
+    if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
+    sbr_opts o = resolve(opts);
+    int rc = ensure_hetero(c, (size_t)n_col, (size_t)o.knot_capacity, (size_t)K);
+    if (rc) return rc;
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, p, lambda, o.ode_maxiters, (int32_t)n_col, 0};
+    sbr::HeteroEqArgs ea{kappa, 1e-12, (int32_t)n_u, o.hetero_max_iters, c->lds_cap * 3};
+    sbr::ResultSoA r{out->xi, nullptr, nullptr, out->aw_max, out->tol, out->status, out->iters};
+    mark(c, s);
+    HIP_TRY(c, sbr::launch_hetero(K, betas, dist, eta, t_end, u, la, ea, c->H, r, tau_in, tau_out, s, 0), SBR_EDEVICE);
+    mark(c, s);
+    HIP_TRY(c, sbr::launch_hetero(K, betas, dist, eta, t_end, u, la, ea, c->H, r, tau_in, tau_out, s, 1), SBR_EDEVICE);
+    mark(c, s);
+    return SBR_OK;
+}
+
+int sbr_sweep_hetero(sbr_ctx* c, int32_t K, const double* betas, const double* dist, const double* eta,
+                     const double* t_end, double x0, const double* u, int64_t n_col, int64_t n_u, double p,
+                     double kappa, double lambda, const sbr_opts* opts, sbr_result_soa* out, double* tau_in,
+                     double* tau_out)
+{
+    if (!c || !out || !betas || !dist || !eta || !t_end || !u || K <= 0) return SBR_EARG;
+    if (n_col <= 0 || n_u <= 0) return fail(c, SBR_EARG, "grid size");
+    // LearningParametersHetero checks (heterogeneity_model.jl:33-41)
+    double dsum = 0.0;
+    for (int k = 0; k < K; k++) {
+        if (!(dist[k] >= 0.0)) return fail(c, SBR_EARG, "ArgumentError: distribution weights must be non-negative");
+        dsum = dsum + dist[k];
+    }
+    if (!(fabs(dsum - 1.0) < 1e-10)) return fail(c, SBR_EARG, "ArgumentError: distribution must sum to 1");
+    for (int64_t i = 0; i < n_col * K; i++)
+        if (!(betas[i] > 0.0)) return fail(c, SBR_EARG, "ArgumentError: all learning rates must be positive");
+    for (int64_t i = 0; i < n_col; i++)
+        if (!(eta[i] > 0.0) || !(t_end[i] > 0.0)) return fail(c, SBR_EARG, "ArgumentError: eta/t_end");
+    for (int64_t j = 0; j < n_u; j++)
+        if (!(u[j] >= 0.0)) return fail(c, SBR_EARG, "ArgumentError: u must be non-negative");
+    if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
+    const size_t np = (size_t)n_col * (size_t)n_u;
+    const size_t in_d = (size_t)n_col * K + K + 2 * (size_t)n_col + (size_t)n_u;
+    const size_t out_d = np * 3 + np + 2 * np * K; // xi, aw, tol | status+iters | tin, tout
+    int rc = ensure_stage(c, (in_d + out_d) * 8 + 512);
+    if (rc) return rc;
+    double* d = (double*)c->stage;
+    double *dbeta = d, *ddist = dbeta + (size_t)n_col * K, *deta = ddist + K, *dtend = deta + n_col,
+           *du = dtend + n_col;
+    double* dres = du + n_u;
+    double *dxi = dres, *daw = dxi + np, *dtol = daw + np;
+    uint32_t* dst = (uint32_t*)(dtol + np);
+    int32_t* dit = (int32_t*)(dst + np);
+    double* dtin = (double*)(dit + np);
+    double* dtout = dtin + np * K;
+    hipStream_t s = c->stream;
+    HIP_TRY(c, hipMemcpyAsync(dbeta, betas, (size_t)n_col * K * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+    HIP_TRY(c, hipMemcpyAsync(ddist, dist, (size_t)K * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+    HIP_TRY(c, hipMemcpyAsync(deta, eta, (size_t)n_col * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+    HIP_TRY(c, hipMemcpyAsync(dtend, t_end, (size_t)n_col * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+    HIP_TRY(c, hipMemcpyAsync(du, u, (size_t)n_u * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+    sbr_result_soa r{dxi, nullptr, nullptr, daw, dtol, dst, dit};
+    rc = sbr_sweep_hetero_dev(c, s, K, dbeta, ddist, deta, dtend, x0, du, n_col, n_u, p, kappa, lambda, opts, &r,
+                              tau_in ? dtin : nullptr, tau_out ? dtout : nullptr);
+    if (rc) return rc;
+    if (out->xi) HIP_TRY(c, hipMemcpyAsync(out->xi, dxi, np * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+    if (out->aw_max) HIP_TRY(c, hipMemcpyAsync(out->aw_max, daw, np * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+    if (out->tol) HIP_TRY(c, hipMemcpyAsync(out->tol, dtol, np * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+    if (out->status) HIP_TRY(c, hipMemcpyAsync(out->status, dst, np * 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+    if (out->iters) HIP_TRY(c, hipMemcpyAsync(out->iters, dit, np * 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+    if (tau_in) HIP_TRY(c, hipMemcpyAsync(tau_in, dtin, np * K * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+    if (tau_out) HIP_TRY(c, hipMemcpyAsync(tau_out, dtout, np * K * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+    HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
     return SBR_OK;
 }
 

@@ -1,0 +1,561 @@
+// sbr_hetero.hip — gfx950 kernels for the heterogeneity extension (K coupled
+// learning groups), src/extensions/heterogeneity/.
+//
+//   learn_hetero_kernel<K>        one lane per parameter column: FP64 Tsit5 on
+//                                 dG_k/dt = (1−G_k) β_k Σ_j dist_j G_j with the
+//                                 RMS error norm over K components
+//                                 (heterogeneity_learning.jl:49-94), pdfs
+//                                 (compute_pdf_hetero :114-134) and the K hazard
+//                                 rates on the explicit-grid τ̄ (solver.jl:163-164:
+//                                 η always appended) streamed per knot.
+//   equilibrium_hetero_kernel<K>  one lane per (column, u): K crossing scans,
+//                                 the dist-weighted ξ bisection on [0, 2 max τ̄_OUT]
+//                                 (compute_ξ_hetero :48-144), the multimodality
+//                                 validity check (:175-210) and AW_max over the
+//                                 whole learning grid (get_AW_hetero :316-375).
+// Knot times are staged in LDS; G (AoS [knot][K]) and HR ([K][τ̄]) stay in HBM/L2.
+// Bit-exact against oracle/sbr_oracle.c (sbro_sweep_hetero).
+#include "sbr_device.h"
+#include "sbr_kernels.h"
+
+namespace sbr {
+
+template <int K>
+__device__ __forceinline__ double omega(const double* __restrict__ dist, const double* I)
+{
+    double w = dist[0] * I[0];
+#pragma unroll
+    for (int j = 1; j < K; j++) w = w + dist[j] * I[j];
+    return w;
+}
+
+template <int K>
+__device__ __forceinline__ void rhs(const double* __restrict__ dist, const double* b, const double* I, double* du)
+{
+    const double w = omega<K>(dist, I);
+#pragma unroll
+    for (int k = 0; k < K; k++) du[k] = ((1.0 - I[k]) * b[k]) * w;
+}
+
+template <int K>
+__device__ __forceinline__ double rms(const double* v)
+{
+    if (K == 1) return fabs(v[0]);
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i < K; i++) s = s + v[i] * v[i];
+    return sqrt(s / (double)K);
+}
+
+template <int K>
+__global__ __launch_bounds__(64) void learn_hetero_kernel(const double* __restrict__ betas,
+                                                          const double* __restrict__ dist,
+                                                          const double* __restrict__ eta,
+                                                          const double* __restrict__ t_end, LearnArgs a, HeteroBufs L)
+{
+    const int c = blockIdx.x * 64 + threadIdx.x;
+    if (c >= a.n_beta) return;
+    double b[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) b[k] = betas[(size_t)c * K + k];
+    const double ETA = eta[c], T1 = t_end[c], T0 = 0.0;
+    const size_t cap = (size_t)L.cap;
+    double* __restrict__ T = L.t + (size_t)c * cap;
+    double* __restrict__ Gv = L.G + (size_t)c * cap * K;
+    double* __restrict__ H = L.hr + (size_t)c * K * cap;
+    double* __restrict__ HI = L.hrI + (size_t)c * K * cap;
+    uint32_t st = 0;
+    bool argok = ETA > 0.0 && T1 > T0;
+#pragma unroll
+    for (int k = 0; k < K; k++) argok = argok && (b[k] > 0.0);
+    if (!argok) {
+        L.status[c] = SBR_ARG_INVALID;
+        L.n_knots[c] = 0; L.n_tau[c] = 0; L.n_le[c] = 0; L.n_accept[c] = 0; L.n_reject[c] = 0;
+        return;
+    }
+    const double x0 = a.x0, rtol = a.rtol, atol = a.atol, p = a.p, lam = a.lam;
+    const double dtmax = T1 - T0;
+    const double dtmin = sbr_jl_eps(dmax(fabs(T0), fabs(T1)));
+    double x[K], k1[K], k2[K], k3[K], k4[K], k5[K], k6[K], k7[K], tmp[K], tmp6[K], u[K], buf[K];
+
+    // ---- ode_determine_initdt ----
+    double sk[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) { x[k] = x0; sk[k] = fma(fabs(x0), rtol, atol); buf[k] = x0 / sk[k]; }
+    const double d0 = rms<K>(buf);
+    rhs<K>(dist, b, x, k1);
+#pragma unroll
+    for (int k = 0; k < K; k++) buf[k] = k1[k] / sk[k];
+    const double d1 = rms<K>(buf);
+    double dt0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * (d0 / d1);
+    dt0 = dmin(dt0, dtmax);
+    double dt;
+    if (dt0 < 10.0 * DBL_EPS) {
+        dt = dmax(1e-6, dtmin);
+    } else {
+#pragma unroll
+        for (int k = 0; k < K; k++) u[k] = fma(dt0, k1[k], x0);
+        rhs<K>(dist, b, u, k7);
+        bool same = true;
+#pragma unroll
+        for (int k = 0; k < K; k++) same = same && (k1[k] == k7[k]);
+        if (same) {
+            dt = dmax(dtmin, 100.0 * dt0);
+        } else {
+#pragma unroll
+            for (int k = 0; k < K; k++) buf[k] = (k7[k] - k1[k]) / sk[k];
+            const double d2 = rms<K>(buf) / dt0;
+            const double md = dmax(d1, d2);
+            const double dt1 = (md <= 1e-15) ? dmax(1e-6, dt0 * 1e-3) : sbr_pow_pos(0.01 / md, 1.0 / 6.0);
+            dt = dmax(dtmin, dmin(dmin(100.0 * dt0, dt1), dtmax));
+        }
+    }
+
+    // ---- knot sink: (t, G[K]) + streamed hazard terms per group ----
+    int n = 0, m = 0;
+    double tprev = 0.0, Ik[K], eprev[K], gprev[K];
+    bool past = false, done = false;
+#pragma unroll
+    for (int k = 0; k < K; k++) { Ik[k] = 0.0; eprev[k] = 0.0; gprev[k] = 0.0; }
+    auto push = [&](double t, const double* xs) {
+        if (n >= L.cap) { st |= SBR_KNOT_OVERFLOW; done = true; return; }
+        T[n] = t;
+#pragma unroll
+        for (int k = 0; k < K; k++) Gv[(size_t)n * K + k] = xs[k];
+        if (!past) {
+            const double w = omega<K>(dist, xs);
+            double g[K];
+#pragma unroll
+            for (int k = 0; k < K; k++) g[k] = ((1.0 - xs[k]) * b[k]) * w;
+            if (t <= ETA) {
+                const double E = sbr_exp(lam * t);
+#pragma unroll
+                for (int k = 0; k < K; k++) {
+                    const double e = E * g[k];
+                    Ik[k] = (m == 0) ? 0.0 : Ik[k] + (0.5 * (eprev[k] + e)) * (t - tprev);
+                    H[(size_t)k * cap + m] = (p * E) * g[k];
+                    HI[(size_t)k * cap + m] = Ik[k];
+                    eprev[k] = e;
+                    gprev[k] = g[k];
+                }
+                m++;
+                tprev = t;
+            } else {
+                past = true; // η always appended (explicit grid): pdf(η) on bracket [n-1, n]
+                const double d = (ETA - tprev) / (t - tprev);
+                const double E = sbr_exp(lam * ETA);
+#pragma unroll
+                for (int k = 0; k < K; k++) {
+                    const double pe = gprev[k] * (1.0 - d) + g[k] * d;
+                    const double e = E * pe;
+                    Ik[k] = Ik[k] + (0.5 * (eprev[k] + e)) * (ETA - tprev);
+                    H[(size_t)k * cap + m] = (p * E) * pe;
+                    HI[(size_t)k * cap + m] = Ik[k];
+                }
+                m++;
+            }
+        }
+        n++;
+    };
+
+    double t = T0, qold = CTL_QOLDMIN, q11 = 1.0;
+    AutoSwitch as;
+    int naccept = 0, nreject = 0;
+    push(t, x);
+    int64_t iter = 0;
+    while (t < T1 && !done) {
+        if (++iter > a.maxiters) { st |= SBR_ODE_MAXITERS; break; }
+        dt = dmin(dtmax, dt);
+        dt = dmax(dt, dtmin);
+        dt = dmin(dt, T1 - t);
+        const double a21 = dt * A21;
+#pragma unroll
+        for (int k = 0; k < K; k++) tmp[k] = fma(a21, k1[k], x[k]);
+        rhs<K>(dist, b, tmp, k2);
+#pragma unroll
+        for (int k = 0; k < K; k++) tmp[k] = fma(dt, fma(A31, k1[k], A32 * k2[k]), x[k]);
+        rhs<K>(dist, b, tmp, k3);
+#pragma unroll
+        for (int k = 0; k < K; k++) tmp[k] = fma(dt, fma(A41, k1[k], fma(A42, k2[k], A43 * k3[k])), x[k]);
+        rhs<K>(dist, b, tmp, k4);
+#pragma unroll
+        for (int k = 0; k < K; k++)
+            tmp[k] = fma(dt, fma(A51, k1[k], fma(A52, k2[k], fma(A53, k3[k], A54 * k4[k]))), x[k]);
+        rhs<K>(dist, b, tmp, k5);
+#pragma unroll
+        for (int k = 0; k < K; k++)
+            tmp6[k] = fma(dt, fma(A61, k1[k], fma(A62, k2[k], fma(A63, k3[k], fma(A64, k4[k], A65 * k5[k])))), x[k]);
+        rhs<K>(dist, b, tmp6, k6);
+#pragma unroll
+        for (int k = 0; k < K; k++)
+            u[k] = fma(dt, fma(A71, k1[k], fma(A72, k2[k], fma(A73, k3[k], fma(A74, k4[k], fma(A75, k5[k], A76 * k6[k]))))),
+                       x[k]);
+        rhs<K>(dist, b, u, k7);
+        double eig = 0.0;
+        bool eig_nan = false;
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const double r = fabs((k7[k] - k6[k]) / (u[k] - tmp6[k]));
+            if (r != r) eig_nan = true;
+            else if (r > eig) eig = r;
+        }
+        if (eig_nan) eig = NAN;
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const double ut = dt * fma(BT1, k1[k], fma(BT2, k2[k], fma(BT3, k3[k], fma(BT4, k4[k],
+                                       fma(BT5, k5[k], fma(BT6, k6[k], BT7 * k7[k]))))));
+            buf[k] = ut / fma(dmax(fabs(x[k]), fabs(u[k])), rtol, atol);
+        }
+        const double EEst = rms<K>(buf);
+        const double q = pi_q(EEst, qold, q11);
+        if (EEst <= 1.0) {
+            naccept++;
+            const double dtnew = dt / q;
+            qold = dmax(EEst, CTL_QOLDMIN);
+            double tn = t + dt;
+            if (fabs(tn - T1) < 100.0 * sbr_jl_eps(dmax(t, T1))) tn = T1;
+            t = tn;
+#pragma unroll
+            for (int k = 0; k < K; k++) { x[k] = u[k]; k1[k] = k7[k]; }
+            dt = dmax(dmin(dtmax, dtnew), dtmin);
+            push(t, x);
+        } else {
+            nreject++;
+            dt = dt / dmin(CTL_INV_QMIN, q11 / CTL_GAMMA);
+        }
+        if (!(dt > 0.0) || !isfinite(dt)) { st |= SBR_ODE_FAILED; break; }
+        as.update(eig, dt);
+    }
+    if (as.switched) st |= SBR_STIFF_SWITCH;
+    int n_le = m;
+    if (past) {
+        n_le = m - 1;
+    } else if (!(st & SBR_KNOT_OVERFLOW)) {
+        // no knot beyond η: pdf(η) exists only if the last knot is η itself
+        if (n >= 2 && tprev == ETA) {
+            const double E = sbr_exp(lam * ETA);
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+                // bracket clamps to [n-2, n-1] with δ = 1: gprev*(1-1) ... = g_{n-1}
+                const double pe = 0.0 + gprev[k] * 1.0;
+                H[(size_t)k * cap + m] = (p * E) * pe;
+                HI[(size_t)k * cap + m] = Ik[k];
+            }
+            m++;
+        } else {
+            st |= SBR_OOB;
+        }
+    }
+    if (m > 0 && !(st & SBR_OOB)) {
+        const double omp = 1.0 - p;
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const double Ieta = HI[(size_t)k * cap + m - 1];
+            for (int i = 0; i < m; i++)
+                H[(size_t)k * cap + i] = H[(size_t)k * cap + i] / ((p * HI[(size_t)k * cap + i]) + (omp * Ieta));
+        }
+    }
+    L.n_knots[c] = n;
+    L.n_tau[c] = m;
+    L.n_le[c] = n_le;
+    L.status[c] = st;
+    L.n_accept[c] = naccept;
+    L.n_reject[c] = nreject;
+}
+
+// ---------------------------------------------------------------------------
+// per-point solve
+// ---------------------------------------------------------------------------
+template <int K, class PT>
+struct HCol {
+    PT T;                       // knot times (LDS or global)
+    const double* __restrict__ G;   // [n][K]
+    const double* __restrict__ H;   // [K][cap]
+    int n, ntau, nle;
+    size_t cap;
+    double ETA, T1;
+    __device__ __forceinline__ double tau(int i) const { return i < nle ? T[i] : ETA; }
+    __device__ __forceinline__ double g(int j, int k) const { return G[(size_t)j * K + k]; }
+    // Interpolations gridded-linear value of group k on bracket j (clamped)
+    __device__ __forceinline__ double lerp(int j, int k, double x) const
+    {
+        if (j > n - 2) j = n - 2;
+        if (j < 0) j = 0;
+        const double d = (x - T[j]) / (T[j + 1] - T[j]);
+        return g(j, k) * (1.0 - d) + g(j + 1, k) * d;
+    }
+};
+
+template <int K, class PT>
+__device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const double* __restrict__ dist,
+                                                   const double u, const double kappa, const int max_iters,
+                                                   const double tolerance, const uint32_t lbits, double& xi_o,
+                                                   double& aw_o, double& tol_o, uint32_t& st_o, int& it_o,
+                                                   double* tin, double* tout)
+{
+    xi_o = NAN; aw_o = NAN; tol_o = INFINITY; it_o = 0;
+    const int n = C.n;
+    const double tlo = C.T[0], thi = C.T[n - 1];
+    // ---------------- K crossing scans (optimal_buffer per group) ----------------
+    bool all_eq = true;
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const double* __restrict__ Hk = C.H + (size_t)k * C.cap;
+        bool any = false, all = true, prev = false;
+        int fa = -1, la = -1, cin = -1, cout = -1;
+        for (int i = 0; i < C.ntau; i++) {
+            const bool ab = Hk[i] > u;
+            any |= ab;
+            all &= ab;
+            if (ab) { if (fa < 0) fa = i; la = i; }
+            if (i > 0) {
+                if (!prev && ab && cin < 0) cin = i - 1;
+                if (prev && !ab) cout = i - 1;
+            }
+            prev = ab;
+        }
+        double a, b;
+        if (!any) {
+            a = C.T1; b = C.T1;
+        } else if (all) {
+            a = C.tau(0); b = C.tau(C.ntau - 1);
+        } else {
+            a = C.T1; b = C.T1;
+            if (cin >= 0) {
+                const double t0 = C.tau(cin), t1 = C.tau(cin + 1), h0 = Hk[cin], h1 = Hk[cin + 1];
+                a = t0 + ((u - h0) * (t1 - t0)) / (h1 - h0);
+            }
+            if (cout >= 0) {
+                const double t0 = C.tau(cout), t1 = C.tau(cout + 1), h0 = Hk[cout], h1 = Hk[cout + 1];
+                b = t0 + ((u - h0) * (t1 - t0)) / (h1 - h0);
+            }
+            if (a == C.T1) a = C.tau(fa);
+            if (b == C.T1) b = C.tau(la);
+        }
+        tin[k] = a;
+        tout[k] = b;
+        all_eq = all_eq && (a == b);
+    }
+    if (all_eq) {
+        st_o = SBR_NO_RUN_HR_BELOW_U | SBR_CONVERGED | lbits;
+        tol_o = 0.0;
+        return;
+    }
+    // ---------------- compute_ξ_hetero ----------------
+    uint32_t flag = 0;
+    double guess = (dist[0] * (tin[0] + tout[0])) / 2.0;
+    double mo = tout[0];
+#pragma unroll
+    for (int k = 1; k < K; k++) { guess = guess + (dist[k] * (tin[k] + tout[k])) / 2.0; mo = dmax(mo, tout[k]); }
+    double xmin = 0.0, xmax = mo * 2.0, xnew = guess;
+    // exact brackets and values of the constant lookup points tin_k, tout_k
+    int jin[K], jout[K];
+    double gin[K], gout[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        jin[k] = -1; jout[k] = -1; gin[k] = 0.0; gout[k] = 0.0;
+        if (tin[k] >= tlo && tin[k] <= thi) { jin[k] = ssl_range(C.T, 0, n - 1, tin[k]); gin[k] = C.lerp(jin[k], k, tin[k]); }
+        if (tout[k] >= tlo && tout[k] <= thi) { jout[k] = ssl_range(C.T, 0, n - 1, tout[k]); gout[k] = C.lerp(jout[k], k, tout[k]); }
+    }
+    int jlo = 0, jhi = n - 1;
+    uint32_t s = SBR_NO_RUN_MAXITER;
+    double xi = NAN, tolr = INFINITY;
+    for (int iter = 1; iter <= max_iters; iter++) {
+        it_o = iter;
+        const double dd = xmin - xmax;
+        if (fabs(dd) < 2.0 * sbr_jl_eps(dd)) { s = SBR_NO_RUN_COLLAPSE; break; }
+        if (iter == max_iters - 1) { s = SBR_NO_RUN_MAXITER; break; }
+        const double xo = xnew;
+        if (!(xo >= tlo)) { flag |= SBR_OOB; break; }  // searchsortedlast = 0: BoundsError
+        const int j = ssl_range(C.T, jlo, jhi, xo); // t[jlo] <= ξmin <= xo <= ξmax < t[jhi+1]
+        const int i2 = j + 1 < n - 1 ? j + 1 : n - 1;
+        const double eps = C.T[i2] - C.T[j];
+        double AW = 0.0, AWe = 0.0;
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const double ic = dmin(tin[k], xo), oc = dmin(tout[k], xo);
+            // value and bracket of oc, ic (each is either xo or the group constant)
+            int joc, jic;
+            double Goc, Gic;
+            if (oc == xo) { joc = xo <= thi ? j : -1; Goc = joc >= 0 ? C.lerp(j, k, xo) : 0.0; }
+            else { joc = jout[k]; Goc = gout[k]; }
+            if (ic == xo) { jic = xo <= thi ? j : -1; Gic = jic >= 0 ? C.lerp(j, k, xo) : 0.0; }
+            else { jic = jin[k]; Gic = gin[k]; }
+            if (joc < 0 || jic < 0) flag |= SBR_OOB;
+            const double xoe = oc + eps, xie = ic + eps;
+            double Goce = 0.0, Gice = 0.0;
+            if (xoe <= thi && joc >= 0) Goce = C.lerp(ssl_gallop(C.T, n, joc, xoe), k, xoe);
+            else flag |= SBR_OOB;
+            if (xie <= thi && jic >= 0) Gice = C.lerp(ssl_gallop(C.T, n, jic, xie), k, xie);
+            else flag |= SBR_OOB;
+            AW = AW + dist[k] * (Goc - Gic);
+            AWe = AWe + dist[k] * (Goce - Gice);
+        }
+        if (flag) break;
+        const double err = AW - kappa;
+        const bool inc = AWe >= AW;
+        if (fabs(err) <= tolerance) {
+            if (inc) { s = SBR_RUN; xi = xo; tolr = fabs(err); }
+            else s = SBR_FALSE_EQ;
+            break;
+        } else if (err > 0) {
+            xmax = xo;
+            jhi = j;
+            xnew = 0.5 * (xo + xmin);
+        } else {
+            xmin = xo;
+            jlo = j;
+            xnew = 0.5 * (xo + xmax);
+        }
+    }
+    if (flag) { st_o = flag | lbits; return; }
+    if (s != SBR_RUN) { st_o = s | lbits; return; }
+
+    // ---------------- is_valid_equilibrium_hetero ----------------
+    {
+        double tI[K];
+        int jp[K];
+#pragma unroll
+        for (int k = 0; k < K; k++) { tI[k] = dmax(0.0, xi - tin[k]); jp[k] = 0; }
+        bool prev = false, valid = true;
+        for (int i = 0; i < n && C.T[i] <= xi; i++) {
+            const double ti = C.T[i];
+            double aw = 0.0;
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+                const double a = C.lerp(i, k, ti);
+                const double x = dmax(0.0, ti - tI[k]);
+                while (jp[k] + 1 < n && C.T[jp[k] + 1] <= x) jp[k]++;
+                const double bb = C.lerp(jp[k], k, x);
+                aw = aw + dist[k] * (a - bb);
+            }
+            const bool above = aw > kappa;
+            if (i > 0 && prev && !above) { valid = false; break; }
+            prev = above;
+        }
+        if (!valid) { st_o = SBR_HETERO_INVALID | lbits; return; }
+    }
+    // ---------------- AW_max over the whole learning grid ----------------
+    double icc[K], occ[K];
+    int ja[K], jb[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) { icc[k] = dmin(tin[k], xi); occ[k] = dmin(tout[k], xi); ja[k] = 0; jb[k] = 0; }
+    double mx = -INFINITY;
+    for (int i = 0; i < n; i++) {
+        const double ti = C.T[i];
+        double cum = 0.0;
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const double av = (ti - xi) + icc[k];
+            const double bv = (ti - xi) + occ[k];
+            const double xa = av > 0 ? av : 0.0;
+            const double xb = bv > 0 ? bv : 0.0;
+            if (!(xa <= thi) || !(xb <= thi)) flag |= SBR_OOB;
+            while (ja[k] + 1 < n && C.T[ja[k] + 1] <= xa) ja[k]++;
+            while (jb[k] + 1 < n && C.T[jb[k] + 1] <= xb) jb[k]++;
+            const double gi = C.lerp(ja[k], k, xa);
+            const double go = C.lerp(jb[k], k, xb);
+            const double awin = av >= 0 ? gi : 0.0;
+            const double awout = bv >= 0 ? go : 0.0;
+            cum = cum + dist[k] * (awout - awin);
+        }
+        if (mx == mx && (cum != cum || cum > mx)) mx = cum;
+    }
+    if (flag) { st_o = flag | lbits; return; }
+    xi_o = xi;
+    tol_o = tolr;
+    aw_o = mx;
+    st_o = SBR_RUN | SBR_CONVERGED | lbits;
+}
+
+template <int K, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void equilibrium_hetero_kernel(HeteroBufs L, const double* __restrict__ dist,
+                                                                   const double* __restrict__ eta,
+                                                                   const double* __restrict__ t_end,
+                                                                   const double* __restrict__ u, HeteroEqArgs a,
+                                                                   ResultSoA out, double* __restrict__ tin_out,
+                                                                   double* __restrict__ tout_out)
+{
+    extern __shared__ double smem[];
+    const int c = blockIdx.y;
+    const int n = L.n_knots[c];
+    const uint32_t lst = L.status[c];
+    const size_t cap = (size_t)L.cap;
+    const double* __restrict__ gT = L.t + (size_t)c * cap;
+    const bool fits = n <= a.lds_cap;
+    if (fits)
+        for (int i = threadIdx.x; i < n; i += BLOCK) smem[i] = gT[i];
+    __syncthreads();
+    const int j = blockIdx.x * BLOCK + threadIdx.x;
+    if (j >= a.n_u) return;
+    double dl[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) dl[k] = dist[k];
+    const double uj = u[j];
+    const uint32_t lbits = lst & (SBR_ODE_MAXITERS | SBR_STIFF_SWITCH | SBR_ODE_FAILED | SBR_KNOT_OVERFLOW);
+    double xi, aw, tol, tin[K], tout[K];
+    uint32_t st;
+    int it;
+    if ((lst & (SBR_ARG_INVALID | SBR_OOB)) || n < 2 || !(uj >= 0.0)) {
+        xi = NAN; aw = NAN; tol = INFINITY; it = 0;
+#pragma unroll
+        for (int k = 0; k < K; k++) { tin[k] = NAN; tout[k] = NAN; }
+        st = ((lst & SBR_ARG_INVALID) || !(uj >= 0.0)) ? SBR_ARG_INVALID : (SBR_OOB | lbits);
+    } else if (fits) {
+        HCol<K, const double*> C{smem, L.G + (size_t)c * cap * K, L.hr + (size_t)c * K * cap, n, L.n_tau[c],
+                                 L.n_le[c], cap, eta[c], t_end[c]};
+        solve_hetero_point<K>(C, dl, uj, a.kappa, a.max_iters, a.tolerance, lbits, xi, aw, tol, st, it, tin, tout);
+    } else {
+        HCol<K, const double*> C{gT, L.G + (size_t)c * cap * K, L.hr + (size_t)c * K * cap, n, L.n_tau[c],
+                                 L.n_le[c], cap, eta[c], t_end[c]};
+        solve_hetero_point<K>(C, dl, uj, a.kappa, a.max_iters, a.tolerance, lbits, xi, aw, tol, st, it, tin, tout);
+    }
+    const size_t o = (size_t)c * (size_t)a.n_u + j;
+    out.xi[o] = xi;
+    out.aw_max[o] = aw;
+    out.tol[o] = tol;
+    out.status[o] = st;
+    if (out.iters) out.iters[o] = it;
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        if (tin_out) tin_out[o * K + k] = tin[k];
+        if (tout_out) tout_out[o * K + k] = tout[k];
+    }
+}
+
+template <int K>
+static hipError_t launch_hetero_k(const double* betas, const double* dist, const double* eta, const double* t_end,
+                                  const double* u, const LearnArgs& la, const HeteroEqArgs& ea, const HeteroBufs& L,
+                                  const ResultSoA& out, double* tin, double* tout, hipStream_t s, int phase)
+{
+    if (phase == 0) {
+        hipLaunchKernelGGL(learn_hetero_kernel<K>, dim3((la.n_beta + 63) / 64), dim3(64), 0, s, betas, dist, eta,
+                           t_end, la, L);
+        return hipGetLastError();
+    }
+    const size_t lds = (size_t)ea.lds_cap * sizeof(double);
+    if (ea.n_u >= 256) {
+        hipLaunchKernelGGL((equilibrium_hetero_kernel<K, 256>), dim3((ea.n_u + 255) / 256, la.n_beta), dim3(256), lds, s,
+                           L, dist, eta, t_end, u, ea, out, tin, tout);
+    } else {
+        hipLaunchKernelGGL((equilibrium_hetero_kernel<K, 64>), dim3((ea.n_u + 63) / 64, la.n_beta), dim3(64), lds, s,
+                           L, dist, eta, t_end, u, ea, out, tin, tout);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_hetero(int K, const double* betas, const double* dist, const double* eta, const double* t_end,
+                         const double* u, const LearnArgs& la, const HeteroEqArgs& ea, const HeteroBufs& L,
+                         const ResultSoA& out, double* tin, double* tout, hipStream_t s, int phase)
+{
+    switch (K) {
+    case 1: return launch_hetero_k<1>(betas, dist, eta, t_end, u, la, ea, L, out, tin, tout, s, phase);
+    case 2: return launch_hetero_k<2>(betas, dist, eta, t_end, u, la, ea, L, out, tin, tout, s, phase);
+    case 3: return launch_hetero_k<3>(betas, dist, eta, t_end, u, la, ea, L, out, tin, tout, s, phase);
+    case 4: return launch_hetero_k<4>(betas, dist, eta, t_end, u, la, ea, L, out, tin, tout, s, phase);
+    case 8: return launch_hetero_k<8>(betas, dist, eta, t_end, u, la, ea, L, out, tin, tout, s, phase);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace sbr

@@ -42,6 +42,33 @@ struct ResultSoA {
     int32_t* iters;
 };
 
+// Hetero learning output: t [n_col][cap], G [n_col][cap][K], hr/hrI [n_col][K][cap].
+struct HeteroBufs {
+    double* t;
+    double* G;
+    double* hr;
+    double* hrI;
+    int32_t* n_knots;
+    int32_t* n_tau;
+    int32_t* n_le;
+    uint32_t* status;
+    int32_t* n_accept;
+    int32_t* n_reject;
+    int32_t cap;
+};
+
+struct HeteroEqArgs {
+    double kappa;
+    double tolerance;   // compute_ξ_hetero tolerance (1e-12 absolute)
+    int32_t n_u;
+    int32_t max_iters;  // 500
+    int32_t lds_cap;    // knot times staged in LDS
+};
+
+hipError_t launch_hetero(int K, const double* betas, const double* dist, const double* eta, const double* t_end,
+                         const double* u, const LearnArgs& la, const HeteroEqArgs& ea, const HeteroBufs& L,
+                         const ResultSoA& out, double* tin, double* tout, hipStream_t s, int phase);
+
 hipError_t launch_learn_logistic(const double* beta, const double* eta, const double* t_end, const LearnArgs& a,
                                  const LearnBufs& L, hipStream_t s);
 hipError_t launch_equilibrium(const LearnBufs& L, const double* eta, const double* t_end, const double* u,

@@ -39,7 +39,7 @@ class Opts(ctypes.Structure):
         ("bisect_max_iters", _I32),
         ("early_exit_nan_run", _I32),
         ("knot_capacity", _I32),
-        ("reserved", _I32),
+        ("hetero_max_iters", _I32),
     ]
 
 
