@@ -48,7 +48,13 @@ typedef struct {
     int32_t early_exit_nan_run; /* 1_baseline.jl:147,221: 5; 0 disables */
     int32_t knot_capacity;      /* engine limit on stored knots per β (0 = default 8192) */
     int32_t hetero_max_iters;   /* heterogeneity_solver.jl:49 max_iters = 500 */
+    int32_t flags;              /* SBR_FLAG_* */
+    int32_t pad;
 } sbr_opts;
+
+/* Evaluate every τ̄ knot of the crossing scan and of the AW path (no block
+ * summaries / branch-and-bound).  Same results; for A/B timing and checks. */
+#define SBR_FLAG_EXHAUSTIVE 0x1
 
 typedef struct {
     double* xi;          /* SolvedModel.ξ                       */
@@ -149,6 +155,10 @@ int sbr_timing_read(sbr_ctx* ctx, void* stream, double* learn_ms, double* eq_ms,
  * accepted / rejected RK steps, learning status bits) for flop accounting. */
 int sbr_learn_stats(sbr_ctx* ctx, int64_t n_beta, int32_t* n_knots, int32_t* n_tau, int32_t* n_accept,
                     int32_t* n_reject, uint32_t* status);
+
+/* Device facts the engine sized itself with: LDS bytes per workgroup, knots
+ * staged in LDS per β column, compute units. */
+int sbr_device_info(sbr_ctx* ctx, int32_t* lds_bytes_per_block, int32_t* lds_knot_capacity, int32_t* cu_count);
 
 /* Diagnostics: sbr_exp / sbr_log / sbr_pow_pos (include/sbr_detmath.h)
  * evaluated on the device, for host/device bit-equality tests. */

@@ -201,28 +201,146 @@ __device__ __forceinline__ bool in_range(double x, double tlo, double thi, bool 
     return false;
 }
 
+// Per-workgroup summaries staged in LDS next to the knot grid (null = unavailable):
+//   hmax/hmin  per 64-entry block of HR(τ̄): max over non-NaN entries / min with NaN as −∞,
+//              i.e. "some entry > u" ⇔ hmax > u and "every entry > u" ⇔ hmin > u;
+//   pmc/smc    per 64-knot block of G: prefix max / suffix min over blocks (NaN-propagating).
+struct Summ {
+    const double* hmax;
+    const double* hmin;
+    const double* pmc;
+    const double* smc;
+};
+
+// first i >= s with H[i] > u (or -1); whole blocks are skipped on their summary
 template <class P>
-__device__ __forceinline__ void solve_point(P T, P G, P H, const int n, const int ntau, const int nle,
-                                            const double ETA, const double T1, const bool trunc, const double u,
-                                            const double kappa, const int max_iters, const uint32_t lbits,
-                                            PointResult& r, double* __restrict__ aw_path)
+__device__ __forceinline__ int first_above(P H, const Summ& S, int ntau, int s, double u)
+{
+    int i = s;
+    for (; i < ntau && (i & 63); i++)
+        if (H[i] > u) return i;
+    for (; i < ntau; i += 64) {
+        if (S.hmax[i >> 6] > u) {
+            const int e = i + 64 < ntau ? i + 64 : ntau;
+            for (; i < e; i++)
+                if (H[i] > u) return i;
+            return -1;
+        }
+    }
+    return -1;
+}
+
+// first i >= s with !(H[i] > u) (or -1)
+template <class P>
+__device__ __forceinline__ int first_not_above(P H, const Summ& S, int ntau, int s, double u)
+{
+    int i = s;
+    for (; i < ntau && (i & 63); i++)
+        if (!(H[i] > u)) return i;
+    for (; i < ntau; i += 64) {
+        if (!(S.hmin[i >> 6] > u)) {
+            const int e = i + 64 < ntau ? i + 64 : ntau;
+            for (; i < e; i++)
+                if (!(H[i] > u)) return i;
+            return -1;
+        }
+    }
+    return -1;
+}
+
+// last i <= e with H[i] > u (or -1)
+template <class P>
+__device__ __forceinline__ int last_above(P H, const Summ& S, int e, double u)
+{
+    if (e < 0) return -1;
+    const int b0 = e >> 6;
+    for (int i = e; i >= (b0 << 6); i--)
+        if (H[i] > u) return i;
+    for (int b = b0 - 1; b >= 0; b--) {
+        if (S.hmax[b] > u) {
+            for (int i = (b << 6) + 63; i >= (b << 6); i--)
+                if (H[i] > u) return i;
+            return -1;
+        }
+    }
+    return -1;
+}
+
+// last i <= e with !(H[i] > u) (or -1)
+template <class P>
+__device__ __forceinline__ int last_not_above(P H, const Summ& S, int e, double u)
+{
+    if (e < 0) return -1;
+    const int b0 = e >> 6;
+    for (int i = e; i >= (b0 << 6); i--)
+        if (!(H[i] > u)) return i;
+    for (int b = b0 - 1; b >= 0; b--) {
+        if (!(S.hmin[b] > u)) {
+            for (int i = (b << 6) + 63; i >= (b << 6); i--)
+                if (!(H[i] > u)) return i;
+            return -1;
+        }
+    }
+    return -1;
+}
+
+// The linear scan of optimal_buffer (solver.jl:218-261) answered with block
+// summaries: any/all, first/last index above u, first 0→1 and last 1→0 pair.
+template <class P>
+__device__ __forceinline__ void buffer_scan_blocked(P H, const Summ& S, int ntau, double u, bool& any, bool& all,
+                                                    int& fa, int& la, int& cin, int& cout)
+{
+    fa = first_above(H, S, ntau, 0, u);
+    any = fa >= 0;
+    const int fb = first_not_above(H, S, ntau, 0, u);
+    all = fb < 0;
+    la = any ? last_above(H, S, ntau - 1, u) : -1;
+    cin = -1;
+    cout = -1;
+    if (!any || all) return;
+    if (fa > 0) {
+        cin = fa - 1; // H[0..fa) not above, H[fa] above
+    } else {
+        const int k = first_above(H, S, ntau, fb, u); // first above after the first drop
+        cin = k >= 0 ? k - 1 : -1;
+    }
+    if (la < ntau - 1) {
+        cout = la; // everything after la is not above
+    } else {
+        const int lb = last_not_above(H, S, ntau - 1, u);
+        cout = last_above(H, S, lb, u);
+    }
+}
+
+template <class P>
+__device__ __forceinline__ void solve_point(P T, P G, P H, const Summ& S, const int n, const int ntau,
+                                            const int nle, const double ETA, const double T1, const bool trunc,
+                                            const double u, const double kappa, const int max_iters,
+                                            const uint32_t lbits, PointResult& r, double* __restrict__ aw_path)
 {
     r.xi = NAN; r.aw = NAN; r.tol = INFINITY; r.iters = 0; r.status = 0;
     const double tlo = T[0], thi = T[n - 1];
 
-    // ---------------- optimal_buffer: one pass over the τ̄ grid ----------------
-    bool any = false, all = true, prev = false;
-    int fa = -1, la = -1, cin = -1, cout = -1;
-    for (int i = 0; i < ntau; i++) {
-        const bool ab = H[i] > u;
-        any |= ab;
-        all &= ab;
-        if (ab) { if (fa < 0) fa = i; la = i; }
-        if (i > 0) {
-            if (!prev && ab && cin < 0) cin = i - 1;
-            if (prev && !ab) cout = i - 1;
+    // ---------------- optimal_buffer: crossings of HR(τ̄) with u ----------------
+    bool any, all;
+    int fa, la, cin, cout;
+    if (S.hmax) {
+        buffer_scan_blocked(H, S, ntau, u, any, all, fa, la, cin, cout);
+    } else {
+        any = false; all = true;
+        bool prev = false;
+        fa = la = cin = cout = -1;
+        for (int i = 0; i < ntau; i++) {
+            const bool ab = H[i] > u;
+            any |= ab;
+            all &= ab;
+            if (ab) { if (fa < 0) fa = i; la = i; }
+            if (i > 0) {
+                if (!prev && ab && cin < 0) cin = i - 1;
+                if (prev && !ab) cout = i - 1;
+            }
+            prev = ab;
         }
-        prev = ab;
     }
     auto tau = [&](int i) -> double { return i < nle ? T[i] : ETA; };
     double tin, tout;
@@ -321,23 +439,70 @@ __device__ __forceinline__ void solve_point(P T, P G, P H, const int n, const in
     if (!in_range(0.0, tlo, thi, trunc, flag)) { r.status = flag | lbits; return; }
     const double G0 = lerp_at(T, G, n, ssl_range(T, 0, n - 1, 0.0), 0.0);
     double mx = -INFINITY;
-    int ji = 0, jo = 0;
-    for (int i = 0; i < ntau; i++) {
-        const double ti = tau(i);
-        const double av = (ti - xi) + icc;
-        const double bv = (ti - xi) + occ;
-        const double xa = av > 0 ? av : 0.0;
-        const double xb = bv > 0 ? bv : 0.0;
-        if (!(xa <= thi) || !(xb <= thi)) { flag |= trunc ? SBR_ENGINE_TRUNC : SBR_OOB; break; }
-        while (ji + 1 < n && T[ji + 1] <= xa) ji++;
-        while (jo + 1 < n && T[jo + 1] <= xb) jo++;
-        const double gi = lerp_at(T, G, n, ji, xa);
-        const double go = lerp_at(T, G, n, jo, xb);
-        const double awin = av >= 0 ? gi : 0.0;
-        const double awout = bv >= 0 ? go : 0.0;
-        const double v = (awout - awin) + G0;
-        if (aw_path) aw_path[i] = v;
-        if (mx == mx && (v != v || v > mx)) mx = v;
+    // exact AW_cum(τ̄_i) for i in [i0, i1), folded into the NaN-propagating max
+    auto eval_range = [&](int i0, int i1) {
+        const double a0 = (tau(i0) - xi) + icc, b0 = (tau(i0) - xi) + occ;
+        int ji = ssl_range(T, 0, n - 1, a0 > 0 ? a0 : 0.0);
+        int jo = ssl_range(T, 0, n - 1, b0 > 0 ? b0 : 0.0);
+        for (int i = i0; i < i1; i++) {
+            const double ti = tau(i);
+            const double av = (ti - xi) + icc;
+            const double bv = (ti - xi) + occ;
+            const double xa = av > 0 ? av : 0.0;
+            const double xb = bv > 0 ? bv : 0.0;
+            if (!(xa <= thi) || !(xb <= thi)) { flag |= trunc ? SBR_ENGINE_TRUNC : SBR_OOB; return; }
+            while (ji + 1 < n && T[ji + 1] <= xa) ji++;
+            while (jo + 1 < n && T[jo + 1] <= xb) jo++;
+            const double gi = lerp_at(T, G, n, ji, xa);
+            const double go = lerp_at(T, G, n, jo, xb);
+            const double awin = av >= 0 ? gi : 0.0;
+            const double awout = bv >= 0 ? go : 0.0;
+            const double v = (awout - awin) + G0;
+            if (aw_path) aw_path[i] = v;
+            if (mx == mx && (v != v || v > mx)) mx = v;
+        }
+    };
+    if (!S.pmc || aw_path) {
+        eval_range(0, ntau); // exhaustive (single-point path mode, or summaries unavailable)
+    } else {
+        // Branch and bound over 64-knot blocks of τ̄ — the same maximum, fewer evaluations.
+        // Every argument sequence is nondecreasing in i, so the range check of the
+        // last τ̄ covers the whole path.
+        const double al = (tau(ntau - 1) - xi) + icc, bl = (tau(ntau - 1) - xi) + occ;
+        if (!((al > 0 ? al : 0.0) <= thi) || !((bl > 0 ? bl : 0.0) <= thi)) {
+            flag |= trunc ? SBR_ENGINE_TRUNC : SBR_OOB;
+        } else {
+            const int nblk = (ntau + 63) >> 6;
+            // upper bound of AW_cum over block b: AW_OUT ≤ max G over knots up to the
+            // bracket of the block's last argument, AW_IN ≥ min G over knots from the
+            // bracket of its first argument (coarse prefix-max / suffix-min tables),
+            // plus a rounding margin far above the ≈2e-15 the exact path can add.
+            int ja = 0, jb = 0;
+            auto block_ub = [&](int bk) -> double {
+                const int i0 = bk << 6, i1 = (i0 + 64 < ntau ? i0 + 64 : ntau) - 1;
+                const double av0 = (tau(i0) - xi) + icc;
+                const double bv1 = (tau(i1) - xi) + occ;
+                ja = ssl_gallop(T, n, ja, av0 > 0 ? av0 : 0.0);
+                jb = ssl_gallop(T, n, jb, bv1 > 0 ? bv1 : 0.0);
+                const double hi = S.pmc[(jb + 1 < n - 1 ? jb + 1 : n - 1) >> 6];
+                const double lo = S.smc[(ja < n - 2 ? ja : n - 2) >> 6];
+                const double ub_out = hi > 0.0 ? hi : 0.0;
+                const double lb_in = av0 >= 0 ? lo : (lo < 0.0 ? lo : 0.0);
+                return ((ub_out - lb_in) + G0) + 1e-14;
+            };
+            int best = 0;
+            double bub = -INFINITY;
+            for (int bk = 0; bk < nblk; bk++) {
+                const double ub = block_ub(bk);
+                if (!(ub <= bub)) { bub = ub; best = bk; }
+            }
+            eval_range(best << 6, (best << 6) + 64 < ntau ? (best << 6) + 64 : ntau);
+            ja = 0; jb = 0;
+            for (int bk = 0; bk < nblk && !flag; bk++) {
+                const double ub = block_ub(bk);
+                if (bk != best && !(ub <= mx)) eval_range(bk << 6, (bk << 6) + 64 < ntau ? (bk << 6) + 64 : ntau);
+            }
+        }
     }
     if (flag) { r.status = flag | lbits; return; }
     r.xi = xi;
@@ -363,11 +528,59 @@ __global__ __launch_bounds__(BLOCK) void equilibrium_kernel(LearnBufs L, const d
     double* sT = smem;
     double* sG = smem + a.lds_cap;
     double* sH = smem + 2 * a.lds_cap;
+    // block summaries behind the three knot arrays (lds_cap/64 + 1 entries each)
+    const int nsum = (a.lds_cap >> 6) + 1;
+    double* hmax = smem + 3 * a.lds_cap;
+    double* hmin = hmax + nsum;
+    double* pmc = hmin + nsum;
+    double* smc = pmc + nsum;
     if (fits) {
         for (int i = threadIdx.x; i < n; i += BLOCK) { sT[i] = gT[i]; sG[i] = gG[i]; }
         for (int i = threadIdx.x; i < ntau; i += BLOCK) sH[i] = gH[i];
     }
     __syncthreads();
+    Summ S{nullptr, nullptr, nullptr, nullptr};
+    if (fits && !a.exhaustive) {
+        const int nbh = (ntau + 63) >> 6, nbg = (n + 63) >> 6;
+        for (int bk = threadIdx.x; bk < nbh + nbg; bk += BLOCK) {
+            if (bk < nbh) {
+                double mx = -INFINITY, mn = INFINITY;
+                const int e = (bk << 6) + 64 < ntau ? (bk << 6) + 64 : ntau;
+                for (int i = bk << 6; i < e; i++) {
+                    const double h = sH[i];
+                    if (h > mx) mx = h;                         // NaN never > u: ignore it
+                    mn = (h != h) ? -INFINITY : (h < mn ? h : mn); // NaN is "not above"
+                }
+                hmax[bk] = mx;
+                hmin[bk] = mn;
+            } else {
+                const int g = bk - nbh;
+                double mx = -INFINITY, mn = INFINITY;
+                const int e = (g << 6) + 64 < n ? (g << 6) + 64 : n;
+                for (int i = g << 6; i < e; i++) {
+                    const double v = sG[i];
+                    if (v != v) { mx = NAN; mn = NAN; break; }
+                    if (v > mx) mx = v;
+                    if (v < mn) mn = v;
+                }
+                pmc[g] = mx; // block max for now
+                smc[g] = mn; // block min for now
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) { // prefix max / suffix min over blocks (NaN-propagating)
+            for (int g = 1; g < nbg; g++) {
+                const double a0 = pmc[g - 1], b0 = pmc[g];
+                pmc[g] = (a0 != a0 || b0 != b0) ? NAN : (a0 > b0 ? a0 : b0);
+            }
+            for (int g = nbg - 2; g >= 0; g--) {
+                const double a0 = smc[g + 1], b0 = smc[g];
+                smc[g] = (a0 != a0 || b0 != b0) ? NAN : (a0 < b0 ? a0 : b0);
+            }
+        }
+        __syncthreads();
+        S = Summ{hmax, hmin, pmc, smc};
+    }
     const int j = blockIdx.x * BLOCK + threadIdx.x;
     if (j >= a.n_u) return;
     const double uj = u[j];
@@ -380,8 +593,10 @@ __global__ __launch_bounds__(BLOCK) void equilibrium_kernel(LearnBufs L, const d
         r.status = ((lst & SBR_ARG_INVALID) || !(uj >= 0.0)) ? SBR_ARG_INVALID : (SBR_OOB | lbits);
     } else {
         const bool trunc = gT[n - 1] < T1;
-        if (fits) solve_point(sT, sG, sH, n, ntau, nle, ETA, T1, trunc, uj, a.kappa, a.max_iters, lbits, r, a.aw_path);
-        else solve_point(gT, gG, gH, n, ntau, nle, ETA, T1, trunc, uj, a.kappa, a.max_iters, lbits, r, a.aw_path);
+        if (fits)
+            solve_point(sT, sG, sH, S, n, ntau, nle, ETA, T1, trunc, uj, a.kappa, a.max_iters, lbits, r, a.aw_path);
+        else
+            solve_point(gT, gG, gH, S, n, ntau, nle, ETA, T1, trunc, uj, a.kappa, a.max_iters, lbits, r, a.aw_path);
     }
     const size_t o = (size_t)b * (size_t)a.n_u + j;
     out.xi[o] = r.xi;
@@ -407,7 +622,7 @@ hipError_t launch_learn_logistic(const double* beta, const double* eta, const do
 hipError_t launch_equilibrium(const LearnBufs& L, const double* eta, const double* t_end, const double* u,
                               const EqArgs& a, const ResultSoA& out, int n_beta, hipStream_t s)
 {
-    const size_t lds = (size_t)3 * a.lds_cap * sizeof(double);
+    const size_t lds = ((size_t)3 * a.lds_cap + 4 * ((a.lds_cap >> 6) + 1)) * sizeof(double);
     if (a.n_u >= 1024) {
         dim3 grid((a.n_u + 1023) / 1024, n_beta);
         hipLaunchKernelGGL(equilibrium_kernel<1024>, grid, dim3(1024), lds, s, L, eta, t_end, u, a, out);

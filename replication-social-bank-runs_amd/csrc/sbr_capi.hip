@@ -30,6 +30,7 @@ struct sbr_ctx {
     void* stage = nullptr;
     size_t stage_bytes = 0;
     int lds_cap = 0;
+    int lds_smem = 0;
     // kernel timing (HIP events on the launch stream), opt-in via sbr_timing_enable
     bool timing = false;
     std::vector<hipEvent_t> ev_pool;
@@ -175,7 +176,7 @@ int run_baseline(sbr_ctx* c, hipStream_t s, const double* beta, const double* et
     mark(c, s);
     HIP_TRY(c, sbr::launch_learn_logistic(beta, eta, t_end, la, c->L, s), SBR_EDEVICE);
     mark(c, s);
-    sbr::EqArgs ea{kappa, (int32_t)n_u, o.bisect_max_iters, c->lds_cap, aw_path};
+    sbr::EqArgs ea{kappa, (int32_t)n_u, o.bisect_max_iters, c->lds_cap, aw_path, (o.flags & SBR_FLAG_EXHAUSTIVE) ? 1 : 0};
     HIP_TRY(c, sbr::launch_equilibrium(c->L, eta, t_end, u, ea, out, (int)n_beta, s), SBR_EDEVICE);
     mark(c, s);
     return SBR_OK;
@@ -194,6 +195,8 @@ void sbr_default_opts(sbr_opts* o)
     o->early_exit_nan_run = 5;
     o->knot_capacity = kDefaultCap;
     o->hetero_max_iters = 500;
+    o->flags = 0;
+    o->pad = 0;
 }
 
 int sbr_init(int device, sbr_ctx** out)
@@ -211,8 +214,9 @@ int sbr_init(int device, sbr_ctx** out)
     int smem = 0;
     (void)hipDeviceGetAttribute(&smem, hipDeviceAttributeMaxSharedMemoryPerBlock, device);
     if (smem <= 0) smem = 65536;
-    // 3 doubles per staged knot (t, G, HR); keep 1 KiB slack
-    c->lds_cap = (smem - 1024) / 24;
+    c->lds_smem = smem;
+    // 3 doubles per staged knot (t, G, HR) + 4 block-summary doubles per 64 knots; 1 KiB slack
+    c->lds_cap = (int)(((long)(smem - 1024) * 64) / (8 * (3 * 64 + 4)));
     *out = c;
     return SBR_OK;
 }
@@ -489,6 +493,17 @@ int sbr_sweep_hetero(sbr_ctx* c, int32_t K, const double* betas, const double* d
     if (tau_in) HIP_TRY(c, hipMemcpyAsync(tau_in, dtin, np * K * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
     if (tau_out) HIP_TRY(c, hipMemcpyAsync(tau_out, dtout, np * K * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
     HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
+    return SBR_OK;
+}
+
+int sbr_device_info(sbr_ctx* c, int32_t* lds_bytes_per_block, int32_t* lds_knot_capacity, int32_t* cu_count)
+{
+    if (!c) return SBR_EARG;
+    int cus = 0;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
+    if (lds_bytes_per_block) *lds_bytes_per_block = c->lds_smem;
+    if (lds_knot_capacity) *lds_knot_capacity = c->lds_cap;
+    if (cu_count) *cu_count = cus;
     return SBR_OK;
 }
 

@@ -32,8 +32,9 @@ struct EqArgs {
     double kappa;
     int32_t n_u;
     int32_t max_iters;
-    int32_t lds_cap;    // knots staged in LDS per workgroup (3 doubles each)
+    int32_t lds_cap;    // knots staged in LDS per workgroup (3 doubles each + block summaries)
     double* aw_path;    // optional AW_cum(τ̄) output for single-point mode (n_u == 1)
+    int32_t exhaustive; // 1: linear crossing scan + every AW knot (no block summaries)
 };
 
 struct ResultSoA {

@@ -16,7 +16,7 @@ from .engine import (  # noqa: F401
     solve_equilibrium_baseline,
     solve_learning,
 )
-from .grids import BaselineGrid, fig4_grid, fig5_grid, julia_range  # noqa: F401
+from .grids import BaselineGrid, HeteroGrid, fig4_grid, fig5_grid, hetero_config4, hetero_script_grid, julia_range  # noqa: F401,E501
 from .model import (  # noqa: F401
     EconomicParameters,
     LearningParameters,

@@ -21,6 +21,7 @@ _I32 = ctypes.c_int32
 _P = ctypes.c_void_p
 
 SBR_OK, SBR_EARG, SBR_EDEVICE, SBR_ENOMEM = 0, -1, -2, -3
+SBR_FLAG_EXHAUSTIVE = 0x1
 
 
 class SBRNativeError(RuntimeError):
@@ -40,6 +41,8 @@ class Opts(ctypes.Structure):
         ("early_exit_nan_run", _I32),
         ("knot_capacity", _I32),
         ("hetero_max_iters", _I32),
+        ("flags", _I32),
+        ("pad", _I32),
     ]
 
 
@@ -79,6 +82,10 @@ _SIGS = {
     "sbr_timing_enable": (ctypes.c_int, [_P, ctypes.c_int]),
     "sbr_timing_read": (ctypes.c_int, [_P, _P, _P, _P, _P]),
     "sbr_learn_stats": (ctypes.c_int, [_P, _I64, _P, _P, _P, _P, _P]),
+    "sbr_device_info": (ctypes.c_int, [_P, _P, _P, _P]),
+    "sbr_sweep_hetero": (ctypes.c_int, [_P, _I32, _P, _P, _P, _P, _D, _P, _I64, _I64, _D, _D, _D, _P, _P, _P, _P]),
+    "sbr_sweep_hetero_dev": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P, _P, _D, _P, _I64, _I64, _D, _D, _D, _P, _P, _P,
+                                            _P]),
 }
 
 _lib: ctypes.CDLL | None = None

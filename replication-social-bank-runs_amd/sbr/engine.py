@@ -59,7 +59,7 @@ class Engine:
 
     # ------------------------------------------------------------------ sweeps
     def sweep_baseline(self, grid: BaselineGrid, early_exit: int = 0, max_iters: int = 100,
-                       knot_capacity: int = 8192, with_iters: bool = True) -> dict:
+                       knot_capacity: int = 8192, with_iters: bool = True, exhaustive: bool = False) -> dict:
         """Every (β, u) of ``grid`` through learning → HR → buffers → bisection
         → AW_max.  Returns [n_beta, n_u] arrays (row i = β_i).  ``early_exit=5``
         applies the reference's 5-consecutive-no-run rule as a post-pass."""
@@ -69,7 +69,7 @@ class Engine:
         out["iters"] = np.empty(nb * nu, np.int32) if with_iters else None
         soa = _lib.ResultSoA(*[_ptr(out[k]) for k in (*RESULT_FIELDS, "status", "iters")])
         opts = _lib.default_opts(early_exit_nan_run=early_exit, bisect_max_iters=max_iters,
-                                 knot_capacity=knot_capacity)
+                                 knot_capacity=knot_capacity, flags=_lib.SBR_FLAG_EXHAUSTIVE if exhaustive else 0)
         rc = self._L.sbr_sweep_baseline(self._ctx, _ptr(grid.beta), _ptr(grid.eta), _ptr(grid.t_end), grid.x0,
                                         _ptr(grid.u), nb, nu, grid.p, grid.kappa, grid.lam, ctypes.byref(opts),
                                         ctypes.byref(soa))
@@ -77,14 +77,15 @@ class Engine:
         return {k: (v.reshape(nb, nu) if v is not None else None) for k, v in out.items()}
 
     def sweep_baseline_dev(self, beta, eta, t_end, u, p, kappa, lam, x0, out: dict, stream: int | None = None,
-                           max_iters: int = 100, knot_capacity: int = 8192):
+                           max_iters: int = 100, knot_capacity: int = 8192, exhaustive: bool = False):
         """Device-pointer variant on torch tensors (float64 cuda) — no host sync.
         ``out`` holds preallocated tensors xi/tau_in_unc/tau_out_unc/aw_max/tol
         (float64), status (int32 viewed as uint32) and optional iters (int32)."""
         nb, nu = beta.numel(), u.numel()
         soa = _lib.ResultSoA(*[(out[k].data_ptr() if out.get(k) is not None else None)
                                for k in (*RESULT_FIELDS, "status", "iters")])
-        opts = _lib.default_opts(early_exit_nan_run=0, bisect_max_iters=max_iters, knot_capacity=knot_capacity)
+        opts = _lib.default_opts(early_exit_nan_run=0, bisect_max_iters=max_iters, knot_capacity=knot_capacity,
+                                 flags=_lib.SBR_FLAG_EXHAUSTIVE if exhaustive else 0)
         rc = self._L.sbr_sweep_baseline_dev(self._ctx, stream, beta.data_ptr(), eta.data_ptr(), t_end.data_ptr(),
                                             x0, u.data_ptr(), nb, nu, p, kappa, lam, ctypes.byref(opts),
                                             ctypes.byref(soa))
@@ -119,6 +120,55 @@ class Engine:
         k = int(nt[0])
         return dict(xi=res[0], tau_in_unc=res[1], tau_out_unc=res[2], aw_max=res[3], tol=res[4],
                     status=int(st[0]), tau=tau[:k].copy(), hr=hr[:k].copy(), aw_cum=aw[:k].copy())
+
+    def sweep_hetero(self, betas, dist, eta, t_end, u, p, kappa, lam, x0=1e-4, knot_capacity: int = 8192,
+                     with_groups: bool = True) -> dict:
+        """Heterogeneity sweep: ``betas`` [n_col, K] group rates per column,
+        ``eta``/``t_end`` per column, every u.  Returns [n_col, n_u] arrays and,
+        with ``with_groups``, per-group buffers [n_col, n_u, K]."""
+        betas = np.ascontiguousarray(np.atleast_2d(betas), np.float64)
+        n_col, K = betas.shape
+        dist = np.ascontiguousarray(dist, np.float64)
+        eta = np.ascontiguousarray(np.broadcast_to(eta, (n_col,)), np.float64)
+        t_end = np.ascontiguousarray(np.broadcast_to(t_end, (n_col,)), np.float64)
+        u = np.ascontiguousarray(np.atleast_1d(u), np.float64)
+        nu = len(u)
+        out = {k: np.empty(n_col * nu) for k in ("xi", "aw_max", "tol")}
+        out["status"] = np.empty(n_col * nu, np.uint32)
+        out["iters"] = np.empty(n_col * nu, np.int32)
+        tin = np.empty(n_col * nu * K) if with_groups else None
+        tout = np.empty(n_col * nu * K) if with_groups else None
+        soa = _lib.ResultSoA(_ptr(out["xi"]), None, None, _ptr(out["aw_max"]), _ptr(out["tol"]),
+                             _ptr(out["status"]), _ptr(out["iters"]))
+        opts = _lib.default_opts(knot_capacity=knot_capacity)
+        rc = self._L.sbr_sweep_hetero(self._ctx, K, _ptr(betas), _ptr(dist), _ptr(eta), _ptr(t_end), x0, _ptr(u),
+                                      n_col, nu, p, kappa, lam, ctypes.byref(opts), ctypes.byref(soa), _ptr(tin),
+                                      _ptr(tout))
+        check(rc, self._ctx, "sbr_sweep_hetero")
+        res = {k: v.reshape(n_col, nu) for k, v in out.items()}
+        if with_groups:
+            res["tau_in_unc"] = tin.reshape(n_col, nu, K)
+            res["tau_out_unc"] = tout.reshape(n_col, nu, K)
+        return res
+
+    def sweep_hetero_dev(self, K, betas, dist, eta, t_end, u, p, kappa, lam, x0, out: dict,
+                         stream: int | None = None, knot_capacity: int = 8192):
+        """Device-pointer hetero sweep on torch tensors (no host sync)."""
+        n_col, nu = eta.numel(), u.numel()
+        soa = _lib.ResultSoA(out["xi"].data_ptr(), None, None, out["aw_max"].data_ptr(), out["tol"].data_ptr(),
+                             out["status"].data_ptr(), out["iters"].data_ptr() if out.get("iters") is not None
+                             else None)
+        opts = _lib.default_opts(knot_capacity=knot_capacity)
+        rc = self._L.sbr_sweep_hetero_dev(self._ctx, stream, K, betas.data_ptr(), dist.data_ptr(), eta.data_ptr(),
+                                          t_end.data_ptr(), x0, u.data_ptr(), n_col, nu, p, kappa, lam,
+                                          ctypes.byref(opts), ctypes.byref(soa), None, None)
+        check(rc, self._ctx, "sbr_sweep_hetero_dev")
+
+    def device_info(self) -> dict:
+        a, b, c = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        check(self._L.sbr_device_info(self._ctx, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)), self._ctx,
+              "sbr_device_info")
+        return dict(lds_bytes_per_block=a.value, lds_knot_capacity=b.value, cu_count=c.value)
 
     def timing_enable(self, on: bool = True):
         check(self._L.sbr_timing_enable(self._ctx, int(on)), self._ctx, "sbr_timing_enable")

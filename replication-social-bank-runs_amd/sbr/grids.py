@@ -66,3 +66,64 @@ def fig5_grid(n: int = 500, n_u: int | None = None) -> BaselineGrid:
     beta = 1.0 / amt
     u = julia_range("0.001", "1", n if n_u is None else n_u)
     return BaselineGrid(beta, u, 15.0, 30.0, name=f"fig5_{n}x{n if n_u is None else n_u}")
+
+
+def _jl_sum(xs) -> float:
+    s = 0.0
+    for x in xs:
+        s += x
+    return s
+
+
+class HeteroGrid:
+    """K-group heterogeneity sweep: columns of group rates × u rows.  η is
+    re-derived per column (η_bar / Σ dist·βs, heterogeneity_model.jl:131-132),
+    tspan is carried from the base model (copy-modify, :157-179)."""
+
+    def __init__(self, betas, dist, u, eta_bar=30.0, t_end=None, p=0.9, kappa=0.3, lam=0.1, x0=1e-4, name=""):
+        self.betas = np.ascontiguousarray(np.atleast_2d(betas), np.float64)
+        self.dist = np.ascontiguousarray(dist, np.float64)
+        self.u = np.ascontiguousarray(np.atleast_1d(u), np.float64)
+        self.eta = np.array([eta_bar / _jl_sum(self.dist * b) for b in self.betas])
+        if t_end is None:
+            t_end = 2 * self.eta
+        self.t_end = np.ascontiguousarray(np.broadcast_to(t_end, self.eta.shape), np.float64)
+        self.p, self.kappa, self.lam, self.x0 = float(p), float(kappa), float(lam), float(x0)
+        self.name = name
+
+    @property
+    def K(self):
+        return self.betas.shape[1]
+
+    @property
+    def shape(self):
+        return (self.betas.shape[0], len(self.u))
+
+    @property
+    def n_points(self):
+        return self.shape[0] * self.shape[1]
+
+    def subset(self, idx) -> "HeteroGrid":
+        g = HeteroGrid.__new__(HeteroGrid)
+        g.__dict__.update(self.__dict__)
+        g.betas, g.eta, g.t_end = self.betas[idx], self.eta[idx], self.t_end[idx]
+        return g
+
+
+def hetero_script_grid() -> HeteroGrid:
+    """scripts/2_heterogeneity.jl:38-49: βs = [0.125, 12.5], dist = [0.9, 0.1], η_bar = 30,
+    u = 0.1, p = 0.9, κ = 0.3, λ = 0.1 (tspan = (0, 2η))."""
+    return HeteroGrid([[0.125, 12.5]], [0.9, 0.1], [0.1], name="hetero_script")
+
+
+def hetero_config4(n_s: int = 1024, n_u: int = 1024, K: int = 8) -> HeteroGrid:
+    """BASELINE config 4 (concretised in SURVEY.md §8(d)): βs_k = s·0.125·100^((k−1)/(K−1))
+    spanning Fig 9's 0.125…12.5 at s = 1, dist_k = 1/K, s = 1 ./ range(1e-3, 1, n_s),
+    u = range(0.001, 1, n_u), η_bar = 30, p = 0.9, κ = 0.3, λ = 0.1; η re-derived per
+    column, tspan carried from s = 1."""
+    base = np.array([0.125 * 100.0 ** (k / (K - 1)) for k in range(K)]) if K > 1 else np.array([0.125])
+    dist = np.full(K, 1.0 / K)
+    s = 1.0 / julia_range("0.001", "1", n_s)
+    betas = s[:, None] * base[None, :]
+    t_end = 2 * 30.0 / _jl_sum(dist * base)
+    return HeteroGrid(betas, dist, julia_range("0.001", "1", n_u), 30.0, t_end, name=f"hetero_K{K}_{n_s}x{n_u}")

@@ -153,3 +153,21 @@ def test_fig5_5000_run_mask(engine, golden):
     got = np.array([np.argmin(r) if not r.all() else len(r) for r in run])
     assert np.array_equal(got, pref), f"{int((got != pref).sum())} columns differ"
     assert run.sum() == 8736564
+
+
+def test_blocked_scan_and_pruned_aw_equal_exhaustive(engine):
+    """Block-summary crossing scan + branch-and-bound AW_max give exactly the
+    exhaustive per-knot results (a different search, the same arithmetic)."""
+    for grid in (sbr.fig5_grid(512), sbr.fig4_grid(5000), sbr.BaselineGrid([0.5, 1.0, 3.0, 61.654026637430945], sbr.julia_range("0.0", "2.0", 777), 15.0, 30.0, p=1.0)):
+        a = engine.sweep_baseline(grid)
+        b = engine.sweep_baseline(grid, exhaustive=True)
+        for f in FIELDS:
+            assert_bitwise(a[f], b[f], f)
+        assert np.array_equal(a["status"], b["status"])
+        assert np.array_equal(a["iters"], b["iters"])
+
+
+def test_device_info(engine):
+    info = engine.device_info()
+    assert info["cu_count"] == 256
+    assert info["lds_knot_capacity"] >= 3400  # every config-3 column staged in LDS

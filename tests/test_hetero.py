@@ -1,0 +1,73 @@
+"""Heterogeneity extension (src/extensions/heterogeneity/): oracle pinned to
+the committed figure, GPU kernels bit-identical to the oracle."""
+import numpy as np
+import pytest
+
+import sbr
+from golden_util import interp
+
+
+def _hetero_oracle(oracle, g):
+    return oracle.sweep_hetero(g.betas, g.dist, g.eta, g.t_end, g.u, g.p, g.kappa, g.lam, g.x0)
+
+
+def test_hetero_script_figure(oracle, golden):
+    """scripts/2_heterogeneity.jl: ξ (vline; the x tick step must be one of GR's
+    nice steps and exactly one matches), AW_max and the AW curves on
+    range(0, 2ξ, 1000) (aggregate_withdrawals_hetero.pdf)."""
+    gold = golden("hetero.json")
+    g = sbr.hetero_script_grid()
+    r = _hetero_oracle(oracle, g)
+    assert r["status"][0, 0] & sbr.STATUS["SBR_RUN"]
+    xi = r["xi"][0, 0]
+    span = gold["x_last"] - gold["x_first"]
+    cands = [step / gold["tick_spacing_px"] * span / 2 for step in (1, 2, 2.5, 5, 10)]
+    prec = 0.02 / span * 2 * max(cands)
+    hits = [c for c in cands if abs(c - xi) <= prec]
+    assert len(hits) == 1, (xi, cands)
+    # AW_total(t) on t = range(0, 2ξ, 1000): rebuild the path on the learning grid
+    t, G, _ = oracle.learn_hetero(g.betas[0], g.dist, g.t_end[0])
+    tin, tout = r["tau_in_unc"][0, 0], r["tau_out_unc"][0, 0]
+    ts = np.linspace(0.0, 2 * xi, 1000)
+    cum = np.zeros(len(t))
+    groups = []
+    for k in range(g.K):
+        ic, oc = min(tin[k], xi), min(tout[k], xi)
+        a, b = (t - xi) + ic, (t - xi) + oc
+        awin = np.where(a >= 0, interp(t, G[:, k], np.where(a > 0, a, 0.0)), 0.0)
+        awout = np.where(b >= 0, interp(t, G[:, k], np.where(b > 0, b, 0.0)), 0.0)
+        cum = cum + g.dist[k] * (awout - awin)
+        groups.append(awout - awin)
+    assert abs(r["aw_max"][0, 0] - np.max(cum)) < 1e-15
+    tol = 2 * gold["aw_precision"] + 3e-4  # plus the ξ uncertainty of the x map
+    assert np.max(np.abs(interp(t, cum, ts) - np.array(gold["aw_total"]))) < tol
+    assert np.max(np.abs(interp(t, groups[0], ts) - np.array(gold["aw_group1"]))) < tol
+    assert np.max(np.abs(interp(t, groups[1], ts) - np.array(gold["aw_group2"]))) < tol
+
+
+def test_hetero_k1_reduces_to_baseline_semantics(oracle):
+    """K = 1, dist = [1]: the coupled ODE is the logistic (ω = G); the hetero
+    solver differs from the baseline only where the reference code differs
+    (bracket [0, 2τ̄_OUT], tol 1e-12, explicit-grid η, AW on the full grid)."""
+    g = sbr.HeteroGrid([[1.0]], [1.0], sbr.julia_range("0.001", "0.2", 40), eta_bar=15.0, t_end=30.0, p=0.5,
+                       kappa=0.6, lam=0.01)
+    r = _hetero_oracle(oracle, g)
+    base = oracle.sweep_baseline([1.0], 15.0, 30.0, g.u, 0.5, 0.6, 0.01)
+    run_h = (r["status"] & 1) > 0
+    run_b = (base["status"] & 1) > 0
+    assert np.array_equal(run_h, run_b)
+    assert np.nanmax(np.abs(r["xi"] - base["xi"])) < 1e-9
+
+
+@pytest.mark.gpu
+def test_hetero_gpu_bitwise_script_and_grid(engine, oracle):
+    for g in (sbr.hetero_script_grid(), sbr.hetero_config4(24, 48, 8), sbr.hetero_config4(10, 30, 4),
+              sbr.hetero_config4(8, 20, 2)):
+        gg = engine.sweep_hetero(g.betas, g.dist, g.eta, g.t_end, g.u, g.p, g.kappa, g.lam, g.x0)
+        o = _hetero_oracle(oracle, g)
+        for f in ("xi", "aw_max", "tol", "tau_in_unc", "tau_out_unc"):
+            a, b = gg[f], o[f]
+            same = (a == b) | (np.isnan(a) & np.isnan(b))
+            assert same.all(), (g.name, f, int((~same).sum()))
+        assert np.array_equal(gg["status"], o["status"]), g.name
+        assert np.array_equal(gg["iters"], o["iters"]), g.name
