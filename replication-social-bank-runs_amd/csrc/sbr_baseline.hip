@@ -35,18 +35,15 @@ __global__ __launch_bounds__(64) void learn_logistic_kernel(const double* __rest
     const size_t row = (size_t)b * (size_t)L.cap;
     double* __restrict__ T = L.t + row;
     double* __restrict__ Gv = L.G + row;
-    double* __restrict__ H = L.hr + row;
-    double* __restrict__ HI = L.hrI + row;
     uint32_t st = 0;
-    int n = 0, m = 0;
-    bool pushed = false;
+    int n = 0;
 
     if (!(BETA > 0.0) || !(T1 > T0) || !(ETA > 0.0)) { // LearningParameters / EconomicParameters checks
         L.status[b] = SBR_ARG_INVALID;
         L.n_knots[b] = 0; L.n_tau[b] = 0; L.n_le[b] = 0; L.n_accept[b] = 0; L.n_reject[b] = 0;
         return;
     }
-    const double x0 = a.x0, rtol = a.rtol, atol = a.atol, p = a.p, lam = a.lam;
+    const double x0 = a.x0, rtol = a.rtol, atol = a.atol;
     const double dtmax = T1 - T0;
     const double dtmin = sbr_jl_eps(dmax(fabs(T0), fabs(T1)));
 
@@ -73,42 +70,15 @@ __global__ __launch_bounds__(64) void learn_logistic_kernel(const double* __rest
         }
     }
 
-    // ---- knot sink: store (t, G) and stream the hazard terms ----
-    double tprev = 0.0, gprev = 0.0, eprev = 0.0, I = 0.0, tlast = 0.0, bound = -INFINITY;
+    // ---- knot sink: store (t, G); the hazard stage runs afterwards in parallel ----
+    double tlast = 0.0, bound = -INFINITY;
     bool past = false, done = false;
     int jstar = -1;
     auto push = [&](double t, double x) {
         if (n >= L.cap) { st |= SBR_KNOT_OVERFLOW; done = true; return; }
         T[n] = t;
         Gv[n] = x;
-        const double g = (BETA * x) * (1.0 - x); // compute_pdf_symbolic_baseline
-        if (!past) {
-            if (t <= ETA) {
-                const double E = sbr_exp(lam * t);
-                const double e = E * g;
-                I = (m == 0) ? 0.0 : I + (0.5 * (eprev + e)) * (t - tprev);
-                H[m] = (p * E) * g;
-                HI[m] = I;
-                m++;
-                eprev = e; tprev = t; gprev = g;
-            } else {
-                past = true;
-                jstar = n;
-                if (m == 0) {
-                    st |= SBR_OOB; // pdf(η) with η < t0: BoundsError
-                } else if (tprev != ETA) { // append η (solver.jl:159-160), pdf(η) on bracket [n-1, n]
-                    const double d = (ETA - tprev) / (t - tprev);
-                    const double pe = gprev * (1.0 - d) + g * d;
-                    const double E = sbr_exp(lam * ETA);
-                    const double e = E * pe;
-                    I = I + (0.5 * (eprev + e)) * (ETA - tprev);
-                    H[m] = (p * E) * pe;
-                    HI[m] = I;
-                    m++;
-                    pushed = true;
-                }
-            }
-        }
+        if (!past && t > ETA) { past = true; jstar = n; }
         // furthest point any lookup of the equilibrium stage can reach
         if (n >= 1 && (jstar < 0 || n <= jstar)) bound = dmax(bound, t + (t - tlast));
         tlast = t;
@@ -116,7 +86,8 @@ __global__ __launch_bounds__(64) void learn_logistic_kernel(const double* __rest
         if (a.stop_after_eta && past && t >= bound) done = true;
     };
 
-    double t = T0, x = x0, qold = CTL_QOLDMIN, q11 = 1.0;
+    const double LOG_QOLDMIN = sbr_log(CTL_QOLDMIN);
+    double t = T0, x = x0, qold = CTL_QOLDMIN, q11 = 1.0, lqold = LOG_QOLDMIN;
     AutoSwitch as;
     int naccept = 0, nreject = 0;
     push(t, x);
@@ -146,11 +117,22 @@ __global__ __launch_bounds__(64) void learn_logistic_kernel(const double* __rest
         const double ut =
             dt * fma(BT1, k1, fma(BT2, k2, fma(BT3, k3, fma(BT4, k4, fma(BT5, k5, fma(BT6, k6, BT7 * k7))))));
         const double EEst = fabs(ut / fma(dmax(fabs(x), fabs(u)), rtol, atol));
-        const double q = pi_q(EEst, qold, q11);
+        // stepsize_controller!(PIController) with log(qold) carried over from the
+        // step that set qold: same operations as pi_q (sbr_pow_pos = exp(y·log x)).
+        double q, le = 0.0;
+        if (EEst == 0.0) {
+            q = CTL_INV_QMAX;
+        } else {
+            le = sbr_log(EEst);
+            q11 = sbr_exp(CTL_BETA1 * le);
+            q = q11 / sbr_exp(CTL_BETA2 * lqold);
+            q = dmax(CTL_INV_QMAX, dmin(CTL_INV_QMIN, q / CTL_GAMMA));
+        }
         if (EEst <= 1.0) {
             naccept++;
             const double dtnew = dt / q;
             qold = dmax(EEst, CTL_QOLDMIN);
+            lqold = (qold == EEst) ? le : LOG_QOLDMIN;
             double tn = t + dt;
             if (fabs(tn - T1) < 100.0 * sbr_jl_eps(dmax(t, T1))) tn = T1;
             t = tn;
@@ -166,21 +148,98 @@ __global__ __launch_bounds__(64) void learn_logistic_kernel(const double* __rest
         as.update(eig, dt);
     }
     if (as.switched) st |= SBR_STIFF_SWITCH;
-    if (!past && !(st & SBR_KNOT_OVERFLOW)) {
-        // integration ended at t_end without a knot beyond η
-        if (m == 0 || tprev != ETA) st |= SBR_OOB; // pdf(η) beyond the last knot
-    }
-    // ---- HR second pass (solver.jl:180-182) ----
-    if (m > 0 && !(st & SBR_OOB)) {
-        const double Ieta = HI[m - 1], omp = 1.0 - p;
-        for (int i = 0; i < m; i++) H[i] = H[i] / ((p * HI[i]) + (omp * Ieta));
-    }
     L.n_knots[b] = n;
-    L.n_tau[b] = m;
-    L.n_le[b] = pushed ? m - 1 : m;
     L.status[b] = st;
     L.n_accept[b] = naccept;
     L.n_reject[b] = nreject;
+}
+
+// ============================================================================
+// Hazard kernel — hazard_rate (solver.jl:153-185) for one β column per
+// workgroup: τ̄ = knots ≤ η (+ η), pdf g = βG(1−G) (learning.jl:170), then
+// e = exp(λτ̄)·g, the cumulative trapezoid (sequential, in the reference's
+// order) and HR = (p·exp(λτ̄))·g / (p·I + (1−p)·I_η).
+// ============================================================================
+constexpr int HZ_BLOCK = 256;
+
+__global__ __launch_bounds__(HZ_BLOCK) void hazard_kernel(const double* __restrict__ beta,
+                                                          const double* __restrict__ eta, LearnArgs a, LearnBufs L)
+{
+    extern __shared__ double term[]; // trapezoid terms, then I
+    __shared__ int s_m;
+    const int b = blockIdx.x;
+    const int n = L.n_knots[b];
+    const uint32_t st = L.status[b];
+    if (st & SBR_ARG_INVALID) return; // learn kernel already wrote the row
+    const size_t row = (size_t)b * (size_t)L.cap;
+    const double* __restrict__ T = L.t + row;
+    const double* __restrict__ Gv = L.G + row;
+    double* __restrict__ H = L.hr + row;
+    const double BETA = beta[b], ETA = eta[b], p = a.p, lam = a.lam;
+    if (threadIdx.x == 0) { // m = #knots ≤ η (sorted: searchsortedlast + 1)
+        int lo = 0, hi = n;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (T[mid] <= ETA) lo = mid + 1;
+            else hi = mid;
+        }
+        s_m = lo;
+    }
+    __syncthreads();
+    const int m = s_m;
+    bool oob = false, push;
+    if (m < n) {
+        push = (m == 0) || T[m - 1] != ETA; // solver.jl:159
+        oob = (m == 0);                       // pdf(η) with η < t_0
+    } else {
+        push = (m == 0) || T[m - 1] != ETA;
+        oob = push;                           // no knot beyond η to interpolate pdf(η)
+    }
+    const int ntau = m + (push ? 1 : 0);
+    if (oob || ntau > a.hz_cap) {
+        if (threadIdx.x == 0) {
+            L.status[b] = st | (oob ? SBR_OOB : SBR_KNOT_OVERFLOW);
+            L.n_tau[b] = 0;
+            L.n_le[b] = 0;
+        }
+        return;
+    }
+    // e_i and the numerator (p·E_i)·pdf_i; the trapezoid term of i pairs e_{i-1}, e_i
+    auto pdf_at = [&](int i) -> double {
+        if (i < m) { const double x = Gv[i]; return (BETA * x) * (1.0 - x); }
+        // η on bracket [m-1, m]
+        const double g0 = (BETA * Gv[m - 1]) * (1.0 - Gv[m - 1]);
+        const double g1 = (BETA * Gv[m]) * (1.0 - Gv[m]);
+        const double d = (ETA - T[m - 1]) / (T[m] - T[m - 1]);
+        return g0 * (1.0 - d) + g1 * d;
+    };
+    auto tau_at = [&](int i) -> double { return i < m ? T[i] : ETA; };
+    for (int i = threadIdx.x; i < ntau; i += HZ_BLOCK) {
+        const double ti = tau_at(i);
+        const double E = sbr_exp(lam * ti);
+        const double g = pdf_at(i);
+        H[i] = (p * E) * g;
+        if (i > 0) {
+            const double tp = tau_at(i - 1);
+            const double ep = sbr_exp(lam * tp) * pdf_at(i - 1);
+            term[i] = (0.5 * (ep + E * g)) * (ti - tp);
+        } else {
+            term[0] = 0.0;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) { // I_i = I_{i-1} + term_i, left to right (solver.jl:173-175)
+        double I = 0.0;
+        for (int i = 1; i < ntau; i++) {
+            I = I + term[i];
+            term[i] = I;
+        }
+        L.n_tau[b] = ntau;
+        L.n_le[b] = m;
+    }
+    __syncthreads();
+    const double Ieta = term[ntau - 1], omp = 1.0 - p;
+    for (int i = threadIdx.x; i < ntau; i += HZ_BLOCK) H[i] = H[i] / ((p * term[i]) + (omp * Ieta));
 }
 
 // ============================================================================
@@ -616,6 +675,10 @@ hipError_t launch_learn_logistic(const double* beta, const double* eta, const do
 {
     dim3 grid((a.n_beta + 63) / 64);
     hipLaunchKernelGGL(learn_logistic_kernel, grid, dim3(64), 0, s, beta, eta, t_end, a, L);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(hazard_kernel, dim3(a.n_beta), dim3(HZ_BLOCK), (size_t)a.hz_cap * sizeof(double), s, beta,
+                       eta, a, L);
     return hipGetLastError();
 }
 

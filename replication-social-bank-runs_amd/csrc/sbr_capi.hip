@@ -149,6 +149,14 @@ sbr_opts resolve(const sbr_opts* o)
     return r;
 }
 
+// τ̄ entries the hazard kernel keeps in LDS (≤ knot capacity, ≤ the LDS per workgroup)
+int32_t hz_cap(const sbr_ctx* c, const sbr_opts& o)
+{
+    const int lds = c->lds_smem > 0 ? c->lds_smem : 65536;
+    const int cap = (lds - 1024) / 8;
+    return o.knot_capacity + 1 < cap ? o.knot_capacity + 1 : cap;
+}
+
 hipEvent_t next_event(sbr_ctx* c)
 {
     if (c->ev_used == c->ev_pool.size()) {
@@ -172,7 +180,7 @@ int run_baseline(sbr_ctx* c, hipStream_t s, const double* beta, const double* et
 {
     int rc = ensure_learn(c, (size_t)n_beta, (size_t)o.knot_capacity);
     if (rc) return rc;
-    sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, p, lambda, o.ode_maxiters, (int32_t)n_beta, 1};
+    sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, p, lambda, o.ode_maxiters, (int32_t)n_beta, 1, hz_cap(c, o), 0};
     mark(c, s);
     HIP_TRY(c, sbr::launch_learn_logistic(beta, eta, t_end, la, c->L, s), SBR_EDEVICE);
     mark(c, s);
@@ -315,7 +323,7 @@ int sbr_learn_baseline(sbr_ctx* c, const double* beta, const double* eta, const 
     HIP_TRY(c, hipMemcpyAsync(dbeta, beta, n_beta * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
     HIP_TRY(c, hipMemcpyAsync(deta, eta, n_beta * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
     HIP_TRY(c, hipMemcpyAsync(dtend, t_end, n_beta * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
-    sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, 0.5, 1.0, o.ode_maxiters, (int32_t)n_beta, stop_after_eta};
+    sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, 0.5, 1.0, o.ode_maxiters, (int32_t)n_beta, stop_after_eta, hz_cap(c, o), 0};
     HIP_TRY(c, sbr::launch_learn_logistic(dbeta, deta, dtend, la, c->L, s), SBR_EDEVICE);
     const size_t w = (size_t)o.knot_capacity;
     if (t_out)
@@ -429,7 +437,7 @@ int sbr_sweep_hetero_dev(sbr_ctx* c, void* stream, int32_t K, const double* beta
     int rc = ensure_hetero(c, (size_t)n_col, (size_t)o.knot_capacity, (size_t)K);
     if (rc) return rc;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-    sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, p, lambda, o.ode_maxiters, (int32_t)n_col, 0};
+    sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, p, lambda, o.ode_maxiters, (int32_t)n_col, 0, 0, 0};
     sbr::HeteroEqArgs ea{kappa, 1e-12, (int32_t)n_u, o.hetero_max_iters, c->lds_cap * 3};
     sbr::ResultSoA r{out->xi, nullptr, nullptr, out->aw_max, out->tol, out->status, out->iters};
     mark(c, s);

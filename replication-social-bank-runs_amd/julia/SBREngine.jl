@@ -1,0 +1,119 @@
+#=
+SBREngine.jl — Julia binding of libsbr (include/sbr.h) for the reference's scripts.
+
+Drop-in for the β×u loops of scripts/1_baseline.jl (Fig 4 :151-192, Fig 5 :224-267) and the
+heterogeneity sweep: one `ccall` per grid instead of one solve_learning /
+solve_equilibrium_baseline / get_AW_functions! per point.  Plain-pointer C ABI; Julia owns every
+array (`GC.@preserve`), the library owns device memory.
+
+NOT EXECUTED IN THIS REPOSITORY: the build image has no Julia.  The Python binding
+(replication-social-bank-runs_amd/sbr/_lib.py) calls the same symbols with the same layouts and
+is what the tests exercise.
+=#
+module SBREngine
+
+const libsbr = joinpath(@__DIR__, "..", "lib", "libsbr.so")
+
+# sbr_status.h
+const SBR_RUN = UInt32(0x0001)
+const SBR_CONVERGED = UInt32(0x0002)
+const SBR_SKIPPED_EARLY_EXIT = UInt32(0x0100)
+
+struct Opts            # sbr_opts
+    ode_reltol::Float64
+    ode_abstol::Float64
+    ode_maxiters::Int64
+    bisect_max_iters::Int32
+    early_exit_nan_run::Int32
+    knot_capacity::Int32
+    hetero_max_iters::Int32
+    flags::Int32
+    pad::Int32
+end
+Opts(; early_exit = 5) = Opts(eps(), eps(), 100_000, 100, early_exit, 8192, 500, 0, 0)
+
+struct ResultSoA       # sbr_result_soa
+    xi::Ptr{Float64}
+    tau_in_unc::Ptr{Float64}
+    tau_out_unc::Ptr{Float64}
+    aw_max::Ptr{Float64}
+    tol::Ptr{Float64}
+    status::Ptr{UInt32}
+    iters::Ptr{Int32}
+end
+
+mutable struct Context
+    ptr::Ptr{Cvoid}
+    function Context(device::Integer = 0)
+        r = Ref{Ptr{Cvoid}}(C_NULL)
+        rc = ccall((:sbr_init, libsbr), Cint, (Cint, Ptr{Ptr{Cvoid}}), device, r)
+        rc == 0 || error("sbr_init failed ($rc): no usable MI355X")
+        ctx = new(r[])
+        finalizer(c -> ccall((:sbr_free, libsbr), Cint, (Ptr{Cvoid},), c.ptr), ctx)
+        return ctx
+    end
+end
+
+function check(ctx::Context, rc)
+    rc == 0 && return
+    msg = unsafe_string(ccall((:sbr_last_error, libsbr), Cstring, (Ptr{Cvoid},), ctx.ptr))
+    rc == -1 ? throw(ArgumentError(msg)) : error("libsbr: $msg ($rc)")
+end
+
+"""
+    solve_equilibrium_grid(ctx, β_vals, u_vals; η, tspan_end, x0, p, κ, λ, early_exit=5)
+
+Batched `solve_learning` + `solve_equilibrium_baseline` + `get_AW_functions!` for every
+(β, u).  `η`/`tspan_end` are per-β (scalars broadcast): the copy-modify constructor of
+model.jl:189-211 carries η = 15, tspan = (0, 30) for every β of Fig 5.  Returns
+`(max_AW_matrix, ξ, τ̄_IN, τ̄_OUT, status)` as [u, β] matrices — `max_AW_matrix` is the
+matrix of scripts/1_baseline.jl:213 (NaN = no run or skipped by the 5-NaN rule).
+"""
+function solve_equilibrium_grid(ctx::Context, β_vals, u_vals; η = 15.0, tspan_end = 30.0, x0 = 1e-4,
+                                p = 0.5, κ = 0.6, λ = 0.01, early_exit = 5)
+    β = collect(Float64, β_vals); u = collect(Float64, u_vals)
+    nb, nu = length(β), length(u)
+    ηv = fill(Float64(η), nb) .+ 0 .* β
+    tv = fill(Float64(tspan_end), nb)
+    # u-fastest layout [u, β] == Julia's column-major max_AW_matrix[j, i]
+    xi = Matrix{Float64}(undef, nu, nb); tin = similar(xi); tout = similar(xi)
+    aw = similar(xi); tol = similar(xi); st = Matrix{UInt32}(undef, nu, nb)
+    opts = Ref(Opts(; early_exit))
+    GC.@preserve β u ηv tv xi tin tout aw tol st begin
+        soa = Ref(ResultSoA(pointer(xi), pointer(tin), pointer(tout), pointer(aw), pointer(tol), pointer(st),
+                            Ptr{Int32}(C_NULL)))
+        rc = ccall((:sbr_sweep_baseline, libsbr), Cint,
+                   (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Float64, Ptr{Float64}, Int64, Int64,
+                    Float64, Float64, Float64, Ref{Opts}, Ref{ResultSoA}),
+                   ctx.ptr, β, ηv, tv, x0, u, nb, nu, p, κ, λ, opts, soa)
+        check(ctx, rc)
+    end
+    return (max_AW_matrix = aw, ξ = xi, τ_bar_IN_UNC = tin, τ_bar_OUT_UNC = tout, status = st)
+end
+
+"""
+    solve_equilibrium_hetero_grid(ctx, βs_cols, dist, u_vals; η, tspan_end, x0, p, κ, λ)
+
+`βs_cols` is K × n_col (column c = the group rates of one parameter column); η per column.
+"""
+function solve_equilibrium_hetero_grid(ctx::Context, βs_cols::AbstractMatrix, dist, u_vals; η, tspan_end,
+                                       x0 = 1e-4, p = 0.9, κ = 0.3, λ = 0.1)
+    B = Matrix{Float64}(βs_cols); K, nc = size(B)
+    d = collect(Float64, dist); u = collect(Float64, u_vals); nu = length(u)
+    ηv = collect(Float64, η); tv = fill(Float64(tspan_end), nc) .+ 0 .* ηv
+    xi = Matrix{Float64}(undef, nu, nc); aw = similar(xi); tol = similar(xi); st = Matrix{UInt32}(undef, nu, nc)
+    tin = Array{Float64}(undef, K, nu, nc); tout = similar(tin)
+    opts = Ref(Opts(; early_exit = 0))
+    GC.@preserve B d u ηv tv xi aw tol st tin tout begin
+        soa = Ref(ResultSoA(pointer(xi), C_NULL, C_NULL, pointer(aw), pointer(tol), pointer(st), C_NULL))
+        rc = ccall((:sbr_sweep_hetero, libsbr), Cint,
+                   (Ptr{Cvoid}, Int32, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Float64,
+                    Ptr{Float64}, Int64, Int64, Float64, Float64, Float64, Ref{Opts}, Ref{ResultSoA},
+                    Ptr{Float64}, Ptr{Float64}),
+                   ctx.ptr, K, B, d, ηv, tv, x0, u, nc, nu, p, κ, λ, opts, soa, tin, tout)
+        check(ctx, rc)
+    end
+    return (AW_max = aw, ξ = xi, τ_bar_IN_UNCs = tin, τ_bar_OUT_UNCs = tout, status = st)
+end
+
+end # module
