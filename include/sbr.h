@@ -46,7 +46,7 @@ typedef struct {
     int64_t ode_maxiters;       /* DiffEq default maxiters = 1e5 */
     int32_t bisect_max_iters;   /* solver.jl:309 max_iters = 100 */
     int32_t early_exit_nan_run; /* 1_baseline.jl:147,221: 5; 0 disables */
-    int32_t knot_capacity;      /* engine limit on stored knots per β (0 = default 8192) */
+    int32_t knot_capacity;      /* engine limit on stored knots per β (0 = default 65536) */
     int32_t hetero_max_iters;   /* heterogeneity_solver.jl:49 max_iters = 500 */
     int32_t flags;              /* SBR_FLAG_* */
     int32_t pad;
@@ -66,7 +66,7 @@ typedef struct {
     int32_t* iters;      /* bisection iterations (may be NULL)  */
 } sbr_result_soa;
 
-/* Fills *o with the reference defaults (eps() tolerances, 1e5, 100, 5, 8192). */
+/* Fills *o with the reference defaults (eps() tolerances, 1e5, 100, 5, 65536, 500). */
 void sbr_default_opts(sbr_opts* o);
 
 /* Creates a context on HIP device `device` (the caller's rank-local GPU). */

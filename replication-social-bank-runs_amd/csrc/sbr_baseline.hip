@@ -165,7 +165,7 @@ constexpr int HZ_BLOCK = 256;
 __global__ __launch_bounds__(HZ_BLOCK) void hazard_kernel(const double* __restrict__ beta,
                                                           const double* __restrict__ eta, LearnArgs a, LearnBufs L)
 {
-    extern __shared__ double term[]; // trapezoid terms, then I
+    extern __shared__ double lterm[]; // trapezoid terms, then I (HBM scratch beyond hz_cap)
     __shared__ int s_m;
     const int b = blockIdx.x;
     const int n = L.n_knots[b];
@@ -196,9 +196,10 @@ __global__ __launch_bounds__(HZ_BLOCK) void hazard_kernel(const double* __restri
         oob = push;                           // no knot beyond η to interpolate pdf(η)
     }
     const int ntau = m + (push ? 1 : 0);
-    if (oob || ntau > a.hz_cap) {
+    double* term = ntau <= a.hz_cap ? lterm : L.hrI + row;
+    if (oob) {
         if (threadIdx.x == 0) {
-            L.status[b] = st | (oob ? SBR_OOB : SBR_KNOT_OVERFLOW);
+            L.status[b] = st | SBR_OOB;
             L.n_tau[b] = 0;
             L.n_le[b] = 0;
         }

@@ -39,7 +39,7 @@ struct sbr_ctx {
 
 namespace {
 
-constexpr int kDefaultCap = 8192;
+constexpr int kDefaultCap = 65536; // the longest Fig 5 tail (β ≈ 2000) needs 20k knots below η
 
 int fail(sbr_ctx* c, int code, const char* what, hipError_t e = hipSuccess)
 {

@@ -59,7 +59,7 @@ class Engine:
 
     # ------------------------------------------------------------------ sweeps
     def sweep_baseline(self, grid: BaselineGrid, early_exit: int = 0, max_iters: int = 100,
-                       knot_capacity: int = 8192, with_iters: bool = True, exhaustive: bool = False) -> dict:
+                       knot_capacity: int = 65536, with_iters: bool = True, exhaustive: bool = False) -> dict:
         """Every (β, u) of ``grid`` through learning → HR → buffers → bisection
         → AW_max.  Returns [n_beta, n_u] arrays (row i = β_i).  ``early_exit=5``
         applies the reference's 5-consecutive-no-run rule as a post-pass."""
@@ -77,7 +77,7 @@ class Engine:
         return {k: (v.reshape(nb, nu) if v is not None else None) for k, v in out.items()}
 
     def sweep_baseline_dev(self, beta, eta, t_end, u, p, kappa, lam, x0, out: dict, stream: int | None = None,
-                           max_iters: int = 100, knot_capacity: int = 8192, exhaustive: bool = False):
+                           max_iters: int = 100, knot_capacity: int = 65536, exhaustive: bool = False):
         """Device-pointer variant on torch tensors (float64 cuda) — no host sync.
         ``out`` holds preallocated tensors xi/tau_in_unc/tau_out_unc/aw_max/tol
         (float64), status (int32 viewed as uint32) and optional iters (int32)."""
@@ -91,7 +91,7 @@ class Engine:
                                             ctypes.byref(soa))
         check(rc, self._ctx, "sbr_sweep_baseline_dev")
 
-    def learn_baseline(self, beta, eta, t_end, x0=1e-4, stop_after_eta=False, cap=8192):
+    def learn_baseline(self, beta, eta, t_end, x0=1e-4, stop_after_eta=False, cap=65536):
         beta = np.ascontiguousarray(beta, np.float64)
         nb = len(beta)
         eta = np.ascontiguousarray(np.broadcast_to(eta, beta.shape), np.float64)
@@ -106,7 +106,7 @@ class Engine:
         check(rc, self._ctx, "sbr_learn_baseline")
         return [(T[i, : nk[i]].copy(), G[i, : nk[i]].copy(), int(st[i])) for i in range(nb)]
 
-    def solve_point_paths(self, beta, eta, t_end, u, p, kappa, lam, x0=1e-4, cap=8192):
+    def solve_point_paths(self, beta, eta, t_end, u, p, kappa, lam, x0=1e-4, cap=65536):
         res = np.zeros(5)
         st = np.zeros(1, np.uint32)
         tau = np.zeros(cap)
@@ -121,7 +121,7 @@ class Engine:
         return dict(xi=res[0], tau_in_unc=res[1], tau_out_unc=res[2], aw_max=res[3], tol=res[4],
                     status=int(st[0]), tau=tau[:k].copy(), hr=hr[:k].copy(), aw_cum=aw[:k].copy())
 
-    def sweep_hetero(self, betas, dist, eta, t_end, u, p, kappa, lam, x0=1e-4, knot_capacity: int = 8192,
+    def sweep_hetero(self, betas, dist, eta, t_end, u, p, kappa, lam, x0=1e-4, knot_capacity: int = 16384,
                      with_groups: bool = True) -> dict:
         """Heterogeneity sweep: ``betas`` [n_col, K] group rates per column,
         ``eta``/``t_end`` per column, every u.  Returns [n_col, n_u] arrays and,
@@ -152,7 +152,7 @@ class Engine:
         return res
 
     def sweep_hetero_dev(self, K, betas, dist, eta, t_end, u, p, kappa, lam, x0, out: dict,
-                         stream: int | None = None, knot_capacity: int = 8192):
+                         stream: int | None = None, knot_capacity: int = 16384):
         """Device-pointer hetero sweep on torch tensors (no host sync)."""
         n_col, nu = eta.numel(), u.numel()
         soa = _lib.ResultSoA(out["xi"].data_ptr(), None, None, out["aw_max"].data_ptr(), out["tol"].data_ptr(),
