@@ -233,7 +233,9 @@ static int tsit5_solve(rhs_fn f, void* ctx, int m, double t0, double t1, const d
     }
 
     /* ---- main loop (solve! / loopheader! / loopfooter!) ---- */
-    double t = t0, qold = CTL_QOLDMIN, q11 = 1.0;
+    const double LOG_QOLDMIN = sbr_log(CTL_QOLDMIN);
+    const double snap = 100.0 * sbr_jl_eps(t1);
+    double t = t0, qold = CTL_QOLDMIN, lqold = LOG_QOLDMIN;
     autoswitch_t as = {0, 0};
     st->t_switch = NAN;
     if (knots_push(kn, t0, x)) return -1;
@@ -282,27 +284,32 @@ static int tsit5_solve(rhs_fn f, void* ctx, int m, double t0, double t1, const d
             buf[i] = ut / fma(dmax(fabs(x[i]), fabs(u[i])), rtol, atol);
         }
         double EEst = rms_norm(buf, m);
-        /* stepsize_controller!(PIController) */
-        double q;
+        /* stepsize_controller!(PIController): q = EEst^β1 / qold^β2 / γ clamped to
+         * [1/qmax, 1/qmin], evaluated as one exponential exp(β1 log EEst − β2 log qold)
+         * (OrdinaryDiffEq uses DiffEqBase.fastpow, a Float32 approximation, for both
+         * powers).  log(qold) is carried from the step that set qold. */
+        double q, le = 0.0;
         if (EEst == 0.0) {
             q = CTL_INV_QMAX;
         } else {
-            q11 = sbr_pow_pos(EEst, CTL_BETA1);
-            q = q11 / sbr_pow_pos(qold, CTL_BETA2);
+            le = sbr_log(EEst);
+            q = sbr_exp(CTL_BETA1 * le - CTL_BETA2 * lqold);
             q = dmax(CTL_INV_QMAX, dmin(CTL_INV_QMIN, q / CTL_GAMMA));
         }
         if (EEst <= 1.0) { /* accept */
             st->naccept++;
             double dtnew = dt / q;
             qold = dmax(EEst, CTL_QOLDMIN);
+            lqold = (qold == EEst) ? le : LOG_QOLDMIN;
             double tn = t + dt;
-            if (fabs(tn - t1) < 100.0 * sbr_jl_eps(dmax(t, t1))) tn = t1;
+            if (fabs(tn - t1) < snap) tn = t1; /* 100 eps(max(t, t_end)), t < t_end */
             t = tn;
             for (int i = 0; i < m; i++) { x[i] = u[i]; k1[i] = k7[i]; }
             dt = dmax(dmin(dtmax, dtnew), dtmin); /* calc_dt_propose! */
             if (knots_push(kn, t, x)) return -1;
-        } else { /* reject */
+        } else { /* reject: step_reject_controller!, q11 = EEst^β1 */
             st->nreject++;
+            const double q11 = sbr_exp(CTL_BETA1 * le);
             dt = dt / dmin(CTL_INV_QMIN, q11 / CTL_GAMMA);
         }
         if (!(dt > 0.0) || !isfinite(dt)) { st->status |= SBR_ODE_FAILED; break; }

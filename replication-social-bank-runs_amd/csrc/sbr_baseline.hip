@@ -87,7 +87,8 @@ __global__ __launch_bounds__(64) void learn_logistic_kernel(const double* __rest
     };
 
     const double LOG_QOLDMIN = sbr_log(CTL_QOLDMIN);
-    double t = T0, x = x0, qold = CTL_QOLDMIN, q11 = 1.0, lqold = LOG_QOLDMIN;
+    const double snap = 100.0 * sbr_jl_eps(T1); // fixed_t_for_floatingpoint_error!: t < t_end
+    double t = T0, x = x0, qold = CTL_QOLDMIN, lqold = LOG_QOLDMIN;
     AutoSwitch as;
     int naccept = 0, nreject = 0;
     push(t, x);
@@ -124,8 +125,7 @@ __global__ __launch_bounds__(64) void learn_logistic_kernel(const double* __rest
             q = CTL_INV_QMAX;
         } else {
             le = sbr_log(EEst);
-            q11 = sbr_exp(CTL_BETA1 * le);
-            q = q11 / sbr_exp(CTL_BETA2 * lqold);
+            q = sbr_exp(CTL_BETA1 * le - CTL_BETA2 * lqold);
             q = dmax(CTL_INV_QMAX, dmin(CTL_INV_QMIN, q / CTL_GAMMA));
         }
         if (EEst <= 1.0) {
@@ -134,7 +134,7 @@ __global__ __launch_bounds__(64) void learn_logistic_kernel(const double* __rest
             qold = dmax(EEst, CTL_QOLDMIN);
             lqold = (qold == EEst) ? le : LOG_QOLDMIN;
             double tn = t + dt;
-            if (fabs(tn - T1) < 100.0 * sbr_jl_eps(dmax(t, T1))) tn = T1;
+            if (fabs(tn - T1) < snap) tn = T1;
             t = tn;
             x = u;
             k1 = k7;
@@ -142,6 +142,7 @@ __global__ __launch_bounds__(64) void learn_logistic_kernel(const double* __rest
             push(t, x);
         } else {
             nreject++;
+            const double q11 = sbr_exp(CTL_BETA1 * le);
             dt = dt / dmin(CTL_INV_QMIN, q11 / CTL_GAMMA);
         }
         if (!(dt > 0.0) || !isfinite(dt)) { st |= SBR_ODE_FAILED; break; }

@@ -43,15 +43,6 @@ constexpr double DBL_EPS = 2.220446049250313e-16;
 __device__ __forceinline__ double dmin(double a, double b) { return a < b ? a : b; }
 __device__ __forceinline__ double dmax(double a, double b) { return a > b ? a : b; }
 
-// stepsize_controller!(::PIController): returns q, updates q11
-__device__ __forceinline__ double pi_q(double EEst, double qold, double& q11)
-{
-    if (EEst == 0.0) return CTL_INV_QMAX;
-    q11 = sbr_pow_pos(EEst, CTL_BETA1);
-    double q = q11 / sbr_pow_pos(qold, CTL_BETA2);
-    return dmax(CTL_INV_QMAX, dmin(CTL_INV_QMIN, q / CTL_GAMMA));
-}
-
 struct AutoSwitch {
     int count = 0;
     bool switched = false;

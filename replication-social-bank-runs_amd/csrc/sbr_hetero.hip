@@ -158,7 +158,9 @@ __global__ __launch_bounds__(64) void learn_hetero_kernel(const double* __restri
         n++;
     };
 
-    double t = T0, qold = CTL_QOLDMIN, q11 = 1.0;
+    const double LOG_QOLDMIN = sbr_log(CTL_QOLDMIN);
+    const double snap = 100.0 * sbr_jl_eps(T1);
+    double t = T0, qold = CTL_QOLDMIN, lqold = LOG_QOLDMIN;
     AutoSwitch as;
     int naccept = 0, nreject = 0;
     push(t, x);
@@ -207,13 +209,21 @@ __global__ __launch_bounds__(64) void learn_hetero_kernel(const double* __restri
             buf[k] = ut / fma(dmax(fabs(x[k]), fabs(u[k])), rtol, atol);
         }
         const double EEst = rms<K>(buf);
-        const double q = pi_q(EEst, qold, q11);
+        double q, le = 0.0;
+        if (EEst == 0.0) {
+            q = CTL_INV_QMAX;
+        } else {
+            le = sbr_log(EEst);
+            q = sbr_exp(CTL_BETA1 * le - CTL_BETA2 * lqold);
+            q = dmax(CTL_INV_QMAX, dmin(CTL_INV_QMIN, q / CTL_GAMMA));
+        }
         if (EEst <= 1.0) {
             naccept++;
             const double dtnew = dt / q;
             qold = dmax(EEst, CTL_QOLDMIN);
+            lqold = (qold == EEst) ? le : LOG_QOLDMIN;
             double tn = t + dt;
-            if (fabs(tn - T1) < 100.0 * sbr_jl_eps(dmax(t, T1))) tn = T1;
+            if (fabs(tn - T1) < snap) tn = T1;
             t = tn;
 #pragma unroll
             for (int k = 0; k < K; k++) { x[k] = u[k]; k1[k] = k7[k]; }
@@ -221,6 +231,7 @@ __global__ __launch_bounds__(64) void learn_hetero_kernel(const double* __restri
             push(t, x);
         } else {
             nreject++;
+            const double q11 = sbr_exp(CTL_BETA1 * le);
             dt = dt / dmin(CTL_INV_QMIN, q11 / CTL_GAMMA);
         }
         if (!(dt > 0.0) || !isfinite(dt)) { st |= SBR_ODE_FAILED; break; }

@@ -1,0 +1,22 @@
+#!/usr/bin/env bash
+# PMC counter passes on a short bench run (one counter group per rocprofv3 run).
+set -u
+OUT=gpurun_out/pmc
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+timeout -k 5 60 rocprofv3 -L > "$OUT/counters_list.txt" 2>&1 || true
+i=0
+while read -r grp; do
+  [ -z "$grp" ] && continue
+  i=$((i+1))
+  timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d "$OUT/p$i" -o pass -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} > "$OUT/p$i.log" 2>&1
+  rc=$?
+  echo "pass $i [$grp] rc=$rc" | tee -a "$OUT/passes.log"
+  if [ $rc -ne 0 ]; then echo "stopping after failed pass" | tee -a "$OUT/passes.log"; exit $rc; fi
+done <<'GROUPS'
+SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS
+SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU_FMA_F64
+SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 GRBM_GUI_ACTIVE GRBM_COUNT
+FETCH_SIZE
+WRITE_SIZE
+GROUPS
