@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--n", type=int, default=2048, help="β columns per GPU and u rows")
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-stride", type=int, default=8, help="cpu_baseline samples every k-th β column")
+    ap.add_argument("--cpu-stride", type=int, default=2, help="cpu_baseline samples every k-th β column")
     ap.add_argument("--traffic", default=str(REPO / "profiles" / "traffic_latest.json"))
     return ap.parse_args()
 

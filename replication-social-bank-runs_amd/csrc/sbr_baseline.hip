@@ -162,6 +162,8 @@ __global__ __launch_bounds__(64) void learn_logistic_kernel(const double* __rest
 // order) and HR = (p·exp(λτ̄))·g / (p·I + (1−p)·I_η).
 // ============================================================================
 constexpr int HZ_BLOCK = 256;
+constexpr int HZ_CHUNK = 16;
+constexpr int EQ_TILE = 4096;  // u values per equilibrium block (one block per β column up to this)
 
 __global__ __launch_bounds__(HZ_BLOCK) void hazard_kernel(const double* __restrict__ beta,
                                                           const double* __restrict__ eta, LearnArgs a, LearnBufs L)
@@ -231,8 +233,20 @@ __global__ __launch_bounds__(HZ_BLOCK) void hazard_kernel(const double* __restri
     }
     __syncthreads();
     if (threadIdx.x == 0) { // I_i = I_{i-1} + term_i, left to right (solver.jl:173-175)
+        // The chain of adds is inherently serial (reassociating would change the
+        // rounding); load HZ_CHUNK terms per round so only the adds are dependent.
         double I = 0.0;
-        for (int i = 1; i < ntau; i++) {
+        int i0 = 1;
+        for (; i0 + HZ_CHUNK <= ntau; i0 += HZ_CHUNK) {
+            double v[HZ_CHUNK];
+#pragma unroll
+            for (int k = 0; k < HZ_CHUNK; k++) v[k] = term[i0 + k];
+#pragma unroll
+            for (int k = 0; k < HZ_CHUNK; k++) { I = I + v[k]; v[k] = I; }
+#pragma unroll
+            for (int k = 0; k < HZ_CHUNK; k++) term[i0 + k] = v[k];
+        }
+        for (int i = i0; i < ntau; i++) {
             I = I + term[i];
             term[i] = I;
         }
@@ -595,6 +609,8 @@ __global__ __launch_bounds__(BLOCK) void equilibrium_kernel(LearnBufs L, const d
     double* hmin = hmax + nsum;
     double* pmc = hmin + nsum;
     double* smc = pmc + nsum;
+    __shared__ int eq_next;
+    if (threadIdx.x == 0) eq_next = 0;
     if (fits) {
         for (int i = threadIdx.x; i < n; i += BLOCK) { sT[i] = gT[i]; sG[i] = gG[i]; }
         for (int i = threadIdx.x; i < ntau; i += BLOCK) sH[i] = gH[i];
@@ -642,31 +658,45 @@ __global__ __launch_bounds__(BLOCK) void equilibrium_kernel(LearnBufs L, const d
         __syncthreads();
         S = Summ{hmax, hmin, pmc, smc};
     }
-    const int j = blockIdx.x * BLOCK + threadIdx.x;
-    if (j >= a.n_u) return;
-    const double uj = u[j];
+    // Points are handed out to waves 64 at a time from an LDS counter, so a
+    // wave that drew cheap no-run points goes back for more instead of idling
+    // at the end of the block while the run points (bisection + AW_max) of its
+    // neighbours finish.  Consecutive u in one wave keep its lanes on similar
+    // control paths (runs form a prefix in u on the paper's grids).
+    const int j0 = blockIdx.x * EQ_TILE;
+    const int j1 = j0 + EQ_TILE < a.n_u ? j0 + EQ_TILE : a.n_u;
+    const int lane = threadIdx.x & 63;
     const double ETA = eta[b], T1 = t_end[b];
     const uint32_t lbits = lst & (SBR_ODE_MAXITERS | SBR_STIFF_SWITCH | SBR_ODE_FAILED | SBR_KNOT_OVERFLOW);
-    PointResult r;
-    if (lst & (SBR_ARG_INVALID | SBR_OOB) || n < 2 || !(uj >= 0.0)) {
-        r.xi = NAN; r.aw = NAN; r.tol = INFINITY; r.iters = 0;
-        r.tin = NAN; r.tout = NAN;
-        r.status = ((lst & SBR_ARG_INVALID) || !(uj >= 0.0)) ? SBR_ARG_INVALID : (SBR_OOB | lbits);
-    } else {
-        const bool trunc = gT[n - 1] < T1;
-        if (fits)
+    const bool bad_col = (lst & (SBR_ARG_INVALID | SBR_OOB)) || n < 2;
+    const bool trunc = n >= 2 && gT[n - 1] < T1;
+    for (;;) {
+        int base = 0;
+        if (lane == 0) base = atomicAdd(&eq_next, 64);
+        base = __builtin_amdgcn_readfirstlane(base);
+        if (j0 + base >= j1) break;
+        const int j = j0 + base + lane;
+        if (j >= j1) continue;
+        const double uj = u[j];
+        PointResult r;
+        if (bad_col || !(uj >= 0.0)) {
+            r.xi = NAN; r.aw = NAN; r.tol = INFINITY; r.iters = 0;
+            r.tin = NAN; r.tout = NAN;
+            r.status = ((lst & SBR_ARG_INVALID) || !(uj >= 0.0)) ? SBR_ARG_INVALID : (SBR_OOB | lbits);
+        } else if (fits) {
             solve_point(sT, sG, sH, S, n, ntau, nle, ETA, T1, trunc, uj, a.kappa, a.max_iters, lbits, r, a.aw_path);
-        else
+        } else {
             solve_point(gT, gG, gH, S, n, ntau, nle, ETA, T1, trunc, uj, a.kappa, a.max_iters, lbits, r, a.aw_path);
+        }
+        const size_t o = (size_t)b * (size_t)a.n_u + j;
+        out.xi[o] = r.xi;
+        out.tau_in_unc[o] = r.tin;
+        out.tau_out_unc[o] = r.tout;
+        out.aw_max[o] = r.aw;
+        out.tol[o] = r.tol;
+        out.status[o] = r.status;
+        if (out.iters) out.iters[o] = r.iters;
     }
-    const size_t o = (size_t)b * (size_t)a.n_u + j;
-    out.xi[o] = r.xi;
-    out.tau_in_unc[o] = r.tin;
-    out.tau_out_unc[o] = r.tout;
-    out.aw_max[o] = r.aw;
-    out.tol[o] = r.tol;
-    out.status[o] = r.status;
-    if (out.iters) out.iters[o] = r.iters;
 }
 
 // ============================================================================
@@ -688,16 +718,16 @@ hipError_t launch_equilibrium(const LearnBufs& L, const double* eta, const doubl
                               const EqArgs& a, const ResultSoA& out, int n_beta, hipStream_t s)
 {
     const size_t lds = ((size_t)3 * a.lds_cap + 4 * ((a.lds_cap >> 6) + 1)) * sizeof(double);
-    if (a.n_u >= 1024) {
-        dim3 grid((a.n_u + 1023) / 1024, n_beta);
+    // one block per (β column, tile of EQ_TILE u values); block size by tile width
+    const int tiles = (a.n_u + EQ_TILE - 1) / EQ_TILE;
+    const int w = a.n_u < EQ_TILE ? a.n_u : EQ_TILE;
+    dim3 grid(tiles, n_beta);
+    if (w > 256)
         hipLaunchKernelGGL(equilibrium_kernel<1024>, grid, dim3(1024), lds, s, L, eta, t_end, u, a, out);
-    } else if (a.n_u >= 256) {
-        dim3 grid((a.n_u + 255) / 256, n_beta);
+    else if (w > 64)
         hipLaunchKernelGGL(equilibrium_kernel<256>, grid, dim3(256), lds, s, L, eta, t_end, u, a, out);
-    } else {
-        dim3 grid((a.n_u + 63) / 64, n_beta);
+    else
         hipLaunchKernelGGL(equilibrium_kernel<64>, grid, dim3(64), lds, s, L, eta, t_end, u, a, out);
-    }
     return hipGetLastError();
 }
 

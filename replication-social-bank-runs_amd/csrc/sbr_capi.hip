@@ -149,11 +149,12 @@ sbr_opts resolve(const sbr_opts* o)
     return r;
 }
 
-// τ̄ entries the hazard kernel keeps in LDS (≤ knot capacity, ≤ the LDS per workgroup)
+// τ̄ entries the hazard kernel keeps in LDS (32 KiB: five hazard blocks share a
+// CU; the paper's grids need ~3k, longer columns fall back to HBM scratch)
 int32_t hz_cap(const sbr_ctx* c, const sbr_opts& o)
 {
-    const int lds = c->lds_smem > 0 ? c->lds_smem : 65536;
-    const int cap = (lds - 1024) / 8;
+    (void)c;
+    const int cap = 4096;
     return o.knot_capacity + 1 < cap ? o.knot_capacity + 1 : cap;
 }
 
