@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-stride", type=int, default=2, help="cpu_baseline samples every k-th β column")
+    ap.add_argument("--phases", action="store_true",
+                    help="also time the equilibrium kernel stopped after each stage (diagnostic flags)")
     ap.add_argument("--traffic", default=str(REPO / "profiles" / "traffic_latest.json"))
     return ap.parse_args()
 
@@ -177,12 +179,42 @@ def main():
             "traffic": traffic,
         },
     }
+    if a.phases:
+        res["eq_phase_ms"] = phase_breakdown(eng, beta, eta, t_end, u, p, kappa, lam, x0, out, stream, dev)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(beta_h, u_h, a.cpu_stride, p, kappa, lam, x0)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def phase_breakdown(eng, beta, eta, t_end, u, p, kappa, lam, x0, out, stream, dev, reps=3):
+    """Equilibrium-kernel time when every point stops after the crossing scan,
+    after the bisection, and in full; plus AW blocks evaluated per run point."""
+    from sbr import _lib
+    res = {}
+    for name, fl in (("buffer", _lib.SBR_FLAG_DIAG_STOP_AFTER_BUFFER), ("bisect", _lib.SBR_FLAG_DIAG_STOP_AFTER_BISECT),
+                     ("full", 0), ("full_exhaustive_aw", -1)):
+        kw = dict(exhaustive=True) if fl == -1 else dict(flags=fl)
+        eng.sweep_baseline_dev(beta, eta, t_end, u, p, kappa, lam, x0, out, stream=stream, **kw)
+        torch.cuda.synchronize(dev)
+        eng.timing_read(stream)
+        eng.timing_enable(True)
+        for _ in range(reps):
+            eng.sweep_baseline_dev(beta, eta, t_end, u, p, kappa, lam, x0, out, stream=stream, **kw)
+        torch.cuda.synchronize(dev)
+        _, eq_ms, nc = eng.timing_read(stream)
+        eng.timing_enable(False)
+        res[name] = eq_ms / max(nc, 1)
+    eng.sweep_baseline_dev(beta, eta, t_end, u, p, kappa, lam, x0, out, stream=stream,
+                           flags=_lib.SBR_FLAG_DIAG_COUNT_AW_BLOCKS)
+    torch.cuda.synchronize(dev)
+    st = out["status"].cpu().numpy().view(np.uint32)
+    nb = out["iters"].cpu().numpy()[(st & sbr.STATUS["SBR_RUN"]) > 0]
+    res["aw_blocks_per_run_point"] = float(nb.mean()) if nb.size else 0.0
+    res["run_points"] = int(nb.size)
+    return res
 
 
 def cpu_baseline(beta_h, u_h, stride, p, kappa, lam, x0):

@@ -55,6 +55,13 @@ typedef struct {
 /* Evaluate every τ̄ knot of the crossing scan and of the AW path (no block
  * summaries / branch-and-bound).  Same results; for A/B timing and checks. */
 #define SBR_FLAG_EXHAUSTIVE 0x1
+/* Diagnostics (timing breakdown only — results are NOT the reference's):
+ * stop every point after the crossing scan / after the ξ bisection, or
+ * report the number of 64-knot AW blocks evaluated in `iters` instead of
+ * the bisection count. */
+#define SBR_FLAG_DIAG_STOP_AFTER_BUFFER 0x100
+#define SBR_FLAG_DIAG_STOP_AFTER_BISECT 0x200
+#define SBR_FLAG_DIAG_COUNT_AW_BLOCKS 0x400
 
 typedef struct {
     double* xi;          /* SolvedModel.ξ                       */

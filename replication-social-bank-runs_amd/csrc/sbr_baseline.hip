@@ -391,7 +391,8 @@ template <class P>
 __device__ __forceinline__ void solve_point(P T, P G, P H, const Summ& S, const int n, const int ntau,
                                             const int nle, const double ETA, const double T1, const bool trunc,
                                             const double u, const double kappa, const int max_iters,
-                                            const uint32_t lbits, PointResult& r, double* __restrict__ aw_path)
+                                            const uint32_t lbits, PointResult& r, double* __restrict__ aw_path,
+                                            const int diag)
 {
     r.xi = NAN; r.aw = NAN; r.tol = INFINITY; r.iters = 0; r.status = 0;
     const double tlo = T[0], thi = T[n - 1];
@@ -438,6 +439,7 @@ __device__ __forceinline__ void solve_point(P T, P G, P H, const Summ& S, const 
     }
     r.tin = tin;
     r.tout = tout;
+    if (diag & 1) return;
     if (tin == tout) {
         r.status = SBR_NO_RUN_HR_BELOW_U | SBR_CONVERGED | lbits;
         r.tol = 0.0;
@@ -507,6 +509,8 @@ __device__ __forceinline__ void solve_point(P T, P G, P H, const Summ& S, const 
     }
     if (flag) { r.status = flag | lbits; return; }
     if (s != SBR_RUN) { r.status = s | lbits; return; }
+    if (diag & 2) return;
+    int nblk_eval = 0;
 
     // ---------------- get_AW on the HR grid + AW_max ----------------
     const double icc = (tin >= xi) ? xi : tin;
@@ -514,11 +518,12 @@ __device__ __forceinline__ void solve_point(P T, P G, P H, const Summ& S, const 
     if (!in_range(0.0, tlo, thi, trunc, flag)) { r.status = flag | lbits; return; }
     const double G0 = lerp_at(T, G, n, ssl_range(T, 0, n - 1, 0.0), 0.0);
     double mx = -INFINITY;
-    // exact AW_cum(τ̄_i) for i in [i0, i1), folded into the NaN-propagating max
-    auto eval_range = [&](int i0, int i1) {
+    // exact AW_cum(τ̄_i) for i in [i0, i1), folded into the NaN-propagating max;
+    // ha/hb: predicted brackets of a(τ̄_i0), b(τ̄_i0) (search hints, any side)
+    auto eval_range = [&](int i0, int i1, int ha, int hb) {
         const double a0 = (tau(i0) - xi) + icc, b0 = (tau(i0) - xi) + occ;
-        int ji = ssl_range(T, 0, n - 1, a0 > 0 ? a0 : 0.0);
-        int jo = ssl_range(T, 0, n - 1, b0 > 0 ? b0 : 0.0);
+        int ji = ssl_near(T, n, ha, a0 > 0 ? a0 : 0.0);
+        int jo = ssl_near(T, n, hb, b0 > 0 ? b0 : 0.0);
         for (int i = i0; i < i1; i++) {
             const double ti = tau(i);
             const double av = (ti - xi) + icc;
@@ -533,14 +538,15 @@ __device__ __forceinline__ void solve_point(P T, P G, P H, const Summ& S, const 
             const double awin = av >= 0 ? gi : 0.0;
             const double awout = bv >= 0 ? go : 0.0;
             const double v = (awout - awin) + G0;
+            if ((diag & 4) && ((i & 7) == 0 || i == i0)) nblk_eval++;
             if (aw_path) aw_path[i] = v;
             if (mx == mx && (v != v || v > mx)) mx = v;
         }
     };
     if (!S.pmc || aw_path) {
-        eval_range(0, ntau); // exhaustive (single-point path mode, or summaries unavailable)
+        eval_range(0, ntau, 0, 0); // exhaustive (single-point path mode, or summaries unavailable)
     } else {
-        // Branch and bound over 64-knot blocks of τ̄ — the same maximum, fewer evaluations.
+        // Branch and bound over τ̄ blocks — the same maximum, far fewer evaluations.
         // Every argument sequence is nondecreasing in i, so the range check of the
         // last τ̄ covers the whole path.
         const double al = (tau(ntau - 1) - xi) + icc, bl = (tau(ntau - 1) - xi) + occ;
@@ -548,34 +554,47 @@ __device__ __forceinline__ void solve_point(P T, P G, P H, const Summ& S, const 
             flag |= trunc ? SBR_ENGINE_TRUNC : SBR_OOB;
         } else {
             const int nblk = (ntau + 63) >> 6;
-            // upper bound of AW_cum over block b: AW_OUT ≤ max G over knots up to the
-            // bracket of the block's last argument, AW_IN ≥ min G over knots from the
-            // bracket of its first argument (coarse prefix-max / suffix-min tables),
-            // plus a rounding margin far above the ≈2e-15 the exact path can add.
-            int ja = 0, jb = 0;
-            auto block_ub = [&](int bk) -> double {
-                const int i0 = bk << 6, i1 = (i0 + 64 < ntau ? i0 + 64 : ntau) - 1;
-                const double av0 = (tau(i0) - xi) + icc;
-                const double bv1 = (tau(i1) - xi) + occ;
-                ja = ssl_gallop(T, n, ja, av0 > 0 ? av0 : 0.0);
-                jb = ssl_gallop(T, n, jb, bv1 > 0 ? bv1 : 0.0);
-                const double hi = S.pmc[(jb + 1 < n - 1 ? jb + 1 : n - 1) >> 6];
-                const double lo = S.smc[(ja < n - 2 ? ja : n - 2) >> 6];
+            auto xa_of = [&](int i) { const double v = (tau(i) - xi) + icc; return v > 0 ? v : 0.0; };
+            auto xb_of = [&](int i) { const double v = (tau(i) - xi) + occ; return v > 0 ? v : 0.0; };
+            // Upper bound of AW_cum over τ̄ indices [i0, i1] given ja = bracket of a(τ̄_i0)
+            // and jb = bracket of b(τ̄_i1): AW_OUT ≤ max G over knots ≤ jb+1, AW_IN ≥ min G
+            // over knots ≥ ja (8-knot prefix-max / suffix-min tables), plus a rounding
+            // margin far above the ≈2e-15 the exact path can add.
+            auto ub_of = [&](int i0, int ja, int jb) -> double {
+                const double hi = S.pmc[(jb + 1 < n - 1 ? jb + 1 : n - 1) >> 3];
+                const double lo = S.smc[(ja < n - 2 ? ja : n - 2) >> 3];
                 const double ub_out = hi > 0.0 ? hi : 0.0;
-                const double lb_in = av0 >= 0 ? lo : (lo < 0.0 ? lo : 0.0);
+                const double lb_in = ((tau(i0) - xi) + icc) >= 0 ? lo : (lo < 0.0 ? lo : 0.0);
                 return ((ub_out - lb_in) + G0) + 1e-14;
             };
-            int best = 0;
+            // pass 1: 64-wide bounds; the most promising block is evaluated first
+            // (brackets are searched from the previous block's plus the block width:
+            // a(τ̄_i) and b(τ̄_i) are τ̄_i shifted by constants, so they advance with i)
+            int ja = 0, jb = 0, best = 0, bja = 0, bjb = 0;
             double bub = -INFINITY;
             for (int bk = 0; bk < nblk; bk++) {
-                const double ub = block_ub(bk);
-                if (!(ub <= bub)) { bub = ub; best = bk; }
+                const int i0 = bk << 6, i1 = (i0 + 64 < ntau ? i0 + 64 : ntau) - 1;
+                ja = ssl_near(T, n, bk ? ja + 64 : 0, xa_of(i0));
+                jb = ssl_near(T, n, bk ? jb + 64 : 0, xb_of(i1));
+                const double ub = ub_of(i0, ja, jb);
+                if (!(ub <= bub)) { bub = ub; best = bk; bja = ja; bjb = jb; }
             }
-            eval_range(best << 6, (best << 6) + 64 < ntau ? (best << 6) + 64 : ntau);
-            ja = 0; jb = 0;
-            for (int bk = 0; bk < nblk && !flag; bk++) {
-                const double ub = block_ub(bk);
-                if (bk != best && !(ub <= mx)) eval_range(bk << 6, (bk << 6) + 64 < ntau ? (bk << 6) + 64 : ntau);
+            eval_range(best << 6, (best << 6) + 64 < ntau ? (best << 6) + 64 : ntau, bja, bjb - 63);
+            // pass 2: every other block whose bound beats the running max is refined
+            // into 8-wide sub-blocks with their own bounds
+            for (int bk = 0; bk < nblk && !flag && mx == mx; bk++) {
+                const int i0 = bk << 6, ie = i0 + 64 < ntau ? i0 + 64 : ntau;
+                ja = ssl_near(T, n, bk ? ja + 64 : 0, xa_of(i0));
+                jb = ssl_near(T, n, bk ? jb + 64 : 0, xb_of(ie - 1));
+                if (bk == best || ub_of(i0, ja, jb) <= mx) continue;
+                int sa = ja, se = jb - (ie - 1 - i0); // predictions for the first sub-block
+                for (int s0 = i0; s0 < ie && mx == mx; s0 += 8) {
+                    const int s1 = (s0 + 8 < ie ? s0 + 8 : ie) - 1;
+                    sa = ssl_near(T, n, s0 == i0 ? sa : sa + 8, xa_of(s0));
+                    const int hb = s0 == i0 ? se : se + 1; // prediction for b(τ̄_s0)
+                    se = ssl_near(T, n, se + (s0 == i0 ? s1 - s0 : 8), xb_of(s1));
+                    if (!(ub_of(s0, sa, se) <= mx)) eval_range(s0, s1 + 1, sa, hb);
+                }
             }
         }
     }
@@ -584,6 +603,7 @@ __device__ __forceinline__ void solve_point(P T, P G, P H, const Summ& S, const 
     r.tol = tolr;
     r.aw = mx;
     r.status = SBR_RUN | SBR_CONVERGED | lbits;
+    if (diag & 4) r.iters = nblk_eval;
 }
 
 template <int BLOCK>
@@ -604,11 +624,11 @@ __global__ __launch_bounds__(BLOCK) void equilibrium_kernel(LearnBufs L, const d
     double* sG = smem + a.lds_cap;
     double* sH = smem + 2 * a.lds_cap;
     // block summaries behind the three knot arrays (lds_cap/64 + 1 entries each)
-    const int nsum = (a.lds_cap >> 6) + 1;
+    const int nsum = (a.lds_cap >> 6) + 1, nsum8 = (a.lds_cap >> 3) + 1;
     double* hmax = smem + 3 * a.lds_cap;
     double* hmin = hmax + nsum;
     double* pmc = hmin + nsum;
-    double* smc = pmc + nsum;
+    double* smc = pmc + nsum8;
     __shared__ int eq_next;
     if (threadIdx.x == 0) eq_next = 0;
     if (fits) {
@@ -618,7 +638,7 @@ __global__ __launch_bounds__(BLOCK) void equilibrium_kernel(LearnBufs L, const d
     __syncthreads();
     Summ S{nullptr, nullptr, nullptr, nullptr};
     if (fits && !a.exhaustive) {
-        const int nbh = (ntau + 63) >> 6, nbg = (n + 63) >> 6;
+        const int nbh = (ntau + 63) >> 6, nbg = (n + 7) >> 3;
         for (int bk = threadIdx.x; bk < nbh + nbg; bk += BLOCK) {
             if (bk < nbh) {
                 double mx = -INFINITY, mn = INFINITY;
@@ -633,8 +653,8 @@ __global__ __launch_bounds__(BLOCK) void equilibrium_kernel(LearnBufs L, const d
             } else {
                 const int g = bk - nbh;
                 double mx = -INFINITY, mn = INFINITY;
-                const int e = (g << 6) + 64 < n ? (g << 6) + 64 : n;
-                for (int i = g << 6; i < e; i++) {
+                const int e = (g << 3) + 8 < n ? (g << 3) + 8 : n;
+                for (int i = g << 3; i < e; i++) {
                     const double v = sG[i];
                     if (v != v) { mx = NAN; mn = NAN; break; }
                     if (v > mx) mx = v;
@@ -645,11 +665,13 @@ __global__ __launch_bounds__(BLOCK) void equilibrium_kernel(LearnBufs L, const d
             }
         }
         __syncthreads();
-        if (threadIdx.x == 0) { // prefix max / suffix min over blocks (NaN-propagating)
+        // prefix max / suffix min over blocks (NaN-propagating), two waves at once
+        if (threadIdx.x == 0) {
             for (int g = 1; g < nbg; g++) {
                 const double a0 = pmc[g - 1], b0 = pmc[g];
                 pmc[g] = (a0 != a0 || b0 != b0) ? NAN : (a0 > b0 ? a0 : b0);
             }
+        } else if (threadIdx.x == (BLOCK > 64 ? 64 : 1)) {
             for (int g = nbg - 2; g >= 0; g--) {
                 const double a0 = smc[g + 1], b0 = smc[g];
                 smc[g] = (a0 != a0 || b0 != b0) ? NAN : (a0 < b0 ? a0 : b0);
@@ -684,9 +706,9 @@ __global__ __launch_bounds__(BLOCK) void equilibrium_kernel(LearnBufs L, const d
             r.tin = NAN; r.tout = NAN;
             r.status = ((lst & SBR_ARG_INVALID) || !(uj >= 0.0)) ? SBR_ARG_INVALID : (SBR_OOB | lbits);
         } else if (fits) {
-            solve_point(sT, sG, sH, S, n, ntau, nle, ETA, T1, trunc, uj, a.kappa, a.max_iters, lbits, r, a.aw_path);
+            solve_point(sT, sG, sH, S, n, ntau, nle, ETA, T1, trunc, uj, a.kappa, a.max_iters, lbits, r, a.aw_path, a.diag);
         } else {
-            solve_point(gT, gG, gH, S, n, ntau, nle, ETA, T1, trunc, uj, a.kappa, a.max_iters, lbits, r, a.aw_path);
+            solve_point(gT, gG, gH, S, n, ntau, nle, ETA, T1, trunc, uj, a.kappa, a.max_iters, lbits, r, a.aw_path, a.diag);
         }
         const size_t o = (size_t)b * (size_t)a.n_u + j;
         out.xi[o] = r.xi;
@@ -717,7 +739,7 @@ hipError_t launch_learn_logistic(const double* beta, const double* eta, const do
 hipError_t launch_equilibrium(const LearnBufs& L, const double* eta, const double* t_end, const double* u,
                               const EqArgs& a, const ResultSoA& out, int n_beta, hipStream_t s)
 {
-    const size_t lds = ((size_t)3 * a.lds_cap + 4 * ((a.lds_cap >> 6) + 1)) * sizeof(double);
+    const size_t lds = ((size_t)3 * a.lds_cap + 2 * ((a.lds_cap >> 6) + 1) + 2 * ((a.lds_cap >> 3) + 1)) * sizeof(double);
     // one block per (β column, tile of EQ_TILE u values); block size by tile width
     const int tiles = (a.n_u + EQ_TILE - 1) / EQ_TILE;
     const int w = a.n_u < EQ_TILE ? a.n_u : EQ_TILE;

@@ -185,7 +185,8 @@ int run_baseline(sbr_ctx* c, hipStream_t s, const double* beta, const double* et
     mark(c, s);
     HIP_TRY(c, sbr::launch_learn_logistic(beta, eta, t_end, la, c->L, s), SBR_EDEVICE);
     mark(c, s);
-    sbr::EqArgs ea{kappa, (int32_t)n_u, o.bisect_max_iters, c->lds_cap, aw_path, (o.flags & SBR_FLAG_EXHAUSTIVE) ? 1 : 0};
+    sbr::EqArgs ea{kappa, (int32_t)n_u, o.bisect_max_iters, c->lds_cap, aw_path, (o.flags & SBR_FLAG_EXHAUSTIVE) ? 1 : 0,
+                    (o.flags >> 8) & 7};
     HIP_TRY(c, sbr::launch_equilibrium(c->L, eta, t_end, u, ea, out, (int)n_beta, s), SBR_EDEVICE);
     mark(c, s);
     return SBR_OK;
@@ -225,7 +226,8 @@ int sbr_init(int device, sbr_ctx** out)
     if (smem <= 0) smem = 65536;
     c->lds_smem = smem;
     // 3 doubles per staged knot (t, G, HR) + 4 block-summary doubles per 64 knots; 1 KiB slack
-    c->lds_cap = (int)(((long)(smem - 1024) * 64) / (8 * (3 * 64 + 4)));
+    // per 64 knots: t, G, HR (3·64) + HR max/min (2) + 8-knot G prefix-max/suffix-min (16)
+    c->lds_cap = (int)(((long)(smem - 1024) * 64) / (8 * (3 * 64 + 2 + 16)));
     *out = c;
     return SBR_OK;
 }

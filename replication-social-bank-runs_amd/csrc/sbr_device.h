@@ -84,6 +84,23 @@ __device__ __forceinline__ int ssl_gallop(P t, int n, int j0, double x)
     return ssl_range(t, lo, hi, x);
 }
 
+// searchsortedlast from an arbitrary hint h (a prediction, either side of the
+// answer): gallop forward or backward from h.  Requires t[0] <= x.
+template <class P>
+__device__ __forceinline__ int ssl_near(P t, int n, int h, double x)
+{
+    h = h < 0 ? 0 : (h > n - 1 ? n - 1 : h);
+    if (t[h] <= x) return ssl_gallop(t, n, h, x);
+    int hi = h - 1, lo = h - 1, step = 1; // invariant: t[hi + 1] > x
+    while (lo > 0 && t[lo] > x) {
+        hi = lo - 1;
+        lo = hi - step;
+        step <<= 1;
+        if (lo < 0) lo = 0;
+    }
+    return ssl_range(t, lo, hi, x);
+}
+
 // Interpolations.jl gridded Linear on bracket j (clamped to [0, n-2]):
 // v[j]*(1-δ) + v[j+1]*δ with δ = (x - t[j]) / (t[j+1] - t[j]).
 template <class P, class Q>

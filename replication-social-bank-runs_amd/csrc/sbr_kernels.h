@@ -37,6 +37,7 @@ struct EqArgs {
     int32_t lds_cap;    // knots staged in LDS per workgroup (3 doubles each + block summaries)
     double* aw_path;    // optional AW_cum(τ̄) output for single-point mode (n_u == 1)
     int32_t exhaustive; // 1: linear crossing scan + every AW knot (no block summaries)
+    int32_t diag;       // SBR_FLAG_DIAG_* bits >> 8 (timing breakdown only)
 };
 
 struct ResultSoA {

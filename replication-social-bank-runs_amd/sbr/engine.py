@@ -77,7 +77,8 @@ class Engine:
         return {k: (v.reshape(nb, nu) if v is not None else None) for k, v in out.items()}
 
     def sweep_baseline_dev(self, beta, eta, t_end, u, p, kappa, lam, x0, out: dict, stream: int | None = None,
-                           max_iters: int = 100, knot_capacity: int = 65536, exhaustive: bool = False):
+                           max_iters: int = 100, knot_capacity: int = 65536, exhaustive: bool = False,
+                           flags: int = 0):
         """Device-pointer variant on torch tensors (float64 cuda) — no host sync.
         ``out`` holds preallocated tensors xi/tau_in_unc/tau_out_unc/aw_max/tol
         (float64), status (int32 viewed as uint32) and optional iters (int32)."""
@@ -85,7 +86,7 @@ class Engine:
         soa = _lib.ResultSoA(*[(out[k].data_ptr() if out.get(k) is not None else None)
                                for k in (*RESULT_FIELDS, "status", "iters")])
         opts = _lib.default_opts(early_exit_nan_run=0, bisect_max_iters=max_iters, knot_capacity=knot_capacity,
-                                 flags=_lib.SBR_FLAG_EXHAUSTIVE if exhaustive else 0)
+                                 flags=(_lib.SBR_FLAG_EXHAUSTIVE if exhaustive else 0) | flags)
         rc = self._L.sbr_sweep_baseline_dev(self._ctx, stream, beta.data_ptr(), eta.data_ptr(), t_end.data_ptr(),
                                             x0, u.data_ptr(), nb, nu, p, kappa, lam, ctypes.byref(opts),
                                             ctypes.byref(soa))
