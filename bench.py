@@ -6,7 +6,12 @@ Workload (BASELINE config 3): the Fig 5 grid of scripts/1_baseline.jl:210-212 at
 2048), η = 15 and tspan = (0, 30) for every β (copy-modify carry-over) — 4,194,304
 equilibria per GPU.  One step = one full sweep: learning (Tsit5 + hazard) for every
 β column, then buffers + ξ bisection + AW_max for every (β, u), every point solved
-(no early exit), inputs already resident in HBM, results written to HBM.
+(no early exit), inputs already resident in HBM, results written to HBM.  The K
+timed steps are K grids handed to sbr_sweep_baseline_batch_dev, which pipelines
+them: the learning stage of step k+1 (latency-bound, 32 waves) runs on a second,
+highest-priority stream while the equilibrium stage of step k fills the CUs.
+Every step's learning and equilibrium run in full inside the timed region
+(--no-pipeline: one serial sweep call per step).
 
 N GPUs (torchrun, one process per GPU, RCCL): weak scaling — rank r owns the β
 columns r, r+N, r+2N, … of a 2048·N-column grid (same u axis), so per-GPU work is
@@ -52,6 +57,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--n", type=int, default=2048, help="β columns per GPU and u rows")
     ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="one sbr_sweep_baseline_dev call per step (no learning/equilibrium overlap across steps)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-stride", type=int, default=2, help="cpu_baseline samples every k-th β column")
     ap.add_argument("--phases", action="store_true",
@@ -78,13 +85,16 @@ def main():
     nb, nu = len(beta_h), len(u_h)
     p, kappa, lam, x0 = 0.5, 0.6, 0.01, 1e-4
 
-    beta = torch.from_numpy(beta_h).to(dev)
-    eta = torch.full((nb,), 15.0, dtype=torch.float64, device=dev)
-    t_end = torch.full((nb,), 30.0, dtype=torch.float64, device=dev)
+    pipe = not a.no_pipeline
+    nbat = max(a.steps, a.warmup, 1) if pipe else 1
+    # one row per batch (= step); every batch is the full config-3 grid, recomputed
+    beta = torch.from_numpy(beta_h).to(dev).repeat(nbat, 1)
+    eta = torch.full((nbat, nb), 15.0, dtype=torch.float64, device=dev)
+    t_end = torch.full((nbat, nb), 30.0, dtype=torch.float64, device=dev)
     u = torch.from_numpy(u_h).to(dev)
-    out = {k: torch.empty(nb * nu, dtype=torch.float64, device=dev) for k in sbr.engine.RESULT_FIELDS}
-    out["status"] = torch.empty(nb * nu, dtype=torch.int32, device=dev)
-    out["iters"] = torch.empty(nb * nu, dtype=torch.int32, device=dev)
+    out = {k: torch.empty(nbat, nb * nu, dtype=torch.float64, device=dev) for k in sbr.engine.RESULT_FIELDS}
+    out["status"] = torch.empty(nbat, nb * nu, dtype=torch.int32, device=dev)
+    out["iters"] = torch.empty(nbat, nb * nu, dtype=torch.int32, device=dev)
     gather = world > 1 and not a.no_gather
     if gather and rank == 0:
         g_aw = [torch.empty(nb * nu, dtype=torch.float64, device=dev) for _ in range(world)]
@@ -95,14 +105,29 @@ def main():
     eng = sbr.Engine(local)
     stream = torch.cuda.current_stream(dev).cuda_stream
 
-    def step():
-        eng.sweep_baseline_dev(beta, eta, t_end, u, p, kappa, lam, x0, out, stream=stream)
-        if gather:
-            dist.gather(out["aw_max"], g_aw, dst=0)
-            dist.gather(out["status"], g_st, dst=0)
+    def gather_batch(k):
+        dist.gather(out["aw_max"][k], g_aw, dst=0)
+        dist.gather(out["status"][k], g_st, dst=0)
 
-    for _ in range(a.warmup):
-        step()
+    def run_steps(n):
+        """n steps: pipelined, one batch call of n grids (learning of step k+1
+        overlaps the equilibrium of step k); else one sweep call per step."""
+        if n <= 0:
+            return
+        if pipe:
+            eng.sweep_baseline_batch_dev(beta[:n], eta[:n], t_end[:n], u, p, kappa, lam, x0,
+                                         {k: v[:n] for k, v in out.items()}, stream=stream)
+            for k in range(n):
+                if gather:
+                    gather_batch(k)
+        else:
+            one = {k: v[0] for k, v in out.items()}
+            for _ in range(n):
+                eng.sweep_baseline_dev(beta[0], eta[0], t_end[0], u, p, kappa, lam, x0, one, stream=stream)
+                if gather:
+                    gather_batch(0)
+
+    run_steps(a.warmup)
     torch.cuda.synchronize(dev)
     eng.timing_read(stream)  # drop anything recorded so far
     eng.timing_enable(True)
@@ -110,8 +135,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
+    run_steps(a.steps)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -125,8 +149,9 @@ def main():
 
     # ---- algorithmic flops of this rank's last step (from the kernels' own outputs) ----
     ls = eng.learn_stats(nb)
-    iters = out["iters"].cpu().numpy().reshape(nb, nu).astype(np.int64)
-    status = out["status"].cpu().numpy().view(np.uint32).reshape(nb, nu)
+    last = (a.steps - 1) if pipe else 0
+    iters = out["iters"][last].cpu().numpy().reshape(nb, nu).astype(np.int64)
+    status = out["status"][last].cpu().numpy().view(np.uint32).reshape(nb, nu)
     run = (status & sbr.STATUS["SBR_RUN"]) > 0
     n_tau = ls["n_tau"].astype(np.int64)
     f_eq = (F_BUFFER * nb * nu + F_BISECT_ITER * int(iters.sum())
@@ -166,6 +191,7 @@ def main():
             "n_beta_per_gpu": nb, "n_u": nu, "eta": 15.0, "t_end": 30.0, "p": p, "kappa": kappa,
             "lambda": lam, "x0": x0, "early_exit": False, "gather": gather,
             "parallelism": f"beta-column shards x{world}",
+            "pipelined": pipe,
         },
         "kernel_ms_per_step": {"learn_logistic": learn_ms / max(ncalls, 1), "equilibrium": eq_ms / max(ncalls, 1)},
         "flops_per_step": {"equilibrium": f_eq, "learn": f_learn},
@@ -180,7 +206,8 @@ def main():
         },
     }
     if a.phases:
-        res["eq_phase_ms"] = phase_breakdown(eng, beta, eta, t_end, u, p, kappa, lam, x0, out, stream, dev)
+        res["eq_phase_ms"] = phase_breakdown(eng, beta[0], eta[0], t_end[0], u, p, kappa, lam, x0,
+                                             {k: v[0] for k, v in out.items()}, stream, dev)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(beta_h, u_h, a.cpu_stride, p, kappa, lam, x0)
     if rank == 0:

@@ -103,6 +103,22 @@ int sbr_sweep_baseline_dev(sbr_ctx* ctx, void* stream, const double* beta, const
                            double kappa, double lambda, const sbr_opts* opts, sbr_result_soa* out);
 
 /*
+ * n_batch grids that share n_beta, n_u, u and the scalars, swept back to back
+ * and pipelined: the learning stage (latency-bound, one lane per β) of batch
+ * k+1 runs on a second, highest-priority stream while the equilibrium stage of
+ * batch k fills the CUs.  beta/eta/t_end are [n_batch × n_beta] (row k =
+ * batch k); every out field is [n_batch × n_beta × n_u] (iters may be NULL).
+ * Device pointers; inputs are read after the work already enqueued on
+ * `stream`, results are complete for work enqueued on `stream` afterwards.
+ * Each batch gives exactly what sbr_sweep_baseline_dev gives for it.  Use a
+ * context from one stream at a time.
+ */
+int sbr_sweep_baseline_batch_dev(sbr_ctx* ctx, void* stream, int64_t n_batch, const double* beta,
+                                 const double* eta, const double* t_end, double x0, const double* u,
+                                 int64_t n_beta, int64_t n_u, double p, double kappa, double lambda,
+                                 const sbr_opts* opts, sbr_result_soa* out);
+
+/*
  * Learning only — solve_learning (learning.jl:109-124) for n_beta β at once.
  * Writes, per β, the knot grid t and CDF values G of the adaptive ODE
  * solution (row i at [i*cap .. i*cap + n_knots[i]) ); g = βG(1−G) is implied

@@ -29,6 +29,9 @@ __global__ __launch_bounds__(64) void learn_logistic_kernel(const double* __rest
                                                             const double* __restrict__ t_end, LearnArgs a,
                                                             LearnBufs L)
 {
+    // latency-bound (one serial ODE per lane): take issue priority over co-resident
+    // equilibrium waves of a previous batch
+    __builtin_amdgcn_s_setprio(3);
     const int b = blockIdx.x * 64 + threadIdx.x;
     if (b >= a.n_beta) return;
     const double BETA = beta[b], ETA = eta[b], T1 = t_end[b], T0 = 0.0;
@@ -168,8 +171,11 @@ constexpr int EQ_TILE = 4096;  // u values per equilibrium block (one block per 
 __global__ __launch_bounds__(HZ_BLOCK) void hazard_kernel(const double* __restrict__ beta,
                                                           const double* __restrict__ eta, LearnArgs a, LearnBufs L)
 {
-    extern __shared__ double lterm[]; // trapezoid terms, then I (HBM scratch beyond hz_cap)
+    // Trapezoid terms, then I, go to the column's HBM scratch row (L2-resident
+    // while the block runs): no LDS, so hazard blocks of the next batch can share
+    // CUs with an equilibrium kernel that holds all of their LDS.
     __shared__ int s_m;
+    __builtin_amdgcn_s_setprio(3);
     const int b = blockIdx.x;
     const int n = L.n_knots[b];
     const uint32_t st = L.status[b];
@@ -199,7 +205,7 @@ __global__ __launch_bounds__(HZ_BLOCK) void hazard_kernel(const double* __restri
         oob = push;                           // no knot beyond η to interpolate pdf(η)
     }
     const int ntau = m + (push ? 1 : 0);
-    double* term = ntau <= a.hz_cap ? lterm : L.hrI + row;
+    double* __restrict__ term = L.hrI + row;
     if (oob) {
         if (threadIdx.x == 0) {
             L.status[b] = st | SBR_OOB;
@@ -518,12 +524,16 @@ __device__ __forceinline__ void solve_point(P T, P G, P H, const Summ& S, const 
     if (!in_range(0.0, tlo, thi, trunc, flag)) { r.status = flag | lbits; return; }
     const double G0 = lerp_at(T, G, n, ssl_range(T, 0, n - 1, 0.0), 0.0);
     double mx = -INFINITY;
-    // exact AW_cum(τ̄_i) for i in [i0, i1), folded into the NaN-propagating max;
-    // ha/hb: predicted brackets of a(τ̄_i0), b(τ̄_i0) (search hints, any side)
-    auto eval_range = [&](int i0, int i1, int ha, int hb) {
-        const double a0 = (tau(i0) - xi) + icc, b0 = (tau(i0) - xi) + occ;
-        int ji = ssl_near(T, n, ha, a0 > 0 ? a0 : 0.0);
-        int jo = ssl_near(T, n, hb, b0 > 0 ? b0 : 0.0);
+    auto xa_of = [&](int i) { const double v = (tau(i) - xi) + icc; return v > 0 ? v : 0.0; };
+    auto xb_of = [&](int i) { const double v = (tau(i) - xi) + occ; return v > 0 ? v : 0.0; };
+    // Brackets of a(τ̄_i) and b(τ̄_i) are searched from the last one found, moved by
+    // the τ̄ distance (both are τ̄_i shifted by a constant, so they advance with i).
+    int ra_i = 0, ra_j = 0, rb_i = 0, rb_j = 0;
+    auto brk_a = [&](int i) { ra_j = ssl_near(T, n, ra_j + (i - ra_i), xa_of(i)); ra_i = i; return ra_j; };
+    auto brk_b = [&](int i) { rb_j = ssl_near(T, n, rb_j + (i - rb_i), xb_of(i)); rb_i = i; return rb_j; };
+    // exact AW_cum(τ̄_i) for i in [i0, i1), folded into the NaN-propagating max
+    auto eval_range = [&](int i0, int i1) {
+        int ji = brk_a(i0), jo = brk_b(i0);
         for (int i = i0; i < i1; i++) {
             const double ti = tau(i);
             const double av = (ti - xi) + icc;
@@ -544,56 +554,60 @@ __device__ __forceinline__ void solve_point(P T, P G, P H, const Summ& S, const 
         }
     };
     if (!S.pmc || aw_path) {
-        eval_range(0, ntau, 0, 0); // exhaustive (single-point path mode, or summaries unavailable)
+        eval_range(0, ntau); // exhaustive (single-point path mode, or summaries unavailable)
     } else {
-        // Branch and bound over τ̄ blocks — the same maximum, far fewer evaluations.
-        // Every argument sequence is nondecreasing in i, so the range check of the
-        // last τ̄ covers the whole path.
+        // Branch and bound over a 256/64/8 hierarchy of τ̄ ranges — the same maximum,
+        // far fewer evaluations.  Every argument sequence is nondecreasing in i, so the
+        // range check of the last τ̄ covers the whole path.
         const double al = (tau(ntau - 1) - xi) + icc, bl = (tau(ntau - 1) - xi) + occ;
         if (!((al > 0 ? al : 0.0) <= thi) || !((bl > 0 ? bl : 0.0) <= thi)) {
             flag |= trunc ? SBR_ENGINE_TRUNC : SBR_OOB;
         } else {
-            const int nblk = (ntau + 63) >> 6;
-            auto xa_of = [&](int i) { const double v = (tau(i) - xi) + icc; return v > 0 ? v : 0.0; };
-            auto xb_of = [&](int i) { const double v = (tau(i) - xi) + occ; return v > 0 ? v : 0.0; };
-            // Upper bound of AW_cum over τ̄ indices [i0, i1] given ja = bracket of a(τ̄_i0)
-            // and jb = bracket of b(τ̄_i1): AW_OUT ≤ max G over knots ≤ jb+1, AW_IN ≥ min G
-            // over knots ≥ ja (8-knot prefix-max / suffix-min tables), plus a rounding
-            // margin far above the ≈2e-15 the exact path can add.
-            auto ub_of = [&](int i0, int ja, int jb) -> double {
+            // Upper bound of AW_cum over τ̄ indices [i0, i1]: AW_OUT ≤ max G over knots
+            // ≤ bracket(b(τ̄_i1)) + 1, AW_IN ≥ min G over knots ≥ bracket(a(τ̄_i0)) (8-knot
+            // prefix-max / suffix-min tables), plus a rounding margin far above the
+            // ≈2e-15 the exact path can add.
+            auto ub_rng = [&](int i0, int i1) -> double {
+                const int ja = brk_a(i0), jb = brk_b(i1);
                 const double hi = S.pmc[(jb + 1 < n - 1 ? jb + 1 : n - 1) >> 3];
                 const double lo = S.smc[(ja < n - 2 ? ja : n - 2) >> 3];
                 const double ub_out = hi > 0.0 ? hi : 0.0;
                 const double lb_in = ((tau(i0) - xi) + icc) >= 0 ? lo : (lo < 0.0 ? lo : 0.0);
                 return ((ub_out - lb_in) + G0) + 1e-14;
             };
-            // pass 1: 64-wide bounds; the most promising block is evaluated first
-            // (brackets are searched from the previous block's plus the block width:
-            // a(τ̄_i) and b(τ̄_i) are τ̄_i shifted by constants, so they advance with i)
-            int ja = 0, jb = 0, best = 0, bja = 0, bjb = 0;
-            double bub = -INFINITY;
-            for (int bk = 0; bk < nblk; bk++) {
-                const int i0 = bk << 6, i1 = (i0 + 64 < ntau ? i0 + 64 : ntau) - 1;
-                ja = ssl_near(T, n, bk ? ja + 64 : 0, xa_of(i0));
-                jb = ssl_near(T, n, bk ? jb + 64 : 0, xb_of(i1));
-                const double ub = ub_of(i0, ja, jb);
-                if (!(ub <= bub)) { bub = ub; best = bk; bja = ja; bjb = jb; }
+            auto end_of = [&](int i0, int w) { return i0 + w < ntau ? i0 + w : ntau; };
+            // pass 1: descend to the most promising 8-wide range and evaluate it
+            int bs = 0;
+            double bu = -INFINITY;
+            for (int i0 = 0; i0 < ntau; i0 += 256) {
+                const double ub = ub_rng(i0, end_of(i0, 256) - 1);
+                if (!(ub <= bu)) { bu = ub; bs = i0; }
             }
-            eval_range(best << 6, (best << 6) + 64 < ntau ? (best << 6) + 64 : ntau, bja, bjb - 63);
-            // pass 2: every other block whose bound beats the running max is refined
-            // into 8-wide sub-blocks with their own bounds
-            for (int bk = 0; bk < nblk && !flag && mx == mx; bk++) {
-                const int i0 = bk << 6, ie = i0 + 64 < ntau ? i0 + 64 : ntau;
-                ja = ssl_near(T, n, bk ? ja + 64 : 0, xa_of(i0));
-                jb = ssl_near(T, n, bk ? jb + 64 : 0, xb_of(ie - 1));
-                if (bk == best || ub_of(i0, ja, jb) <= mx) continue;
-                int sa = ja, se = jb - (ie - 1 - i0); // predictions for the first sub-block
-                for (int s0 = i0; s0 < ie && mx == mx; s0 += 8) {
-                    const int s1 = (s0 + 8 < ie ? s0 + 8 : ie) - 1;
-                    sa = ssl_near(T, n, s0 == i0 ? sa : sa + 8, xa_of(s0));
-                    const int hb = s0 == i0 ? se : se + 1; // prediction for b(τ̄_s0)
-                    se = ssl_near(T, n, se + (s0 == i0 ? s1 - s0 : 8), xb_of(s1));
-                    if (!(ub_of(s0, sa, se) <= mx)) eval_range(s0, s1 + 1, sa, hb);
+            int bb = bs;
+            bu = -INFINITY;
+            for (int i0 = bs; i0 < end_of(bs, 256); i0 += 64) {
+                const double ub = ub_rng(i0, end_of(i0, 64) - 1);
+                if (!(ub <= bu)) { bu = ub; bb = i0; }
+            }
+            int b8 = bb;
+            bu = -INFINITY;
+            for (int i0 = bb; i0 < end_of(bb, 64); i0 += 8) {
+                const double ub = ub_rng(i0, end_of(i0, 8) - 1);
+                if (!(ub <= bu)) { bu = ub; b8 = i0; }
+            }
+            eval_range(b8, end_of(b8, 8));
+            // pass 2: every range whose bound beats the running max is refined
+            for (int s0 = 0; s0 < ntau && !flag && mx == mx; s0 += 256) {
+                const int se = end_of(s0, 256);
+                if (ub_rng(s0, se - 1) <= mx) continue;
+                for (int k0 = s0; k0 < se && !flag && mx == mx; k0 += 64) {
+                    const int ke = end_of(k0, 64);
+                    if (ub_rng(k0, ke - 1) <= mx) continue;
+                    for (int i0 = k0; i0 < ke && !flag && mx == mx; i0 += 8) {
+                        const int ie = end_of(i0, 8);
+                        if (i0 == b8 || ub_rng(i0, ie - 1) <= mx) continue;
+                        eval_range(i0, ie);
+                    }
                 }
             }
         }
@@ -731,7 +745,7 @@ hipError_t launch_learn_logistic(const double* beta, const double* eta, const do
     hipLaunchKernelGGL(learn_logistic_kernel, grid, dim3(64), 0, s, beta, eta, t_end, a, L);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(hazard_kernel, dim3(a.n_beta), dim3(HZ_BLOCK), (size_t)a.hz_cap * sizeof(double), s, beta,
+    hipLaunchKernelGGL(hazard_kernel, dim3(a.n_beta), dim3(HZ_BLOCK), 0, s, beta,
                        eta, a, L);
     return hipGetLastError();
 }

@@ -20,9 +20,13 @@ struct sbr_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     std::string err;
-    // learning workspace
-    size_t ws_beta = 0, ws_cap = 0;
-    sbr::LearnBufs L{};
+    // learning workspaces: slot 0 for single sweeps, slots 0/1 alternate in a
+    // pipelined batch (learning of batch k+1 overlaps the equilibrium of batch k)
+    size_t ws_beta[2] = {0, 0}, ws_cap[2] = {0, 0};
+    sbr::LearnBufs LW[2]{};
+    int last_slot = 0;
+    hipStream_t lstream = nullptr; // learning stream of pipelined batches (highest priority)
+    hipEvent_t ev_in = nullptr, ev_learned[2] = {nullptr, nullptr}, ev_eq[2] = {nullptr, nullptr};
     // hetero learning workspace
     size_t hs_col = 0, hs_cap = 0, hs_K = 0;
     sbr::HeteroBufs H{};
@@ -31,10 +35,15 @@ struct sbr_ctx {
     size_t stage_bytes = 0;
     int lds_cap = 0;
     int lds_smem = 0;
-    // kernel timing (HIP events on the launch stream), opt-in via sbr_timing_enable
+    // kernel timing (HIP event pairs on the launching stream), opt-in via sbr_timing_enable
     bool timing = false;
     std::vector<hipEvent_t> ev_pool;
     size_t ev_used = 0;
+    struct TRec {
+        int kind; // 0 learning (+ hazard), 1 equilibrium
+        hipEvent_t a, b;
+    };
+    std::vector<TRec> trec;
 };
 
 namespace {
@@ -56,34 +65,35 @@ int fail(sbr_ctx* c, int code, const char* what, hipError_t e = hipSuccess)
         if (_e != hipSuccess) return fail((ctx), (code), #expr, _e); \
     } while (0)
 
-void free_learn(sbr_ctx* c)
+void free_learn(sbr_ctx* c, int slot)
 {
-    void* ps[] = {c->L.t, c->L.G, c->L.hr, c->L.hrI, c->L.n_knots, c->L.n_tau, c->L.n_le, c->L.status,
-                  c->L.n_accept, c->L.n_reject};
+    sbr::LearnBufs& L = c->LW[slot];
+    void* ps[] = {L.t, L.G, L.hr, L.hrI, L.n_knots, L.n_tau, L.n_le, L.status, L.n_accept, L.n_reject};
     for (void* p : ps)
         if (p) (void)hipFree(p);
-    c->L = sbr::LearnBufs{};
-    c->ws_beta = c->ws_cap = 0;
+    L = sbr::LearnBufs{};
+    c->ws_beta[slot] = c->ws_cap[slot] = 0;
 }
 
-int ensure_learn(sbr_ctx* c, size_t n_beta, size_t cap)
+int ensure_learn(sbr_ctx* c, size_t n_beta, size_t cap, int slot = 0)
 {
-    if (n_beta <= c->ws_beta && cap == c->ws_cap) return SBR_OK;
-    free_learn(c);
+    if (n_beta <= c->ws_beta[slot] && cap == c->ws_cap[slot]) return SBR_OK;
+    free_learn(c, slot);
+    sbr::LearnBufs& L = c->LW[slot];
     const size_t slab = n_beta * cap * sizeof(double);
-    HIP_TRY(c, hipMalloc(&c->L.t, slab), SBR_ENOMEM);
-    HIP_TRY(c, hipMalloc(&c->L.G, slab), SBR_ENOMEM);
-    HIP_TRY(c, hipMalloc(&c->L.hr, slab), SBR_ENOMEM);
-    HIP_TRY(c, hipMalloc(&c->L.hrI, slab), SBR_ENOMEM);
-    HIP_TRY(c, hipMalloc(&c->L.n_knots, n_beta * 4), SBR_ENOMEM);
-    HIP_TRY(c, hipMalloc(&c->L.n_tau, n_beta * 4), SBR_ENOMEM);
-    HIP_TRY(c, hipMalloc(&c->L.n_le, n_beta * 4), SBR_ENOMEM);
-    HIP_TRY(c, hipMalloc(&c->L.status, n_beta * 4), SBR_ENOMEM);
-    HIP_TRY(c, hipMalloc(&c->L.n_accept, n_beta * 4), SBR_ENOMEM);
-    HIP_TRY(c, hipMalloc(&c->L.n_reject, n_beta * 4), SBR_ENOMEM);
-    c->L.cap = (int32_t)cap;
-    c->ws_beta = n_beta;
-    c->ws_cap = cap;
+    HIP_TRY(c, hipMalloc(&L.t, slab), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&L.G, slab), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&L.hr, slab), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&L.hrI, slab), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&L.n_knots, n_beta * 4), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&L.n_tau, n_beta * 4), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&L.n_le, n_beta * 4), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&L.status, n_beta * 4), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&L.n_accept, n_beta * 4), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&L.n_reject, n_beta * 4), SBR_ENOMEM);
+    L.cap = (int32_t)cap;
+    c->ws_beta[slot] = n_beta;
+    c->ws_cap[slot] = cap;
     return SBR_OK;
 }
 
@@ -149,15 +159,6 @@ sbr_opts resolve(const sbr_opts* o)
     return r;
 }
 
-// τ̄ entries the hazard kernel keeps in LDS (32 KiB: five hazard blocks share a
-// CU; the paper's grids need ~3k, longer columns fall back to HBM scratch)
-int32_t hz_cap(const sbr_ctx* c, const sbr_opts& o)
-{
-    (void)c;
-    const int cap = 4096;
-    return o.knot_capacity + 1 < cap ? o.knot_capacity + 1 : cap;
-}
-
 hipEvent_t next_event(sbr_ctx* c)
 {
     if (c->ev_used == c->ev_pool.size()) {
@@ -168,11 +169,33 @@ hipEvent_t next_event(sbr_ctx* c)
     return c->ev_pool[c->ev_used++];
 }
 
-void mark(sbr_ctx* c, hipStream_t s)
+hipEvent_t tstart(sbr_ctx* c, hipStream_t s)
 {
-    if (!c->timing) return;
+    if (!c->timing) return nullptr;
     hipEvent_t e = next_event(c);
     if (e) (void)hipEventRecord(e, s);
+    return e;
+}
+
+void tend(sbr_ctx* c, hipStream_t s, int kind, hipEvent_t a)
+{
+    if (!c->timing || !a) return;
+    hipEvent_t e = next_event(c);
+    if (!e) return;
+    (void)hipEventRecord(e, s);
+    c->trec.push_back({kind, a, e});
+}
+
+int launch_eq(sbr_ctx* c, hipStream_t s, const sbr::LearnBufs& L, const double* eta, const double* t_end,
+              const double* u, int64_t n_beta, int64_t n_u, double kappa, const sbr_opts& o,
+              const sbr::ResultSoA& out, double* aw_path)
+{
+    sbr::EqArgs ea{kappa, (int32_t)n_u, o.bisect_max_iters, c->lds_cap, aw_path, (o.flags & SBR_FLAG_EXHAUSTIVE) ? 1 : 0,
+                   (o.flags >> 8) & 7};
+    hipEvent_t t0 = tstart(c, s);
+    HIP_TRY(c, sbr::launch_equilibrium(L, eta, t_end, u, ea, out, (int)n_beta, s), SBR_EDEVICE);
+    tend(c, s, 1, t0);
+    return SBR_OK;
 }
 
 int run_baseline(sbr_ctx* c, hipStream_t s, const double* beta, const double* eta, const double* t_end, double x0,
@@ -181,15 +204,12 @@ int run_baseline(sbr_ctx* c, hipStream_t s, const double* beta, const double* et
 {
     int rc = ensure_learn(c, (size_t)n_beta, (size_t)o.knot_capacity);
     if (rc) return rc;
-    sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, p, lambda, o.ode_maxiters, (int32_t)n_beta, 1, hz_cap(c, o), 0};
-    mark(c, s);
-    HIP_TRY(c, sbr::launch_learn_logistic(beta, eta, t_end, la, c->L, s), SBR_EDEVICE);
-    mark(c, s);
-    sbr::EqArgs ea{kappa, (int32_t)n_u, o.bisect_max_iters, c->lds_cap, aw_path, (o.flags & SBR_FLAG_EXHAUSTIVE) ? 1 : 0,
-                    (o.flags >> 8) & 7};
-    HIP_TRY(c, sbr::launch_equilibrium(c->L, eta, t_end, u, ea, out, (int)n_beta, s), SBR_EDEVICE);
-    mark(c, s);
-    return SBR_OK;
+    c->last_slot = 0;
+    sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, p, lambda, o.ode_maxiters, (int32_t)n_beta, 1, 0};
+    hipEvent_t t0 = tstart(c, s);
+    HIP_TRY(c, sbr::launch_learn_logistic(beta, eta, t_end, la, c->LW[0], s), SBR_EDEVICE);
+    tend(c, s, 0, t0);
+    return launch_eq(c, s, c->LW[0], eta, t_end, u, n_beta, n_u, kappa, o, out, aw_path);
 }
 
 }  // namespace
@@ -237,8 +257,14 @@ int sbr_free(sbr_ctx* c)
     if (!c) return SBR_OK;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
-    free_learn(c);
+    if (c->lstream) (void)hipStreamSynchronize(c->lstream);
+    free_learn(c, 0);
+    free_learn(c, 1);
     free_hetero(c);
+    hipEvent_t evs[] = {c->ev_in, c->ev_learned[0], c->ev_learned[1], c->ev_eq[0], c->ev_eq[1]};
+    for (hipEvent_t e : evs)
+        if (e) (void)hipEventDestroy(e);
+    if (c->lstream) (void)hipStreamDestroy(c->lstream);
     if (c->stage) (void)hipFree(c->stage);
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(c->stream);
@@ -252,7 +278,8 @@ int sbr_sweep_baseline_dev(sbr_ctx* c, void* stream, const double* beta, const d
                            double x0, const double* u, int64_t n_beta, int64_t n_u, double p, double kappa,
                            double lambda, const sbr_opts* opts, sbr_result_soa* out)
 {
-    if (!c || !out) return SBR_EARG;
+    if (!c || !out || !out->xi || !out->tau_in_unc || !out->tau_out_unc || !out->aw_max || !out->tol || !out->status)
+        return SBR_EARG;
     if (n_beta <= 0 || n_u <= 0 || n_beta > (1 << 30) || n_u > (1 << 30)) return fail(c, SBR_EARG, "grid size");
     if (!scalars_valid(x0, p, kappa, lambda)) return fail(c, SBR_EARG, "ArgumentError: x0/p/kappa/lambda");
     if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
@@ -260,6 +287,62 @@ int sbr_sweep_baseline_dev(sbr_ctx* c, void* stream, const double* beta, const d
     sbr::ResultSoA r{out->xi, out->tau_in_unc, out->tau_out_unc, out->aw_max, out->tol, out->status, out->iters};
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     return run_baseline(c, s, beta, eta, t_end, x0, u, n_beta, n_u, p, kappa, lambda, o, r, nullptr);
+}
+
+int sbr_sweep_baseline_batch_dev(sbr_ctx* c, void* stream, int64_t n_batch, const double* beta, const double* eta,
+                                 const double* t_end, double x0, const double* u, int64_t n_beta, int64_t n_u,
+                                 double p, double kappa, double lambda, const sbr_opts* opts, sbr_result_soa* out)
+{
+    if (!c || !out || !beta || !eta || !t_end || !u) return SBR_EARG;
+    if (!out->xi || !out->tau_in_unc || !out->tau_out_unc || !out->aw_max || !out->tol || !out->status) return SBR_EARG;
+    if (n_batch <= 0 || n_beta <= 0 || n_u <= 0 || n_beta > (1 << 30) || n_u > (1 << 30))
+        return fail(c, SBR_EARG, "grid size");
+    if (!scalars_valid(x0, p, kappa, lambda)) return fail(c, SBR_EARG, "ArgumentError: x0/p/kappa/lambda");
+    if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
+    sbr_opts o = resolve(opts);
+    for (int k = 0; k < 2 && k < n_batch; k++) {
+        int rc = ensure_learn(c, (size_t)n_beta, (size_t)o.knot_capacity, k);
+        if (rc) return rc;
+    }
+    if (!c->lstream) {
+        int lo = 0, hi = 0;
+        (void)hipDeviceGetStreamPriorityRange(&lo, &hi); // hi = greatest priority
+        HIP_TRY(c, hipStreamCreateWithPriority(&c->lstream, hipStreamNonBlocking, hi), SBR_EDEVICE);
+        hipEvent_t* evs[] = {&c->ev_in, &c->ev_learned[0], &c->ev_learned[1], &c->ev_eq[0], &c->ev_eq[1]};
+        for (hipEvent_t* e : evs) HIP_TRY(c, hipEventCreateWithFlags(e, hipEventDisableTiming), SBR_EDEVICE);
+    }
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    hipStream_t ls = c->lstream;
+    const size_t np = (size_t)n_beta * (size_t)n_u;
+    sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, p, lambda, o.ode_maxiters, (int32_t)n_beta, 1, 0};
+    // inputs are ready once prior work on the caller's stream is
+    HIP_TRY(c, hipEventRecord(c->ev_in, s), SBR_EDEVICE);
+    HIP_TRY(c, hipStreamWaitEvent(ls, c->ev_in, 0), SBR_EDEVICE);
+    for (int64_t k = 0; k < n_batch; k++) {
+        const int slot = (int)(k & 1);
+        const double* bk = beta + k * n_beta;
+        const double* ek = eta + k * n_beta;
+        const double* tk = t_end + k * n_beta;
+        // the slot's previous reader (equilibrium of batch k-2) must be done
+        if (k >= 2) HIP_TRY(c, hipStreamWaitEvent(ls, c->ev_eq[slot], 0), SBR_EDEVICE);
+        hipEvent_t t0 = tstart(c, ls);
+        HIP_TRY(c, sbr::launch_learn_logistic(bk, ek, tk, la, c->LW[slot], ls), SBR_EDEVICE);
+        tend(c, ls, 0, t0);
+        HIP_TRY(c, hipEventRecord(c->ev_learned[slot], ls), SBR_EDEVICE);
+        HIP_TRY(c, hipStreamWaitEvent(s, c->ev_learned[slot], 0), SBR_EDEVICE);
+        sbr::ResultSoA r{out->xi ? out->xi + k * np : nullptr,
+                         out->tau_in_unc ? out->tau_in_unc + k * np : nullptr,
+                         out->tau_out_unc ? out->tau_out_unc + k * np : nullptr,
+                         out->aw_max ? out->aw_max + k * np : nullptr,
+                         out->tol ? out->tol + k * np : nullptr,
+                         out->status ? out->status + k * np : nullptr,
+                         out->iters ? out->iters + k * np : nullptr};
+        int rc = launch_eq(c, s, c->LW[slot], ek, tk, u, n_beta, n_u, kappa, o, r, nullptr);
+        if (rc) return rc;
+        HIP_TRY(c, hipEventRecord(c->ev_eq[slot], s), SBR_EDEVICE);
+        c->last_slot = slot;
+    }
+    return SBR_OK;
 }
 
 int sbr_sweep_baseline(sbr_ctx* c, const double* beta, const double* eta, const double* t_end, double x0,
@@ -326,15 +409,15 @@ int sbr_learn_baseline(sbr_ctx* c, const double* beta, const double* eta, const 
     HIP_TRY(c, hipMemcpyAsync(dbeta, beta, n_beta * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
     HIP_TRY(c, hipMemcpyAsync(deta, eta, n_beta * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
     HIP_TRY(c, hipMemcpyAsync(dtend, t_end, n_beta * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
-    sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, 0.5, 1.0, o.ode_maxiters, (int32_t)n_beta, stop_after_eta, hz_cap(c, o), 0};
-    HIP_TRY(c, sbr::launch_learn_logistic(dbeta, deta, dtend, la, c->L, s), SBR_EDEVICE);
+    sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, 0.5, 1.0, o.ode_maxiters, (int32_t)n_beta, stop_after_eta, 0};
+    HIP_TRY(c, sbr::launch_learn_logistic(dbeta, deta, dtend, la, c->LW[0], s), SBR_EDEVICE);
     const size_t w = (size_t)o.knot_capacity;
     if (t_out)
-        HIP_TRY(c, hipMemcpy2DAsync(t_out, cap * 8, c->L.t, w * 8, w * 8, n_beta, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        HIP_TRY(c, hipMemcpy2DAsync(t_out, cap * 8, c->LW[0].t, w * 8, w * 8, n_beta, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
     if (G_out)
-        HIP_TRY(c, hipMemcpy2DAsync(G_out, cap * 8, c->L.G, w * 8, w * 8, n_beta, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
-    if (n_knots) HIP_TRY(c, hipMemcpyAsync(n_knots, c->L.n_knots, n_beta * 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
-    if (status) HIP_TRY(c, hipMemcpyAsync(status, c->L.status, n_beta * 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        HIP_TRY(c, hipMemcpy2DAsync(G_out, cap * 8, c->LW[0].G, w * 8, w * 8, n_beta, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+    if (n_knots) HIP_TRY(c, hipMemcpyAsync(n_knots, c->LW[0].n_knots, n_beta * 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+    if (status) HIP_TRY(c, hipMemcpyAsync(status, c->LW[0].status, n_beta * 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
     HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
     return SBR_OK;
 }
@@ -364,17 +447,17 @@ int sbr_solve_point_paths(sbr_ctx* c, double beta, double eta, double t_end, dou
     HIP_TRY(c, hipMemcpyAsync(res, dres, 40, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
     HIP_TRY(c, hipMemcpyAsync(status, dst, 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
     int32_t nt = 0, nle = 0, nk = 0;
-    HIP_TRY(c, hipMemcpyAsync(&nt, c->L.n_tau, 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
-    HIP_TRY(c, hipMemcpyAsync(&nle, c->L.n_le, 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
-    HIP_TRY(c, hipMemcpyAsync(&nk, c->L.n_knots, 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+    HIP_TRY(c, hipMemcpyAsync(&nt, c->LW[0].n_tau, 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+    HIP_TRY(c, hipMemcpyAsync(&nle, c->LW[0].n_le, 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+    HIP_TRY(c, hipMemcpyAsync(&nk, c->LW[0].n_knots, 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
     HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
     if (n_tau) *n_tau = nt;
     if (nt > cap) return fail(c, SBR_EARG, "path capacity too small");
     if (tau) {
-        HIP_TRY(c, hipMemcpy(tau, c->L.t, (size_t)nle * 8, hipMemcpyDeviceToHost), SBR_EDEVICE);
+        HIP_TRY(c, hipMemcpy(tau, c->LW[0].t, (size_t)nle * 8, hipMemcpyDeviceToHost), SBR_EDEVICE);
         if (nt > nle) tau[nle] = eta;
     }
-    if (hr) HIP_TRY(c, hipMemcpy(hr, c->L.hr, (size_t)nt * 8, hipMemcpyDeviceToHost), SBR_EDEVICE);
+    if (hr) HIP_TRY(c, hipMemcpy(hr, c->LW[0].hr, (size_t)nt * 8, hipMemcpyDeviceToHost), SBR_EDEVICE);
     if (aw_cum) {
         if (*status & SBR_RUN) HIP_TRY(c, hipMemcpy(aw_cum, dpath, (size_t)nt * 8, hipMemcpyDeviceToHost), SBR_EDEVICE);
         else for (int i = 0; i < nt; i++) aw_cum[i] = NAN;
@@ -388,6 +471,7 @@ int sbr_timing_enable(sbr_ctx* c, int on)
     if (!c) return SBR_EARG;
     c->timing = on != 0;
     c->ev_used = 0;
+    c->trec.clear();
     return SBR_OK;
 }
 
@@ -398,29 +482,30 @@ int sbr_timing_read(sbr_ctx* c, void* stream, double* learn_ms, double* eq_ms, i
     HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
     double a = 0.0, b = 0.0;
     int32_t n = 0;
-    for (size_t i = 0; i + 3 <= c->ev_used; i += 3) {
-        float t1 = 0.f, t2 = 0.f;
-        HIP_TRY(c, hipEventElapsedTime(&t1, c->ev_pool[i], c->ev_pool[i + 1]), SBR_EDEVICE);
-        HIP_TRY(c, hipEventElapsedTime(&t2, c->ev_pool[i + 1], c->ev_pool[i + 2]), SBR_EDEVICE);
-        a += t1;
-        b += t2;
-        n++;
+    if (c->lstream) HIP_TRY(c, hipStreamSynchronize(c->lstream), SBR_EDEVICE);
+    for (const auto& r : c->trec) {
+        float t = 0.f;
+        HIP_TRY(c, hipEventElapsedTime(&t, r.a, r.b), SBR_EDEVICE);
+        if (r.kind == 0) a += t;
+        else { b += t; n++; }
     }
     if (learn_ms) *learn_ms = a;
     if (eq_ms) *eq_ms = b;
     if (n_calls) *n_calls = n;
     c->ev_used = 0;
+    c->trec.clear();
     return SBR_OK;
 }
 
 int sbr_learn_stats(sbr_ctx* c, int64_t n_beta, int32_t* n_knots, int32_t* n_tau, int32_t* n_accept,
                     int32_t* n_reject, uint32_t* status)
 {
-    if (!c || n_beta <= 0 || (size_t)n_beta > c->ws_beta) return SBR_EARG;
+    if (!c || n_beta <= 0 || (size_t)n_beta > c->ws_beta[c->last_slot]) return SBR_EARG;
     if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
     HIP_TRY(c, hipDeviceSynchronize(), SBR_EDEVICE);
-    struct { int32_t* h; void* d; } cp[] = {{n_knots, c->L.n_knots}, {n_tau, c->L.n_tau}, {n_accept, c->L.n_accept},
-                                           {n_reject, c->L.n_reject}, {(int32_t*)status, c->L.status}};
+    const sbr::LearnBufs& L = c->LW[c->last_slot];
+    struct { int32_t* h; void* d; } cp[] = {{n_knots, L.n_knots}, {n_tau, L.n_tau}, {n_accept, L.n_accept},
+                                           {n_reject, L.n_reject}, {(int32_t*)status, L.status}};
     for (auto& x : cp)
         if (x.h) HIP_TRY(c, hipMemcpy(x.h, x.d, (size_t)n_beta * 4, hipMemcpyDeviceToHost), SBR_EDEVICE);
     return SBR_OK;
@@ -440,14 +525,15 @@ int sbr_sweep_hetero_dev(sbr_ctx* c, void* stream, int32_t K, const double* beta
     int rc = ensure_hetero(c, (size_t)n_col, (size_t)o.knot_capacity, (size_t)K);
     if (rc) return rc;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-    sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, p, lambda, o.ode_maxiters, (int32_t)n_col, 0, 0, 0};
+    sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, p, lambda, o.ode_maxiters, (int32_t)n_col, 0, 0};
     sbr::HeteroEqArgs ea{kappa, 1e-12, (int32_t)n_u, o.hetero_max_iters, c->lds_cap * 3};
     sbr::ResultSoA r{out->xi, nullptr, nullptr, out->aw_max, out->tol, out->status, out->iters};
-    mark(c, s);
+    hipEvent_t t0 = tstart(c, s);
     HIP_TRY(c, sbr::launch_hetero(K, betas, dist, eta, t_end, u, la, ea, c->H, r, tau_in, tau_out, s, 0), SBR_EDEVICE);
-    mark(c, s);
+    tend(c, s, 0, t0);
+    t0 = tstart(c, s);
     HIP_TRY(c, sbr::launch_hetero(K, betas, dist, eta, t_end, u, la, ea, c->H, r, tau_in, tau_out, s, 1), SBR_EDEVICE);
-    mark(c, s);
+    tend(c, s, 1, t0);
     return SBR_OK;
 }
 

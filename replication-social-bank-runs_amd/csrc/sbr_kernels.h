@@ -26,7 +26,6 @@ struct LearnArgs {
     int64_t maxiters;
     int32_t n_beta;
     int32_t stop_after_eta;
-    int32_t hz_cap;     // τ̄ entries the hazard kernel can hold in LDS
     int32_t pad;
 };
 

@@ -18,7 +18,7 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from . import _lib
-from ._lib import SBRNativeError, check
+from ._lib import ArgumentError, SBRNativeError, check
 from .grids import BaselineGrid
 from .model import EconomicParameters, LearningParameters
 
@@ -91,6 +91,24 @@ class Engine:
                                             x0, u.data_ptr(), nb, nu, p, kappa, lam, ctypes.byref(opts),
                                             ctypes.byref(soa))
         check(rc, self._ctx, "sbr_sweep_baseline_dev")
+
+    def sweep_baseline_batch_dev(self, beta, eta, t_end, u, p, kappa, lam, x0, out: dict, stream: int | None = None,
+                                 max_iters: int = 100, knot_capacity: int = 65536, flags: int = 0):
+        """Pipelined sweep of several grids on torch tensors (float64 cuda):
+        ``beta``/``eta``/``t_end`` are [n_batch, n_beta]; every ``out`` tensor
+        is [n_batch, n_beta * n_u] (see sbr_sweep_baseline_batch_dev)."""
+        nbat, nb = beta.shape
+        nu = u.numel()
+        if tuple(eta.shape) != (nbat, nb) or tuple(t_end.shape) != (nbat, nb):
+            raise ArgumentError("eta and t_end must be [n_batch, n_beta] like beta")
+        soa = _lib.ResultSoA(*[(out[k].data_ptr() if out.get(k) is not None else None)
+                               for k in (*RESULT_FIELDS, "status", "iters")])
+        opts = _lib.default_opts(early_exit_nan_run=0, bisect_max_iters=max_iters, knot_capacity=knot_capacity,
+                                 flags=flags)
+        rc = self._L.sbr_sweep_baseline_batch_dev(self._ctx, stream, nbat, beta.data_ptr(), eta.data_ptr(),
+                                                  t_end.data_ptr(), x0, u.data_ptr(), nb, nu, p, kappa, lam,
+                                                  ctypes.byref(opts), ctypes.byref(soa))
+        check(rc, self._ctx, "sbr_sweep_baseline_batch_dev")
 
     def learn_baseline(self, beta, eta, t_end, x0=1e-4, stop_after_eta=False, cap=65536):
         beta = np.ascontiguousarray(beta, np.float64)

@@ -171,3 +171,33 @@ def test_device_info(engine):
     info = engine.device_info()
     assert info["cu_count"] == 256
     assert info["lds_knot_capacity"] >= 3400  # every config-3 column staged in LDS
+
+
+def test_pipelined_batches_equal_single_sweeps(engine):
+    """sbr_sweep_baseline_batch_dev (learning of batch k+1 overlapping the
+    equilibrium of batch k on two streams, alternating workspaces) returns for
+    every batch exactly what a single sweep of that grid returns."""
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda", 0)
+    base = sbr.fig5_grid(384)
+    betas = np.stack([base.beta, base.beta[::-1], base.beta * 0.5, base.beta])
+    etas = np.stack([np.full(384, 15.0), np.full(384, 10.0), np.full(384, 15.0), np.full(384, 7.5)])
+    tends = np.stack([np.full(384, 30.0), np.full(384, 30.0), np.full(384, 20.0), np.full(384, 30.0)])
+    nbat, nb, nu = betas.shape[0], betas.shape[1], len(base.u)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    out = {f: torch.empty(nbat, nb * nu, dtype=torch.float64, device=dev) for f in FIELDS}
+    out["status"] = torch.empty(nbat, nb * nu, dtype=torch.int32, device=dev)
+    out["iters"] = torch.empty(nbat, nb * nu, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    engine.sweep_baseline_batch_dev(t(betas), t(etas), t(tends), t(base.u), base.p, base.kappa, base.lam, base.x0,
+                                    out, stream=stream)
+    torch.cuda.synchronize(dev)
+    for k in range(nbat):
+        g = sbr.BaselineGrid(betas[k], base.u, etas[k], tends[k], x0=base.x0, p=base.p, kappa=base.kappa,
+                             lam=base.lam)
+        ref = engine.sweep_baseline(g)
+        for f in FIELDS:
+            assert_bitwise(out[f][k].cpu().numpy().reshape(nb, nu), ref[f], f"batch {k} {f}")
+        st = out["status"][k].cpu().numpy().view(np.uint32).reshape(nb, nu)
+        assert np.array_equal(st, ref["status"])
+        assert np.array_equal(out["iters"][k].cpu().numpy().reshape(nb, nu), ref["iters"])
