@@ -43,7 +43,7 @@ typedef struct sbr_ctx sbr_ctx;
 typedef struct {
     double ode_reltol;          /* learning.jl:43 reltol = eps() */
     double ode_abstol;          /* learning.jl:43 abstol = eps() */
-    int64_t ode_maxiters;       /* DiffEq default maxiters = 1e5 */
+    int64_t ode_maxiters;       /* OrdinaryDiffEq default maxiters = 1e6 (SBR_DEFAULT_ODE_MAXITERS) */
     int32_t bisect_max_iters;   /* solver.jl:309 max_iters = 100 */
     int32_t early_exit_nan_run; /* 1_baseline.jl:147,221: 5; 0 disables */
     int32_t knot_capacity;      /* engine limit on stored knots per β (0 = default 65536) */
@@ -73,7 +73,7 @@ typedef struct {
     int32_t* iters;      /* bisection iterations (may be NULL)  */
 } sbr_result_soa;
 
-/* Fills *o with the reference defaults (eps() tolerances, 1e5, 100, 5, 65536, 500). */
+/* Fills *o with the reference defaults (eps() tolerances, 1e6, 100, 5, 65536, 500). */
 void sbr_default_opts(sbr_opts* o);
 
 /* Creates a context on HIP device `device` (the caller's rank-local GPU). */

@@ -22,12 +22,16 @@
 #define SBR_HETERO_INVALID      0x0040u /* is_valid_equilibrium_hetero false (hetero :245)     */
 #define SBR_OOB                 0x0080u /* reference would raise BoundsError                   */
 #define SBR_SKIPPED_EARLY_EXIT  0x0100u /* 5-consecutive-NaN rule (1_baseline.jl:236-244)      */
-#define SBR_ODE_MAXITERS        0x0200u /* integrator hit maxiters (DiffEq default 1e5)        */
+#define SBR_ODE_MAXITERS        0x0200u /* integrator hit maxiters (default 1e6, see below)    */
 #define SBR_ARG_INVALID         0x0400u /* parameter validation failed (model.jl:31-35,71-76)  */
 #define SBR_STIFF_SWITCH        0x0800u /* AutoSwitch would have moved to Rosenbrock23         */
 #define SBR_SOCIAL_NOT_CONVERGED 0x1000u /* fixed point hit max_iter / stopped (social :390)   */
 #define SBR_KNOT_OVERFLOW       0x2000u /* engine knot capacity exceeded (engine limit)        */
 #define SBR_ODE_FAILED          0x4000u /* non-finite step size / state                        */
 #define SBR_ENGINE_TRUNC        0x8000u /* engine bug: lookup past a truncated knot grid       */
+
+/* OrdinaryDiffEqCore __init: maxiters = anyadaptive(alg) ? 1000000 : typemax(Int).
+ * Every loop iteration (accepted or rejected step) counts. */
+#define SBR_DEFAULT_ODE_MAXITERS 1000000
 
 #endif /* SBR_STATUS_H */

@@ -61,7 +61,7 @@ def _ptr(a: np.ndarray | None):
 EPS = float(np.finfo(np.float64).eps)
 
 
-def learn_logistic(beta, t_end, x0=1e-4, t0=0.0, rtol=EPS, atol=EPS, maxiters=100_000, cap=1 << 16):
+def learn_logistic(beta, t_end, x0=1e-4, t0=0.0, rtol=EPS, atol=EPS, maxiters=1_000_000, cap=1 << 16):
     t = np.empty(cap)
     G = np.empty(cap)
     stats = np.zeros(4, np.int64)
@@ -182,3 +182,60 @@ def sweep_hetero(betas, dist, eta, t_end, u, p, kappa, lam, x0=1e-4, max_iters=5
     out["tau_out_unc"] = o["tau_out_unc"].reshape(n_col, nu, K)
     out["n_knots"] = nk
     return out
+
+
+def _social_sigs(L):
+    L.sbro_sweep_social.restype = ctypes.c_int
+    L.sbro_sweep_social.argtypes = ([_P, _P, _D, _P, _I64, _I64, _D, _D, _D, _P, _I32, _D, _I32, _I32, _I32]
+                                    + [_P] * 9)
+
+
+def sweep_social(beta, eta, u, p, kappa, lam, cmp, x0=1e-4, tol=1e-4, max_iter=500, bisect_max_iters=100,
+                 nthreads=0, stats=False):
+    """solve_equilibrium_social_learning (social_learning_solver.jl:63-263) over β columns × u.
+    cmp: [n_beta, n_cmp] comparison grids (range(0, η_b, length=1000), :103)."""
+    L = lib()
+    _social_sigs(L)
+    beta = np.ascontiguousarray(np.atleast_1d(beta), np.float64)
+    nb = len(beta)
+    eta = np.ascontiguousarray(np.broadcast_to(eta, (nb,)), np.float64)
+    u = np.ascontiguousarray(np.atleast_1d(u), np.float64)
+    nu = len(u)
+    cmp = np.ascontiguousarray(np.broadcast_to(np.atleast_2d(cmp), (nb, np.atleast_2d(cmp).shape[1])), np.float64)
+    o = {k: np.empty(nb * nu) for k in ("xi", "tau_in_unc", "tau_out_unc", "aw_max", "tol")}
+    o["status"] = np.empty(nb * nu, np.uint32)
+    o["iters"] = np.empty(nb * nu, np.int32)
+    o["fp_iters"] = np.empty(nb * nu, np.int32)
+    st = np.zeros(nb * nu * 4, np.int64) if stats else None
+    rc = L.sbro_sweep_social(_ptr(beta), _ptr(eta), x0, _ptr(u), nb, nu, p, kappa, lam, _ptr(cmp), cmp.shape[1], tol,
+                             max_iter, bisect_max_iters, nthreads, _ptr(o["xi"]), _ptr(o["tau_in_unc"]),
+                             _ptr(o["tau_out_unc"]), _ptr(o["aw_max"]), _ptr(o["tol"]), _ptr(o["status"]),
+                             _ptr(o["iters"]), _ptr(o["fp_iters"]), _ptr(st))
+    if rc != 0:
+        raise RuntimeError("oracle social sweep failed")
+    out = {k: v.reshape(nb, nu) for k, v in o.items()}
+    if stats:
+        s = st.reshape(nb, nu, 4)
+        out.update(n_knots=s[..., 0], n_accept=s[..., 1], n_reject=s[..., 2])
+    return out
+
+
+def social_point(beta, eta, u, p, kappa, lam, cmp, x0=1e-4, tol=1e-4, max_iter=500, cap=1 << 18):
+    """One solve_equilibrium_social_learning point with the last iterate's
+    learning knots (t, G) and HR grid τ̄ (to rebuild the plotted AW paths)."""
+    L = lib()
+    L.sbro_social_point.restype = _I64
+    L.sbro_social_point.argtypes = [_D, _D, _D, _D, _D, _D, _D, _P, _I32, _D, _I32, _P, _P, _P, _P, _P, _P, _I64, _P]
+    cmp = np.ascontiguousarray(cmp, np.float64)
+    res = np.zeros(5)
+    st = np.zeros(1, np.uint32)
+    fi = np.zeros(1, np.int32)
+    t, G, tau = np.empty(cap), np.empty(cap), np.empty(cap)
+    ntau = np.zeros(1, np.int64)
+    n = L.sbro_social_point(beta, eta, x0, u, p, kappa, lam, _ptr(cmp), len(cmp), tol, max_iter, _ptr(res), _ptr(st),
+                            _ptr(fi), _ptr(t), _ptr(G), _ptr(tau), cap, _ptr(ntau))
+    if n < 0:
+        raise RuntimeError(f"oracle social path buffer too small ({-n} needed)")
+    k = int(ntau[0])
+    return dict(xi=res[0], tau_in_unc=res[1], tau_out_unc=res[2], aw_max=res[3], tol=res[4], status=int(st[0]),
+                fp_iters=int(fi[0]), t=t[:n].copy(), G=G[:n].copy(), hr_tau=tau[:k].copy())

@@ -47,6 +47,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <stdio.h>
 #ifdef _OPENMP
 #include <omp.h>
 #endif
@@ -577,7 +578,7 @@ int sbro_sweep_baseline(const double* beta, const double* eta, const double* t_e
         double x0v = x0;
         double bb = beta[b];
         if (tsit5_solve(rhs_logistic, &bb, 1, 0.0, t_end[b], &x0v, 2.220446049250313e-16, 2.220446049250313e-16,
-                        100000, &kn, &st)) { err |= 1; continue; }
+                        SBR_DEFAULT_ODE_MAXITERS, &kn, &st)) { err |= 1; continue; }
         if (nknots) nknots[b] = kn.n;
         int64_t n = kn.n;
         double* g = (double*)malloc((size_t)n * sizeof(double));
@@ -660,7 +661,7 @@ int64_t sbro_learn_hetero(const double* betas, const double* dist, int32_t K, do
     for (int k = 0; k < K; k++) x0v[k] = x0;
     hetero_ctx hc = {K, betas, dist};
     const double e = 2.220446049250313e-16;
-    if (K < 1 || K > MAXK || tsit5_solve(rhs_hetero, &hc, K, 0.0, t1, x0v, e, e, 100000, &kn, &st)) {
+    if (K < 1 || K > MAXK || tsit5_solve(rhs_hetero, &hc, K, 0.0, t1, x0v, e, e, SBR_DEFAULT_ODE_MAXITERS, &kn, &st)) {
         knots_free(&kn);
         return -1;
     }
@@ -800,7 +801,7 @@ int sbro_sweep_hetero(int32_t K, const double* betas, const double* dist, const 
         for (int k = 0; k < K; k++) x0v[k] = x0;
         hetero_ctx hc = {K, bk, dist};
         const double e = 2.220446049250313e-16;
-        if (tsit5_solve(rhs_hetero, &hc, K, 0.0, t_end[c], x0v, e, e, 100000, &kn, &st)) { err |= 1; continue; }
+        if (tsit5_solve(rhs_hetero, &hc, K, 0.0, t_end[c], x0v, e, e, SBR_DEFAULT_ODE_MAXITERS, &kn, &st)) { err |= 1; continue; }
         int64_t n = kn.n;
         if (nknots) nknots[c] = n;
         /* compute_pdf_hetero: pdf_k = (1 − I_k) β_k ω at the knots */
@@ -860,4 +861,196 @@ int sbro_sweep_hetero(int32_t K, const double* betas, const double* dist, const 
         knots_free(&kn);
     }
     return err ? -1 : 0;
+}
+
+/* ======================================================================== */
+/* Social-learning extension: endogenous learning fixed point               */
+/* social_learning_dynamics.jl:58-114, social_learning_solver.jl:63-263     */
+/* ======================================================================== */
+typedef struct {
+    double beta;
+    const double* t; /* AW_old knots */
+    const double* v; /* AW_old values */
+    int64_t n;
+} social_ctx;
+
+/* ODE_social_learning!: du = (1 − I) β AW_old(t)  (social_learning_dynamics.jl:61-67);
+ * AW_old(t) is a Throw()-extrapolating LinearInterpolation (BoundsError -> oob) */
+static void rhs_social(void* ctx, double t, const double* x, double* dx, int* oob)
+{
+    const social_ctx* s = (const social_ctx*)ctx;
+    double aw = interp_s(s->t, s->v, 1, s->n, t, oob);
+    dx[0] = ((1.0 - x[0]) * s->beta) * aw;
+}
+
+/* One (β, u) point of solve_equilibrium_social_learning (social_learning_solver.jl:63-263).
+ * tspan = (0, η) (:79); cmp = range(0, η, length=n_cmp) supplied by the caller
+ * (:103).  Returns the last inner SolvedModel's fields (:262) like the
+ * reference; the fixed-point outcome goes to SBR_SOCIAL_NOT_CONVERGED and
+ * *fp_iters.  stats (may be NULL) = {ODE knots of the last iterate, Σ accepted
+ * steps, Σ rejected steps, max knots over iterates}. */
+typedef struct {
+    double *t, *G, *tau; /* last iterate's learning knots and HR grid (caller-allocated, cap each) */
+    int64_t cap, n, n_tau;
+} social_paths_t;
+
+static void social_point(double beta, double eta, double x0, double u, double p, double kappa, double lambda,
+                         const double* cmp, int32_t n_cmp, double tol, int32_t max_iter, int32_t bisect_max_iters,
+                         point_t* out, int32_t* fp_iters, int64_t* stats, social_paths_t* paths)
+{
+    const double e = 2.220446049250313e-16;
+    memset(out, 0, sizeof(*out));
+    out->xi = NAN; out->aw_max = NAN; out->tol = INFINITY; out->tin = out->tout = NAN;
+    *fp_iters = 0;
+    int64_t s_acc = 0, s_rej = 0, s_max = 0;
+    uint32_t ode_bits = 0;
+    /* initial guess: baseline SI learning on (0, η); AW_old = G on its knots (:89-94) */
+    knots_t old = {0};
+    ode_stats_t st;
+    double x0v = x0, bb = beta;
+    if (tsit5_solve(rhs_logistic, &bb, 1, 0.0, eta, &x0v, e, e, SBR_DEFAULT_ODE_MAXITERS, &old, &st)) {
+        out->status = SBR_ODE_FAILED; knots_free(&old); return;
+    }
+    ode_bits |= st.status & (SBR_ODE_MAXITERS | SBR_STIFF_SWITCH | SBR_ODE_FAILED | SBR_OOB);
+    double xi_new = 0.0;
+    int converged = 0, have_result = 0, stop_oob = 0;
+    int32_t iter;
+    for (iter = 1; iter <= max_iter; iter++) {
+        double xi_old = xi_new;
+        /* (a) learning from withdrawals: tspan (0, η), eps tolerances (:128-130) */
+        knots_t kn = {0};
+        social_ctx sc = {beta, old.t, old.x, old.n};
+        x0v = x0;
+        if (tsit5_solve(rhs_social, &sc, 1, 0.0, eta, &x0v, e, e, SBR_DEFAULT_ODE_MAXITERS, &kn, &st)) {
+            out->status = SBR_ODE_FAILED; knots_free(&kn); break;
+        }
+        s_acc += st.naccept; s_rej += st.nreject;
+        if (kn.n > s_max) s_max = kn.n;
+        if (getenv("SBRO_DEBUG"))
+            fprintf(stderr, "social it %d: knots %ld acc %ld rej %ld status %x\n", iter, (long)kn.n, (long)st.naccept,
+                    (long)st.nreject, st.status);
+        ode_bits |= st.status & (SBR_ODE_MAXITERS | SBR_STIFF_SWITCH | SBR_ODE_FAILED);
+        if (st.status & SBR_OOB) { stop_oob = 1; knots_free(&kn); break; }
+        int64_t n = kn.n;
+        /* compute_pdf_social_learning (:98-114): g = (1 − G) β AW_old(t) at the knots */
+        double* awo = (double*)malloc((size_t)n * sizeof(double));
+        double* g = (double*)malloc((size_t)n * sizeof(double));
+        int oob = 0;
+        for (int64_t i = 0; i < n; i++) {
+            awo[i] = interp_s(old.t, old.x, 1, old.n, kn.t[i], &oob);
+            g[i] = ((1.0 - kn.x[i]) * beta) * awo[i];
+        }
+        /* (b) baseline equilibrium on the new learning; t_end = tspan[2] = η (:139-143) */
+        hazard_t h;
+        hazard_rate(kn.t, g, n, p, lambda, eta, 0, &h);
+        h.oob |= oob;
+        point_t r;
+        double* aw = (double*)malloc((size_t)h.n * sizeof(double));
+        equilibrium_point(kn.t, kn.x, n, &h, eta, u, kappa, bisect_max_iters, &r, aw);
+        *out = r;
+        have_result = 1;
+        if (paths) {
+            paths->n = n; paths->n_tau = h.n;
+            if (n <= paths->cap && h.n <= paths->cap) {
+                memcpy(paths->t, kn.t, (size_t)n * sizeof(double));
+                memcpy(paths->G, kn.x, (size_t)n * sizeof(double));
+                memcpy(paths->tau, h.tau, (size_t)h.n * sizeof(double));
+            }
+        }
+        if (r.status & SBR_OOB) { stop_oob = 1; }
+        else {
+            int stop = 0;
+            if (!(r.status & SBR_RUN)) {
+                /* no equilibrium with this learning: ξ += η/500 (:150-156) */
+                xi_new = xi_old + eta / 500.0;
+                if (xi_new > eta) stop = 1;
+                else get_aw(xi_new, r.tin, r.tout, h.tau, h.n, kn.t, kn.x, n, aw, &oob);
+            } else {
+                xi_new = r.xi; /* aw already holds get_AW(ξ, …) on the HR grid */
+            }
+            if (oob) stop_oob = 1;
+            if (!stop && !stop_oob) {
+                /* ∞-norm on the comparison grid, before damping (:162-163, :195-196) */
+                double err = 0.0;
+                for (int32_t k = 0; k < n_cmp; k++) {
+                    double d = fabs(interp_s(h.tau, aw, 1, h.n, cmp[k], &oob) -
+                                    interp_s(old.t, old.x, 1, old.n, cmp[k], &oob));
+                    if (k == 0) err = d;
+                    else if (!(err != err || err > d)) err = d; /* generic_normInf: NaN sticks */
+                }
+                if (oob) stop_oob = 1;
+                else if (err < tol) {
+                    converged = 1;
+                } else {
+                    /* damping α = 1/2 on the new knots (:174-178, :218-222) */
+                    for (int64_t i = 0; i < n; i++) {
+                        double vn = interp_s(h.tau, aw, 1, h.n, kn.t[i], &oob);
+                        awo[i] = 0.5 * awo[i] + 0.5 * vn;
+                    }
+                    if (oob) stop_oob = 1;
+                    knots_free(&old);
+                    old.t = kn.t; old.x = awo; old.n = n; old.cap = kn.cap; old.K = 1;
+                    kn.t = NULL; awo = NULL;
+                }
+            }
+            if (stop) { free(aw); free(g); free(awo); hazard_free(&h); knots_free(&kn); break; }
+        }
+        free(aw); free(g); free(awo);
+        hazard_free(&h);
+        knots_free(&kn);
+        if (converged || stop_oob) break;
+    }
+    if (iter > max_iter) iter = max_iter;
+    *fp_iters = iter;
+    knots_free(&old);
+    if (stop_oob || !have_result) {
+        out->xi = NAN; out->aw_max = NAN; out->tol = INFINITY;
+        out->status = (out->status & ~(SBR_RUN | SBR_CONVERGED)) | SBR_OOB;
+    }
+    out->status |= ode_bits;
+    if (!converged) out->status |= SBR_SOCIAL_NOT_CONVERGED;
+    if (stats) { stats[0] = s_max; stats[1] = s_acc; stats[2] = s_rej; stats[3] = s_max; }
+}
+
+/* Social sweep over β columns × u; column b has η = eta[b]; cmp is
+ * [n_beta][n_cmp] (the caller's range(0, η_b, length = n_cmp)). */
+int sbro_sweep_social(const double* beta, const double* eta, double x0, const double* u, int64_t n_beta, int64_t n_u,
+                      double p, double kappa, double lambda, const double* cmp, int32_t n_cmp, double tol,
+                      int32_t max_iter, int32_t bisect_max_iters, int32_t nthreads, double* xi, double* tin,
+                      double* tout, double* aw_max, double* tl, uint32_t* status, int32_t* iters, int32_t* fp_iters,
+                      int64_t* stats)
+{
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 1)
+#endif
+    for (int64_t o = 0; o < n_beta * n_u; o++) {
+        int64_t b = o / n_u, j = o % n_u;
+        point_t r;
+        int32_t fi;
+        social_point(beta[b], eta[b], x0, u[j], p, kappa, lambda, cmp + b * n_cmp, n_cmp, tol, max_iter,
+                     bisect_max_iters, &r, &fi, stats ? stats + 4 * o : NULL, NULL);
+        xi[o] = r.xi; tin[o] = r.tin; tout[o] = r.tout; aw_max[o] = r.aw_max; tl[o] = r.tol;
+        status[o] = r.status;
+        if (iters) iters[o] = r.iters;
+        if (fp_iters) fp_iters[o] = fi;
+    }
+    return 0;
+}
+
+/* single social point with the last iterate's paths (learning knots t/G and the
+ * HR grid τ̄) for the figure checks; res = {ξ, τ̄_IN, τ̄_OUT, AW_max, tol}.
+ * Returns the knot count (negative -needed if cap is too small). */
+int64_t sbro_social_point(double beta, double eta, double x0, double u, double p, double kappa, double lambda,
+                          const double* cmp, int32_t n_cmp, double tol, int32_t max_iter, double* res,
+                          uint32_t* status, int32_t* fp_iters, double* t_out, double* G_out, double* tau_out,
+                          int64_t cap, int64_t* n_tau)
+{
+    social_paths_t sp = {t_out, G_out, tau_out, cap, 0, 0};
+    point_t r;
+    social_point(beta, eta, x0, u, p, kappa, lambda, cmp, n_cmp, tol, max_iter, 100, &r, fp_iters, NULL, &sp);
+    res[0] = r.xi; res[1] = r.tin; res[2] = r.tout; res[3] = r.aw_max; res[4] = r.tol;
+    *status = r.status;
+    *n_tau = sp.n_tau;
+    return (sp.n > cap || sp.n_tau > cap) ? -(sp.n > sp.n_tau ? sp.n : sp.n_tau) : sp.n;
 }

@@ -152,7 +152,7 @@ sbr_opts resolve(const sbr_opts* o)
     if (o) {
         r = *o;
         if (r.knot_capacity <= 0) r.knot_capacity = kDefaultCap;
-        if (r.ode_maxiters <= 0) r.ode_maxiters = 100000;
+        if (r.ode_maxiters <= 0) r.ode_maxiters = SBR_DEFAULT_ODE_MAXITERS;
         if (r.bisect_max_iters <= 0) r.bisect_max_iters = 100;
         if (r.hetero_max_iters <= 0) r.hetero_max_iters = 500;
     }
@@ -220,7 +220,7 @@ void sbr_default_opts(sbr_opts* o)
 {
     o->ode_reltol = 2.220446049250313e-16;
     o->ode_abstol = 2.220446049250313e-16;
-    o->ode_maxiters = 100000;
+    o->ode_maxiters = SBR_DEFAULT_ODE_MAXITERS;
     o->bisect_max_iters = 100;
     o->early_exit_nan_run = 5;
     o->knot_capacity = kDefaultCap;

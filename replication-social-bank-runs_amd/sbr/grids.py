@@ -9,22 +9,63 @@ in exact arithmetic — which is what ``fractions.Fraction`` gives here.
 from __future__ import annotations
 
 from fractions import Fraction
+from math import gcd
 
 import numpy as np
 
 __all__ = ["julia_range", "fig4_grid", "fig5_grid", "BaselineGrid"]
 
 
-def _rat(x) -> Fraction:
-    if isinstance(x, str):
-        return Fraction(x)
-    return Fraction(repr(float(x)))
+_MAXINTFLOAT32 = 16777216  # maxintfloat(narrow(Float64)) = maxintfloat(Float32)
+_MAXINTFLOAT64 = 9007199254740992
+
+
+def _julia_rat(x: float):
+    """Base.rat (range.jl): continued-fraction rational (a, b) with a/b == x in
+    Float64, bounded by maxintfloat(Float32); (c, d) of the last convergent
+    within the bound otherwise."""
+    y = float(x)
+    a = d = 1
+    b = c = 0
+    m = _MAXINTFLOAT32
+    while abs(y) <= m:
+        f = int(y)  # trunc
+        y -= f
+        a, c = f * a + c, a
+        b, d = f * b + d, b
+        if max(abs(a), abs(b)) > m:
+            return c, d
+        if float(a) / float(b) == x:
+            break
+        if y == 0.0:
+            break
+        y = 1.0 / y
+    return a, b
+
+
+def _endpoints(a, b):
+    """Exact rationals Julia's _linspace(start, stop, len) interpolates between:
+    the Base.rat representations when both pass its round-trip checks (short
+    decimals like 0.001 -> 1/1000, 100/3 for 33.333333333333336), else the
+    binary64 values themselves (the TwicePrecision fallback)."""
+    fa, fb = float(Fraction(a)) if isinstance(a, str) else float(a), float(Fraction(b)) if isinstance(b, str) else float(b)
+    an, ad = _julia_rat(fa)
+    bn, bd = _julia_rat(fb)
+    if ad != 0 and bd != 0:
+        den = ad * bd // gcd(ad, bd)
+        if den != 0 and abs(den * fa) <= _MAXINTFLOAT64 and abs(den * fb) <= _MAXINTFLOAT64:
+            sn, en = round(den * fa), round(den * fb)
+            if sn / den == fa and en / den == fb:
+                return Fraction(sn, den), Fraction(en, den)
+    return Fraction(fa), Fraction(fb)
 
 
 def julia_range(a, b, n: int) -> np.ndarray:
+    """range(a, b, length=n) for Float64 endpoints (elements correctly rounded
+    from Julia's exact rational endpoints; TwicePrecision agrees to the ulp)."""
     if n == 1:
-        return np.array([float(_rat(a))])
-    A, B = _rat(a), _rat(b)
+        return np.array([float(Fraction(a)) if isinstance(a, str) else float(a)])
+    A, B = _endpoints(a, b)
     step = (B - A) / (n - 1)
     return np.array([float(A + step * k) for k in range(n)], dtype=np.float64)
 

@@ -26,7 +26,7 @@ def test_library_exports_every_header_symbol():
 def test_default_opts_are_the_reference_defaults():
     o = _lib.default_opts()
     assert o.ode_reltol == np.finfo(np.float64).eps == o.ode_abstol  # learning.jl:43
-    assert o.ode_maxiters == 100000
+    assert o.ode_maxiters == 1_000_000
     assert o.bisect_max_iters == 100  # solver.jl:309
     assert o.early_exit_nan_run == 5  # 1_baseline.jl:147,221
 
