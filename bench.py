@@ -64,11 +64,18 @@ def parse():
     ap.add_argument("--phases", action="store_true",
                     help="also time the equilibrium kernel stopped after each stage (diagnostic flags)")
     ap.add_argument("--traffic", default=str(REPO / "profiles" / "traffic_latest.json"))
+    ap.add_argument("--workload", choices=("baseline", "social"), default="baseline",
+                    help="baseline: BASELINE config 3 (the metric); social: config 5 per-GPU share")
+    ap.add_argument("--social-cols", type=int, default=64, help="social: β columns per GPU (config 5: 512/8)")
+    ap.add_argument("--social-max-iter", type=int, default=500)
+    ap.add_argument("--social-prof", action="store_true", help="social: per-phase cycle breakdown (diagnostic)")
     return ap.parse_args()
 
 
 def main():
     a = parse()
+    if a.workload == "social":
+        return main_social(a)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -210,6 +217,108 @@ def main():
                                              {k: v[0] for k, v in out.items()}, stream, dev)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(beta_h, u_h, a.cpu_stride, p, kappa, lam, x0)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def main_social(a):
+    """BASELINE config 5: the social-learning fixed point (social_learning_solver.jl:63-263,
+    tol 1e-4, max_iter 500 as in scripts/4_social_learning.jl:55) on β = 1/range(0.01, 2, 512)
+    × u = range(0.001, 1, 512) with m_social's other parameters (η = 30/0.9 carried).  Weak
+    scaling: rank r owns β columns r, r+N, … of a (cols·N)-column grid; cols = 64 makes N = 8
+    exactly the 512×512 config.  One step = the whole fixed point for every point."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    ncol = a.social_cols * world
+    # the config-5 β axis (512 columns); fewer ranks take an evenly strided share of it
+    n_axis = max(512, ncol)
+    stride = n_axis // ncol if n_axis % ncol == 0 else 1
+    amt = sbr.julia_range("0.01", "2", n_axis)
+    cols = np.arange(rank, ncol, world) * stride
+    beta_h = 1.0 / amt[cols]
+    u_h = sbr.julia_range("0.001", "1", 512)
+    eta_v = 30.0 / 0.9
+    nb, nu = len(beta_h), len(u_h)
+    p, kappa, lam, x0, tol = 0.99, 0.25, 0.25, 1e-4, 1e-4
+    cmp_h = np.stack([sbr.julia_range(0.0, eta_v, 1000)] * nb)
+    beta = torch.from_numpy(beta_h).to(dev)
+    eta = torch.full((nb,), eta_v, dtype=torch.float64, device=dev)
+    u = torch.from_numpy(u_h).to(dev)
+    cmp = torch.from_numpy(cmp_h).to(dev)
+    out = {k: torch.empty(nb * nu, dtype=torch.float64, device=dev) for k in sbr.engine.RESULT_FIELDS}
+    out["status"] = torch.empty(nb * nu, dtype=torch.int32, device=dev)
+    out["iters"] = torch.empty(nb * nu, dtype=torch.int32, device=dev)
+    out["fp_iters"] = torch.empty(nb * nu, dtype=torch.int32, device=dev)
+    out["rk_steps"] = torch.empty(nb * nu, dtype=torch.int64, device=dev)
+    eng = sbr.Engine(local)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    gather = world > 1 and not a.no_gather
+    g_aw = [torch.empty(nb * nu, dtype=torch.float64, device=dev) for _ in range(world)] if gather and rank == 0 \
+        else None
+
+    flags = sbr._lib.SBR_FLAG_DIAG_SOCIAL_PROF if a.social_prof else 0
+
+    def step():
+        eng.sweep_social_dev(beta, eta, u, p, kappa, lam, cmp, x0, out, tol=tol, max_iter=a.social_max_iter,
+                             stream=stream, flags=flags)
+        if gather:
+            dist.gather(out["aw_max"], g_aw, dst=0)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    eng.timing_read(stream)
+    eng.timing_enable(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    init_ms, iter_ms, ncalls = eng.timing_read(stream)
+    eng.timing_enable(False)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    steps = out["rk_steps"].cpu().numpy()
+    st = out["status"].cpu().numpy().view(np.uint32)
+    fp = out["fp_iters"].cpu().numpy()
+    total_pts = nb * nu * world
+    res = {
+        "metric": "equilibria solved/sec on β×u grid (FP64), social-learning fixed point",
+        "value": total_pts * a.steps / elapsed,
+        "unit": "equilibria/s",
+        "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (deterministic config-5 parameter grid; no RNG in the reference)",
+        "config": {"workload": f"social_fixed_point_{nb}x{nu}_per_gpu (BASELINE config 5 share)",
+                   "n_beta_per_gpu": nb, "n_u": nu, "eta": eta_v, "p": p, "kappa": kappa, "lambda": lam,
+                   "tol": tol, "max_iter": a.social_max_iter, "parallelism": f"beta-column shards x{world}"},
+        "kernel_ms_per_step": {"social_init": init_ms / max(ncalls, 1), "social_iterates": iter_ms / max(ncalls, 1)},
+        "rk_steps_per_point": float(steps.mean()),
+        "fp_iters_mean": float(fp.mean()), "fp_iters_max": int(fp.max()),
+        "run_fraction": float(((st & sbr.STATUS["SBR_RUN"]) > 0).mean()),
+        "not_converged_fraction": float(((st & sbr.STATUS["SBR_SOCIAL_NOT_CONVERGED"]) > 0).mean()),
+    }
+    if a.social_prof:
+        pr = eng.social_prof_read()
+        names = ("cmp_prelude", "ode", "hazard_scan", "bisection", "aw_norm", "damping_awmax")
+        tot = max(sum(pr[:6]), 1)
+        res["social_prof"] = {"cycle_share": {k: pr[i] / tot for i, k in enumerate(names)},
+                              "cycles_per_rk_step_ode": pr[1] / max(pr[7], 1),
+                              "slow_lookups_per_step": pr[6] / max(pr[7], 1)}
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:

@@ -49,7 +49,7 @@ typedef struct {
     int32_t knot_capacity;      /* engine limit on stored knots per β (0 = default 65536) */
     int32_t hetero_max_iters;   /* heterogeneity_solver.jl:49 max_iters = 500 */
     int32_t flags;              /* SBR_FLAG_* */
-    int32_t pad;
+    int32_t pad;                /* social sweep: knot capacity per buffer (0 = default 98304) */
 } sbr_opts;
 
 /* Evaluate every τ̄ knot of the crossing scan and of the AW path (no block
@@ -62,6 +62,9 @@ typedef struct {
 #define SBR_FLAG_DIAG_STOP_AFTER_BUFFER 0x100
 #define SBR_FLAG_DIAG_STOP_AFTER_BISECT 0x200
 #define SBR_FLAG_DIAG_COUNT_AW_BLOCKS 0x400
+/* Diagnostics of the social sweep: per-phase shader-cycle sums, read with
+ * sbr_social_prof_read (results unchanged). */
+#define SBR_FLAG_DIAG_SOCIAL_PROF 0x800
 
 typedef struct {
     double* xi;          /* SolvedModel.ξ                       */
@@ -160,6 +163,42 @@ int sbr_sweep_hetero_dev(sbr_ctx* ctx, void* stream, int32_t K, const double* be
                          const double* eta, const double* t_end, double x0, const double* u, int64_t n_col,
                          int64_t n_u, double p, double kappa, double lambda, const sbr_opts* opts,
                          sbr_result_soa* out, double* tau_in, double* tau_out);
+
+/*
+ * Social-learning extension sweep — for each β column b and each u:
+ *     solve_equilibrium_social_learning(ModelParameters(β_b, η_b, u, p, κ, λ, x0); tol, max_iter)
+ *                                          social_learning_solver.jl:63-263
+ *     get_AW_functions!(result).AW_max     solver.jl:553-576
+ * i.e. the fixed point between learning from aggregate withdrawals
+ * (social_learning_dynamics.jl:58-114) and the baseline equilibrium, damped
+ * by 1/2, with tspan = (0, η) (:79).  cmp_grid is [n_beta × n_cmp]: row b is
+ * collect(range(0.0, η_b, length = 1000)) of :103 (passed in so that a Julia
+ * caller hands over Julia's own range elements).  Results are the returned
+ * SolvedModel (the last inner equilibrium, :262) u-fastest; the fixed-point
+ * outcome is SBR_SOCIAL_NOT_CONVERGED (max_iter reached, ξ search past η, or a
+ * BoundsError of the reference: SBR_OOB) and fp_iters (may be NULL);
+ * rk_steps (may be NULL) = Tsit5 steps attempted per point, for flop counts.
+ * Host pointers; synchronous.  The HBM workspace is 5 × capacity doubles per
+ * point in flight (opts->pad, default 98304 knots: ≈3.9 MB); large grids run
+ * in chunks that fit sbr_set_social_workspace (default 60 % of free HBM).
+ */
+int sbr_sweep_social(sbr_ctx* ctx, const double* beta, const double* eta, double x0, const double* u, int64_t n_beta,
+                     int64_t n_u, double p, double kappa, double lambda, const double* cmp_grid, int32_t n_cmp,
+                     double tol, int32_t max_iter, const sbr_opts* opts, sbr_result_soa* out, int32_t* fp_iters,
+                     int64_t* rk_steps);
+/* Same on device pointers, enqueued on `stream` without synchronising (all
+ * max_iter iterates are launched; finished points drop out of the worklist). */
+int sbr_sweep_social_dev(sbr_ctx* ctx, void* stream, const double* beta, const double* eta, double x0,
+                         const double* u, int64_t n_beta, int64_t n_u, double p, double kappa, double lambda,
+                         const double* cmp_grid, int32_t n_cmp, double tol, int32_t max_iter, const sbr_opts* opts,
+                         sbr_result_soa* out, int32_t* fp_iters, int64_t* rk_steps);
+/* Workspace budget in bytes for social sweeps (0 = 60 % of free HBM at call time). */
+int sbr_set_social_workspace(sbr_ctx* ctx, int64_t bytes);
+/* Diagnostics: sums over the points of the last social sweep run with
+ * SBR_FLAG_DIAG_SOCIAL_PROF — shader cycles in [0] comparison-grid prelude,
+ * [1] forced ODE, [2] hazard + crossing scan, [3] bisection, [4] AW norm,
+ * [5] damping / AW_max; [6] stage lookups past the register window; [7] RK steps. */
+int sbr_social_prof_read(sbr_ctx* ctx, int64_t* out8);
 
 /* 5-consecutive-no-run early exit (1_baseline.jl:236-244) as a post-pass on
  * host arrays: points after `threshold` consecutive non-runs in a β column get

@@ -142,7 +142,7 @@ static inline int64_t ssl(const double* t, int64_t n, double x)
 static inline double interp_s(const double* t, const double* v, int64_t stride, int64_t n, double x,
                               int* oob)
 {
-    if (!(x >= t[0] && x <= t[n - 1])) {
+    if (n < 2 || !(x >= t[0] && x <= t[n - 1])) { /* (a 1-knot grid has no interpolant) */
         *oob = 1;
         return NAN;
     }

@@ -30,6 +30,17 @@ struct sbr_ctx {
     // hetero learning workspace
     size_t hs_col = 0, hs_cap = 0, hs_K = 0;
     sbr::HeteroBufs H{};
+    // social-learning workspace (sbr_social.hip): per point 5 knot buffers + n_cmp
+    size_t so_pts = 0, so_cap = 0, so_cmp = 0;
+    double *so_ws = nullptr, *so_cmpo = nullptr, *so_xi = nullptr;
+    int32_t *so_n_old = nullptr, *so_live = nullptr, *so_work[2] = {nullptr, nullptr}, *so_count = nullptr;
+    uint32_t *so_slots = nullptr, *so_bits = nullptr;
+    int64_t* so_steps = nullptr;
+    int32_t* so_count_host = nullptr; // pinned
+    int64_t so_budget = 0;            // workspace bytes (0: 60 % of free HBM)
+    int64_t* so_prof = nullptr;       // SBR_FLAG_DIAG_SOCIAL_PROF: [pts][8]
+    size_t so_prof_pts = 0;
+    std::vector<int64_t> so_prof_acc; // host sums over the chunks of the last sweep
     // host-API staging
     void* stage = nullptr;
     size_t stage_bytes = 0;
@@ -125,6 +136,42 @@ int ensure_hetero(sbr_ctx* c, size_t n_col, size_t cap, size_t K)
     c->hs_col = n_col;
     c->hs_cap = cap;
     c->hs_K = K;
+    return SBR_OK;
+}
+
+void free_social(sbr_ctx* c)
+{
+    void* ps[] = {c->so_ws, c->so_cmpo, c->so_xi, c->so_n_old, c->so_live, c->so_work[0], c->so_work[1],
+                  c->so_count, c->so_slots, c->so_bits, c->so_steps};
+    for (void* p : ps)
+        if (p) (void)hipFree(p);
+    c->so_ws = c->so_cmpo = c->so_xi = nullptr;
+    c->so_n_old = c->so_live = c->so_work[0] = c->so_work[1] = c->so_count = nullptr;
+    c->so_slots = c->so_bits = nullptr;
+    c->so_steps = nullptr;
+    c->so_pts = c->so_cap = c->so_cmp = 0;
+}
+
+int ensure_social(sbr_ctx* c, size_t pts, size_t cap, size_t n_cmp)
+{
+    if (pts <= c->so_pts && cap == c->so_cap && n_cmp <= c->so_cmp) return SBR_OK;
+    free_social(c);
+    // wave-blocked layout (sbr_social.hip BView): whole 64-point groups
+    HIP_TRY(c, hipMalloc(&c->so_ws, ((pts + 63) / 64) * 64 * 5 * cap * 8), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&c->so_cmpo, pts * n_cmp * 8), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&c->so_xi, pts * 8), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&c->so_n_old, pts * 4), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&c->so_live, pts * 4), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&c->so_work[0], pts * 4), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&c->so_work[1], pts * 4), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&c->so_count, 2 * 4), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&c->so_slots, pts * 4), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&c->so_bits, pts * 4), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&c->so_steps, pts * 8), SBR_ENOMEM);
+    if (!c->so_count_host) HIP_TRY(c, hipHostMalloc(&c->so_count_host, 2 * 4), SBR_ENOMEM);
+    c->so_pts = pts;
+    c->so_cap = cap;
+    c->so_cmp = n_cmp;
     return SBR_OK;
 }
 
@@ -261,6 +308,9 @@ int sbr_free(sbr_ctx* c)
     free_learn(c, 0);
     free_learn(c, 1);
     free_hetero(c);
+    free_social(c);
+    if (c->so_prof) (void)hipFree(c->so_prof);
+    if (c->so_count_host) (void)hipHostFree(c->so_count_host);
     hipEvent_t evs[] = {c->ev_in, c->ev_learned[0], c->ev_learned[1], c->ev_eq[0], c->ev_eq[1]};
     for (hipEvent_t e : evs)
         if (e) (void)hipEventDestroy(e);
@@ -589,6 +639,177 @@ int sbr_sweep_hetero(sbr_ctx* c, int32_t K, const double* betas, const double* d
     if (out->iters) HIP_TRY(c, hipMemcpyAsync(out->iters, dit, np * 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
     if (tau_in) HIP_TRY(c, hipMemcpyAsync(tau_in, dtin, np * K * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
     if (tau_out) HIP_TRY(c, hipMemcpyAsync(tau_out, dtout, np * K * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+    HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
+    return SBR_OK;
+}
+
+int sbr_social_prof_read(sbr_ctx* c, int64_t* out8)
+{
+    if (!c || !out8) return SBR_EARG;
+    for (int k = 0; k < 8; k++) out8[k] = k < (int)c->so_prof_acc.size() ? c->so_prof_acc[k] : 0;
+    return SBR_OK;
+}
+
+int sbr_set_social_workspace(sbr_ctx* c, int64_t bytes)
+{
+    if (!c || bytes < 0) return SBR_EARG;
+    c->so_budget = bytes;
+    return SBR_OK;
+}
+
+}  // extern "C"
+
+namespace {
+constexpr int kSocialDefaultCap = 98304; // ≈1.4× the longest iterate seen on config 5 (≈70k knots)
+
+int social_checks(sbr_ctx* c, const double* beta, const double* eta, const double* u, int64_t n_beta, int64_t n_u,
+                  double x0, double p, double kappa, double lambda, const double* cmp, int32_t n_cmp, double tol,
+                  int32_t max_iter, sbr_result_soa* out)
+{
+    if (!c || !out || !beta || !eta || !u || !cmp) return SBR_EARG;
+    if (!out->xi || !out->tau_in_unc || !out->tau_out_unc || !out->aw_max || !out->tol || !out->status)
+        return fail(c, SBR_EARG, "result arrays");
+    if (n_beta <= 0 || n_u <= 0 || n_beta * n_u > (int64_t(1) << 40)) return fail(c, SBR_EARG, "grid size");
+    if (n_cmp < 1 || max_iter < 1 || !(tol > 0.0)) return fail(c, SBR_EARG, "n_cmp / max_iter / tol");
+    if (!scalars_valid(x0, p, kappa, lambda)) return fail(c, SBR_EARG, "ArgumentError: x0/p/kappa/lambda");
+    return SBR_OK;
+}
+
+// the whole fixed point for every point, chunked by workspace size; poll > 0
+// reads the live count every `poll` iterates and stops once it is zero
+int run_social(sbr_ctx* c, hipStream_t s, const double* beta, const double* eta, double x0, const double* u,
+               int64_t n_beta, int64_t n_u, double p, double kappa, double lambda, const double* cmp, int32_t n_cmp,
+               double tol, int32_t max_iter, const sbr_opts& o, sbr_result_soa* out, int32_t* fp_iters,
+               int64_t* rk_steps, int poll)
+{
+    const int64_t n_total = n_beta * n_u;
+    size_t cap = o.pad > 0 ? (size_t)o.pad : (size_t)kSocialDefaultCap;
+    cap = (cap + 15) & ~(size_t)15; // 16-knot lines of the wave-blocked layout
+    const size_t per_pt = 5 * cap * 8 + (size_t)n_cmp * 8 + 64;
+    int64_t budget = c->so_budget;
+    if (budget <= 0) {
+        size_t fr = 0, tot = 0;
+        HIP_TRY(c, hipMemGetInfo(&fr, &tot), SBR_EDEVICE);
+        budget = (int64_t)((double)(fr + c->so_pts * (5 * c->so_cap * 8 + c->so_cmp * 8 + 64)) * 0.6);
+    }
+    int64_t chunk = budget / (int64_t)per_pt;
+    if (chunk < 64) return fail(c, SBR_ENOMEM, "social workspace budget below 64 points");
+    if (chunk > (1 << 30)) chunk = 1 << 30;
+    if (chunk >= n_total) chunk = n_total;
+    else chunk &= ~(int64_t)63; // whole wave groups
+    int rc = ensure_social(c, (size_t)chunk, cap, (size_t)n_cmp);
+    if (rc) return rc;
+    const bool prof = (o.flags & SBR_FLAG_DIAG_SOCIAL_PROF) != 0;
+    if (prof && c->so_prof_pts < (size_t)chunk) {
+        if (c->so_prof) (void)hipFree(c->so_prof);
+        c->so_prof = nullptr;
+        c->so_prof_pts = 0;
+        HIP_TRY(c, hipMalloc(&c->so_prof, (size_t)chunk * 64), SBR_ENOMEM);
+        c->so_prof_pts = (size_t)chunk;
+    }
+    c->so_prof_acc.assign(8, 0);
+    for (int64_t pt0 = 0; pt0 < n_total; pt0 += chunk) {
+        const int32_t npts = (int32_t)((n_total - pt0) < chunk ? (n_total - pt0) : chunk);
+        sbr::SocialArgs a{};
+        a.beta = beta; a.eta = eta; a.u = u; a.cmp = cmp;
+        a.pt0 = pt0; a.n_pts = npts; a.n_u = (int32_t)n_u; a.n_cmp = n_cmp;
+        a.max_iter = max_iter; a.bisect_max_iters = o.bisect_max_iters; a.cap = (int32_t)cap;
+        a.maxiters = o.ode_maxiters;
+        a.x0 = x0; a.p = p; a.kappa = kappa; a.lam = lambda; a.tol = tol; a.rtol = o.ode_reltol; a.atol = o.ode_abstol;
+        a.ws = c->so_ws; a.cmpo = c->so_cmpo; a.n_old = c->so_n_old; a.slots = c->so_slots; a.xi_new = c->so_xi;
+        a.bits = c->so_bits; a.steps = c->so_steps; a.live = c->so_live; a.work = c->so_work[0];
+        a.count = c->so_count;
+        a.out = sbr::ResultSoA{out->xi, out->tau_in_unc, out->tau_out_unc, out->aw_max, out->tol, out->status,
+                               out->iters};
+        a.fp_iters = fp_iters;
+        a.steps_out = rk_steps;
+        a.prof = prof ? c->so_prof : nullptr;
+        if (prof) HIP_TRY(c, hipMemsetAsync(c->so_prof, 0, (size_t)npts * 64, s), SBR_EDEVICE);
+        hipEvent_t t0 = tstart(c, s);
+        HIP_TRY(c, sbr::launch_social_init(a, s), SBR_EDEVICE);
+        tend(c, s, 0, t0);
+        t0 = tstart(c, s);
+        for (int it = 1; it <= max_iter; it++) {
+            const int k = (it - 1) & 1;
+            HIP_TRY(c, sbr::launch_social_iter(a, it, c->so_work[k], c->so_count + k, c->so_work[k ^ 1],
+                                               c->so_count + (k ^ 1), s),
+                    SBR_EDEVICE);
+            if (poll > 0 && (it % poll == 0) && it < max_iter) {
+                HIP_TRY(c, hipMemcpyAsync(c->so_count_host, c->so_count + (k ^ 1), 4, hipMemcpyDeviceToHost, s),
+                        SBR_EDEVICE);
+                HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
+                if (c->so_count_host[0] == 0) break;
+            }
+        }
+        tend(c, s, 1, t0);
+        if (prof) {
+            std::vector<int64_t> h((size_t)npts * 8);
+            HIP_TRY(c, hipMemcpyAsync(h.data(), c->so_prof, h.size() * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+            HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
+            for (size_t i = 0; i < h.size(); i++) c->so_prof_acc[i & 7] += h[i];
+        }
+    }
+    return SBR_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int sbr_sweep_social_dev(sbr_ctx* c, void* stream, const double* beta, const double* eta, double x0, const double* u,
+                         int64_t n_beta, int64_t n_u, double p, double kappa, double lambda, const double* cmp_grid,
+                         int32_t n_cmp, double tol, int32_t max_iter, const sbr_opts* opts, sbr_result_soa* out,
+                         int32_t* fp_iters, int64_t* rk_steps)
+{
+    int rc = social_checks(c, beta, eta, u, n_beta, n_u, x0, p, kappa, lambda, cmp_grid, n_cmp, tol, max_iter, out);
+    if (rc) return rc;
+    if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
+    sbr_opts o = resolve(opts);
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    return run_social(c, s, beta, eta, x0, u, n_beta, n_u, p, kappa, lambda, cmp_grid, n_cmp, tol, max_iter, o, out,
+                      fp_iters, rk_steps, 0);
+}
+
+int sbr_sweep_social(sbr_ctx* c, const double* beta, const double* eta, double x0, const double* u, int64_t n_beta,
+                     int64_t n_u, double p, double kappa, double lambda, const double* cmp_grid, int32_t n_cmp,
+                     double tol, int32_t max_iter, const sbr_opts* opts, sbr_result_soa* out, int32_t* fp_iters,
+                     int64_t* rk_steps)
+{
+    int rc = social_checks(c, beta, eta, u, n_beta, n_u, x0, p, kappa, lambda, cmp_grid, n_cmp, tol, max_iter, out);
+    if (rc) return rc;
+    for (int64_t i = 0; i < n_beta; i++)
+        if (!(beta[i] > 0.0) || !(eta[i] > 0.0)) return fail(c, SBR_EARG, "ArgumentError: beta/eta must be positive");
+    for (int64_t j = 0; j < n_u; j++)
+        if (!(u[j] >= 0.0)) return fail(c, SBR_EARG, "ArgumentError: u must be non-negative");
+    if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
+    sbr_opts o = resolve(opts);
+    const size_t np = (size_t)(n_beta * n_u);
+    const size_t in_d = 2 * (size_t)n_beta + (size_t)n_u + (size_t)n_beta * n_cmp;
+    const size_t out_d = np * 5 + np + np + np; // 5 doubles | status+iters | fp_iters+pad | steps
+    rc = ensure_stage(c, (in_d + out_d) * 8 + 1024);
+    if (rc) return rc;
+    double* d = (double*)c->stage;
+    double *dbeta = d, *deta = dbeta + n_beta, *du = deta + n_beta, *dcmp = du + n_u;
+    double* dres = dcmp + (size_t)n_beta * n_cmp;
+    double *dxi = dres, *dtin = dxi + np, *dtout = dtin + np, *daw = dtout + np, *dtol = daw + np;
+    uint32_t* dst = (uint32_t*)(dtol + np);
+    int32_t* dit = (int32_t*)(dst + np);
+    int32_t* dfp = dit + np;
+    int64_t* dsteps = (int64_t*)(dfp + 2 * np);
+    hipStream_t s = c->stream;
+    HIP_TRY(c, hipMemcpyAsync(dbeta, beta, (size_t)n_beta * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+    HIP_TRY(c, hipMemcpyAsync(deta, eta, (size_t)n_beta * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+    HIP_TRY(c, hipMemcpyAsync(du, u, (size_t)n_u * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+    HIP_TRY(c, hipMemcpyAsync(dcmp, cmp_grid, (size_t)n_beta * n_cmp * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+    sbr_result_soa r{dxi, dtin, dtout, daw, dtol, dst, dit};
+    rc = run_social(c, s, dbeta, deta, x0, du, n_beta, n_u, p, kappa, lambda, dcmp, n_cmp, tol, max_iter, o, &r, dfp,
+                    dsteps, 8);
+    if (rc) return rc;
+    struct { void* h; const void* dv; size_t b; } cp[] = {
+        {out->xi, dxi, np * 8}, {out->tau_in_unc, dtin, np * 8}, {out->tau_out_unc, dtout, np * 8},
+        {out->aw_max, daw, np * 8}, {out->tol, dtol, np * 8}, {out->status, dst, np * 4},
+        {out->iters, dit, np * 4}, {fp_iters, dfp, np * 4}, {rk_steps, dsteps, np * 8}};
+    for (auto& x : cp)
+        if (x.h) HIP_TRY(c, hipMemcpyAsync(x.h, x.dv, x.b, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
     HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
     return SBR_OK;
 }

@@ -68,6 +68,42 @@ struct HeteroEqArgs {
     int32_t lds_cap;    // knot times staged in LDS
 };
 
+// Social-learning fixed point (sbr_social.hip): one lane per point; per-point
+// workspace of 5 knot buffers × cap doubles (point-major) + n_cmp doubles.
+struct SocialArgs {
+    const double* beta;  // [n_beta]
+    const double* eta;   // [n_beta]
+    const double* u;     // [n_u]
+    const double* cmp;   // [n_beta][n_cmp] comparison grids range(0, η, n_cmp)
+    int64_t pt0;         // first global point (β-major, u-fastest) of this chunk
+    int32_t n_pts;       // points in this chunk
+    int32_t n_u;
+    int32_t n_cmp;
+    int32_t max_iter;    // fixed-point iterations (script: 500)
+    int32_t bisect_max_iters;
+    int32_t cap;         // knots per buffer
+    int64_t maxiters;    // ODE maxiters
+    double x0, p, kappa, lam, tol, rtol, atol;
+    double* ws;          // [n_pts][5][cap]
+    double* cmpo;        // [n_pts][n_cmp]
+    int32_t* n_old;      // knots of AW_{n-1}
+    uint32_t* slots;     // buffer permutation (5 × 3 bits)
+    double* xi_new;      // ξ carried between iterates
+    uint32_t* bits;      // accumulated ODE status bits
+    int64_t* steps;      // RK steps attempted (accepted + rejected), all iterates
+    int32_t* live;       // 1 while the point iterates
+    int32_t* work;       // initial worklist (filled by the init kernel)
+    int32_t* count;      // initial worklist length
+    ResultSoA out;       // global result arrays (indexed pt0 + local)
+    int32_t* fp_iters;   // fixed-point iterations (may be null)
+    int64_t* steps_out;  // RK steps per point, written when it finishes (may be null)
+    int64_t* prof;       // diagnostics [n_pts][8] cycles per phase + counters (may be null)
+};
+
+hipError_t launch_social_init(const SocialArgs& a, hipStream_t s);
+hipError_t launch_social_iter(const SocialArgs& a, int iter, const int32_t* work, const int32_t* count,
+                              int32_t* work_out, int32_t* count_out, hipStream_t s);
+
 hipError_t launch_hetero(int K, const double* betas, const double* dist, const double* eta, const double* t_end,
                          const double* u, const LearnArgs& la, const HeteroEqArgs& ea, const HeteroBufs& L,
                          const ResultSoA& out, double* tin, double* tout, hipStream_t s, int phase);

@@ -1,0 +1,860 @@
+// sbr_social.hip — gfx950 kernels for the social-learning extension sweep:
+// every (β, u) point runs the fixed point of solve_equilibrium_social_learning
+// (src/extensions/social_learning/social_learning_solver.jl:63-263):
+//
+//   AW_0 = G of the baseline SI learning on (0, η)               (:89-94)
+//   repeat  G_n  = Tsit5 solve of dG/dt = (1 − G) β AW_{n−1}(t)   (dynamics.jl:58-78)
+//           r_n  = solve_equilibrium_baseline on G_n              (:139-143)
+//           AW*  = get_AW(ξ_n or ξ_{n−1} + η/500, …) on G_n        (:147-200)
+//           stop if ‖AW* − AW_{n−1}‖_∞ on range(0, η, 1000) < tol  (:162-172, :195-212)
+//           AW_n = ½ AW_{n−1} + ½ AW* on G_n's knots              (:174-178, :218-222)
+//
+// Layout and schedule:
+//  * one lane per grid point for the whole fixed point — the forced ODE is a
+//    serial chain of ~10⁵ Tsit5 steps per iterate, so points are the only
+//    parallelism; lanes of a wave hold consecutive u of one β column;
+//  * each point owns five knot buffers of `cap` doubles in HBM (point-major:
+//    a lane walks its own contiguous rows): AW_{n−1} knots/values, G_n knots,
+//    values and AW_{n−1}(t_i) at those knots; buffers rotate between iterates;
+//  * one launch per fixed-point iterate over a worklist of unfinished points;
+//    a single-workgroup ballot compaction (order-preserving, deterministic)
+//    retires finished lanes so later iterates launch only live waves.
+//
+// Bit-exact against oracle/sbr_oracle.c social_point (same operation order,
+// -ffp-contract=off, fma() where the oracle has it, shared sbr_exp/sbr_log).
+#include "sbr_device.h"
+#include "sbr_kernels.h"
+
+namespace sbr {
+
+namespace {
+
+// One point's knot buffer in the wave-blocked layout: 16 consecutive knots of a
+// point fill one 128-byte line, and the 64 points of a wave group interleave
+// line by line (an 8 KiB row per 16-knot block).  A lane still streams its own
+// lines sequentially, but a wave's 64 concurrent accesses fall within a few
+// MiB instead of 64 separate multi-MiB rows (page/TLB locality).
+struct BView {
+    double* p; // ws + (group·5 + slot)·cap·64 + lane·16
+    __device__ __forceinline__ double& operator[](int k) const { return p[((k >> 4) << 10) + (k & 15)]; }
+};
+
+// Bracket search with an 8-knot window of knot times held in registers: the
+// walks below advance a few knots per lookup, so brackets come from register
+// compares and only the interpolation operands are loaded (independent loads,
+// no dependent search chains).  Returns exactly searchsortedlast's index.
+struct Win8 {
+    BView t;
+    int n;
+    int wb;        // window base: tw[k] = t[wb + k] (+Inf past the grid)
+    double tw[8];
+    // branch-free refill: eight independent loads (index clamped into the grid)
+    __device__ __forceinline__ void load(int base)
+    {
+        wb = base;
+        const int last = n > 0 ? n - 1 : 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const int i = base + k;
+            const double v = t[i < last ? i : last];
+            tw[k] = (i < n) ? v : (double)INFINITY;
+        }
+    }
+    __device__ __forceinline__ void init(BView tt, int nn)
+    {
+        t = tt;
+        n = nn;
+        load(0);
+    }
+    __device__ int slow_find(double x) const
+    {
+        return (x >= tw[0]) ? ssl_gallop(t, n, wb + 7, x) : ssl_range(t, 0, wb, x);
+    }
+    // largest j with t[j] <= x; requires t[0] <= x; the window does not move
+    __device__ __forceinline__ int find(double x) const
+    {
+        int c = 0;
+#pragma unroll
+        for (int k = 1; k < 7; k++) c += (tw[k] <= x) ? 1 : 0;
+        int j = wb + c;
+        if (!(x >= tw[0] && x < tw[7])) j = slow_find(x);
+        return j;
+    }
+    // same, then re-centre the window on the answer once it is 4+ knots ahead
+    __device__ __forceinline__ int find_advance(double x)
+    {
+        const int j = find(x);
+        if (j - wb >= 4 || j < wb) load(j);
+        return j;
+    }
+};
+
+// gridded-linear value on bracket j (clamped to [0, n-2]) with unconditional
+// loads, NaN + oob when x is outside [t_0, t_{n-1}] (oracle interp_s)
+__device__ __forceinline__ double lerp_sel(BView t, BView v, int n, int j, double x, bool in)
+{
+    j = j > n - 2 ? n - 2 : j;
+    j = j < 0 ? 0 : j;
+    const double t0 = t[j], t1 = t[j + 1], v0 = v[j], v1 = v[j + 1];
+    const double d = (x - t0) / (t1 - t0);
+    const double r = v0 * (1.0 - d) + v1 * d;
+    return in ? r : (double)NAN;
+}
+
+// Interpolations.jl gridded Linear with Throw() (oracle interp_s): NaN + oob
+// outside [t_0, t_{n-1}].  Monotone walker over one knot grid.
+struct Walker {
+    Win8 w;
+    BView v;
+    double tfirst, tlast;
+    __device__ __forceinline__ void init(BView tt, BView vv, int nn)
+    {
+        w.init(tt, nn);
+        v = vv;
+        tfirst = nn > 0 ? tt[0] : 0.0;
+        tlast = nn > 0 ? tt[nn - 1] : 0.0;
+    }
+    __device__ __forceinline__ double at(double x, bool& oob)
+    {
+        const bool in = w.n >= 2 && x >= tfirst && x <= tlast;
+        oob |= !in;
+        const int j = in ? w.find_advance(x) : 0;
+        return lerp_sel(w.t, v, w.n, j, x, in);
+    }
+    // bracket only (clamped like lerp_at); requires t[0] <= x <= t[n-1]
+    __device__ __forceinline__ int bracket(double x)
+    {
+        const int j = w.find_advance(x);
+        return j > w.n - 2 ? w.n - 2 : j;
+    }
+};
+
+// full-range lookup (non-monotone callers: the bisection)
+__device__ __forceinline__ double interp_full(BView t, BView v, int n, double x, bool& oob)
+{
+    if (n < 2 || !(x >= t[0] && x <= t[n - 1])) { oob = true; return (double)NAN; }
+    return lerp_at(t, v, n, ssl_range(t, 0, n - 1, x), x);
+}
+
+__device__ __forceinline__ BView buf(const SocialArgs& a, int l, int slot)
+{
+    return BView{a.ws + ((size_t)(l >> 6) * 5 + (size_t)slot) * (size_t)a.cap * 64 + (size_t)(l & 63) * 16};
+}
+
+// ---------------------------------------------------------------------------
+// Tsit5 on one scalar ODE (oracle tsit5_solve with m = 1): initial dt of
+// ode_determine_initdt, PI control, tstop clipping / snap, AutoSwitch test.
+// Rhs: double f(double t, double x)  (may set oob through its own state);
+// Sink: bool push(double t, double x, bool exact_last_stage) — false = stop.
+// ---------------------------------------------------------------------------
+struct OdeOut {
+    int64_t naccept = 0, nreject = 0;
+    uint32_t status = 0;
+};
+
+template <class Rhs, class Sink>
+__device__ __forceinline__ void tsit5_scalar(Rhs& f, Sink& push, double T1, double x0, double rtol, double atol,
+                                             int64_t maxiters, OdeOut& o)
+{
+    const double T0 = 0.0;
+    const double dtmax = T1 - T0;
+    const double dtmin = sbr_jl_eps(dmax(fabs(T0), fabs(T1)));
+    // ---- ode_determine_initdt ----
+    const double sk = fma(fabs(x0), rtol, atol);
+    const double d0 = fabs(x0 / sk);
+    double k1 = f(T0, x0);
+    const double d1 = fabs(k1 / sk);
+    double dt0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * (d0 / d1);
+    dt0 = dmin(dt0, dtmax);
+    double dt;
+    if (dt0 < 10.0 * DBL_EPS) {
+        dt = dmax(1e-6, dtmin);
+    } else {
+        const double u1 = fma(dt0, k1, x0);
+        const double f1 = f(T0 + dt0, u1);
+        if (k1 == f1) {
+            dt = dmax(dtmin, 100.0 * dt0);
+        } else {
+            const double d2 = fabs((f1 - k1) / sk) / dt0;
+            const double md = dmax(d1, d2);
+            const double dt1 = (md <= 1e-15) ? dmax(1e-6, dt0 * 1e-3) : sbr_pow_pos(0.01 / md, 1.0 / 6.0);
+            dt = dmax(dtmin, dmin(dmin(100.0 * dt0, dt1), dtmax));
+        }
+    }
+    const double LOG_QOLDMIN = sbr_log(CTL_QOLDMIN);
+    const double snap = 100.0 * sbr_jl_eps(T1);
+    double t = T0, x = x0, lqold = LOG_QOLDMIN;
+    AutoSwitch as;
+    if (!push(t, x, false)) return; // (the last RHS call was at T0 + dt0, not T0)
+    int64_t iter = 0;
+    while (t < T1) {
+        if (++iter > maxiters) { o.status |= SBR_ODE_MAXITERS; break; }
+        dt = dmin(dtmax, dt);
+        dt = dmax(dt, dtmin);
+        dt = dmin(dt, T1 - t);
+        double tmp = fma(dt * A21, k1, x);
+        const double k2 = f(fma(C1, dt, t), tmp);
+        tmp = fma(dt, fma(A31, k1, A32 * k2), x);
+        const double k3 = f(fma(C2, dt, t), tmp);
+        tmp = fma(dt, fma(A41, k1, fma(A42, k2, A43 * k3)), x);
+        const double k4 = f(fma(C3, dt, t), tmp);
+        tmp = fma(dt, fma(A51, k1, fma(A52, k2, fma(A53, k3, A54 * k4))), x);
+        const double k5 = f(fma(C4, dt, t), tmp);
+        const double tmp6 = fma(dt, fma(A61, k1, fma(A62, k2, fma(A63, k3, fma(A64, k4, A65 * k5)))), x);
+        const double k6 = f(t + dt, tmp6);
+        const double u =
+            fma(dt, fma(A71, k1, fma(A72, k2, fma(A73, k3, fma(A74, k4, fma(A75, k5, A76 * k6))))), x);
+        const double k7 = f(t + dt, u);
+        const double eigr = fabs((k7 - k6) / (u - tmp6));
+        const double eig = (eigr != eigr) ? (double)NAN : eigr;
+        const double ut =
+            dt * fma(BT1, k1, fma(BT2, k2, fma(BT3, k3, fma(BT4, k4, fma(BT5, k5, fma(BT6, k6, BT7 * k7))))));
+        const double EEst = fabs(ut / fma(dmax(fabs(x), fabs(u)), rtol, atol));
+        double q, le = 0.0;
+        if (EEst == 0.0) {
+            q = CTL_INV_QMAX;
+        } else {
+            le = sbr_log(EEst);
+            q = sbr_exp(CTL_BETA1 * le - CTL_BETA2 * lqold);
+            q = dmax(CTL_INV_QMAX, dmin(CTL_INV_QMIN, q / CTL_GAMMA));
+        }
+        if (EEst <= 1.0) {
+            o.naccept++;
+            const double dtnew = dt / q;
+            const double qold = dmax(EEst, CTL_QOLDMIN);
+            lqold = (qold == EEst) ? le : LOG_QOLDMIN;
+            const double tdt = t + dt;
+            double tn = tdt;
+            if (fabs(tn - T1) < snap) tn = T1;
+            t = tn;
+            x = u;
+            k1 = k7;
+            dt = dmax(dmin(dtmax, dtnew), dtmin);
+            if (!push(t, x, tn == tdt)) return;
+        } else {
+            o.nreject++;
+            const double q11 = sbr_exp(CTL_BETA1 * le);
+            dt = dt / dmin(CTL_INV_QMIN, q11 / CTL_GAMMA);
+        }
+        if (!(dt > 0.0) || !isfinite(dt)) { o.status |= SBR_ODE_FAILED; break; }
+        as.update(eig, dt);
+    }
+    if (as.switched) o.status |= SBR_STIFF_SWITCH;
+}
+
+// dx/dt = βx(1 − x) (learning.jl:45-48)
+struct LogisticRhs {
+    double beta;
+    __device__ __forceinline__ double operator()(double, double x) const { return (beta * x) * (1.0 - x); }
+};
+
+// dG/dt = (1 − G) β AW_old(t) (social_learning_dynamics.jl:61-67).  All stage
+// times of a step (t + c_i·dt, t + dt) are known when the step starts, so the
+// five AW_old lookups are done up front (prepare): brackets from the register
+// window anchored at the step's t, then 20 independent operand loads and five
+// independent divisions — off the serial chain of the RK stages.
+struct SocialRhs {
+    double beta;
+    BView to;
+    BView vo;
+    int n;
+    double tfirst, tlast;
+    Win8 w;
+    double aw[5];
+    double last_aw;
+    bool oob;
+    int slow;   // diagnostics: stage lookups past the register window
+    __device__ __forceinline__ void init(double b, BView t_, BView v_, int n_)
+    {
+        slow = 0;
+        beta = b; to = t_; vo = v_; n = n_;
+        tfirst = n > 0 ? to[0] : 0.0;
+        tlast = n > 0 ? to[n - 1] : 0.0;
+        w.init(to, n);
+        oob = false;
+        last_aw = 0.0;
+    }
+    __device__ __forceinline__ double lookup(double x)
+    {
+        if (n < 2 || !(x >= tfirst && x <= tlast)) { oob = true; return (double)NAN; }
+        return lerp_at(to, vo, n, w.find(x), x);
+    }
+    // generic evaluation (initial-dt probes)
+    __device__ __forceinline__ double eval(double t, double x)
+    {
+        const double a = lookup(t);
+        last_aw = a;
+        return ((1.0 - x) * beta) * a;
+    }
+    __device__ __forceinline__ void prepare(double t, double dt)
+    {
+        const double xs[5] = {fma(C1, dt, t), fma(C2, dt, t), fma(C3, dt, t), fma(C4, dt, t), t + dt};
+        int js[5];
+        bool in[5];
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            in[k] = n >= 2 && xs[k] >= tfirst && xs[k] <= tlast;
+            slow += (in[k] && !(xs[k] < w.tw[7])) ? 1 : 0;
+            js[k] = in[k] ? w.find(xs[k]) : 0;
+        }
+        // 20 independent operand loads, then five independent divisions
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            aw[k] = lerp_sel(to, vo, n, js[k], xs[k], in[k]);
+            oob |= !in[k];
+        }
+        last_aw = aw[4];
+    }
+    // stage s = 1..6 (k2..k7): times C1..C4, then t + dt twice
+    __device__ __forceinline__ double stage(int s, double x) const
+    {
+        return ((1.0 - x) * beta) * aw[s < 5 ? s - 1 : 4];
+    }
+    __device__ __forceinline__ void accepted(double t)
+    {
+        if (n >= 2 && t >= tfirst && t <= tlast) (void)w.find_advance(t);
+    }
+};
+
+// Tsit5 loop for the social ODE: tsit5_scalar with the stage lookups batched
+// by SocialRhs::prepare (same arithmetic, same order of the RK operations).
+template <class Sink>
+__device__ __forceinline__ void tsit5_social(SocialRhs& f, Sink& push, double T1, double x0, double rtol,
+                                             double atol, int64_t maxiters, OdeOut& o)
+{
+    const double T0 = 0.0;
+    const double dtmax = T1 - T0;
+    const double dtmin = sbr_jl_eps(dmax(fabs(T0), fabs(T1)));
+    const double sk = fma(fabs(x0), rtol, atol);
+    const double d0 = fabs(x0 / sk);
+    double k1 = f.eval(T0, x0);
+    const double aw0 = f.last_aw;
+    const double d1 = fabs(k1 / sk);
+    double dt0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * (d0 / d1);
+    dt0 = dmin(dt0, dtmax);
+    double dt;
+    if (dt0 < 10.0 * DBL_EPS) {
+        dt = dmax(1e-6, dtmin);
+    } else {
+        const double u1 = fma(dt0, k1, x0);
+        const double f1 = f.eval(T0 + dt0, u1);
+        if (k1 == f1) {
+            dt = dmax(dtmin, 100.0 * dt0);
+        } else {
+            const double d2 = fabs((f1 - k1) / sk) / dt0;
+            const double md = dmax(d1, d2);
+            const double dt1 = (md <= 1e-15) ? dmax(1e-6, dt0 * 1e-3) : sbr_pow_pos(0.01 / md, 1.0 / 6.0);
+            dt = dmax(dtmin, dmin(dmin(100.0 * dt0, dt1), dtmax));
+        }
+    }
+    const double LOG_QOLDMIN = sbr_log(CTL_QOLDMIN);
+    const double snap = 100.0 * sbr_jl_eps(T1);
+    double t = T0, x = x0, lqold = LOG_QOLDMIN;
+    AutoSwitch as;
+    if (!push(t, x, aw0)) return;
+    int64_t iter = 0;
+    while (t < T1) {
+        if (++iter > maxiters) { o.status |= SBR_ODE_MAXITERS; break; }
+        dt = dmin(dtmax, dt);
+        dt = dmax(dt, dtmin);
+        dt = dmin(dt, T1 - t);
+        f.prepare(t, dt);
+        double tmp = fma(dt * A21, k1, x);
+        const double k2 = f.stage(1, tmp);
+        tmp = fma(dt, fma(A31, k1, A32 * k2), x);
+        const double k3 = f.stage(2, tmp);
+        tmp = fma(dt, fma(A41, k1, fma(A42, k2, A43 * k3)), x);
+        const double k4 = f.stage(3, tmp);
+        tmp = fma(dt, fma(A51, k1, fma(A52, k2, fma(A53, k3, A54 * k4))), x);
+        const double k5 = f.stage(4, tmp);
+        const double tmp6 = fma(dt, fma(A61, k1, fma(A62, k2, fma(A63, k3, fma(A64, k4, A65 * k5)))), x);
+        const double k6 = f.stage(5, tmp6);
+        const double u =
+            fma(dt, fma(A71, k1, fma(A72, k2, fma(A73, k3, fma(A74, k4, fma(A75, k5, A76 * k6))))), x);
+        const double k7 = f.stage(6, u);
+        const double eigr = fabs((k7 - k6) / (u - tmp6));
+        const double eig = (eigr != eigr) ? (double)NAN : eigr;
+        const double ut =
+            dt * fma(BT1, k1, fma(BT2, k2, fma(BT3, k3, fma(BT4, k4, fma(BT5, k5, fma(BT6, k6, BT7 * k7))))));
+        const double EEst = fabs(ut / fma(dmax(fabs(x), fabs(u)), rtol, atol));
+        double q, le = 0.0;
+        if (EEst == 0.0) {
+            q = CTL_INV_QMAX;
+        } else {
+            le = sbr_log(EEst);
+            q = sbr_exp(CTL_BETA1 * le - CTL_BETA2 * lqold);
+            q = dmax(CTL_INV_QMAX, dmin(CTL_INV_QMIN, q / CTL_GAMMA));
+        }
+        if (EEst <= 1.0) {
+            o.naccept++;
+            const double dtnew = dt / q;
+            const double qold = dmax(EEst, CTL_QOLDMIN);
+            lqold = (qold == EEst) ? le : LOG_QOLDMIN;
+            const double tdt = t + dt;
+            double tn = tdt;
+            if (fabs(tn - T1) < snap) tn = T1;
+            t = tn;
+            x = u;
+            k1 = k7;
+            dt = dmax(dmin(dtmax, dtnew), dtmin);
+            // AW_old at the new knot: the t + dt stage lookup unless snapped to T1
+            if (!push(t, x, tn == tdt ? f.last_aw : f.lookup(t))) return;
+            f.accepted(t);
+        } else {
+            o.nreject++;
+            const double q11 = sbr_exp(CTL_BETA1 * le);
+            dt = dt / dmin(CTL_INV_QMIN, q11 / CTL_GAMMA);
+        }
+        if (!(dt > 0.0) || !isfinite(dt)) { o.status |= SBR_ODE_FAILED; break; }
+        as.update(eig, dt);
+    }
+    if (as.switched) o.status |= SBR_STIFF_SWITCH;
+}
+
+}  // namespace
+
+// ============================================================================
+// init: baseline learning on (0, η) as AW_0 (social_learning_solver.jl:89-94)
+// ============================================================================
+__global__ __launch_bounds__(64) void social_init_kernel(SocialArgs a)
+{
+    const int l = blockIdx.x * 64 + threadIdx.x;
+    if (l >= a.n_pts) return;
+    const int64_t g = a.pt0 + l;
+    const int b = (int)(g / a.n_u);
+    const double BETA = a.beta[b], ETA = a.eta[b];
+    BView T = buf(a, l, 0);
+    BView V = buf(a, l, 1);
+    int n = 0;
+    uint32_t st = 0;
+    LogisticRhs f{BETA};
+    auto push = [&](double t, double x, bool) {
+        if (n >= a.cap) { st |= SBR_KNOT_OVERFLOW; return false; }
+        T[n] = t;
+        V[n] = x;
+        n++;
+        return true;
+    };
+    OdeOut o;
+    tsit5_scalar(f, push, ETA, a.x0, a.rtol, a.atol, a.maxiters, o);
+    st |= o.status & (SBR_ODE_MAXITERS | SBR_STIFF_SWITCH | SBR_ODE_FAILED);
+    a.n_old[l] = n;
+    a.slots[l] = 0u | (1u << 3) | (2u << 6) | (3u << 9) | (4u << 12);
+    a.xi_new[l] = 0.0;
+    a.bits[l] = st;
+    a.steps[l] = o.naccept + o.nreject;
+    a.work[l] = l;
+    // SolvedModel before any iterate (oracle social_point's initial `out`)
+    a.out.xi[g] = (double)NAN;
+    a.out.tau_in_unc[g] = (double)NAN;
+    a.out.tau_out_unc[g] = (double)NAN;
+    a.out.aw_max[g] = (double)NAN;
+    a.out.tol[g] = (double)INFINITY;
+    a.out.status[g] = 0;
+    if (a.out.iters) a.out.iters[g] = 0;
+    if (a.fp_iters) a.fp_iters[g] = 0;
+    if (st & SBR_KNOT_OVERFLOW) { // engine limit: the point cannot be represented
+        a.out.status[g] = SBR_KNOT_OVERFLOW | SBR_SOCIAL_NOT_CONVERGED;
+        if (a.steps_out) a.steps_out[g] = a.steps[l];
+        a.live[l] = 0;
+    } else {
+        a.live[l] = 1;
+    }
+    if (l == 0) a.count[0] = a.n_pts;
+}
+
+// ============================================================================
+// one fixed-point iterate for every live point of the worklist
+// ============================================================================
+__global__ __launch_bounds__(64) void social_iter_kernel(SocialArgs a, int iter, const int32_t* __restrict__ work,
+                                                         const int32_t* __restrict__ count)
+{
+    const int w = blockIdx.x * 64 + threadIdx.x;
+    if (w >= *count) return;
+    const int l = work[w];
+    if (!a.live[l]) return; // retired by the init kernel (knot overflow)
+    const int64_t g = a.pt0 + l;
+    const int b = (int)(g / a.n_u);
+    const int ju = (int)(g % a.n_u);
+    const double BETA = a.beta[b], ETA = a.eta[b], U = a.u[ju];
+    const double* __restrict__ CMP = a.cmp + (size_t)b * a.n_cmp;
+    const uint32_t P = a.slots[l];
+    const int s_to = P & 7, s_vo = (P >> 3) & 7, s_t = (P >> 6) & 7, s_G = (P >> 9) & 7, s_aw = (P >> 12) & 7;
+    BView TO = buf(a, l, s_to);
+    BView VO = buf(a, l, s_vo);
+    BView T = buf(a, l, s_t);
+    BView Gv = buf(a, l, s_G);
+    BView AWO = buf(a, l, s_aw);
+    double* CMPO = a.cmpo + (size_t)l * a.n_cmp;
+    const int n_old = a.n_old[l];
+    uint32_t bits = a.bits[l];
+    const double xi_old = a.xi_new[l];
+
+    // diagnostics: per-phase shader cycles (SBR_FLAG_DIAG_SOCIAL_PROF)
+    int64_t* PR = a.prof ? a.prof + (size_t)l * 8 : nullptr;
+    int64_t c0 = PR ? (int64_t)clock64() : 0;
+    auto stamp = [&](int k) {
+        if (PR) { const int64_t c1 = (int64_t)clock64(); PR[k] += c1 - c0; c0 = c1; }
+    };
+    // AW_{n-1} on the comparison grid, needed after its buffers are recycled
+    bool cmp_oob = false;
+    {
+        Walker wo;
+        wo.init(TO, VO, n_old);
+        for (int k = 0; k < a.n_cmp; k++) CMPO[k] = wo.at(CMP[k], cmp_oob);
+    }
+
+    stamp(0);
+    // ---- (a) learning from withdrawals on (0, η) ----
+    SocialRhs f;
+    f.init(BETA, TO, VO, n_old);
+    int n = 0;
+    bool overflow = false;
+    auto push = [&](double t, double x, double aw) {
+        if (n >= a.cap) { overflow = true; return false; }
+        T[n] = t;
+        Gv[n] = x;
+        AWO[n] = aw;
+        n++;
+        return true;
+    };
+    OdeOut o;
+    tsit5_social(f, push, ETA, a.x0, a.rtol, a.atol, a.maxiters, o);
+    stamp(1);
+    if (PR) { PR[6] += f.slow; PR[7] += o.naccept + o.nreject; }
+    if (f.oob) o.status |= SBR_OOB;
+    a.steps[l] += o.naccept + o.nreject;
+    bits |= o.status & (SBR_ODE_MAXITERS | SBR_STIFF_SWITCH | SBR_ODE_FAILED);
+
+    bool finish = false, converged = false, stop_oob = false, need_awmax = false;
+    double xi_r = (double)NAN, tin = (double)NAN, tout = (double)NAN, tol_r = (double)INFINITY;
+    uint32_t st_r = 0;
+    int32_t it_r = 0;
+    bool have_r = false;
+    double xi_n = xi_old;
+
+    if (overflow) {
+        finish = true;
+        bits |= SBR_KNOT_OVERFLOW;
+        stop_oob = false;
+    } else if (o.status & SBR_OOB) {
+        finish = true;
+        stop_oob = true; // previous iterate's SolvedModel stays in `out`
+    } else {
+        have_r = true;
+        // ---- hazard_rate (solver.jl:153-185) on τ̄ = knots (t_n = η, else the η
+        // append needs pdf(η) past the grid: BoundsError) ----
+        const bool h_oob = !(n >= 2 && T[n - 1] == ETA);
+        if (h_oob) {
+            st_r = SBR_OOB;
+        } else {
+            BView X = TO; // AW_{n-1} knots are dead now: exp(λτ̄) scratch
+            const double lam = a.lam, p = a.p, omp = 1.0 - p;
+            // pass A: ∫ trapezoid to η
+            double I = 0.0;
+            double ex = sbr_exp(lam * T[0]);
+            X[0] = ex;
+            double eprev = ex * (((1.0 - Gv[0]) * BETA) * AWO[0]);
+            for (int i = 1; i < n; i++) {
+                ex = sbr_exp(lam * T[i]);
+                X[i] = ex;
+                const double ei = ex * (((1.0 - Gv[i]) * BETA) * AWO[i]);
+                I = I + (0.5 * (eprev + ei)) * (T[i] - T[i - 1]);
+                eprev = ei;
+            }
+            const double Ieta = I;
+            // pass B: HR and optimal_buffer's crossing scan (solver.jl:211-264), streamed
+            bool any = false, all = true;
+            int first_above = -1, last_above = -1;
+            double tin_c = ETA, tout_c = ETA;
+            bool have_in = false;
+            I = 0.0;
+            double pdf = ((1.0 - Gv[0]) * BETA) * AWO[0];
+            eprev = X[0] * pdf;
+            double hr_prev = ((p * X[0]) * pdf) / ((p * I) + (omp * Ieta));
+            double tprev = T[0];
+            {
+                const bool ab = hr_prev > U;
+                any |= ab; all &= ab;
+                if (ab) { first_above = 0; last_above = 0; }
+            }
+            for (int i = 1; i < n; i++) {
+                pdf = ((1.0 - Gv[i]) * BETA) * AWO[i];
+                const double ei = X[i] * pdf;
+                const double ti = T[i];
+                I = I + (0.5 * (eprev + ei)) * (ti - tprev);
+                eprev = ei;
+                const double hr = ((p * X[i]) * pdf) / ((p * I) + (omp * Ieta));
+                const bool ab = hr > U, abp = hr_prev > U;
+                any |= ab; all &= ab;
+                if (ab) { if (first_above < 0) first_above = i; last_above = i; }
+                if (!have_in && !abp && ab) {
+                    tin_c = tprev + ((U - hr_prev) * (ti - tprev)) / (hr - hr_prev);
+                    have_in = true;
+                }
+                if (abp && !ab) tout_c = tprev + ((U - hr_prev) * (ti - tprev)) / (hr - hr_prev);
+                hr_prev = hr;
+                tprev = ti;
+            }
+            if (!any) { tin = ETA; tout = ETA; }
+            else if (all) { tin = T[0]; tout = T[n - 1]; }
+            else {
+                tin = tin_c; tout = tout_c;
+                if (tin == ETA) tin = T[first_above];
+                if (tout == ETA) tout = T[last_above];
+            }
+            stamp(2);
+            // ---- solve_equilibrium_baseline (solver.jl:413-462) / compute_ξ (:308-376) ----
+            if (tin == tout) {
+                st_r = SBR_NO_RUN_HR_BELOW_U | SBR_CONVERGED;
+                tol_r = 0.0;
+            } else {
+                const double tolerance = 10.0 * sbr_jl_eps(a.kappa);
+                double xnew = (tin + tout) / 2.0, xmin = tin, xmax = tout;
+                bool boob = false;
+                st_r = SBR_NO_RUN_MAXITER;
+                for (int32_t k = 1; k <= a.bisect_max_iters; k++) {
+                    it_r = k;
+                    const double d = xmin - xmax;
+                    if (fabs(d) < 2.0 * sbr_jl_eps(d)) { st_r = SBR_NO_RUN_COLLAPSE; break; }
+                    if (k == a.bisect_max_iters - 1) { st_r = SBR_NO_RUN_MAXITER; break; }
+                    const double xo = xnew;
+                    const double ic = dmin(tin, xo), oc = dmin(tout, xo);
+                    const double AW = interp_full(T, Gv, n, oc, boob) - interp_full(T, Gv, n, ic, boob);
+                    int idx = -1;
+                    if (xo >= T[0]) idx = ssl_range(T, 0, n - 1, xo);
+                    if (idx < 0 || idx + 1 >= n) { st_r = SBR_OOB; break; }
+                    const double eps = T[idx + 1] - T[idx];
+                    const double AWe =
+                        interp_full(T, Gv, n, oc + eps, boob) - interp_full(T, Gv, n, ic + eps, boob);
+                    if (boob) { st_r = SBR_OOB; break; }
+                    const double err = AW - a.kappa;
+                    const bool inc = AWe >= AW;
+                    if (fabs(err) <= tolerance) {
+                        if (inc) { st_r = SBR_RUN | SBR_CONVERGED; xi_r = xo; tol_r = fabs(err); }
+                        else st_r = SBR_FALSE_EQ;
+                        break;
+                    } else if (err > 0) {
+                        xmax = xo;
+                        xnew = 0.5 * (xo + xmin);
+                    } else {
+                        xmin = xo;
+                        xnew = 0.5 * (xo + xmax);
+                    }
+                }
+            }
+        }
+        stamp(3);
+        if (st_r & SBR_OOB) { tin = h_oob ? (double)NAN : tin; tout = h_oob ? (double)NAN : tout; }
+        if (!(st_r & SBR_RUN)) { xi_r = (double)NAN; tol_r = (st_r & SBR_NO_RUN_HR_BELOW_U) ? 0.0 : (double)INFINITY; }
+
+        if (st_r & SBR_OOB) {
+            finish = true;
+            stop_oob = true;
+        } else {
+            bool stop = false;
+            if (!(st_r & SBR_RUN)) {
+                xi_n = xi_old + ETA / 500.0; // social_learning_solver.jl:150-156
+                if (xi_n > ETA) stop = true;
+            } else {
+                xi_n = xi_r;
+            }
+            if (stop) {
+                finish = true;
+            } else {
+                // get_AW(ξ_n, τ̄_IN, τ̄_OUT, HR, G_n) (solver.jl:495-532) evaluated pointwise
+                const double XI = xi_n;
+                const double ic = (tin >= XI) ? XI : tin;
+                const double oc = (tout > XI) ? XI : tout;
+                bool aoob = false;
+                const double G0 = interp_full(T, Gv, n, 0.0, aoob);
+                Walker wa, wb, wa2, wb2;
+                wa.init(T, Gv, n); wb.init(T, Gv, n); wa2.init(T, Gv, n); wb2.init(T, Gv, n);
+                auto aw_at = [&](double tau, Walker& A, Walker& B) {
+                    const double xa = (tau - XI) + ic;
+                    const double xb = (tau - XI) + oc;
+                    const double gi = A.at(xa > 0 ? xa : 0.0, aoob);
+                    const double go = B.at(xb > 0 ? xb : 0.0, aoob);
+                    const double awin = xa >= 0 ? gi : 0.0;
+                    const double awout = xb >= 0 ? go : 0.0;
+                    return (awout - awin) + G0;
+                };
+                // ∞-norm against AW_{n-1} on range(0, η, 1000) before damping (:162-163, :195-196)
+                double err = 0.0;
+                {
+                    Walker wt;
+                    wt.init(T, T, n);
+                    for (int k = 0; k < a.n_cmp; k++) {
+                        const double c = CMP[k];
+                        double vnew;
+                        if (n < 2 || !(c >= T[0] && c <= T[n - 1])) {
+                            aoob = true;
+                            vnew = (double)NAN;
+                        } else {
+                            const int j = wt.bracket(c);
+                            const double d = (c - T[j]) / (T[j + 1] - T[j]);
+                            vnew = aw_at(T[j], wa, wb) * (1.0 - d) + aw_at(T[j + 1], wa2, wb2) * d;
+                        }
+                        const double dd = fabs(vnew - CMPO[k]);
+                        if (k == 0) err = dd;
+                        else if (!(err != err || err > dd)) err = dd;
+                    }
+                }
+                stamp(4);
+                if (aoob || cmp_oob) {
+                    finish = true;
+                    stop_oob = true;
+                } else if (err < a.tol) {
+                    finish = true;
+                    converged = true;
+                    need_awmax = (st_r & SBR_RUN) != 0;
+                } else {
+                    // damping α = 1/2 on G_n's knots (:174-178, :218-222): AW* at its own
+                    // knot i is aw_i·(1−0) + aw_{i+1}·0 (i < n−1), aw_{n−2}·0 + aw_{n−1}·1
+                    Walker da, db;
+                    da.init(T, Gv, n); db.init(T, Gv, n);
+                    double aw_i = aw_at(T[0], da, db);
+                    for (int i = 0; i < n - 1; i++) {
+                        const double aw_n = aw_at(T[i + 1], da, db);
+                        const double vn = aw_i * (1.0 - 0.0) + aw_n * 0.0;
+                        AWO[i] = 0.5 * AWO[i] + 0.5 * vn;
+                        if (i == n - 2) {
+                            const double vl = aw_i * (1.0 - 1.0) + aw_n * 1.0;
+                            AWO[n - 1] = 0.5 * AWO[n - 1] + 0.5 * vl;
+                        }
+                        aw_i = aw_n;
+                    }
+                    if (aoob) { finish = true; stop_oob = true; }
+                    else if (iter >= a.max_iter) { finish = true; need_awmax = (st_r & SBR_RUN) != 0; }
+                }
+            }
+        }
+    }
+
+    double awmax = (double)NAN;
+    if (need_awmax) { // get_AW_functions!(r).AW_max (solver.jl:553-576) on r's own ξ
+        const double XI = xi_r;
+        const double ic = (tin >= XI) ? XI : tin;
+        const double oc = (tout > XI) ? XI : tout;
+        bool aoob = false;
+        const double G0 = interp_full(T, Gv, n, 0.0, aoob);
+        Walker A, B;
+        A.init(T, Gv, n); B.init(T, Gv, n);
+        double mx = -(double)INFINITY;
+        for (int i = 0; i < n; i++) {
+            const double xa = (T[i] - XI) + ic;
+            const double xb = (T[i] - XI) + oc;
+            const double gi = A.at(xa > 0 ? xa : 0.0, aoob);
+            const double go = B.at(xb > 0 ? xb : 0.0, aoob);
+            const double awin = xa >= 0 ? gi : 0.0;
+            const double awout = xb >= 0 ? go : 0.0;
+            const double v = (awout - awin) + G0;
+            if (mx == mx && (v != v || v > mx)) mx = v;
+        }
+        awmax = mx;
+    }
+
+    stamp(5);
+    // ---- write the iterate's SolvedModel (the oracle's `*out = r`) ----
+    if (have_r) {
+        a.out.xi[g] = xi_r;
+        a.out.tau_in_unc[g] = tin;
+        a.out.tau_out_unc[g] = tout;
+        a.out.aw_max[g] = awmax;
+        a.out.tol[g] = tol_r;
+        a.out.status[g] = st_r;
+        if (a.out.iters) a.out.iters[g] = it_r;
+    }
+    if (!finish && iter >= a.max_iter) finish = true;
+    if (finish) {
+        uint32_t s = a.out.status[g];
+        if (stop_oob) {
+            a.out.xi[g] = (double)NAN;
+            a.out.aw_max[g] = (double)NAN;
+            a.out.tol[g] = (double)INFINITY;
+            s = (s & ~(SBR_RUN | SBR_CONVERGED)) | SBR_OOB;
+        }
+        if (bits & SBR_KNOT_OVERFLOW) {
+            a.out.xi[g] = (double)NAN;
+            a.out.aw_max[g] = (double)NAN;
+            a.out.tol[g] = (double)INFINITY;
+            s = (s & ~(SBR_RUN | SBR_CONVERGED));
+        }
+        s |= bits & (SBR_ODE_MAXITERS | SBR_STIFF_SWITCH | SBR_ODE_FAILED | SBR_KNOT_OVERFLOW);
+        if (!converged) s |= SBR_SOCIAL_NOT_CONVERGED;
+        a.out.status[g] = s;
+        if (a.fp_iters) a.fp_iters[g] = iter;
+        if (a.steps_out) a.steps_out[g] = a.steps[l];
+        a.live[l] = 0;
+    } else {
+        a.live[l] = 1;
+        a.xi_new[l] = xi_n;
+        a.n_old[l] = n;
+        a.bits[l] = bits;
+        // rotate: AW_n = (t_n, damped) ; free = old knots, old values, G_n
+        a.slots[l] = (uint32_t)s_t | ((uint32_t)s_aw << 3) | ((uint32_t)s_to << 6) | ((uint32_t)s_vo << 9) |
+                     ((uint32_t)s_G << 12);
+    }
+}
+
+// ============================================================================
+// order-preserving worklist compaction: one workgroup, ballot + prefix per wave
+// ============================================================================
+constexpr int CMP_BLOCK = 1024;
+
+__global__ __launch_bounds__(CMP_BLOCK) void social_compact_kernel(const int32_t* __restrict__ work_in,
+                                                                   const int32_t* __restrict__ count_in,
+                                                                   const int32_t* __restrict__ live,
+                                                                   int32_t* __restrict__ work_out,
+                                                                   int32_t* __restrict__ count_out)
+{
+    __shared__ int s_wave[CMP_BLOCK / 64];
+    __shared__ int s_base;
+    const int n = *count_in;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (threadIdx.x == 0) s_base = 0;
+    __syncthreads();
+    for (int off = 0; off < n; off += CMP_BLOCK) {
+        const int i = off + threadIdx.x;
+        int id = 0;
+        bool keep = false;
+        if (i < n) {
+            id = work_in[i];
+            keep = live[id] != 0;
+        }
+        const uint64_t m = __ballot(keep);
+        const int before = __popcll(m & ((1ull << lane) - 1ull));
+        if (lane == 0) s_wave[wv] = __popcll(m);
+        __syncthreads();
+        int wbase = s_base;
+        for (int k = 0; k < wv; k++) wbase += s_wave[k];
+        if (keep) work_out[wbase + before] = id;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int tot = 0;
+            for (int k = 0; k < CMP_BLOCK / 64; k++) tot += s_wave[k];
+            s_base += tot;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *count_out = s_base;
+}
+
+hipError_t launch_social_init(const SocialArgs& a, hipStream_t s)
+{
+    hipLaunchKernelGGL(social_init_kernel, dim3((a.n_pts + 63) / 64), dim3(64), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_social_iter(const SocialArgs& a, int iter, const int32_t* work, const int32_t* count,
+                              int32_t* work_out, int32_t* count_out, hipStream_t s)
+{
+    hipLaunchKernelGGL(social_iter_kernel, dim3((a.n_pts + 63) / 64), dim3(64), 0, s, a, iter, work, count);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(social_compact_kernel, dim3(1), dim3(CMP_BLOCK), 0, s, work, count, a.live, work_out,
+                       count_out);
+    return hipGetLastError();
+}
+
+}  // namespace sbr

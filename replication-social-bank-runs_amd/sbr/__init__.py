@@ -14,6 +14,7 @@ from .engine import (  # noqa: F401
     default_engine,
     get_AW_functions,
     solve_equilibrium_baseline,
+    solve_equilibrium_social_learning,
     solve_learning,
 )
 from .grids import BaselineGrid, HeteroGrid, fig4_grid, fig5_grid, hetero_config4, hetero_script_grid, julia_range  # noqa: F401,E501

@@ -25,6 +25,7 @@ SBR_FLAG_EXHAUSTIVE = 0x1
 SBR_FLAG_DIAG_STOP_AFTER_BUFFER = 0x100
 SBR_FLAG_DIAG_STOP_AFTER_BISECT = 0x200
 SBR_FLAG_DIAG_COUNT_AW_BLOCKS = 0x400
+SBR_FLAG_DIAG_SOCIAL_PROF = 0x800
 
 
 class SBRNativeError(RuntimeError):
@@ -45,7 +46,7 @@ class Opts(ctypes.Structure):
         ("knot_capacity", _I32),
         ("hetero_max_iters", _I32),
         ("flags", _I32),
-        ("pad", _I32),
+        ("pad", _I32),  # social sweep knot capacity per buffer (0 = 98304)
     ]
 
 
@@ -91,6 +92,12 @@ _SIGS = {
     "sbr_sweep_hetero": (ctypes.c_int, [_P, _I32, _P, _P, _P, _P, _D, _P, _I64, _I64, _D, _D, _D, _P, _P, _P, _P]),
     "sbr_sweep_hetero_dev": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P, _P, _D, _P, _I64, _I64, _D, _D, _D, _P, _P, _P,
                                             _P]),
+    "sbr_sweep_social": (ctypes.c_int, [_P, _P, _P, _D, _P, _I64, _I64, _D, _D, _D, _P, _I32, _D, _I32, _P, _P, _P,
+                                        _P]),
+    "sbr_sweep_social_dev": (ctypes.c_int, [_P, _P, _P, _P, _D, _P, _I64, _I64, _D, _D, _D, _P, _I32, _D, _I32, _P,
+                                            _P, _P, _P]),
+    "sbr_set_social_workspace": (ctypes.c_int, [_P, _I64]),
+    "sbr_social_prof_read": (ctypes.c_int, [_P, _P]),
 }
 
 _lib: ctypes.CDLL | None = None

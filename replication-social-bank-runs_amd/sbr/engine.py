@@ -7,6 +7,10 @@ Reference call surface → here:
   get_AW_functions!(result)                         solver.jl:553     → get_AW_functions(result)
   the Fig 4 / Fig 5 double loops                    1_baseline.jl:151-192, 224-267
                                                                       → Engine.sweep_baseline(grid)
+  solve_equilibrium_social_learning(model; tol, max_iter)
+                                                    social_learning_solver.jl:63
+                                                                      → solve_equilibrium_social_learning(model)
+                                                                        / Engine.sweep_social(...)
 There is no CPU fallback: without libsbr.so or a GPU every call raises.
 """
 from __future__ import annotations
@@ -19,8 +23,8 @@ import numpy as np
 
 from . import _lib
 from ._lib import ArgumentError, SBRNativeError, check
-from .grids import BaselineGrid
-from .model import EconomicParameters, LearningParameters
+from .grids import BaselineGrid, julia_range
+from .model import EconomicParameters, LearningParameters, ModelParameters
 
 _P = ctypes.c_void_p
 
@@ -183,6 +187,58 @@ class Engine:
                                           ctypes.byref(opts), ctypes.byref(soa), None, None)
         check(rc, self._ctx, "sbr_sweep_hetero_dev")
 
+    def sweep_social(self, beta, eta, u, p, kappa, lam, cmp=None, x0=1e-4, tol=1e-4, max_iter=500,
+                     knot_capacity: int = 0, workspace_bytes: int | None = None) -> dict:
+        """Social-learning sweep (social_learning_solver.jl:63-263) over β columns × u.
+        ``cmp`` [n_beta, n_cmp]: the comparison grids range(0, η_b, length=1000) (built
+        with Julia's range semantics when omitted).  Returns [n_beta, n_u] arrays."""
+        beta = np.ascontiguousarray(np.atleast_1d(beta), np.float64)
+        nb = len(beta)
+        eta = np.ascontiguousarray(np.broadcast_to(eta, (nb,)), np.float64)
+        u = np.ascontiguousarray(np.atleast_1d(u), np.float64)
+        nu = len(u)
+        if cmp is None:
+            cmp = np.stack([julia_range(0.0, float(e), 1000) for e in eta])
+        cmp = np.ascontiguousarray(np.broadcast_to(np.atleast_2d(cmp), (nb, np.atleast_2d(cmp).shape[1])),
+                                   np.float64)
+        out = {k: np.empty(nb * nu) for k in ("xi", "tau_in_unc", "tau_out_unc", "aw_max", "tol")}
+        out["status"] = np.empty(nb * nu, np.uint32)
+        out["iters"] = np.empty(nb * nu, np.int32)
+        out["fp_iters"] = np.empty(nb * nu, np.int32)
+        out["rk_steps"] = np.empty(nb * nu, np.int64)
+        soa = _lib.ResultSoA(*[_ptr(out[k]) for k in ("xi", "tau_in_unc", "tau_out_unc", "aw_max", "tol", "status",
+                                                      "iters")])
+        opts = _lib.default_opts(pad=knot_capacity)
+        if workspace_bytes is not None:
+            check(self._L.sbr_set_social_workspace(self._ctx, int(workspace_bytes)), self._ctx,
+                  "sbr_set_social_workspace")
+        rc = self._L.sbr_sweep_social(self._ctx, _ptr(beta), _ptr(eta), x0, _ptr(u), nb, nu, p, kappa, lam, _ptr(cmp),
+                                      cmp.shape[1], tol, max_iter, ctypes.byref(opts), ctypes.byref(soa),
+                                      _ptr(out["fp_iters"]), _ptr(out["rk_steps"]))
+        check(rc, self._ctx, "sbr_sweep_social")
+        return {k: v.reshape(nb, nu) for k, v in out.items()}
+
+    def sweep_social_dev(self, beta, eta, u, p, kappa, lam, cmp, x0, out: dict, tol=1e-4, max_iter=500,
+                         stream: int | None = None, knot_capacity: int = 0, flags: int = 0):
+        """Device-pointer social sweep on torch tensors (enqueue only)."""
+        nb, nu = beta.numel(), u.numel()
+        soa = _lib.ResultSoA(*[out[k].data_ptr() if out.get(k) is not None else None
+                               for k in ("xi", "tau_in_unc", "tau_out_unc", "aw_max", "tol", "status", "iters")])
+        opts = _lib.default_opts(pad=knot_capacity, flags=flags)
+        fp = out.get("fp_iters")
+        rk = out.get("rk_steps")
+        rc = self._L.sbr_sweep_social_dev(self._ctx, stream, beta.data_ptr(), eta.data_ptr(), x0, u.data_ptr(), nb, nu,
+                                          p, kappa, lam, cmp.data_ptr(), cmp.shape[-1], tol, max_iter,
+                                          ctypes.byref(opts), ctypes.byref(soa),
+                                          fp.data_ptr() if fp is not None else None,
+                                          rk.data_ptr() if rk is not None else None)
+        check(rc, self._ctx, "sbr_sweep_social_dev")
+
+    def social_prof_read(self) -> list[int]:
+        v = (ctypes.c_int64 * 8)()
+        check(self._L.sbr_social_prof_read(self._ctx, v), self._ctx, "sbr_social_prof_read")
+        return list(v)
+
     def device_info(self) -> dict:
         a, b, c = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
         check(self._L.sbr_device_info(self._ctx, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)), self._ctx,
@@ -308,6 +364,27 @@ def solve_equilibrium_baseline(lr: LearningResults, econ: EconomicParameters,
     bankrun = bool(st & _lib.SBR_RUN)
     return SolvedModel(r["xi"], r["tau_in_unc"], r["tau_out_unc"], LinearInterpolation(r["tau"], r["hr"]), bankrun,
                        (lp, econ), lr, bool(st & _lib.SBR_CONVERGED), r["tol"], st, aw_cum=r["aw_cum"])
+
+
+def solve_equilibrium_social_learning(model: ModelParameters, tol: float = 1e-4, max_iter: int = 250,
+                                      engine: Engine | None = None) -> SolvedModel:
+    """social_learning_solver.jl:63-263 for one ModelParameters on the GPU: tspan is
+    overridden to (0, η) (:79); returns the last inner equilibrium like the reference
+    (HR / AW paths are not materialised for the social path; ``status`` carries
+    SBR_SOCIAL_NOT_CONVERGED and the fixed-point iteration count is ``fp_iters``)."""
+    eng = engine or default_engine()
+    lp, econ = model.learning, model.economic
+    r = eng.sweep_social([lp.beta], econ.eta, [econ.u], econ.p, econ.kappa, econ.lam, x0=float(np.ravel(lp.x0)[0]),
+                         tol=tol, max_iter=max_iter)
+    st = int(r["status"][0, 0])
+    lr = LearningResults(LearningParameters(lp.beta, (0.0, econ.eta), lp.x0), None, None, np.empty(0), st)
+    sm = SolvedModel(float(r["xi"][0, 0]), float(r["tau_in_unc"][0, 0]), float(r["tau_out_unc"][0, 0]), None,
+                     bool(st & _lib.SBR_RUN), (lr.params, econ), lr, bool(st & _lib.SBR_CONVERGED),
+                     float(r["tol"][0, 0]), st)
+    sm.fp_iters = int(r["fp_iters"][0, 0])
+    if sm.bankrun:
+        sm.aw = dict(AW_max=float(r["aw_max"][0, 0]))
+    return sm
 
 
 def get_AW_functions(result: SolvedModel):

@@ -63,3 +63,14 @@ def test_no_gpu_means_loud_failure():
         pytest.skip("a GPU is present")
     with pytest.raises(sbr.SBRNativeError):
         sbr.Engine(0)
+
+
+def test_social_entry_points_validate_arguments():
+    """ArgumentError mirrors for the social sweep are raised before any device work
+    (no GPU needed to reach them: a null context is rejected first)."""
+    import ctypes
+    L = sbr.load()
+    soa = sbr._lib.ResultSoA()
+    rc = L.sbr_sweep_social(None, None, None, 1e-4, None, 1, 1, 0.5, 0.5, 0.5, None, 1000, 1e-4, 10, None,
+                            ctypes.byref(soa), None, None)
+    assert rc == sbr._lib.SBR_EARG

@@ -1,0 +1,91 @@
+"""GPU parity for the social-learning extension: the gfx950 fixed-point
+kernels (sbr_social.hip), called through libsbr's C ABI, against the CPU
+oracle's restatement of solve_equilibrium_social_learning
+(social_learning_solver.jl:63-263) — bit for bit on every output field, every
+status bit, the bisection count and the fixed-point iteration count."""
+import numpy as np
+import pytest
+
+import sbr
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = ("xi", "tau_in_unc", "tau_out_unc", "aw_max", "tol")
+ETA = 30.0 / 0.9  # m_social: η = η_bar / β at β = 0.9 (4_social_learning.jl:36-43), carried by copy-modify
+P, KAPPA, LAM = 0.99, 0.25, 0.25
+
+
+def assert_bitwise(a, b, name):
+    a = np.asarray(a)
+    b = np.asarray(b)
+    same = (a == b) | (np.isnan(a) & np.isnan(b))
+    if not same.all():
+        idx = np.argwhere(~same)[:5]
+        raise AssertionError(f"{name}: {int((~same).sum())} mismatches, e.g. "
+                             f"{[(tuple(i), a[tuple(i)], b[tuple(i)]) for i in idx]}")
+
+
+def _compare(g, o):
+    for k in FIELDS:
+        assert_bitwise(g[k], o[k], k)
+    assert_bitwise(g["status"], o["status"], "status")
+    assert_bitwise(g["iters"], o["iters"], "bisection iterations")
+    assert_bitwise(g["fp_iters"], o["fp_iters"], "fixed-point iterations")
+
+
+def _both(engine, oracle, beta, u, tol=1e-4, max_iter=500):
+    cmp = sbr.julia_range(0.0, ETA, 1000)
+    g = engine.sweep_social(beta, ETA, u, P, KAPPA, LAM, cmp=cmp, tol=tol, max_iter=max_iter)
+    o = oracle.sweep_social(beta, ETA, u, P, KAPPA, LAM, cmp, tol=tol, max_iter=max_iter)
+    return g, o
+
+
+def test_social_script_point(engine, oracle, golden):
+    """scripts/4_social_learning.jl:55-56 (β = 0.9, u = 0.5, tol 1e-4, max_iter 500):
+    converges (≈50 iterates of ≈10⁵ Tsit5 steps); GPU == oracle, and ξ* matches the figure."""
+    g, o = _both(engine, oracle, [0.9], [0.5])
+    _compare(g, o)
+    gold = golden("social_learning.json")["social"]
+    assert g["status"][0, 0] & sbr.STATUS["SBR_RUN"]
+    assert not g["status"][0, 0] & sbr.STATUS["SBR_SOCIAL_NOT_CONVERGED"]
+    assert abs(g["xi"][0, 0] - gold["xi"]) <= 1.5 * gold["xi_precision"] + 2e-5
+    assert g["rk_steps"][0, 0] > 10 ** 6
+
+
+def test_social_no_run_and_oob_paths(engine, oracle):
+    """u above every iterate's hazard (ξ += η/500 branch, converging without a run) and
+    a steep β with tiny u whose bisection reads past the (0, η) grid (the reference's
+    BoundsError → SBR_OOB, fixed point stopped)."""
+    g, o = _both(engine, oracle, [0.9], [0.9, 50.0])
+    _compare(g, o)
+    assert np.all(g["status"] & sbr.STATUS["SBR_NO_RUN_HR_BELOW_U"])
+    g, o = _both(engine, oracle, [100.0], [0.001])
+    _compare(g, o)
+    assert g["status"][0, 0] & sbr.STATUS["SBR_OOB"]
+
+
+def test_social_config5_subgrid_capped(engine, oracle):
+    """A subgrid of BASELINE config 5 (β = 1/range(0.01, 2, 512), u = range(0.001, 1, 512))
+    with max_iter = 4: every point stops at the cap, so the result is the 4th iterate's
+    equilibrium incl. AW_max (social_learning_solver.jl:233-242)."""
+    beta = 1.0 / sbr.julia_range("0.01", "2", 512)
+    u = sbr.julia_range("0.001", "1", 512)
+    bsel = beta[[0, 37, 128, 300, 511]]
+    usel = u[[0, 3, 25, 60, 140, 255, 511]]
+    g, o = _both(engine, oracle, bsel, usel, max_iter=4)
+    _compare(g, o)
+    assert (g["fp_iters"] <= 4).all()
+
+
+def test_social_chunked_workspace(engine):
+    """Grids larger than the workspace run in chunks with identical results."""
+    beta = 1.0 / sbr.julia_range("0.01", "2", 512)[::40]
+    u = sbr.julia_range("0.001", "1", 512)[::40]
+    cmp = np.stack([sbr.julia_range(0.0, ETA, 1000)] * len(beta))
+    full = engine.sweep_social(beta, ETA, u, P, KAPPA, LAM, cmp=cmp, max_iter=2)
+    per_pt = 5 * 98304 * 8 + 1000 * 8 + 64
+    small = engine.sweep_social(beta, ETA, u, P, KAPPA, LAM, cmp=cmp, max_iter=2, workspace_bytes=70 * per_pt)
+    engine.sweep_social([0.9], ETA, [0.5], P, KAPPA, LAM, cmp=cmp[:1], max_iter=1, workspace_bytes=0)
+    assert len(beta) * len(u) > 2 * 70
+    for k in FIELDS + ("status", "iters", "fp_iters", "rk_steps"):
+        assert_bitwise(small[k], full[k], k)
