@@ -181,13 +181,19 @@ int sbr_sweep_hetero_dev(sbr_ctx* ctx, void* stream, int32_t K, const double* be
  * Host pointers; synchronous.  The HBM workspace is 5 × capacity doubles per
  * point in flight (opts->pad, default 98304 knots: ≈3.9 MB); large grids run
  * in chunks that fit sbr_set_social_workspace (default 60 % of free HBM).
+ * Points whose iterates outgrow the capacity (the non-converging fringe of
+ * config 5 reaches 450k knots) are re-run from scratch at 4× the capacity,
+ * up to 4M knots, so results equal an unbounded grid's; only beyond that
+ * does a point end with SBR_KNOT_OVERFLOW.
  */
 int sbr_sweep_social(sbr_ctx* ctx, const double* beta, const double* eta, double x0, const double* u, int64_t n_beta,
                      int64_t n_u, double p, double kappa, double lambda, const double* cmp_grid, int32_t n_cmp,
                      double tol, int32_t max_iter, const sbr_opts* opts, sbr_result_soa* out, int32_t* fp_iters,
                      int64_t* rk_steps);
-/* Same on device pointers, enqueued on `stream` without synchronising (all
- * max_iter iterates are launched; finished points drop out of the worklist). */
+/* Same on device pointers, enqueued on `stream` (all max_iter iterates are
+ * launched; finished points drop out of the worklist).  The stream is
+ * synchronised once at the end to find knot-capacity overflows (re-run as
+ * above); the call returns when every point is final. */
 int sbr_sweep_social_dev(sbr_ctx* ctx, void* stream, const double* beta, const double* eta, double x0,
                          const double* u, int64_t n_beta, int64_t n_u, double p, double kappa, double lambda,
                          const double* cmp_grid, int32_t n_cmp, double tol, int32_t max_iter, const sbr_opts* opts,

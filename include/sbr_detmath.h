@@ -8,13 +8,17 @@
  * §8(a) a15).  The GPU's ocml exp/log and glibc's exp/log are both < 1 ulp
  * but not bit-identical, which would make GPU-vs-oracle parity a tolerance
  * question and let run/no-run decisions flip at boundaries.  Both sides
- * therefore call these functions: plain IEEE double arithmetic only (+ - * /,
- * no fma), evaluated in the written order (every consumer is compiled with
- * -ffp-contract=off), so the host and gfx950 results are bit-identical.
+ * therefore call these functions: plain IEEE double arithmetic (+ - * / and
+ * explicit fma(), which is exact on both sides: v_fma_f64 / vfmadd), evaluated
+ * in the written order (every consumer is compiled with -ffp-contract=off),
+ * so the host and gfx950 results are bit-identical.
  *
  * Algorithms: the classic Cody–Waite reduced exp with a degree-5 rational
- * remez correction and the atanh-series log (the fdlibm formulation, public
- * domain algorithm).  Accuracy < 1 ulp in the ranges used here.  They are
+ * remez correction and the atanh-series log (the fdlibm formulations, public
+ * domain algorithms; the log polynomial in fma).  Accuracy < 1 ulp in the
+ * ranges used here.  (An fma/Estrin exp without the division was tried: its
+ * different last-bit rounding moved one column of the 5000² paper mask —
+ * tools/check_mask5000.py — so the figure-pinned formulation stays.)  They are
  * NOT Julia's Base.exp / Base.log bit-for-bit: those are table-driven; the
  * difference is ≤ 1 ulp and is covered by the parity statement in DESIGN.md.
  */
@@ -22,6 +26,9 @@
 #define SBR_DETMATH_H
 
 #include <stdint.h>
+#if !defined(__HIPCC__)
+#include <math.h>
+#endif
 
 #if defined(__HIPCC__)
 #define SBR_HD __host__ __device__ static inline
@@ -92,7 +99,8 @@ SBR_HD double sbr_exp(double x)
 }
 
 /* log: x = 2^k m, m in [sqrt(2)/2, sqrt(2)), log(m) = 2 atanh(f/(2+f)) with
- * the fdlibm polynomial.  Branch-free; special inputs selected at the end. */
+ * the fdlibm polynomial, evaluated in fma.  Branch-free; special inputs
+ * selected at the end. */
 SBR_HD double sbr_log(double x)
 {
     const double Lg1 = 6.666666666666735130e-01, Lg2 = 3.999999999940941908e-01;
@@ -116,10 +124,12 @@ SBR_HD double sbr_log(double x)
     const double s = f / (2.0 + f);
     const double z = s * s;
     const double w = z * z;
-    const double R = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7))) + w * (Lg2 + w * (Lg4 + w * Lg6));
-    const double hfsq = 0.5 * f * f;
+    const double t1 = w * fma(w, fma(w, Lg6, Lg4), Lg2);
+    const double t2 = z * fma(w, fma(w, fma(w, Lg7, Lg5), Lg3), Lg1);
+    const double R = t2 + t1;
+    const double hfsq = (0.5 * f) * f;
     const double dk = (double)k;
-    const double res = dk * SBR_LN2_HI - ((hfsq - (s * (hfsq + R) + dk * SBR_LN2_LO)) - f);
+    const double res = dk * SBR_LN2_HI - ((hfsq - fma(s, hfsq + R, dk * SBR_LN2_LO)) - f);
     const double qnan = sbr_bitsd(0x7ff8000000000000ull);
     const double ninf = sbr_bitsd(0xfff0000000000000ull);
     const double sp = (x != x) ? x : (x < 0.0 ? qnan : (x == 0.0 ? ninf : x)); /* +inf -> +inf */

@@ -93,6 +93,7 @@ __global__ __launch_bounds__(64) void learn_logistic_kernel(const double* __rest
     const double snap = 100.0 * sbr_jl_eps(T1); // fixed_t_for_floatingpoint_error!: t < t_end
     double t = T0, x = x0, qold = CTL_QOLDMIN, lqold = LOG_QOLDMIN;
     AutoSwitch as;
+    const ConstDiv by_gamma(CTL_GAMMA);
     int naccept = 0, nreject = 0;
     push(t, x);
     int64_t iter = 0;
@@ -129,7 +130,7 @@ __global__ __launch_bounds__(64) void learn_logistic_kernel(const double* __rest
         } else {
             le = sbr_log(EEst);
             q = sbr_exp(CTL_BETA1 * le - CTL_BETA2 * lqold);
-            q = dmax(CTL_INV_QMAX, dmin(CTL_INV_QMIN, q / CTL_GAMMA));
+            q = dmax(CTL_INV_QMAX, dmin(CTL_INV_QMIN, by_gamma(q)));
         }
         if (EEst <= 1.0) {
             naccept++;
@@ -146,7 +147,7 @@ __global__ __launch_bounds__(64) void learn_logistic_kernel(const double* __rest
         } else {
             nreject++;
             const double q11 = sbr_exp(CTL_BETA1 * le);
-            dt = dt / dmin(CTL_INV_QMIN, q11 / CTL_GAMMA);
+            dt = dt / dmin(CTL_INV_QMIN, by_gamma(q11));
         }
         if (!(dt > 0.0) || !isfinite(dt)) { st |= SBR_ODE_FAILED; break; }
         as.update(eig, dt);

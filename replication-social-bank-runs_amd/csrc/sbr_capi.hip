@@ -660,7 +660,8 @@ int sbr_set_social_workspace(sbr_ctx* c, int64_t bytes)
 }  // extern "C"
 
 namespace {
-constexpr int kSocialDefaultCap = 98304; // ≈1.4× the longest iterate seen on config 5 (≈70k knots)
+constexpr int kSocialDefaultCap = 98304;  // ≈1.4× the typical longest iterate on config 5 (≈70k knots)
+constexpr int kSocialMaxCap = 1 << 22;    // overflow retries grow 4× per pass up to this
 
 int social_checks(sbr_ctx* c, const double* beta, const double* eta, const double* u, int64_t n_beta, int64_t n_u,
                   double x0, double p, double kappa, double lambda, const double* cmp, int32_t n_cmp, double tol,
@@ -675,16 +676,14 @@ int social_checks(sbr_ctx* c, const double* beta, const double* eta, const doubl
     return SBR_OK;
 }
 
-// the whole fixed point for every point, chunked by workspace size; poll > 0
-// reads the live count every `poll` iterates and stops once it is zero
-int run_social(sbr_ctx* c, hipStream_t s, const double* beta, const double* eta, double x0, const double* u,
-               int64_t n_beta, int64_t n_u, double p, double kappa, double lambda, const double* cmp, int32_t n_cmp,
-               double tol, int32_t max_iter, const sbr_opts& o, sbr_result_soa* out, int32_t* fp_iters,
-               int64_t* rk_steps, int poll)
+// one pass of the whole fixed point over points [0, n_total) (list == nullptr)
+// or over the global point indices list[0 .. n_total), chunked by workspace
+// size; poll > 0 reads the live count every `poll` iterates and stops early.
+int run_social_pass(sbr_ctx* c, hipStream_t s, const double* beta, const double* eta, double x0, const double* u,
+                    int64_t n_u, double p, double kappa, double lambda, const double* cmp, int32_t n_cmp, double tol,
+                    int32_t max_iter, const sbr_opts& o, sbr_result_soa* out, int32_t* fp_iters, int64_t* rk_steps,
+                    int poll, size_t cap, const int64_t* list, int64_t n_total)
 {
-    const int64_t n_total = n_beta * n_u;
-    size_t cap = o.pad > 0 ? (size_t)o.pad : (size_t)kSocialDefaultCap;
-    cap = (cap + 15) & ~(size_t)15; // 16-knot lines of the wave-blocked layout
     const size_t per_pt = 5 * cap * 8 + (size_t)n_cmp * 8 + 64;
     int64_t budget = c->so_budget;
     if (budget <= 0) {
@@ -693,10 +692,11 @@ int run_social(sbr_ctx* c, hipStream_t s, const double* beta, const double* eta,
         budget = (int64_t)((double)(fr + c->so_pts * (5 * c->so_cap * 8 + c->so_cmp * 8 + 64)) * 0.6);
     }
     int64_t chunk = budget / (int64_t)per_pt;
-    if (chunk < 64) return fail(c, SBR_ENOMEM, "social workspace budget below 64 points");
+    if (chunk < 64 && !list) return fail(c, SBR_ENOMEM, "social workspace budget below 64 points");
+    if (chunk < 1) chunk = 1; // overflow retries: at least one point at a time
     if (chunk > (1 << 30)) chunk = 1 << 30;
     if (chunk >= n_total) chunk = n_total;
-    else chunk &= ~(int64_t)63; // whole wave groups
+    else if (chunk >= 64) chunk &= ~(int64_t)63; // whole wave groups
     int rc = ensure_social(c, (size_t)chunk, cap, (size_t)n_cmp);
     if (rc) return rc;
     const bool prof = (o.flags & SBR_FLAG_DIAG_SOCIAL_PROF) != 0;
@@ -707,12 +707,12 @@ int run_social(sbr_ctx* c, hipStream_t s, const double* beta, const double* eta,
         HIP_TRY(c, hipMalloc(&c->so_prof, (size_t)chunk * 64), SBR_ENOMEM);
         c->so_prof_pts = (size_t)chunk;
     }
-    c->so_prof_acc.assign(8, 0);
     for (int64_t pt0 = 0; pt0 < n_total; pt0 += chunk) {
         const int32_t npts = (int32_t)((n_total - pt0) < chunk ? (n_total - pt0) : chunk);
         sbr::SocialArgs a{};
         a.beta = beta; a.eta = eta; a.u = u; a.cmp = cmp;
-        a.pt0 = pt0; a.n_pts = npts; a.n_u = (int32_t)n_u; a.n_cmp = n_cmp;
+        a.pt0 = list ? 0 : pt0; a.pts = list ? list + pt0 : nullptr;
+        a.n_pts = npts; a.n_u = (int32_t)n_u; a.n_cmp = n_cmp;
         a.max_iter = max_iter; a.bisect_max_iters = o.bisect_max_iters; a.cap = (int32_t)cap;
         a.maxiters = o.ode_maxiters;
         a.x0 = x0; a.p = p; a.kappa = kappa; a.lam = lambda; a.tol = tol; a.rtol = o.ode_reltol; a.atol = o.ode_abstol;
@@ -748,6 +748,48 @@ int run_social(sbr_ctx* c, hipStream_t s, const double* beta, const double* eta,
             HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
             for (size_t i = 0; i < h.size(); i++) c->so_prof_acc[i & 7] += h[i];
         }
+    }
+    return SBR_OK;
+}
+
+// Every point at the default knot capacity, then the (few) points whose iterates
+// outgrew it again, from scratch, at 4x the capacity, up to kSocialMaxCap: the
+// results are those of an unbounded grid.  Finding them synchronises `s` once.
+int run_social(sbr_ctx* c, hipStream_t s, const double* beta, const double* eta, double x0, const double* u,
+               int64_t n_beta, int64_t n_u, double p, double kappa, double lambda, const double* cmp, int32_t n_cmp,
+               double tol, int32_t max_iter, const sbr_opts& o, sbr_result_soa* out, int32_t* fp_iters,
+               int64_t* rk_steps, int poll)
+{
+    const int64_t n_total = n_beta * n_u;
+    size_t cap = o.pad > 0 ? (size_t)o.pad : (size_t)kSocialDefaultCap;
+    cap = (cap + 15) & ~(size_t)15; // 16-knot lines of the wave-blocked layout
+    c->so_prof_acc.assign(8, 0);
+    int rc = run_social_pass(c, s, beta, eta, x0, u, n_u, p, kappa, lambda, cmp, n_cmp, tol, max_iter, o, out,
+                             fp_iters, rk_steps, poll, cap, nullptr, n_total);
+    if (rc) return rc;
+    std::vector<uint32_t> st((size_t)n_total);
+    int64_t* dlist = nullptr;
+    while (cap < (size_t)kSocialMaxCap) {
+        HIP_TRY(c, hipMemcpyAsync(st.data(), out->status, (size_t)n_total * 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
+        std::vector<int64_t> idx;
+        for (int64_t g = 0; g < n_total; g++)
+            if (st[(size_t)g] & SBR_KNOT_OVERFLOW) idx.push_back(g);
+        if (idx.empty()) break;
+        cap = cap * 4 < (size_t)kSocialMaxCap ? cap * 4 : (size_t)kSocialMaxCap;
+        if (dlist) (void)hipFree(dlist);
+        dlist = nullptr;
+        HIP_TRY(c, hipMalloc(&dlist, idx.size() * 8), SBR_ENOMEM);
+        hipError_t e = hipMemcpyAsync(dlist, idx.data(), idx.size() * 8, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) { (void)hipFree(dlist); return fail(c, SBR_EDEVICE, "overflow list", e); }
+        rc = run_social_pass(c, s, beta, eta, x0, u, n_u, p, kappa, lambda, cmp, n_cmp, tol, max_iter, o, out,
+                             fp_iters, rk_steps, poll, cap, dlist, (int64_t)idx.size());
+        if (rc) { (void)hipFree(dlist); return rc; }
+    }
+    if (dlist) {
+        (void)hipStreamSynchronize(s);
+        (void)hipFree(dlist);
     }
     return SBR_OK;
 }

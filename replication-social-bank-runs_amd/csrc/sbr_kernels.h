@@ -76,6 +76,7 @@ struct SocialArgs {
     const double* u;     // [n_u]
     const double* cmp;   // [n_beta][n_cmp] comparison grids range(0, η, n_cmp)
     int64_t pt0;         // first global point (β-major, u-fastest) of this chunk
+    const int64_t* pts;  // or: explicit global point indices (overflow retries), may be null
     int32_t n_pts;       // points in this chunk
     int32_t n_u;
     int32_t n_cmp;

@@ -36,7 +36,12 @@ namespace {
 // MiB instead of 64 separate multi-MiB rows (page/TLB locality).
 struct BView {
     double* p; // ws + (group·5 + slot)·cap·64 + lane·16
-    __device__ __forceinline__ double& operator[](int k) const { return p[((k >> 4) << 10) + (k & 15)]; }
+    // 32-bit byte offset (a group's buffer is < 4 GiB): one shift-and-or pair, no sign extension
+    __device__ __forceinline__ double& operator[](int k) const
+    {
+        const uint32_t u = (uint32_t)k;
+        return *(double*)((char*)p + (((u >> 4) << 13) | ((u & 15u) << 3)));
+    }
 };
 
 // Bracket search with an 8-knot window of knot times held in registers: the
@@ -185,6 +190,7 @@ __device__ __forceinline__ void tsit5_scalar(Rhs& f, Sink& push, double T1, doub
     const double snap = 100.0 * sbr_jl_eps(T1);
     double t = T0, x = x0, lqold = LOG_QOLDMIN;
     AutoSwitch as;
+    const ConstDiv by_gamma(CTL_GAMMA);
     if (!push(t, x, false)) return; // (the last RHS call was at T0 + dt0, not T0)
     int64_t iter = 0;
     while (t < T1) {
@@ -216,7 +222,7 @@ __device__ __forceinline__ void tsit5_scalar(Rhs& f, Sink& push, double T1, doub
         } else {
             le = sbr_log(EEst);
             q = sbr_exp(CTL_BETA1 * le - CTL_BETA2 * lqold);
-            q = dmax(CTL_INV_QMAX, dmin(CTL_INV_QMIN, q / CTL_GAMMA));
+            q = dmax(CTL_INV_QMAX, dmin(CTL_INV_QMIN, by_gamma(q)));
         }
         if (EEst <= 1.0) {
             o.naccept++;
@@ -234,7 +240,7 @@ __device__ __forceinline__ void tsit5_scalar(Rhs& f, Sink& push, double T1, doub
         } else {
             o.nreject++;
             const double q11 = sbr_exp(CTL_BETA1 * le);
-            dt = dt / dmin(CTL_INV_QMIN, q11 / CTL_GAMMA);
+            dt = dt / dmin(CTL_INV_QMIN, by_gamma(q11));
         }
         if (!(dt > 0.0) || !isfinite(dt)) { o.status |= SBR_ODE_FAILED; break; }
         as.update(eig, dt);
@@ -295,14 +301,19 @@ struct SocialRhs {
         for (int k = 0; k < 5; k++) {
             in[k] = n >= 2 && xs[k] >= tfirst && xs[k] <= tlast;
             slow += (in[k] && !(xs[k] < w.tw[7])) ? 1 : 0;
-            js[k] = in[k] ? w.find(xs[k]) : 0;
+            js[k] = w.find(in[k] ? xs[k] : tfirst);
         }
         // 20 independent operand loads, then five independent divisions
+#ifdef SBR_EXPERIMENT_NOLOOKUP
+#pragma unroll
+        for (int k = 0; k < 5; k++) aw[k] = in[k] ? 0.5 + 1e-3 * xs[k] : (double)NAN;
+#else
 #pragma unroll
         for (int k = 0; k < 5; k++) {
             aw[k] = lerp_sel(to, vo, n, js[k], xs[k], in[k]);
             oob |= !in[k];
         }
+#endif
         last_aw = aw[4];
     }
     // stage s = 1..6 (k2..k7): times C1..C4, then t + dt twice
@@ -351,6 +362,7 @@ __device__ __forceinline__ void tsit5_social(SocialRhs& f, Sink& push, double T1
     const double snap = 100.0 * sbr_jl_eps(T1);
     double t = T0, x = x0, lqold = LOG_QOLDMIN;
     AutoSwitch as;
+    const ConstDiv by_gamma(CTL_GAMMA);
     if (!push(t, x, aw0)) return;
     int64_t iter = 0;
     while (t < T1) {
@@ -383,7 +395,7 @@ __device__ __forceinline__ void tsit5_social(SocialRhs& f, Sink& push, double T1
         } else {
             le = sbr_log(EEst);
             q = sbr_exp(CTL_BETA1 * le - CTL_BETA2 * lqold);
-            q = dmax(CTL_INV_QMAX, dmin(CTL_INV_QMIN, q / CTL_GAMMA));
+            q = dmax(CTL_INV_QMAX, dmin(CTL_INV_QMIN, by_gamma(q)));
         }
         if (EEst <= 1.0) {
             o.naccept++;
@@ -403,7 +415,7 @@ __device__ __forceinline__ void tsit5_social(SocialRhs& f, Sink& push, double T1
         } else {
             o.nreject++;
             const double q11 = sbr_exp(CTL_BETA1 * le);
-            dt = dt / dmin(CTL_INV_QMIN, q11 / CTL_GAMMA);
+            dt = dt / dmin(CTL_INV_QMIN, by_gamma(q11));
         }
         if (!(dt > 0.0) || !isfinite(dt)) { o.status |= SBR_ODE_FAILED; break; }
         as.update(eig, dt);
@@ -420,7 +432,7 @@ __global__ __launch_bounds__(64) void social_init_kernel(SocialArgs a)
 {
     const int l = blockIdx.x * 64 + threadIdx.x;
     if (l >= a.n_pts) return;
-    const int64_t g = a.pt0 + l;
+    const int64_t g = a.pts ? a.pts[l] : a.pt0 + l;
     const int b = (int)(g / a.n_u);
     const double BETA = a.beta[b], ETA = a.eta[b];
     BView T = buf(a, l, 0);
@@ -473,7 +485,7 @@ __global__ __launch_bounds__(64) void social_iter_kernel(SocialArgs a, int iter,
     if (w >= *count) return;
     const int l = work[w];
     if (!a.live[l]) return; // retired by the init kernel (knot overflow)
-    const int64_t g = a.pt0 + l;
+    const int64_t g = a.pts ? a.pts[l] : a.pt0 + l;
     const int b = (int)(g / a.n_u);
     const int ju = (int)(g % a.n_u);
     const double BETA = a.beta[b], ETA = a.eta[b], U = a.u[ju];

@@ -6,12 +6,13 @@ missing, the calls raise ``SBRNativeError``.
 from __future__ import annotations
 
 import ctypes
+import os
 import re
 from pathlib import Path
 
 PKG_ROOT = Path(__file__).resolve().parent.parent  # replication-social-bank-runs_amd/
 REPO_ROOT = PKG_ROOT.parent
-LIB_PATH = PKG_ROOT / "lib" / "libsbr.so"
+LIB_PATH = Path(os.environ["SBR_LIB"]) if os.environ.get("SBR_LIB") else PKG_ROOT / "lib" / "libsbr.so"
 HEADER = REPO_ROOT / "include" / "sbr.h"
 STATUS_HEADER = REPO_ROOT / "include" / "sbr_status.h"
 

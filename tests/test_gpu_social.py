@@ -53,15 +53,20 @@ def test_social_script_point(engine, oracle, golden):
 
 
 def test_social_no_run_and_oob_paths(engine, oracle):
-    """u above every iterate's hazard (ξ += η/500 branch, converging without a run) and
-    a steep β with tiny u whose bisection reads past the (0, η) grid (the reference's
-    BoundsError → SBR_OOB, fixed point stopped)."""
+    """u above every iterate's hazard (ξ += η/500 branch, converging without a run), and
+    two small-u points of the config-5 grid whose fixed point ends in the reference's
+    BoundsError (SBR_OOB): one in the bisection's ε lookup past the (0, η) grid, one in
+    the forced ODE itself (a stage time past AW_old's last knot → SBR_ODE_FAILED)."""
     g, o = _both(engine, oracle, [0.9], [0.9, 50.0])
     _compare(g, o)
     assert np.all(g["status"] & sbr.STATUS["SBR_NO_RUN_HR_BELOW_U"])
-    g, o = _both(engine, oracle, [100.0], [0.001])
-    _compare(g, o)
-    assert g["status"][0, 0] & sbr.STATUS["SBR_OOB"]
+    beta = 1.0 / sbr.julia_range("0.01", "2", 512)
+    u = sbr.julia_range("0.001", "1", 512)
+    for b, uu in ((beta[20], u[3]), (beta[0], u[2])):
+        g, o = _both(engine, oracle, [b], [uu])
+        _compare(g, o)
+        assert g["status"][0, 0] & sbr.STATUS["SBR_OOB"]
+        assert g["status"][0, 0] & sbr.STATUS["SBR_SOCIAL_NOT_CONVERGED"]
 
 
 def test_social_config5_subgrid_capped(engine, oracle):

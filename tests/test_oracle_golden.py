@@ -162,3 +162,24 @@ def test_no_autoswitch_on_config_grid(oracle):
     for b in grid.beta[::16]:
         t, G, st = oracle.learn_logistic(float(b), 30.0)
         assert st["status"] & sbr.STATUS["SBR_STIFF_SWITCH"] == 0
+
+
+def test_fig5_5000_mask_boundaries(oracle, golden):
+    """The 5000² paper mask (comp_stat_cross_heatmap_AW_large.pdf) at every
+    column's run/no-run boundary on the CPU oracle: u index P−1 runs, P does not
+    (the full 25M-point mask is checked on the GPU)."""
+    grid = sbr.fig5_grid(5000)
+    pref = np.array(golden("fig5_prefix.json")["n5000"]["prefix"])
+    RUN = sbr.STATUS["SBR_RUN"]
+    from concurrent.futures import ThreadPoolExecutor
+
+    def col(c):
+        P = int(pref[c])
+        idx = [i for i in (P - 1, P) if 0 <= i < len(grid.u)]
+        r = oracle.sweep_baseline([grid.beta[c]], 15.0, 30.0, grid.u[idx], grid.p, grid.kappa, grid.lam, grid.x0)
+        run = (r["status"][0] & RUN) > 0
+        return all(run[k] == (i < P) for k, i in enumerate(idx))
+
+    with ThreadPoolExecutor(8) as ex:
+        ok = list(ex.map(col, range(len(grid.beta))))
+    assert all(ok), [c for c, v in enumerate(ok) if not v]
