@@ -64,8 +64,10 @@ def parse():
     ap.add_argument("--phases", action="store_true",
                     help="also time the equilibrium kernel stopped after each stage (diagnostic flags)")
     ap.add_argument("--traffic", default=str(REPO / "profiles" / "traffic_latest.json"))
-    ap.add_argument("--workload", choices=("baseline", "social"), default="baseline",
-                    help="baseline: BASELINE config 3 (the metric); social: config 5 per-GPU share")
+    ap.add_argument("--workload", choices=("baseline", "social", "hetero"), default="baseline",
+                    help="baseline: BASELINE config 3 (the metric); social: config 5 per-GPU share; "
+                         "hetero: config 4 (K = 8, 1024x1024 per GPU)")
+    ap.add_argument("--hetero-n", type=int, default=1024, help="hetero: columns per GPU and u rows")
     ap.add_argument("--social-cols", type=int, default=64, help="social: β columns per GPU (config 5: 512/8)")
     ap.add_argument("--social-max-iter", type=int, default=500)
     ap.add_argument("--social-prof", action="store_true", help="social: per-phase cycle breakdown (diagnostic)")
@@ -76,6 +78,8 @@ def main():
     a = parse()
     if a.workload == "social":
         return main_social(a)
+    if a.workload == "hetero":
+        return main_hetero(a)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -223,6 +227,100 @@ def main():
         dist.destroy_process_group()
 
 
+def main_hetero(a):
+    """BASELINE config 4 (concretised in SURVEY.md §8(d), sbr.grids.hetero_config4): K = 8
+    learning groups, βs_k = s·0.125·100^((k−1)/7), dist_k = 1/8, s = 1/range(1e-3, 1, n·N),
+    u = range(0.001, 1, n), η = η_bar/Σdist·βs per column, tspan carried from s = 1.
+    Weak scaling: rank r owns columns r, r+N, …  One step = learning (K-group Tsit5 +
+    K hazards) for every column and buffers + ξ bisection + validity check + AW_max for
+    every (column, u)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    n = a.hetero_n
+    full = sbr.hetero_config4(n * world, n, K=8)
+    g = full.subset(np.arange(rank, n * world, world))
+    nb, nu, K = g.betas.shape[0], len(g.u), g.K
+    betas = torch.from_numpy(np.ascontiguousarray(g.betas)).to(dev)
+    distw = torch.from_numpy(g.dist).to(dev)
+    eta = torch.from_numpy(np.ascontiguousarray(g.eta)).to(dev)
+    t_end = torch.from_numpy(np.ascontiguousarray(g.t_end)).to(dev)
+    u = torch.from_numpy(g.u).to(dev)
+    out = {k: torch.empty(nb * nu, dtype=torch.float64, device=dev) for k in ("xi", "aw_max", "tol")}
+    out["status"] = torch.empty(nb * nu, dtype=torch.int32, device=dev)
+    out["iters"] = torch.empty(nb * nu, dtype=torch.int32, device=dev)
+    eng = sbr.Engine(local)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    gather = world > 1 and not a.no_gather
+    g_aw = [torch.empty(nb * nu, dtype=torch.float64, device=dev) for _ in range(world)] if gather and rank == 0 \
+        else None
+
+    def step():
+        eng.sweep_hetero_dev(K, betas, distw, eta, t_end, u, g.p, g.kappa, g.lam, g.x0, out, stream=stream)
+        if gather:
+            dist.gather(out["aw_max"], g_aw, dst=0)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    eng.timing_read(stream)
+    eng.timing_enable(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    learn_ms, eq_ms, ncalls = eng.timing_read(stream)
+    eng.timing_enable(False)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    st = out["status"].cpu().numpy().view(np.uint32)
+    res = {
+        "metric": "equilibria solved/sec on β×u grid (FP64), heterogeneity extension K=8",
+        "value": nb * nu * world * a.steps / elapsed,
+        "unit": "equilibria/s",
+        "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (deterministic config-4 parameter grid; no RNG in the reference)",
+        "config": {"workload": f"hetero_K8_{nb}x{nu}_per_gpu (BASELINE config 4)", "n_col_per_gpu": nb,
+                   "n_u": nu, "K": K, "eta_bar": 30.0, "p": g.p, "kappa": g.kappa, "lambda": g.lam,
+                   "parallelism": f"column shards x{world}"},
+        "kernel_ms_per_step": {"learn_hetero": learn_ms / max(ncalls, 1), "equilibrium_hetero": eq_ms / max(ncalls, 1)},
+        "run_fraction": float(((st & sbr.STATUS["SBR_RUN"]) > 0).mean()),
+        "stiff_switch_fraction": float(((st & sbr.STATUS["SBR_STIFF_SWITCH"]) > 0).mean()),
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        sys.path.insert(0, str(REPO / "oracle"))
+        import oracle as O  # noqa: E402  (test infrastructure: cpu_baseline leg only)
+
+        O.build()
+        cores = max(1, min(16, len(os.sched_getaffinity(0))))
+        sub = g.subset(np.arange(0, nb, 16))
+        t1 = time.perf_counter()
+        O.sweep_hetero(sub.betas, sub.dist, sub.eta, sub.t_end, sub.u, sub.p, sub.kappa, sub.lam, sub.x0,
+                       nthreads=cores)
+        dt = time.perf_counter() - t1
+        pts = sub.betas.shape[0] * nu
+        res["cpu_baseline"] = {"value": pts / dt, "unit": "equilibria/s", "cores": cores, "kind": "port",
+                               "sample": f"{sub.betas.shape[0]} columns (every 16th) x {nu} u = {pts} equilibria "
+                                         f"in {dt:.2f} s"}
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main_social(a):
     """BASELINE config 5: the social-learning fixed point (social_learning_solver.jl:63-263,
     tol 1e-4, max_iter 500 as in scripts/4_social_learning.jl:55) on β = 1/range(0.01, 2, 512)
@@ -312,6 +410,21 @@ def main_social(a):
         "run_fraction": float(((st & sbr.STATUS["SBR_RUN"]) > 0).mean()),
         "not_converged_fraction": float(((st & sbr.STATUS["SBR_SOCIAL_NOT_CONVERGED"]) > 0).mean()),
     }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        sys.path.insert(0, str(REPO / "oracle"))
+        import oracle as O  # noqa: E402  (test infrastructure: cpu_baseline leg only)
+
+        O.build()
+        cores = max(1, min(16, len(os.sched_getaffinity(0))))
+        bsel, usel = beta_h[::8], u_h[::128]  # 8 β x 4 u = 32 points spread over the grid
+        t1 = time.perf_counter()
+        O.sweep_social(bsel, eta_v, usel, p, kappa, lam, cmp_h[: len(bsel)], x0=x0, tol=tol,
+                       max_iter=a.social_max_iter, nthreads=cores)
+        dt = time.perf_counter() - t1
+        pts = len(bsel) * len(usel)
+        res["cpu_baseline"] = {"value": pts / dt, "unit": "equilibria/s", "cores": cores, "kind": "port",
+                               "sample": f"{len(bsel)} β (every 8th) x {len(usel)} u (every 128th) = {pts} "
+                                         f"fixed points in {dt:.2f} s"}
     if a.social_prof:
         pr = eng.social_prof_read()
         names = ("cmp_prelude", "ode", "hazard_scan", "bisection", "aw_norm", "damping_awmax")

@@ -1,8 +1,8 @@
 #=
 SBREngine.jl — Julia binding of libsbr (include/sbr.h) for the reference's scripts.
 
-Drop-in for the β×u loops of scripts/1_baseline.jl (Fig 4 :151-192, Fig 5 :224-267) and the
-heterogeneity sweep: one `ccall` per grid instead of one solve_learning /
+Drop-in for the β×u loops of scripts/1_baseline.jl (Fig 4 :151-192, Fig 5 :224-267), the
+heterogeneity sweep and the social-learning fixed point over a grid: one `ccall` per grid instead of one solve_learning /
 solve_equilibrium_baseline / get_AW_functions! per point.  Plain-pointer C ABI; Julia owns every
 array (`GC.@preserve`), the library owns device memory.
 
@@ -18,6 +18,8 @@ const libsbr = joinpath(@__DIR__, "..", "lib", "libsbr.so")
 const SBR_RUN = UInt32(0x0001)
 const SBR_CONVERGED = UInt32(0x0002)
 const SBR_SKIPPED_EARLY_EXIT = UInt32(0x0100)
+const SBR_OOB = UInt32(0x0080)
+const SBR_SOCIAL_NOT_CONVERGED = UInt32(0x1000)
 
 struct Opts            # sbr_opts
     ode_reltol::Float64
@@ -30,7 +32,8 @@ struct Opts            # sbr_opts
     flags::Int32
     pad::Int32
 end
-Opts(; early_exit = 5) = Opts(eps(), eps(), 100_000, 100, early_exit, 8192, 500, 0, 0)
+# pad = social knot capacity per buffer (0: library default 98304)
+Opts(; early_exit = 5) = Opts(eps(), eps(), 1_000_000, 100, early_exit, 65536, 500, 0, 0)
 
 struct ResultSoA       # sbr_result_soa
     xi::Ptr{Float64}
@@ -114,6 +117,42 @@ function solve_equilibrium_hetero_grid(ctx::Context, βs_cols::AbstractMatrix, d
         check(ctx, rc)
     end
     return (AW_max = aw, ξ = xi, τ_bar_IN_UNCs = tin, τ_bar_OUT_UNCs = tout, status = st)
+end
+
+"""
+    solve_equilibrium_social_learning_grid(ctx, β_vals, u_vals; η, x0, p, κ, λ, tol=1e-4, max_iter=500)
+
+Batched `solve_equilibrium_social_learning(ModelParameters(…); tol, max_iter)`
+(src/extensions/social_learning/social_learning_solver.jl:63-263) for every (β, u), plus
+`get_AW_functions!(result).AW_max`.  `η` per β (copy-modify carries η = η_bar/β_base as in
+scripts/4_social_learning.jl); the comparison grid of :103 is handed over as Julia's own
+`collect(range(0.0, η, length = 1000))`.  Returns [u, β] matrices; `fp_iters` = fixed-point
+iterations; `status & SBR_SOCIAL_NOT_CONVERGED` marks points the reference leaves unconverged
+(or where it would raise a BoundsError: `SBR_OOB`).
+"""
+function solve_equilibrium_social_learning_grid(ctx::Context, β_vals, u_vals; η, x0 = 1e-4, p = 0.99,
+                                                κ = 0.25, λ = 0.25, tol = 1e-4, max_iter = 500)
+    β = collect(Float64, β_vals); u = collect(Float64, u_vals)
+    nb, nu = length(β), length(u)
+    ηv = fill(Float64(η), nb) .+ 0 .* β
+    cmp = reduce(hcat, [collect(range(0.0, e, length = 1000)) for e in ηv])   # 1000 × nb, column b = β_b's grid
+    xi = Matrix{Float64}(undef, nu, nb); tin = similar(xi); tout = similar(xi)
+    aw = similar(xi); tl = similar(xi); st = Matrix{UInt32}(undef, nu, nb)
+    fp = Matrix{Int32}(undef, nu, nb); steps = Matrix{Int64}(undef, nu, nb)
+    opts = Ref(Opts(; early_exit = 0))
+    GC.@preserve β u ηv cmp xi tin tout aw tl st fp steps begin
+        soa = Ref(ResultSoA(pointer(xi), pointer(tin), pointer(tout), pointer(aw), pointer(tl), pointer(st),
+                            Ptr{Int32}(C_NULL)))
+        rc = ccall((:sbr_sweep_social, libsbr), Cint,
+                   (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Float64, Ptr{Float64}, Int64, Int64, Float64, Float64,
+                    Float64, Ptr{Float64}, Int32, Float64, Int32, Ref{Opts}, Ref{ResultSoA}, Ptr{Int32},
+                    Ptr{Int64}),
+                   ctx.ptr, β, ηv, x0, u, nb, nu, p, κ, λ, cmp, Int32(1000), tol, Int32(max_iter), opts, soa,
+                   fp, steps)
+        check(ctx, rc)
+    end
+    return (AW_max = aw, ξ = xi, τ_bar_IN_UNC = tin, τ_bar_OUT_UNC = tout, tolerance = tl, status = st,
+            fp_iters = fp, rk_steps = steps)
 end
 
 end # module

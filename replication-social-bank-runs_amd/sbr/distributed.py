@@ -18,9 +18,10 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from .grids import BaselineGrid
+from .grids import BaselineGrid, HeteroGrid, julia_range
 
 FLOAT_FIELDS = ("xi", "tau_in_unc", "tau_out_unc", "aw_max", "tol")
+INT_FIELDS = ("status", "iters", "fp_iters")
 
 
 def shard_columns(n_cols: int, world: int, rank: int) -> np.ndarray:
@@ -35,17 +36,19 @@ def max_shard(n_cols: int, world: int) -> int:
 def gather_columns(local: dict, n_cols: int, n_u: int, world: int, rank: int, device, root: int = 0):
     """Gather per-rank column blocks (numpy [n_local, n_u]) to `root` and put
     them back in global column order.  Returns the full dict on root, None
-    elsewhere.  Each field travels as one padded tensor per rank (RCCL/gloo gather)."""
+    elsewhere.  Each field travels as one padded tensor per rank (RCCL/gloo gather);
+    floats as float64, status / iteration counts as int32."""
     m = max_shard(n_cols, world)
     out = {} if rank == root else None
-    for f in (*FLOAT_FIELDS, "status"):
+    for f in (*FLOAT_FIELDS, *INT_FIELDS):
         if f not in local:
             continue
         a = np.asarray(local[f])
-        dt = torch.float64 if f != "status" else torch.int32
-        pad = np.zeros((m, n_u), dtype=np.float64 if f != "status" else np.int32)
-        src = a.view(np.int32) if f == "status" else a
-        pad[: a.shape[0]] = src
+        if a.ndim != 2:  # per-group hetero buffers [n, n_u, K] stay on the ranks
+            continue
+        is_int = f in INT_FIELDS
+        pad = np.zeros((m, n_u), dtype=np.int32 if is_int else np.float64)
+        pad[: a.shape[0]] = a.view(np.int32) if is_int else a
         t = torch.from_numpy(pad).to(device)
         bufs = [torch.empty_like(t) for _ in range(world)] if rank == root else None
         dist.gather(t, bufs, dst=root)
@@ -54,23 +57,33 @@ def gather_columns(local: dict, n_cols: int, n_u: int, world: int, rank: int, de
             for r in range(world):
                 cols = shard_columns(n_cols, world, r)
                 full[cols] = bufs[r].cpu().numpy()[: len(cols)]
-            out[f] = full.view(np.uint32) if f == "status" else full
+            out[f] = full.view(a.dtype) if is_int else full
     return out
+
+
+def _world_rank():
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    return world, rank
+
+
+def _device(device):
+    if device is None:
+        device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cpu"
+    return device
 
 
 def sweep_baseline_sharded(grid: BaselineGrid, compute: Callable[[BaselineGrid], dict] | None = None,
                            device=None, root: int = 0):
     """Shard `grid` over the ranks of the default process group, solve each
     shard with `compute` (default: this rank's GPU through libsbr), gather to root."""
-    world = dist.get_world_size() if dist.is_initialized() else 1
-    rank = dist.get_rank() if dist.is_initialized() else 0
+    world, rank = _world_rank()
     if compute is None:
         from .engine import default_engine
 
         eng = default_engine()
         compute = lambda g: eng.sweep_baseline(g)  # noqa: E731
-    if device is None:
-        device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cpu"
+    device = _device(device)
     cols = shard_columns(len(grid.beta), world, rank)
     local = compute(grid.subset(cols)) if len(cols) else {f: np.zeros((0, len(grid.u))) for f in FLOAT_FIELDS}
     if "status" not in local:
@@ -78,3 +91,46 @@ def sweep_baseline_sharded(grid: BaselineGrid, compute: Callable[[BaselineGrid],
     if world == 1:
         return local
     return gather_columns(local, len(grid.beta), len(grid.u), world, rank, device, root)
+
+
+def sweep_hetero_sharded(grid: HeteroGrid, compute: Callable[[HeteroGrid], dict] | None = None, device=None,
+                         root: int = 0):
+    """Heterogeneity sweep sharded over parameter columns like the baseline
+    (rank r owns columns r, r+N, …); per-group buffers stay on the ranks."""
+    world, rank = _world_rank()
+    if compute is None:
+        from .engine import default_engine
+
+        eng = default_engine()
+        compute = lambda g: eng.sweep_hetero(g.betas, g.dist, g.eta, g.t_end, g.u, g.p, g.kappa, g.lam,  # noqa: E731
+                                             g.x0, with_groups=False)
+    cols = shard_columns(grid.betas.shape[0], world, rank)
+    local = compute(grid.subset(cols))
+    if world == 1:
+        return local
+    return gather_columns(local, grid.betas.shape[0], len(grid.u), world, rank, _device(device), root)
+
+
+def sweep_social_sharded(beta, eta, u, p, kappa, lam, cmp=None, x0=1e-4, tol=1e-4, max_iter=500,
+                         compute: Callable[..., dict] | None = None, device=None, root: int = 0):
+    """Social-learning sweep (social_learning_solver.jl:63-263) sharded over β
+    columns; every point is an independent fixed point, so the only exchange is
+    the gather of the results.  compute(beta, eta, u, cmp) solves one shard."""
+    world, rank = _world_rank()
+    beta = np.ascontiguousarray(np.atleast_1d(beta), np.float64)
+    eta = np.ascontiguousarray(np.broadcast_to(eta, beta.shape), np.float64)
+    u = np.ascontiguousarray(np.atleast_1d(u), np.float64)
+    if cmp is None:
+        cmp = np.stack([julia_range(0.0, float(e), 1000) for e in eta])
+    cmp = np.ascontiguousarray(np.broadcast_to(np.atleast_2d(cmp), (len(beta), np.atleast_2d(cmp).shape[1])))
+    if compute is None:
+        from .engine import default_engine
+
+        eng = default_engine()
+        compute = lambda b, e, uu, c: eng.sweep_social(b, e, uu, p, kappa, lam, cmp=c, x0=x0, tol=tol,  # noqa: E731
+                                                       max_iter=max_iter)
+    cols = shard_columns(len(beta), world, rank)
+    local = compute(beta[cols], eta[cols], u, cmp[cols])
+    if world == 1:
+        return local
+    return gather_columns(local, len(beta), len(u), world, rank, _device(device), root)

@@ -58,6 +58,51 @@ def test_sharded_sweep_equals_single_process(tmp_path, oracle, world):
     assert np.array_equal(got["status"], ref["status"])
 
 
+def _worker_ext(rank, world, port, out_path):
+    """Social and hetero sweeps sharded the same way (oracle as per-rank compute)."""
+    import torch.distributed as dist
+
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    sys.path.insert(0, os.path.join(REPO, "replication-social-bank-runs_amd"))
+    import oracle as O
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    beta, u, eta = _social_axes()
+    soc = D.sweep_social_sharded(beta, eta, u, 0.99, 0.25, 0.25, max_iter=3, device="cpu",
+                                 compute=lambda b, e, uu, c: O.sweep_social(b, e, uu, 0.99, 0.25, 0.25, c,
+                                                                            max_iter=3))
+    hg = sbr.hetero_config4(5, 7, K=2)
+    het = D.sweep_hetero_sharded(hg, device="cpu", compute=lambda g: O.sweep_hetero(
+        g.betas, g.dist, g.eta, g.t_end, g.u, g.p, g.kappa, g.lam, g.x0))
+    if rank == 0:
+        np.savez(out_path, **{"s_" + k: v for k, v in soc.items()}, **{"h_" + k: v for k, v in het.items()})
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _social_axes():
+    beta = 1.0 / sbr.julia_range("0.01", "2", 512)[[0, 100, 300, 511, 200]]
+    u = sbr.julia_range("0.001", "1", 512)[[40, 300]]
+    return beta, u, 30.0 / 0.9
+
+
+def test_sharded_social_and_hetero_equal_single_process(tmp_path, oracle):
+    out = str(tmp_path / "res.npz")
+    mp.spawn(_worker_ext, args=(2, _free_port(), out), nprocs=2, join=True)
+    got = np.load(out)
+    beta, u, eta = _social_axes()
+    ref = oracle.sweep_social(beta, eta, u, 0.99, 0.25, 0.25, sbr.julia_range(0.0, eta, 1000), max_iter=3)
+    for f in ("xi", "tau_in_unc", "tau_out_unc", "aw_max", "tol", "status", "iters", "fp_iters"):
+        a, b = got["s_" + f], ref[f]
+        assert a.shape == b.shape and np.array_equal(a, b, equal_nan=a.dtype.kind == "f"), f
+    hg = sbr.hetero_config4(5, 7, K=2)
+    href = oracle.sweep_hetero(hg.betas, hg.dist, hg.eta, hg.t_end, hg.u, hg.p, hg.kappa, hg.lam, hg.x0)
+    for f in ("xi", "aw_max", "tol", "status", "iters"):
+        a, b = got["h_" + f], href[f]
+        assert a.shape == b.shape and np.array_equal(a, b, equal_nan=a.dtype.kind == "f"), f
+
+
 def test_shard_columns_partition():
     for n, w in ((2048, 8), (37, 3), (5, 8)):
         parts = [D.shard_columns(n, w, r) for r in range(w)]
