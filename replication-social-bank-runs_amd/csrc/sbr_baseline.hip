@@ -168,6 +168,7 @@ __global__ __launch_bounds__(64) void learn_logistic_kernel(const double* __rest
 constexpr int HZ_BLOCK = 256;
 constexpr int HZ_CHUNK = 16;
 constexpr int EQ_TILE = 4096;  // u values per equilibrium block (one block per β column up to this)
+constexpr int kAwWin = 6;      // 8-blocks each side of the predicted AW peak evaluated first
 
 __global__ __launch_bounds__(HZ_BLOCK) void hazard_kernel(const double* __restrict__ beta,
                                                           const double* __restrict__ eta, LearnArgs a, LearnBufs L)
@@ -292,6 +293,8 @@ struct Summ {
     const double* hmin;
     const double* pmc;
     const double* smc;
+    bool mono; // G nondecreasing over the knots (no NaN): prefix max / suffix min are knot values
+    double t_half; // time where G crosses 1/2 (lerp inverse), NaN if it does not: AW peak predictor
 };
 
 // first i >= s with H[i] > u (or -1); whole blocks are skipped on their summary
@@ -466,7 +469,7 @@ __device__ __forceinline__ void solve_point(P T, P G, P H, const Summ& S, const 
     int jlo = ssl_range(T, 0, n - 1, xmin);
     int jhi = ssl_range(T, 0, n - 1, xmax);
     const int jtin = jlo;
-    double c_ic_x = NAN, c_ic_v = 0.0, c_ice_x = NAN, c_ice_v = 0.0;
+    double c_ic_x = NAN, c_ic_v = 0.0;
     uint32_t s = SBR_NO_RUN_MAXITER;
     double xi = NAN, tolr = INFINITY;
     for (int iter = 1; iter <= max_iters; iter++) {
@@ -492,20 +495,20 @@ __device__ __forceinline__ void solve_point(P T, P G, P H, const Summ& S, const 
         // ε = local knot spacing at ξ_old (solver.jl:336-338)
         if (j + 1 >= n) { flag |= trunc ? SBR_ENGINE_TRUNC : SBR_OOB; break; }
         const double eps = T[j + 1] - T[j];
-        double Goce = 0.0, Gice = 0.0;
         const double xoe = oc + eps, xie = ic + eps;
-        if (in_range(xoe, tlo, thi, trunc, flag)) Goce = lerp_at(T, G, n, ssl_gallop(T, n, joc, xoe), xoe);
-        if (in_range(xie, tlo, thi, trunc, flag)) {
-            if (xie == c_ice_x) Gice = c_ice_v;
-            else { Gice = lerp_at(T, G, n, ssl_gallop(T, n, jic, xie), xie); c_ice_x = xie; c_ice_v = Gice; }
-        }
+        // the slope probe AW(ξ + ε) only decides the terminal iterate (solver.jl:345-352);
+        // its lookups' BoundsError checks still run every iterate, in the reference's order
+        const bool oke = in_range(xoe, tlo, thi, trunc, flag);
+        const bool oki = in_range(xie, tlo, thi, trunc, flag);
         if (flag) break;
         const double AW = Goc - Gic;
-        const double AWe = Goce - Gice;
         const double err = AW - kappa;
-        const bool inc = AWe >= AW;
         if (fabs(err) <= tolerance) {
-            if (inc) { s = SBR_RUN; xi = xo; tolr = fabs(err); }
+            double Goce = 0.0, Gice = 0.0;
+            if (oke) Goce = lerp_at(T, G, n, ssl_gallop(T, n, joc, xoe), xoe);
+            if (oki) Gice = lerp_at(T, G, n, ssl_gallop(T, n, jic, xie), xie);
+            const double AWe = Goce - Gice;
+            if (AWe >= AW) { s = SBR_RUN; xi = xo; tolr = fabs(err); }
             else s = SBR_FALSE_EQ;
             break;
         } else if (err > 0) {
@@ -568,35 +571,53 @@ __device__ __forceinline__ void solve_point(P T, P G, P H, const Summ& S, const 
             // ≤ bracket(b(τ̄_i1)) + 1, AW_IN ≥ min G over knots ≥ bracket(a(τ̄_i0)) (8-knot
             // prefix-max / suffix-min tables), plus a rounding margin far above the
             // ≈2e-15 the exact path can add.
+            // When G is nondecreasing (every learning CDF of the configs) the prefix max up to
+            // knot k is G[k] and the suffix min from k is G[k]: knot-exact bounds, loose by one
+            // knot interval instead of an 8-knot block on each side.
             auto ub_rng = [&](int i0, int i1) -> double {
                 const int ja = brk_a(i0), jb = brk_b(i1);
-                const double hi = S.pmc[(jb + 1 < n - 1 ? jb + 1 : n - 1) >> 3];
-                const double lo = S.smc[(ja < n - 2 ? ja : n - 2) >> 3];
+                const int kh = jb + 1 < n - 1 ? jb + 1 : n - 1, kl = ja < n - 2 ? ja : n - 2;
+                const double hi = S.mono ? G[kh] : S.pmc[kh >> 3];
+                const double lo = S.mono ? G[kl] : S.smc[kl >> 3];
                 const double ub_out = hi > 0.0 ? hi : 0.0;
                 const double lb_in = ((tau(i0) - xi) + icc) >= 0 ? lo : (lo < 0.0 ? lo : 0.0);
                 return ((ub_out - lb_in) + G0) + 1e-14;
             };
             auto end_of = [&](int i0, int w) { return i0 + w < ntau ? i0 + w : ntau; };
-            // pass 1: descend to the most promising 8-wide range and evaluate it
-            int bs = 0;
-            double bu = -INFINITY;
-            for (int i0 = 0; i0 < ntau; i0 += 256) {
-                const double ub = ub_rng(i0, end_of(i0, 256) - 1);
-                if (!(ub <= bu)) { bu = ub; bs = i0; }
+            // pass 1: a first running maximum.  For a logistic-shaped CDF the continuous
+            // maximiser of G(τ − s_out) − G(τ − s_in) sits where G(τ − s_out) + G(τ − s_in) = 1,
+            // i.e. at τ* = t_half + (s_in + s_out)/2: evaluate the 8-blocks around it
+            // (a heuristic — exactness comes from pass 2's bounds).  Otherwise descend the
+            // bound hierarchy to the most promising 8-block.
+            int b8 = -1, w0 = 0, w1 = 0;
+            const double tstar = S.t_half + 0.5 * ((xi - icc) + (xi - occ));
+            if (tstar == tstar && tstar >= tau(0) && tstar <= tau(ntau - 1)) {
+                const int ic = ssl_range(T, 0, (nle > 0 ? nle : 1) - 1, tstar < T[0] ? T[0] : tstar);
+                const int c8 = (ic < ntau ? ic : ntau - 1) & ~7;
+                w0 = c8 - 8 * kAwWin > 0 ? c8 - 8 * kAwWin : 0;
+                w1 = end_of(c8, 8 * (kAwWin + 1));
+                eval_range(w0, w1);
+            } else {
+                int bs = 0;
+                double bu = -INFINITY;
+                for (int i0 = 0; i0 < ntau; i0 += 256) {
+                    const double ub = ub_rng(i0, end_of(i0, 256) - 1);
+                    if (!(ub <= bu)) { bu = ub; bs = i0; }
+                }
+                int bb = bs;
+                bu = -INFINITY;
+                for (int i0 = bs; i0 < end_of(bs, 256); i0 += 64) {
+                    const double ub = ub_rng(i0, end_of(i0, 64) - 1);
+                    if (!(ub <= bu)) { bu = ub; bb = i0; }
+                }
+                b8 = bb;
+                bu = -INFINITY;
+                for (int i0 = bb; i0 < end_of(bb, 64); i0 += 8) {
+                    const double ub = ub_rng(i0, end_of(i0, 8) - 1);
+                    if (!(ub <= bu)) { bu = ub; b8 = i0; }
+                }
+                eval_range(b8, end_of(b8, 8));
             }
-            int bb = bs;
-            bu = -INFINITY;
-            for (int i0 = bs; i0 < end_of(bs, 256); i0 += 64) {
-                const double ub = ub_rng(i0, end_of(i0, 64) - 1);
-                if (!(ub <= bu)) { bu = ub; bb = i0; }
-            }
-            int b8 = bb;
-            bu = -INFINITY;
-            for (int i0 = bb; i0 < end_of(bb, 64); i0 += 8) {
-                const double ub = ub_rng(i0, end_of(i0, 8) - 1);
-                if (!(ub <= bu)) { bu = ub; b8 = i0; }
-            }
-            eval_range(b8, end_of(b8, 8));
             // pass 2: every range whose bound beats the running max is refined
             for (int s0 = 0; s0 < ntau && !flag && mx == mx; s0 += 256) {
                 const int se = end_of(s0, 256);
@@ -606,7 +627,7 @@ __device__ __forceinline__ void solve_point(P T, P G, P H, const Summ& S, const 
                     if (ub_rng(k0, ke - 1) <= mx) continue;
                     for (int i0 = k0; i0 < ke && !flag && mx == mx; i0 += 8) {
                         const int ie = end_of(i0, 8);
-                        if (i0 == b8 || ub_rng(i0, ie - 1) <= mx) continue;
+                        if (i0 == b8 || (i0 >= w0 && ie <= w1) || ub_rng(i0, ie - 1) <= mx) continue;
                         eval_range(i0, ie);
                     }
                 }
@@ -651,7 +672,10 @@ __global__ __launch_bounds__(BLOCK) void equilibrium_kernel(LearnBufs L, const d
         for (int i = threadIdx.x; i < ntau; i += BLOCK) sH[i] = gH[i];
     }
     __syncthreads();
-    Summ S{nullptr, nullptr, nullptr, nullptr};
+    Summ S{nullptr, nullptr, nullptr, nullptr, false, (double)NAN};
+    __shared__ int s_nonmono;
+    __shared__ double s_thalf;
+    if (threadIdx.x == 0) { s_nonmono = 0; s_thalf = NAN; }
     if (fits && !a.exhaustive) {
         const int nbh = (ntau + 63) >> 6, nbg = (n + 7) >> 3;
         for (int bk = threadIdx.x; bk < nbh + nbg; bk += BLOCK) {
@@ -669,12 +693,17 @@ __global__ __launch_bounds__(BLOCK) void equilibrium_kernel(LearnBufs L, const d
                 const int g = bk - nbh;
                 double mx = -INFINITY, mn = INFINITY;
                 const int e = (g << 3) + 8 < n ? (g << 3) + 8 : n;
+                double prev = g > 0 ? sG[(g << 3) - 1] : -INFINITY;
+                bool mono = true;
                 for (int i = g << 3; i < e; i++) {
                     const double v = sG[i];
-                    if (v != v) { mx = NAN; mn = NAN; break; }
+                    if (v != v) { mx = NAN; mn = NAN; mono = false; break; }
                     if (v > mx) mx = v;
                     if (v < mn) mn = v;
+                    mono &= v >= prev;
+                    prev = v;
                 }
+                if (!mono) s_nonmono = 1;
                 pmc[g] = mx; // block max for now
                 smc[g] = mn; // block min for now
             }
@@ -682,6 +711,16 @@ __global__ __launch_bounds__(BLOCK) void equilibrium_kernel(LearnBufs L, const d
         __syncthreads();
         // prefix max / suffix min over blocks (NaN-propagating), two waves at once
         if (threadIdx.x == 0) {
+            // t_half: first knot interval with G[k] <= 1/2 < G[k+1] (heuristic only)
+            int lo = 0, hi = n - 1;
+            if (n >= 2 && sG[0] <= 0.5 && sG[n - 1] > 0.5) {
+                while (hi - lo > 1) {
+                    const int mid = (lo + hi) >> 1;
+                    if (sG[mid] <= 0.5) lo = mid;
+                    else hi = mid;
+                }
+                s_thalf = sT[lo] + (0.5 - sG[lo]) * (sT[hi] - sT[lo]) / (sG[hi] - sG[lo]);
+            }
             for (int g = 1; g < nbg; g++) {
                 const double a0 = pmc[g - 1], b0 = pmc[g];
                 pmc[g] = (a0 != a0 || b0 != b0) ? NAN : (a0 > b0 ? a0 : b0);
@@ -693,7 +732,7 @@ __global__ __launch_bounds__(BLOCK) void equilibrium_kernel(LearnBufs L, const d
             }
         }
         __syncthreads();
-        S = Summ{hmax, hmin, pmc, smc};
+        S = Summ{hmax, hmin, pmc, smc, s_nonmono == 0, s_thalf};
     }
     // Points are handed out to waves 64 at a time from an LDS counter, so a
     // wave that drew cheap no-run points goes back for more instead of idling

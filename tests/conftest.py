@@ -55,6 +55,15 @@ def oracle():
 
 @pytest.fixture(scope="session")
 def engine():
+    # PyTorch-ROCm bundles its own HIP runtime: let torch bring up the device first
+    # (as bench.py does), so libsbr binds to the runtime already in the process.
+    try:
+        import torch
+
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    except ImportError:
+        pass
     import sbr
 
     return sbr.Engine(int(os.environ.get("LOCAL_RANK", "0")))
