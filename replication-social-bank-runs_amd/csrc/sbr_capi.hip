@@ -20,13 +20,16 @@ struct sbr_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     std::string err;
-    // learning workspaces: slot 0 for single sweeps, slots 0/1 alternate in a
-    // pipelined batch (learning of batch k+1 overlaps the equilibrium of batch k)
-    size_t ws_beta[2] = {0, 0}, ws_cap[2] = {0, 0};
-    sbr::LearnBufs LW[2]{};
+    // learning workspaces: slot 0 for single sweeps; a pipelined batch rotates through
+    // kLearnSlots slots, each learned on its own highest-priority stream, so the
+    // learning of the next kLearnSlots-1 batches (latency-bound: 32 waves each) runs
+    // concurrently with the equilibrium of the current one
+    static constexpr int kLearnSlots = 3;
+    size_t ws_beta[kLearnSlots] = {}, ws_cap[kLearnSlots] = {};
+    sbr::LearnBufs LW[kLearnSlots]{};
     int last_slot = 0;
-    hipStream_t lstream = nullptr; // learning stream of pipelined batches (highest priority)
-    hipEvent_t ev_in = nullptr, ev_learned[2] = {nullptr, nullptr}, ev_eq[2] = {nullptr, nullptr};
+    hipStream_t lstream[kLearnSlots] = {};
+    hipEvent_t ev_in = nullptr, ev_learned[kLearnSlots] = {}, ev_eq[kLearnSlots] = {};
     // hetero learning workspace
     size_t hs_col = 0, hs_cap = 0, hs_K = 0;
     sbr::HeteroBufs H{};
@@ -304,17 +307,19 @@ int sbr_free(sbr_ctx* c)
     if (!c) return SBR_OK;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
-    if (c->lstream) (void)hipStreamSynchronize(c->lstream);
-    free_learn(c, 0);
-    free_learn(c, 1);
+    for (hipStream_t ls : c->lstream)
+        if (ls) (void)hipStreamSynchronize(ls);
+    for (int k = 0; k < sbr_ctx::kLearnSlots; k++) free_learn(c, k);
     free_hetero(c);
     free_social(c);
     if (c->so_prof) (void)hipFree(c->so_prof);
     if (c->so_count_host) (void)hipHostFree(c->so_count_host);
-    hipEvent_t evs[] = {c->ev_in, c->ev_learned[0], c->ev_learned[1], c->ev_eq[0], c->ev_eq[1]};
-    for (hipEvent_t e : evs)
-        if (e) (void)hipEventDestroy(e);
-    if (c->lstream) (void)hipStreamDestroy(c->lstream);
+    if (c->ev_in) (void)hipEventDestroy(c->ev_in);
+    for (int k = 0; k < sbr_ctx::kLearnSlots; k++) {
+        if (c->ev_learned[k]) (void)hipEventDestroy(c->ev_learned[k]);
+        if (c->ev_eq[k]) (void)hipEventDestroy(c->ev_eq[k]);
+        if (c->lstream[k]) (void)hipStreamDestroy(c->lstream[k]);
+    }
     if (c->stage) (void)hipFree(c->stage);
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(c->stream);
@@ -350,31 +355,35 @@ int sbr_sweep_baseline_batch_dev(sbr_ctx* c, void* stream, int64_t n_batch, cons
     if (!scalars_valid(x0, p, kappa, lambda)) return fail(c, SBR_EARG, "ArgumentError: x0/p/kappa/lambda");
     if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
     sbr_opts o = resolve(opts);
-    for (int k = 0; k < 2 && k < n_batch; k++) {
+    const int nslot = sbr_ctx::kLearnSlots;
+    for (int k = 0; k < nslot && k < n_batch; k++) {
         int rc = ensure_learn(c, (size_t)n_beta, (size_t)o.knot_capacity, k);
         if (rc) return rc;
     }
-    if (!c->lstream) {
+    if (!c->lstream[0]) {
         int lo = 0, hi = 0;
         (void)hipDeviceGetStreamPriorityRange(&lo, &hi); // hi = greatest priority
-        HIP_TRY(c, hipStreamCreateWithPriority(&c->lstream, hipStreamNonBlocking, hi), SBR_EDEVICE);
-        hipEvent_t* evs[] = {&c->ev_in, &c->ev_learned[0], &c->ev_learned[1], &c->ev_eq[0], &c->ev_eq[1]};
-        for (hipEvent_t* e : evs) HIP_TRY(c, hipEventCreateWithFlags(e, hipEventDisableTiming), SBR_EDEVICE);
+        for (int k = 0; k < nslot; k++) {
+            HIP_TRY(c, hipStreamCreateWithPriority(&c->lstream[k], hipStreamNonBlocking, hi), SBR_EDEVICE);
+            HIP_TRY(c, hipEventCreateWithFlags(&c->ev_learned[k], hipEventDisableTiming), SBR_EDEVICE);
+            HIP_TRY(c, hipEventCreateWithFlags(&c->ev_eq[k], hipEventDisableTiming), SBR_EDEVICE);
+        }
+        HIP_TRY(c, hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming), SBR_EDEVICE);
     }
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-    hipStream_t ls = c->lstream;
     const size_t np = (size_t)n_beta * (size_t)n_u;
     sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, p, lambda, o.ode_maxiters, (int32_t)n_beta, 1, 0};
     // inputs are ready once prior work on the caller's stream is
     HIP_TRY(c, hipEventRecord(c->ev_in, s), SBR_EDEVICE);
-    HIP_TRY(c, hipStreamWaitEvent(ls, c->ev_in, 0), SBR_EDEVICE);
+    for (int k = 0; k < nslot; k++) HIP_TRY(c, hipStreamWaitEvent(c->lstream[k], c->ev_in, 0), SBR_EDEVICE);
     for (int64_t k = 0; k < n_batch; k++) {
-        const int slot = (int)(k & 1);
+        const int slot = (int)(k % nslot);
+        hipStream_t ls = c->lstream[slot];
         const double* bk = beta + k * n_beta;
         const double* ek = eta + k * n_beta;
         const double* tk = t_end + k * n_beta;
-        // the slot's previous reader (equilibrium of batch k-2) must be done
-        if (k >= 2) HIP_TRY(c, hipStreamWaitEvent(ls, c->ev_eq[slot], 0), SBR_EDEVICE);
+        // the slot's previous reader (equilibrium of batch k - nslot) must be done
+        if (k >= nslot) HIP_TRY(c, hipStreamWaitEvent(ls, c->ev_eq[slot], 0), SBR_EDEVICE);
         hipEvent_t t0 = tstart(c, ls);
         HIP_TRY(c, sbr::launch_learn_logistic(bk, ek, tk, la, c->LW[slot], ls), SBR_EDEVICE);
         tend(c, ls, 0, t0);
@@ -532,7 +541,8 @@ int sbr_timing_read(sbr_ctx* c, void* stream, double* learn_ms, double* eq_ms, i
     HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
     double a = 0.0, b = 0.0;
     int32_t n = 0;
-    if (c->lstream) HIP_TRY(c, hipStreamSynchronize(c->lstream), SBR_EDEVICE);
+    for (hipStream_t ls : c->lstream)
+        if (ls) HIP_TRY(c, hipStreamSynchronize(ls), SBR_EDEVICE);
     for (const auto& r : c->trec) {
         float t = 0.f;
         HIP_TRY(c, hipEventElapsedTime(&t, r.a, r.b), SBR_EDEVICE);

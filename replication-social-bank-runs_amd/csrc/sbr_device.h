@@ -52,21 +52,30 @@ __device__ __forceinline__ double dmax(double a, double b) { return a > b ? a : 
 // the correctly rounded a / b, bit for bit; a = +Inf is selected explicitly.
 // Callers: the PI controller's q/γ (q ∈ [1e-45, 1e42]) and the AutoSwitch
 // stiffness ratio (only compared with 0.9).
+__device__ __forceinline__ double rcp_refined(double b)
+{
+    double y = __builtin_amdgcn_rcp(b);
+    double e = fma(-b, y, 1.0);
+    y = fma(y, e, y);
+    e = fma(-b, y, 1.0);
+    return fma(y, e, y);
+}
+
+// a / b given r = rcp_refined(b): the sequence's last three steps.  Bit-identical to
+// `a / b` when b is in [2^-960, 2^900] and a is 0 or in [2^-960, 2^767] (no scaling).
+__device__ __forceinline__ double div_rcp(double a, double b, double r)
+{
+    const double q0 = a * r;
+    const double rem = fma(-b, q0, a);
+    return fma(rem, r, q0);
+}
+
 struct ConstDiv {
     double b, r;
-    __device__ __forceinline__ explicit ConstDiv(double b_) : b(b_)
-    {
-        double y = __builtin_amdgcn_rcp(b_);
-        double e = fma(-b_, y, 1.0);
-        y = fma(y, e, y);
-        e = fma(-b_, y, 1.0);
-        r = fma(y, e, y);
-    }
+    __device__ __forceinline__ explicit ConstDiv(double b_) : b(b_), r(rcp_refined(b_)) {}
     __device__ __forceinline__ double operator()(double a) const
     {
-        const double q0 = a * r;
-        const double rem = fma(-b, q0, a);
-        const double q = fma(rem, r, q0);
+        const double q = div_rcp(a, b, r);
         return a == (double)INFINITY ? (double)INFINITY : q;
     }
 };

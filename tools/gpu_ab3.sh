@@ -2,7 +2,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 L=$PWD/replication-social-bank-runs_amd/lib
-for lib in libsbr_w4 libsbr_w6 libsbr_w8; do
+for lib in libsbr_w6 libsbr_ilerp; do
   SBR_LIB=$L/$lib.so timeout -k 10 200 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --phases > gpurun_out/ab3_$lib.json 2> gpurun_out/ab3_$lib.err || exit 1
   python -c "import json;d=json.load(open('gpurun_out/ab3_$lib.json'));print('$lib', round(d['value']/1e6,1), d['kernel_ms_per_step'], d['eq_phase_ms'])"
 done
