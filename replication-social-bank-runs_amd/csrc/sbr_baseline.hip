@@ -548,7 +548,9 @@ __device__ __forceinline__ void solve_point(P T, P G, P H, const Summ& S, const 
             while (ji + 1 < n && T[ji + 1] <= xa) ji++;
             while (jo + 1 < n && T[jo + 1] <= xb) jo++;
             const double gi = lerp_at(T, G, n, ji, xa);
-            const double go = lerp_at(T, G, n, jo, xb);
+            // b(τ̄_i) = (τ̄_i − ξ) + ξ is τ̄_i itself whenever τ̄_i − ξ is exact (Sterbenz):
+            // then δ = 0 and the lerp is G[j]·(1 − 0) + G[j+1]·0, no division
+            const double go = (xb == T[jo] && jo < n - 1) ? G[jo] * 1.0 + G[jo + 1] * 0.0 : lerp_at(T, G, n, jo, xb);
             const double awin = av >= 0 ? gi : 0.0;
             const double awout = bv >= 0 ? go : 0.0;
             const double v = (awout - awin) + G0;
