@@ -95,6 +95,31 @@ function solve_equilibrium_grid(ctx::Context, β_vals, u_vals; η = 15.0, tspan_
 end
 
 """
+    solve_point_paths(ctx, β, u; η, tspan_end, x0, p, κ, λ, cap = 1 << 16)
+
+One point with paths — `solve_learning` + `solve_equilibrium_baseline` + `get_AW`
+(src/baseline/solver.jl:413-462, 495-532) — returning the hazard grid τ̄, HR(τ̄) and AW_cum(τ̄),
+from which a maintainer rebuilds the `LinearInterpolation`s the plotting code consumes
+(`HR = LinearInterpolation(τ̄, hr)`, `AW_cum = LinearInterpolation(τ̄, aw_cum)`, plotting.jl:156-210).
+"""
+function solve_point_paths(ctx::Context, β, u; η = 15.0, tspan_end = 30.0, x0 = 1e-4, p = 0.5, κ = 0.6,
+                           λ = 0.01, cap = 1 << 16)
+    res = zeros(Float64, 5); st = Ref{UInt32}(0); nt = Ref{Int64}(0)
+    τ = Vector{Float64}(undef, cap); hr = similar(τ); aw = similar(τ)
+    opts = Ref(Opts(; early_exit = 0))
+    GC.@preserve res τ hr aw begin
+        rc = ccall((:sbr_solve_point_paths, libsbr), Cint,
+                   (Ptr{Cvoid}, Float64, Float64, Float64, Float64, Float64, Float64, Float64, Float64, Ref{Opts},
+                    Ptr{Float64}, Ref{UInt32}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Int64, Ref{Int64}),
+                   ctx.ptr, β, η, tspan_end, x0, u, p, κ, λ, opts, res, st, τ, hr, aw, cap, nt)
+        check(ctx, rc)
+    end
+    k = nt[]
+    return (ξ = res[1], τ_bar_IN_UNC = res[2], τ_bar_OUT_UNC = res[3], AW_max = res[4], tolerance = res[5],
+            status = st[], τ_bar = τ[1:k], HR = hr[1:k], AW_cum = aw[1:k])
+end
+
+"""
     solve_equilibrium_hetero_grid(ctx, βs_cols, dist, u_vals; η, tspan_end, x0, p, κ, λ)
 
 `βs_cols` is K × n_col (column c = the group rates of one parameter column); η per column.
