@@ -300,6 +300,22 @@ def main_hetero(a):
         "run_fraction": float(((st & sbr.STATUS["SBR_RUN"]) > 0).mean()),
         "stiff_switch_fraction": float(((st & sbr.STATUS["SBR_STIFF_SWITCH"]) > 0).mean()),
     }
+    if a.phases:
+        from sbr import _lib
+        ph = {}
+        for name, fl in (("scans", 0x100), ("bisect", 0x200), ("validity", 0x400), ("full", 0)):
+            eng.sweep_hetero_dev(K, betas, distw, eta, t_end, u, g.p, g.kappa, g.lam, g.x0, out, stream=stream,
+                                 flags=fl)
+            torch.cuda.synchronize(dev)
+            eng.timing_read(stream)
+            eng.timing_enable(True)
+            eng.sweep_hetero_dev(K, betas, distw, eta, t_end, u, g.p, g.kappa, g.lam, g.x0, out, stream=stream,
+                                 flags=fl)
+            torch.cuda.synchronize(dev)
+            _, e_ms, nc = eng.timing_read(stream)
+            eng.timing_enable(False)
+            ph[name] = e_ms / max(nc, 1)
+        res["eq_phase_ms"] = ph
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         sys.path.insert(0, str(REPO / "oracle"))
         import oracle as O  # noqa: E402  (test infrastructure: cpu_baseline leg only)

@@ -58,7 +58,8 @@ typedef struct {
 /* Diagnostics (timing breakdown only — results are NOT the reference's):
  * stop every point after the crossing scan / after the ξ bisection, or
  * report the number of 64-knot AW blocks evaluated in `iters` instead of
- * the bisection count. */
+ * the bisection count.  In the hetero sweep 0x400 stops after the validity
+ * check instead. */
 #define SBR_FLAG_DIAG_STOP_AFTER_BUFFER 0x100
 #define SBR_FLAG_DIAG_STOP_AFTER_BISECT 0x200
 #define SBR_FLAG_DIAG_COUNT_AW_BLOCKS 0x400

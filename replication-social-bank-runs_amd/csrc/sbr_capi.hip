@@ -586,7 +586,8 @@ int sbr_sweep_hetero_dev(sbr_ctx* c, void* stream, int32_t K, const double* beta
     if (rc) return rc;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, p, lambda, o.ode_maxiters, (int32_t)n_col, 0, 0};
-    sbr::HeteroEqArgs ea{kappa, 1e-12, (int32_t)n_u, o.hetero_max_iters, c->lds_cap * 3};
+    sbr::HeteroEqArgs ea{kappa, 1e-12, (int32_t)n_u, o.hetero_max_iters, c->lds_cap * 3,
+                         (o.flags & SBR_FLAG_EXHAUSTIVE) ? 1 : 0, (o.flags >> 8) & 7};
     sbr::ResultSoA r{out->xi, nullptr, nullptr, out->aw_max, out->tol, out->status, out->iters};
     hipEvent_t t0 = tstart(c, s);
     HIP_TRY(c, sbr::launch_hetero(K, betas, dist, eta, t_end, u, la, ea, c->H, r, tau_in, tau_out, s, 0), SBR_EDEVICE);

@@ -303,7 +303,7 @@ __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const d
                                                    const double u, const double kappa, const int max_iters,
                                                    const double tolerance, const uint32_t lbits, double& xi_o,
                                                    double& aw_o, double& tol_o, uint32_t& st_o, int& it_o,
-                                                   double* tin, double* tout)
+                                                   double* tin, double* tout, const bool mono, const int diag)
 {
     xi_o = NAN; aw_o = NAN; tol_o = INFINITY; it_o = 0;
     const int n = C.n;
@@ -353,6 +353,7 @@ __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const d
         tol_o = 0.0;
         return;
     }
+    if (diag & 1) return; // timing diagnostics: stop after the crossing scans
     // ---------------- compute_ξ_hetero ----------------
     uint32_t flag = 0;
     double guess = (dist[0] * (tin[0] + tout[0])) / 2.0;
@@ -394,17 +395,26 @@ __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const d
             if (ic == xo) { jic = xo <= thi ? j : -1; Gic = jic >= 0 ? C.lerp(j, k, xo) : 0.0; }
             else { jic = jin[k]; Gic = gin[k]; }
             if (joc < 0 || jic < 0) flag |= SBR_OOB;
+            // the slope probe only decides the terminal iterate: range checks every
+            // iterate (BoundsError order of heterogeneity_solver.jl:81-95), lerps later
             const double xoe = oc + eps, xie = ic + eps;
-            double Goce = 0.0, Gice = 0.0;
-            if (xoe <= thi && joc >= 0) Goce = C.lerp(ssl_gallop(C.T, n, joc, xoe), k, xoe);
-            else flag |= SBR_OOB;
-            if (xie <= thi && jic >= 0) Gice = C.lerp(ssl_gallop(C.T, n, jic, xie), k, xie);
-            else flag |= SBR_OOB;
+            if (!(xoe <= thi && joc >= 0)) flag |= SBR_OOB;
+            if (!(xie <= thi && jic >= 0)) flag |= SBR_OOB;
             AW = AW + dist[k] * (Goc - Gic);
-            AWe = AWe + dist[k] * (Goce - Gice);
         }
         if (flag) break;
         const double err = AW - kappa;
+        if (fabs(err) <= tolerance) {
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+                const double ic = dmin(tin[k], xo), oc = dmin(tout[k], xo);
+                const int joc = oc == xo ? j : jout[k], jic = ic == xo ? j : jin[k];
+                const double xoe = oc + eps, xie = ic + eps;
+                const double Goce = C.lerp(ssl_gallop(C.T, n, joc, xoe), k, xoe);
+                const double Gice = C.lerp(ssl_gallop(C.T, n, jic, xie), k, xie);
+                AWe = AWe + dist[k] * (Goce - Gice);
+            }
+        }
         const bool inc = AWe >= AW;
         if (fabs(err) <= tolerance) {
             if (inc) { s = SBR_RUN; xi = xo; tolr = fabs(err); }
@@ -422,6 +432,7 @@ __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const d
     }
     if (flag) { st_o = flag | lbits; return; }
     if (s != SBR_RUN) { st_o = s | lbits; return; }
+    if (diag & 2) return; // ... after the bisection
 
     // ---------------- is_valid_equilibrium_hetero ----------------
     {
@@ -447,31 +458,118 @@ __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const d
         }
         if (!valid) { st_o = SBR_HETERO_INVALID | lbits; return; }
     }
+    if (diag & 4) return; // ... after the validity check
     // ---------------- AW_max over the whole learning grid ----------------
     double icc[K], occ[K];
-    int ja[K], jb[K];
 #pragma unroll
-    for (int k = 0; k < K; k++) { icc[k] = dmin(tin[k], xi); occ[k] = dmin(tout[k], xi); ja[k] = 0; jb[k] = 0; }
+    for (int k = 0; k < K; k++) { icc[k] = dmin(tin[k], xi); occ[k] = dmin(tout[k], xi); }
     double mx = -INFINITY;
-    for (int i = 0; i < n; i++) {
-        const double ti = C.T[i];
-        double cum = 0.0;
+    // exact AW_total(t_i) for i in [i0, i1), walkers started by searches from per-group hints
+    int ha[K], hb[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) { ha[k] = 0; hb[k] = 0; }
+    auto eval_range = [&](int i0, int i1) {
+        int ja[K], jb[K];
 #pragma unroll
         for (int k = 0; k < K; k++) {
-            const double av = (ti - xi) + icc[k];
-            const double bv = (ti - xi) + occ[k];
-            const double xa = av > 0 ? av : 0.0;
-            const double xb = bv > 0 ? bv : 0.0;
-            if (!(xa <= thi) || !(xb <= thi)) flag |= SBR_OOB;
-            while (ja[k] + 1 < n && C.T[ja[k] + 1] <= xa) ja[k]++;
-            while (jb[k] + 1 < n && C.T[jb[k] + 1] <= xb) jb[k]++;
-            const double gi = C.lerp(ja[k], k, xa);
-            const double go = C.lerp(jb[k], k, xb);
-            const double awin = av >= 0 ? gi : 0.0;
-            const double awout = bv >= 0 ? go : 0.0;
-            cum = cum + dist[k] * (awout - awin);
+            const double av = (C.T[i0] - xi) + icc[k], bv = (C.T[i0] - xi) + occ[k];
+            ha[k] = ssl_near(C.T, n, ha[k], av > 0 ? av : 0.0);
+            hb[k] = ssl_near(C.T, n, hb[k], bv > 0 ? bv : 0.0);
+            ja[k] = ha[k];
+            jb[k] = hb[k];
         }
-        if (mx == mx && (cum != cum || cum > mx)) mx = cum;
+        for (int i = i0; i < i1; i++) {
+            const double ti = C.T[i];
+            double cum = 0.0;
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+                const double av = (ti - xi) + icc[k];
+                const double bv = (ti - xi) + occ[k];
+                const double xa = av > 0 ? av : 0.0;
+                const double xb = bv > 0 ? bv : 0.0;
+                if (!(xa <= thi) || !(xb <= thi)) flag |= SBR_OOB;
+                while (ja[k] + 1 < n && C.T[ja[k] + 1] <= xa) ja[k]++;
+                while (jb[k] + 1 < n && C.T[jb[k] + 1] <= xb) jb[k]++;
+                const double gi = C.lerp(ja[k], k, xa);
+                const double go = C.lerp(jb[k], k, xb);
+                const double awin = av >= 0 ? gi : 0.0;
+                const double awout = bv >= 0 ? go : 0.0;
+                cum = cum + dist[k] * (awout - awin);
+            }
+            if (mx == mx && (cum != cum || cum > mx)) mx = cum;
+        }
+    };
+    if (!mono) {
+        eval_range(0, n);
+    } else {
+        // Every group CDF is nondecreasing on the knots, so over knots [i0, i1] AW_OUT,k is
+        // at most G_k at the knot after b_k(t_i1)'s bracket and AW_IN,k at least G_k at
+        // a_k(t_i0)'s bracket (0 where masked): branch and bound over 256/64/8-knot ranges,
+        // the same maximum with a fraction of the K·2 lerps per knot.  Arguments are
+        // nondecreasing in i, so the last knot's range check covers the whole path.
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const double av = (C.T[n - 1] - xi) + icc[k], bv = (C.T[n - 1] - xi) + occ[k];
+            if (!((av > 0 ? av : 0.0) <= thi) || !((bv > 0 ? bv : 0.0) <= thi)) flag |= SBR_OOB;
+        }
+        auto ub_rng = [&](int i0, int i1) -> double {
+            double sum = 0.0;
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+                const double bv = (C.T[i1] - xi) + occ[k];
+                double hi = 0.0;
+                if (bv >= 0) {
+                    hb[k] = ssl_near(C.T, n, hb[k], bv);
+                    const double g = C.g(hb[k] + 1 < n - 1 ? hb[k] + 1 : n - 1, k);
+                    hi = g > 0.0 ? g : 0.0;
+                }
+                const double av = (C.T[i0] - xi) + icc[k];
+                double lo = 0.0;
+                if (av >= 0) {
+                    ha[k] = ssl_near(C.T, n, ha[k], av);
+                    lo = C.g(ha[k], k);
+                } else {
+                    lo = C.g(0, k) < 0.0 ? C.g(0, k) : 0.0;
+                }
+                sum = sum + dist[k] * (hi - lo);
+            }
+            return sum + 1e-14;
+        };
+        auto end_of = [&](int i0, int w) { return i0 + w < n ? i0 + w : n; };
+        if (!flag) {
+            int bs = 0;
+            double bu = -INFINITY;
+            for (int i0 = 0; i0 < n; i0 += 256) {
+                const double ub = ub_rng(i0, end_of(i0, 256) - 1);
+                if (!(ub <= bu)) { bu = ub; bs = i0; }
+            }
+            int bb = bs;
+            bu = -INFINITY;
+            for (int i0 = bs; i0 < end_of(bs, 256); i0 += 64) {
+                const double ub = ub_rng(i0, end_of(i0, 64) - 1);
+                if (!(ub <= bu)) { bu = ub; bb = i0; }
+            }
+            int b8 = bb;
+            bu = -INFINITY;
+            for (int i0 = bb; i0 < end_of(bb, 64); i0 += 8) {
+                const double ub = ub_rng(i0, end_of(i0, 8) - 1);
+                if (!(ub <= bu)) { bu = ub; b8 = i0; }
+            }
+            eval_range(b8, end_of(b8, 8));
+            for (int s0 = 0; s0 < n && mx == mx; s0 += 256) {
+                const int se = end_of(s0, 256);
+                if (ub_rng(s0, se - 1) <= mx) continue;
+                for (int k0 = s0; k0 < se && mx == mx; k0 += 64) {
+                    const int ke = end_of(k0, 64);
+                    if (ub_rng(k0, ke - 1) <= mx) continue;
+                    for (int i0 = k0; i0 < ke && mx == mx; i0 += 8) {
+                        const int ie = end_of(i0, 8);
+                        if (i0 == b8 || ub_rng(i0, ie - 1) <= mx) continue;
+                        eval_range(i0, ie);
+                    }
+                }
+            }
+        }
     }
     if (flag) { st_o = flag | lbits; return; }
     xi_o = xi;
@@ -495,9 +593,25 @@ __global__ __launch_bounds__(BLOCK) void equilibrium_hetero_kernel(HeteroBufs L,
     const size_t cap = (size_t)L.cap;
     const double* __restrict__ gT = L.t + (size_t)c * cap;
     const bool fits = n <= a.lds_cap;
+    __shared__ int s_nonmono;
+    if (threadIdx.x == 0) s_nonmono = a.exhaustive;
     if (fits)
         for (int i = threadIdx.x; i < n; i += BLOCK) smem[i] = gT[i];
     __syncthreads();
+
+    {   // every group CDF nondecreasing on the knots (no NaN)?  -> AW_max branch and bound
+        const double* __restrict__ Gc = L.G + (size_t)c * cap * K;
+        bool ok = true;
+        for (int i = 1 + threadIdx.x; i < n; i += BLOCK)
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+                const double g1 = Gc[(size_t)i * K + k], g0 = Gc[(size_t)(i - 1) * K + k];
+                ok &= g1 >= g0 && g0 == g0;
+            }
+        if (!ok) s_nonmono = 1;
+    }
+    __syncthreads();
+    const bool mono = s_nonmono == 0;
     const int j = blockIdx.x * BLOCK + threadIdx.x;
     if (j >= a.n_u) return;
     double dl[K];
@@ -516,11 +630,13 @@ __global__ __launch_bounds__(BLOCK) void equilibrium_hetero_kernel(HeteroBufs L,
     } else if (fits) {
         HCol<K, const double*> C{smem, L.G + (size_t)c * cap * K, L.hr + (size_t)c * K * cap, n, L.n_tau[c],
                                  L.n_le[c], cap, eta[c], t_end[c]};
-        solve_hetero_point<K>(C, dl, uj, a.kappa, a.max_iters, a.tolerance, lbits, xi, aw, tol, st, it, tin, tout);
+        solve_hetero_point<K>(C, dl, uj, a.kappa, a.max_iters, a.tolerance, lbits, xi, aw, tol, st, it, tin, tout,
+                              mono, a.diag);
     } else {
         HCol<K, const double*> C{gT, L.G + (size_t)c * cap * K, L.hr + (size_t)c * K * cap, n, L.n_tau[c],
                                  L.n_le[c], cap, eta[c], t_end[c]};
-        solve_hetero_point<K>(C, dl, uj, a.kappa, a.max_iters, a.tolerance, lbits, xi, aw, tol, st, it, tin, tout);
+        solve_hetero_point<K>(C, dl, uj, a.kappa, a.max_iters, a.tolerance, lbits, xi, aw, tol, st, it, tin, tout,
+                              mono, a.diag);
     }
     const size_t o = (size_t)c * (size_t)a.n_u + j;
     out.xi[o] = xi;

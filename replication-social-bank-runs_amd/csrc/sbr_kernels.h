@@ -66,6 +66,8 @@ struct HeteroEqArgs {
     int32_t n_u;
     int32_t max_iters;  // 500
     int32_t lds_cap;    // knot times staged in LDS
+    int32_t exhaustive; // 1: evaluate AW over every knot (no branch and bound)
+    int32_t diag;       // SBR_FLAG_DIAG_* bits >> 8 (timing breakdown only)
 };
 
 // Social-learning fixed point (sbr_social.hip): one lane per point; per-point

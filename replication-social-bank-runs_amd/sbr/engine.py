@@ -145,7 +145,7 @@ class Engine:
                     status=int(st[0]), tau=tau[:k].copy(), hr=hr[:k].copy(), aw_cum=aw[:k].copy())
 
     def sweep_hetero(self, betas, dist, eta, t_end, u, p, kappa, lam, x0=1e-4, knot_capacity: int = 16384,
-                     with_groups: bool = True) -> dict:
+                     with_groups: bool = True, exhaustive: bool = False) -> dict:
         """Heterogeneity sweep: ``betas`` [n_col, K] group rates per column,
         ``eta``/``t_end`` per column, every u.  Returns [n_col, n_u] arrays and,
         with ``with_groups``, per-group buffers [n_col, n_u, K]."""
@@ -163,7 +163,7 @@ class Engine:
         tout = np.empty(n_col * nu * K) if with_groups else None
         soa = _lib.ResultSoA(_ptr(out["xi"]), None, None, _ptr(out["aw_max"]), _ptr(out["tol"]),
                              _ptr(out["status"]), _ptr(out["iters"]))
-        opts = _lib.default_opts(knot_capacity=knot_capacity)
+        opts = _lib.default_opts(knot_capacity=knot_capacity, flags=_lib.SBR_FLAG_EXHAUSTIVE if exhaustive else 0)
         rc = self._L.sbr_sweep_hetero(self._ctx, K, _ptr(betas), _ptr(dist), _ptr(eta), _ptr(t_end), x0, _ptr(u),
                                       n_col, nu, p, kappa, lam, ctypes.byref(opts), ctypes.byref(soa), _ptr(tin),
                                       _ptr(tout))
@@ -175,13 +175,13 @@ class Engine:
         return res
 
     def sweep_hetero_dev(self, K, betas, dist, eta, t_end, u, p, kappa, lam, x0, out: dict,
-                         stream: int | None = None, knot_capacity: int = 16384):
+                         stream: int | None = None, knot_capacity: int = 16384, flags: int = 0):
         """Device-pointer hetero sweep on torch tensors (no host sync)."""
         n_col, nu = eta.numel(), u.numel()
         soa = _lib.ResultSoA(out["xi"].data_ptr(), None, None, out["aw_max"].data_ptr(), out["tol"].data_ptr(),
                              out["status"].data_ptr(), out["iters"].data_ptr() if out.get("iters") is not None
                              else None)
-        opts = _lib.default_opts(knot_capacity=knot_capacity)
+        opts = _lib.default_opts(knot_capacity=knot_capacity, flags=flags)
         rc = self._L.sbr_sweep_hetero_dev(self._ctx, stream, K, betas.data_ptr(), dist.data_ptr(), eta.data_ptr(),
                                           t_end.data_ptr(), x0, u.data_ptr(), n_col, nu, p, kappa, lam,
                                           ctypes.byref(opts), ctypes.byref(soa), None, None)

@@ -71,3 +71,15 @@ def test_hetero_gpu_bitwise_script_and_grid(engine, oracle):
             assert same.all(), (g.name, f, int((~same).sum()))
         assert np.array_equal(gg["status"], o["status"]), g.name
         assert np.array_equal(gg["iters"], o["iters"]), g.name
+
+
+@pytest.mark.gpu
+def test_hetero_aw_branch_and_bound_equals_exhaustive(engine):
+    """AW_max by branch and bound over monotone group CDFs == every knot evaluated
+    (a different search, the same arithmetic), on a config-4 subgrid."""
+    g = sbr.hetero_config4(64, 96, 8)
+    a = engine.sweep_hetero(g.betas, g.dist, g.eta, g.t_end, g.u, g.p, g.kappa, g.lam, g.x0, with_groups=False)
+    b = engine.sweep_hetero(g.betas, g.dist, g.eta, g.t_end, g.u, g.p, g.kappa, g.lam, g.x0, with_groups=False,
+                            exhaustive=True)
+    for f in ("xi", "aw_max", "tol", "status", "iters"):
+        assert np.array_equal(a[f], b[f], equal_nan=a[f].dtype.kind == "f"), f
