@@ -18,6 +18,7 @@
 // Bit-exact against oracle/sbr_oracle.c (see sbr_device.h).
 #include "sbr_device.h"
 #include "sbr_kernels.h"
+#include "sbr_scan.h"
 
 namespace sbr {
 
@@ -296,106 +297,6 @@ struct Summ {
     bool mono; // G nondecreasing over the knots (no NaN): prefix max / suffix min are knot values
     double t_half; // time where G crosses 1/2 (lerp inverse), NaN if it does not: AW peak predictor
 };
-
-// first i >= s with H[i] > u (or -1); whole blocks are skipped on their summary
-template <class P>
-__device__ __forceinline__ int first_above(P H, const Summ& S, int ntau, int s, double u)
-{
-    int i = s;
-    for (; i < ntau && (i & 63); i++)
-        if (H[i] > u) return i;
-    for (; i < ntau; i += 64) {
-        if (S.hmax[i >> 6] > u) {
-            const int e = i + 64 < ntau ? i + 64 : ntau;
-            for (; i < e; i++)
-                if (H[i] > u) return i;
-            return -1;
-        }
-    }
-    return -1;
-}
-
-// first i >= s with !(H[i] > u) (or -1)
-template <class P>
-__device__ __forceinline__ int first_not_above(P H, const Summ& S, int ntau, int s, double u)
-{
-    int i = s;
-    for (; i < ntau && (i & 63); i++)
-        if (!(H[i] > u)) return i;
-    for (; i < ntau; i += 64) {
-        if (!(S.hmin[i >> 6] > u)) {
-            const int e = i + 64 < ntau ? i + 64 : ntau;
-            for (; i < e; i++)
-                if (!(H[i] > u)) return i;
-            return -1;
-        }
-    }
-    return -1;
-}
-
-// last i <= e with H[i] > u (or -1)
-template <class P>
-__device__ __forceinline__ int last_above(P H, const Summ& S, int e, double u)
-{
-    if (e < 0) return -1;
-    const int b0 = e >> 6;
-    for (int i = e; i >= (b0 << 6); i--)
-        if (H[i] > u) return i;
-    for (int b = b0 - 1; b >= 0; b--) {
-        if (S.hmax[b] > u) {
-            for (int i = (b << 6) + 63; i >= (b << 6); i--)
-                if (H[i] > u) return i;
-            return -1;
-        }
-    }
-    return -1;
-}
-
-// last i <= e with !(H[i] > u) (or -1)
-template <class P>
-__device__ __forceinline__ int last_not_above(P H, const Summ& S, int e, double u)
-{
-    if (e < 0) return -1;
-    const int b0 = e >> 6;
-    for (int i = e; i >= (b0 << 6); i--)
-        if (!(H[i] > u)) return i;
-    for (int b = b0 - 1; b >= 0; b--) {
-        if (!(S.hmin[b] > u)) {
-            for (int i = (b << 6) + 63; i >= (b << 6); i--)
-                if (!(H[i] > u)) return i;
-            return -1;
-        }
-    }
-    return -1;
-}
-
-// The linear scan of optimal_buffer (solver.jl:218-261) answered with block
-// summaries: any/all, first/last index above u, first 0→1 and last 1→0 pair.
-template <class P>
-__device__ __forceinline__ void buffer_scan_blocked(P H, const Summ& S, int ntau, double u, bool& any, bool& all,
-                                                    int& fa, int& la, int& cin, int& cout)
-{
-    fa = first_above(H, S, ntau, 0, u);
-    any = fa >= 0;
-    const int fb = first_not_above(H, S, ntau, 0, u);
-    all = fb < 0;
-    la = any ? last_above(H, S, ntau - 1, u) : -1;
-    cin = -1;
-    cout = -1;
-    if (!any || all) return;
-    if (fa > 0) {
-        cin = fa - 1; // H[0..fa) not above, H[fa] above
-    } else {
-        const int k = first_above(H, S, ntau, fb, u); // first above after the first drop
-        cin = k >= 0 ? k - 1 : -1;
-    }
-    if (la < ntau - 1) {
-        cout = la; // everything after la is not above
-    } else {
-        const int lb = last_not_above(H, S, ntau - 1, u);
-        cout = last_above(H, S, lb, u);
-    }
-}
 
 template <class P>
 __device__ __forceinline__ void solve_point(P T, P G, P H, const Summ& S, const int n, const int ntau,

@@ -17,6 +17,7 @@
 // Bit-exact against oracle/sbr_oracle.c (sbro_sweep_hetero).
 #include "sbr_device.h"
 #include "sbr_kernels.h"
+#include "sbr_scan.h"
 
 namespace sbr {
 
@@ -286,6 +287,8 @@ struct HCol {
     int n, ntau, nle;
     size_t cap;
     double ETA, T1;
+    const double* __restrict__ hsum; // [2][K][nblk] per-64 HR block max / min (LDS), or null
+    int nblk;
     __device__ __forceinline__ double tau(int i) const { return i < nle ? T[i] : ETA; }
     __device__ __forceinline__ double g(int j, int k) const { return G[(size_t)j * K + k]; }
     // Interpolations gridded-linear value of group k on bracket j (clamped)
@@ -315,16 +318,22 @@ __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const d
         const double* __restrict__ Hk = C.H + (size_t)k * C.cap;
         bool any = false, all = true, prev = false;
         int fa = -1, la = -1, cin = -1, cout = -1;
-        for (int i = 0; i < C.ntau; i++) {
-            const bool ab = Hk[i] > u;
-            any |= ab;
-            all &= ab;
-            if (ab) { if (fa < 0) fa = i; la = i; }
-            if (i > 0) {
-                if (!prev && ab && cin < 0) cin = i - 1;
-                if (prev && !ab) cout = i - 1;
+        if (C.hsum) {
+            struct { const double* hmax; const double* hmin; } S{C.hsum + (size_t)k * C.nblk,
+                                                                 C.hsum + (size_t)(K + k) * C.nblk};
+            buffer_scan_blocked(Hk, S, C.ntau, u, any, all, fa, la, cin, cout);
+        } else {
+            for (int i = 0; i < C.ntau; i++) {
+                const bool ab = Hk[i] > u;
+                any |= ab;
+                all &= ab;
+                if (ab) { if (fa < 0) fa = i; la = i; }
+                if (i > 0) {
+                    if (!prev && ab && cin < 0) cin = i - 1;
+                    if (prev && !ab) cout = i - 1;
+                }
+                prev = ab;
             }
-            prev = ab;
         }
         double a, b;
         if (!any) {
@@ -610,6 +619,27 @@ __global__ __launch_bounds__(BLOCK) void equilibrium_hetero_kernel(HeteroBufs L,
             }
         if (!ok) s_nonmono = 1;
     }
+    // per-group 64-entry block max / min of HR (sbr_scan.h) at the top of the LDS slab
+    const int ntau = L.n_tau[c];
+    const int nblk = (ntau + 63) >> 6;
+    const bool sums = fits && n + 2 * K * nblk <= a.lds_cap;
+    double* hsum = smem + (a.lds_cap - 2 * K * nblk);
+    if (sums) {
+        const double* __restrict__ Hc = L.hr + (size_t)c * K * cap;
+        for (int q = threadIdx.x; q < K * nblk; q += BLOCK) {
+            const int k = q / nblk, bk = q - k * nblk;
+            const double* __restrict__ Hk = Hc + (size_t)k * cap;
+            double mx = -INFINITY, mn = INFINITY;
+            const int e = (bk << 6) + 64 < ntau ? (bk << 6) + 64 : ntau;
+            for (int i = bk << 6; i < e; i++) {
+                const double h = Hk[i];
+                if (h > mx) mx = h;                            // NaN never > u: ignore it
+                mn = (h != h) ? -INFINITY : (h < mn ? h : mn);  // NaN is "not above"
+            }
+            hsum[(size_t)k * nblk + bk] = mx;
+            hsum[(size_t)(K + k) * nblk + bk] = mn;
+        }
+    }
     __syncthreads();
     const bool mono = s_nonmono == 0;
     const int j = blockIdx.x * BLOCK + threadIdx.x;
@@ -629,12 +659,12 @@ __global__ __launch_bounds__(BLOCK) void equilibrium_hetero_kernel(HeteroBufs L,
         st = ((lst & SBR_ARG_INVALID) || !(uj >= 0.0)) ? SBR_ARG_INVALID : (SBR_OOB | lbits);
     } else if (fits) {
         HCol<K, const double*> C{smem, L.G + (size_t)c * cap * K, L.hr + (size_t)c * K * cap, n, L.n_tau[c],
-                                 L.n_le[c], cap, eta[c], t_end[c]};
+                                 L.n_le[c], cap, eta[c], t_end[c], sums && !a.exhaustive ? hsum : nullptr, nblk};
         solve_hetero_point<K>(C, dl, uj, a.kappa, a.max_iters, a.tolerance, lbits, xi, aw, tol, st, it, tin, tout,
                               mono, a.diag);
     } else {
         HCol<K, const double*> C{gT, L.G + (size_t)c * cap * K, L.hr + (size_t)c * K * cap, n, L.n_tau[c],
-                                 L.n_le[c], cap, eta[c], t_end[c]};
+                                 L.n_le[c], cap, eta[c], t_end[c], nullptr, 0};
         solve_hetero_point<K>(C, dl, uj, a.kappa, a.max_iters, a.tolerance, lbits, xi, aw, tol, st, it, tin, tout,
                               mono, a.diag);
     }
