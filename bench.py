@@ -71,6 +71,7 @@ def parse():
     ap.add_argument("--social-cols", type=int, default=64, help="social: β columns per GPU (config 5: 512/8)")
     ap.add_argument("--social-max-iter", type=int, default=500)
     ap.add_argument("--social-prof", action="store_true", help="social: per-phase cycle breakdown (diagnostic)")
+    ap.add_argument("--social-dump", default="", help="social: save per-point status/fp_iters/rk_steps (.npz)")
     return ap.parse_args()
 
 
@@ -409,6 +410,9 @@ def main_social(a):
     steps = out["rk_steps"].cpu().numpy()
     st = out["status"].cpu().numpy().view(np.uint32)
     fp = out["fp_iters"].cpu().numpy()
+    if a.social_dump:
+        np.savez(a.social_dump, beta=beta_h, u=u_h, status=st, fp_iters=fp, rk_steps=steps,
+                 xi=out["xi"].cpu().numpy(), aw_max=out["aw_max"].cpu().numpy())
     total_pts = nb * nu * world
     res = {
         "metric": "equilibria solved/sec on β×u grid (FP64), social-learning fixed point",
@@ -420,7 +424,9 @@ def main_social(a):
         "config": {"workload": f"social_fixed_point_{nb}x{nu}_per_gpu (BASELINE config 5 share)",
                    "n_beta_per_gpu": nb, "n_u": nu, "eta": eta_v, "p": p, "kappa": kappa, "lambda": lam,
                    "tol": tol, "max_iter": a.social_max_iter, "parallelism": f"beta-column shards x{world}"},
-        "kernel_ms_per_step": {"social_init": init_ms / max(ncalls, 1), "social_iterates": iter_ms / max(ncalls, 1)},
+        "kernel_ms_per_step": {"social_init": init_ms / max(a.steps, 1), "social_iterates": iter_ms / max(a.steps, 1)},
+        "passes_per_step": ncalls / max(a.steps, 1),
+        "knot_overflow": eng.social_overflow_stats(),
         "rk_steps_per_point": float(steps.mean()),
         "fp_iters_mean": float(fp.mean()), "fp_iters_max": int(fp.max()),
         "run_fraction": float(((st & sbr.STATUS["SBR_RUN"]) > 0).mean()),

@@ -182,10 +182,13 @@ int sbr_sweep_hetero_dev(sbr_ctx* ctx, void* stream, int32_t K, const double* be
  * Host pointers; synchronous.  The HBM workspace is 5 × capacity doubles per
  * point in flight (opts->pad, default 98304 knots: ≈3.9 MB); large grids run
  * in chunks that fit sbr_set_social_workspace (default 60 % of free HBM).
- * Points whose iterates outgrow the capacity (the non-converging fringe of
- * config 5 reaches 450k knots) are re-run from scratch at 4× the capacity,
- * up to 4M knots, so results equal an unbounded grid's; only beyond that
- * does a point end with SBR_KNOT_OVERFLOW.
+ * A point whose iterate outgrows the capacity (the non-converging fringe of
+ * config 5 reaches 450k knots) moves with its AW_{n-1} into a pool of up to
+ * 256 slots of 16× the capacity (held beside the workspace, ≤ 15 % of free
+ * HBM) and redoes that iterate there within the same sweep; a point that
+ * outgrows the pool too, or finds it full, is re-run from scratch at 4× the
+ * pool capacity, up to 4M knots, so results equal an unbounded grid's; only
+ * beyond that does a point end with SBR_KNOT_OVERFLOW.
  */
 int sbr_sweep_social(sbr_ctx* ctx, const double* beta, const double* eta, double x0, const double* u, int64_t n_beta,
                      int64_t n_u, double p, double kappa, double lambda, const double* cmp_grid, int32_t n_cmp,
@@ -206,6 +209,9 @@ int sbr_set_social_workspace(sbr_ctx* ctx, int64_t bytes);
  * [1] forced ODE, [2] hazard + crossing scan, [3] bisection, [4] AW norm,
  * [5] damping / AW_max; [6] stage lookups past the register window; [7] RK steps. */
 int sbr_social_prof_read(sbr_ctx* ctx, int64_t* out8);
+/* Diagnostics of the last social sweep: points promoted into the pool and
+ * points re-run from scratch at a larger capacity (either may be NULL). */
+int sbr_social_overflow_stats(sbr_ctx* ctx, int64_t* promoted, int64_t* rerun);
 
 /* 5-consecutive-no-run early exit (1_baseline.jl:236-244) as a post-pass on
  * host arrays: points after `threshold` consecutive non-runs in a β column get

@@ -239,3 +239,48 @@ def social_point(beta, eta, u, p, kappa, lam, cmp, x0=1e-4, tol=1e-4, max_iter=5
     k = int(ntau[0])
     return dict(xi=res[0], tau_in_unc=res[1], tau_out_unc=res[2], aw_max=res[3], tol=res[4], status=int(st[0]),
                 fp_iters=int(fi[0]), t=t[:n].copy(), G=G[:n].copy(), hr_tau=tau[:k].copy())
+
+
+def sweep_interest(beta, eta, t_end, u, p, kappa, lam, r, delta, x0=1e-4, max_iters=100, nthreads=0):
+    """solve_learning + solve_equilibrium_interest (interest_rate_solver.jl:51-150) +
+    get_AW_functions_interest!(…).AW_max over β columns × u; rk_steps = value-function
+    Tsit5 steps per point (0 when r = 0)."""
+    L = lib()
+    L.sbro_sweep_interest.restype = ctypes.c_int
+    L.sbro_sweep_interest.argtypes = [_P, _P, _P, _D, _P, _I64, _I64, _D, _D, _D, _D, _D, _I32, _I32] + [_P] * 8
+    beta = np.ascontiguousarray(np.atleast_1d(beta), np.float64)
+    nb = len(beta)
+    eta = np.ascontiguousarray(np.broadcast_to(eta, (nb,)), np.float64)
+    t_end = np.ascontiguousarray(np.broadcast_to(t_end, (nb,)), np.float64)
+    u = np.ascontiguousarray(np.atleast_1d(u), np.float64)
+    nu = len(u)
+    o = {k: np.empty(nb * nu) for k in ("xi", "tau_in_unc", "tau_out_unc", "aw_max", "tol")}
+    o["status"] = np.empty(nb * nu, np.uint32)
+    o["iters"] = np.empty(nb * nu, np.int32)
+    o["rk_steps"] = np.empty(nb * nu, np.int64)
+    rc = L.sbro_sweep_interest(_ptr(beta), _ptr(eta), _ptr(t_end), x0, _ptr(u), nb, nu, p, kappa, lam, r, delta,
+                               max_iters, nthreads, _ptr(o["xi"]), _ptr(o["tau_in_unc"]), _ptr(o["tau_out_unc"]),
+                               _ptr(o["aw_max"]), _ptr(o["tol"]), _ptr(o["status"]), _ptr(o["iters"]),
+                               _ptr(o["rk_steps"]))
+    if rc != 0:
+        raise RuntimeError("oracle interest sweep failed")
+    return {k: v.reshape(nb, nu) for k, v in o.items()}
+
+
+def interest_point(beta, eta, t_end, u, p, kappa, lam, r, delta, x0=1e-4, cap=1 << 16):
+    """One interest-rate equilibrium with its HR grid τ̄, HR(τ̄) and the value function
+    V(τ̄) saved on that grid (value_function_solver.jl:66-112, saveat = HR knots)."""
+    L = lib()
+    L.sbro_interest_point.restype = _I64
+    L.sbro_interest_point.argtypes = [_D, _D, _D, _D, _D, _D, _D, _D, _D, _D, _P, _P, _P, _P, _P, _I64, _P]
+    res = np.zeros(5)
+    st = np.zeros(1, np.uint32)
+    tau, hr, V = np.empty(cap), np.empty(cap), np.empty(cap)
+    nv = np.zeros(1, np.int64)
+    n = L.sbro_interest_point(beta, eta, t_end, x0, u, p, kappa, lam, r, delta, _ptr(res), _ptr(st), _ptr(tau),
+                              _ptr(hr), _ptr(V), cap, _ptr(nv))
+    if n < 0:
+        raise RuntimeError(f"oracle interest path buffer too small ({-n} needed)")
+    k = int(nv[0])
+    return dict(xi=res[0], tau_in_unc=res[1], tau_out_unc=res[2], aw_max=res[3], tol=res[4], status=int(st[0]),
+                hr_tau=tau[:n].copy(), hr=hr[:n].copy(), V=V[:k].copy())

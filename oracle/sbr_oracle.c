@@ -28,6 +28,9 @@
  *              heterogeneity_solver.jl:48-144,175-210,241-293,316-375
  *   social     src/extensions/social_learning/social_learning_dynamics.jl:58-114,
  *              social_learning_solver.jl:63-263
+ *   interest   src/extensions/interest_rates/value_function_solver.jl:66-112,
+ *              interest_rate_solver.jl:51-150 (+ Tsit5's dense-output
+ *              interpolant for `saveat`, OrdinaryDiffEqTsit5 — not vendored)
  *
  * Parity pinning: the reference is Julia and cannot run in this container or
  * on the GPU box.  This restatement is pinned by the
@@ -194,14 +197,31 @@ static inline double rms_norm(const double* v, int m)
     return sqrt(s / (double)m);
 }
 
+/* called after every accepted step with (tprev, t, dt, uprev, u, k1..k7) — the
+ * integrator state OrdinaryDiffEq's savevalues! sees (saveat interpolation) */
+typedef void (*step_fn)(void* ctx, double tprev, double t, double dt, const double* uprev, const double* u,
+                        const double* const* k);
+
+static int tsit5_solve_cb(rhs_fn f, void* ctx, int m, double t0, double t1, const double* x0, double rtol,
+                          double atol, int64_t maxiters, knots_t* kn, ode_stats_t* st, step_fn on_step,
+                          void* step_ctx);
+
 static int tsit5_solve(rhs_fn f, void* ctx, int m, double t0, double t1, const double* x0, double rtol,
                        double atol, int64_t maxiters, knots_t* kn, ode_stats_t* st)
+{
+    return tsit5_solve_cb(f, ctx, m, t0, t1, x0, rtol, atol, maxiters, kn, st, NULL, NULL);
+}
+
+/* kn == NULL: no knots kept (saveat problems keep only what on_step saves) */
+static int tsit5_solve_cb(rhs_fn f, void* ctx, int m, double t0, double t1, const double* x0, double rtol,
+                          double atol, int64_t maxiters, knots_t* kn, ode_stats_t* st, step_fn on_step,
+                          void* step_ctx)
 {
     double x[MAXK], k1[MAXK], k2[MAXK], k3[MAXK], k4[MAXK], k5[MAXK], k6[MAXK], k7[MAXK];
     double tmp[MAXK], tmp6[MAXK], u[MAXK], sk[MAXK], buf[MAXK], f1[MAXK];
     int oob = 0;
     memset(st, 0, sizeof(*st));
-    kn->K = m;
+    if (kn) kn->K = m;
     const double dtmax = t1 - t0;
     const double dtmin = sbr_jl_eps(dmax(fabs(t0), fabs(t1)));
 
@@ -239,7 +259,7 @@ static int tsit5_solve(rhs_fn f, void* ctx, int m, double t0, double t1, const d
     double t = t0, qold = CTL_QOLDMIN, lqold = LOG_QOLDMIN;
     autoswitch_t as = {0, 0};
     st->t_switch = NAN;
-    if (knots_push(kn, t0, x)) return -1;
+    if (kn && knots_push(kn, t0, x)) return -1;
     int64_t iter = 0;
     while (t < t1) {
         if (++iter > maxiters) { st->status |= SBR_ODE_MAXITERS; break; }
@@ -304,10 +324,14 @@ static int tsit5_solve(rhs_fn f, void* ctx, int m, double t0, double t1, const d
             lqold = (qold == EEst) ? le : LOG_QOLDMIN;
             double tn = t + dt;
             if (fabs(tn - t1) < snap) tn = t1; /* 100 eps(max(t, t_end)), t < t_end */
+            if (on_step) {
+                const double* const ks[7] = {k1, k2, k3, k4, k5, k6, k7};
+                on_step(step_ctx, t, tn, dt, x, u, ks);
+            }
             t = tn;
             for (int i = 0; i < m; i++) { x[i] = u[i]; k1[i] = k7[i]; }
             dt = dmax(dmin(dtmax, dtnew), dtmin); /* calc_dt_propose! */
-            if (knots_push(kn, t, x)) return -1;
+            if (kn && knots_push(kn, t, x)) return -1;
         } else { /* reject: step_reject_controller!, q11 = EEst^β1 */
             st->nreject++;
             const double q11 = sbr_exp(CTL_BETA1 * le);
@@ -1053,4 +1077,214 @@ int64_t sbro_social_point(double beta, double eta, double x0, double u, double p
     *status = r.status;
     *n_tau = sp.n_tau;
     return (sp.n > cap || sp.n_tau > cap) ? -(sp.n > sp.n_tau ? sp.n : sp.n_tau) : sp.n;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Interest-rate extension (src/extensions/interest_rates/)                  */
+/* ------------------------------------------------------------------------ */
+/* Tsit5 dense-output coefficients (OrdinaryDiffEqTsit5 Tsit5Interp; not
+ * vendored).  Check: b_i(Θ=1) sums to the tableau's last row A7i (b7(1) = 0). */
+static const double R11 = 1.0, R12 = -2.763706197274826, R13 = 2.9132554618219126, R14 = -1.0530884977290216;
+static const double R22 = 0.13169999999999998, R23 = -0.2234, R24 = 0.1017;
+static const double R32 = 3.9302962368947516, R33 = -5.941033872131505, R34 = 2.490627285651253;
+static const double R42 = -12.411077166933676, R43 = 30.33818863028232, R44 = -16.548102889244902;
+static const double R52 = 37.50931341651104, R53 = -88.1789048947664, R54 = 47.37952196281928;
+static const double R62 = -27.896526289197286, R63 = 65.09189467479366, R64 = -34.87065786149660;
+static const double R72 = 1.5, R73 = -4.0, R74 = 2.5;
+
+/* _ode_interpolant(Θ, dt, y0, y1, k, ::Tsit5Cache, nothing, Val{0}) under
+ * @muladd: Horner polynomials (evalpoly → muladd) and the 7-term sum nested
+ * as muladd(k1, b1Θ, muladd(k2, b2Θ, … muladd(k6, b6Θ, k7·b7Θ))). */
+static double tsit5_dense(double th, double dt, double y0, const double* const* k)
+{
+    const double th2 = th * th;
+    const double b1 = th * fma(th, fma(th, fma(th, R14, R13), R12), R11);
+    const double b2 = th2 * fma(th, fma(th, R24, R23), R22);
+    const double b3 = th2 * fma(th, fma(th, R34, R33), R32);
+    const double b4 = th2 * fma(th, fma(th, R44, R43), R42);
+    const double b5 = th2 * fma(th, fma(th, R54, R53), R52);
+    const double b6 = th2 * fma(th, fma(th, R64, R63), R62);
+    const double b7 = th2 * fma(th, fma(th, R74, R73), R72);
+    const double sum = fma(k[0][0], b1, fma(k[1][0], b2, fma(k[2][0], b3, fma(k[3][0], b4,
+                           fma(k[4][0], b5, fma(k[5][0], b6, k[6][0] * b7))))));
+    return fma(dt, sum, y0);
+}
+
+typedef struct {
+    const double* tau; /* HR grid τ̄ */
+    const double* hr;
+    int64_t n;
+    double delta, r, u;
+} vf_ctx;
+
+/* hjb_equation! (value_function_solver.jl:86-95):
+ * dV = (h + δ)(1 − V) + max(u + rV − h, 0), h = HR(τ̄) (Throw() outside the grid) */
+static void rhs_value(void* ctx, double t, const double* V, double* dV, int* oob)
+{
+    const vf_ctx* c = (const vf_ctx*)ctx;
+    const double h = INTERP(c->tau, c->hr, c->n, t, oob);
+    const double x = (c->u + c->r * V[0]) - h;
+    const double re = (x != x) ? x : (x > 0.0 ? x : 0.0); /* Julia max(x, 0.0): NaN wins, max(-0.0, 0.0) = 0.0 */
+    dV[0] = (h + c->delta) * (1.0 - V[0]) + re;
+}
+
+typedef struct {
+    const double* grid; /* saveat = the HR grid */
+    int64_t n, next;
+    double* V;
+} saveat_t;
+
+/* savevalues! with saveat: every pending point ≤ t, interpolated at
+ * Θ = (s − tprev)/dt unless it is t itself (then the step's u) */
+static void saveat_step(void* ctx, double tprev, double t, double dt, const double* y0, const double* y1,
+                        const double* const* k)
+{
+    saveat_t* s = (saveat_t*)ctx;
+    while (s->next < s->n && s->grid[s->next] <= t) {
+        const double ts = s->grid[s->next];
+        s->V[s->next++] = (ts != t) ? tsit5_dense((ts - tprev) / dt, dt, y0[0], k) : y1[0];
+    }
+}
+
+/* solve_value_function(hr, δ, r, u; tol = eps()) on the HR grid; returns the
+ * saved prefix length (== n unless the solve stopped early), V[0..) values */
+static int64_t value_function(const hazard_t* h, double delta, double r, double u, int64_t maxiters, double* V,
+                              ode_stats_t* st)
+{
+    vf_ctx c = {h->tau, h->hr, h->n, delta, r, u};
+    const double V0 = (u + delta) / (r + delta);
+    saveat_t sv = {h->tau, h->n, 1, V};
+    V[0] = V0; /* save_start: τ̄_1 = 0 = tspan[1] */
+    const double eps = 2.220446049250313e-16;
+    tsit5_solve_cb(rhs_value, &c, 1, 0.0, h->tau[h->n - 1], &V0, eps, eps, maxiters, NULL, st, saveat_step, &sv);
+    return sv.next;
+}
+
+/* solve_equilibrium_interest (interest_rate_solver.jl:51-150) for one u given
+ * the learning knots and the hazard; V_out (may be NULL) receives V on the grid */
+static void interest_point(const double* t, const double* G, int64_t n, const hazard_t* h, double t_end, double u,
+                           double kappa, double r, double delta, int32_t max_iters, point_t* res, double* V_out,
+                           int64_t* n_v, int64_t* steps, double* aw_path)
+{
+    memset(res, 0, sizeof(*res));
+    res->xi = NAN;
+    res->aw_max = NAN;
+    res->tol = INFINITY;
+    if (n_v) *n_v = 0;
+    if (steps) *steps = 0;
+    if (h->oob) { res->status = SBR_OOB; res->tin = res->tout = NAN; return; }
+    uint32_t bits = 0;
+    if (r > 0.0) {
+        double* V = (double*)malloc((size_t)h->n * sizeof(double));
+        double* hv = (double*)malloc((size_t)h->n * sizeof(double));
+        ode_stats_t st;
+        const int64_t ns = value_function(h, delta, r, u, SBR_DEFAULT_ODE_MAXITERS, V, &st);
+        bits = st.status & (SBR_ODE_MAXITERS | SBR_STIFF_SWITCH | SBR_ODE_FAILED | SBR_OOB);
+        if (steps) *steps = st.naccept + st.nreject;
+        if (n_v) *n_v = ns;
+        if (V_out) memcpy(V_out, V, (size_t)ns * sizeof(double));
+        /* h_rV on V's knots (= the saved grid): HR(t) − r·V(t), both interpolants
+         * evaluated at their own knots (interest_rate_solver.jl:88-90) */
+        int oob = 0;
+        for (int64_t i = 0; i < ns; i++)
+            hv[i] = INTERP(h->tau, h->hr, h->n, h->tau[i], &oob) - r * INTERP(h->tau, V, ns, h->tau[i], &oob);
+        if (oob || (bits & SBR_OOB)) {
+            res->status = SBR_OOB | bits;
+            res->tin = res->tout = NAN;
+            free(V); free(hv);
+            return;
+        }
+        optimal_buffer(u, h->tau, hv, ns, t_end, &res->tin, &res->tout);
+        free(V);
+        free(hv);
+    } else {
+        optimal_buffer(u, h->tau, h->hr, h->n, t_end, &res->tin, &res->tout);
+    }
+    if (res->tin == res->tout) {
+        res->status = SBR_NO_RUN_HR_BELOW_U | SBR_CONVERGED | bits;
+        res->tol = 0.0;
+        return;
+    }
+    double xi, tol;
+    uint32_t s = compute_xi(res->tin, res->tout, t, G, n, kappa, max_iters, &xi, &tol, &res->iters);
+    if (s != SBR_RUN) { res->status = s | bits; return; }
+    int oob = 0;
+    double mx = get_aw(xi, res->tin, res->tout, h->tau, h->n, t, G, n, aw_path, &oob);
+    if (oob) { res->status = SBR_OOB | bits; return; }
+    res->xi = xi;
+    res->tol = tol;
+    res->aw_max = mx;
+    res->status = SBR_RUN | SBR_CONVERGED | bits;
+}
+
+/* β × u sweep of the interest-rate equilibrium: learning + hazard per β
+ * column (as the baseline), then the value function and equilibrium per u. */
+int sbro_sweep_interest(const double* beta, const double* eta, const double* t_end, double x0, const double* u,
+                        int64_t n_beta, int64_t n_u, double p, double kappa, double lambda, double r, double delta,
+                        int32_t max_iters, int32_t nthreads, double* xi, double* tin, double* tout, double* aw_max,
+                        double* tol, uint32_t* status, int32_t* iters, int64_t* steps)
+{
+    int rc = 0;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 1) reduction(| : rc)
+#endif
+    for (int64_t b = 0; b < n_beta; b++) {
+        const double eps = 2.220446049250313e-16;
+        knots_t kn = {0};
+        ode_stats_t st;
+        double bt = beta[b];
+        if (tsit5_solve(rhs_logistic, &bt, 1, 0.0, t_end[b], &x0, eps, eps, SBR_DEFAULT_ODE_MAXITERS, &kn, &st)) {
+            rc |= 1;
+            continue;
+        }
+        double* g = (double*)malloc((size_t)kn.n * sizeof(double));
+        for (int64_t i = 0; i < kn.n; i++) g[i] = (bt * kn.x[i]) * (1.0 - kn.x[i]);
+        hazard_t h;
+        hazard_rate(kn.t, g, kn.n, p, lambda, eta[b], 0, &h);
+        const uint32_t lbits = st.status & (SBR_ODE_MAXITERS | SBR_STIFF_SWITCH | SBR_ODE_FAILED);
+        for (int64_t j = 0; j < n_u; j++) {
+            const int64_t o = b * n_u + j;
+            point_t res;
+            int64_t ns = 0;
+            interest_point(kn.t, kn.x, kn.n, &h, t_end[b], u[j], kappa, r, delta, max_iters, &res, NULL, NULL,
+                           steps ? &ns : NULL, NULL);
+            xi[o] = res.xi; tin[o] = res.tin; tout[o] = res.tout; aw_max[o] = res.aw_max; tol[o] = res.tol;
+            status[o] = res.status | lbits;
+            if (iters) iters[o] = res.iters;
+            if (steps) steps[o] = ns;
+        }
+        hazard_free(&h);
+        free(g);
+        knots_free(&kn);
+    }
+    return rc;
+}
+
+/* one point with its paths (figure parity): res[5] = ξ, τ̄_IN, τ̄_OUT, AW_max, tol;
+ * hr_tau / hr_v / V (n_hr each, caller-sized ≥ the learning knot count + 1) */
+int64_t sbro_interest_point(double beta, double eta, double t_end, double x0, double u, double p, double kappa,
+                            double lambda, double r, double delta, double* res, uint32_t* status, double* hr_tau,
+                            double* hr_v, double* V, int64_t cap, int64_t* n_v)
+{
+    const double eps = 2.220446049250313e-16;
+    knots_t kn = {0};
+    ode_stats_t st;
+    if (tsit5_solve(rhs_logistic, &beta, 1, 0.0, t_end, &x0, eps, eps, SBR_DEFAULT_ODE_MAXITERS, &kn, &st)) return -1;
+    double* g = (double*)malloc((size_t)kn.n * sizeof(double));
+    for (int64_t i = 0; i < kn.n; i++) g[i] = (beta * kn.x[i]) * (1.0 - kn.x[i]);
+    hazard_t h;
+    hazard_rate(kn.t, g, kn.n, p, lambda, eta, 0, &h);
+    int64_t nh = h.n;
+    if (nh > cap) { hazard_free(&h); free(g); knots_free(&kn); return -nh; }
+    point_t pr;
+    interest_point(kn.t, kn.x, kn.n, &h, t_end, u, kappa, r, delta, 100, &pr, V, n_v, NULL, NULL);
+    res[0] = pr.xi; res[1] = pr.tin; res[2] = pr.tout; res[3] = pr.aw_max; res[4] = pr.tol;
+    *status = pr.status | (st.status & (SBR_ODE_MAXITERS | SBR_STIFF_SWITCH | SBR_ODE_FAILED));
+    memcpy(hr_tau, h.tau, (size_t)nh * sizeof(double));
+    memcpy(hr_v, h.hr, (size_t)nh * sizeof(double));
+    hazard_free(&h);
+    free(g);
+    knots_free(&kn);
+    return nh;
 }

@@ -299,6 +299,13 @@ struct Summ {
 };
 
 template <class P>
+__device__ __forceinline__ void solve_from_buffers(P T, P G, P H, const Summ& S, const int n, const int ntau,
+                                                   const int nle, const double ETA, const double T1, const bool trunc,
+                                                   const double u, const double kappa, const int max_iters,
+                                                   const uint32_t lbits, PointResult& r, double* __restrict__ aw_path,
+                                                   const int diag, const double tin, const double tout);
+
+template <class P>
 __device__ __forceinline__ void solve_point(P T, P G, P H, const Summ& S, const int n, const int ntau,
                                             const int nle, const double ETA, const double T1, const bool trunc,
                                             const double u, const double kappa, const int max_iters,
@@ -306,7 +313,7 @@ __device__ __forceinline__ void solve_point(P T, P G, P H, const Summ& S, const 
                                             const int diag)
 {
     r.xi = NAN; r.aw = NAN; r.tol = INFINITY; r.iters = 0; r.status = 0;
-    const double tlo = T[0], thi = T[n - 1];
+    (void)0;
 
     // ---------------- optimal_buffer: crossings of HR(τ̄) with u ----------------
     bool any, all;
@@ -351,6 +358,21 @@ __device__ __forceinline__ void solve_point(P T, P G, P H, const Summ& S, const 
     r.tin = tin;
     r.tout = tout;
     if (diag & 1) return;
+    solve_from_buffers(T, G, H, S, n, ntau, nle, ETA, T1, trunc, u, kappa, max_iters, lbits, r, aw_path, diag,
+                       tin, tout);
+}
+
+// solve_equilibrium_baseline from the buffer times on (solver.jl:429-462) + get_AW / AW_max:
+// no run if τ̄_IN == τ̄_OUT, else compute_ξ on G and AW_max on the τ̄ grid.
+template <class P>
+__device__ __forceinline__ void solve_from_buffers(P T, P G, P H, const Summ& S, const int n, const int ntau,
+                                                   const int nle, const double ETA, const double T1, const bool trunc,
+                                                   const double u, const double kappa, const int max_iters,
+                                                   const uint32_t lbits, PointResult& r, double* __restrict__ aw_path,
+                                                   const int diag, const double tin, const double tout)
+{
+    const double tlo = T[0], thi = T[n - 1];
+    auto tau = [&](int i) -> double { return i < nle ? T[i] : ETA; };
     if (tin == tout) {
         r.status = SBR_NO_RUN_HR_BELOW_U | SBR_CONVERGED | lbits;
         r.tol = 0.0;
@@ -376,7 +398,7 @@ __device__ __forceinline__ void solve_point(P T, P G, P H, const Summ& S, const 
     for (int iter = 1; iter <= max_iters; iter++) {
         r.iters = iter;
         const double dd = xmin - xmax;
-        if (fabs(dd) < 2.0 * sbr_jl_eps(dd)) { s = SBR_NO_RUN_COLLAPSE; break; }
+        if (collapsed(dd)) { s = SBR_NO_RUN_COLLAPSE; break; }
         if (iter == max_iters - 1) { s = SBR_NO_RUN_MAXITER; break; }
         const double xo = xnew;
         const double ic = dmin(tin, xo), oc = dmin(tout, xo);

@@ -39,7 +39,16 @@ struct sbr_ctx {
     int32_t *so_n_old = nullptr, *so_live = nullptr, *so_work[2] = {nullptr, nullptr}, *so_count = nullptr;
     uint32_t *so_slots = nullptr, *so_bits = nullptr;
     int64_t* so_steps = nullptr;
+    // promotion pool (sbr::SocialPool); so_count = [list 0, list 1, pool used, pool live]
+    size_t pl_slots = 0, pl_cap = 0, pl_cmp = 0;
+    double *pl_ws = nullptr, *pl_cmpo = nullptr, *pl_xi = nullptr;
+    int32_t *pl_n_old = nullptr, *pl_live = nullptr, *pl_it = nullptr, *pl_ready = nullptr;
+    uint32_t *pl_perm = nullptr, *pl_bits = nullptr;
+    int64_t *pl_steps = nullptr, *pl_pts = nullptr;
     int32_t* so_count_host = nullptr; // pinned
+    sbr::SocialArgs* so_args_dev = nullptr;  // {main, pool} arguments of the iterate kernel
+    sbr::SocialArgs* so_args_host = nullptr; // pinned staging for them
+    int64_t so_promoted = 0, so_rerun = 0; // last sweep: points promoted into the pool / re-run larger
     int64_t so_budget = 0;            // workspace bytes (0: 60 % of free HBM)
     int64_t* so_prof = nullptr;       // SBR_FLAG_DIAG_SOCIAL_PROF: [pts][8]
     size_t so_prof_pts = 0;
@@ -167,14 +176,51 @@ int ensure_social(sbr_ctx* c, size_t pts, size_t cap, size_t n_cmp)
     HIP_TRY(c, hipMalloc(&c->so_live, pts * 4), SBR_ENOMEM);
     HIP_TRY(c, hipMalloc(&c->so_work[0], pts * 4), SBR_ENOMEM);
     HIP_TRY(c, hipMalloc(&c->so_work[1], pts * 4), SBR_ENOMEM);
-    HIP_TRY(c, hipMalloc(&c->so_count, 2 * 4), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&c->so_count, 8 * 4), SBR_ENOMEM);
     HIP_TRY(c, hipMalloc(&c->so_slots, pts * 4), SBR_ENOMEM);
     HIP_TRY(c, hipMalloc(&c->so_bits, pts * 4), SBR_ENOMEM);
     HIP_TRY(c, hipMalloc(&c->so_steps, pts * 8), SBR_ENOMEM);
-    if (!c->so_count_host) HIP_TRY(c, hipHostMalloc(&c->so_count_host, 2 * 4), SBR_ENOMEM);
+    if (!c->so_count_host) HIP_TRY(c, hipHostMalloc(&c->so_count_host, 8 * 4), SBR_ENOMEM);
+    if (!c->so_args_dev) HIP_TRY(c, hipMalloc(&c->so_args_dev, 2 * sizeof(sbr::SocialArgs)), SBR_ENOMEM);
+    if (!c->so_args_host) HIP_TRY(c, hipHostMalloc(&c->so_args_host, 2 * sizeof(sbr::SocialArgs)), SBR_ENOMEM);
     c->so_pts = pts;
     c->so_cap = cap;
     c->so_cmp = n_cmp;
+    return SBR_OK;
+}
+
+void free_pool(sbr_ctx* c)
+{
+    void* ps[] = {c->pl_ws, c->pl_cmpo, c->pl_xi, c->pl_n_old, c->pl_live, c->pl_it, c->pl_ready,
+                  c->pl_perm, c->pl_bits, c->pl_steps, c->pl_pts};
+    for (void* p : ps)
+        if (p) (void)hipFree(p);
+    c->pl_ws = c->pl_cmpo = c->pl_xi = nullptr;
+    c->pl_n_old = c->pl_live = c->pl_it = c->pl_ready = nullptr;
+    c->pl_perm = c->pl_bits = nullptr;
+    c->pl_steps = c->pl_pts = nullptr;
+    c->pl_slots = c->pl_cap = c->pl_cmp = 0;
+}
+
+int ensure_pool(sbr_ctx* c, size_t slots, size_t cap, size_t n_cmp)
+{
+    if (slots <= c->pl_slots && cap == c->pl_cap && n_cmp <= c->pl_cmp) return SBR_OK;
+    free_pool(c);
+    slots = (slots + 63) & ~(size_t)63;
+    HIP_TRY(c, hipMalloc(&c->pl_ws, slots * 5 * cap * 8), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&c->pl_cmpo, slots * n_cmp * 8), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&c->pl_xi, slots * 8), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&c->pl_n_old, slots * 4), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&c->pl_live, slots * 4), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&c->pl_it, slots * 4), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&c->pl_ready, slots * 4), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&c->pl_perm, slots * 4), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&c->pl_bits, slots * 4), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&c->pl_steps, slots * 8), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&c->pl_pts, slots * 8), SBR_ENOMEM);
+    c->pl_slots = slots;
+    c->pl_cap = cap;
+    c->pl_cmp = n_cmp;
     return SBR_OK;
 }
 
@@ -312,8 +358,11 @@ int sbr_free(sbr_ctx* c)
     for (int k = 0; k < sbr_ctx::kLearnSlots; k++) free_learn(c, k);
     free_hetero(c);
     free_social(c);
+    free_pool(c);
     if (c->so_prof) (void)hipFree(c->so_prof);
     if (c->so_count_host) (void)hipHostFree(c->so_count_host);
+    if (c->so_args_dev) (void)hipFree(c->so_args_dev);
+    if (c->so_args_host) (void)hipHostFree(c->so_args_host);
     if (c->ev_in) (void)hipEventDestroy(c->ev_in);
     for (int k = 0; k < sbr_ctx::kLearnSlots; k++) {
         if (c->ev_learned[k]) (void)hipEventDestroy(c->ev_learned[k]);
@@ -661,6 +710,14 @@ int sbr_social_prof_read(sbr_ctx* c, int64_t* out8)
     return SBR_OK;
 }
 
+int sbr_social_overflow_stats(sbr_ctx* c, int64_t* promoted, int64_t* rerun)
+{
+    if (!c) return SBR_EARG;
+    if (promoted) *promoted = c->so_promoted;
+    if (rerun) *rerun = c->so_rerun;
+    return SBR_OK;
+}
+
 int sbr_set_social_workspace(sbr_ctx* c, int64_t bytes)
 {
     if (!c || bytes < 0) return SBR_EARG;
@@ -673,6 +730,8 @@ int sbr_set_social_workspace(sbr_ctx* c, int64_t bytes)
 namespace {
 constexpr int kSocialDefaultCap = 98304;  // ≈1.4× the typical longest iterate on config 5 (≈70k knots)
 constexpr int kSocialMaxCap = 1 << 22;    // overflow retries grow 4× per pass up to this
+constexpr int64_t kPoolSlots = 256;       // promotion pool slots (points that outgrow the capacity)
+constexpr int kSocialInner = 16;          // fixed-point iterates per launch (compaction in between)
 
 int social_checks(sbr_ctx* c, const double* beta, const double* eta, const double* u, int64_t n_beta, int64_t n_u,
                   double x0, double p, double kappa, double lambda, const double* cmp, int32_t n_cmp, double tol,
@@ -689,18 +748,24 @@ int social_checks(sbr_ctx* c, const double* beta, const double* eta, const doubl
 
 // one pass of the whole fixed point over points [0, n_total) (list == nullptr)
 // or over the global point indices list[0 .. n_total), chunked by workspace
-// size; poll > 0 reads the live count every `poll` iterates and stops early.
+// size; poll > 0 reads the live counts after every launch and stops early.
+// Points whose iterate outgrows `cap` are promoted into the pool (16× the
+// capacity) and redo that iterate from the pool blocks of the same or the next launch.
 int run_social_pass(sbr_ctx* c, hipStream_t s, const double* beta, const double* eta, double x0, const double* u,
                     int64_t n_u, double p, double kappa, double lambda, const double* cmp, int32_t n_cmp, double tol,
                     int32_t max_iter, const sbr_opts& o, sbr_result_soa* out, int32_t* fp_iters, int64_t* rk_steps,
-                    int poll, size_t cap, const int64_t* list, int64_t n_total)
+                    int poll, size_t cap, size_t pcap, const int64_t* list, int64_t n_total)
 {
     const size_t per_pt = 5 * cap * 8 + (size_t)n_cmp * 8 + 64;
-    int64_t budget = c->so_budget;
-    if (budget <= 0) {
+    const size_t per_slot = 5 * pcap * 8 + (size_t)n_cmp * 8 + 64;
+    int64_t budget = c->so_budget, pbudget = 0;
+    {
         size_t fr = 0, tot = 0;
         HIP_TRY(c, hipMemGetInfo(&fr, &tot), SBR_EDEVICE);
-        budget = (int64_t)((double)(fr + c->so_pts * (5 * c->so_cap * 8 + c->so_cmp * 8 + 64)) * 0.6);
+        const double avail = (double)fr + (double)c->so_pts * (5 * c->so_cap * 8 + c->so_cmp * 8 + 64) +
+                             (double)c->pl_slots * (5 * c->pl_cap * 8 + c->pl_cmp * 8 + 64);
+        if (budget <= 0) budget = (int64_t)(avail * 0.6);
+        pbudget = (int64_t)(avail * 0.15);
     }
     int64_t chunk = budget / (int64_t)per_pt;
     if (chunk < 64 && !list) return fail(c, SBR_ENOMEM, "social workspace budget below 64 points");
@@ -710,6 +775,15 @@ int run_social_pass(sbr_ctx* c, hipStream_t s, const double* beta, const double*
     else if (chunk >= 64) chunk &= ~(int64_t)63; // whole wave groups
     int rc = ensure_social(c, (size_t)chunk, cap, (size_t)n_cmp);
     if (rc) return rc;
+    // pool: up to kPoolSlots slots (whole wave groups) within its budget
+    int64_t nslots = pcap > cap ? pbudget / (int64_t)per_slot : 0;
+    if (nslots > kPoolSlots) nslots = kPoolSlots;
+    if (nslots > chunk) nslots = chunk;
+    if (nslots >= 64) nslots &= ~(int64_t)63;
+    if (nslots > 0) {
+        rc = ensure_pool(c, (size_t)nslots, pcap, (size_t)n_cmp);
+        if (rc) return rc;
+    }
     const bool prof = (o.flags & SBR_FLAG_DIAG_SOCIAL_PROF) != 0;
     if (prof && c->so_prof_pts < (size_t)chunk) {
         if (c->so_prof) (void)hipFree(c->so_prof);
@@ -735,24 +809,56 @@ int run_social_pass(sbr_ctx* c, hipStream_t s, const double* beta, const double*
         a.fp_iters = fp_iters;
         a.steps_out = rk_steps;
         a.prof = prof ? c->so_prof : nullptr;
+        a.pool = sbr::SocialPool{};
+        sbr::SocialArgs b{}; // the pool's own arguments (n_pts = 0: no pool blocks)
+        if (nslots > 0) {
+            a.pool = sbr::SocialPool{c->pl_ws,    (int32_t)pcap, (int32_t)nslots, c->so_count + 2, c->so_count + 3,
+                                     c->pl_pts,   c->pl_n_old,   c->pl_perm,      c->pl_xi,        c->pl_bits,
+                                     c->pl_steps, c->pl_live,    c->pl_it,        c->pl_ready};
+            b = a;
+            b.pt0 = 0; b.pts = c->pl_pts; b.n_pts = (int32_t)nslots; b.cap = (int32_t)pcap;
+            b.ws = c->pl_ws; b.cmpo = c->pl_cmpo; b.n_old = c->pl_n_old; b.slots = c->pl_perm; b.xi_new = c->pl_xi;
+            b.bits = c->pl_bits; b.steps = c->pl_steps; b.live = c->pl_live; b.work = nullptr; b.count = nullptr;
+            b.prof = nullptr;
+            b.pool = sbr::SocialPool{};
+            b.it_cur = c->pl_it; b.ready = c->pl_ready; b.n_live = c->so_count + 3;
+            HIP_TRY(c, hipMemsetAsync(c->pl_ready, 0, (size_t)nslots * 4, s), SBR_EDEVICE);
+        }
+        HIP_TRY(c, hipMemsetAsync(c->so_count + 2, 0, 2 * 4, s), SBR_EDEVICE); // pool allocator + live
+        // (the staging buffer is reused by the next chunk only after this one's final sync)
+        c->so_args_host[0] = a;
+        c->so_args_host[1] = b;
+        HIP_TRY(c, hipMemcpyAsync(c->so_args_dev, c->so_args_host, 2 * sizeof(sbr::SocialArgs),
+                                  hipMemcpyHostToDevice, s),
+                SBR_EDEVICE);
         if (prof) HIP_TRY(c, hipMemsetAsync(c->so_prof, 0, (size_t)npts * 64, s), SBR_EDEVICE);
         hipEvent_t t0 = tstart(c, s);
         HIP_TRY(c, sbr::launch_social_init(a, s), SBR_EDEVICE);
         tend(c, s, 0, t0);
         t0 = tstart(c, s);
-        for (int it = 1; it <= max_iter; it++) {
-            const int k = (it - 1) & 1;
-            HIP_TRY(c, sbr::launch_social_iter(a, it, c->so_work[k], c->so_count + k, c->so_work[k ^ 1],
-                                               c->so_count + (k ^ 1), s),
+        // kSocialInner iterates per launch; a point promoted during a launch redoes that
+        // iterate in the same or the next launch: one launch past max_iter drains the pool
+        const int n_launch = (max_iter + kSocialInner - 1) / kSocialInner + (nslots > 0 ? 1 : 0);
+        for (int q = 0; q < n_launch; q++) {
+            const int k = q & 1, it = 1 + q * kSocialInner;
+            HIP_TRY(c, sbr::launch_social_iter(a, b, c->so_args_dev, it, kSocialInner, c->so_work[k],
+                                               c->so_count + k, c->so_work[k ^ 1], c->so_count + (k ^ 1), s),
                     SBR_EDEVICE);
-            if (poll > 0 && (it % poll == 0) && it < max_iter) {
-                HIP_TRY(c, hipMemcpyAsync(c->so_count_host, c->so_count + (k ^ 1), 4, hipMemcpyDeviceToHost, s),
+            if (poll > 0 && q + 1 < n_launch) {
+                HIP_TRY(c, hipMemcpyAsync(c->so_count_host, c->so_count, 4 * 4, hipMemcpyDeviceToHost, s),
                         SBR_EDEVICE);
                 HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
-                if (c->so_count_host[0] == 0) break;
+                if (c->so_count_host[k ^ 1] == 0 && c->so_count_host[3] == 0) break;
             }
         }
         tend(c, s, 1, t0);
+        // promotions of this chunk (diagnostics), and the sync that frees the argument staging
+        HIP_TRY(c, hipMemcpyAsync(c->so_count_host + 2, c->so_count + 2, 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
+        if (nslots > 0) {
+            const int64_t used = c->so_count_host[2];
+            c->so_promoted += used < nslots ? used : nslots;
+        }
         if (prof) {
             std::vector<int64_t> h((size_t)npts * 8);
             HIP_TRY(c, hipMemcpyAsync(h.data(), c->so_prof, h.size() * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
@@ -763,9 +869,12 @@ int run_social_pass(sbr_ctx* c, hipStream_t s, const double* beta, const double*
     return SBR_OK;
 }
 
-// Every point at the default knot capacity, then the (few) points whose iterates
-// outgrew it again, from scratch, at 4x the capacity, up to kSocialMaxCap: the
-// results are those of an unbounded grid.  Finding them synchronises `s` once.
+size_t pool_cap(size_t cap) { return cap * 16 < (size_t)kSocialMaxCap ? cap * 16 : (size_t)kSocialMaxCap; }
+
+// Every point at the default knot capacity with a 16× promotion pool, then the
+// (rare) points that outgrew the pool or found it full, from scratch, at 4× the
+// pool capacity, up to kSocialMaxCap: the results are those of an unbounded
+// grid.  Finding them synchronises `s` once.
 int run_social(sbr_ctx* c, hipStream_t s, const double* beta, const double* eta, double x0, const double* u,
                int64_t n_beta, int64_t n_u, double p, double kappa, double lambda, const double* cmp, int32_t n_cmp,
                double tol, int32_t max_iter, const sbr_opts& o, sbr_result_soa* out, int32_t* fp_iters,
@@ -774,20 +883,25 @@ int run_social(sbr_ctx* c, hipStream_t s, const double* beta, const double* eta,
     const int64_t n_total = n_beta * n_u;
     size_t cap = o.pad > 0 ? (size_t)o.pad : (size_t)kSocialDefaultCap;
     cap = (cap + 15) & ~(size_t)15; // 16-knot lines of the wave-blocked layout
+    if (cap > (size_t)kSocialMaxCap) cap = (size_t)kSocialMaxCap;
     c->so_prof_acc.assign(8, 0);
+    c->so_promoted = c->so_rerun = 0;
     int rc = run_social_pass(c, s, beta, eta, x0, u, n_u, p, kappa, lambda, cmp, n_cmp, tol, max_iter, o, out,
-                             fp_iters, rk_steps, poll, cap, nullptr, n_total);
+                             fp_iters, rk_steps, poll, cap, pool_cap(cap), nullptr, n_total);
     if (rc) return rc;
     std::vector<uint32_t> st((size_t)n_total);
     int64_t* dlist = nullptr;
-    while (cap < (size_t)kSocialMaxCap) {
+    size_t reached = pool_cap(cap);
+    while (reached < (size_t)kSocialMaxCap) {
         HIP_TRY(c, hipMemcpyAsync(st.data(), out->status, (size_t)n_total * 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
         HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
         std::vector<int64_t> idx;
         for (int64_t g = 0; g < n_total; g++)
             if (st[(size_t)g] & SBR_KNOT_OVERFLOW) idx.push_back(g);
         if (idx.empty()) break;
-        cap = cap * 4 < (size_t)kSocialMaxCap ? cap * 4 : (size_t)kSocialMaxCap;
+        c->so_rerun += (int64_t)idx.size();
+        cap = reached * 4 < (size_t)kSocialMaxCap ? reached * 4 : (size_t)kSocialMaxCap;
+        reached = cap;
         if (dlist) (void)hipFree(dlist);
         dlist = nullptr;
         HIP_TRY(c, hipMalloc(&dlist, idx.size() * 8), SBR_ENOMEM);
@@ -795,7 +909,7 @@ int run_social(sbr_ctx* c, hipStream_t s, const double* beta, const double* eta,
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         if (e != hipSuccess) { (void)hipFree(dlist); return fail(c, SBR_EDEVICE, "overflow list", e); }
         rc = run_social_pass(c, s, beta, eta, x0, u, n_u, p, kappa, lambda, cmp, n_cmp, tol, max_iter, o, out,
-                             fp_iters, rk_steps, poll, cap, dlist, (int64_t)idx.size());
+                             fp_iters, rk_steps, poll, cap, cap, dlist, (int64_t)idx.size());
         if (rc) { (void)hipFree(dlist); return rc; }
     }
     if (dlist) {

@@ -40,6 +40,12 @@ constexpr double AUTOSWITCH_TOL = 0.9;
 constexpr int AUTOSWITCH_MAXSTIFF = 10;
 constexpr double DBL_EPS = 2.220446049250313e-16;
 
+// The bisection's collapse test `abs(d) < 2·eps(d)` (solver.jl:440) in one
+// compare: for a normal d, 2·eps(d) = 2^(e-51) is far below |d| ≥ 2^e; for a
+// subnormal d, eps(d) = 2^-1074, so the test holds exactly when |d| ≤ 2^-1074
+// (d = ±0 or ±denorm_min); NaN and ±Inf fail both forms.
+__device__ __forceinline__ bool collapsed(double d) { return fabs(d) <= 4.9406564584124654e-324; }
+
 __device__ __forceinline__ double dmin(double a, double b) { return a < b ? a : b; }
 __device__ __forceinline__ double dmax(double a, double b) { return a > b ? a : b; }
 

@@ -385,7 +385,7 @@ __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const d
     for (int iter = 1; iter <= max_iters; iter++) {
         it_o = iter;
         const double dd = xmin - xmax;
-        if (fabs(dd) < 2.0 * sbr_jl_eps(dd)) { s = SBR_NO_RUN_COLLAPSE; break; }
+        if (collapsed(dd)) { s = SBR_NO_RUN_COLLAPSE; break; }
         if (iter == max_iters - 1) { s = SBR_NO_RUN_MAXITER; break; }
         const double xo = xnew;
         if (!(xo >= tlo)) { flag |= SBR_OOB; break; }  // searchsortedlast = 0: BoundsError

@@ -70,8 +70,29 @@ struct HeteroEqArgs {
     int32_t diag;       // SBR_FLAG_DIAG_* bits >> 8 (timing breakdown only)
 };
 
+// Promotion pool of the social sweep: a point whose iterate outgrows the knot
+// capacity moves (AW_{n-1} and its carried state) into a free slot here and
+// redoes that iterate from the pool blocks of the same or the next launch,
+// concurrently with the main worklist.
+struct SocialPool {
+    double* ws;          // [n_slots][5][cap] wave-blocked like the main workspace
+    int32_t cap;
+    int32_t n_slots;
+    int32_t* used;       // slot allocator (atomic counter)
+    int32_t* n_live;     // promoted points not finished yet
+    int64_t* pts;        // slot -> global point
+    int32_t* n_old;
+    uint32_t* slots;
+    double* xi_new;
+    uint32_t* bits;
+    int64_t* steps;
+    int32_t* live;
+    int32_t* it_cur;     // next iterate of the slot's point
+    int32_t* ready;      // 1 once the slot's state is published (release / acquire)
+};
+
 // Social-learning fixed point (sbr_social.hip): one lane per point; per-point
-// workspace of 5 knot buffers × cap doubles (point-major) + n_cmp doubles.
+// workspace of 5 knot buffers × cap doubles (wave-blocked) + n_cmp doubles.
 struct SocialArgs {
     const double* beta;  // [n_beta]
     const double* eta;   // [n_beta]
@@ -101,11 +122,20 @@ struct SocialArgs {
     int32_t* fp_iters;   // fixed-point iterations (may be null)
     int64_t* steps_out;  // RK steps per point, written when it finishes (may be null)
     int64_t* prof;       // diagnostics [n_pts][8] cycles per phase + counters (may be null)
+    SocialPool pool;     // large-capacity slots for points that outgrow `cap` (ws null: none)
+    // set on the pool's own arguments only: per-point iterate, published flag, live counter
+    int32_t* it_cur;
+    int32_t* ready;
+    int32_t* n_live;
 };
 
 hipError_t launch_social_init(const SocialArgs& a, hipStream_t s);
-hipError_t launch_social_iter(const SocialArgs& a, int iter, const int32_t* work, const int32_t* count,
-                              int32_t* work_out, int32_t* count_out, hipStream_t s);
+// n_inner iterates (from `iter`) over `work`/`count` plus every published pool
+// slot (`p`, n_pts = 0: no pool), then the ordered compaction of the main
+// worklist into work_out; args_dev holds {a, p} in device memory
+hipError_t launch_social_iter(const SocialArgs& a, const SocialArgs& p, const SocialArgs* args_dev, int iter,
+                              int n_inner, const int32_t* work, const int32_t* count, int32_t* work_out,
+                              int32_t* count_out, hipStream_t s);
 
 hipError_t launch_hetero(int K, const double* betas, const double* dist, const double* eta, const double* t_end,
                          const double* u, const LearnArgs& la, const HeteroEqArgs& ea, const HeteroBufs& L,

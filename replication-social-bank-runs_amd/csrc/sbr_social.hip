@@ -13,9 +13,11 @@
 //  * one lane per grid point for the whole fixed point — the forced ODE is a
 //    serial chain of ~10⁵ Tsit5 steps per iterate, so points are the only
 //    parallelism; lanes of a wave hold consecutive u of one β column;
-//  * each point owns five knot buffers of `cap` doubles in HBM (point-major:
-//    a lane walks its own contiguous rows): AW_{n−1} knots/values, G_n knots,
-//    values and AW_{n−1}(t_i) at those knots; buffers rotate between iterates;
+//  * each point owns five knot buffers of `cap` doubles in HBM (wave-blocked,
+//    see BView): AW_{n−1} knots/values, G_n knots, values and AW_{n−1}(t_i) at
+//    those knots; buffers rotate between iterates;
+//  * a point whose iterate outgrows `cap` moves into a promotion pool of 16×
+//    the capacity and redoes that iterate there (pool blocks of the same launch);
 //  * one launch per fixed-point iterate over a worklist of unfinished points;
 //    a single-workgroup ballot compaction (order-preserving, deterministic)
 //    retires finished lanes so later iterates launch only live waves.
@@ -141,9 +143,40 @@ __device__ __forceinline__ double interp_full(BView t, BView v, int n, double x,
     return lerp_at(t, v, n, ssl_range(t, 0, n - 1, x), x);
 }
 
-__device__ __forceinline__ BView buf(const SocialArgs& a, int l, int slot)
+__device__ __forceinline__ BView buf_at(double* ws, int cap, int l, int slot)
 {
-    return BView{a.ws + ((size_t)(l >> 6) * 5 + (size_t)slot) * (size_t)a.cap * 64 + (size_t)(l & 63) * 16};
+    return BView{ws + ((size_t)(l >> 6) * 5 + (size_t)slot) * (size_t)cap * 64 + (size_t)(l & 63) * 16};
+}
+__device__ __forceinline__ BView buf(const SocialArgs& a, int l, int slot) { return buf_at(a.ws, a.cap, l, slot); }
+
+// Move a point whose iterate outgrew the knot capacity into a pool slot with
+// its state from before that iterate (AW_{n-1}, ξ, status bits, step count);
+// the pool blocks of this or the next launch redo the iterate.  False when
+// the pool is full (the point then retires with SBR_KNOT_OVERFLOW and the
+// host re-runs it at a larger capacity).
+__device__ bool promote(const SocialArgs& a, int l, int64_t g, int iter, BView TO, BView VO, int n_old)
+{
+    const SocialPool& q = a.pool;
+    if (n_old > q.cap) return false;
+    const int s = atomicAdd(q.used, 1);
+    if (s >= q.n_slots) return false;
+    BView BT = buf_at(q.ws, q.cap, s, 0), BV = buf_at(q.ws, q.cap, s, 1);
+    for (int i = 0; i < n_old; i++) {
+        BT[i] = TO[i];
+        BV[i] = VO[i];
+    }
+    q.n_old[s] = n_old;
+    q.slots[s] = 0u | (1u << 3) | (2u << 6) | (3u << 9) | (4u << 12);
+    q.xi_new[s] = a.xi_new[l];
+    q.bits[s] = a.bits[l];
+    q.steps[s] = a.steps[l];
+    q.live[s] = 1;
+    q.pts[s] = g;
+    q.it_cur[s] = iter;
+    atomicAdd(q.n_live, 1);
+    __hip_atomic_store(q.ready + s, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    a.live[l] = 0;
+    return true;
 }
 
 // ---------------------------------------------------------------------------
@@ -476,15 +509,12 @@ __global__ __launch_bounds__(64) void social_init_kernel(SocialArgs a)
 }
 
 // ============================================================================
-// one fixed-point iterate for every live point of the worklist
 // ============================================================================
-__global__ __launch_bounds__(64) void social_iter_kernel(SocialArgs a, int iter, const int32_t* __restrict__ work,
-                                                         const int32_t* __restrict__ count)
+// one fixed-point iterate of point l (local index into a's per-point state);
+// false once the point has finished or moved into the promotion pool
+// ============================================================================
+__device__ __forceinline__ bool social_iterate(const SocialArgs& a, int l, int iter)
 {
-    const int w = blockIdx.x * 64 + threadIdx.x;
-    if (w >= *count) return;
-    const int l = work[w];
-    if (!a.live[l]) return; // retired by the init kernel (knot overflow)
     const int64_t g = a.pts ? a.pts[l] : a.pt0 + l;
     const int b = (int)(g / a.n_u);
     const int ju = (int)(g % a.n_u);
@@ -535,6 +565,7 @@ __global__ __launch_bounds__(64) void social_iter_kernel(SocialArgs a, int iter,
     stamp(1);
     if (PR) { PR[6] += f.slow; PR[7] += o.naccept + o.nreject; }
     if (f.oob) o.status |= SBR_OOB;
+    if (overflow && a.pool.ws && promote(a, l, g, iter, TO, VO, n_old)) return false;
     a.steps[l] += o.naccept + o.nreject;
     bits |= o.status & (SBR_ODE_MAXITERS | SBR_STIFF_SWITCH | SBR_ODE_FAILED);
 
@@ -628,7 +659,7 @@ __global__ __launch_bounds__(64) void social_iter_kernel(SocialArgs a, int iter,
                 for (int32_t k = 1; k <= a.bisect_max_iters; k++) {
                     it_r = k;
                     const double d = xmin - xmax;
-                    if (fabs(d) < 2.0 * sbr_jl_eps(d)) { st_r = SBR_NO_RUN_COLLAPSE; break; }
+                    if (collapsed(d)) { st_r = SBR_NO_RUN_COLLAPSE; break; }
                     if (k == a.bisect_max_iters - 1) { st_r = SBR_NO_RUN_MAXITER; break; }
                     const double xo = xnew;
                     const double ic = dmin(tin, xo), oc = dmin(tout, xo);
@@ -798,15 +829,56 @@ __global__ __launch_bounds__(64) void social_iter_kernel(SocialArgs a, int iter,
         if (a.fp_iters) a.fp_iters[g] = iter;
         if (a.steps_out) a.steps_out[g] = a.steps[l];
         a.live[l] = 0;
-    } else {
-        a.live[l] = 1;
-        a.xi_new[l] = xi_n;
-        a.n_old[l] = n;
-        a.bits[l] = bits;
-        // rotate: AW_n = (t_n, damped) ; free = old knots, old values, G_n
-        a.slots[l] = (uint32_t)s_t | ((uint32_t)s_aw << 3) | ((uint32_t)s_to << 6) | ((uint32_t)s_vo << 9) |
-                     ((uint32_t)s_G << 12);
+        if (a.n_live) atomicSub(a.n_live, 1);
+        return false;
     }
+    a.live[l] = 1;
+    if (a.it_cur) a.it_cur[l] = iter + 1;
+    a.xi_new[l] = xi_n;
+    a.n_old[l] = n;
+    a.bits[l] = bits;
+    // rotate: AW_n = (t_n, damped) ; free = old knots, old values, G_n
+    a.slots[l] = (uint32_t)s_t | ((uint32_t)s_aw << 3) | ((uint32_t)s_to << 6) | ((uint32_t)s_vo << 9) |
+                 ((uint32_t)s_G << 12);
+    return true;
+}
+
+// ============================================================================
+// up to n_inner fixed-point iterates for every live point of the worklist
+// ============================================================================
+// Lanes run their iterates back to back; the grid-wide boundary (and the
+// worklist compaction after it) comes every n_inner iterates, so a launch is
+// not held to the slowest point of every single iterate.
+// Blocks past the main worklist's grid serve the promotion pool: slot l runs
+// its own next iterates once published (a point promoted during this launch is
+// picked up here or by the next launch; either way it redoes that iterate).
+// args[0]: the main worklist's arguments, args[1]: the pool's (n_pts = 0: none),
+// in device memory so that the wave-uniform choice between them stays scalar loads.
+__global__ __launch_bounds__(64) void social_iter_kernel(const SocialArgs* __restrict__ args, int iter_arg,
+                                                         int n_inner, const int32_t* __restrict__ work,
+                                                         const int32_t* __restrict__ count)
+{
+    const SocialArgs& sa = args[0];
+    const SocialArgs& pa = args[1];
+    const int nbs = (sa.n_pts + 63) >> 6;
+    const bool in_pool = (int)blockIdx.x >= nbs;
+    int l, iter;
+    if (!in_pool) {
+        const int w = blockIdx.x * 64 + threadIdx.x;
+        if (w >= *count) return;
+        l = work[w];
+        if (!sa.live[l]) return; // retired by the init kernel (knot overflow)
+        iter = iter_arg;
+    } else {
+        l = ((int)blockIdx.x - nbs) * 64 + threadIdx.x;
+        if (l >= pa.n_pts) return;
+        if (__hip_atomic_load(pa.ready + l, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
+        if (!pa.live[l]) return;
+        iter = pa.it_cur[l];
+    }
+    const SocialArgs& a = args[in_pool ? 1 : 0];
+    for (int k = 0; k < n_inner; k++)
+        if (!social_iterate(a, l, iter + k)) break;
 }
 
 // ============================================================================
@@ -858,10 +930,12 @@ hipError_t launch_social_init(const SocialArgs& a, hipStream_t s)
     return hipGetLastError();
 }
 
-hipError_t launch_social_iter(const SocialArgs& a, int iter, const int32_t* work, const int32_t* count,
-                              int32_t* work_out, int32_t* count_out, hipStream_t s)
+hipError_t launch_social_iter(const SocialArgs& a, const SocialArgs& p, const SocialArgs* args_dev, int iter,
+                              int n_inner, const int32_t* work, const int32_t* count, int32_t* work_out,
+                              int32_t* count_out, hipStream_t s)
 {
-    hipLaunchKernelGGL(social_iter_kernel, dim3((a.n_pts + 63) / 64), dim3(64), 0, s, a, iter, work, count);
+    hipLaunchKernelGGL(social_iter_kernel, dim3((a.n_pts + 63) / 64 + (p.n_pts + 63) / 64), dim3(64), 0, s,
+                       args_dev, iter, n_inner, work, count);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(social_compact_kernel, dim3(1), dim3(CMP_BLOCK), 0, s, work, count, a.live, work_out,

@@ -99,6 +99,7 @@ _SIGS = {
                                             _P, _P, _P]),
     "sbr_set_social_workspace": (ctypes.c_int, [_P, _I64]),
     "sbr_social_prof_read": (ctypes.c_int, [_P, _P]),
+    "sbr_social_overflow_stats": (ctypes.c_int, [_P, _P, _P]),
 }
 
 _lib: ctypes.CDLL | None = None

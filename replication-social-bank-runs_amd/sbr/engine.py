@@ -239,6 +239,13 @@ class Engine:
         check(self._L.sbr_social_prof_read(self._ctx, v), self._ctx, "sbr_social_prof_read")
         return list(v)
 
+    def social_overflow_stats(self) -> dict:
+        """Last social sweep: points promoted into the 16x pool / re-run from scratch larger."""
+        a, b = ctypes.c_int64(), ctypes.c_int64()
+        check(self._L.sbr_social_overflow_stats(self._ctx, ctypes.byref(a), ctypes.byref(b)), self._ctx,
+              "sbr_social_overflow_stats")
+        return dict(promoted=a.value, rerun=b.value)
+
     def device_info(self) -> dict:
         a, b, c = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
         check(self._L.sbr_device_info(self._ctx, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)), self._ctx,

@@ -94,3 +94,27 @@ def test_social_chunked_workspace(engine):
     assert len(beta) * len(u) > 2 * 70
     for k in FIELDS + ("status", "iters", "fp_iters", "rk_steps"):
         assert_bitwise(small[k], full[k], k)
+
+
+def test_social_knot_overflow_promotion_and_rerun(engine, oracle):
+    """Iterates that outgrow the knot capacity: at 4096 knots points move mid-sweep into
+    the 16x pool and redo the iterate from their saved AW_{n-1}; at 1024 knots the pool
+    (16384) overflows as well and points re-run from scratch at 65536+.  Every field,
+    status bit, iteration count and RK step count equals the default-capacity sweep and
+    the oracle."""
+    beta = 1.0 / sbr.julia_range("0.01", "2", 512)
+    u = sbr.julia_range("0.001", "1", 512)
+    bsel = beta[[0, 128, 511]]
+    usel = u[[25, 140, 511]]
+    cmp = sbr.julia_range(0.0, ETA, 1000)
+    o = oracle.sweep_social(bsel, ETA, usel, P, KAPPA, LAM, cmp, max_iter=6)
+    ref = engine.sweep_social(bsel, ETA, usel, P, KAPPA, LAM, cmp=cmp, max_iter=6)
+    assert engine.social_overflow_stats() == dict(promoted=0, rerun=0)
+    _compare(ref, o)
+    for cap, want in ((4096, "promoted"), (1024, "rerun")):
+        g = engine.sweep_social(bsel, ETA, usel, P, KAPPA, LAM, cmp=cmp, max_iter=6, knot_capacity=cap)
+        stats = engine.social_overflow_stats()
+        assert stats[want] > 0, (cap, stats)
+        _compare(g, o)
+        assert_bitwise(g["rk_steps"], ref["rk_steps"], f"rk_steps at capacity {cap}")
+        assert not (g["status"] & sbr.STATUS["SBR_KNOT_OVERFLOW"]).any()

@@ -230,6 +230,39 @@ def hetero_figure(ref: Path):
     )
 
 
+# --------------------------------------------------------------------------- interest rates
+def interest_figures(ref: Path):
+    """scripts/3_interest_rates.jl (β=1, η_bar=15, u=0, p=0.5, κ=0.6, λ=0.01, r=0.06, δ=0.1).
+    value_function.pdf (:88-117): V on τ = range(0, min(η, last V knot), 500), drawn at
+    t = ξ − τ for t ≥ 0 in reverse, xlims (0, max t) — the count of drawn samples and the
+    first sample's offset from the t = 0 axis give ξ; the y map comes from two known values,
+    V(τ = 0) = (u+δ)/(r+δ) (the last sample) and the terminal line δ/(δ−r).
+    hazard_decomposition.pdf (:123-185): h(τ) and the rV(τ) threshold on
+    τ = range(0, min(η, ξ), 1000) share one y scale, so y_h / y_rV = HR(τ_k) / (r V(τ_k)) is
+    scale-free; sample j of each drawn path is τ index 999 − j."""
+    P = stroked_paths(ref / "output/figures/interest_rates/value_function.pdf")
+    v = by_color(P, ROYALBLUE, lambda n: n > 10)[0]
+    term = by_color(P, (0.6627, 0.6627, 0.6627), 2)[0][0][1]
+    x_axis0 = 52.59  # t = 0 (left gridline / axis)
+    x_axis1 = v[-1][0]  # t = ξ − 0 = ξ, the last sample (xlims (0, max t))
+    r, delta, u = 0.06, 0.1, 0.0
+    V0, Vterm = (u + delta) / (r + delta), delta / (delta - r)
+    sy = (term - v[-1][1]) / (Vterm - V0)
+    vf = dict(n_samples=len(v), tau_step_den=499, eta=15.0, x_first=v[0][0], x_axis0=x_axis0, x_axis1=x_axis1,
+              V=[round(V0 + (y - v[-1][1]) / sy, 6) for _, y in reversed(v)], V_precision=0.01 / sy,
+              note="V[k] = V(τ_k), τ_k = 15 k / 499, k = 0..n-1 (the drawn path reversed); "
+                   "ξ − τ_{n−1} = ξ (x_first − x_axis0) / (x_axis1 − x_axis0)")
+    H = stroked_paths(ref / "output/figures/interest_rates/hazard_decomposition.pdf")
+    h = by_color(H, (0.7804, 0.0824, 0.5216), 1000)[0]
+    th = by_color(H, (0.6627, 0.6627, 0.6627), 1000)[0]
+    y0 = 44.21
+    hz = dict(n=1000, y0=y0, y_h=[y for _, y in h], y_rV=[y for _, y in th], y_precision=0.005,
+              note="path sample j is τ index 999 − j of range(0, min(η, ξ), 1000); "
+                   "(y_h − y0)/(y_rV − y0) = HR(τ)/(r V(τ))")
+    return dict(params=dict(beta=1.0, eta_bar=15.0, eta=15.0, t_end=30.0, u=u, p=0.5, kappa=0.6, lam=0.01, r=r,
+                            delta=delta), value_function=vf, hazard_decomposition=hz)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
@@ -278,6 +311,7 @@ def main():
     het = dict(params=dict(betas=[0.125, 12.5], dist=[0.9, 0.1], eta_bar=30.0, u=0.1, p=0.9, kappa=0.3, lam=0.1),
                **hetero_figure(ref))
     (OUT / "hetero.json").write_text(json.dumps(het, indent=1))
+    (OUT / "interest_rates.json").write_text(json.dumps(interest_figures(ref)))
     print("wrote", sorted(p.name for p in OUT.iterdir()))
 
 
