@@ -64,9 +64,11 @@ def parse():
     ap.add_argument("--phases", action="store_true",
                     help="also time the equilibrium kernel stopped after each stage (diagnostic flags)")
     ap.add_argument("--traffic", default=str(REPO / "profiles" / "traffic_latest.json"))
-    ap.add_argument("--workload", choices=("baseline", "social", "hetero"), default="baseline",
+    ap.add_argument("--workload", choices=("baseline", "social", "hetero", "interest"), default="baseline",
                     help="baseline: BASELINE config 3 (the metric); social: config 5 per-GPU share; "
-                         "hetero: config 4 (K = 8, 1024x1024 per GPU)")
+                         "hetero: config 4 (K = 8, 1024x1024 per GPU); interest: the interest-rate "
+                         "extension on the Fig 5 grid (500x500 per GPU, r = 0.06, delta = 0.1)")
+    ap.add_argument("--interest-n", type=int, default=500, help="interest: β columns per GPU and u rows")
     ap.add_argument("--hetero-n", type=int, default=1024, help="hetero: columns per GPU and u rows")
     ap.add_argument("--social-cols", type=int, default=64, help="social: β columns per GPU (config 5: 512/8)")
     ap.add_argument("--social-max-iter", type=int, default=500)
@@ -81,6 +83,8 @@ def main():
         return main_social(a)
     if a.workload == "hetero":
         return main_hetero(a)
+    if a.workload == "interest":
+        return main_interest(a)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -331,6 +335,103 @@ def main_hetero(a):
         pts = sub.betas.shape[0] * nu
         res["cpu_baseline"] = {"value": pts / dt, "unit": "equilibria/s", "cores": cores, "kind": "port",
                                "sample": f"{sub.betas.shape[0]} columns (every 16th) x {nu} u = {pts} equilibria "
+                                         f"in {dt:.2f} s"}
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def main_interest(a):
+    """Interest-rate extension (interest_rate_solver.jl:51-150, value_function_solver.jl:66-112)
+    on the Fig 5 grid shape: β = 1/range(1e-4, 1, n·N) (η = 15, tspan (0, 30) carried),
+    u = range(0.001, 1, n), p = 0.5, κ = 0.6, λ = 0.01 and scripts/3_interest_rates.jl's
+    r = 0.06, δ = 0.1.  Weak scaling over β columns.  One step = learning + hazard per
+    column and, per (β, u), the value-function Tsit5 solve on the HR grid, the buffers
+    on h − rV, the ξ bisection and AW_max."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    n = a.interest_n
+    beta_all = 1.0 / sbr.julia_range("0.0001", "1", n * world)
+    beta_h = np.ascontiguousarray(beta_all[rank::world])
+    u_h = sbr.julia_range("0.001", "1", n)
+    nb, nu = len(beta_h), len(u_h)
+    r_, delta, p, kappa, lam, x0 = 0.06, 0.1, 0.5, 0.6, 0.01, 1e-4
+    beta = torch.from_numpy(beta_h).to(dev)
+    eta = torch.full((nb,), 15.0, dtype=torch.float64, device=dev)
+    t_end = torch.full((nb,), 30.0, dtype=torch.float64, device=dev)
+    u = torch.from_numpy(u_h).to(dev)
+    out = {k: torch.empty(nb * nu, dtype=torch.float64, device=dev) for k in sbr.engine.RESULT_FIELDS}
+    out["status"] = torch.empty(nb * nu, dtype=torch.int32, device=dev)
+    out["iters"] = torch.empty(nb * nu, dtype=torch.int32, device=dev)
+    out["rk_steps"] = torch.empty(nb * nu, dtype=torch.int64, device=dev)
+    eng = sbr.Engine(local)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    gather = world > 1 and not a.no_gather
+    g_aw = [torch.empty(nb * nu, dtype=torch.float64, device=dev) for _ in range(world)] if gather and rank == 0 \
+        else None
+
+    def step():
+        eng.sweep_interest_dev(beta, eta, t_end, u, p, kappa, lam, r_, delta, x0, out, stream=stream)
+        if gather:
+            dist.gather(out["aw_max"], g_aw, dst=0)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    eng.timing_read(stream)
+    eng.timing_enable(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    learn_ms, eq_ms, ncalls = eng.timing_read(stream)
+    eng.timing_enable(False)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    st = out["status"].cpu().numpy().view(np.uint32)
+    steps = out["rk_steps"].cpu().numpy()
+    res = {
+        "metric": "equilibria solved/sec on β×u grid (FP64), interest-rate extension (value function per point)",
+        "value": nb * nu * world * a.steps / elapsed,
+        "unit": "equilibria/s",
+        "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (deterministic Fig-5-shaped parameter grid; no RNG in the reference)",
+        "config": {"workload": f"interest_fig5_{nb}x{nu}_per_gpu (extension, SURVEY.md §8(f) rank 2)",
+                   "n_beta_per_gpu": nb, "n_u": nu, "r": r_, "delta": delta, "eta": 15.0, "t_end": 30.0, "p": p,
+                   "kappa": kappa, "lambda": lam, "parallelism": f"beta-column shards x{world}"},
+        "kernel_ms_per_step": {"learn_logistic": learn_ms / max(ncalls, 1), "interest_equilibrium": eq_ms / max(ncalls, 1)},
+        "value_fn_rk_steps_per_point": float(steps.mean()),
+        "run_fraction": float(((st & sbr.STATUS["SBR_RUN"]) > 0).mean()),
+        "stiff_switch_fraction": float(((st & sbr.STATUS["SBR_STIFF_SWITCH"]) > 0).mean()),
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        sys.path.insert(0, str(REPO / "oracle"))
+        import oracle as O  # noqa: E402  (test infrastructure: cpu_baseline leg only)
+
+        O.build()
+        cores = max(1, min(16, len(os.sched_getaffinity(0))))
+        sub = beta_h[::10]
+        t1 = time.perf_counter()
+        O.sweep_interest(sub, 15.0, 30.0, u_h, p, kappa, lam, r_, delta, nthreads=cores)
+        dt = time.perf_counter() - t1
+        pts = len(sub) * nu
+        res["cpu_baseline"] = {"value": pts / dt, "unit": "equilibria/s", "cores": cores, "kind": "port",
+                               "sample": f"{len(sub)} columns (every 10th) x {nu} u = {pts} equilibria "
                                          f"in {dt:.2f} s"}
     if rank == 0:
         print(json.dumps(res), flush=True)

@@ -213,6 +213,28 @@ int sbr_social_prof_read(sbr_ctx* ctx, int64_t* out8);
  * points re-run from scratch at a larger capacity (either may be NULL). */
 int sbr_social_overflow_stats(sbr_ctx* ctx, int64_t* promoted, int64_t* rerun);
 
+/* Interest-rate extension over a β × u grid (one call replaces the loop over
+ *     lr = solve_learning(ModelParametersInterest(β_i, η_i, tspan = (0, t_end_i), …).learning)
+ *     r  = solve_equilibrium_interest(lr, econ(u_j, p, κ, λ, r, δ), model)
+ *                                          interest_rate_solver.jl:51-150
+ *     get_AW_functions_interest!(r).AW_max  interest_rate_solver.jl:163-184
+ * ): with r > 0 every point integrates the value function
+ *     dV/dτ̄ = (HR(τ̄) + δ)(1 − V) + max(u + rV − HR(τ̄), 0),  V(0) = (u+δ)/(r+δ)
+ * (value_function_solver.jl:66-112; Tsit5, reltol = abstol = opts->ode_reltol/abstol,
+ * saved on the HR grid by the method's dense output) and takes its buffers from
+ * h − rV > u; r = 0 is the baseline sweep.  Result layout and status bits as
+ * sbr_sweep_baseline (no early-exit post-pass); rk_steps (may be NULL) = value-
+ * function Tsit5 steps per point.  SBR_EARG unless 0 <= r < delta
+ * (interest_rate_model.jl:48-50).  Host pointers; synchronous. */
+int sbr_sweep_interest(sbr_ctx* ctx, const double* beta, const double* eta, const double* t_end, double x0,
+                       const double* u, int64_t n_beta, int64_t n_u, double p, double kappa, double lambda, double r,
+                       double delta, const sbr_opts* opts, sbr_result_soa* out, int64_t* rk_steps);
+/* Same on device pointers, enqueued on `stream`. */
+int sbr_sweep_interest_dev(sbr_ctx* ctx, void* stream, const double* beta, const double* eta, const double* t_end,
+                           double x0, const double* u, int64_t n_beta, int64_t n_u, double p, double kappa,
+                           double lambda, double r, double delta, const sbr_opts* opts, sbr_result_soa* out,
+                           int64_t* rk_steps);
+
 /* 5-consecutive-no-run early exit (1_baseline.jl:236-244) as a post-pass on
  * host arrays: points after `threshold` consecutive non-runs in a β column get
  * SBR_SKIPPED_EARLY_EXIT, xi = aw_max = NaN, tol = Inf. */

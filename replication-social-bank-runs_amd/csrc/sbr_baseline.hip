@@ -567,10 +567,284 @@ __device__ __forceinline__ void solve_from_buffers(P T, P G, P H, const Summ& S,
     if (diag & 4) r.iters = nblk_eval;
 }
 
-template <int BLOCK>
+// ============================================================================
+// Interest-rate extension (src/extensions/interest_rates/)
+// ============================================================================
+// τ̄ grid view: knots ≤ η, then η (hazard_rate's grid, solver.jl:155-161)
+template <class P>
+struct TauView {
+    P T;
+    int nle;
+    double eta;
+    __device__ __forceinline__ double operator[](int i) const { return i < nle ? T[i] : eta; }
+};
+
+// Tsit5 dense-output coefficients (OrdinaryDiffEqTsit5 Tsit5Interp) — as oracle tsit5_dense
+constexpr double R11 = 1.0, R12 = -2.763706197274826, R13 = 2.9132554618219126, R14 = -1.0530884977290216;
+constexpr double R22 = 0.13169999999999998, R23 = -0.2234, R24 = 0.1017;
+constexpr double R32 = 3.9302962368947516, R33 = -5.941033872131505, R34 = 2.490627285651253;
+constexpr double R42 = -12.411077166933676, R43 = 30.33818863028232, R44 = -16.548102889244902;
+constexpr double R52 = 37.50931341651104, R53 = -88.1789048947664, R54 = 47.37952196281928;
+constexpr double R62 = -27.896526289197286, R63 = 65.09189467479366, R64 = -34.87065786149660;
+constexpr double R72 = 1.5, R73 = -4.0, R74 = 2.5;
+
+// the step's interpolant at Θ (saveat): Horner b_i(Θ), nested muladd sum
+__device__ __forceinline__ double tsit5_dense(double th, double dt, double y0, double k1, double k2, double k3,
+                                              double k4, double k5, double k6, double k7)
+{
+    const double th2 = th * th;
+    const double b1 = th * fma(th, fma(th, fma(th, R14, R13), R12), R11);
+    const double b2 = th2 * fma(th, fma(th, R24, R23), R22);
+    const double b3 = th2 * fma(th, fma(th, R34, R33), R32);
+    const double b4 = th2 * fma(th, fma(th, R44, R43), R42);
+    const double b5 = th2 * fma(th, fma(th, R54, R53), R52);
+    const double b6 = th2 * fma(th, fma(th, R64, R63), R62);
+    const double b7 = th2 * fma(th, fma(th, R74, R73), R72);
+    const double sum = fma(k1, b1, fma(k2, b2, fma(k3, b3, fma(k4, b4, fma(k5, b5, fma(k6, b6, k7 * b7))))));
+    return fma(dt, sum, y0);
+}
+
+// hjb_equation! (value_function_solver.jl:86-95): dV = (h + δ)(1 − V) + max(u + rV − h, 0)
+// with h = HR(τ̄) (gridded linear, Throw()); brackets galloped from the step's own.
+template <class P>
+struct ValueRhs {
+    TauView<P> tau;
+    P H;
+    int ntau;
+    double delta, r, u, tlo, thi;
+    int jb;
+    bool oob;
+    __device__ __forceinline__ double hr(double t)
+    {
+        if (ntau < 2 || !(t >= tlo && t <= thi)) { oob = true; return (double)NAN; }
+        const int j = (tau[jb] <= t) ? ssl_gallop(tau, ntau, jb, t) : ssl_range(tau, 0, jb, t);
+        return lerp_at(tau, H, ntau, j, t);
+    }
+    __device__ __forceinline__ double operator()(double t, double V)
+    {
+        const double h = hr(t);
+        const double x = (u + r * V) - h;
+        const double re = (x != x) ? x : (x > 0.0 ? x : 0.0); // Julia max(x, 0.0)
+        return (h + delta) * (1.0 - V) + re;
+    }
+    __device__ __forceinline__ void accepted(double t)
+    {
+        if (ntau >= 2 && t >= tlo && t <= thi) jb = ssl_gallop(tau, ntau, jb, t);
+    }
+};
+
+// The value function saved on the HR grid (saveat) streamed into optimal_buffer
+// on h − rV (interest_rate_solver.jl:84-93, solver.jl:211-264): V(τ̄_i) and HR(τ̄_i)
+// are their interpolants at their own knots (v_i·(1−0) + v_{i+1}·0, the last knot
+// v_{n−2}·0 + v_{n−1}·1), so knot i is scanned once V_{i+1} is known.
+template <class P>
+struct SaveScan {
+    TauView<P> tau;
+    P H;
+    int ntau;
+    double r, u;
+    int next;        // grid index of the next saved value
+    double vprev;    // V at knot next − 1 (its h − rV waits for V_next)
+    double vprev2;   // V at knot next − 2
+    int nh;          // h − rV values scanned
+    double hprev;    // h − rV at knot nh − 1
+    bool any, all;
+    int fa, la, cin, cout;
+    double tin_x, tout_x; // crossing lerps (valid when cin / cout ≥ 0)
+    __device__ __forceinline__ void init(double V0)
+    {
+        next = 1; vprev = V0; vprev2 = 0.0; nh = 0; hprev = 0.0;
+        any = false; all = true; fa = la = cin = cout = -1; tin_x = tout_x = 0.0;
+    }
+    __device__ __forceinline__ void scan(double hv)
+    {
+        const int i = nh;
+        const bool ab = hv > u;
+        any |= ab;
+        all &= ab;
+        if (ab) { if (fa < 0) fa = i; la = i; }
+        if (i > 0) {
+            const bool pab = hprev > u;
+            const double t0 = tau[i - 1], t1 = tau[i];
+            if (!pab && ab && cin < 0) { cin = i - 1; tin_x = t0 + ((u - hprev) * (t1 - t0)) / (hv - hprev); }
+            if (pab && !ab) { cout = i - 1; tout_x = t0 + ((u - hprev) * (t1 - t0)) / (hv - hprev); }
+        }
+        hprev = hv;
+        nh = i + 1;
+    }
+    // V_k saved (k = next): knot k − 1 is interior to V's grid now
+    __device__ __forceinline__ void save(double v)
+    {
+        const int i = next - 1;
+        const double ti = tau[i], t1 = tau[i + 1];
+        const double d = (ti - ti) / (t1 - ti);
+        const double Vi = vprev * (1.0 - d) + v * d;
+        scan(lerp_at(tau, H, ntau, i, ti) - r * Vi);
+        vprev2 = vprev;
+        vprev = v;
+        next++;
+    }
+    // after the solve: the last saved knot (j = n − 2, δ = 1)
+    __device__ __forceinline__ void finish()
+    {
+        const int i = next - 1;
+        const double t0 = tau[i - 1], ti = tau[i];
+        const double d = (ti - t0) / (ti - t0);
+        const double Vi = vprev2 * (1.0 - d) + vprev * d;
+        scan(lerp_at(tau, H, ntau, i, ti) - r * Vi);
+    }
+};
+
+// Tsit5 (oracle tsit5_solve_cb, m = 1) with the accepted-step hook on_step(tprev, t, dt,
+// uprev, u, k1..k7) that OrdinaryDiffEq's savevalues! sees.
+template <class Rhs, class OnStep>
+__device__ __forceinline__ void tsit5_hooked(Rhs& f, OnStep& on_step, double T1, double x0, double rtol,
+                                             double atol, int64_t maxiters, uint32_t& status, int64_t& nsteps)
+{
+    const double T0 = 0.0;
+    const double dtmax = T1 - T0;
+    const double dtmin = sbr_jl_eps(dmax(fabs(T0), fabs(T1)));
+    const double sk = fma(fabs(x0), rtol, atol);
+    const double d0 = fabs(x0 / sk);
+    double k1 = f(T0, x0);
+    const double d1 = fabs(k1 / sk);
+    double dt0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * (d0 / d1);
+    dt0 = dmin(dt0, dtmax);
+    double dt;
+    if (dt0 < 10.0 * DBL_EPS) {
+        dt = dmax(1e-6, dtmin);
+    } else {
+        const double u1 = fma(dt0, k1, x0);
+        const double f1 = f(T0 + dt0, u1);
+        if (k1 == f1) {
+            dt = dmax(dtmin, 100.0 * dt0);
+        } else {
+            const double d2 = fabs((f1 - k1) / sk) / dt0;
+            const double md = dmax(d1, d2);
+            const double dt1 = (md <= 1e-15) ? dmax(1e-6, dt0 * 1e-3) : sbr_pow_pos(0.01 / md, 1.0 / 6.0);
+            dt = dmax(dtmin, dmin(dmin(100.0 * dt0, dt1), dtmax));
+        }
+    }
+    const double LOG_QOLDMIN = sbr_log(CTL_QOLDMIN);
+    const double snap = 100.0 * sbr_jl_eps(T1);
+    double t = T0, x = x0, lqold = LOG_QOLDMIN;
+    AutoSwitch as;
+    const ConstDiv by_gamma(CTL_GAMMA);
+    int64_t iter = 0, nacc = 0, nrej = 0;
+    while (t < T1) {
+        if (++iter > maxiters) { status |= SBR_ODE_MAXITERS; break; }
+        dt = dmin(dtmax, dt);
+        dt = dmax(dt, dtmin);
+        dt = dmin(dt, T1 - t);
+        double tmp = fma(dt * A21, k1, x);
+        const double k2 = f(fma(C1, dt, t), tmp);
+        tmp = fma(dt, fma(A31, k1, A32 * k2), x);
+        const double k3 = f(fma(C2, dt, t), tmp);
+        tmp = fma(dt, fma(A41, k1, fma(A42, k2, A43 * k3)), x);
+        const double k4 = f(fma(C3, dt, t), tmp);
+        tmp = fma(dt, fma(A51, k1, fma(A52, k2, fma(A53, k3, A54 * k4))), x);
+        const double k5 = f(fma(C4, dt, t), tmp);
+        const double tmp6 = fma(dt, fma(A61, k1, fma(A62, k2, fma(A63, k3, fma(A64, k4, A65 * k5)))), x);
+        const double k6 = f(t + dt, tmp6);
+        const double u =
+            fma(dt, fma(A71, k1, fma(A72, k2, fma(A73, k3, fma(A74, k4, fma(A75, k5, A76 * k6))))), x);
+        const double k7 = f(t + dt, u);
+        const double eigr = fabs((k7 - k6) / (u - tmp6));
+        const double eig = (eigr != eigr) ? (double)NAN : eigr;
+        const double ut =
+            dt * fma(BT1, k1, fma(BT2, k2, fma(BT3, k3, fma(BT4, k4, fma(BT5, k5, fma(BT6, k6, BT7 * k7))))));
+        const double EEst = fabs(ut / fma(dmax(fabs(x), fabs(u)), rtol, atol));
+        double q, le = 0.0;
+        if (EEst == 0.0) {
+            q = CTL_INV_QMAX;
+        } else {
+            le = sbr_log(EEst);
+            q = sbr_exp(CTL_BETA1 * le - CTL_BETA2 * lqold);
+            q = dmax(CTL_INV_QMAX, dmin(CTL_INV_QMIN, by_gamma(q)));
+        }
+        if (EEst <= 1.0) {
+            nacc++;
+            const double dtnew = dt / q;
+            const double qold = dmax(EEst, CTL_QOLDMIN);
+            lqold = (qold == EEst) ? le : LOG_QOLDMIN;
+            double tn = t + dt;
+            if (fabs(tn - T1) < snap) tn = T1;
+            on_step(t, tn, dt, x, u, k1, k2, k3, k4, k5, k6, k7);
+            t = tn;
+            x = u;
+            k1 = k7;
+            dt = dmax(dmin(dtmax, dtnew), dtmin);
+            f.accepted(t);
+        } else {
+            nrej++;
+            const double q11 = sbr_exp(CTL_BETA1 * le);
+            dt = dt / dmin(CTL_INV_QMIN, by_gamma(q11));
+        }
+        if (!(dt > 0.0) || !isfinite(dt)) { status |= SBR_ODE_FAILED; break; }
+        as.update(eig, dt);
+    }
+    if (as.switched) status |= SBR_STIFF_SWITCH;
+    nsteps = nacc + nrej;
+}
+
+// solve_equilibrium_interest (interest_rate_solver.jl:51-150) for one u with r > 0:
+// V on the HR grid, optimal_buffer on h − rV, then the baseline's compute_ξ / AW.
+template <class P>
+__device__ __forceinline__ void solve_interest_point(P T, P G, P H, const Summ& S, const int n, const int ntau,
+                                                     const int nle, const double ETA, const double T1,
+                                                     const bool trunc, const double u, const double kappa,
+                                                     const int max_iters, const uint32_t lbits,
+                                                     const InterestArgs& ia, PointResult& r, int64_t& nsteps,
+                                                     const int diag)
+{
+    r.xi = NAN; r.aw = NAN; r.tol = INFINITY; r.iters = 0; r.status = 0;
+    nsteps = 0;
+    const TauView<P> tau{T, nle, ETA};
+    ValueRhs<P> f{tau, H, ntau, ia.delta, ia.r, u, ntau > 0 ? tau[0] : 0.0, ntau > 0 ? tau[ntau - 1] : 0.0, 0, false};
+    const double V0 = (u + ia.delta) / (ia.r + ia.delta);
+    SaveScan<P> sv{tau, H, ntau, ia.r, u};
+    sv.init(V0);
+    auto on_step = [&](double tprev, double tn, double dt, double y0, double y1, double k1, double k2, double k3,
+                       double k4, double k5, double k6, double k7) {
+        while (sv.next < ntau && tau[sv.next] <= tn) {
+            const double ts = tau[sv.next];
+            sv.save(ts != tn ? tsit5_dense((ts - tprev) / dt, dt, y0, k1, k2, k3, k4, k5, k6, k7) : y1);
+        }
+    };
+    uint32_t vbits = 0;
+    tsit5_hooked(f, on_step, ntau > 0 ? tau[ntau - 1] : 0.0, V0, ia.rtol, ia.atol, ia.maxiters, vbits, nsteps);
+    if (f.oob) vbits |= SBR_OOB;
+    const uint32_t bits = lbits | (vbits & (SBR_ODE_MAXITERS | SBR_STIFF_SWITCH | SBR_ODE_FAILED));
+    if ((vbits & SBR_OOB) || sv.next < 2) { // HR lookup past the grid / a 1-knot V interpolant: BoundsError
+        r.status = SBR_OOB | bits;
+        r.tin = NAN; r.tout = NAN;
+        return;
+    }
+    sv.finish();
+    const int ns = sv.nh;
+    double tin, tout;
+    if (!sv.any) {
+        tin = T1; tout = T1;
+    } else if (sv.all) {
+        tin = tau[0]; tout = tau[ns - 1];
+    } else {
+        tin = sv.cin >= 0 ? sv.tin_x : T1;
+        tout = sv.cout >= 0 ? sv.tout_x : T1;
+        if (tin == T1) tin = tau[sv.fa];
+        if (tout == T1) tout = tau[sv.la];
+    }
+    r.tin = tin;
+    r.tout = tout;
+    if (diag & 1) { r.status = bits; return; }
+    solve_from_buffers(T, G, H, S, n, ntau, nle, ETA, T1, trunc, u, kappa, max_iters, bits, r, nullptr, diag, tin,
+                       tout);
+}
+
+template <int BLOCK, bool INTEREST>
 __global__ __launch_bounds__(BLOCK) void equilibrium_kernel(LearnBufs L, const double* __restrict__ eta,
                                                             const double* __restrict__ t_end,
-                                                            const double* __restrict__ u, EqArgs a, ResultSoA out)
+                                                            const double* __restrict__ u, EqArgs a, InterestArgs ia,
+                                                            ResultSoA out)
 {
     extern __shared__ double smem[];
     const int b = blockIdx.y;
@@ -680,16 +954,25 @@ __global__ __launch_bounds__(BLOCK) void equilibrium_kernel(LearnBufs L, const d
         if (j >= j1) continue;
         const double uj = u[j];
         PointResult r;
+        int64_t vsteps = 0;
         if (bad_col || !(uj >= 0.0)) {
             r.xi = NAN; r.aw = NAN; r.tol = INFINITY; r.iters = 0;
             r.tin = NAN; r.tout = NAN;
             r.status = ((lst & SBR_ARG_INVALID) || !(uj >= 0.0)) ? SBR_ARG_INVALID : (SBR_OOB | lbits);
+        } else if (INTEREST && ia.r > 0.0) {
+            if (fits)
+                solve_interest_point(sT, sG, sH, S, n, ntau, nle, ETA, T1, trunc, uj, a.kappa, a.max_iters, lbits, ia,
+                                     r, vsteps, a.diag);
+            else
+                solve_interest_point(gT, gG, gH, S, n, ntau, nle, ETA, T1, trunc, uj, a.kappa, a.max_iters, lbits, ia,
+                                     r, vsteps, a.diag);
         } else if (fits) {
             solve_point(sT, sG, sH, S, n, ntau, nle, ETA, T1, trunc, uj, a.kappa, a.max_iters, lbits, r, a.aw_path, a.diag);
         } else {
             solve_point(gT, gG, gH, S, n, ntau, nle, ETA, T1, trunc, uj, a.kappa, a.max_iters, lbits, r, a.aw_path, a.diag);
         }
         const size_t o = (size_t)b * (size_t)a.n_u + j;
+        if (INTEREST && ia.steps) ia.steps[o] = vsteps;
         out.xi[o] = r.xi;
         out.tau_in_unc[o] = r.tin;
         out.tau_out_unc[o] = r.tout;
@@ -723,12 +1006,33 @@ hipError_t launch_equilibrium(const LearnBufs& L, const double* eta, const doubl
     const int tiles = (a.n_u + EQ_TILE - 1) / EQ_TILE;
     const int w = a.n_u < EQ_TILE ? a.n_u : EQ_TILE;
     dim3 grid(tiles, n_beta);
+    const InterestArgs none{0.0, 1.0, 0.0, 0.0, 0, nullptr};
     if (w > 256)
-        hipLaunchKernelGGL(equilibrium_kernel<1024>, grid, dim3(1024), lds, s, L, eta, t_end, u, a, out);
+        hipLaunchKernelGGL((equilibrium_kernel<1024, false>), grid, dim3(1024), lds, s, L, eta, t_end, u, a, none, out);
     else if (w > 64)
-        hipLaunchKernelGGL(equilibrium_kernel<256>, grid, dim3(256), lds, s, L, eta, t_end, u, a, out);
+        hipLaunchKernelGGL((equilibrium_kernel<256, false>), grid, dim3(256), lds, s, L, eta, t_end, u, a, none, out);
     else
-        hipLaunchKernelGGL(equilibrium_kernel<64>, grid, dim3(64), lds, s, L, eta, t_end, u, a, out);
+        hipLaunchKernelGGL((equilibrium_kernel<64, false>), grid, dim3(64), lds, s, L, eta, t_end, u, a, none, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_interest(const LearnBufs& L, const double* eta, const double* t_end, const double* u,
+                           const EqArgs& a, const InterestArgs& ia, const ResultSoA& out, int n_beta, hipStream_t s)
+{
+    const size_t lds = ((size_t)3 * a.lds_cap + 2 * ((a.lds_cap >> 6) + 1) + 2 * ((a.lds_cap >> 3) + 1)) * sizeof(double);
+    // every lane integrates its own value function (~5·10⁴ Tsit5 steps): one wave per 64 u
+    // of the column so that all of them run at once (the LDS slab allows one block per CU)
+    const int tiles = (a.n_u + EQ_TILE - 1) / EQ_TILE;
+    const int w = a.n_u < EQ_TILE ? a.n_u : EQ_TILE;
+    dim3 grid(tiles, n_beta);
+    if (w > 512)
+        hipLaunchKernelGGL((equilibrium_kernel<1024, true>), grid, dim3(1024), lds, s, L, eta, t_end, u, a, ia, out);
+    else if (w > 256)
+        hipLaunchKernelGGL((equilibrium_kernel<512, true>), grid, dim3(512), lds, s, L, eta, t_end, u, a, ia, out);
+    else if (w > 64)
+        hipLaunchKernelGGL((equilibrium_kernel<256, true>), grid, dim3(256), lds, s, L, eta, t_end, u, a, ia, out);
+    else
+        hipLaunchKernelGGL((equilibrium_kernel<64, true>), grid, dim3(64), lds, s, L, eta, t_end, u, a, ia, out);
     return hipGetLastError();
 }
 

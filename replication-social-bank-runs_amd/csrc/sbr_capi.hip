@@ -308,6 +308,30 @@ int run_baseline(sbr_ctx* c, hipStream_t s, const double* beta, const double* et
     return launch_eq(c, s, c->LW[0], eta, t_end, u, n_beta, n_u, kappa, o, out, aw_path);
 }
 
+int run_interest(sbr_ctx* c, hipStream_t s, const double* beta, const double* eta, const double* t_end, double x0,
+                 const double* u, int64_t n_beta, int64_t n_u, double p, double kappa, double lambda, double r,
+                 double delta, const sbr_opts& o, const sbr::ResultSoA& out, int64_t* steps)
+{
+    int rc = ensure_learn(c, (size_t)n_beta, (size_t)o.knot_capacity);
+    if (rc) return rc;
+    c->last_slot = 0;
+    sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, p, lambda, o.ode_maxiters, (int32_t)n_beta, 1, 0};
+    hipEvent_t t0 = tstart(c, s);
+    HIP_TRY(c, sbr::launch_learn_logistic(beta, eta, t_end, la, c->LW[0], s), SBR_EDEVICE);
+    tend(c, s, 0, t0);
+    sbr::EqArgs ea{kappa, (int32_t)n_u, o.bisect_max_iters, c->lds_cap, nullptr,
+                   (o.flags & SBR_FLAG_EXHAUSTIVE) ? 1 : 0, (o.flags >> 8) & 7};
+    sbr::InterestArgs ia{r, delta, o.ode_reltol, o.ode_abstol, o.ode_maxiters, steps};
+    t0 = tstart(c, s);
+    HIP_TRY(c, sbr::launch_interest(c->LW[0], eta, t_end, u, ea, ia, out, (int)n_beta, s), SBR_EDEVICE);
+    tend(c, s, 1, t0);
+    return SBR_OK;
+}
+
+// EconomicParametersInterest / solve_value_function checks (interest_rate_model.jl:40-50,
+// value_function_solver.jl:67-69)
+bool interest_valid(double r, double delta) { return r >= 0.0 && delta > 0.0 && r < delta; }
+
 }  // namespace
 
 extern "C" {
@@ -495,6 +519,69 @@ int sbr_sweep_baseline(sbr_ctx* c, const double* beta, const double* eta, const 
     HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
     if (o.early_exit_nan_run > 0 && out->status && out->xi && out->aw_max && out->tol)
         sbr_apply_early_exit(n_beta, n_u, o.early_exit_nan_run, out);
+    return SBR_OK;
+}
+
+int sbr_sweep_interest_dev(sbr_ctx* c, void* stream, const double* beta, const double* eta, const double* t_end,
+                           double x0, const double* u, int64_t n_beta, int64_t n_u, double p, double kappa,
+                           double lambda, double r, double delta, const sbr_opts* opts, sbr_result_soa* out,
+                           int64_t* rk_steps)
+{
+    if (!c || !out || !out->xi || !out->tau_in_unc || !out->tau_out_unc || !out->aw_max || !out->tol || !out->status)
+        return SBR_EARG;
+    if (n_beta <= 0 || n_u <= 0 || n_beta > (1 << 30) || n_u > (1 << 30)) return fail(c, SBR_EARG, "grid size");
+    if (!scalars_valid(x0, p, kappa, lambda)) return fail(c, SBR_EARG, "ArgumentError: x0/p/kappa/lambda");
+    if (!interest_valid(r, delta)) return fail(c, SBR_EARG, "ArgumentError: need 0 <= r < delta");
+    if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
+    sbr_opts o = resolve(opts);
+    sbr::ResultSoA rs{out->xi, out->tau_in_unc, out->tau_out_unc, out->aw_max, out->tol, out->status, out->iters};
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    return run_interest(c, s, beta, eta, t_end, x0, u, n_beta, n_u, p, kappa, lambda, r, delta, o, rs, rk_steps);
+}
+
+int sbr_sweep_interest(sbr_ctx* c, const double* beta, const double* eta, const double* t_end, double x0,
+                       const double* u, int64_t n_beta, int64_t n_u, double p, double kappa, double lambda, double r,
+                       double delta, const sbr_opts* opts, sbr_result_soa* out, int64_t* rk_steps)
+{
+    if (!c || !out || !beta || !eta || !t_end || !u) return SBR_EARG;
+    if (n_beta <= 0 || n_u <= 0) return fail(c, SBR_EARG, "grid size");
+    if (!scalars_valid(x0, p, kappa, lambda)) return fail(c, SBR_EARG, "ArgumentError: x0/p/kappa/lambda");
+    if (!interest_valid(r, delta)) return fail(c, SBR_EARG, "ArgumentError: need 0 <= r < delta");
+    for (int64_t i = 0; i < n_beta; i++)
+        if (!(beta[i] > 0.0) || !(t_end[i] > 0.0) || !(eta[i] > 0.0))
+            return fail(c, SBR_EARG, "ArgumentError: beta/eta/t_end must be positive");
+    for (int64_t j = 0; j < n_u; j++)
+        if (!(u[j] >= 0.0)) return fail(c, SBR_EARG, "ArgumentError: u must be non-negative");
+    if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
+    sbr_opts o = resolve(opts);
+    const size_t np = (size_t)n_beta * (size_t)n_u;
+    const size_t in_bytes = (3 * (size_t)n_beta + (size_t)n_u) * 8;
+    const size_t out_bytes = np * (5 * 8 + 4 + 4 + 8);
+    int rc = ensure_stage(c, in_bytes + out_bytes + 256);
+    if (rc) return rc;
+    char* base = (char*)c->stage;
+    double* dbeta = (double*)base;
+    double* deta = dbeta + n_beta;
+    double* dtend = deta + n_beta;
+    double* du = dtend + n_beta;
+    double* dres = (double*)(base + ((in_bytes + 255) & ~(size_t)255));
+    int64_t* dsteps = (int64_t*)(dres + 5 * np);
+    sbr::ResultSoA rs{dres, dres + np, dres + 2 * np, dres + 3 * np, dres + 4 * np, (uint32_t*)(dsteps + np),
+                      (int32_t*)((uint32_t*)(dsteps + np) + np)};
+    hipStream_t s = c->stream;
+    HIP_TRY(c, hipMemcpyAsync(dbeta, beta, n_beta * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+    HIP_TRY(c, hipMemcpyAsync(deta, eta, n_beta * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+    HIP_TRY(c, hipMemcpyAsync(dtend, t_end, n_beta * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+    HIP_TRY(c, hipMemcpyAsync(du, u, n_u * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+    rc = run_interest(c, s, dbeta, deta, dtend, x0, du, n_beta, n_u, p, kappa, lambda, r, delta, o, rs, dsteps);
+    if (rc) return rc;
+    double* hs[5] = {out->xi, out->tau_in_unc, out->tau_out_unc, out->aw_max, out->tol};
+    for (int k = 0; k < 5; k++)
+        if (hs[k]) HIP_TRY(c, hipMemcpyAsync(hs[k], dres + k * np, np * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+    if (out->status) HIP_TRY(c, hipMemcpyAsync(out->status, rs.status, np * 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+    if (out->iters) HIP_TRY(c, hipMemcpyAsync(out->iters, rs.iters, np * 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+    if (rk_steps) HIP_TRY(c, hipMemcpyAsync(rk_steps, dsteps, np * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+    HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
     return SBR_OK;
 }
 

@@ -39,6 +39,14 @@ struct EqArgs {
     int32_t diag;       // SBR_FLAG_DIAG_* bits >> 8 (timing breakdown only)
 };
 
+// Interest-rate extension (sbr_baseline.hip interest mode): value function on the HR grid.
+struct InterestArgs {
+    double r, delta;     // interest rate, deposit maturity rate (0 ≤ r < δ); r = 0: the baseline
+    double rtol, atol;   // value-function Tsit5 tolerances (value_function_solver.jl:66: eps())
+    int64_t maxiters;
+    int64_t* steps;      // value-function RK steps per point (may be null)
+};
+
 struct ResultSoA {
     double *xi, *tau_in_unc, *tau_out_unc, *aw_max, *tol;
     uint32_t* status;
@@ -145,5 +153,8 @@ hipError_t launch_learn_logistic(const double* beta, const double* eta, const do
                                  const LearnBufs& L, hipStream_t s);
 hipError_t launch_equilibrium(const LearnBufs& L, const double* eta, const double* t_end, const double* u,
                               const EqArgs& a, const ResultSoA& out, int n_beta, hipStream_t s);
+// solve_equilibrium_interest per (β, u) on the same learning buffers
+hipError_t launch_interest(const LearnBufs& L, const double* eta, const double* t_end, const double* u,
+                           const EqArgs& a, const InterestArgs& ia, const ResultSoA& out, int n_beta, hipStream_t s);
 
 }  // namespace sbr

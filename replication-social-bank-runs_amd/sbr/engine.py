@@ -234,6 +234,42 @@ class Engine:
                                           rk.data_ptr() if rk is not None else None)
         check(rc, self._ctx, "sbr_sweep_social_dev")
 
+    def sweep_interest(self, beta, eta, t_end, u, p, kappa, lam, r, delta, x0=1e-4, max_iters: int = 100,
+                       knot_capacity: int = 65536) -> dict:
+        """Interest-rate extension over β columns × u (interest_rate_solver.jl:51-150 +
+        get_AW_functions_interest!): the value function on the HR grid and buffers from
+        h − rV (r > 0), the baseline for r = 0.  Returns [n_beta, n_u] arrays incl.
+        rk_steps (value-function Tsit5 steps per point)."""
+        beta = np.ascontiguousarray(np.atleast_1d(beta), np.float64)
+        nb = len(beta)
+        eta = np.ascontiguousarray(np.broadcast_to(eta, (nb,)), np.float64)
+        t_end = np.ascontiguousarray(np.broadcast_to(t_end, (nb,)), np.float64)
+        u = np.ascontiguousarray(np.atleast_1d(u), np.float64)
+        nu = len(u)
+        out = {k: np.empty(nb * nu) for k in RESULT_FIELDS}
+        out["status"] = np.empty(nb * nu, np.uint32)
+        out["iters"] = np.empty(nb * nu, np.int32)
+        out["rk_steps"] = np.empty(nb * nu, np.int64)
+        soa = _lib.ResultSoA(*[_ptr(out[k]) for k in (*RESULT_FIELDS, "status", "iters")])
+        opts = _lib.default_opts(early_exit_nan_run=0, bisect_max_iters=max_iters, knot_capacity=knot_capacity)
+        rc = self._L.sbr_sweep_interest(self._ctx, _ptr(beta), _ptr(eta), _ptr(t_end), x0, _ptr(u), nb, nu, p, kappa,
+                                        lam, r, delta, ctypes.byref(opts), ctypes.byref(soa), _ptr(out["rk_steps"]))
+        check(rc, self._ctx, "sbr_sweep_interest")
+        return {k: v.reshape(nb, nu) for k, v in out.items()}
+
+    def sweep_interest_dev(self, beta, eta, t_end, u, p, kappa, lam, r, delta, x0, out: dict,
+                           stream: int | None = None, max_iters: int = 100, knot_capacity: int = 65536):
+        """Device-pointer interest sweep on torch tensors (enqueue only)."""
+        nb, nu = beta.numel(), u.numel()
+        soa = _lib.ResultSoA(*[(out[k].data_ptr() if out.get(k) is not None else None)
+                               for k in (*RESULT_FIELDS, "status", "iters")])
+        opts = _lib.default_opts(early_exit_nan_run=0, bisect_max_iters=max_iters, knot_capacity=knot_capacity)
+        rk = out.get("rk_steps")
+        rc = self._L.sbr_sweep_interest_dev(self._ctx, stream, beta.data_ptr(), eta.data_ptr(), t_end.data_ptr(), x0,
+                                            u.data_ptr(), nb, nu, p, kappa, lam, r, delta, ctypes.byref(opts),
+                                            ctypes.byref(soa), rk.data_ptr() if rk is not None else None)
+        check(rc, self._ctx, "sbr_sweep_interest_dev")
+
     def social_prof_read(self) -> list[int]:
         v = (ctypes.c_int64 * 8)()
         check(self._L.sbr_social_prof_read(self._ctx, v), self._ctx, "sbr_social_prof_read")

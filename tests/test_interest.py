@@ -72,3 +72,44 @@ def test_interest_reentry_raises_xi_threshold(oracle):
                                  P["delta"])
     assert r["tau_in_unc"] > base["tau_in_unc"]
     assert len(r["V"]) == len(r["hr_tau"])
+
+
+def _grid():
+    beta = 1.0 / sbr.julia_range("0.0001", "1", 500)[::50]  # Fig 5 columns (η = 15, tspan (0, 30) carried)
+    u = sbr.julia_range("0.001", "1", 500)[::20]
+    return beta, u
+
+
+@pytest.mark.gpu
+def test_interest_gpu_bitwise(engine, oracle):
+    """GPU interest sweep == the oracle bit for bit (every field, status, bisection count,
+    value-function RK step count) on Fig-5 columns at r = 0.06, δ = 0.1, on the script
+    point, and the r = 0 branch == the baseline sweep."""
+    beta, u = _grid()
+    for r, delta, bb, uu in ((0.06, 0.1, beta, u), (0.06, 0.1, [1.0], [0.0, 0.05, 0.1]), (0.02, 0.5, beta[:4], u),
+                             (0.0, 0.1, beta, u)):
+        g = engine.sweep_interest(bb, 15.0, 30.0, uu, 0.5, 0.6, 0.01, r, delta)
+        o = oracle.sweep_interest(bb, 15.0, 30.0, uu, 0.5, 0.6, 0.01, r, delta)
+        for k in ("xi", "tau_in_unc", "tau_out_unc", "aw_max", "tol", "status", "iters", "rk_steps"):
+            a, b = g[k], o[k]
+            same = (a == b) | (np.isnan(a) & np.isnan(b)) if a.dtype.kind == "f" else (a == b)
+            assert same.all(), (r, delta, k, int((~same).sum()))
+    g = engine.sweep_interest([1.0], 15.0, 30.0, [0.0], 0.5, 0.6, 0.01, 0.06, 0.1)
+    assert g["status"][0, 0] & sbr.STATUS["SBR_RUN"]
+
+
+def test_interest_capi_argument_errors():
+    """The C ABI rejects a null context / result block before any device work (the
+    0 <= r < δ check of interest_rate_model.jl:48-50 follows on a live context)."""
+    L = sbr.load()
+    rc = L.sbr_sweep_interest(None, None, None, None, 1e-4, None, 1, 1, 0.5, 0.6, 0.01, 0.06, 0.1, None, None, None)
+    assert rc == sbr._lib.SBR_EARG
+    rc = L.sbr_sweep_interest_dev(None, None, None, None, None, 1e-4, None, 1, 1, 0.5, 0.6, 0.01, 0.2, 0.1, None,
+                                  None, None)
+    assert rc == sbr._lib.SBR_EARG
+
+
+@pytest.mark.gpu
+def test_interest_gpu_rejects_r_not_below_delta(engine):
+    with pytest.raises(sbr.ArgumentError):
+        engine.sweep_interest([1.0], 15.0, 30.0, [0.1], 0.5, 0.6, 0.01, 0.1, 0.1)
