@@ -180,4 +180,35 @@ function solve_equilibrium_social_learning_grid(ctx::Context, Î²_vals, u_vals; Î
             fp_iters = fp, rk_steps = steps)
 end
 
+"""
+    solve_equilibrium_interest_grid(ctx, Î²_vals, u_vals; r, Î´, Î· = 15.0, tspan_end = 30.0, x0 = 1e-4,
+                                    p = 0.5, Îº = 0.6, Î» = 0.01)
+
+`solve_learning` + `solve_equilibrium_interest` (interest_rate_solver.jl:51-150) +
+`get_AW_functions_interest!(â€¦).AW_max` for every (Î²_i, u_j), Î· and tspan carried as in
+the Fig 5 copy-modify loop.  Matrices are n_u Ã— n_Î²; `rk_steps` counts the value
+function's Tsit5 steps per point.
+"""
+function solve_equilibrium_interest_grid(ctx::Context, Î²_vals, u_vals; r, Î´, Î· = 15.0, tspan_end = 30.0,
+                                         x0 = 1e-4, p = 0.5, Îº = 0.6, Î» = 0.01)
+    Î² = collect(Float64, Î²_vals); u = collect(Float64, u_vals)
+    nb, nu = length(Î²), length(u)
+    Î·v = fill(Float64(Î·), nb); tv = fill(Float64(tspan_end), nb)
+    xi = Matrix{Float64}(undef, nu, nb); tin = similar(xi); tout = similar(xi)
+    aw = similar(xi); tl = similar(xi); st = Matrix{UInt32}(undef, nu, nb)
+    steps = Matrix{Int64}(undef, nu, nb)
+    opts = Ref(Opts(; early_exit = 0))
+    GC.@preserve Î² u Î·v tv xi tin tout aw tl st steps begin
+        soa = Ref(ResultSoA(pointer(xi), pointer(tin), pointer(tout), pointer(aw), pointer(tl), pointer(st),
+                            Ptr{Int32}(C_NULL)))
+        rc = ccall((:sbr_sweep_interest, libsbr), Cint,
+                   (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Float64, Ptr{Float64}, Int64, Int64,
+                    Float64, Float64, Float64, Float64, Float64, Ref{Opts}, Ref{ResultSoA}, Ptr{Int64}),
+                   ctx.ptr, Î², Î·v, tv, x0, u, nb, nu, p, Îº, Î», r, Î´, opts, soa, steps)
+        check(ctx, rc)
+    end
+    return (AW_max = aw, Î¾ = xi, Ï„_bar_IN_UNC = tin, Ï„_bar_OUT_UNC = tout, tolerance = tl, status = st,
+            rk_steps = steps)
+end
+
 end # module

@@ -134,3 +134,25 @@ def sweep_social_sharded(beta, eta, u, p, kappa, lam, cmp=None, x0=1e-4, tol=1e-
     if world == 1:
         return local
     return gather_columns(local, len(beta), len(u), world, rank, _device(device), root)
+
+
+def sweep_interest_sharded(beta, eta, t_end, u, p, kappa, lam, r, delta, x0=1e-4,
+                           compute: Callable[..., dict] | None = None, device=None, root: int = 0):
+    """Interest-rate sweep (interest_rate_solver.jl:51-150) sharded over β columns:
+    every point's value function and equilibrium are independent, so the only
+    exchange is the result gather.  compute(beta, eta, t_end, u) solves one shard."""
+    world, rank = _world_rank()
+    beta = np.ascontiguousarray(np.atleast_1d(beta), np.float64)
+    eta = np.ascontiguousarray(np.broadcast_to(eta, beta.shape), np.float64)
+    t_end = np.ascontiguousarray(np.broadcast_to(t_end, beta.shape), np.float64)
+    u = np.ascontiguousarray(np.atleast_1d(u), np.float64)
+    if compute is None:
+        from .engine import default_engine
+
+        eng = default_engine()
+        compute = lambda b, e, t, uu: eng.sweep_interest(b, e, t, uu, p, kappa, lam, r, delta, x0=x0)  # noqa: E731
+    cols = shard_columns(len(beta), world, rank)
+    local = compute(beta[cols], eta[cols], t_end[cols], u)
+    if world == 1:
+        return local
+    return gather_columns(local, len(beta), len(u), world, rank, _device(device), root)

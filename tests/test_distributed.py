@@ -75,10 +75,19 @@ def _worker_ext(rank, world, port, out_path):
     hg = sbr.hetero_config4(5, 7, K=2)
     het = D.sweep_hetero_sharded(hg, device="cpu", compute=lambda g: O.sweep_hetero(
         g.betas, g.dist, g.eta, g.t_end, g.u, g.p, g.kappa, g.lam, g.x0))
+    ib, iu = _interest_axes()
+    itr = D.sweep_interest_sharded(ib, 15.0, 30.0, iu, 0.5, 0.6, 0.01, 0.06, 0.1, device="cpu",
+                                   compute=lambda b, e, t, uu: O.sweep_interest(b, e, t, uu, 0.5, 0.6, 0.01, 0.06,
+                                                                                0.1))
     if rank == 0:
-        np.savez(out_path, **{"s_" + k: v for k, v in soc.items()}, **{"h_" + k: v for k, v in het.items()})
+        np.savez(out_path, **{"s_" + k: v for k, v in soc.items()}, **{"h_" + k: v for k, v in het.items()},
+                 **{"i_" + k: v for k, v in itr.items()})
     dist.barrier()
     dist.destroy_process_group()
+
+
+def _interest_axes():
+    return 1.0 / sbr.julia_range("0.0001", "1", 500)[[0, 60, 250, 499, 120]], sbr.julia_range("0.001", "1", 500)[::60]
 
 
 def _social_axes():
@@ -87,7 +96,7 @@ def _social_axes():
     return beta, u, 30.0 / 0.9
 
 
-def test_sharded_social_and_hetero_equal_single_process(tmp_path, oracle):
+def test_sharded_social_hetero_interest_equal_single_process(tmp_path, oracle):
     out = str(tmp_path / "res.npz")
     mp.spawn(_worker_ext, args=(2, _free_port(), out), nprocs=2, join=True)
     got = np.load(out)
@@ -95,6 +104,11 @@ def test_sharded_social_and_hetero_equal_single_process(tmp_path, oracle):
     ref = oracle.sweep_social(beta, eta, u, 0.99, 0.25, 0.25, sbr.julia_range(0.0, eta, 1000), max_iter=3)
     for f in ("xi", "tau_in_unc", "tau_out_unc", "aw_max", "tol", "status", "iters", "fp_iters"):
         a, b = got["s_" + f], ref[f]
+        assert a.shape == b.shape and np.array_equal(a, b, equal_nan=a.dtype.kind == "f"), f
+    ib, iu = _interest_axes()
+    iref = oracle.sweep_interest(ib, 15.0, 30.0, iu, 0.5, 0.6, 0.01, 0.06, 0.1)
+    for f in ("xi", "tau_in_unc", "tau_out_unc", "aw_max", "tol", "status", "iters"):
+        a, b = got["i_" + f], iref[f]
         assert a.shape == b.shape and np.array_equal(a, b, equal_nan=a.dtype.kind == "f"), f
     hg = sbr.hetero_config4(5, 7, K=2)
     href = oracle.sweep_hetero(hg.betas, hg.dist, hg.eta, hg.t_end, hg.u, hg.p, hg.kappa, hg.lam, hg.x0)
