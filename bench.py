@@ -53,7 +53,7 @@ F_HAZARD_KNOT = 3 + F_EXP + 1 + 4 + 2 + 3  # g, exp, e, trapezoid, numerator, HR
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--n", type=int, default=2048, help="β columns per GPU and u rows")
     ap.add_argument("--no-gather", action="store_true")
