@@ -235,6 +235,16 @@ int sbr_sweep_interest_dev(sbr_ctx* ctx, void* stream, const double* beta, const
                            double lambda, double r, double delta, const sbr_opts* opts, sbr_result_soa* out,
                            int64_t* rk_steps);
 
+/* One interest-rate equilibrium with the paths scripts/3_interest_rates.jl
+ * plots (value_function.pdf, hazard_decomposition.pdf): τ̄ grid and HR (n_tau),
+ * V on that grid (n_v; 0 when r = 0, fewer than n_tau if the value-function
+ * solve stopped early) and AW_cum on the grid (NaN without a run).
+ * res = {ξ, τ̄_IN, τ̄_OUT, AW_max, tol}; arrays hold `cap` doubles. */
+int sbr_interest_point_paths(sbr_ctx* ctx, double beta, double eta, double t_end, double x0, double u, double p,
+                             double kappa, double lambda, double r, double delta, const sbr_opts* opts, double* res,
+                             uint32_t* status, double* tau, double* hr, double* V, double* aw_cum, int64_t cap,
+                             int64_t* n_tau, int64_t* n_v);
+
 /* 5-consecutive-no-run early exit (1_baseline.jl:236-244) as a post-pass on
  * host arrays: points after `threshold` consecutive non-runs in a β column get
  * SBR_SKIPPED_EARLY_EXIT, xi = aw_max = NaN, tol = Inf. */

@@ -272,15 +272,15 @@ def interest_point(beta, eta, t_end, u, p, kappa, lam, r, delta, x0=1e-4, cap=1 
     V(τ̄) saved on that grid (value_function_solver.jl:66-112, saveat = HR knots)."""
     L = lib()
     L.sbro_interest_point.restype = _I64
-    L.sbro_interest_point.argtypes = [_D, _D, _D, _D, _D, _D, _D, _D, _D, _D, _P, _P, _P, _P, _P, _I64, _P]
+    L.sbro_interest_point.argtypes = [_D, _D, _D, _D, _D, _D, _D, _D, _D, _D, _P, _P, _P, _P, _P, _P, _I64, _P]
     res = np.zeros(5)
     st = np.zeros(1, np.uint32)
-    tau, hr, V = np.empty(cap), np.empty(cap), np.empty(cap)
+    tau, hr, V, aw = np.empty(cap), np.empty(cap), np.empty(cap), np.empty(cap)
     nv = np.zeros(1, np.int64)
     n = L.sbro_interest_point(beta, eta, t_end, x0, u, p, kappa, lam, r, delta, _ptr(res), _ptr(st), _ptr(tau),
-                              _ptr(hr), _ptr(V), cap, _ptr(nv))
+                              _ptr(hr), _ptr(V), _ptr(aw), cap, _ptr(nv))
     if n < 0:
         raise RuntimeError(f"oracle interest path buffer too small ({-n} needed)")
     k = int(nv[0])
     return dict(xi=res[0], tau_in_unc=res[1], tau_out_unc=res[2], aw_max=res[3], tol=res[4], status=int(st[0]),
-                hr_tau=tau[:n].copy(), hr=hr[:n].copy(), V=V[:k].copy())
+                hr_tau=tau[:n].copy(), hr=hr[:n].copy(), V=V[:k].copy(), aw_cum=aw[:n].copy())

@@ -1265,7 +1265,7 @@ int sbro_sweep_interest(const double* beta, const double* eta, const double* t_e
  * hr_tau / hr_v / V (n_hr each, caller-sized ≥ the learning knot count + 1) */
 int64_t sbro_interest_point(double beta, double eta, double t_end, double x0, double u, double p, double kappa,
                             double lambda, double r, double delta, double* res, uint32_t* status, double* hr_tau,
-                            double* hr_v, double* V, int64_t cap, int64_t* n_v)
+                            double* hr_v, double* V, double* aw, int64_t cap, int64_t* n_v)
 {
     const double eps = 2.220446049250313e-16;
     knots_t kn = {0};
@@ -1278,7 +1278,9 @@ int64_t sbro_interest_point(double beta, double eta, double t_end, double x0, do
     int64_t nh = h.n;
     if (nh > cap) { hazard_free(&h); free(g); knots_free(&kn); return -nh; }
     point_t pr;
-    interest_point(kn.t, kn.x, kn.n, &h, t_end, u, kappa, r, delta, 100, &pr, V, n_v, NULL, NULL);
+    interest_point(kn.t, kn.x, kn.n, &h, t_end, u, kappa, r, delta, 100, &pr, V, n_v, NULL, aw);
+    if (aw && !(pr.status & SBR_RUN))
+        for (int64_t i = 0; i < nh; i++) aw[i] = NAN;
     res[0] = pr.xi; res[1] = pr.tin; res[2] = pr.tout; res[3] = pr.aw_max; res[4] = pr.tol;
     *status = pr.status | (st.status & (SBR_ODE_MAXITERS | SBR_STIFF_SWITCH | SBR_ODE_FAILED));
     memcpy(hr_tau, h.tau, (size_t)nh * sizeof(double));

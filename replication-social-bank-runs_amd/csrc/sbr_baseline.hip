@@ -643,6 +643,7 @@ struct SaveScan {
     P H;
     int ntau;
     double r, u;
+    double* vpath;   // single-point mode: every saved V (may be null)
     int next;        // grid index of the next saved value
     double vprev;    // V at knot next − 1 (its h − rV waits for V_next)
     double vprev2;   // V at knot next − 2
@@ -654,6 +655,7 @@ struct SaveScan {
     __device__ __forceinline__ void init(double V0)
     {
         next = 1; vprev = V0; vprev2 = 0.0; nh = 0; hprev = 0.0;
+        if (vpath) vpath[0] = V0;
         any = false; all = true; fa = la = cin = cout = -1; tin_x = tout_x = 0.0;
     }
     __device__ __forceinline__ void scan(double hv)
@@ -676,6 +678,7 @@ struct SaveScan {
     __device__ __forceinline__ void save(double v)
     {
         const int i = next - 1;
+        if (vpath) vpath[next] = v;
         const double ti = tau[i], t1 = tau[i + 1];
         const double d = (ti - ti) / (t1 - ti);
         const double Vi = vprev * (1.0 - d) + v * d;
@@ -795,14 +798,14 @@ __device__ __forceinline__ void solve_interest_point(P T, P G, P H, const Summ& 
                                                      const bool trunc, const double u, const double kappa,
                                                      const int max_iters, const uint32_t lbits,
                                                      const InterestArgs& ia, PointResult& r, int64_t& nsteps,
-                                                     const int diag)
+                                                     double* __restrict__ aw_path, const int diag)
 {
     r.xi = NAN; r.aw = NAN; r.tol = INFINITY; r.iters = 0; r.status = 0;
     nsteps = 0;
     const TauView<P> tau{T, nle, ETA};
     ValueRhs<P> f{tau, H, ntau, ia.delta, ia.r, u, ntau > 0 ? tau[0] : 0.0, ntau > 0 ? tau[ntau - 1] : 0.0, 0, false};
     const double V0 = (u + ia.delta) / (ia.r + ia.delta);
-    SaveScan<P> sv{tau, H, ntau, ia.r, u};
+    SaveScan<P> sv{tau, H, ntau, ia.r, u, ia.v_path};
     sv.init(V0);
     auto on_step = [&](double tprev, double tn, double dt, double y0, double y1, double k1, double k2, double k3,
                        double k4, double k5, double k6, double k7) {
@@ -813,6 +816,7 @@ __device__ __forceinline__ void solve_interest_point(P T, P G, P H, const Summ& 
     };
     uint32_t vbits = 0;
     tsit5_hooked(f, on_step, ntau > 0 ? tau[ntau - 1] : 0.0, V0, ia.rtol, ia.atol, ia.maxiters, vbits, nsteps);
+    if (ia.v_count) *ia.v_count = sv.next;
     if (f.oob) vbits |= SBR_OOB;
     const uint32_t bits = lbits | (vbits & (SBR_ODE_MAXITERS | SBR_STIFF_SWITCH | SBR_ODE_FAILED));
     if ((vbits & SBR_OOB) || sv.next < 2) { // HR lookup past the grid / a 1-knot V interpolant: BoundsError
@@ -836,7 +840,7 @@ __device__ __forceinline__ void solve_interest_point(P T, P G, P H, const Summ& 
     r.tin = tin;
     r.tout = tout;
     if (diag & 1) { r.status = bits; return; }
-    solve_from_buffers(T, G, H, S, n, ntau, nle, ETA, T1, trunc, u, kappa, max_iters, bits, r, nullptr, diag, tin,
+    solve_from_buffers(T, G, H, S, n, ntau, nle, ETA, T1, trunc, u, kappa, max_iters, bits, r, aw_path, diag, tin,
                        tout);
 }
 
@@ -962,10 +966,10 @@ __global__ __launch_bounds__(BLOCK) void equilibrium_kernel(LearnBufs L, const d
         } else if (INTEREST && ia.r > 0.0) {
             if (fits)
                 solve_interest_point(sT, sG, sH, S, n, ntau, nle, ETA, T1, trunc, uj, a.kappa, a.max_iters, lbits, ia,
-                                     r, vsteps, a.diag);
+                                     r, vsteps, a.aw_path, a.diag);
             else
                 solve_interest_point(gT, gG, gH, S, n, ntau, nle, ETA, T1, trunc, uj, a.kappa, a.max_iters, lbits, ia,
-                                     r, vsteps, a.diag);
+                                     r, vsteps, a.aw_path, a.diag);
         } else if (fits) {
             solve_point(sT, sG, sH, S, n, ntau, nle, ETA, T1, trunc, uj, a.kappa, a.max_iters, lbits, r, a.aw_path, a.diag);
         } else {
@@ -1006,7 +1010,7 @@ hipError_t launch_equilibrium(const LearnBufs& L, const double* eta, const doubl
     const int tiles = (a.n_u + EQ_TILE - 1) / EQ_TILE;
     const int w = a.n_u < EQ_TILE ? a.n_u : EQ_TILE;
     dim3 grid(tiles, n_beta);
-    const InterestArgs none{0.0, 1.0, 0.0, 0.0, 0, nullptr};
+    const InterestArgs none{0.0, 1.0, 0.0, 0.0, 0, nullptr, nullptr, nullptr};
     if (w > 256)
         hipLaunchKernelGGL((equilibrium_kernel<1024, false>), grid, dim3(1024), lds, s, L, eta, t_end, u, a, none, out);
     else if (w > 64)

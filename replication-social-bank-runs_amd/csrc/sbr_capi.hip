@@ -310,7 +310,8 @@ int run_baseline(sbr_ctx* c, hipStream_t s, const double* beta, const double* et
 
 int run_interest(sbr_ctx* c, hipStream_t s, const double* beta, const double* eta, const double* t_end, double x0,
                  const double* u, int64_t n_beta, int64_t n_u, double p, double kappa, double lambda, double r,
-                 double delta, const sbr_opts& o, const sbr::ResultSoA& out, int64_t* steps)
+                 double delta, const sbr_opts& o, const sbr::ResultSoA& out, int64_t* steps, double* aw_path = nullptr,
+                 double* v_path = nullptr, int32_t* v_count = nullptr)
 {
     int rc = ensure_learn(c, (size_t)n_beta, (size_t)o.knot_capacity);
     if (rc) return rc;
@@ -319,9 +320,9 @@ int run_interest(sbr_ctx* c, hipStream_t s, const double* beta, const double* et
     hipEvent_t t0 = tstart(c, s);
     HIP_TRY(c, sbr::launch_learn_logistic(beta, eta, t_end, la, c->LW[0], s), SBR_EDEVICE);
     tend(c, s, 0, t0);
-    sbr::EqArgs ea{kappa, (int32_t)n_u, o.bisect_max_iters, c->lds_cap, nullptr,
+    sbr::EqArgs ea{kappa, (int32_t)n_u, o.bisect_max_iters, c->lds_cap, aw_path,
                    (o.flags & SBR_FLAG_EXHAUSTIVE) ? 1 : 0, (o.flags >> 8) & 7};
-    sbr::InterestArgs ia{r, delta, o.ode_reltol, o.ode_abstol, o.ode_maxiters, steps};
+    sbr::InterestArgs ia{r, delta, o.ode_reltol, o.ode_abstol, o.ode_maxiters, steps, v_path, v_count};
     t0 = tstart(c, s);
     HIP_TRY(c, sbr::launch_interest(c->LW[0], eta, t_end, u, ea, ia, out, (int)n_beta, s), SBR_EDEVICE);
     tend(c, s, 1, t0);
@@ -582,6 +583,58 @@ int sbr_sweep_interest(sbr_ctx* c, const double* beta, const double* eta, const 
     if (out->iters) HIP_TRY(c, hipMemcpyAsync(out->iters, rs.iters, np * 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
     if (rk_steps) HIP_TRY(c, hipMemcpyAsync(rk_steps, dsteps, np * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
     HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
+    return SBR_OK;
+}
+
+int sbr_interest_point_paths(sbr_ctx* c, double beta, double eta, double t_end, double x0, double u, double p,
+                             double kappa, double lambda, double r, double delta, const sbr_opts* opts, double* res,
+                             uint32_t* status, double* tau, double* hr, double* V, double* aw_cum, int64_t cap,
+                             int64_t* n_tau, int64_t* n_v)
+{
+    if (!c || !res || !status) return SBR_EARG;
+    if (!scalars_valid(x0, p, kappa, lambda) || !(beta > 0) || !(eta > 0) || !(t_end > 0) || !(u >= 0))
+        return fail(c, SBR_EARG, "ArgumentError");
+    if (!interest_valid(r, delta)) return fail(c, SBR_EARG, "ArgumentError: need 0 <= r < delta");
+    if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
+    sbr_opts o = resolve(opts);
+    const size_t kc = (size_t)o.knot_capacity;
+    int rc = ensure_stage(c, 4 * 8 + 5 * 8 + 8 + 8 + 2 * kc * 8 + 512);
+    if (rc) return rc;
+    double* d = (double*)c->stage;
+    double hin[4] = {beta, eta, t_end, u};
+    hipStream_t s = c->stream;
+    HIP_TRY(c, hipMemcpyAsync(d, hin, 32, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+    double* dres = d + 4;
+    uint32_t* dst = (uint32_t*)(dres + 5);
+    int32_t* dnv = (int32_t*)(dres + 6);
+    double* dpath = dres + 7;
+    double* dv = dpath + kc;
+    HIP_TRY(c, hipMemsetAsync(dnv, 0, 4, s), SBR_EDEVICE);
+    sbr::ResultSoA rs{dres, dres + 1, dres + 2, dres + 3, dres + 4, dst, nullptr};
+    rc = run_interest(c, s, d, d + 1, d + 2, x0, d + 3, 1, 1, p, kappa, lambda, r, delta, o, rs, nullptr, dpath,
+                      r > 0.0 ? dv : nullptr, dnv);
+    if (rc) return rc;
+    HIP_TRY(c, hipMemcpyAsync(res, dres, 40, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+    HIP_TRY(c, hipMemcpyAsync(status, dst, 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+    int32_t nt = 0, nle = 0, nv = 0;
+    HIP_TRY(c, hipMemcpyAsync(&nt, c->LW[0].n_tau, 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+    HIP_TRY(c, hipMemcpyAsync(&nle, c->LW[0].n_le, 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+    HIP_TRY(c, hipMemcpyAsync(&nv, dnv, 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+    HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
+    if (r <= 0.0) nv = 0;
+    if (n_tau) *n_tau = nt;
+    if (n_v) *n_v = nv;
+    if (nt > cap) return fail(c, SBR_EARG, "path capacity too small");
+    if (tau) {
+        HIP_TRY(c, hipMemcpy(tau, c->LW[0].t, (size_t)nle * 8, hipMemcpyDeviceToHost), SBR_EDEVICE);
+        if (nt > nle) tau[nle] = eta;
+    }
+    if (hr) HIP_TRY(c, hipMemcpy(hr, c->LW[0].hr, (size_t)nt * 8, hipMemcpyDeviceToHost), SBR_EDEVICE);
+    if (V && nv > 0) HIP_TRY(c, hipMemcpy(V, dv, (size_t)nv * 8, hipMemcpyDeviceToHost), SBR_EDEVICE);
+    if (aw_cum) {
+        if (*status & SBR_RUN) HIP_TRY(c, hipMemcpy(aw_cum, dpath, (size_t)nt * 8, hipMemcpyDeviceToHost), SBR_EDEVICE);
+        else for (int i = 0; i < nt; i++) aw_cum[i] = NAN;
+    }
     return SBR_OK;
 }
 

@@ -45,6 +45,8 @@ struct InterestArgs {
     double rtol, atol;   // value-function Tsit5 tolerances (value_function_solver.jl:66: eps())
     int64_t maxiters;
     int64_t* steps;      // value-function RK steps per point (may be null)
+    double* v_path;      // single-point mode (n_u = 1): V on the HR grid (may be null)
+    int32_t* v_count;    // ... and the number of saved values
 };
 
 struct ResultSoA {

@@ -2,7 +2,7 @@
 SBREngine.jl â€” Julia binding of libsbr (include/sbr.h) for the reference's scripts.
 
 Drop-in for the Î²Ã—u loops of scripts/1_baseline.jl (Fig 4 :151-192, Fig 5 :224-267), the
-heterogeneity sweep and the social-learning fixed point over a grid: one `ccall` per grid instead of one solve_learning /
+heterogeneity sweep, the social-learning fixed point and the interest-rate equilibrium over a grid: one `ccall` per grid instead of one solve_learning /
 solve_equilibrium_baseline / get_AW_functions! per point.  Plain-pointer C ABI; Julia owns every
 array (`GC.@preserve`), the library owns device memory.
 
@@ -209,6 +209,31 @@ function solve_equilibrium_interest_grid(ctx::Context, Î²_vals, u_vals; r, Î´, Î
     end
     return (AW_max = aw, Î¾ = xi, Ï„_bar_IN_UNC = tin, Ï„_bar_OUT_UNC = tout, tolerance = tl, status = st,
             rk_steps = steps)
+end
+
+"""
+    solve_interest_point_paths(ctx, Î², u; r, Î´, Î· = 15.0, tspan_end = 30.0, x0 = 1e-4, p = 0.5, Îº = 0.6, Î» = 0.01)
+
+`solve_equilibrium_interest` for one point with what `scripts/3_interest_rates.jl` plots:
+`V = LinearInterpolation(Ï„_bar[1:length(V)], V)` is the reference's value-function
+interpolant (saved on the HR grid), `HR = LinearInterpolation(Ï„_bar, HR)`.
+"""
+function solve_interest_point_paths(ctx::Context, Î², u; r, Î´, Î· = 15.0, tspan_end = 30.0, x0 = 1e-4, p = 0.5,
+                                    Îº = 0.6, Î» = 0.01, cap = 1 << 16)
+    res = zeros(Float64, 5); st = Ref{UInt32}(0); nt = Ref{Int64}(0); nv = Ref{Int64}(0)
+    Ï„ = Vector{Float64}(undef, cap); hr = similar(Ï„); V = similar(Ï„); aw = similar(Ï„)
+    opts = Ref(Opts(; early_exit = 0))
+    GC.@preserve res Ï„ hr V aw begin
+        rc = ccall((:sbr_interest_point_paths, libsbr), Cint,
+                   (Ptr{Cvoid}, Float64, Float64, Float64, Float64, Float64, Float64, Float64, Float64, Float64,
+                    Float64, Ref{Opts}, Ptr{Float64}, Ref{UInt32}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
+                    Ptr{Float64}, Int64, Ref{Int64}, Ref{Int64}),
+                   ctx.ptr, Î², Î·, tspan_end, x0, u, p, Îº, Î», r, Î´, opts, res, st, Ï„, hr, V, aw, cap, nt, nv)
+        check(ctx, rc)
+    end
+    k = nt[]; m = nv[]
+    return (Î¾ = res[1], Ï„_bar_IN_UNC = res[2], Ï„_bar_OUT_UNC = res[3], AW_max = res[4], tolerance = res[5],
+            status = st[], Ï„_bar = Ï„[1:k], HR = hr[1:k], V = V[1:m], AW_cum = aw[1:k])
 end
 
 end # module

@@ -257,6 +257,22 @@ class Engine:
         check(rc, self._ctx, "sbr_sweep_interest")
         return {k: v.reshape(nb, nu) for k, v in out.items()}
 
+    def interest_point_paths(self, beta, eta, t_end, u, p, kappa, lam, r, delta, x0=1e-4, cap=65536) -> dict:
+        """One interest-rate equilibrium with τ̄, HR(τ̄), V(τ̄) (saved on the HR grid) and
+        AW_cum(τ̄) — what scripts/3_interest_rates.jl plots."""
+        res = np.zeros(5)
+        st = np.zeros(1, np.uint32)
+        tau, hr, V, aw = np.empty(cap), np.empty(cap), np.empty(cap), np.empty(cap)
+        nt, nv = ctypes.c_int64(), ctypes.c_int64()
+        opts = _lib.default_opts(early_exit_nan_run=0)
+        rc = self._L.sbr_interest_point_paths(self._ctx, beta, eta, t_end, x0, u, p, kappa, lam, r, delta,
+                                              ctypes.byref(opts), _ptr(res), _ptr(st), _ptr(tau), _ptr(hr), _ptr(V),
+                                              _ptr(aw), cap, ctypes.byref(nt), ctypes.byref(nv))
+        check(rc, self._ctx, "sbr_interest_point_paths")
+        k, m = nt.value, nv.value
+        return dict(xi=res[0], tau_in_unc=res[1], tau_out_unc=res[2], aw_max=res[3], tol=res[4], status=int(st[0]),
+                    hr_tau=tau[:k].copy(), hr=hr[:k].copy(), V=V[:m].copy(), aw_cum=aw[:k].copy())
+
     def sweep_interest_dev(self, beta, eta, t_end, u, p, kappa, lam, r, delta, x0, out: dict,
                            stream: int | None = None, max_iters: int = 100, knot_capacity: int = 65536):
         """Device-pointer interest sweep on torch tensors (enqueue only)."""

@@ -113,3 +113,17 @@ def test_interest_capi_argument_errors():
 def test_interest_gpu_rejects_r_not_below_delta(engine):
     with pytest.raises(sbr.ArgumentError):
         engine.sweep_interest([1.0], 15.0, 30.0, [0.1], 0.5, 0.6, 0.01, 0.1, 0.1)
+
+
+@pytest.mark.gpu
+def test_interest_point_paths_bitwise(engine, oracle):
+    """sbr_interest_point_paths (the script's single point with its plotted paths: τ̄, HR,
+    V saved on the HR grid, AW_cum) == the oracle bit for bit; a no-run u and r = 0 too."""
+    for u, r in ((0.0, 0.06), (0.05, 0.06), (0.9, 0.06), (0.1, 0.0)):
+        g = engine.interest_point_paths(1.0, 15.0, 30.0, u, 0.5, 0.6, 0.01, r, 0.1)
+        o = oracle.interest_point(1.0, 15.0, 30.0, u, 0.5, 0.6, 0.01, r, 0.1)
+        assert g["status"] == o["status"], (u, r)
+        for k in ("xi", "tau_in_unc", "tau_out_unc", "aw_max", "tol", "hr_tau", "hr", "V", "aw_cum"):
+            a, b = np.atleast_1d(g[k]), np.atleast_1d(o[k])
+            assert a.shape == b.shape and np.array_equal(a, b, equal_nan=True), (u, r, k)
+    assert len(engine.interest_point_paths(1.0, 15.0, 30.0, 0.0, 0.5, 0.6, 0.01, 0.0, 0.1)["V"]) == 0
