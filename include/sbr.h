@@ -164,6 +164,16 @@ int sbr_sweep_hetero_dev(sbr_ctx* ctx, void* stream, int32_t K, const double* be
                          const double* eta, const double* t_end, double x0, const double* u, int64_t n_col,
                          int64_t n_u, double p, double kappa, double lambda, const sbr_opts* opts,
                          sbr_result_soa* out, double* tau_in, double* tau_out);
+/* One heterogeneity equilibrium with what scripts/2_heterogeneity.jl plots
+ * (aggregate_withdrawals_hetero.pdf): learning knots t[n] and group CDFs G[n][K]
+ * (solve_SInetwork_hetero), the per-group buffers, and AW_total on the knots
+ * (get_AW_functions_hetero!, heterogeneity_solver.jl:386; NaN without a run), from
+ * which each group's AW curve follows.  res = {ξ, AW_max, tol}; t / aw_total hold
+ * `cap` doubles, G cap·K. */
+int sbr_hetero_point_paths(sbr_ctx* ctx, int32_t K, const double* betas, const double* dist, double eta, double t_end,
+                           double x0, double u, double p, double kappa, double lambda, const sbr_opts* opts,
+                           double* res, uint32_t* status, double* tau_in, double* tau_out, double* t, double* G,
+                           double* aw_total, int64_t cap, int64_t* n_knots);
 
 /*
  * Social-learning extension sweep — for each β column b and each u:

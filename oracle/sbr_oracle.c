@@ -1079,6 +1079,29 @@ int64_t sbro_social_point(double beta, double eta, double x0, double u, double p
     return (sp.n > cap || sp.n_tau > cap) ? -(sp.n > sp.n_tau ? sp.n : sp.n_tau) : sp.n;
 }
 
+/* one hetero point with its paths (aggregate_withdrawals_hetero.pdf): res = {ξ, AW_max, tol};
+ * learning knots t[n], G[n][K], per-group buffers, AW_total on the knots (NaN without a run) */
+int64_t sbro_hetero_point_paths(int32_t K, const double* betas, const double* dist, double eta, double t_end,
+                                double x0, double u, double p, double kappa, double lambda, double* res,
+                                uint32_t* status, double* tin, double* tout, double* t_out, double* G_out,
+                                double* aw_out, int64_t cap)
+{
+    int32_t it = 0;
+    int64_t nk = 0;
+    if (sbro_sweep_hetero(K, betas, dist, &eta, &t_end, x0, &u, 1, 1, p, kappa, lambda, 500, 1e-12, 1, &res[0],
+                          &res[1], &res[2], status, &it, tin, tout, &nk))
+        return -1;
+    const int64_t n = sbro_learn_hetero(betas, dist, K, t_end, x0, t_out, G_out, cap, NULL);
+    if (n < 0) return n;
+    if (*status & SBR_RUN) {
+        int oob = 0;
+        (void)aw_max_hetero(res[0], tin, tout, dist, K, t_out, G_out, n, aw_out, &oob);
+    } else {
+        for (int64_t i = 0; i < n; i++) aw_out[i] = NAN;
+    }
+    return n;
+}
+
 /* ------------------------------------------------------------------------ */
 /* Interest-rate extension (src/extensions/interest_rates/)                  */
 /* ------------------------------------------------------------------------ */

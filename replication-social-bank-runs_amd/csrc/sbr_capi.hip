@@ -46,6 +46,7 @@ struct sbr_ctx {
     uint32_t *pl_perm = nullptr, *pl_bits = nullptr;
     int64_t *pl_steps = nullptr, *pl_pts = nullptr;
     int32_t* so_count_host = nullptr; // pinned
+    double* het_aw_path = nullptr;      // set only inside sbr_hetero_point_paths
     sbr::SocialArgs* so_args_dev = nullptr;  // {main, pool} arguments of the iterate kernel
     sbr::SocialArgs* so_args_host = nullptr; // pinned staging for them
     int64_t so_promoted = 0, so_rerun = 0; // last sweep: points promoted into the pool / re-run larger
@@ -776,7 +777,7 @@ int sbr_sweep_hetero_dev(sbr_ctx* c, void* stream, int32_t K, const double* beta
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, p, lambda, o.ode_maxiters, (int32_t)n_col, 0, 0};
     sbr::HeteroEqArgs ea{kappa, 1e-12, (int32_t)n_u, o.hetero_max_iters, c->lds_cap * 3,
-                         (o.flags & SBR_FLAG_EXHAUSTIVE) ? 1 : 0, (o.flags >> 8) & 7};
+                         (o.flags & SBR_FLAG_EXHAUSTIVE) ? 1 : 0, (o.flags >> 8) & 7, c->het_aw_path};
     sbr::ResultSoA r{out->xi, nullptr, nullptr, out->aw_max, out->tol, out->status, out->iters};
     hipEvent_t t0 = tstart(c, s);
     HIP_TRY(c, sbr::launch_hetero(K, betas, dist, eta, t_end, u, la, ea, c->H, r, tau_in, tau_out, s, 0), SBR_EDEVICE);
@@ -784,6 +785,62 @@ int sbr_sweep_hetero_dev(sbr_ctx* c, void* stream, int32_t K, const double* beta
     t0 = tstart(c, s);
     HIP_TRY(c, sbr::launch_hetero(K, betas, dist, eta, t_end, u, la, ea, c->H, r, tau_in, tau_out, s, 1), SBR_EDEVICE);
     tend(c, s, 1, t0);
+    return SBR_OK;
+}
+
+int sbr_hetero_point_paths(sbr_ctx* c, int32_t K, const double* betas, const double* dist, double eta, double t_end,
+                           double x0, double u, double p, double kappa, double lambda, const sbr_opts* opts,
+                           double* res, uint32_t* status, double* tau_in, double* tau_out, double* t, double* G,
+                           double* aw_total, int64_t cap, int64_t* n_knots)
+{
+    if (!c || !res || !status || !betas || !dist) return SBR_EARG;
+    if (K != 1 && K != 2 && K != 3 && K != 4 && K != 8) return fail(c, SBR_EARG, "K must be 1, 2, 3, 4 or 8");
+    double dsum = 0.0;
+    for (int k = 0; k < K; k++) {
+        if (!(dist[k] >= 0.0)) return fail(c, SBR_EARG, "ArgumentError: distribution weights must be non-negative");
+        if (!(betas[k] > 0.0)) return fail(c, SBR_EARG, "ArgumentError: all learning rates must be positive");
+        dsum = dsum + dist[k];
+    }
+    if (!(fabs(dsum - 1.0) < 1e-10)) return fail(c, SBR_EARG, "ArgumentError: distribution must sum to 1");
+    if (!scalars_valid(x0, p, kappa, lambda) || !(eta > 0) || !(t_end > 0) || !(u >= 0))
+        return fail(c, SBR_EARG, "ArgumentError");
+    if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
+    sbr_opts o = resolve(opts);
+    const size_t kc = (size_t)o.knot_capacity;
+    int rc = ensure_stage(c, (2 * (size_t)K + 3 + 4 + 2 * (size_t)K + kc) * 8 + 512);
+    if (rc) return rc;
+    double* d = (double*)c->stage;
+    double *dbeta = d, *ddist = d + K, *deta = d + 2 * K, *dtend = deta + 1, *du = dtend + 1;
+    double* dres = du + 1; // xi, aw, tol
+    uint32_t* dst = (uint32_t*)(dres + 3);
+    double* dtin = dres + 4;
+    double* dtout = dtin + K;
+    double* dpath = dtout + K;
+    hipStream_t s = c->stream;
+    const double hin[3] = {eta, t_end, u};
+    HIP_TRY(c, hipMemcpyAsync(dbeta, betas, (size_t)K * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+    HIP_TRY(c, hipMemcpyAsync(ddist, dist, (size_t)K * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+    HIP_TRY(c, hipMemcpyAsync(deta, hin, 24, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+    sbr_result_soa r{dres, nullptr, nullptr, dres + 1, dres + 2, dst, nullptr};
+    c->het_aw_path = dpath;
+    rc = sbr_sweep_hetero_dev(c, s, K, dbeta, ddist, deta, dtend, x0, du, 1, 1, p, kappa, lambda, &o, &r, dtin, dtout);
+    c->het_aw_path = nullptr;
+    if (rc) return rc;
+    int32_t n = 0;
+    HIP_TRY(c, hipMemcpyAsync(res, dres, 24, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+    HIP_TRY(c, hipMemcpyAsync(status, dst, 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+    if (tau_in) HIP_TRY(c, hipMemcpyAsync(tau_in, dtin, (size_t)K * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+    if (tau_out) HIP_TRY(c, hipMemcpyAsync(tau_out, dtout, (size_t)K * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+    HIP_TRY(c, hipMemcpyAsync(&n, c->H.n_knots, 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+    HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
+    if (n_knots) *n_knots = n;
+    if (n > cap) return fail(c, SBR_EARG, "path capacity too small");
+    if (t) HIP_TRY(c, hipMemcpy(t, c->H.t, (size_t)n * 8, hipMemcpyDeviceToHost), SBR_EDEVICE);
+    if (G) HIP_TRY(c, hipMemcpy(G, c->H.G, (size_t)n * K * 8, hipMemcpyDeviceToHost), SBR_EDEVICE);
+    if (aw_total) {
+        if (*status & SBR_RUN) HIP_TRY(c, hipMemcpy(aw_total, dpath, (size_t)n * 8, hipMemcpyDeviceToHost), SBR_EDEVICE);
+        else for (int i = 0; i < n; i++) aw_total[i] = NAN;
+    }
     return SBR_OK;
 }
 

@@ -306,7 +306,8 @@ __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const d
                                                    const double u, const double kappa, const int max_iters,
                                                    const double tolerance, const uint32_t lbits, double& xi_o,
                                                    double& aw_o, double& tol_o, uint32_t& st_o, int& it_o,
-                                                   double* tin, double* tout, const bool mono, const int diag)
+                                                   double* tin, double* tout, const bool mono, const int diag,
+                                                   double* __restrict__ aw_path)
 {
     xi_o = NAN; aw_o = NAN; tol_o = INFINITY; it_o = 0;
     const int n = C.n;
@@ -505,6 +506,7 @@ __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const d
                 const double awout = bv >= 0 ? go : 0.0;
                 cum = cum + dist[k] * (awout - awin);
             }
+            if (aw_path) aw_path[i] = cum;
             if (mx == mx && (cum != cum || cum > mx)) mx = cum;
         }
     };
@@ -603,7 +605,7 @@ __global__ __launch_bounds__(BLOCK) void equilibrium_hetero_kernel(HeteroBufs L,
     const double* __restrict__ gT = L.t + (size_t)c * cap;
     const bool fits = n <= a.lds_cap;
     __shared__ int s_nonmono;
-    if (threadIdx.x == 0) s_nonmono = a.exhaustive;
+    if (threadIdx.x == 0) s_nonmono = a.exhaustive || a.aw_path; // path mode: every knot
     if (fits)
         for (int i = threadIdx.x; i < n; i += BLOCK) smem[i] = gT[i];
     __syncthreads();
@@ -661,12 +663,12 @@ __global__ __launch_bounds__(BLOCK) void equilibrium_hetero_kernel(HeteroBufs L,
         HCol<K, const double*> C{smem, L.G + (size_t)c * cap * K, L.hr + (size_t)c * K * cap, n, L.n_tau[c],
                                  L.n_le[c], cap, eta[c], t_end[c], sums && !a.exhaustive ? hsum : nullptr, nblk};
         solve_hetero_point<K>(C, dl, uj, a.kappa, a.max_iters, a.tolerance, lbits, xi, aw, tol, st, it, tin, tout,
-                              mono, a.diag);
+                              mono, a.diag, a.aw_path);
     } else {
         HCol<K, const double*> C{gT, L.G + (size_t)c * cap * K, L.hr + (size_t)c * K * cap, n, L.n_tau[c],
                                  L.n_le[c], cap, eta[c], t_end[c], nullptr, 0};
         solve_hetero_point<K>(C, dl, uj, a.kappa, a.max_iters, a.tolerance, lbits, xi, aw, tol, st, it, tin, tout,
-                              mono, a.diag);
+                              mono, a.diag, a.aw_path);
     }
     const size_t o = (size_t)c * (size_t)a.n_u + j;
     out.xi[o] = xi;

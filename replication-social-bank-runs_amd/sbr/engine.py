@@ -11,6 +11,9 @@ Reference call surface → here:
                                                     social_learning_solver.jl:63
                                                                       → solve_equilibrium_social_learning(model)
                                                                         / Engine.sweep_social(...)
+  solve_SInetwork_hetero + solve_equilibrium_hetero heterogeneity_*.jl → Engine.sweep_hetero / hetero_point_paths
+  solve_equilibrium_interest(lr, econ, model)       interest_rate_solver.jl:51
+                                                                      → Engine.sweep_interest / interest_point_paths
 There is no CPU fallback: without libsbr.so or a GPU every call raises.
 """
 from __future__ import annotations
@@ -256,6 +259,26 @@ class Engine:
                                         lam, r, delta, ctypes.byref(opts), ctypes.byref(soa), _ptr(out["rk_steps"]))
         check(rc, self._ctx, "sbr_sweep_interest")
         return {k: v.reshape(nb, nu) for k, v in out.items()}
+
+    def hetero_point_paths(self, betas, dist, eta, t_end, u, p, kappa, lam, x0=1e-4, cap=65536) -> dict:
+        """One heterogeneity equilibrium with learning knots t, group CDFs G [n, K], the
+        per-group buffers and AW_total(t) — what scripts/2_heterogeneity.jl plots."""
+        betas = np.ascontiguousarray(betas, np.float64)
+        dist = np.ascontiguousarray(dist, np.float64)
+        K = len(dist)
+        res = np.zeros(3)
+        st = np.zeros(1, np.uint32)
+        tin, tout = np.empty(K), np.empty(K)
+        t, G, aw = np.empty(cap), np.empty(cap * K), np.empty(cap)
+        nk = ctypes.c_int64()
+        opts = _lib.default_opts(early_exit_nan_run=0, knot_capacity=16384)
+        rc = self._L.sbr_hetero_point_paths(self._ctx, K, _ptr(betas), _ptr(dist), eta, t_end, x0, u, p, kappa, lam,
+                                            ctypes.byref(opts), _ptr(res), _ptr(st), _ptr(tin), _ptr(tout), _ptr(t),
+                                            _ptr(G), _ptr(aw), cap, ctypes.byref(nk))
+        check(rc, self._ctx, "sbr_hetero_point_paths")
+        n = nk.value
+        return dict(xi=res[0], aw_max=res[1], tol=res[2], status=int(st[0]), tau_in_unc=tin, tau_out_unc=tout,
+                    t=t[:n].copy(), G=G[:n * K].reshape(n, K).copy(), aw_total=aw[:n].copy())
 
     def interest_point_paths(self, beta, eta, t_end, u, p, kappa, lam, r, delta, x0=1e-4, cap=65536) -> dict:
         """One interest-rate equilibrium with τ̄, HR(τ̄), V(τ̄) (saved on the HR grid) and

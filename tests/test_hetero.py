@@ -83,3 +83,28 @@ def test_hetero_aw_branch_and_bound_equals_exhaustive(engine):
                             exhaustive=True)
     for f in ("xi", "aw_max", "tol", "status", "iters"):
         assert np.array_equal(a[f], b[f], equal_nan=a[f].dtype.kind == "f"), f
+
+
+@pytest.mark.gpu
+def test_hetero_point_paths_bitwise(engine, oracle):
+    """sbr_hetero_point_paths (the script point with its plotted paths: learning knots, the
+    group CDFs, per-group buffers, AW_total on the knots) == the oracle bit for bit."""
+    g = sbr.hetero_script_grid()
+    for u in (g.u[0], 0.9):
+        a = engine.hetero_point_paths(g.betas[0], g.dist, g.eta[0], g.t_end[0], u, g.p, g.kappa, g.lam)
+        b = oracle.hetero_point_paths(g.betas[0], g.dist, g.eta[0], g.t_end[0], u, g.p, g.kappa, g.lam)
+        assert a["status"] == b["status"], u
+        for k in ("xi", "aw_max", "tol", "tau_in_unc", "tau_out_unc", "t", "G", "aw_total"):
+            x, y = np.atleast_1d(a[k]), np.atleast_1d(b[k])
+            assert x.shape == y.shape and np.array_equal(x, y, equal_nan=True), (u, k)
+        if a["status"] & sbr.STATUS["SBR_RUN"]:
+            assert np.max(a["aw_total"]) == a["aw_max"]
+
+
+def test_hetero_point_paths_oracle_figure(oracle, golden):
+    """The oracle's path output reproduces the script figure's AW_total maximum."""
+    g = sbr.hetero_script_grid()
+    r = oracle.hetero_point_paths(g.betas[0], g.dist, g.eta[0], g.t_end[0], g.u[0], g.p, g.kappa, g.lam)
+    assert r["status"] & sbr.STATUS["SBR_RUN"]
+    assert np.nanmax(r["aw_total"]) == r["aw_max"]
+    assert r["G"].shape == (len(r["t"]), len(g.dist))
