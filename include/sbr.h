@@ -212,6 +212,15 @@ int sbr_sweep_social_dev(sbr_ctx* ctx, void* stream, const double* beta, const d
                          const double* u, int64_t n_beta, int64_t n_u, double p, double kappa, double lambda,
                          const double* cmp_grid, int32_t n_cmp, double tol, int32_t max_iter, const sbr_opts* opts,
                          sbr_result_soa* out, int32_t* fp_iters, int64_t* rk_steps);
+/* One social-learning fixed point with the learning knots t[n], G[n] of the
+ * returned SolvedModel (the last inner equilibrium, social_learning_solver.jl:262)
+ * — with ξ, τ̄_IN, τ̄_OUT they rebuild the AW curves scripts/4_social_learning.jl
+ * plots (get_AW on τ̄ = knots ≤ η (+ η)).  res = {ξ, τ̄_IN, τ̄_OUT, AW_max, tol};
+ * t / G hold `cap` doubles; SBR_EARG if the knots do not fit. */
+int sbr_social_point_paths(sbr_ctx* ctx, double beta, double eta, double x0, double u, double p, double kappa,
+                           double lambda, const double* cmp_grid, int32_t n_cmp, double tol, int32_t max_iter,
+                           const sbr_opts* opts, double* res, uint32_t* status, int32_t* fp_iters, double* t,
+                           double* G, int64_t cap, int64_t* n_knots);
 /* Workspace budget in bytes for social sweeps (0 = 60 % of free HBM at call time). */
 int sbr_set_social_workspace(sbr_ctx* ctx, int64_t bytes);
 /* Diagnostics: sums over the points of the last social sweep run with

@@ -47,6 +47,9 @@ struct sbr_ctx {
     int64_t *pl_steps = nullptr, *pl_pts = nullptr;
     int32_t* so_count_host = nullptr; // pinned
     double* het_aw_path = nullptr;      // set only inside sbr_hetero_point_paths
+    double *so_path_t = nullptr, *so_path_G = nullptr; // set only inside sbr_social_point_paths
+    int32_t* so_path_n = nullptr;
+    int32_t so_path_cap = 0;
     sbr::SocialArgs* so_args_dev = nullptr;  // {main, pool} arguments of the iterate kernel
     sbr::SocialArgs* so_args_host = nullptr; // pinned staging for them
     int64_t so_promoted = 0, so_rerun = 0; // last sweep: points promoted into the pool / re-run larger
@@ -1006,6 +1009,7 @@ int run_social_pass(sbr_ctx* c, hipStream_t s, const double* beta, const double*
         a.fp_iters = fp_iters;
         a.steps_out = rk_steps;
         a.prof = prof ? c->so_prof : nullptr;
+        a.path_t = c->so_path_t; a.path_G = c->so_path_G; a.path_n = c->so_path_n; a.path_cap = c->so_path_cap;
         a.pool = sbr::SocialPool{};
         sbr::SocialArgs b{}; // the pool's own arguments (n_pts = 0: no pool blocks)
         if (nslots > 0) {
@@ -1131,6 +1135,45 @@ int sbr_sweep_social_dev(sbr_ctx* c, void* stream, const double* beta, const dou
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     return run_social(c, s, beta, eta, x0, u, n_beta, n_u, p, kappa, lambda, cmp_grid, n_cmp, tol, max_iter, o, out,
                       fp_iters, rk_steps, 0);
+}
+
+int sbr_social_point_paths(sbr_ctx* c, double beta, double eta, double x0, double u, double p, double kappa,
+                           double lambda, const double* cmp_grid, int32_t n_cmp, double tol, int32_t max_iter,
+                           const sbr_opts* opts, double* res, uint32_t* status, int32_t* fp_iters, double* t,
+                           double* G, int64_t cap, int64_t* n_knots)
+{
+    if (!c || !res || !status || !t || !G || cap <= 0 || cap > (int64_t(1) << 30)) return SBR_EARG;
+    double* d = nullptr;
+    const size_t kc = (size_t)cap;
+    HIP_TRY(c, hipMalloc(&d, (2 * kc + 8) * 8), SBR_ENOMEM);
+    c->so_path_t = d;
+    c->so_path_G = d + kc;
+    c->so_path_n = (int32_t*)(d + 2 * kc);
+    c->so_path_cap = (int32_t)cap;
+    hipError_t e = hipMemset(c->so_path_n, 0, 4);
+    double xi, tin, tout, aw, tl;
+    int64_t steps = 0;
+    sbr_result_soa out{&xi, &tin, &tout, &aw, &tl, status, nullptr};
+    int rc = e == hipSuccess ? sbr_sweep_social(c, &beta, &eta, x0, &u, 1, 1, p, kappa, lambda, cmp_grid, n_cmp, tol,
+                                                max_iter, opts, &out, fp_iters, &steps)
+                             : fail(c, SBR_EDEVICE, "hipMemset", e);
+    c->so_path_t = c->so_path_G = nullptr;
+    c->so_path_n = nullptr;
+    c->so_path_cap = 0;
+    int32_t n = 0;
+    if (rc == SBR_OK) {
+        e = hipMemcpy(&n, d + 2 * kc, 4, hipMemcpyDeviceToHost);
+        const int64_t m = n < 0 ? 0 : n;
+        if (e == hipSuccess && m > 0) e = hipMemcpy(t, d, (size_t)m * 8, hipMemcpyDeviceToHost);
+        if (e == hipSuccess && m > 0) e = hipMemcpy(G, d + kc, (size_t)m * 8, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) rc = fail(c, SBR_EDEVICE, "social path copy", e);
+    }
+    (void)hipFree(d);
+    if (rc) return rc;
+    res[0] = xi; res[1] = tin; res[2] = tout; res[3] = aw; res[4] = tl;
+    if (n_knots) *n_knots = n < 0 ? -n : n;
+    if (n < 0) return fail(c, SBR_EARG, "path capacity too small");
+    return SBR_OK;
 }
 
 int sbr_sweep_social(sbr_ctx* c, const double* beta, const double* eta, double x0, const double* u, int64_t n_beta,

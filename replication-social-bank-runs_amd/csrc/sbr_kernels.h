@@ -138,6 +138,12 @@ struct SocialArgs {
     int32_t* it_cur;
     int32_t* ready;
     int32_t* n_live;
+    // single-point path mode: the learning knots of every iterate's equilibrium (the
+    // returned SolvedModel's are the last written); path_n = knots (−knots if > path_cap)
+    double* path_t;
+    double* path_G;
+    int32_t* path_n;
+    int32_t path_cap;
 };
 
 hipError_t launch_social_init(const SocialArgs& a, hipStream_t s);

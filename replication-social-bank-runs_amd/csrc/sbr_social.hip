@@ -807,6 +807,15 @@ __device__ __forceinline__ bool social_iterate(const SocialArgs& a, int l, int i
         a.out.tol[g] = tol_r;
         a.out.status[g] = st_r;
         if (a.out.iters) a.out.iters[g] = it_r;
+        if (a.path_t) { // single-point path mode (the SolvedModel's learning knots)
+            if (n <= a.path_cap) {
+                for (int i = 0; i < n; i++) {
+                    a.path_t[i] = T[i];
+                    a.path_G[i] = Gv[i];
+                }
+            }
+            *a.path_n = n <= a.path_cap ? n : -n;
+        }
     }
     if (!finish && iter >= a.max_iter) finish = true;
     if (finish) {

@@ -236,4 +236,57 @@ function solve_interest_point_paths(ctx::Context, β, u; r, δ, η = 15.0, tspan
             status = st[], τ_bar = τ[1:k], HR = hr[1:k], V = V[1:m], AW_cum = aw[1:k])
 end
 
+"""
+    solve_social_point_paths(ctx, β, u; η, x0 = 1e-4, p = 0.99, κ = 0.25, λ = 0.25, tol = 1e-4, max_iter = 500)
+
+`solve_equilibrium_social_learning` for one point with the learning knots `t`, `G` of the
+returned `SolvedModel`; `LinearInterpolation(t, G)` is its `learning_cdf`, from which `get_AW`
+rebuilds the curves of `scripts/4_social_learning.jl` (HR grid τ̄ = knots ≤ η, plus η).
+"""
+function solve_social_point_paths(ctx::Context, β, u; η, x0 = 1e-4, p = 0.99, κ = 0.25, λ = 0.25, tol = 1e-4,
+                                  max_iter = 500, cap = 1 << 20)
+    cmp = collect(range(0.0, Float64(η), length = 1000))
+    res = zeros(Float64, 5); st = Ref{UInt32}(0); fp = Ref{Int32}(0); nk = Ref{Int64}(0)
+    t = Vector{Float64}(undef, cap); G = similar(t)
+    opts = Ref(Opts(; early_exit = 0))
+    GC.@preserve cmp res t G begin
+        rc = ccall((:sbr_social_point_paths, libsbr), Cint,
+                   (Ptr{Cvoid}, Float64, Float64, Float64, Float64, Float64, Float64, Float64, Ptr{Float64}, Int32,
+                    Float64, Int32, Ref{Opts}, Ptr{Float64}, Ref{UInt32}, Ref{Int32}, Ptr{Float64}, Ptr{Float64},
+                    Int64, Ref{Int64}),
+                   ctx.ptr, β, η, x0, u, p, κ, λ, cmp, Int32(1000), tol, Int32(max_iter), opts, res, st, fp, t, G,
+                   cap, nk)
+        check(ctx, rc)
+    end
+    k = nk[]
+    return (ξ = res[1], τ_bar_IN_UNC = res[2], τ_bar_OUT_UNC = res[3], AW_max = res[4], tolerance = res[5],
+            status = st[], fp_iters = fp[], t = t[1:k], G = G[1:k])
+end
+
+"""
+    solve_hetero_point_paths(ctx, βs, dist, u; η, tspan_end, x0 = 1e-4, p = 0.9, κ = 0.3, λ = 0.1)
+
+One heterogeneity equilibrium with the learning knots `t`, the group CDFs `G` (n × K), the
+per-group buffers and `AW_total` on the knots (`get_AW_functions_hetero!`).
+"""
+function solve_hetero_point_paths(ctx::Context, βs, dist, u; η, tspan_end, x0 = 1e-4, p = 0.9, κ = 0.3, λ = 0.1,
+                                  cap = 1 << 16)
+    b = collect(Float64, βs); d = collect(Float64, dist); K = length(d)
+    res = zeros(Float64, 3); st = Ref{UInt32}(0); nk = Ref{Int64}(0)
+    tin = zeros(Float64, K); tout = zeros(Float64, K)
+    t = Vector{Float64}(undef, cap); G = Vector{Float64}(undef, cap * K); aw = similar(t)
+    opts = Ref(Opts(; early_exit = 0))
+    GC.@preserve b d res tin tout t G aw begin
+        rc = ccall((:sbr_hetero_point_paths, libsbr), Cint,
+                   (Ptr{Cvoid}, Int32, Ptr{Float64}, Ptr{Float64}, Float64, Float64, Float64, Float64, Float64,
+                    Float64, Float64, Ref{Opts}, Ptr{Float64}, Ref{UInt32}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
+                    Ptr{Float64}, Ptr{Float64}, Int64, Ref{Int64}),
+                   ctx.ptr, K, b, d, η, tspan_end, x0, u, p, κ, λ, opts, res, st, tin, tout, t, G, aw, cap, nk)
+        check(ctx, rc)
+    end
+    n = nk[]
+    return (ξ = res[1], AW_max = res[2], tolerance = res[3], status = st[], τ_bar_IN_UNCs = tin,
+            τ_bar_OUT_UNCs = tout, t = t[1:n], G = permutedims(reshape(G[1:n*K], K, n)), AW_total = aw[1:n])
+end
+
 end # module

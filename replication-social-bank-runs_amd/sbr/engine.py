@@ -260,6 +260,27 @@ class Engine:
         check(rc, self._ctx, "sbr_sweep_interest")
         return {k: v.reshape(nb, nu) for k, v in out.items()}
 
+    def social_point_paths(self, beta, eta, u, p, kappa, lam, cmp=None, x0=1e-4, tol=1e-4, max_iter=500,
+                           cap=1 << 20) -> dict:
+        """One social-learning fixed point with the learning knots (t, G) of the returned
+        SolvedModel — what scripts/4_social_learning.jl plots (AW curves rebuilt from them)."""
+        if cmp is None:
+            cmp = julia_range(0.0, float(eta), 1000)
+        cmp = np.ascontiguousarray(cmp, np.float64)
+        res = np.zeros(5)
+        st = np.zeros(1, np.uint32)
+        fp = np.zeros(1, np.int32)
+        t, G = np.empty(cap), np.empty(cap)
+        nk = ctypes.c_int64()
+        opts = _lib.default_opts()
+        rc = self._L.sbr_social_point_paths(self._ctx, beta, eta, x0, u, p, kappa, lam, _ptr(cmp), len(cmp), tol,
+                                            max_iter, ctypes.byref(opts), _ptr(res), _ptr(st), _ptr(fp), _ptr(t),
+                                            _ptr(G), cap, ctypes.byref(nk))
+        check(rc, self._ctx, "sbr_social_point_paths")
+        n = nk.value
+        return dict(xi=res[0], tau_in_unc=res[1], tau_out_unc=res[2], aw_max=res[3], tol=res[4], status=int(st[0]),
+                    fp_iters=int(fp[0]), t=t[:n].copy(), G=G[:n].copy())
+
     def hetero_point_paths(self, betas, dist, eta, t_end, u, p, kappa, lam, x0=1e-4, cap=65536) -> dict:
         """One heterogeneity equilibrium with learning knots t, group CDFs G [n, K], the
         per-group buffers and AW_total(t) — what scripts/2_heterogeneity.jl plots."""

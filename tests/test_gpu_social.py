@@ -118,3 +118,19 @@ def test_social_knot_overflow_promotion_and_rerun(engine, oracle):
         _compare(g, o)
         assert_bitwise(g["rk_steps"], ref["rk_steps"], f"rk_steps at capacity {cap}")
         assert not (g["status"] & sbr.STATUS["SBR_KNOT_OVERFLOW"]).any()
+
+
+def test_social_point_paths_bitwise(engine, oracle):
+    """sbr_social_point_paths: the returned SolvedModel's learning knots (t, G) — from which
+    scripts/4_social_learning.jl's AW curves are rebuilt — equal the oracle's, on the script
+    point and on a BoundsError point (where the previous iterate's SolvedModel is returned)."""
+    beta = 1.0 / sbr.julia_range("0.01", "2", 512)
+    u = sbr.julia_range("0.001", "1", 512)
+    cmp = sbr.julia_range(0.0, ETA, 1000)
+    for b, uu in ((0.9, 0.5), (beta[20], u[3])):
+        g = engine.social_point_paths(b, ETA, uu, P, KAPPA, LAM, cmp=cmp)
+        o = oracle.social_point(b, ETA, uu, P, KAPPA, LAM, cmp)
+        assert g["status"] == o["status"] and g["fp_iters"] == o["fp_iters"], (b, uu)
+        for k in ("xi", "tau_in_unc", "tau_out_unc", "aw_max", "tol", "t", "G"):
+            x, y = np.atleast_1d(g[k]), np.atleast_1d(o[k])
+            assert x.shape == y.shape and np.array_equal(x, y, equal_nan=True), (b, uu, k)
