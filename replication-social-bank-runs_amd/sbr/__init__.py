@@ -13,7 +13,12 @@ from .engine import (  # noqa: F401
     SolvedModel,
     default_engine,
     get_AW_functions,
+    SolvedModelHetero,
+    SolvedModelInterest,
+    get_AW_functions_interest,
     solve_equilibrium_baseline,
+    solve_equilibrium_hetero,
+    solve_equilibrium_interest,
     solve_equilibrium_social_learning,
     solve_learning,
 )
@@ -24,6 +29,8 @@ from .model import (  # noqa: F401
     ModelParameters,
     ModelParametersHetero,
     LearningParametersHetero,
+    EconomicParametersInterest,
+    ModelParametersInterest,
 )
 
 __version__ = "0.1.0"

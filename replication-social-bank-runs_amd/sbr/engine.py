@@ -27,7 +27,8 @@ import numpy as np
 from . import _lib
 from ._lib import ArgumentError, SBRNativeError, check
 from .grids import BaselineGrid, julia_range
-from .model import EconomicParameters, LearningParameters, ModelParameters
+from .model import (EconomicParameters, EconomicParametersInterest, LearningParameters, ModelParameters,
+                    ModelParametersHetero, ModelParametersInterest)
 
 _P = ctypes.c_void_p
 
@@ -510,3 +511,64 @@ def get_AW_functions(result: SolvedModel):
     result.aw = dict(AW_cum=LinearInterpolation(tg, result.aw_cum), AW_OUT=LinearInterpolation(tg, aw_out),
                      AW_IN=LinearInterpolation(tg, aw_in), AW_max=float(np.max(result.aw_cum)))
     return result.aw
+
+
+@dataclass
+class SolvedModelInterest(SolvedModel):
+    """interest_rate_model.jl:200-245: SolvedModel plus the value function V
+    (LinearInterpolation on the HR grid; None when r = 0)."""
+
+    V: LinearInterpolation | None = field(repr=False, default=None)
+
+
+def solve_equilibrium_interest(lr: LearningResults, econ: EconomicParametersInterest,
+                               model: ModelParametersInterest | None = None,
+                               engine: Engine | None = None) -> SolvedModelInterest:
+    """interest_rate_solver.jl:51-150 for one point on the GPU: HR, the value function
+    saved on the HR grid (r > 0), buffers on h − rV, compute_ξ, and the AW paths."""
+    eng = engine or default_engine()
+    lp = lr.params
+    r = eng.interest_point_paths(lp.beta, econ.eta, lp.tspan[1], econ.u, econ.p, econ.kappa, econ.lam, econ.r,
+                                 econ.delta, lp.x0)
+    st = r["status"]
+    V = LinearInterpolation(r["hr_tau"][:len(r["V"])], r["V"]) if econ.r > 0 and len(r["V"]) >= 2 else None
+    return SolvedModelInterest(r["xi"], r["tau_in_unc"], r["tau_out_unc"], LinearInterpolation(r["hr_tau"], r["hr"]),
+                               bool(st & _lib.SBR_RUN), (lp, econ) if model is None else model, lr,
+                               bool(st & _lib.SBR_CONVERGED), r["tol"], st, aw_cum=r["aw_cum"], V=V)
+
+
+def get_AW_functions_interest(result: SolvedModelInterest):
+    """interest_rate_solver.jl:161-184: the baseline get_AW on the HR grid (None without a run)."""
+    return get_AW_functions(result)
+
+
+@dataclass
+class SolvedModelHetero:
+    """heterogeneity_model.jl SolvedModelHetero: ξ, the per-group buffers, the learning
+    knots / group CDFs and AW_total on the knots (get_AW_functions_hetero!)."""
+
+    xi: float
+    tau_bar_IN_UNCs: np.ndarray
+    tau_bar_OUT_UNCs: np.ndarray
+    bankrun: bool
+    converged: bool
+    tolerance: float
+    status: int
+    t: np.ndarray = field(repr=False)
+    G: np.ndarray = field(repr=False)
+    AW_total: np.ndarray = field(repr=False)
+    AW_max: float = float("nan")
+
+
+def solve_equilibrium_hetero(model: ModelParametersHetero, engine: Engine | None = None) -> SolvedModelHetero:
+    """solve_SInetwork_hetero + solve_equilibrium_hetero + get_AW_functions_hetero!
+    (heterogeneity_learning.jl:49, heterogeneity_solver.jl:241, :386) for one model."""
+    eng = engine or default_engine()
+    lp, e = model.learning, model.economic
+    if lp.tspan[0] != 0.0:
+        raise _lib.ArgumentError("the engine integrates from t = 0 (every reference call site does)")
+    r = eng.hetero_point_paths(np.array(lp.betas), np.array(lp.dist), e.eta, lp.tspan[1], e.u, e.p, e.kappa, e.lam,
+                               lp.x0)
+    st = r["status"]
+    return SolvedModelHetero(r["xi"], r["tau_in_unc"], r["tau_out_unc"], bool(st & _lib.SBR_RUN),
+                             bool(st & _lib.SBR_CONVERGED), r["tol"], st, r["t"], r["G"], r["aw_total"], r["aw_max"])

@@ -184,3 +184,58 @@ class ModelParametersHetero:
                    tspan=base.learning.tspan, x0=base.learning.x0)
         cur.update(kw)
         return ModelParametersHetero.make(**cur)
+
+
+@dataclass(frozen=True)
+class EconomicParametersInterest:
+    """interest_rate_model.jl:25-54: the baseline economic parameters plus the
+    interest rate r and deposit maturity rate δ (0 ≤ r < δ)."""
+
+    u: float
+    p: float
+    kappa: float
+    lam: float
+    eta_bar: float
+    eta: float
+    r: float
+    delta: float
+
+    def __post_init__(self):
+        EconomicParameters(self.u, self.p, self.kappa, self.lam, self.eta_bar, self.eta)  # shared checks (:40-45)
+        if not self.r >= 0:
+            raise ArgumentError(f"Interest rate r must be non-negative, got r = {self.r}")
+        if not self.delta > 0:
+            raise ArgumentError(f"Recovery rate δ must be positive, got δ = {self.delta}")
+        if not self.r < self.delta:
+            raise ArgumentError("Interest rate r must be less than recovery rate δ for convergence, "
+                                f"got r = {self.r}, δ = {self.delta}")
+
+
+@dataclass(frozen=True)
+class ModelParametersInterest:
+    """interest_rate_model.jl:82-92 with the keyword constructor (:120-148; η = η_bar/β,
+    tspan = (0, 2η), r = 0, δ = 0.1 defaults) and the copy-modify one (:161-185)."""
+
+    learning: LearningParameters
+    economic: EconomicParametersInterest
+
+    @staticmethod
+    def make(beta=1.0, eta=None, eta_bar=15.0, u=0.1, p=0.5, kappa=0.6, lam=0.01, r=0.0, delta=0.1, tspan=None,
+             x0=0.0001):
+        if eta is None:
+            eta = _fdiv(eta_bar, beta)
+        if tspan is None:
+            tspan = (0.0, 2 * eta)
+        return ModelParametersInterest(LearningParameters(beta, tspan, x0),
+                                       EconomicParametersInterest(u, p, kappa, lam, eta_bar, eta, r, delta))
+
+    @staticmethod
+    def modify(base: "ModelParametersInterest", **kw) -> "ModelParametersInterest":
+        e = base.economic
+        cur = dict(beta=base.learning.beta, eta=e.eta, eta_bar=e.eta_bar, u=e.u, p=e.p, kappa=e.kappa, lam=e.lam,
+                   r=e.r, delta=e.delta, tspan=base.learning.tspan, x0=base.learning.x0)
+        unknown = set(kw) - set(cur)
+        if unknown:
+            raise TypeError(f"unknown parameters {sorted(unknown)}")
+        cur.update(kw)
+        return ModelParametersInterest.make(**cur)

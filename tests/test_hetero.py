@@ -108,3 +108,17 @@ def test_hetero_point_paths_oracle_figure(oracle, golden):
     assert r["status"] & sbr.STATUS["SBR_RUN"]
     assert np.nanmax(r["aw_total"]) == r["aw_max"]
     assert r["G"].shape == (len(r["t"]), len(g.dist))
+
+
+@pytest.mark.gpu
+def test_hetero_reference_call_surface(engine, oracle):
+    """scripts/2_heterogeneity.jl through the host mirror: ModelParametersHetero →
+    solve_equilibrium_hetero (learning + equilibrium + AW paths), equal to the oracle."""
+    g = sbr.hetero_script_grid()
+    m = sbr.ModelParametersHetero.make(g.betas[0], g.dist, eta_bar=30.0, u=float(g.u[0]), p=g.p, kappa=g.kappa,
+                                       lam=g.lam)
+    r = sbr.solve_equilibrium_hetero(m, engine=engine)
+    o = oracle.hetero_point_paths(g.betas[0], g.dist, m.economic.eta, m.learning.tspan[1], float(g.u[0]), g.p,
+                                  g.kappa, g.lam)
+    assert r.status == o["status"] and r.xi == o["xi"] and r.AW_max == o["aw_max"]
+    assert np.array_equal(r.AW_total, o["aw_total"])

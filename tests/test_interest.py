@@ -127,3 +127,18 @@ def test_interest_point_paths_bitwise(engine, oracle):
             a, b = np.atleast_1d(g[k]), np.atleast_1d(o[k])
             assert a.shape == b.shape and np.array_equal(a, b, equal_nan=True), (u, r, k)
     assert len(engine.interest_point_paths(1.0, 15.0, 30.0, 0.0, 0.5, 0.6, 0.01, 0.0, 0.1)["V"]) == 0
+
+
+@pytest.mark.gpu
+def test_interest_reference_call_surface(engine, oracle):
+    """scripts/3_interest_rates.jl's calls through the host mirror: solve_learning →
+    solve_equilibrium_interest → get_AW_functions_interest, equal to the oracle."""
+    m = sbr.ModelParametersInterest.make(beta=1.0, eta_bar=15.0, u=0.0, p=0.5, kappa=0.6, lam=0.01, r=0.06,
+                                         delta=0.1)
+    lr = sbr.solve_learning(m.learning, engine=engine)
+    res = sbr.solve_equilibrium_interest(lr, m.economic, m, engine=engine)
+    o = _script_point(oracle)
+    assert res.xi == o["xi"] and res.bankrun and res.V is not None
+    assert np.array_equal(res.V.coefs, o["V"])
+    aw = sbr.get_AW_functions_interest(res)
+    assert aw["AW_max"] == o["aw_max"]

@@ -54,3 +54,20 @@ def test_julia_range_is_exact_decimal_interpolation():
     g = sbr.fig5_grid(500)
     assert g.beta[0] == 1e4 and g.beta[-1] == 1.0 and g.u[-1] == 1.0
     assert np.all(np.diff(g.beta) < 0)
+
+
+def test_interest_parameters_mirror_reference_checks():
+    """interest_rate_model.jl:38-54, 120-185: defaults, η = η_bar/β, tspan = (0, 2η),
+    the 0 ≤ r < δ checks, and copy-modify carrying η / tspan."""
+    m = sbr.ModelParametersInterest.make(beta=1.0, eta_bar=15.0, u=0.0, r=0.06, delta=0.1)
+    assert m.economic.eta == 15.0 and m.learning.tspan == (0.0, 30.0)
+    assert (m.economic.r, m.economic.delta) == (0.06, 0.1)
+    d = sbr.ModelParametersInterest.make()
+    assert (d.economic.r, d.economic.delta, d.economic.u) == (0.0, 0.1, 0.1)
+    for kw in (dict(r=-0.01), dict(delta=0.0), dict(r=0.1, delta=0.1), dict(kappa=1.0), dict(u=-1.0)):
+        with pytest.raises(sbr.ArgumentError):
+            sbr.ModelParametersInterest.make(**kw)
+    m2 = sbr.ModelParametersInterest.modify(m, beta=2.0)
+    assert m2.economic.eta == 15.0 and m2.learning.tspan == (0.0, 30.0)  # carried, as in the reference
+    with pytest.raises(TypeError):
+        sbr.ModelParametersInterest.modify(m, gamma=1.0)
