@@ -166,6 +166,9 @@ __global__ __launch_bounds__(64) void learn_logistic_kernel(const double* __rest
 // e = exp(λτ̄)·g, the cumulative trapezoid (sequential, in the reference's
 // order) and HR = (p·exp(λτ̄))·g / (p·I + (1−p)·I_η).
 // ============================================================================
+#ifndef SBR_EQ_WIDE
+#define SBR_EQ_WIDE 768
+#endif
 constexpr int HZ_BLOCK = 256;
 constexpr int HZ_CHUNK = 16;
 constexpr int EQ_TILE = 4096;  // u values per equilibrium block (one block per β column up to this)
@@ -858,13 +861,18 @@ __global__ __launch_bounds__(BLOCK) void equilibrium_kernel(LearnBufs L, const d
     const double* __restrict__ gT = L.t + row;
     const double* __restrict__ gG = L.G + row;
     const double* __restrict__ gH = L.hr + row;
-    const bool fits = n <= a.lds_cap && ntau <= a.lds_cap;
+    // Baseline: t and G staged (HR is read once per point by the blocked crossing scan, from
+    // L2, with its block summaries in LDS) so that two workgroups fit a CU's LDS; the
+    // interest mode stages HR too (its value functions look it up every RK stage).
+    constexpr int NS = INTEREST ? 3 : 2;
+    const bool fits = n <= a.lds_cap && (!INTEREST || ntau <= a.lds_cap);
     double* sT = smem;
     double* sG = smem + a.lds_cap;
-    double* sH = smem + 2 * a.lds_cap;
+    double* sH = INTEREST ? smem + 2 * a.lds_cap : nullptr;
+    const double* __restrict__ cH = INTEREST ? sH : gH;
     // block summaries behind the three knot arrays (lds_cap/64 + 1 entries each)
     const int nsum = (a.lds_cap >> 6) + 1, nsum8 = (a.lds_cap >> 3) + 1;
-    double* hmax = smem + 3 * a.lds_cap;
+    double* hmax = smem + NS * a.lds_cap;
     double* hmin = hmax + nsum;
     double* pmc = hmin + nsum;
     double* smc = pmc + nsum8;
@@ -872,7 +880,8 @@ __global__ __launch_bounds__(BLOCK) void equilibrium_kernel(LearnBufs L, const d
     if (threadIdx.x == 0) eq_next = 0;
     if (fits) {
         for (int i = threadIdx.x; i < n; i += BLOCK) { sT[i] = gT[i]; sG[i] = gG[i]; }
-        for (int i = threadIdx.x; i < ntau; i += BLOCK) sH[i] = gH[i];
+        if (INTEREST)
+            for (int i = threadIdx.x; i < ntau; i += BLOCK) sH[i] = gH[i];
     }
     __syncthreads();
     Summ S{nullptr, nullptr, nullptr, nullptr, false, (double)NAN};
@@ -886,7 +895,7 @@ __global__ __launch_bounds__(BLOCK) void equilibrium_kernel(LearnBufs L, const d
                 double mx = -INFINITY, mn = INFINITY;
                 const int e = (bk << 6) + 64 < ntau ? (bk << 6) + 64 : ntau;
                 for (int i = bk << 6; i < e; i++) {
-                    const double h = sH[i];
+                    const double h = cH[i];
                     if (h > mx) mx = h;                         // NaN never > u: ignore it
                     mn = (h != h) ? -INFINITY : (h < mn ? h : mn); // NaN is "not above"
                 }
@@ -971,7 +980,8 @@ __global__ __launch_bounds__(BLOCK) void equilibrium_kernel(LearnBufs L, const d
                 solve_interest_point(gT, gG, gH, S, n, ntau, nle, ETA, T1, trunc, uj, a.kappa, a.max_iters, lbits, ia,
                                      r, vsteps, a.aw_path, a.diag);
         } else if (fits) {
-            solve_point(sT, sG, sH, S, n, ntau, nle, ETA, T1, trunc, uj, a.kappa, a.max_iters, lbits, r, a.aw_path, a.diag);
+            solve_point((const double*)sT, (const double*)sG, cH, S, n, ntau, nle, ETA, T1, trunc, uj, a.kappa,
+                        a.max_iters, lbits, r, a.aw_path, a.diag);
         } else {
             solve_point(gT, gG, gH, S, n, ntau, nle, ETA, T1, trunc, uj, a.kappa, a.max_iters, lbits, r, a.aw_path, a.diag);
         }
@@ -1005,14 +1015,16 @@ hipError_t launch_learn_logistic(const double* beta, const double* eta, const do
 hipError_t launch_equilibrium(const LearnBufs& L, const double* eta, const double* t_end, const double* u,
                               const EqArgs& a, const ResultSoA& out, int n_beta, hipStream_t s)
 {
-    const size_t lds = ((size_t)3 * a.lds_cap + 2 * ((a.lds_cap >> 6) + 1) + 2 * ((a.lds_cap >> 3) + 1)) * sizeof(double);
-    // one block per (β column, tile of EQ_TILE u values); block size by tile width
+    const size_t lds = ((size_t)2 * a.lds_cap + 2 * ((a.lds_cap >> 6) + 1) + 2 * ((a.lds_cap >> 3) + 1)) * sizeof(double);
+    // one block per (β column, tile of EQ_TILE u values); block size by tile width.  Wide
+    // tiles use 12-wave blocks: two per CU (LDS holds two columns' t and G) = 6 waves/SIMD.
     const int tiles = (a.n_u + EQ_TILE - 1) / EQ_TILE;
     const int w = a.n_u < EQ_TILE ? a.n_u : EQ_TILE;
     dim3 grid(tiles, n_beta);
     const InterestArgs none{0.0, 1.0, 0.0, 0.0, 0, nullptr, nullptr, nullptr};
     if (w > 256)
-        hipLaunchKernelGGL((equilibrium_kernel<1024, false>), grid, dim3(1024), lds, s, L, eta, t_end, u, a, none, out);
+        hipLaunchKernelGGL((equilibrium_kernel<SBR_EQ_WIDE, false>), grid, dim3(SBR_EQ_WIDE), lds, s, L, eta, t_end, u, a,
+                           none, out);
     else if (w > 64)
         hipLaunchKernelGGL((equilibrium_kernel<256, false>), grid, dim3(256), lds, s, L, eta, t_end, u, a, none, out);
     else

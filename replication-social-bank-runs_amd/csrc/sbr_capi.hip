@@ -60,7 +60,7 @@ struct sbr_ctx {
     // host-API staging
     void* stage = nullptr;
     size_t stage_bytes = 0;
-    int lds_cap = 0;
+    int lds_cap = 0, lds_cap_b = 0;
     int lds_smem = 0;
     // kernel timing (HIP event pairs on the launching stream), opt-in via sbr_timing_enable
     bool timing = false;
@@ -290,8 +290,8 @@ int launch_eq(sbr_ctx* c, hipStream_t s, const sbr::LearnBufs& L, const double* 
               const double* u, int64_t n_beta, int64_t n_u, double kappa, const sbr_opts& o,
               const sbr::ResultSoA& out, double* aw_path)
 {
-    sbr::EqArgs ea{kappa, (int32_t)n_u, o.bisect_max_iters, c->lds_cap, aw_path, (o.flags & SBR_FLAG_EXHAUSTIVE) ? 1 : 0,
-                   (o.flags >> 8) & 7};
+    sbr::EqArgs ea{kappa, (int32_t)n_u, o.bisect_max_iters, c->lds_cap_b, aw_path,
+                   (o.flags & SBR_FLAG_EXHAUSTIVE) ? 1 : 0, (o.flags >> 8) & 7};
     hipEvent_t t0 = tstart(c, s);
     HIP_TRY(c, sbr::launch_equilibrium(L, eta, t_end, u, ea, out, (int)n_beta, s), SBR_EDEVICE);
     tend(c, s, 1, t0);
@@ -373,6 +373,8 @@ int sbr_init(int device, sbr_ctx** out)
     // 3 doubles per staged knot (t, G, HR) + 4 block-summary doubles per 64 knots; 1 KiB slack
     // per 64 knots: t, G, HR (3·64) + HR max/min (2) + 8-knot G prefix-max/suffix-min (16)
     c->lds_cap = (int)(((long)(smem - 1024) * 64) / (8 * (3 * 64 + 2 + 16)));
+    // baseline equilibrium kernel: t, G (2·64) + summaries per 64 knots, two workgroups per CU
+    c->lds_cap_b = (int)(((long)(smem / 2 - 1024) * 64) / (8 * (2 * 64 + 2 + 16)));
     *out = c;
     return SBR_OK;
 }
