@@ -169,6 +169,9 @@ __global__ __launch_bounds__(64) void learn_logistic_kernel(const double* __rest
 #ifndef SBR_EQ_WIDE
 #define SBR_EQ_WIDE 768
 #endif
+#ifndef SBR_EQ_MINW
+#define SBR_EQ_MINW 6 // waves per SIMD the baseline equilibrium kernel must fit (two 12-wave blocks per CU)
+#endif
 constexpr int HZ_BLOCK = 256;
 constexpr int HZ_CHUNK = 16;
 constexpr int EQ_TILE = 4096;  // u values per equilibrium block (one block per β column up to this)
@@ -463,7 +466,15 @@ __device__ __forceinline__ void solve_from_buffers(P T, P G, P H, const Summ& S,
     auto brk_b = [&](int i) { rb_j = ssl_near(T, n, rb_j + (i - rb_i), xb_of(i)); rb_i = i; return rb_j; };
     // exact AW_cum(τ̄_i) for i in [i0, i1), folded into the NaN-propagating max
     auto eval_range = [&](int i0, int i1) {
-        int ji = brk_a(i0), jo = brk_b(i0);
+        // The brackets of a(τ̄_i) and b(τ̄_i) only move forward with i: keep each bracket's
+        // two knots (t, G) in registers and slide them, so a knot costs the LDS loads of
+        // the knots the brackets pass (≈1 per argument) instead of a fresh search + 4 lerp
+        // operands each.  Bracket k = min(searchsortedlast, n − 2), as lerp_at clamps it.
+        int ka = brk_a(i0), kb = brk_b(i0);
+        ka = ka < n - 2 ? ka : n - 2;
+        kb = kb < n - 2 ? kb : n - 2;
+        double ta0 = T[ka], ta1 = T[ka + 1], ga0 = G[ka], ga1 = G[ka + 1];
+        double tb0 = T[kb], tb1 = T[kb + 1], gb0 = G[kb], gb1 = G[kb + 1];
         for (int i = i0; i < i1; i++) {
             const double ti = tau(i);
             const double av = (ti - xi) + icc;
@@ -471,12 +482,15 @@ __device__ __forceinline__ void solve_from_buffers(P T, P G, P H, const Summ& S,
             const double xa = av > 0 ? av : 0.0;
             const double xb = bv > 0 ? bv : 0.0;
             if (!(xa <= thi) || !(xb <= thi)) { flag |= trunc ? SBR_ENGINE_TRUNC : SBR_OOB; return; }
-            while (ji + 1 < n && T[ji + 1] <= xa) ji++;
-            while (jo + 1 < n && T[jo + 1] <= xb) jo++;
-            const double gi = lerp_at(T, G, n, ji, xa);
+            while (ka < n - 2 && ta1 <= xa) { ka++; ta0 = ta1; ga0 = ga1; ta1 = T[ka + 1]; ga1 = G[ka + 1]; }
+            while (kb < n - 2 && tb1 <= xb) { kb++; tb0 = tb1; gb0 = gb1; tb1 = T[kb + 1]; gb1 = G[kb + 1]; }
+            const double da = (xa - ta0) / (ta1 - ta0);
+            const double gi = ga0 * (1.0 - da) + ga1 * da;
             // b(τ̄_i) = (τ̄_i − ξ) + ξ is τ̄_i itself whenever τ̄_i − ξ is exact (Sterbenz):
             // then δ = 0 and the lerp is G[j]·(1 − 0) + G[j+1]·0, no division
-            const double go = (xb == T[jo] && jo < n - 1) ? G[jo] * 1.0 + G[jo + 1] * 0.0 : lerp_at(T, G, n, jo, xb);
+            double go;
+            if (xb == tb0) go = gb0 * 1.0 + gb1 * 0.0;
+            else { const double db = (xb - tb0) / (tb1 - tb0); go = gb0 * (1.0 - db) + gb1 * db; }
             const double awin = av >= 0 ? gi : 0.0;
             const double awout = bv >= 0 ? go : 0.0;
             const double v = (awout - awin) + G0;
@@ -484,6 +498,8 @@ __device__ __forceinline__ void solve_from_buffers(P T, P G, P H, const Summ& S,
             if (aw_path) aw_path[i] = v;
             if (mx == mx && (v != v || v > mx)) mx = v;
         }
+        ra_j = ka; ra_i = i1 - 1;
+        rb_j = kb; rb_i = i1 - 1;
     };
     if (!S.pmc || aw_path) {
         eval_range(0, ntau); // exhaustive (single-point path mode, or summaries unavailable)
@@ -848,7 +864,7 @@ __device__ __forceinline__ void solve_interest_point(P T, P G, P H, const Summ& 
 }
 
 template <int BLOCK, bool INTEREST>
-__global__ __launch_bounds__(BLOCK) void equilibrium_kernel(LearnBufs L, const double* __restrict__ eta,
+__global__ __launch_bounds__(BLOCK, INTEREST ? 1 : SBR_EQ_MINW) void equilibrium_kernel(LearnBufs L, const double* __restrict__ eta,
                                                             const double* __restrict__ t_end,
                                                             const double* __restrict__ u, EqArgs a, InterestArgs ia,
                                                             ResultSoA out)
