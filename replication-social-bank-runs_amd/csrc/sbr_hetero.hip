@@ -307,7 +307,7 @@ __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const d
                                                    const double tolerance, const uint32_t lbits, double& xi_o,
                                                    double& aw_o, double& tol_o, uint32_t& st_o, int& it_o,
                                                    double* tin, double* tout, const bool mono, const int diag,
-                                                   double* __restrict__ aw_path)
+                                                   double* __restrict__ aw_path, const double env)
 {
     xi_o = NAN; aw_o = NAN; tol_o = INFINITY; it_o = 0;
     const int n = C.n;
@@ -513,9 +513,10 @@ __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const d
     if (!mono) {
         eval_range(0, n);
     } else {
-        // Every group CDF is nondecreasing on the knots, so over knots [i0, i1] AW_OUT,k is
-        // at most G_k at the knot after b_k(t_i1)'s bracket and AW_IN,k at least G_k at
-        // a_k(t_i0)'s bracket (0 where masked): branch and bound over 256/64/8-knot ranges,
+        // Every group CDF is nondecreasing on the knots up to its drawdown Δ_k, so over knots
+        // [i0, i1] AW_OUT,k is at most G_k at the knot after b_k(t_i1)'s bracket + Δ_k and AW_IN,k
+        // at least G_k at a_k(t_i0)'s bracket − Δ_k (0 where masked; `env` = Σ dist_k·2Δ_k):
+        // branch and bound over 256/64/8-knot ranges,
         // the same maximum with a fraction of the K·2 lerps per knot.  Arguments are
         // nondecreasing in i, so the last knot's range check covers the whole path.
 #pragma unroll
@@ -544,7 +545,7 @@ __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const d
                 }
                 sum = sum + dist[k] * (hi - lo);
             }
-            return sum + 1e-14;
+            return (sum + 1e-14) + env;
         };
         auto end_of = [&](int i0, int w) { return i0 + w < n ? i0 + w : n; };
         if (!flag) {
@@ -610,16 +611,36 @@ __global__ __launch_bounds__(BLOCK) void equilibrium_hetero_kernel(HeteroBufs L,
         for (int i = threadIdx.x; i < n; i += BLOCK) smem[i] = gT[i];
     __syncthreads();
 
-    {   // every group CDF nondecreasing on the knots (no NaN)?  -> AW_max branch and bound
+    // Group CDF drawdown for the AW_max branch and bound: Tsit5 at eps() leaves ulp-sized
+    // decreases in the saturated tail (G_k = 1 − 2^-53 after 1.0: most config-4 columns), so
+    // the bounds take G_k[j] ± Δ_k for the prefix max / suffix min, with
+    // Δ_k = (#decreases)·(largest decrease) ≥ the largest drawdown max_{j<j'} G_k[j] − G_k[j'].
+    // NaN anywhere -> exhaustive evaluation.
+    __shared__ int s_dcnt[K];
+    __shared__ unsigned long long s_dmax[K];
+    if (threadIdx.x < K) { s_dcnt[threadIdx.x] = 0; s_dmax[threadIdx.x] = 0ull; }
+    __syncthreads();
+    {
         const double* __restrict__ Gc = L.G + (size_t)c * cap * K;
-        bool ok = true;
+        bool nan = false;
+        int cnt[K];
+        double dm[K];
+#pragma unroll
+        for (int k = 0; k < K; k++) { cnt[k] = 0; dm[k] = 0.0; }
         for (int i = 1 + threadIdx.x; i < n; i += BLOCK)
 #pragma unroll
             for (int k = 0; k < K; k++) {
                 const double g1 = Gc[(size_t)i * K + k], g0 = Gc[(size_t)(i - 1) * K + k];
-                ok &= g1 >= g0 && g0 == g0;
+                if (g0 != g0 || g1 != g1) nan = true;
+                else if (g1 < g0) { cnt[k]++; dm[k] = dmax(dm[k], g0 - g1); }
             }
-        if (!ok) s_nonmono = 1;
+        if (nan) s_nonmono = 1;
+#pragma unroll
+        for (int k = 0; k < K; k++)
+            if (cnt[k]) {
+                atomicAdd(&s_dcnt[k], cnt[k]);
+                atomicMax(&s_dmax[k], (unsigned long long)__double_as_longlong(dm[k])); // dm > 0: ordered as bits
+            }
     }
     // per-group 64-entry block max / min of HR (sbr_scan.h) at the top of the LDS slab
     const int ntau = L.n_tau[c];
@@ -644,6 +665,10 @@ __global__ __launch_bounds__(BLOCK) void equilibrium_hetero_kernel(HeteroBufs L,
     }
     __syncthreads();
     const bool mono = s_nonmono == 0;
+    double env = 0.0; // Σ_k dist_k · 2Δ_k, added to every branch-and-bound bound
+#pragma unroll
+    for (int k = 0; k < K; k++)
+        env = env + dist[k] * (2.0 * ((double)s_dcnt[k] * __longlong_as_double((long long)s_dmax[k])));
     const int j = blockIdx.x * BLOCK + threadIdx.x;
     if (j >= a.n_u) return;
     double dl[K];
@@ -663,12 +688,12 @@ __global__ __launch_bounds__(BLOCK) void equilibrium_hetero_kernel(HeteroBufs L,
         HCol<K, const double*> C{smem, L.G + (size_t)c * cap * K, L.hr + (size_t)c * K * cap, n, L.n_tau[c],
                                  L.n_le[c], cap, eta[c], t_end[c], sums && !a.exhaustive ? hsum : nullptr, nblk};
         solve_hetero_point<K>(C, dl, uj, a.kappa, a.max_iters, a.tolerance, lbits, xi, aw, tol, st, it, tin, tout,
-                              mono, a.diag, a.aw_path);
+                              mono, a.diag, a.aw_path, env);
     } else {
         HCol<K, const double*> C{gT, L.G + (size_t)c * cap * K, L.hr + (size_t)c * K * cap, n, L.n_tau[c],
                                  L.n_le[c], cap, eta[c], t_end[c], nullptr, 0};
         solve_hetero_point<K>(C, dl, uj, a.kappa, a.max_iters, a.tolerance, lbits, xi, aw, tol, st, it, tin, tout,
-                              mono, a.diag, a.aw_path);
+                              mono, a.diag, a.aw_path, env);
     }
     const size_t o = (size_t)c * (size_t)a.n_u + j;
     out.xi[o] = xi;
