@@ -445,26 +445,66 @@ __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const d
     if (diag & 2) return; // ... after the bisection
 
     // ---------------- is_valid_equilibrium_hetero ----------------
+    // valid ⇔ no knot pair (t_{i−1}, t_i), t_i ≤ ξ, with AW(t_{i−1}) > κ ≥ AW(t_i), where
+    // AW(t) = Σ dist_k (G_k(t) − G_k(max(0, t − τ_I,k))) (heterogeneity_solver.jl:190-207).
     {
         double tI[K];
         int jp[K];
 #pragma unroll
         for (int k = 0; k < K; k++) { tI[k] = dmax(0.0, xi - tin[k]); jp[k] = 0; }
         bool prev = false, valid = true;
-        for (int i = 0; i < n && C.T[i] <= xi; i++) {
-            const double ti = C.T[i];
-            double aw = 0.0;
+        // the reference's per-knot test on knots [i0, i1) with walkers jp at x(t_i0)'s bracket
+        auto exact = [&](int i0, int i1) {
+            for (int i = i0; i < i1; i++) {
+                const double ti = C.T[i];
+                double aw = 0.0;
 #pragma unroll
-            for (int k = 0; k < K; k++) {
-                const double a = C.lerp(i, k, ti);
-                const double x = dmax(0.0, ti - tI[k]);
-                while (jp[k] + 1 < n && C.T[jp[k] + 1] <= x) jp[k]++;
-                const double bb = C.lerp(jp[k], k, x);
-                aw = aw + dist[k] * (a - bb);
+                for (int k = 0; k < K; k++) {
+                    const double a = C.lerp(i, k, ti);
+                    const double x = dmax(0.0, ti - tI[k]);
+                    while (jp[k] + 1 < n && C.T[jp[k] + 1] <= x) jp[k]++;
+                    const double bb = C.lerp(jp[k], k, x);
+                    aw = aw + dist[k] * (a - bb);
+                }
+                const bool above = aw > kappa;
+                if (i > 0 && prev && !above) { valid = false; return; }
+                prev = above;
             }
-            const bool above = aw > kappa;
-            if (i > 0 && prev && !above) { valid = false; break; }
-            prev = above;
+        };
+        const int m = ssl_range(C.T, 0, n - 1, xi) + 1; // knots with t ≤ ξ (ξ ≥ t_0 here)
+        if (!mono) {
+            exact(0, m);
+        } else {
+            // 64-knot blocks bounded as in AW_max (G_k nondecreasing up to Δ_k): a block whose
+            // bounds put every knot on one side of κ is decided without evaluating it; only
+            // blocks straddling κ (near the crossing) are evaluated knot by knot.
+            int hl[K], hh[K];
+#pragma unroll
+            for (int k = 0; k < K; k++) { hl[k] = 0; hh[k] = 0; }
+            for (int i0 = 0; i0 < m && valid; i0 += 64) {
+                const int i1 = (i0 + 64 < m ? i0 + 64 : m) - 1;
+                double lb = 0.0, ub = 0.0;
+#pragma unroll
+                for (int k = 0; k < K; k++) {
+                    hl[k] = ssl_near(C.T, n, hl[k], dmax(0.0, C.T[i0] - tI[k]));
+                    hh[k] = ssl_near(C.T, n, hh[k] > hl[k] ? hh[k] : hl[k], dmax(0.0, C.T[i1] - tI[k]));
+                    const int kh = hh[k] + 1 < n - 1 ? hh[k] + 1 : n - 1;
+                    lb = lb + dist[k] * (C.g(i0, k) - C.g(kh, k));
+                    ub = ub + dist[k] * (C.g(i1, k) - C.g(hl[k], k));
+                }
+                lb = (lb - env) - 1e-14;
+                ub = (ub + env) + 1e-14;
+                if (ub <= kappa) {        // every knot not above κ
+                    if (i0 > 0 && prev) valid = false;
+                    prev = false;
+                } else if (lb > kappa) {  // every knot above κ
+                    prev = true;
+                } else {
+#pragma unroll
+                    for (int k = 0; k < K; k++) jp[k] = hl[k];
+                    exact(i0, i1 + 1);
+                }
+            }
         }
         if (!valid) { st_o = SBR_HETERO_INVALID | lbits; return; }
     }
