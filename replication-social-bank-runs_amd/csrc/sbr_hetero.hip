@@ -486,8 +486,9 @@ __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const d
                 double lb = 0.0, ub = 0.0;
 #pragma unroll
                 for (int k = 0; k < K; k++) {
-                    hl[k] = ssl_near(C.T, n, hl[k], dmax(0.0, C.T[i0] - tI[k]));
-                    hh[k] = ssl_near(C.T, n, hh[k] > hl[k] ? hh[k] : hl[k], dmax(0.0, C.T[i1] - tI[k]));
+                    // hints: the previous block's last bracket, then this block's first + its width
+                    hl[k] = ssl_near(C.T, n, hh[k], dmax(0.0, C.T[i0] - tI[k]));
+                    hh[k] = ssl_near(C.T, n, hl[k] + (i1 - i0), dmax(0.0, C.T[i1] - tI[k]));
                     const int kh = hh[k] + 1 < n - 1 ? hh[k] + 1 : n - 1;
                     lb = lb + dist[k] * (C.g(i0, k) - C.g(kh, k));
                     ub = ub + dist[k] * (C.g(i1, k) - C.g(hl[k], k));
@@ -518,16 +519,21 @@ __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const d
     int ha[K], hb[K];
 #pragma unroll
     for (int k = 0; k < K; k++) { ha[k] = 0; hb[k] = 0; }
+    // the knot index each hint set was found for: a later search for knot i starts from
+    // hint + (i − that index) (the shifted arguments move with the knots), not from the hint
+    int ia = 0, ib = 0;
     auto eval_range = [&](int i0, int i1) {
         int ja[K], jb[K];
 #pragma unroll
         for (int k = 0; k < K; k++) {
             const double av = (C.T[i0] - xi) + icc[k], bv = (C.T[i0] - xi) + occ[k];
-            ha[k] = ssl_near(C.T, n, ha[k], av > 0 ? av : 0.0);
-            hb[k] = ssl_near(C.T, n, hb[k], bv > 0 ? bv : 0.0);
+            ha[k] = ssl_near(C.T, n, ha[k] + (i0 - ia), av > 0 ? av : 0.0);
+            hb[k] = ssl_near(C.T, n, hb[k] + (i0 - ib), bv > 0 ? bv : 0.0);
             ja[k] = ha[k];
             jb[k] = hb[k];
         }
+        ia = i0;
+        ib = i0;
         for (int i = i0; i < i1; i++) {
             const double ti = C.T[i];
             double cum = 0.0;
@@ -571,20 +577,22 @@ __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const d
                 const double bv = (C.T[i1] - xi) + occ[k];
                 double hi = 0.0;
                 if (bv >= 0) {
-                    hb[k] = ssl_near(C.T, n, hb[k], bv);
+                    hb[k] = ssl_near(C.T, n, hb[k] + (i1 - ib), bv);
                     const double g = C.g(hb[k] + 1 < n - 1 ? hb[k] + 1 : n - 1, k);
                     hi = g > 0.0 ? g : 0.0;
                 }
                 const double av = (C.T[i0] - xi) + icc[k];
                 double lo = 0.0;
                 if (av >= 0) {
-                    ha[k] = ssl_near(C.T, n, ha[k], av);
+                    ha[k] = ssl_near(C.T, n, ha[k] + (i0 - ia), av);
                     lo = C.g(ha[k], k);
                 } else {
                     lo = C.g(0, k) < 0.0 ? C.g(0, k) : 0.0;
                 }
                 sum = sum + dist[k] * (hi - lo);
             }
+            ia = i0;
+            ib = i1;
             return (sum + 1e-14) + env;
         };
         auto end_of = [&](int i0, int w) { return i0 + w < n ? i0 + w : n; };
