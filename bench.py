@@ -264,13 +264,33 @@ def main_hetero(a):
     g_aw = [torch.empty(nb * nu, dtype=torch.float64, device=dev) for _ in range(world)] if gather and rank == 0 \
         else None
 
-    def step():
-        eng.sweep_hetero_dev(K, betas, distw, eta, t_end, u, g.p, g.kappa, g.lam, g.x0, out, stream=stream)
-        if gather:
-            dist.gather(out["aw_max"], g_aw, dst=0)
+    pipe = not a.no_pipeline
+    nbat = max(a.steps, a.warmup, 1) if pipe else 1
+    if pipe:  # one row per batch (= step), every batch the full per-rank grid, recomputed
+        out_b = {k: torch.empty(nbat, nb * nu, dtype=v.dtype, device=dev) for k, v in out.items()}
+        betas_b = betas.unsqueeze(0).repeat(nbat, 1, 1).contiguous()
+        eta_b = eta.unsqueeze(0).repeat(nbat, 1).contiguous()
+        t_end_b = t_end.unsqueeze(0).repeat(nbat, 1).contiguous()
 
-    for _ in range(a.warmup):
-        step()
+    def run_steps(m):
+        """m steps: pipelined, one batch call of m grids (learning of step k+1 overlaps the
+        equilibrium of step k); else one sweep call per step."""
+        if m <= 0:
+            return
+        if pipe:
+            eng.sweep_hetero_batch_dev(K, betas_b[:m], distw, eta_b[:m], t_end_b[:m], u, g.p, g.kappa, g.lam, g.x0,
+                                       {k: v[:m] for k, v in out_b.items()}, stream=stream)
+            for k in range(m):
+                if gather:
+                    dist.gather(out_b["aw_max"][k], g_aw, dst=0)
+            out["status"].copy_(out_b["status"][m - 1])
+        else:
+            for _ in range(m):
+                eng.sweep_hetero_dev(K, betas, distw, eta, t_end, u, g.p, g.kappa, g.lam, g.x0, out, stream=stream)
+                if gather:
+                    dist.gather(out["aw_max"], g_aw, dst=0)
+
+    run_steps(a.warmup)
     torch.cuda.synchronize(dev)
     eng.timing_read(stream)
     eng.timing_enable(True)
@@ -278,8 +298,7 @@ def main_hetero(a):
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
+    run_steps(a.steps)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -300,7 +319,7 @@ def main_hetero(a):
         "data": "synthetic (deterministic config-4 parameter grid; no RNG in the reference)",
         "config": {"workload": f"hetero_K8_{nb}x{nu}_per_gpu (BASELINE config 4)", "n_col_per_gpu": nb,
                    "n_u": nu, "K": K, "eta_bar": 30.0, "p": g.p, "kappa": g.kappa, "lambda": g.lam,
-                   "parallelism": f"column shards x{world}"},
+                   "parallelism": f"column shards x{world}", "pipelined": pipe},
         "kernel_ms_per_step": {"learn_hetero": learn_ms / max(ncalls, 1), "equilibrium_hetero": eq_ms / max(ncalls, 1)},
         "run_fraction": float(((st & sbr.STATUS["SBR_RUN"]) > 0).mean()),
         "stiff_switch_fraction": float(((st & sbr.STATUS["SBR_STIFF_SWITCH"]) > 0).mean()),

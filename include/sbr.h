@@ -164,6 +164,21 @@ int sbr_sweep_hetero_dev(sbr_ctx* ctx, void* stream, int32_t K, const double* be
                          const double* eta, const double* t_end, double x0, const double* u, int64_t n_col,
                          int64_t n_u, double p, double kappa, double lambda, const sbr_opts* opts,
                          sbr_result_soa* out, double* tau_in, double* tau_out);
+
+/*
+ * n_batch heterogeneity grids that share K, dist, n_col, n_u, u and the scalars, swept back
+ * to back and pipelined like sbr_sweep_baseline_batch_dev: the learning of batch k+1
+ * (solve_SInetwork_hetero, latency-bound: one lane per column) runs on a highest-priority
+ * stream into the second of two workspaces while the equilibrium of batch k fills the CUs.
+ * betas is [n_batch × n_col × K], eta/t_end [n_batch × n_col], every out field
+ * [n_batch × n_col × n_u] (iters may be NULL), tau_in/tau_out [n_batch × n_col × n_u × K]
+ * or NULL.  Device pointers, enqueued on `stream`; each batch gives exactly what
+ * sbr_sweep_hetero_dev gives for it.  Use a context from one stream at a time.
+ */
+int sbr_sweep_hetero_batch_dev(sbr_ctx* ctx, void* stream, int64_t n_batch, int32_t K, const double* betas,
+                               const double* dist, const double* eta, const double* t_end, double x0,
+                               const double* u, int64_t n_col, int64_t n_u, double p, double kappa, double lambda,
+                               const sbr_opts* opts, sbr_result_soa* out, double* tau_in, double* tau_out);
 /* One heterogeneity equilibrium with what scripts/2_heterogeneity.jl plots
  * (aggregate_withdrawals_hetero.pdf): learning knots t[n] and group CDFs G[n][K]
  * (solve_SInetwork_hetero), the per-group buffers, and AW_total on the knots

@@ -30,9 +30,11 @@ struct sbr_ctx {
     int last_slot = 0;
     hipStream_t lstream[kLearnSlots] = {};
     hipEvent_t ev_in = nullptr, ev_learned[kLearnSlots] = {}, ev_eq[kLearnSlots] = {};
-    // hetero learning workspace
+    // hetero learning workspace; H2 is the second slot of a pipelined hetero batch
     size_t hs_col = 0, hs_cap = 0, hs_K = 0;
     sbr::HeteroBufs H{};
+    size_t hs2_col = 0, hs2_cap = 0, hs2_K = 0;
+    sbr::HeteroBufs H2{};
     // social-learning workspace (sbr_social.hip): per point 5 knot buffers + n_cmp
     size_t so_pts = 0, so_cap = 0, so_cmp = 0;
     double *so_ws = nullptr, *so_cmpo = nullptr, *so_xi = nullptr;
@@ -124,35 +126,46 @@ int ensure_learn(sbr_ctx* c, size_t n_beta, size_t cap, int slot = 0)
     return SBR_OK;
 }
 
-void free_hetero(sbr_ctx* c)
+void free_hetero_bufs(sbr::HeteroBufs& H, size_t& col, size_t& cap, size_t& K)
 {
-    void* ps[] = {c->H.t, c->H.G, c->H.hr, c->H.hrI, c->H.n_knots, c->H.n_tau, c->H.n_le, c->H.status,
-                  c->H.n_accept, c->H.n_reject};
+    void* ps[] = {H.t, H.G, H.hr, H.hrI, H.n_knots, H.n_tau, H.n_le, H.status, H.n_accept, H.n_reject};
     for (void* p : ps)
         if (p) (void)hipFree(p);
-    c->H = sbr::HeteroBufs{};
-    c->hs_col = c->hs_cap = c->hs_K = 0;
+    H = sbr::HeteroBufs{};
+    col = cap = K = 0;
+}
+
+void free_hetero(sbr_ctx* c)
+{
+    free_hetero_bufs(c->H, c->hs_col, c->hs_cap, c->hs_K);
+    free_hetero_bufs(c->H2, c->hs2_col, c->hs2_cap, c->hs2_K);
+}
+
+int ensure_hetero_bufs(sbr_ctx* c, sbr::HeteroBufs& H, size_t& hcol, size_t& hcap, size_t& hK, size_t n_col,
+                       size_t cap, size_t K)
+{
+    if (n_col <= hcol && cap == hcap && K == hK) return SBR_OK;
+    free_hetero_bufs(H, hcol, hcap, hK);
+    HIP_TRY(c, hipMalloc(&H.t, n_col * cap * 8), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&H.G, n_col * cap * K * 8), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&H.hr, n_col * cap * K * 8), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&H.hrI, n_col * cap * K * 8), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&H.n_knots, n_col * 4), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&H.n_tau, n_col * 4), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&H.n_le, n_col * 4), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&H.status, n_col * 4), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&H.n_accept, n_col * 4), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&H.n_reject, n_col * 4), SBR_ENOMEM);
+    H.cap = (int32_t)cap;
+    hcol = n_col;
+    hcap = cap;
+    hK = K;
+    return SBR_OK;
 }
 
 int ensure_hetero(sbr_ctx* c, size_t n_col, size_t cap, size_t K)
 {
-    if (n_col <= c->hs_col && cap == c->hs_cap && K == c->hs_K) return SBR_OK;
-    free_hetero(c);
-    HIP_TRY(c, hipMalloc(&c->H.t, n_col * cap * 8), SBR_ENOMEM);
-    HIP_TRY(c, hipMalloc(&c->H.G, n_col * cap * K * 8), SBR_ENOMEM);
-    HIP_TRY(c, hipMalloc(&c->H.hr, n_col * cap * K * 8), SBR_ENOMEM);
-    HIP_TRY(c, hipMalloc(&c->H.hrI, n_col * cap * K * 8), SBR_ENOMEM);
-    HIP_TRY(c, hipMalloc(&c->H.n_knots, n_col * 4), SBR_ENOMEM);
-    HIP_TRY(c, hipMalloc(&c->H.n_tau, n_col * 4), SBR_ENOMEM);
-    HIP_TRY(c, hipMalloc(&c->H.n_le, n_col * 4), SBR_ENOMEM);
-    HIP_TRY(c, hipMalloc(&c->H.status, n_col * 4), SBR_ENOMEM);
-    HIP_TRY(c, hipMalloc(&c->H.n_accept, n_col * 4), SBR_ENOMEM);
-    HIP_TRY(c, hipMalloc(&c->H.n_reject, n_col * 4), SBR_ENOMEM);
-    c->H.cap = (int32_t)cap;
-    c->hs_col = n_col;
-    c->hs_cap = cap;
-    c->hs_K = K;
-    return SBR_OK;
+    return ensure_hetero_bufs(c, c->H, c->hs_col, c->hs_cap, c->hs_K, n_col, cap, K);
 }
 
 void free_social(sbr_ctx* c)
@@ -424,6 +437,21 @@ int sbr_sweep_baseline_dev(sbr_ctx* c, void* stream, const double* beta, const d
     return run_baseline(c, s, beta, eta, t_end, x0, u, n_beta, n_u, p, kappa, lambda, o, r, nullptr);
 }
 
+// highest-priority learning streams + events of the pipelined batch sweeps
+int ensure_pipe_streams(sbr_ctx* c)
+{
+    if (c->lstream[0]) return SBR_OK;
+    int lo = 0, hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&lo, &hi); // hi = greatest priority
+    for (int k = 0; k < sbr_ctx::kLearnSlots; k++) {
+        HIP_TRY(c, hipStreamCreateWithPriority(&c->lstream[k], hipStreamNonBlocking, hi), SBR_EDEVICE);
+        HIP_TRY(c, hipEventCreateWithFlags(&c->ev_learned[k], hipEventDisableTiming), SBR_EDEVICE);
+        HIP_TRY(c, hipEventCreateWithFlags(&c->ev_eq[k], hipEventDisableTiming), SBR_EDEVICE);
+    }
+    HIP_TRY(c, hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming), SBR_EDEVICE);
+    return SBR_OK;
+}
+
 int sbr_sweep_baseline_batch_dev(sbr_ctx* c, void* stream, int64_t n_batch, const double* beta, const double* eta,
                                  const double* t_end, double x0, const double* u, int64_t n_beta, int64_t n_u,
                                  double p, double kappa, double lambda, const sbr_opts* opts, sbr_result_soa* out)
@@ -440,15 +468,9 @@ int sbr_sweep_baseline_batch_dev(sbr_ctx* c, void* stream, int64_t n_batch, cons
         int rc = ensure_learn(c, (size_t)n_beta, (size_t)o.knot_capacity, k);
         if (rc) return rc;
     }
-    if (!c->lstream[0]) {
-        int lo = 0, hi = 0;
-        (void)hipDeviceGetStreamPriorityRange(&lo, &hi); // hi = greatest priority
-        for (int k = 0; k < nslot; k++) {
-            HIP_TRY(c, hipStreamCreateWithPriority(&c->lstream[k], hipStreamNonBlocking, hi), SBR_EDEVICE);
-            HIP_TRY(c, hipEventCreateWithFlags(&c->ev_learned[k], hipEventDisableTiming), SBR_EDEVICE);
-            HIP_TRY(c, hipEventCreateWithFlags(&c->ev_eq[k], hipEventDisableTiming), SBR_EDEVICE);
-        }
-        HIP_TRY(c, hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming), SBR_EDEVICE);
+    {
+        int rc = ensure_pipe_streams(c);
+        if (rc) return rc;
     }
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     const size_t np = (size_t)n_beta * (size_t)n_u;
@@ -790,6 +812,57 @@ int sbr_sweep_hetero_dev(sbr_ctx* c, void* stream, int32_t K, const double* beta
     t0 = tstart(c, s);
     HIP_TRY(c, sbr::launch_hetero(K, betas, dist, eta, t_end, u, la, ea, c->H, r, tau_in, tau_out, s, 1), SBR_EDEVICE);
     tend(c, s, 1, t0);
+    return SBR_OK;
+}
+
+int sbr_sweep_hetero_batch_dev(sbr_ctx* c, void* stream, int64_t n_batch, int32_t K, const double* betas,
+                               const double* dist, const double* eta, const double* t_end, double x0, const double* u,
+                               int64_t n_col, int64_t n_u, double p, double kappa, double lambda, const sbr_opts* opts,
+                               sbr_result_soa* out, double* tau_in, double* tau_out)
+{
+    if (!c || !out || !out->xi || !out->aw_max || !out->tol || !out->status || !betas || !dist || !eta || !t_end || !u)
+        return SBR_EARG;
+    if (K != 1 && K != 2 && K != 3 && K != 4 && K != 8) return fail(c, SBR_EARG, "K must be 1, 2, 3, 4 or 8");
+    if (n_batch <= 0 || n_col <= 0 || n_u <= 0 || n_col > (1 << 30) || n_u > (1 << 30))
+        return fail(c, SBR_EARG, "grid size");
+    if (!scalars_valid(x0, p, kappa, lambda)) return fail(c, SBR_EARG, "ArgumentError: x0/p/kappa/lambda");
+    if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
+    sbr_opts o = resolve(opts);
+    const size_t cap = (size_t)o.knot_capacity;
+    int rc = ensure_hetero(c, (size_t)n_col, cap, (size_t)K);
+    if (!rc && n_batch > 1) rc = ensure_hetero_bufs(c, c->H2, c->hs2_col, c->hs2_cap, c->hs2_K, (size_t)n_col, cap, (size_t)K);
+    if (!rc) rc = ensure_pipe_streams(c);
+    if (rc) return rc;
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, p, lambda, o.ode_maxiters, (int32_t)n_col, 0, 0};
+    sbr::HeteroEqArgs ea{kappa, 1e-12, (int32_t)n_u, o.hetero_max_iters, c->lds_cap * 3,
+                         (o.flags & SBR_FLAG_EXHAUSTIVE) ? 1 : 0, (o.flags >> 8) & 7, nullptr};
+    const size_t np = (size_t)n_col * (size_t)n_u;
+    HIP_TRY(c, hipEventRecord(c->ev_in, s), SBR_EDEVICE);
+    for (int k = 0; k < 2; k++) HIP_TRY(c, hipStreamWaitEvent(c->lstream[k], c->ev_in, 0), SBR_EDEVICE);
+    for (int64_t k = 0; k < n_batch; k++) {
+        const int slot = (int)(k & 1);
+        hipStream_t ls = c->lstream[slot];
+        const sbr::HeteroBufs& H = slot ? c->H2 : c->H;
+        const double* bk = betas + k * n_col * K;
+        const double* ek = eta + k * n_col;
+        const double* tk = t_end + k * n_col;
+        // the slot's previous reader (equilibrium of batch k - 2) must be done
+        if (k >= 2) HIP_TRY(c, hipStreamWaitEvent(ls, c->ev_eq[slot], 0), SBR_EDEVICE);
+        hipEvent_t t0 = tstart(c, ls);
+        sbr::ResultSoA r{out->xi + k * np, nullptr, nullptr, out->aw_max + k * np, out->tol + k * np,
+                         out->status + k * np, out->iters ? out->iters + k * np : nullptr};
+        double* ti = tau_in ? tau_in + k * np * K : nullptr;
+        double* to = tau_out ? tau_out + k * np * K : nullptr;
+        HIP_TRY(c, sbr::launch_hetero(K, bk, dist, ek, tk, u, la, ea, H, r, ti, to, ls, 0), SBR_EDEVICE);
+        tend(c, ls, 0, t0);
+        HIP_TRY(c, hipEventRecord(c->ev_learned[slot], ls), SBR_EDEVICE);
+        HIP_TRY(c, hipStreamWaitEvent(s, c->ev_learned[slot], 0), SBR_EDEVICE);
+        t0 = tstart(c, s);
+        HIP_TRY(c, sbr::launch_hetero(K, bk, dist, ek, tk, u, la, ea, H, r, ti, to, s, 1), SBR_EDEVICE);
+        tend(c, s, 1, t0);
+        HIP_TRY(c, hipEventRecord(c->ev_eq[slot], s), SBR_EDEVICE);
+    }
     return SBR_OK;
 }
 

@@ -93,6 +93,8 @@ _SIGS = {
     "sbr_sweep_hetero": (ctypes.c_int, [_P, _I32, _P, _P, _P, _P, _D, _P, _I64, _I64, _D, _D, _D, _P, _P, _P, _P]),
     "sbr_sweep_hetero_dev": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P, _P, _D, _P, _I64, _I64, _D, _D, _D, _P, _P, _P,
                                             _P]),
+    "sbr_sweep_hetero_batch_dev": (ctypes.c_int, [_P, _P, _I64, _I32, _P, _P, _P, _P, _D, _P, _I64, _I64, _D, _D,
+                                                  _D, _P, _P, _P, _P]),
     "sbr_sweep_social": (ctypes.c_int, [_P, _P, _P, _D, _P, _I64, _I64, _D, _D, _D, _P, _I32, _D, _I32, _P, _P, _P,
                                         _P]),
     "sbr_sweep_social_dev": (ctypes.c_int, [_P, _P, _P, _P, _D, _P, _I64, _I64, _D, _D, _D, _P, _I32, _D, _I32, _P,

@@ -191,6 +191,24 @@ class Engine:
                                           ctypes.byref(opts), ctypes.byref(soa), None, None)
         check(rc, self._ctx, "sbr_sweep_hetero_dev")
 
+    def sweep_hetero_batch_dev(self, K, betas, dist, eta, t_end, u, p, kappa, lam, x0, out: dict,
+                               stream: int | None = None, knot_capacity: int = 16384, flags: int = 0):
+        """Pipelined hetero sweep of several grids on torch tensors (see
+        sbr_sweep_hetero_batch_dev): ``betas`` [n_batch, n_col, K], ``eta``/``t_end``
+        [n_batch, n_col], every ``out`` tensor [n_batch, n_col * n_u]."""
+        nbat, n_col = eta.shape
+        nu = u.numel()
+        if tuple(betas.shape) != (nbat, n_col, K) or tuple(t_end.shape) != (nbat, n_col):
+            raise ArgumentError("betas must be [n_batch, n_col, K] and t_end [n_batch, n_col]")
+        soa = _lib.ResultSoA(out["xi"].data_ptr(), None, None, out["aw_max"].data_ptr(), out["tol"].data_ptr(),
+                             out["status"].data_ptr(), out["iters"].data_ptr() if out.get("iters") is not None
+                             else None)
+        opts = _lib.default_opts(knot_capacity=knot_capacity, flags=flags)
+        rc = self._L.sbr_sweep_hetero_batch_dev(self._ctx, stream, nbat, K, betas.data_ptr(), dist.data_ptr(),
+                                                eta.data_ptr(), t_end.data_ptr(), x0, u.data_ptr(), n_col, nu, p,
+                                                kappa, lam, ctypes.byref(opts), ctypes.byref(soa), None, None)
+        check(rc, self._ctx, "sbr_sweep_hetero_batch_dev")
+
     def sweep_social(self, beta, eta, u, p, kappa, lam, cmp=None, x0=1e-4, tol=1e-4, max_iter=500,
                      knot_capacity: int = 0, workspace_bytes: int | None = None) -> dict:
         """Social-learning sweep (social_learning_solver.jl:63-263) over β columns × u.

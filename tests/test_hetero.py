@@ -128,3 +128,32 @@ def test_hetero_reference_call_surface(engine, oracle):
                                   g.kappa, g.lam)
     assert r.status == o["status"] and r.xi == o["xi"] and r.AW_max == o["aw_max"]
     assert np.array_equal(r.AW_total, o["aw_total"])
+
+
+@pytest.mark.gpu
+def test_hetero_pipelined_batches_equal_single_sweeps(engine):
+    """sbr_sweep_hetero_batch_dev (learning of batch k+1 on a second stream into the other
+    workspace while batch k's equilibrium runs) returns for every batch exactly what
+    sbr_sweep_hetero returns for that grid."""
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda", 0)
+    full = sbr.hetero_config4(96, 40, 8)
+    subs = [full.subset(np.arange(k, 96, 3)) for k in range(3)]  # three 32-column grids
+    nbat, nc, nu, K = len(subs), 32, len(full.u), full.K
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    out = {f: torch.empty(nbat, nc * nu, dtype=torch.float64, device=dev) for f in ("xi", "aw_max", "tol")}
+    out["status"] = torch.empty(nbat, nc * nu, dtype=torch.int32, device=dev)
+    out["iters"] = torch.empty(nbat, nc * nu, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    engine.sweep_hetero_batch_dev(K, t(np.stack([g.betas for g in subs])), t(full.dist),
+                                  t(np.stack([g.eta for g in subs])), t(np.stack([g.t_end for g in subs])),
+                                  t(full.u), full.p, full.kappa, full.lam, full.x0, out, stream=stream)
+    torch.cuda.synchronize(dev)
+    for k, g in enumerate(subs):
+        ref = engine.sweep_hetero(g.betas, g.dist, g.eta, g.t_end, g.u, g.p, g.kappa, g.lam, g.x0, with_groups=False)
+        for f in ("xi", "aw_max", "tol"):
+            a = out[f][k].cpu().numpy().reshape(nc, nu)
+            assert np.array_equal(a, ref[f].reshape(nc, nu), equal_nan=True), (k, f)
+        assert np.array_equal(out["status"][k].cpu().numpy().view(np.uint32).reshape(nc, nu),
+                              ref["status"].reshape(nc, nu)), k
+        assert np.array_equal(out["iters"][k].cpu().numpy().reshape(nc, nu), ref["iters"].reshape(nc, nu)), k
