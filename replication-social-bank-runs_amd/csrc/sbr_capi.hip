@@ -437,6 +437,13 @@ int sbr_sweep_baseline_dev(sbr_ctx* c, void* stream, const double* beta, const d
     return run_baseline(c, s, beta, eta, t_end, x0, u, n_beta, n_u, p, kappa, lambda, o, r, nullptr);
 }
 
+// hetero equilibrium LDS slab (doubles): knot times + per-group HR summaries of one column,
+// capped so that SBR_HET_MINW workgroups share a CU (config 4: n <= 4.8k knots)
+#ifndef SBR_HET_LDS
+#define SBR_HET_LDS 7168
+#endif
+static int het_lds(const sbr_ctx* c) { return c->lds_cap * 3 < SBR_HET_LDS ? c->lds_cap * 3 : SBR_HET_LDS; }
+
 // highest-priority learning streams + events of the pipelined batch sweeps
 int ensure_pipe_streams(sbr_ctx* c)
 {
@@ -803,7 +810,7 @@ int sbr_sweep_hetero_dev(sbr_ctx* c, void* stream, int32_t K, const double* beta
     if (rc) return rc;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, p, lambda, o.ode_maxiters, (int32_t)n_col, 0, 0};
-    sbr::HeteroEqArgs ea{kappa, 1e-12, (int32_t)n_u, o.hetero_max_iters, c->lds_cap * 3,
+    sbr::HeteroEqArgs ea{kappa, 1e-12, (int32_t)n_u, o.hetero_max_iters, het_lds(c),
                          (o.flags & SBR_FLAG_EXHAUSTIVE) ? 1 : 0, (o.flags >> 8) & 7, c->het_aw_path};
     sbr::ResultSoA r{out->xi, nullptr, nullptr, out->aw_max, out->tol, out->status, out->iters};
     hipEvent_t t0 = tstart(c, s);
@@ -835,7 +842,7 @@ int sbr_sweep_hetero_batch_dev(sbr_ctx* c, void* stream, int64_t n_batch, int32_
     if (rc) return rc;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, p, lambda, o.ode_maxiters, (int32_t)n_col, 0, 0};
-    sbr::HeteroEqArgs ea{kappa, 1e-12, (int32_t)n_u, o.hetero_max_iters, c->lds_cap * 3,
+    sbr::HeteroEqArgs ea{kappa, 1e-12, (int32_t)n_u, o.hetero_max_iters, het_lds(c),
                          (o.flags & SBR_FLAG_EXHAUSTIVE) ? 1 : 0, (o.flags >> 8) & 7, nullptr};
     const size_t np = (size_t)n_col * (size_t)n_u;
     HIP_TRY(c, hipEventRecord(c->ev_in, s), SBR_EDEVICE);

@@ -639,7 +639,10 @@ __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const d
 }
 
 template <int K, int BLOCK>
-__global__ __launch_bounds__(BLOCK) void equilibrium_hetero_kernel(HeteroBufs L, const double* __restrict__ dist,
+#ifndef SBR_HET_MINW
+#define SBR_HET_MINW 2 // waves per SIMD: two 4-wave workgroups per CU (LDS slab: SBR_HET_LDS in sbr_capi.hip)
+#endif
+__global__ __launch_bounds__(BLOCK, SBR_HET_MINW) void equilibrium_hetero_kernel(HeteroBufs L, const double* __restrict__ dist,
                                                                    const double* __restrict__ eta,
                                                                    const double* __restrict__ t_end,
                                                                    const double* __restrict__ u, HeteroEqArgs a,
