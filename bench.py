@@ -11,7 +11,9 @@ timed steps are K grids handed to sbr_sweep_baseline_batch_dev, which pipelines
 them: the learning stage of step k+1 (latency-bound, 32 waves) runs on a second,
 highest-priority stream while the equilibrium stage of step k fills the CUs.
 Every step's learning and equilibrium run in full inside the timed region
-(--no-pipeline: one serial sweep call per step).
+(--no-pipeline: one serial sweep call per step); the first step's learning (≈4 ms)
+cannot overlap anything, so the default 50 steps amortise that pipeline fill to
+≈0.08 ms per step (20 steps: ≈0.2 ms).
 
 N GPUs (torchrun, one process per GPU, RCCL): weak scaling — rank r owns the β
 columns r, r+N, r+2N, … of a 2048·N-column grid (same u axis), so per-GPU work is
@@ -53,7 +55,7 @@ F_HAZARD_KNOT = 3 + F_EXP + 1 + 4 + 2 + 3  # g, exp, e, trapezoid, numerator, HR
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--n", type=int, default=2048, help="β columns per GPU and u rows")
     ap.add_argument("--no-gather", action="store_true")

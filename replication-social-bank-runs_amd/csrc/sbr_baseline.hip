@@ -175,7 +175,10 @@ __global__ __launch_bounds__(64) void learn_logistic_kernel(const double* __rest
 constexpr int HZ_BLOCK = 256;
 constexpr int HZ_CHUNK = 16;
 constexpr int EQ_TILE = 4096;  // u values per equilibrium block (one block per β column up to this)
-constexpr int kAwWin = 6;      // 8-blocks each side of the predicted AW peak evaluated first
+#ifndef SBR_AW_WIN
+#define SBR_AW_WIN 6
+#endif
+constexpr int kAwWin = SBR_AW_WIN; // 8-blocks each side of the predicted AW peak evaluated first
 
 __global__ __launch_bounds__(HZ_BLOCK) void hazard_kernel(const double* __restrict__ beta,
                                                           const double* __restrict__ eta, LearnArgs a, LearnBufs L)
