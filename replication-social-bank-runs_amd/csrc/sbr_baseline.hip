@@ -952,11 +952,13 @@ __global__ __launch_bounds__(BLOCK, INTEREST ? 1 : SBR_EQ_MINW) void equilibrium
                 }
                 s_thalf = sT[lo] + (0.5 - sG[lo]) * (sT[hi] - sT[lo]) / (sG[hi] - sG[lo]);
             }
+            // the tables are read only when G is not monotone (Summ::mono): skip the serial scans
+            if (s_nonmono)
             for (int g = 1; g < nbg; g++) {
                 const double a0 = pmc[g - 1], b0 = pmc[g];
                 pmc[g] = (a0 != a0 || b0 != b0) ? NAN : (a0 > b0 ? a0 : b0);
             }
-        } else if (threadIdx.x == (BLOCK > 64 ? 64 : 1)) {
+        } else if (threadIdx.x == (BLOCK > 64 ? 64 : 1) && s_nonmono) {
             for (int g = nbg - 2; g >= 0; g--) {
                 const double a0 = smc[g + 1], b0 = smc[g];
                 smc[g] = (a0 != a0 || b0 != b0) ? NAN : (a0 < b0 ? a0 : b0);
