@@ -909,19 +909,34 @@ __global__ __launch_bounds__(BLOCK, INTEREST ? 1 : SBR_EQ_MINW) void equilibrium
     if (threadIdx.x == 0) { s_nonmono = 0; s_thalf = NAN; }
     if (fits && !a.exhaustive) {
         const int nbh = (ntau + 63) >> 6, nbg = (n + 7) >> 3;
-        for (int bk = threadIdx.x; bk < nbh + nbg; bk += BLOCK) {
-            if (bk < nbh) {
+        // HR summaries: 8 lanes per 64-entry block, 8 independent loads each (HR is read from
+        // L2), combined across the 8 lanes; then one lane per 8-knot G block
+        const int nq = nbh << 3;
+        for (int bk = threadIdx.x; bk < nq + nbg; bk += BLOCK) {
+            if (bk < nq) {
                 double mx = -INFINITY, mn = INFINITY;
-                const int e = (bk << 6) + 64 < ntau ? (bk << 6) + 64 : ntau;
-                for (int i = bk << 6; i < e; i++) {
-                    const double h = cH[i];
-                    if (h > mx) mx = h;                         // NaN never > u: ignore it
-                    mn = (h != h) ? -INFINITY : (h < mn ? h : mn); // NaN is "not above"
+                const int i0 = bk << 3;
+                double h[8];
+#pragma unroll
+                for (int k = 0; k < 8; k++) h[k] = i0 + k < ntau ? cH[i0 + k] : -INFINITY;
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    if (i0 + k >= ntau) continue;
+                    if (h[k] > mx) mx = h[k];                                 // NaN never > u: ignore it
+                    mn = (h[k] != h[k]) ? -INFINITY : (h[k] < mn ? h[k] : mn); // NaN is "not above"
                 }
-                hmax[bk] = mx;
-                hmin[bk] = mn;
+#pragma unroll
+                for (int off = 1; off < 8; off <<= 1) { // the 8 lanes of a block are aligned in one wave
+                    const double omx = __shfl_xor(mx, off, 8), omn = __shfl_xor(mn, off, 8);
+                    mx = omx > mx ? omx : mx;
+                    mn = omn < mn ? omn : mn;
+                }
+                if ((bk & 7) == 0) {
+                    hmax[bk >> 3] = mx;
+                    hmin[bk >> 3] = mn;
+                }
             } else {
-                const int g = bk - nbh;
+                const int g = bk - nq;
                 double mx = -INFINITY, mn = INFINITY;
                 const int e = (g << 3) + 8 < n ? (g << 3) + 8 : n;
                 double prev = g > 0 ? sG[(g << 3) - 1] : -INFINITY;
