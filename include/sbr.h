@@ -101,7 +101,8 @@ int sbr_sweep_baseline(sbr_ctx* ctx, const double* beta, const double* eta, cons
                        const sbr_opts* opts, sbr_result_soa* out);
 
 /* Same on device pointers (beta/eta/t_end/u and every out field in HBM),
- * enqueued on `stream` (hipStream_t); no host synchronisation. */
+ * enqueued on `stream` (hipStream_t; NULL is HIP's null stream, i.e. torch's default
+ * stream, never a private one); no host synchronisation. */
 int sbr_sweep_baseline_dev(sbr_ctx* ctx, void* stream, const double* beta, const double* eta,
                            const double* t_end, double x0, const double* u, int64_t n_beta, int64_t n_u, double p,
                            double kappa, double lambda, const sbr_opts* opts, sbr_result_soa* out);
@@ -286,7 +287,7 @@ void sbr_apply_early_exit(int64_t n_beta, int64_t n_u, int32_t threshold, sbr_re
 
 /* Kernel timing with HIP events recorded on the launch stream around the
  * learning and equilibrium kernels of every baseline sweep call while
- * enabled; sbr_timing_read synchronises `stream` (NULL = context stream),
+ * enabled; sbr_timing_read synchronises `stream` (NULL = the HIP null stream),
  * returns the summed milliseconds per kernel and the number of calls, and
  * resets the accumulators. */
 int sbr_timing_enable(sbr_ctx* ctx, int on);

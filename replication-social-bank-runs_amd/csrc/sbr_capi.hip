@@ -16,6 +16,10 @@
 #include "../../include/sbr_detmath.h"
 #include "sbr_kernels.h"
 
+#ifndef SBR_EQ_STREAMS
+#define SBR_EQ_STREAMS 1 // equilibrium streams of a pipelined baseline batch (1 or 2)
+#endif
+
 struct sbr_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -30,6 +34,12 @@ struct sbr_ctx {
     int last_slot = 0;
     hipStream_t lstream[kLearnSlots] = {};
     hipEvent_t ev_in = nullptr, ev_learned[kLearnSlots] = {}, ev_eq[kLearnSlots] = {};
+    // fork/join fences between HIP's null stream and `stream` (NullFence)
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    // second equilibrium stream of a pipelined baseline batch (odd batches): the next
+    // batch's workgroups fill the CUs the previous one's tail leaves idle
+    hipStream_t estream2 = nullptr;
+    hipEvent_t ev_e2 = nullptr;
     // hetero learning workspace; H2 is the second slot of a pipelined hetero batch
     size_t hs_col = 0, hs_cap = 0, hs_K = 0;
     sbr::HeteroBufs H{};
@@ -93,6 +103,30 @@ int fail(sbr_ctx* c, int code, const char* what, hipError_t e = hipSuccess)
         hipError_t _e = (expr);                                   \
         if (_e != hipSuccess) return fail((ctx), (code), #expr, _e); \
     } while (0)
+
+// A NULL stream argument of the *_dev entry points names HIP's null stream (torch's
+// default stream).  The work itself runs on the context's non-blocking stream, fenced to
+// the null stream on both sides: it starts after, and null-stream work enqueued after the
+// call starts after it, without putting the kernels on the null stream's queue.
+struct NullFence {
+    sbr_ctx* c;
+    bool on;
+    NullFence(sbr_ctx* c_, void* stream) : c(c_), on(stream == nullptr)
+    {
+        if (on) {
+            (void)hipEventRecord(c->ev_fork, nullptr);
+            (void)hipStreamWaitEvent(c->stream, c->ev_fork, 0);
+        }
+    }
+    ~NullFence()
+    {
+        if (on) {
+            (void)hipEventRecord(c->ev_join, c->stream);
+            (void)hipStreamWaitEvent(nullptr, c->ev_join, 0);
+        }
+    }
+    hipStream_t get(void* stream) const { return on ? c->stream : (hipStream_t)stream; }
+};
 
 void free_learn(sbr_ctx* c, int slot)
 {
@@ -375,7 +409,9 @@ int sbr_init(int device, sbr_ctx** out)
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0 || device < 0 || device >= n) return SBR_EDEVICE;
     sbr_ctx* c = new sbr_ctx();
     c->device = device;
-    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
         delete c;
         return SBR_EDEVICE;
     }
@@ -408,6 +444,10 @@ int sbr_free(sbr_ctx* c)
     if (c->so_args_dev) (void)hipFree(c->so_args_dev);
     if (c->so_args_host) (void)hipHostFree(c->so_args_host);
     if (c->ev_in) (void)hipEventDestroy(c->ev_in);
+    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    if (c->estream2) { (void)hipStreamSynchronize(c->estream2); (void)hipStreamDestroy(c->estream2); }
+    if (c->ev_e2) (void)hipEventDestroy(c->ev_e2);
+    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
     for (int k = 0; k < sbr_ctx::kLearnSlots; k++) {
         if (c->ev_learned[k]) (void)hipEventDestroy(c->ev_learned[k]);
         if (c->ev_eq[k]) (void)hipEventDestroy(c->ev_eq[k]);
@@ -433,7 +473,8 @@ int sbr_sweep_baseline_dev(sbr_ctx* c, void* stream, const double* beta, const d
     if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
     sbr_opts o = resolve(opts);
     sbr::ResultSoA r{out->xi, out->tau_in_unc, out->tau_out_unc, out->aw_max, out->tol, out->status, out->iters};
-    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    NullFence fence(c, stream); // NULL = HIP null stream (torch default stream)
+    hipStream_t s = fence.get(stream);
     return run_baseline(c, s, beta, eta, t_end, x0, u, n_beta, n_u, p, kappa, lambda, o, r, nullptr);
 }
 
@@ -456,6 +497,8 @@ int ensure_pipe_streams(sbr_ctx* c)
         HIP_TRY(c, hipEventCreateWithFlags(&c->ev_eq[k], hipEventDisableTiming), SBR_EDEVICE);
     }
     HIP_TRY(c, hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming), SBR_EDEVICE);
+    HIP_TRY(c, hipStreamCreateWithFlags(&c->estream2, hipStreamNonBlocking), SBR_EDEVICE);
+    HIP_TRY(c, hipEventCreateWithFlags(&c->ev_e2, hipEventDisableTiming), SBR_EDEVICE);
     return SBR_OK;
 }
 
@@ -479,14 +522,18 @@ int sbr_sweep_baseline_batch_dev(sbr_ctx* c, void* stream, int64_t n_batch, cons
         int rc = ensure_pipe_streams(c);
         if (rc) return rc;
     }
-    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    NullFence fence(c, stream); // NULL = HIP null stream (torch default stream)
+    hipStream_t s = fence.get(stream);
     const size_t np = (size_t)n_beta * (size_t)n_u;
     sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, p, lambda, o.ode_maxiters, (int32_t)n_beta, 1, 0};
     // inputs are ready once prior work on the caller's stream is
     HIP_TRY(c, hipEventRecord(c->ev_in, s), SBR_EDEVICE);
     for (int k = 0; k < nslot; k++) HIP_TRY(c, hipStreamWaitEvent(c->lstream[k], c->ev_in, 0), SBR_EDEVICE);
+    const bool two = SBR_EQ_STREAMS > 1 && n_batch > 1;
+    if (two) HIP_TRY(c, hipStreamWaitEvent(c->estream2, c->ev_in, 0), SBR_EDEVICE);
     for (int64_t k = 0; k < n_batch; k++) {
         const int slot = (int)(k % nslot);
+        hipStream_t es = (two && (k & 1)) ? c->estream2 : s; // equilibrium stream of batch k
         hipStream_t ls = c->lstream[slot];
         const double* bk = beta + k * n_beta;
         const double* ek = eta + k * n_beta;
@@ -497,7 +544,7 @@ int sbr_sweep_baseline_batch_dev(sbr_ctx* c, void* stream, int64_t n_batch, cons
         HIP_TRY(c, sbr::launch_learn_logistic(bk, ek, tk, la, c->LW[slot], ls), SBR_EDEVICE);
         tend(c, ls, 0, t0);
         HIP_TRY(c, hipEventRecord(c->ev_learned[slot], ls), SBR_EDEVICE);
-        HIP_TRY(c, hipStreamWaitEvent(s, c->ev_learned[slot], 0), SBR_EDEVICE);
+        HIP_TRY(c, hipStreamWaitEvent(es, c->ev_learned[slot], 0), SBR_EDEVICE);
         sbr::ResultSoA r{out->xi ? out->xi + k * np : nullptr,
                          out->tau_in_unc ? out->tau_in_unc + k * np : nullptr,
                          out->tau_out_unc ? out->tau_out_unc + k * np : nullptr,
@@ -505,10 +552,14 @@ int sbr_sweep_baseline_batch_dev(sbr_ctx* c, void* stream, int64_t n_batch, cons
                          out->tol ? out->tol + k * np : nullptr,
                          out->status ? out->status + k * np : nullptr,
                          out->iters ? out->iters + k * np : nullptr};
-        int rc = launch_eq(c, s, c->LW[slot], ek, tk, u, n_beta, n_u, kappa, o, r, nullptr);
+        int rc = launch_eq(c, es, c->LW[slot], ek, tk, u, n_beta, n_u, kappa, o, r, nullptr);
         if (rc) return rc;
-        HIP_TRY(c, hipEventRecord(c->ev_eq[slot], s), SBR_EDEVICE);
+        HIP_TRY(c, hipEventRecord(c->ev_eq[slot], es), SBR_EDEVICE);
         c->last_slot = slot;
+    }
+    if (two) { // results complete for work enqueued on `stream` afterwards
+        HIP_TRY(c, hipEventRecord(c->ev_e2, c->estream2), SBR_EDEVICE);
+        HIP_TRY(c, hipStreamWaitEvent(s, c->ev_e2, 0), SBR_EDEVICE);
     }
     return SBR_OK;
 }
@@ -571,7 +622,8 @@ int sbr_sweep_interest_dev(sbr_ctx* c, void* stream, const double* beta, const d
     if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
     sbr_opts o = resolve(opts);
     sbr::ResultSoA rs{out->xi, out->tau_in_unc, out->tau_out_unc, out->aw_max, out->tol, out->status, out->iters};
-    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    NullFence fence(c, stream); // NULL = HIP null stream (torch default stream)
+    hipStream_t s = fence.get(stream);
     return run_interest(c, s, beta, eta, t_end, x0, u, n_beta, n_u, p, kappa, lambda, r, delta, o, rs, rk_steps);
 }
 
@@ -761,12 +813,14 @@ int sbr_timing_enable(sbr_ctx* c, int on)
 int sbr_timing_read(sbr_ctx* c, void* stream, double* learn_ms, double* eq_ms, int32_t* n_calls)
 {
     if (!c) return SBR_EARG;
-    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    hipStream_t s = (hipStream_t)stream; // NULL = HIP null stream
     HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
+    HIP_TRY(c, hipStreamSynchronize(c->stream), SBR_EDEVICE); // host-pointer sweeps time on it
     double a = 0.0, b = 0.0;
     int32_t n = 0;
     for (hipStream_t ls : c->lstream)
         if (ls) HIP_TRY(c, hipStreamSynchronize(ls), SBR_EDEVICE);
+    if (c->estream2) HIP_TRY(c, hipStreamSynchronize(c->estream2), SBR_EDEVICE);
     for (const auto& r : c->trec) {
         float t = 0.f;
         HIP_TRY(c, hipEventElapsedTime(&t, r.a, r.b), SBR_EDEVICE);
@@ -808,7 +862,8 @@ int sbr_sweep_hetero_dev(sbr_ctx* c, void* stream, int32_t K, const double* beta
     sbr_opts o = resolve(opts);
     int rc = ensure_hetero(c, (size_t)n_col, (size_t)o.knot_capacity, (size_t)K);
     if (rc) return rc;
-    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    NullFence fence(c, stream); // NULL = HIP null stream (torch default stream)
+    hipStream_t s = fence.get(stream);
     sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, p, lambda, o.ode_maxiters, (int32_t)n_col, 0, 0};
     sbr::HeteroEqArgs ea{kappa, 1e-12, (int32_t)n_u, o.hetero_max_iters, het_lds(c),
                          (o.flags & SBR_FLAG_EXHAUSTIVE) ? 1 : 0, (o.flags >> 8) & 7, c->het_aw_path};
@@ -840,7 +895,8 @@ int sbr_sweep_hetero_batch_dev(sbr_ctx* c, void* stream, int64_t n_batch, int32_
     if (!rc && n_batch > 1) rc = ensure_hetero_bufs(c, c->H2, c->hs2_col, c->hs2_cap, c->hs2_K, (size_t)n_col, cap, (size_t)K);
     if (!rc) rc = ensure_pipe_streams(c);
     if (rc) return rc;
-    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    NullFence fence(c, stream); // NULL = HIP null stream (torch default stream)
+    hipStream_t s = fence.get(stream);
     sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, p, lambda, o.ode_maxiters, (int32_t)n_col, 0, 0};
     sbr::HeteroEqArgs ea{kappa, 1e-12, (int32_t)n_u, o.hetero_max_iters, het_lds(c),
                          (o.flags & SBR_FLAG_EXHAUSTIVE) ? 1 : 0, (o.flags >> 8) & 7, nullptr};
@@ -1214,7 +1270,8 @@ int sbr_sweep_social_dev(sbr_ctx* c, void* stream, const double* beta, const dou
     if (rc) return rc;
     if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
     sbr_opts o = resolve(opts);
-    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    NullFence fence(c, stream); // NULL = HIP null stream (torch default stream)
+    hipStream_t s = fence.get(stream);
     return run_social(c, s, beta, eta, x0, u, n_beta, n_u, p, kappa, lambda, cmp_grid, n_cmp, tol, max_iter, o, out,
                       fp_iters, rk_steps, 0);
 }

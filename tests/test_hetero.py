@@ -157,3 +157,29 @@ def test_hetero_pipelined_batches_equal_single_sweeps(engine):
         assert np.array_equal(out["status"][k].cpu().numpy().view(np.uint32).reshape(nc, nu),
                               ref["status"].reshape(nc, nu)), k
         assert np.array_equal(out["iters"][k].cpu().numpy().reshape(nc, nu), ref["iters"].reshape(nc, nu)), k
+
+
+@pytest.mark.gpu
+def test_hetero_batch_ordered_on_torch_default_stream(engine):
+    """A batch enqueued on torch's default stream (handle 0, HIP's null stream) is complete
+    for torch work enqueued on that stream afterwards, with no host synchronisation in
+    between (bench.py copies the last batch's status this way)."""
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda", 0)
+    g = sbr.hetero_config4(64, 48, 8)
+    nbat, nc, nu, K = 2, 64, len(g.u), g.K
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    out = {f: torch.zeros(nbat, nc * nu, dtype=torch.float64, device=dev) for f in ("xi", "aw_max", "tol")}
+    out["status"] = torch.zeros(nbat, nc * nu, dtype=torch.int32, device=dev)
+    out["iters"] = torch.zeros(nbat, nc * nu, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    assert stream == 0
+    rep = lambda a: t(np.stack([a] * nbat))
+    engine.sweep_hetero_batch_dev(K, rep(g.betas), t(g.dist), rep(g.eta), rep(g.t_end), t(g.u), g.p, g.kappa,
+                                  g.lam, g.x0, out, stream=stream)
+    st = out["status"][nbat - 1].clone()  # enqueued behind the batch on the same stream
+    aw = out["aw_max"][nbat - 1].clone()
+    torch.cuda.synchronize(dev)
+    ref = engine.sweep_hetero(g.betas, g.dist, g.eta, g.t_end, g.u, g.p, g.kappa, g.lam, g.x0, with_groups=False)
+    assert np.array_equal(st.cpu().numpy().view(np.uint32), ref["status"].ravel())
+    assert np.array_equal(aw.cpu().numpy(), ref["aw_max"].ravel(), equal_nan=True)
