@@ -16,10 +16,6 @@
 #include "../../include/sbr_detmath.h"
 #include "sbr_kernels.h"
 
-#ifndef SBR_EQ_STREAMS
-#define SBR_EQ_STREAMS 1 // equilibrium streams of a pipelined baseline batch (1 or 2)
-#endif
-
 struct sbr_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -36,10 +32,6 @@ struct sbr_ctx {
     hipEvent_t ev_in = nullptr, ev_learned[kLearnSlots] = {}, ev_eq[kLearnSlots] = {};
     // fork/join fences between HIP's null stream and `stream` (NullFence)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    // second equilibrium stream of a pipelined baseline batch (odd batches): the next
-    // batch's workgroups fill the CUs the previous one's tail leaves idle
-    hipStream_t estream2 = nullptr;
-    hipEvent_t ev_e2 = nullptr;
     // hetero learning workspace; H2 is the second slot of a pipelined hetero batch
     size_t hs_col = 0, hs_cap = 0, hs_K = 0;
     sbr::HeteroBufs H{};
@@ -445,8 +437,6 @@ int sbr_free(sbr_ctx* c)
     if (c->so_args_host) (void)hipHostFree(c->so_args_host);
     if (c->ev_in) (void)hipEventDestroy(c->ev_in);
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
-    if (c->estream2) { (void)hipStreamSynchronize(c->estream2); (void)hipStreamDestroy(c->estream2); }
-    if (c->ev_e2) (void)hipEventDestroy(c->ev_e2);
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
     for (int k = 0; k < sbr_ctx::kLearnSlots; k++) {
         if (c->ev_learned[k]) (void)hipEventDestroy(c->ev_learned[k]);
@@ -497,8 +487,6 @@ int ensure_pipe_streams(sbr_ctx* c)
         HIP_TRY(c, hipEventCreateWithFlags(&c->ev_eq[k], hipEventDisableTiming), SBR_EDEVICE);
     }
     HIP_TRY(c, hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming), SBR_EDEVICE);
-    HIP_TRY(c, hipStreamCreateWithFlags(&c->estream2, hipStreamNonBlocking), SBR_EDEVICE);
-    HIP_TRY(c, hipEventCreateWithFlags(&c->ev_e2, hipEventDisableTiming), SBR_EDEVICE);
     return SBR_OK;
 }
 
@@ -529,11 +517,9 @@ int sbr_sweep_baseline_batch_dev(sbr_ctx* c, void* stream, int64_t n_batch, cons
     // inputs are ready once prior work on the caller's stream is
     HIP_TRY(c, hipEventRecord(c->ev_in, s), SBR_EDEVICE);
     for (int k = 0; k < nslot; k++) HIP_TRY(c, hipStreamWaitEvent(c->lstream[k], c->ev_in, 0), SBR_EDEVICE);
-    const bool two = SBR_EQ_STREAMS > 1 && n_batch > 1;
-    if (two) HIP_TRY(c, hipStreamWaitEvent(c->estream2, c->ev_in, 0), SBR_EDEVICE);
     for (int64_t k = 0; k < n_batch; k++) {
         const int slot = (int)(k % nslot);
-        hipStream_t es = (two && (k & 1)) ? c->estream2 : s; // equilibrium stream of batch k
+        hipStream_t es = s; // one equilibrium stream (two alternating: 15% slower, r01_ab27)
         hipStream_t ls = c->lstream[slot];
         const double* bk = beta + k * n_beta;
         const double* ek = eta + k * n_beta;
@@ -556,10 +542,6 @@ int sbr_sweep_baseline_batch_dev(sbr_ctx* c, void* stream, int64_t n_batch, cons
         if (rc) return rc;
         HIP_TRY(c, hipEventRecord(c->ev_eq[slot], es), SBR_EDEVICE);
         c->last_slot = slot;
-    }
-    if (two) { // results complete for work enqueued on `stream` afterwards
-        HIP_TRY(c, hipEventRecord(c->ev_e2, c->estream2), SBR_EDEVICE);
-        HIP_TRY(c, hipStreamWaitEvent(s, c->ev_e2, 0), SBR_EDEVICE);
     }
     return SBR_OK;
 }
@@ -820,7 +802,6 @@ int sbr_timing_read(sbr_ctx* c, void* stream, double* learn_ms, double* eq_ms, i
     int32_t n = 0;
     for (hipStream_t ls : c->lstream)
         if (ls) HIP_TRY(c, hipStreamSynchronize(ls), SBR_EDEVICE);
-    if (c->estream2) HIP_TRY(c, hipStreamSynchronize(c->estream2), SBR_EDEVICE);
     for (const auto& r : c->trec) {
         float t = 0.f;
         HIP_TRY(c, hipEventElapsedTime(&t, r.a, r.b), SBR_EDEVICE);

@@ -191,7 +191,13 @@ def test_pipelined_batches_equal_single_sweeps(engine):
     stream = torch.cuda.current_stream(dev).cuda_stream
     engine.sweep_baseline_batch_dev(t(betas), t(etas), t(tends), t(base.u), base.p, base.kappa, base.lam, base.x0,
                                     out, stream=stream)
+    # enqueued behind the call on torch's default stream, no host synchronisation between:
+    # must see every batch complete (whichever equilibrium stream ran it)
+    snap = {f: out[f].clone() for f in ("aw_max", "status")}
     torch.cuda.synchronize(dev)
+    for f in snap:
+        assert torch.equal(snap[f].view(torch.int64) if f == "aw_max" else snap[f],
+                           out[f].view(torch.int64) if f == "aw_max" else out[f]), f
     for k in range(nbat):
         g = sbr.BaselineGrid(betas[k], base.u, etas[k], tends[k], x0=base.x0, p=base.p, kappa=base.kappa,
                              lam=base.lam)
