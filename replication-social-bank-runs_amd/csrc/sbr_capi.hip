@@ -16,6 +16,19 @@
 #include "../../include/sbr_detmath.h"
 #include "sbr_kernels.h"
 
+// Event flags. Timing events only time (no system-scope cache writeback/invalidate when they
+// complete); dependency events between this device's queues release to device scope.
+#ifndef SBR_TIMING_EVENT_FLAGS
+#define SBR_TIMING_EVENT_FLAGS hipEventDisableSystemFence
+#endif
+#ifndef SBR_SYNC_EVENT_FLAGS
+#define SBR_SYNC_EVENT_FLAGS (hipEventDisableTiming | hipEventReleaseToDevice)
+#endif
+
+#ifndef SBR_LEARN_SLOTS
+#define SBR_LEARN_SLOTS 3
+#endif
+
 struct sbr_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -24,7 +37,7 @@ struct sbr_ctx {
     // kLearnSlots slots, each learned on its own highest-priority stream, so the
     // learning of the next kLearnSlots-1 batches (latency-bound: 32 waves each) runs
     // concurrently with the equilibrium of the current one
-    static constexpr int kLearnSlots = 3;
+    static constexpr int kLearnSlots = SBR_LEARN_SLOTS;
     size_t ws_beta[kLearnSlots] = {}, ws_cap[kLearnSlots] = {};
     sbr::LearnBufs LW[kLearnSlots]{};
     int last_slot = 0;
@@ -302,7 +315,7 @@ hipEvent_t next_event(sbr_ctx* c)
 {
     if (c->ev_used == c->ev_pool.size()) {
         hipEvent_t e;
-        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        if (hipEventCreateWithFlags(&e, SBR_TIMING_EVENT_FLAGS) != hipSuccess) return nullptr;
         c->ev_pool.push_back(e);
     }
     return c->ev_pool[c->ev_used++];
@@ -402,8 +415,8 @@ int sbr_init(int device, sbr_ctx** out)
     sbr_ctx* c = new sbr_ctx();
     c->device = device;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&c->ev_fork, SBR_SYNC_EVENT_FLAGS) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_join, SBR_SYNC_EVENT_FLAGS) != hipSuccess) {
         delete c;
         return SBR_EDEVICE;
     }
@@ -483,10 +496,10 @@ int ensure_pipe_streams(sbr_ctx* c)
     (void)hipDeviceGetStreamPriorityRange(&lo, &hi); // hi = greatest priority
     for (int k = 0; k < sbr_ctx::kLearnSlots; k++) {
         HIP_TRY(c, hipStreamCreateWithPriority(&c->lstream[k], hipStreamNonBlocking, hi), SBR_EDEVICE);
-        HIP_TRY(c, hipEventCreateWithFlags(&c->ev_learned[k], hipEventDisableTiming), SBR_EDEVICE);
-        HIP_TRY(c, hipEventCreateWithFlags(&c->ev_eq[k], hipEventDisableTiming), SBR_EDEVICE);
+        HIP_TRY(c, hipEventCreateWithFlags(&c->ev_learned[k], SBR_SYNC_EVENT_FLAGS), SBR_EDEVICE);
+        HIP_TRY(c, hipEventCreateWithFlags(&c->ev_eq[k], SBR_SYNC_EVENT_FLAGS), SBR_EDEVICE);
     }
-    HIP_TRY(c, hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming), SBR_EDEVICE);
+    HIP_TRY(c, hipEventCreateWithFlags(&c->ev_in, SBR_SYNC_EVENT_FLAGS), SBR_EDEVICE);
     return SBR_OK;
 }
 
