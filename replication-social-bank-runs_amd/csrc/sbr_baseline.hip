@@ -187,7 +187,9 @@ __global__ __launch_bounds__(HZ_BLOCK) void hazard_kernel(const double* __restri
     // while the block runs): no LDS, so hazard blocks of the next batch can share
     // CUs with an equilibrium kernel that holds all of their LDS.
     __shared__ int s_m;
+#ifndef SBR_HZ_NOPRIO
     __builtin_amdgcn_s_setprio(3);
+#endif
     const int b = blockIdx.x;
     const int n = L.n_knots[b];
     const uint32_t st = L.status[b];

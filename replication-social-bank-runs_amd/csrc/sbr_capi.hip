@@ -25,6 +25,9 @@
 #define SBR_SYNC_EVENT_FLAGS (hipEventDisableTiming | hipEventReleaseToDevice)
 #endif
 
+#ifndef SBR_LEARN_PRIO_HI
+#define SBR_LEARN_PRIO_HI 1 // learning streams at the greatest stream priority
+#endif
 #ifndef SBR_LEARN_SLOTS
 #define SBR_LEARN_SLOTS 3
 #endif
@@ -495,7 +498,7 @@ int ensure_pipe_streams(sbr_ctx* c)
     int lo = 0, hi = 0;
     (void)hipDeviceGetStreamPriorityRange(&lo, &hi); // hi = greatest priority
     for (int k = 0; k < sbr_ctx::kLearnSlots; k++) {
-        HIP_TRY(c, hipStreamCreateWithPriority(&c->lstream[k], hipStreamNonBlocking, hi), SBR_EDEVICE);
+        HIP_TRY(c, hipStreamCreateWithPriority(&c->lstream[k], hipStreamNonBlocking, SBR_LEARN_PRIO_HI ? hi : lo), SBR_EDEVICE);
         HIP_TRY(c, hipEventCreateWithFlags(&c->ev_learned[k], SBR_SYNC_EVENT_FLAGS), SBR_EDEVICE);
         HIP_TRY(c, hipEventCreateWithFlags(&c->ev_eq[k], SBR_SYNC_EVENT_FLAGS), SBR_EDEVICE);
     }
