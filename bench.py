@@ -41,15 +41,80 @@ import sbr  # noqa: E402
 
 FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X FP64 vector, AMD spec (256 CU x 128 FLOP/clk x 2.4 GHz)
 
-# FP64 operations per equilibrium-kernel stage as the code executes them
-# (add/sub/mul/div = 1, fma = 2, compares/selects/loads = 0)
-F_LERP = 7
-F_BUFFER = 12          # two crossing interpolations (solver.jl:237,250)
-F_BISECT_ITER = 37     # 4 lerps + ε + shifted args + AW/AWe/err + midpoint (solver.jl:326-372)
-F_AW_PER_KNOT = 20     # 2 shifted args x2, 2 lerps, net (solver.jl:511-524)
-F_EXP, F_LOG = 22, 24  # include/sbr_detmath.h
-F_RK_STEP = 21 + 48 + 3 + 14 + 3 + 2 * (F_EXP + F_LOG + 1) + 2 + 5  # Tsit5 step + PI controller
-F_HAZARD_KNOT = 3 + F_EXP + 1 + 4 + 2 + 3  # g, exp, e, trapezoid, numerator, HR division
+# Algorithmic flops per unit of work, SURVEY.md §8(d)'s counting convention (FMA = 2,
+# add/sub/mul/div/exp/pow = 1, compares/branches/searches = 0), counted on the work the
+# reference's algorithm defines — not on what the kernels execute (branch and bound
+# evaluates far fewer AW knots; the executed FP64 work comes from the PMC counters).
+F8_BUFFER = 12        # per point: optimal_buffer's two crossing interpolations (solver.jl:237,250)
+F8_BISECT_ITER = 20   # per compute_ξ iteration: 4 lerps x 4 + 4 (solver.jl:326-372)
+F8_AW_KNOT = 12       # per τ̄ knot of a run point's AW path: 2 lerps x 4 + 4 (solver.jl:511-524, 565)
+F8_RK_STEP = 96       # per attempted Tsit5 step of a scalar ODE (94 + 2)
+F8_HZ_KNOT = 15       # per τ̄ knot of hazard_rate (solver.jl:168-182)
+PMC_SUMMARY = REPO / "profiles" / "pmc_latest.json"
+
+
+def lib_sha() -> str:
+    import hashlib
+    return hashlib.sha256(sbr._lib.LIB_PATH.read_bytes()).hexdigest()[:16]
+
+
+def executed_fp64(kernel_prefix: str, workload: str):
+    """Executed FP64 flops per launch of a kernel from the committed PMC summary
+    (tools/pmc_summary.py), only when it was collected on this very libsbr.so:
+    64·(ADD + MUL + TRANS) + 128·FMA over SQ_INSTS_VALU_*_F64 (wave instructions, every
+    lane counted as active, i.e. an upper bound).  None when unavailable."""
+    try:
+        pm = json.loads(PMC_SUMMARY.read_text())
+    except Exception:
+        return None
+    if pm.get("libsbr_sha16") != lib_sha() or pm.get("workload") != workload:
+        return None
+    for k, c in pm.get("kernels", {}).items():
+        if k.startswith(kernel_prefix) and "SQ_INSTS_VALU_FMA_F64" in c:
+            return (64 * (c.get("SQ_INSTS_VALU_ADD_F64", 0) + c.get("SQ_INSTS_VALU_MUL_F64", 0)
+                          + c.get("SQ_INSTS_VALU_TRANS_F64", 0)) + 128 * c["SQ_INSTS_VALU_FMA_F64"])
+    return None
+
+
+def roofline(kernel: str, flops: float, secs: float, traffic=None, executed=None, limiter="latency") -> dict:
+    """roofline block for `kernel`: algorithmic flops per launch / average launch time.
+    The roof the metric is priced against is the FP64 vector peak (no dense
+    contraction: no MFMA; ≈10⁴ flop/B: not HBM); `bound` names what limits the kernel
+    in practice (PMC: dependent search / division chains, wait and issue stalls)."""
+    ach = flops / secs / 1e12 if secs > 0 else 0.0
+    r = {"bound": limiter, "roof": "valu_fp64", "kernel": kernel, "achieved": ach, "peak": FP64_VALU_PEAK_TFLOPS,
+         "unit": "TFLOP/s", "frac": ach / FP64_VALU_PEAK_TFLOPS, "traffic": traffic,
+         "flops_per_launch": flops, "flop_convention": "SURVEY.md §8(d)"}
+    if executed is not None and secs > 0:
+        r["frac_executed"] = executed / secs / 1e12 / FP64_VALU_PEAK_TFLOPS
+        r["executed_flops_per_launch"] = executed
+    else:
+        r["frac_executed"] = None
+    return r
+
+
+def usable_cores() -> int:
+    """CPUs this process may use: the affinity set, capped by a cgroup v2 cpu.max quota."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if q != "max":
+            n = max(1, min(n, int(int(q) // int(per))))
+    except Exception:
+        pass
+    return n
+
+
+def host_info() -> dict:
+    model = "unknown"
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except Exception:
+        pass
+    return {"nproc": os.cpu_count(), "usable": usable_cores(), "model": model}
 
 
 def parse():
@@ -172,12 +237,10 @@ def main():
     status = out["status"][last].cpu().numpy().view(np.uint32).reshape(nb, nu)
     run = (status & sbr.STATUS["SBR_RUN"]) > 0
     n_tau = ls["n_tau"].astype(np.int64)
-    f_eq = (F_BUFFER * nb * nu + F_BISECT_ITER * int(iters.sum())
-            + int((run * (F_AW_PER_KNOT * n_tau[:, None] + F_LERP)).sum())
-            + 2 * int(n_tau.sum()) * ((nu + 1023) // 1024))
-    f_learn = F_RK_STEP * int((ls["n_accept"] + ls["n_reject"]).sum()) + F_HAZARD_KNOT * int(n_tau.sum())
+    f_eq = (F8_BUFFER * nb * nu + F8_BISECT_ITER * int(iters.sum())
+            + F8_AW_KNOT * int((run * n_tau[:, None]).sum()))
+    f_learn = F8_RK_STEP * int((ls["n_accept"] + ls["n_reject"]).sum()) + F8_HZ_KNOT * int(n_tau.sum())
     eq_s = eq_ms / max(ncalls, 1) / 1e3
-    achieved = f_eq / eq_s / 1e12
 
     total_pts = nb * nu * world
     value = total_pts * a.steps / elapsed
@@ -213,15 +276,12 @@ def main():
         },
         "kernel_ms_per_step": {"learn_logistic": learn_ms / max(ncalls, 1), "equilibrium": eq_ms / max(ncalls, 1)},
         "flops_per_step": {"equilibrium": f_eq, "learn": f_learn},
-        "roofline": {
-            "bound": "valu_fp64",
-            "kernel": "equilibrium_kernel",
-            "achieved": achieved,
-            "peak": FP64_VALU_PEAK_TFLOPS,
-            "unit": "TFLOP/s",
-            "frac": achieved / FP64_VALU_PEAK_TFLOPS,
-            "traffic": traffic,
-        },
+        "work_per_step": {"run_points": int(run.sum()), "bisect_iters": int(iters.sum()),
+                          "aw_knots_run": int((run * n_tau[:, None]).sum()),
+                          "rk_steps": int((ls["n_accept"] + ls["n_reject"]).sum())},
+        "roofline": roofline("equilibrium_kernel", f_eq, eq_s, traffic,
+                             executed_fp64("equilibrium_kernel<", f"fig5_{n}x{n}")),
+        "libsbr_sha16": lib_sha(),
     }
     if a.phases:
         res["eq_phase_ms"] = phase_breakdown(eng, beta[0], eta[0], t_end[0], u, p, kappa, lam, x0,
@@ -312,6 +372,15 @@ def main_hetero(a):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     st = out["status"].cpu().numpy().view(np.uint32)
+    # §8(d)-style algorithmic flops of the equilibrium kernel (batch 0 = learning slot 0):
+    # K buffers, K-group bisection iterations, AW over the whole knot grid on run points
+    # (get_AW_hetero); the validity check is not counted (a lower bound)
+    hs = eng.hetero_learn_stats(nb)
+    it_h = (out_b["iters"][0] if pipe else out["iters"]).cpu().numpy().reshape(nb, nu).astype(np.int64)
+    st0 = (out_b["status"][0] if pipe else out["status"]).cpu().numpy().view(np.uint32).reshape(nb, nu)
+    run_h = (st0 & sbr.STATUS["SBR_RUN"]) > 0
+    nk_h = hs["n_knots"].astype(np.int64)
+    f_eq_h = K * (F8_BUFFER * nb * nu + F8_BISECT_ITER * int(it_h.sum()) + F8_AW_KNOT * int((run_h * nk_h[:, None]).sum()))
     res = {
         "metric": "equilibria solved/sec on β×u grid (FP64), heterogeneity extension K=8",
         "value": nb * nu * world * a.steps / elapsed,
@@ -324,7 +393,13 @@ def main_hetero(a):
                    "parallelism": f"column shards x{world}", "pipelined": pipe},
         "kernel_ms_per_step": {"learn_hetero": learn_ms / max(ncalls, 1), "equilibrium_hetero": eq_ms / max(ncalls, 1)},
         "run_fraction": float(((st & sbr.STATUS["SBR_RUN"]) > 0).mean()),
+        # columns whose AutoSwitch moved to Rosenbrock23 (handled: restated in the engine and the oracle)
         "stiff_switch_fraction": float(((st & sbr.STATUS["SBR_STIFF_SWITCH"]) > 0).mean()),
+        "stiff_switch": "handled (Rosenbrock23 restated, DESIGN.md §2)",
+        "learn_steps_per_column": float((hs["n_accept"] + hs["n_reject"]).mean()),
+        "roofline": roofline("equilibrium_hetero_kernel", f_eq_h, eq_ms / max(ncalls, 1) / 1e3, None,
+                             executed_fp64("equilibrium_hetero_kernel<", f"hetero_K8_{n}x{n}")),
+        "libsbr_sha16": lib_sha(),
     }
     if a.phases:
         from sbr import _lib
@@ -347,7 +422,7 @@ def main_hetero(a):
         import oracle as O  # noqa: E402  (test infrastructure: cpu_baseline leg only)
 
         O.build()
-        cores = max(1, min(16, len(os.sched_getaffinity(0))))
+        cores = usable_cores()
         sub = g.subset(np.arange(0, nb, 16))
         t1 = time.perf_counter()
         O.sweep_hetero(sub.betas, sub.dist, sub.eta, sub.t_end, sub.u, sub.p, sub.kappa, sub.lam, sub.x0,
@@ -355,6 +430,7 @@ def main_hetero(a):
         dt = time.perf_counter() - t1
         pts = sub.betas.shape[0] * nu
         res["cpu_baseline"] = {"value": pts / dt, "unit": "equilibria/s", "cores": cores, "kind": "port",
+                               "host": host_info(),
                                "sample": f"{sub.betas.shape[0]} columns (every 16th) x {nu} u = {pts} equilibria "
                                          f"in {dt:.2f} s"}
     if rank == 0:
@@ -425,6 +501,14 @@ def main_interest(a):
         elapsed = float(t.item())
     st = out["status"].cpu().numpy().view(np.uint32)
     steps = out["rk_steps"].cpu().numpy()
+    ls = eng.learn_stats(nb)
+    it_i = out["iters"].cpu().numpy().reshape(nb, nu).astype(np.int64)
+    run_i = ((st & sbr.STATUS["SBR_RUN"]) > 0).reshape(nb, nu)
+    nt_i = ls["n_tau"].astype(np.int64)
+    # §8(d) flops of the interest kernel: the value-function Tsit5 steps, then the baseline's
+    # buffers / bisection / AW path (the h − rV scan is not counted: a lower bound)
+    f_eq_i = (F8_RK_STEP * int(steps.sum()) + F8_BUFFER * nb * nu + F8_BISECT_ITER * int(it_i.sum())
+              + F8_AW_KNOT * int((run_i * nt_i[:, None]).sum()))
     res = {
         "metric": "equilibria solved/sec on β×u grid (FP64), interest-rate extension (value function per point)",
         "value": nb * nu * world * a.steps / elapsed,
@@ -439,19 +523,23 @@ def main_interest(a):
         "value_fn_rk_steps_per_point": float(steps.mean()),
         "run_fraction": float(((st & sbr.STATUS["SBR_RUN"]) > 0).mean()),
         "stiff_switch_fraction": float(((st & sbr.STATUS["SBR_STIFF_SWITCH"]) > 0).mean()),
+        "roofline": roofline("equilibrium_kernel<*, true> (interest)", f_eq_i, eq_ms / max(ncalls, 1) / 1e3, None,
+                             executed_fp64("equilibrium_kernel<512, true>", f"interest_fig5_{n}x{n}")),
+        "libsbr_sha16": lib_sha(),
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         sys.path.insert(0, str(REPO / "oracle"))
         import oracle as O  # noqa: E402  (test infrastructure: cpu_baseline leg only)
 
         O.build()
-        cores = max(1, min(16, len(os.sched_getaffinity(0))))
+        cores = usable_cores()
         sub = beta_h[::10]
         t1 = time.perf_counter()
         O.sweep_interest(sub, 15.0, 30.0, u_h, p, kappa, lam, r_, delta, nthreads=cores)
         dt = time.perf_counter() - t1
         pts = len(sub) * nu
         res["cpu_baseline"] = {"value": pts / dt, "unit": "equilibria/s", "cores": cores, "kind": "port",
+                               "host": host_info(),
                                "sample": f"{len(sub)} columns (every 10th) x {nu} u = {pts} equilibria "
                                          f"in {dt:.2f} s"}
     if rank == 0:
@@ -553,13 +641,19 @@ def main_social(a):
         "fp_iters_mean": float(fp.mean()), "fp_iters_max": int(fp.max()),
         "run_fraction": float(((st & sbr.STATUS["SBR_RUN"]) > 0).mean()),
         "not_converged_fraction": float(((st & sbr.STATUS["SBR_SOCIAL_NOT_CONVERGED"]) > 0).mean()),
+        "stiff_switch_fraction": float(((st & sbr.STATUS["SBR_STIFF_SWITCH"]) > 0).mean()),
+        # §8(d) flops of the forced-ODE steps only (96 per attempted step; the per-iterate
+        # hazard / bisection / AW / norm work is not counted: a lower bound), over the
+        # whole share's wall time of the iterate kernels
+        "roofline": roofline("social_iter_kernel", F8_RK_STEP * float(steps.sum()), iter_ms / max(a.steps, 1) / 1e3),
+        "libsbr_sha16": lib_sha(),
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         sys.path.insert(0, str(REPO / "oracle"))
         import oracle as O  # noqa: E402  (test infrastructure: cpu_baseline leg only)
 
         O.build()
-        cores = max(1, min(16, len(os.sched_getaffinity(0))))
+        cores = usable_cores()
         bsel, usel = beta_h[::8], u_h[::128]  # 8 β x 4 u = 32 points spread over the grid
         t1 = time.perf_counter()
         O.sweep_social(bsel, eta_v, usel, p, kappa, lam, cmp_h[: len(bsel)], x0=x0, tol=tol,
@@ -567,6 +661,7 @@ def main_social(a):
         dt = time.perf_counter() - t1
         pts = len(bsel) * len(usel)
         res["cpu_baseline"] = {"value": pts / dt, "unit": "equilibria/s", "cores": cores, "kind": "port",
+                               "host": host_info(),
                                "sample": f"{len(bsel)} β (every 8th) x {len(usel)} u (every 128th) = {pts} "
                                          f"fixed points in {dt:.2f} s"}
     if a.social_prof:
@@ -617,13 +712,13 @@ def cpu_baseline(beta_h, u_h, stride, p, kappa, lam, x0):
     import oracle as O  # noqa: E402  (test infrastructure: cpu_baseline leg only)
 
     O.build()
-    cores = max(1, min(16, len(os.sched_getaffinity(0))))
+    cores = usable_cores()
     cols = beta_h[::stride]
     t0 = time.perf_counter()
     O.sweep_baseline(cols, 15.0, 30.0, u_h, p, kappa, lam, x0=x0, nthreads=cores)
     dt = time.perf_counter() - t0
     pts = len(cols) * len(u_h)
-    return {"value": pts / dt, "unit": "equilibria/s", "cores": cores, "kind": "port",
+    return {"value": pts / dt, "unit": "equilibria/s", "cores": cores, "kind": "port", "host": host_info(),
             "sample": f"{len(cols)} β columns (every {stride}th of the {len(beta_h)}) x {len(u_h)} u = {pts} "
                       f"equilibria in {dt:.2f} s"}
 

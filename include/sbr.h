@@ -298,6 +298,11 @@ int sbr_timing_read(sbr_ctx* ctx, void* stream, double* learn_ms, double* eq_ms,
 int sbr_learn_stats(sbr_ctx* ctx, int64_t n_beta, int32_t* n_knots, int32_t* n_tau, int32_t* n_accept,
                     int32_t* n_reject, uint32_t* status);
 
+/* Same for the heterogeneity learning of the last hetero sweep (single-workspace calls:
+ * sbr_sweep_hetero[_dev]; the batch pipeline's slot 0 otherwise). */
+int sbr_hetero_learn_stats(sbr_ctx* ctx, int64_t n_col, int32_t* n_knots, int32_t* n_tau, int32_t* n_accept,
+                           int32_t* n_reject, uint32_t* status);
+
 /* Device facts the engine sized itself with: LDS bytes per workgroup, knots
  * staged in LDS per β column, compute units. */
 int sbr_device_info(sbr_ctx* ctx, int32_t* lds_bytes_per_block, int32_t* lds_knot_capacity, int32_t* cu_count);
@@ -306,6 +311,9 @@ int sbr_device_info(sbr_ctx* ctx, int32_t* lds_bytes_per_block, int32_t* lds_kno
  * evaluated on the device, for host/device bit-equality tests. */
 int sbr_selftest_detmath(sbr_ctx* ctx, const double* x, const double* y, int n, double* exp_out, double* log_out,
                          double* pow_out);
+/* Diagnostics: FastPower.fastpower(x, y) (include/sbr_detmath.h sbr_fastpow, the PI
+ * controller's Float32 power) evaluated on the device. */
+int sbr_selftest_fastpow(sbr_ctx* ctx, const double* x, const double* y, int n, double* out);
 
 #ifdef __cplusplus
 }

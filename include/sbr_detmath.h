@@ -142,4 +142,72 @@ SBR_HD double sbr_pow_pos(double x, double y)
     return x == 0.0 ? 0.0 : sbr_exp(y * sbr_log(x));
 }
 
+/* 10^y, log10(x) for the initial-dt heuristic (ode_determine_initdt's
+ * 10.0^(-(2 + log10(d)) / order)); Julia's Base log10 / ^ are not restated
+ * bit for bit — the first dt is "parity unpinned" at the ulp level. */
+#define SBR_LN10 2.30258509299404568402e+00
+SBR_HD double sbr_log10(double x) { return sbr_log(x) / SBR_LN10; }
+SBR_HD double sbr_exp10(double y) { return sbr_exp(y * SBR_LN10); }
+
+/* ------------------------------------------------------------------------
+ * FastPower.fastpower (FastPower 1.1.3, Manifest.toml:675-678; called by
+ * OrdinaryDiffEqCore's PIController, stepsize_controller!): a Float32
+ * approximation of x^y,
+ *     fastpower(x, y) = Float64(@fastmath exp2(Float32(y) * fastlog2(Float32(x))))
+ * with fastlog2 the rational approximation (x-1)(a(x-1)+b)/((x-1)+c) of
+ * Goldberg's "fast approximate logarithms" (table 2, line 8) on the
+ * significand, and Julia's Base.Math exp2 for Float32 (exp_impl_fast:
+ * N = round(x), r = x - N, the degree-7 Horner kernel in muladd, times 2^N).
+ * Restated from the published algorithm (not vendored).  All Float32
+ * arithmetic is IEEE single precision, evaluated as written (callers are
+ * compiled with -ffp-contract=off; fmaf only where Julia's evalpoly has a
+ * muladd); identical on the host and gfx950.
+ * ------------------------------------------------------------------------ */
+SBR_HD uint32_t sbr_fbits(float x) { uint32_t u; __builtin_memcpy(&u, &x, 4); return u; }
+SBR_HD float sbr_bitsf(uint32_t u) { float x; __builtin_memcpy(&x, &u, 4); return x; }
+
+SBR_HD float sbr_fastlog2f(float x)
+{
+    const float a = 0.338953f, b = 2.198599f, c = 1.523692f;
+    const uint32_t ux1i = sbr_fbits(x);
+    const uint32_t e = (ux1i & 0x7F800000u) >> 23;
+    const int greater = (ux1i & 0x00400000u) != 0u; /* significand > 1.5 */
+    /* greater: halve the significand (exponent 0x3f000000) and compensate with 126 */
+    const float signif0 = sbr_bitsf((ux1i & 0x007FFFFFu) | (greater ? 0x3f000000u : 0x3f800000u));
+    const float fexp = (float)e - (greater ? 126.0f : 127.0f);
+    const float signif = signif0 - 1.0f;
+    return fexp + (signif * (a * signif + b)) / (signif + c);
+}
+
+/* Base.Math.exp_impl_fast(x::Float32, Val(2)) (MAX_EXP = 128, SUBNORM_EXP = 150) */
+SBR_HD float sbr_exp2f_jl(float x)
+{
+    const float inf = sbr_bitsf(0x7f800000u);
+    if (x >= 128.0f) return inf;
+    if (x <= -150.0f) return 0.0f;
+    const float nf = __builtin_rintf(x); /* round(x), ties to even */
+    const float r0 = __builtin_fmaf(nf, -1.0f, x);
+    const float r = __builtin_fmaf(nf, 0.0f, r0);
+    float p = 1.5316464e-5f; /* expb_kernel(Val(2), ::Float32): evalpoly = Horner in muladd */
+    p = __builtin_fmaf(r, p, 0.00015469732f);
+    p = __builtin_fmaf(r, p, 0.0013333423f);
+    p = __builtin_fmaf(r, p, 0.009618025f);
+    p = __builtin_fmaf(r, p, 0.05550411f);
+    p = __builtin_fmaf(r, p, 0.2402265f);
+    p = __builtin_fmaf(r, p, 0.6931472f);
+    p = __builtin_fmaf(r, p, 1.0f);
+    const int32_t n = (int32_t)nf;
+    const float twopk = sbr_bitsf((uint32_t)(n + 127) << 23);
+    return twopk * p;
+}
+
+/* FastPower.fastpower(x, y) for Float64 x, y */
+SBR_HD double sbr_fastpow(double x, double y)
+{
+    if (x == 0.0) return 0.0;
+    const uint64_t bx = sbr_dbits(x) & 0x7fffffffffffffffull, by = sbr_dbits(y) & 0x7fffffffffffffffull;
+    if (bx == 0x7ff0000000000000ull && by == 0x7ff0000000000000ull) return sbr_bitsd(0x7ff0000000000000ull);
+    return (double)sbr_exp2f_jl((float)y * sbr_fastlog2f((float)x));
+}
+
 #endif /* SBR_DETMATH_H */

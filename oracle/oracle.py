@@ -64,11 +64,13 @@ EPS = float(np.finfo(np.float64).eps)
 def learn_logistic(beta, t_end, x0=1e-4, t0=0.0, rtol=EPS, atol=EPS, maxiters=1_000_000, cap=1 << 16):
     t = np.empty(cap)
     G = np.empty(cap)
-    stats = np.zeros(4, np.int64)
+    stats = np.zeros(8, np.int64)
     n = lib().sbro_learn_logistic(beta, t0, t_end, x0, rtol, atol, maxiters, _ptr(t), _ptr(G), cap, _ptr(stats))
     if n < 0:
         raise RuntimeError(f"oracle knot buffer too small ({-n} needed)")
-    return t[:n].copy(), G[:n].copy(), dict(naccept=int(stats[0]), nreject=int(stats[1]), status=int(stats[2]))
+    return t[:n].copy(), G[:n].copy(), dict(naccept=int(stats[0]), nreject=int(stats[1]), status=int(stats[2]),
+                                            t_switch=float(stats[4:5].view(np.float64)[0]),
+                                            nswitch=int(stats[5]), nstiff=int(stats[6]))
 
 
 def equilibrium(t, G, beta, eta, t_end, u, p, kappa, lam, max_iters=100, paths=False):
@@ -121,6 +123,18 @@ def apply_early_exit(res: dict, threshold: int = 5) -> dict:
     return r
 
 
+def fastpow(x, y):
+    """FastPower.fastpower restated (include/sbr_detmath.h sbr_fastpow)."""
+    x = np.ascontiguousarray(x, np.float64)
+    y = np.ascontiguousarray(np.broadcast_to(y, x.shape), np.float64)
+    out = np.empty(len(x))
+    L = lib()
+    L.sbro_fastpow.restype = None
+    L.sbro_fastpow.argtypes = [_P, _P, _I64, _P]
+    L.sbro_fastpow(_ptr(x), _ptr(y), len(x), _ptr(out))
+    return out
+
+
 def detmath(x, y):
     x = np.ascontiguousarray(x, np.float64)
     y = np.ascontiguousarray(y, np.float64)
@@ -145,13 +159,14 @@ def learn_hetero(betas, dist, t_end, x0=1e-4, cap=1 << 16):
     K = len(betas)
     t = np.empty(cap)
     G = np.empty(cap * K)
-    stats = np.zeros(5, np.int64)
+    stats = np.zeros(8, np.int64)
     n = L.sbro_learn_hetero(_ptr(betas), _ptr(dist), K, t_end, x0, _ptr(t), _ptr(G), cap, _ptr(stats))
     if n < 0:
         raise RuntimeError("oracle hetero learning failed")
     return t[:n].copy(), G[: n * K].reshape(n, K).copy(), dict(naccept=int(stats[0]), nreject=int(stats[1]),
                                                                 status=int(stats[2]),
-                                                                t_switch=float(stats[4:5].view(np.float64)[0]))
+                                                                t_switch=float(stats[4:5].view(np.float64)[0]),
+                                                                nswitch=int(stats[5]), nstiff=int(stats[6]))
 
 
 def sweep_hetero(betas, dist, eta, t_end, u, p, kappa, lam, x0=1e-4, max_iters=500, tolerance=1e-12, nthreads=0):

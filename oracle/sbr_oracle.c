@@ -75,17 +75,34 @@ static const double BT1 = -0.00178001105222577714, BT2 = -0.0008164344596567469,
                     BT3 = 0.007880878010261995, BT4 = -0.1447110071732629,
                     BT5 = 0.5823571654525552, BT6 = -0.45808210592918697,
                     BT7 = 0.015151515151515152;
-static const double TSIT5_STABILITY = 3.5068469938049235;
+/* alg_stability_size(::Tsit5) (OrdinaryDiffEqTsit5 alg_utils) */
+#ifndef SBRO_TSIT5_STABILITY
+#define SBRO_TSIT5_STABILITY 3.5068
+#endif
+static const double TSIT5_STABILITY = SBRO_TSIT5_STABILITY;
 
-/* OrdinaryDiffEq PI-controller defaults for a 5th-order method */
+/* Rosenbrock23Tableau (OrdinaryDiffEqRosenbrock 1.18.1): c32 = 6 + sqrt(2), d = 1/(2 + sqrt(2)) */
+static const double ROS23_C32 = 0x1.da827999fcef3p+2; /* 7.414213562373095 */
+static const double ROS23_D = 0x1.2bec333018867p-2;   /* 0.2928932188134525 */
+
+/* OrdinaryDiffEq PI-controller defaults.  The composite algorithm takes the
+ * betas of its current (first) algorithm at init (_composite_beta1_default):
+ * Tsit5's 7/50, 2/25, held for the whole solve — reset_alg_dependent_opts!
+ * compares the Float64 opts with the Rational defaults (7//50 ≠ 0.14 exactly),
+ * so a switch to Rosenbrock23 does not replace them; qmin = max, qmax = min
+ * over the two algorithms' defaults (1/5, 10), gamma 9/10. */
 #define CTL_BETA1 0.14   /* 7//50 */
 #define CTL_BETA2 0.08   /* 2//25 */
 #define CTL_INV_QMIN 5.0 /* qmin = 1//5 */
 #define CTL_INV_QMAX 0.1 /* qmax = 10 */
 #define CTL_GAMMA 0.9
 #define CTL_QOLDMIN 1e-4
+/* AutoSwitch defaults (OrdinaryDiffEqCore composite_algs): maxstiffstep 10,
+ * maxnonstiffstep 3, nonstifftol = stifftol = 9/10, dtfac 2 */
 #define AUTOSWITCH_TOL 0.9
 #define AUTOSWITCH_MAXSTIFF 10
+#define AUTOSWITCH_MAXNONSTIFF 3
+#define AUTOSWITCH_DTFAC 2.0
 
 static inline double dmin(double a, double b) { return a < b ? a : b; }
 static inline double dmax(double a, double b) { return a > b ? a : b; }
@@ -157,36 +174,44 @@ static inline double interp_s(const double* t, const double* v, int64_t stride, 
 }
 #define INTERP(t, v, n, x, oob) interp_s((t), (v), 1, (n), (x), (oob))
 
-/* ------------------------------------------------------------------------ */
-/* AutoSwitch stiffness bookkeeping (OrdinaryDiffEqCore composite)           */
-/* ------------------------------------------------------------------------ */
-typedef struct {
-    int count;
-    int switched;
-} autoswitch_t;
-
-static inline void autoswitch_update(autoswitch_t* as, double eigen_est, double dt)
+/* ForwardDiff derivative of the same interpolant at x (a Dual in the time
+ * argument): δ = (x − t_j)/Δ carries partial 1/Δ, so the value's partial is
+ * v_j·(−(1/Δ)) + v_{j+1}·(1/Δ).  Used for Rosenbrock23's ∂f/∂t. */
+static inline double interp_dx(const double* t, const double* v, int64_t stride, int64_t n, double x, int* oob)
 {
-    double stiffness = fabs(eigen_est * dt / TSIT5_STABILITY);
-    int is_stiff = stiffness > AUTOSWITCH_TOL; /* NaN -> false */
-    if (is_stiff) as->count = as->count < 0 ? 1 : as->count + 1;
-    else as->count = as->count > 0 ? -1 : as->count - 1;
-    if (as->count > AUTOSWITCH_MAXSTIFF) as->switched = 1;
+    if (n < 2 || !(x >= t[0] && x <= t[n - 1])) { *oob = 1; return NAN; }
+    int64_t j = ssl(t, n, x);
+    if (j > n - 2) j = n - 2;
+    if (j < 0) j = 0;
+    const double r = 1.0 / (t[j + 1] - t[j]);
+    return v[j * stride] * (-r) + v[(j + 1) * stride] * r;
 }
 
 /* ------------------------------------------------------------------------ */
-/* Generic Tsit5 on an m-vector ODE with RMS error norm.                     */
-/* rhs(ctx, t, x[m], dx[m], &oob)                                            */
+/* The ODE solver: OrdinaryDiffEq's AutoTsit5(Rosenbrock23()) at the         */
+/* reference's reltol = abstol = eps() (learning.jl:51,                      */
+/* heterogeneity_learning.jl:74, social_learning_dynamics.jl:71,             */
+/* value_function_solver.jl:105).  Restated from OrdinaryDiffEqCore 1.34.0   */
+/* (solve! / loopheader! / loopfooter!, PIController, AutoSwitch),           */
+/* OrdinaryDiffEqTsit5 1.5.0 and OrdinaryDiffEqRosenbrock 1.18.1             */
+/* (Manifest.toml:1511-1515, 1679-1683, 1643-1647) — not vendored.           */
 /* ------------------------------------------------------------------------ */
+/* rhs(ctx, t, x[m], dx[m], &oob) */
 typedef void (*rhs_fn)(void* ctx, double t, const double* x, double* dx, int* oob);
+/* Jacobian J[m×m] (row-major, J[i*m+j] = ∂f_i/∂x_j) and ∂f/∂t at (t, x), as
+ * ForwardDiff's dual arithmetic evaluates them through the RHS expression */
+typedef void (*jac_fn)(void* ctx, double t, const double* x, double* J, double* dT, int* oob);
 
 typedef struct {
     int64_t naccept, nreject;
+    int64_t nstiff;  /* attempted Rosenbrock23 steps */
+    int32_t nswitch; /* algorithm switches (either direction) */
     uint32_t status;
-    double t_switch; /* time at which AutoSwitch would have switched (NaN if never) */
+    double t_switch; /* time of the first switch to Rosenbrock23 (NaN if never) */
 } ode_stats_t;
 
 #define MAXK 64
+#define MAXJ 16 /* largest system with a Rosenbrock23 branch (hetero K <= 8) */
 
 /* RMS norm over m components (DiffEqBase ODE_DEFAULT_NORM); |x| when m == 1 */
 static inline double rms_norm(const double* v, int m)
@@ -197,153 +222,311 @@ static inline double rms_norm(const double* v, int m)
     return sqrt(s / (double)m);
 }
 
-/* called after every accepted step with (tprev, t, dt, uprev, u, k1..k7) — the
- * integrator state OrdinaryDiffEq's savevalues! sees (saveat interpolation) */
-typedef void (*step_fn)(void* ctx, double tprev, double t, double dt, const double* uprev, const double* u,
-                        const double* const* k);
+/* AutoSwitchCache: successive stiffness-test positives count up, negatives
+ * down (composite_algs.jl); is_stiff: |eigen_est·dt / stability(Tsit5)| >
+ * tol, tested in every loopheader! (after the accept/reject dt update,
+ * before fix_dt_at_bounds!).  Returns 1 when the algorithm changes; the
+ * switch scales dt by dtfac (×2 to Rosenbrock23, ÷2 back to Tsit5). */
+typedef struct {
+    int count;
+    int stiff; /* current algorithm is Rosenbrock23 */
+} autoswitch_t;
 
-static int tsit5_solve_cb(rhs_fn f, void* ctx, int m, double t0, double t1, const double* x0, double rtol,
-                          double atol, int64_t maxiters, knots_t* kn, ode_stats_t* st, step_fn on_step,
-                          void* step_ctx);
-
-static int tsit5_solve(rhs_fn f, void* ctx, int m, double t0, double t1, const double* x0, double rtol,
-                       double atol, int64_t maxiters, knots_t* kn, ode_stats_t* st)
+static inline int autoswitch_choose(autoswitch_t* as, double eigen_est, double* dt)
 {
-    return tsit5_solve_cb(f, ctx, m, t0, t1, x0, rtol, atol, maxiters, kn, st, NULL, NULL);
+    double stiffness = fabs(eigen_est * *dt / TSIT5_STABILITY);
+    int is_stiff = stiffness > AUTOSWITCH_TOL; /* NaN -> false */
+    if (is_stiff) as->count = as->count < 0 ? 1 : as->count + 1;
+    else as->count = as->count > 0 ? -1 : as->count - 1;
+    if (!as->stiff && as->count > AUTOSWITCH_MAXSTIFF) {
+        *dt = *dt * AUTOSWITCH_DTFAC;
+        as->stiff = 1;
+        return 1;
+    }
+    if (as->stiff && as->count < -AUTOSWITCH_MAXNONSTIFF) {
+        *dt = *dt / AUTOSWITCH_DTFAC;
+        as->stiff = 0;
+        return 1;
+    }
+    return 0;
+}
+
+/* LinearAlgebra/LinearSolve generic_lufact! with RowMaximum pivoting (the
+ * default LinearSolve choice for length(b) <= 10: GenericLUFactorization):
+ * column scaling by the reciprocal pivot, rank-1 updates A[i,j] -= A[i,k]·A[k,j]
+ * (no fma), row-major A[i*m+j]. */
+static void lu_factor(double* A, int m, int* piv)
+{
+    for (int k = 0; k < m; k++) {
+        int kp = k;
+        if (k < m - 1) {
+            double amax = fabs(A[k * m + k]);
+            for (int i = k + 1; i < m; i++) {
+                const double ai = fabs(A[i * m + k]);
+                if (ai > amax) { kp = i; amax = ai; }
+            }
+        }
+        piv[k] = kp;
+        if (A[kp * m + k] != 0.0) {
+            if (kp != k)
+                for (int j = 0; j < m; j++) { double tmp = A[k * m + j]; A[k * m + j] = A[kp * m + j]; A[kp * m + j] = tmp; }
+            const double inv = 1.0 / A[k * m + k];
+            for (int i = k + 1; i < m; i++) A[i * m + k] = A[i * m + k] * inv;
+        }
+        for (int j = k + 1; j < m; j++)
+            for (int i = k + 1; i < m; i++) A[i * m + j] = A[i * m + j] - A[i * m + k] * A[k * m + j];
+    }
+}
+
+/* ldiv! on the factors = LAPACK getrs (laswp, unit-lower then upper trsv,
+ * column-oriented axpy updates y += (−x_j)·a_ij in fma, division by the pivot) */
+static void lu_solve(const double* A, const int* piv, int m, double* b)
+{
+    for (int k = 0; k < m; k++)
+        if (piv[k] != k) { double tmp = b[k]; b[k] = b[piv[k]]; b[piv[k]] = tmp; }
+    for (int j = 0; j < m; j++) {
+        const double a = -b[j];
+        for (int i = j + 1; i < m; i++) b[i] = fma(a, A[i * m + j], b[i]);
+    }
+    for (int j = m - 1; j >= 0; j--) {
+        b[j] = b[j] / A[j * m + j];
+        const double a = -b[j];
+        for (int i = 0; i < j; i++) b[i] = fma(a, A[i * m + j], b[i]);
+    }
+}
+
+/* opnorm(J, Inf): max row sum of |J_ij| (NaN-propagating max) — the
+ * eigen_est calc_J! sets for a CompositeAlgorithm */
+static double opnorm_inf(const double* J, int m)
+{
+    double nrm = 0.0;
+    for (int i = 0; i < m; i++) {
+        double s = 0.0;
+        for (int j = 0; j < m; j++) s = s + fabs(J[i * m + j]);
+        nrm = (nrm != nrm || s != s) ? NAN : (s > nrm ? s : nrm);
+    }
+    return nrm;
+}
+
+/* called after every accepted step with (tprev, t, dt, uprev, u, k) — the
+ * integrator state OrdinaryDiffEq's savevalues! sees (saveat interpolation);
+ * stiff = 1: k = {k1, k2} of Rosenbrock23, else k1..k7 of Tsit5 */
+typedef void (*step_fn)(void* ctx, double tprev, double t, double dt, const double* uprev, const double* u,
+                        const double* const* k, int stiff);
+
+typedef struct {
+    rhs_fn f;
+    jac_fn jac; /* NULL: no Rosenbrock23 branch restated for this RHS (flag SBR_ODE_FAILED if needed) */
+    void* ctx;
+} ode_sys_t;
+
+/* One Tsit5 step (perform_step!, Tsit5Cache, @muladd): u, k[0..6], EEst and
+ * the AutoSwitch eigenvalue estimate |(k7 − k6)/(u − g6)|_∞ (Hairer II p. 22) */
+static void tsit5_step(const ode_sys_t* S, int m, double t, double dt, const double* x, double* const* k,
+                       double* u, double rtol, double atol, double* EEst, double* eig, int* oob)
+{
+    double tmp[MAXK], tmp6[MAXK], buf[MAXK];
+    double *k1 = k[0], *k2 = k[1], *k3 = k[2], *k4 = k[3], *k5 = k[4], *k6 = k[5], *k7 = k[6];
+    double a = dt * A21;
+    for (int i = 0; i < m; i++) tmp[i] = fma(a, k1[i], x[i]);
+    S->f(S->ctx, fma(C1, dt, t), tmp, k2, oob);
+    for (int i = 0; i < m; i++) tmp[i] = fma(dt, fma(A31, k1[i], A32 * k2[i]), x[i]);
+    S->f(S->ctx, fma(C2, dt, t), tmp, k3, oob);
+    for (int i = 0; i < m; i++) tmp[i] = fma(dt, fma(A41, k1[i], fma(A42, k2[i], A43 * k3[i])), x[i]);
+    S->f(S->ctx, fma(C3, dt, t), tmp, k4, oob);
+    for (int i = 0; i < m; i++)
+        tmp[i] = fma(dt, fma(A51, k1[i], fma(A52, k2[i], fma(A53, k3[i], A54 * k4[i]))), x[i]);
+    S->f(S->ctx, fma(C4, dt, t), tmp, k5, oob);
+    for (int i = 0; i < m; i++)
+        tmp6[i] = fma(dt, fma(A61, k1[i], fma(A62, k2[i], fma(A63, k3[i], fma(A64, k4[i], A65 * k5[i])))), x[i]);
+    S->f(S->ctx, t + dt, tmp6, k6, oob);
+    for (int i = 0; i < m; i++)
+        u[i] = fma(dt, fma(A71, k1[i], fma(A72, k2[i], fma(A73, k3[i], fma(A74, k4[i], fma(A75, k5[i], A76 * k6[i]))))),
+                   x[i]);
+    S->f(S->ctx, t + dt, u, k7, oob);
+    double e = 0.0;
+    int e_nan = 0;
+    for (int i = 0; i < m; i++) {
+        double r = fabs((k7[i] - k6[i]) / (u[i] - tmp6[i]));
+        if (r != r) e_nan = 1;
+        else if (r > e) e = r;
+    }
+    *eig = e_nan ? NAN : e;
+    for (int i = 0; i < m; i++) {
+        double ut = dt * fma(BT1, k1[i],
+                             fma(BT2, k2[i], fma(BT3, k3[i], fma(BT4, k4[i], fma(BT5, k5[i], fma(BT6, k6[i], BT7 * k7[i]))))));
+        buf[i] = ut / fma(dmax(fabs(x[i]), fabs(u[i])), rtol, atol);
+    }
+    *EEst = rms_norm(buf, m);
+}
+
+/* One Rosenbrock23 step (perform_step!, Rosenbrock23Cache, @muladd), with
+ * W = J − I/(dt·d) (calc_W!, W_transform) factored once and the stages
+ * k = (W \ b)·(−1/(dt·d)); FSAL fsal = f(uprev, t); eigen_est = ‖J‖_∞. */
+static void ros23_step(const ode_sys_t* S, int m, double t, double dt, const double* x, const double* fsal,
+                       double* u, double* fnew, double* k1, double* k2, double rtol, double atol, double* EEst,
+                       double* eig, int* oob)
+{
+    double J[MAXJ * MAXJ], W[MAXJ * MAXJ], dT[MAXJ], b[MAXJ], f1[MAXJ], k3[MAXJ], tmp[MAXJ], buf[MAXJ];
+    int piv[MAXJ];
+    const double dtg = dt * ROS23_D;
+    const double invdtg = 1.0 / dtg, neginvdtg = -(1.0 / dtg);
+    const double dto2 = dt / 2.0, dto6 = dt / 6.0;
+    S->jac(S->ctx, t, x, J, dT, oob);
+    *eig = opnorm_inf(J, m);
+    for (int i = 0; i < m * m; i++) W[i] = J[i];
+    for (int i = 0; i < m; i++) W[i * m + i] = fma(-1.0, invdtg, J[i * m + i]);
+    lu_factor(W, m, piv);
+    for (int i = 0; i < m; i++) b[i] = fsal[i] + dtg * dT[i]; /* calc_tderivative!: linsolve_tmp */
+    lu_solve(W, piv, m, b);
+    for (int i = 0; i < m; i++) k1[i] = b[i] * neginvdtg;
+    for (int i = 0; i < m; i++) tmp[i] = fma(dto2, k1[i], x[i]);
+    S->f(S->ctx, t + dto2, tmp, f1, oob);
+    for (int i = 0; i < m; i++) b[i] = f1[i] - k1[i];
+    lu_solve(W, piv, m, b);
+    for (int i = 0; i < m; i++) k2[i] = fma(b[i], neginvdtg, k1[i]);
+    for (int i = 0; i < m; i++) u[i] = fma(dt, k2[i], x[i]);
+    S->f(S->ctx, t + dt, u, fnew, oob);
+    for (int i = 0; i < m; i++)
+        b[i] = fma(dt, dT[i], fma(-2.0, k1[i] - fsal[i], fma(-ROS23_C32, k2[i] - f1[i], fnew[i])));
+    lu_solve(W, piv, m, b);
+    for (int i = 0; i < m; i++) k3[i] = b[i] * neginvdtg;
+    for (int i = 0; i < m; i++) {
+        const double ut = dto6 * (fma(-2.0, k2[i], k1[i]) + k3[i]);
+        buf[i] = ut / fma(dmax(fabs(x[i]), fabs(u[i])), rtol, atol);
+    }
+    *EEst = rms_norm(buf, m);
 }
 
 /* kn == NULL: no knots kept (saveat problems keep only what on_step saves) */
-static int tsit5_solve_cb(rhs_fn f, void* ctx, int m, double t0, double t1, const double* x0, double rtol,
-                          double atol, int64_t maxiters, knots_t* kn, ode_stats_t* st, step_fn on_step,
-                          void* step_ctx)
+static int ode_solve_cb(const ode_sys_t* S, int m, double t0, double t1, const double* x0, double rtol, double atol,
+                        int64_t maxiters, knots_t* kn, ode_stats_t* st, step_fn on_step, void* step_ctx)
 {
-    double x[MAXK], k1[MAXK], k2[MAXK], k3[MAXK], k4[MAXK], k5[MAXK], k6[MAXK], k7[MAXK];
-    double tmp[MAXK], tmp6[MAXK], u[MAXK], sk[MAXK], buf[MAXK], f1[MAXK];
+    double x[MAXK], kk[7][MAXK], u[MAXK], sk[MAXK], buf[MAXK], f1[MAXK], fnew[MAXK];
+    double* const k[7] = {kk[0], kk[1], kk[2], kk[3], kk[4], kk[5], kk[6]};
+    double* fsal = kk[0]; /* k1 of Tsit5 = fsalfirst */
     int oob = 0;
     memset(st, 0, sizeof(*st));
     if (kn) kn->K = m;
     const double dtmax = t1 - t0;
     const double dtmin = sbr_jl_eps(dmax(fabs(t0), fabs(t1)));
 
-    /* ---- ode_determine_initdt (OrdinaryDiffEqCore initdt.jl) ---- */
+    /* ---- ode_determine_initdt (OrdinaryDiffEqCore initdt.jl, @muladd) ---- */
     for (int i = 0; i < m; i++) { x[i] = x0[i]; sk[i] = fma(fabs(x0[i]), rtol, atol); }
     for (int i = 0; i < m; i++) buf[i] = x0[i] / sk[i];
     double d0 = rms_norm(buf, m);
-    f(ctx, t0, x, k1, &oob);
-    for (int i = 0; i < m; i++) buf[i] = k1[i] / sk[i];
+    S->f(S->ctx, t0, x, fsal, &oob);
+    for (int i = 0; i < m; i++) buf[i] = fsal[i] / sk[i];
     double d1 = rms_norm(buf, m);
-    double dt0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * (d0 / d1);
+    double dt0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : (d0 / d1) / 100.0;
     dt0 = dmin(dt0, dtmax);
     double dt;
     if (dt0 < 10.0 * 2.220446049250313e-16) {
         dt = dmax(1e-6, dtmin);
     } else {
-        for (int i = 0; i < m; i++) u[i] = fma(dt0, k1[i], x0[i]);
-        f(ctx, t0 + dt0, u, f1, &oob);
+        for (int i = 0; i < m; i++) u[i] = fma(dt0, fsal[i], x0[i]);
+        S->f(S->ctx, t0 + dt0, u, f1, &oob);
         int same = 1;
-        for (int i = 0; i < m; i++) same &= (k1[i] == f1[i]);
+        for (int i = 0; i < m; i++) same &= (fsal[i] == f1[i]);
         if (same) {
             dt = dmax(dtmin, 100.0 * dt0);
         } else {
-            for (int i = 0; i < m; i++) buf[i] = (f1[i] - k1[i]) / sk[i];
+            for (int i = 0; i < m; i++) buf[i] = (f1[i] - fsal[i]) / sk[i];
             double d2 = rms_norm(buf, m) / dt0;
             double md = dmax(d1, d2);
+            /* 10^(-(2 + log10(md)) / get_current_alg_order) with Tsit5's order 5 */
+            /* dt₁ = (0.01/max(d₁, d₂))^(1/(p+1)) with p = 5 (Tsit5): the exponent 1/6
+             * is pinned by the committed Fig 5 heatmap — with 1/5 the 500² run mask
+             * gains cell (β₂₈₄, u₉₅), where the figure has no run */
             double dt1 = (md <= 1e-15) ? dmax(1e-6, dt0 * 1e-3) : sbr_pow_pos(0.01 / md, 1.0 / 6.0);
             dt = dmax(dtmin, dmin(dmin(100.0 * dt0, dt1), dtmax));
         }
     }
 
-    /* ---- main loop (solve! / loopheader! / loopfooter!) ---- */
-    const double LOG_QOLDMIN = sbr_log(CTL_QOLDMIN);
+    /* ---- main loop (solve! / loopheader! / perform_step! / loopfooter!) ---- */
     const double snap = 100.0 * sbr_jl_eps(t1);
-    double t = t0, qold = CTL_QOLDMIN, lqold = LOG_QOLDMIN;
+    double t = t0, qold = CTL_QOLDMIN;
+    double qold_b2 = sbr_fastpow(qold, CTL_BETA2); /* fastpower(qold, β2), refreshed when qold changes */
+    double eig = 1.0;                              /* integrator.eigen_est = 1/oneunit(t) at init */
     autoswitch_t as = {0, 0};
     st->t_switch = NAN;
     if (kn && knots_push(kn, t0, x)) return -1;
     int64_t iter = 0;
     while (t < t1) {
         if (++iter > maxiters) { st->status |= SBR_ODE_MAXITERS; break; }
-        dt = dmin(dtmax, dt);
+        /* choose_algorithm!: AutoSwitch on the current eigen_est and dt; the new
+         * algorithm's initialize! re-evaluates fsalfirst = f(uprev, t) */
+        if (autoswitch_choose(&as, eig, &dt)) {
+            st->nswitch++;
+            if (as.stiff && st->t_switch != st->t_switch) st->t_switch = t;
+            if (as.stiff && !S->jac) { st->status |= SBR_ODE_FAILED; break; }
+            S->f(S->ctx, t, x, fsal, &oob);
+        }
+        dt = dmin(dtmax, dt); /* fix_dt_at_bounds! */
         dt = dmax(dt, dtmin);
         dt = dmin(dt, t1 - t); /* modify_dt_for_tstops! */
 
-        double a = dt * A21;
-        for (int i = 0; i < m; i++) tmp[i] = fma(a, k1[i], x[i]);
-        f(ctx, fma(C1, dt, t), tmp, k2, &oob);
-        for (int i = 0; i < m; i++) tmp[i] = fma(dt, fma(A31, k1[i], A32 * k2[i]), x[i]);
-        f(ctx, fma(C2, dt, t), tmp, k3, &oob);
-        for (int i = 0; i < m; i++)
-            tmp[i] = fma(dt, fma(A41, k1[i], fma(A42, k2[i], A43 * k3[i])), x[i]);
-        f(ctx, fma(C3, dt, t), tmp, k4, &oob);
-        for (int i = 0; i < m; i++)
-            tmp[i] = fma(dt, fma(A51, k1[i], fma(A52, k2[i], fma(A53, k3[i], A54 * k4[i]))), x[i]);
-        f(ctx, fma(C4, dt, t), tmp, k5, &oob);
-        for (int i = 0; i < m; i++)
-            tmp6[i] = fma(dt, fma(A61, k1[i], fma(A62, k2[i], fma(A63, k3[i], fma(A64, k4[i], A65 * k5[i])))),
-                          x[i]);
-        f(ctx, t + dt, tmp6, k6, &oob);
-        for (int i = 0; i < m; i++)
-            u[i] = fma(dt,
-                       fma(A71, k1[i],
-                           fma(A72, k2[i], fma(A73, k3[i], fma(A74, k4[i], fma(A75, k5[i], A76 * k6[i]))))),
-                       x[i]);
-        f(ctx, t + dt, u, k7, &oob);
-        /* eigenvalue estimate for AutoSwitch: Inf-norm of |(k7-k6)/(u-tmp6)| */
-        double eig = 0.0;
-        int eig_nan = 0;
-        for (int i = 0; i < m; i++) {
-            double r = fabs((k7[i] - k6[i]) / (u[i] - tmp6[i]));
-            if (r != r) eig_nan = 1;
-            else if (r > eig) eig = r;
+        /* check_error!: dt forced to dtmin short of the end (ReturnCode.DtLessThanMin) */
+        if (dt <= dtmin && t + dt < t1) { st->status |= SBR_ODE_FAILED; break; }
+        double EEst;
+        if (as.stiff) {
+            st->nstiff++;
+            ros23_step(S, m, t, dt, x, fsal, u, fnew, k[1], k[2], rtol, atol, &EEst, &eig, &oob);
+        } else {
+            tsit5_step(S, m, t, dt, x, k, u, rtol, atol, &EEst, &eig, &oob);
         }
-        if (eig_nan) eig = NAN;
-        /* error estimate */
-        for (int i = 0; i < m; i++) {
-            double ut = dt * fma(BT1, k1[i],
-                                 fma(BT2, k2[i],
-                                     fma(BT3, k3[i], fma(BT4, k4[i], fma(BT5, k5[i], fma(BT6, k6[i], BT7 * k7[i]))))));
-            buf[i] = ut / fma(dmax(fabs(x[i]), fabs(u[i])), rtol, atol);
-        }
-        double EEst = rms_norm(buf, m);
-        /* stepsize_controller!(PIController): q = EEst^β1 / qold^β2 / γ clamped to
-         * [1/qmax, 1/qmin], evaluated as one exponential exp(β1 log EEst − β2 log qold)
-         * (OrdinaryDiffEq uses DiffEqBase.fastpow, a Float32 approximation, for both
-         * powers).  log(qold) is carried from the step that set qold. */
-        double q, le = 0.0;
+        if (EEst != EEst) { st->status |= SBR_ODE_FAILED; break; } /* NaN trial state: Unstable */
+        /* stepsize_controller!(PIController): q11 = fastpower(EEst, β1),
+         * q = q11 / fastpower(qold, β2), clamped q/γ (FastPower 1.1.3) */
+        double q, q11 = 0.0;
         if (EEst == 0.0) {
             q = CTL_INV_QMAX;
         } else {
-            le = sbr_log(EEst);
-            q = sbr_exp(CTL_BETA1 * le - CTL_BETA2 * lqold);
+#ifdef SBRO_DIAG_EXACTPOW
+            q11 = sbr_exp(CTL_BETA1 * sbr_log(EEst));
+            q = sbr_exp(CTL_BETA1 * sbr_log(EEst) - CTL_BETA2 * sbr_log(qold));
+#else
+            q11 = sbr_fastpow(EEst, CTL_BETA1);
+            q = q11 / qold_b2;
+#endif
             q = dmax(CTL_INV_QMAX, dmin(CTL_INV_QMIN, q / CTL_GAMMA));
         }
-        if (EEst <= 1.0) { /* accept */
+        if (EEst <= 1.0) { /* accept: step_accept_controller!, apply_step! */
             st->naccept++;
             double dtnew = dt / q;
-            qold = dmax(EEst, CTL_QOLDMIN);
-            lqold = (qold == EEst) ? le : LOG_QOLDMIN;
+            const double qn = dmax(EEst, CTL_QOLDMIN);
+            if (qn != qold) { qold = qn; qold_b2 = sbr_fastpow(qold, CTL_BETA2); }
             double tn = t + dt;
             if (fabs(tn - t1) < snap) tn = t1; /* 100 eps(max(t, t_end)), t < t_end */
             if (on_step) {
-                const double* const ks[7] = {k1, k2, k3, k4, k5, k6, k7};
-                on_step(step_ctx, t, tn, dt, x, u, ks);
+                if (as.stiff) {
+                    const double* const ks[2] = {k[1], k[2]};
+                    on_step(step_ctx, t, tn, dt, x, u, ks, 1);
+                } else {
+                    const double* const ks[7] = {k[0], k[1], k[2], k[3], k[4], k[5], k[6]};
+                    on_step(step_ctx, t, tn, dt, x, u, ks, 0);
+                }
             }
             t = tn;
-            for (int i = 0; i < m; i++) { x[i] = u[i]; k1[i] = k7[i]; }
+            const double* fl = as.stiff ? fnew : k[6]; /* fsallast */
+            for (int i = 0; i < m; i++) { x[i] = u[i]; fsal[i] = fl[i]; }
             dt = dmax(dmin(dtmax, dtnew), dtmin); /* calc_dt_propose! */
             if (kn && knots_push(kn, t, x)) return -1;
-        } else { /* reject: step_reject_controller!, q11 = EEst^β1 */
+        } else { /* reject: step_reject_controller!, dt /= min(1/qmin, q11/γ) */
             st->nreject++;
-            const double q11 = sbr_exp(CTL_BETA1 * le);
             dt = dt / dmin(CTL_INV_QMIN, q11 / CTL_GAMMA);
         }
         if (!(dt > 0.0) || !isfinite(dt)) { st->status |= SBR_ODE_FAILED; break; }
-        autoswitch_update(&as, eig, dt);
-        if (as.switched && st->t_switch != st->t_switch) st->t_switch = t;
     }
-    if (as.switched) st->status |= SBR_STIFF_SWITCH;
+    if (st->nswitch > 0) st->status |= SBR_STIFF_SWITCH;
     if (oob) st->status |= SBR_OOB;
     return 0;
+}
+
+static int ode_solve(const ode_sys_t* S, int m, double t0, double t1, const double* x0, double rtol, double atol,
+                     int64_t maxiters, knots_t* kn, ode_stats_t* st)
+{
+    return ode_solve_cb(S, m, t0, t1, x0, rtol, atol, maxiters, kn, st, NULL, NULL);
 }
 
 /* ------------------------------------------------------------------------ */
@@ -356,17 +539,37 @@ static void rhs_logistic(void* ctx, double t, const double* x, double* dx, int* 
     dx[0] = (beta * x[0]) * (1.0 - x[0]);
 }
 
+/* ForwardDiff through (β·x)·(1 − x): partials β and −1, product rule
+ * β·(1 − x) + (−1)·(β·x); autonomous: ∂f/∂t = 0 */
+static void jac_logistic(void* ctx, double t, const double* x, double* J, double* dT, int* oob)
+{
+    (void)t; (void)oob;
+    double beta = *(const double*)ctx;
+    J[0] = beta * (1.0 - x[0]) + (-1.0) * (beta * x[0]);
+    dT[0] = 0.0;
+}
+
+static const ode_sys_t* sys_logistic(double* beta, ode_sys_t* S)
+{
+    S->f = rhs_logistic; S->jac = jac_logistic; S->ctx = beta;
+    return S;
+}
+
 int64_t sbro_learn_logistic(double beta, double t0, double t1, double x0, double rtol, double atol,
                             int64_t maxiters, double* t_out, double* G_out, int64_t cap, int64_t* stats)
 {
     knots_t kn = {0};
     ode_stats_t st;
-    if (tsit5_solve(rhs_logistic, &beta, 1, t0, t1, &x0, rtol, atol, maxiters, &kn, &st)) {
+    ode_sys_t S;
+    if (ode_solve(sys_logistic(&beta, &S), 1, t0, t1, &x0, rtol, atol, maxiters, &kn, &st)) {
         knots_free(&kn);
         return -1;
     }
     int64_t n = kn.n;
-    if (stats) { stats[0] = st.naccept; stats[1] = st.nreject; stats[2] = st.status; stats[3] = n; }
+    if (stats) {
+        stats[0] = st.naccept; stats[1] = st.nreject; stats[2] = st.status; stats[3] = n;
+        memcpy(&stats[4], &st.t_switch, 8); stats[5] = st.nswitch; stats[6] = st.nstiff;
+    }
     if (n > cap) n = -n; /* caller buffer too small: return -needed */
     else {
         memcpy(t_out, kn.t, (size_t)kn.n * sizeof(double));
@@ -599,10 +802,11 @@ int sbro_sweep_baseline(const double* beta, const double* eta, const double* t_e
     for (int64_t b = 0; b < n_beta; b++) {
         knots_t kn = {0};
         ode_stats_t st;
+        ode_sys_t S;
         double x0v = x0;
         double bb = beta[b];
-        if (tsit5_solve(rhs_logistic, &bb, 1, 0.0, t_end[b], &x0v, 2.220446049250313e-16, 2.220446049250313e-16,
-                        SBR_DEFAULT_ODE_MAXITERS, &kn, &st)) { err |= 1; continue; }
+        if (ode_solve(sys_logistic(&bb, &S), 1, 0.0, t_end[b], &x0v, 2.220446049250313e-16, 2.220446049250313e-16,
+                      SBR_DEFAULT_ODE_MAXITERS, &kn, &st)) { err |= 1; continue; }
         if (nknots) nknots[b] = kn.n;
         int64_t n = kn.n;
         double* g = (double*)malloc((size_t)n * sizeof(double));
@@ -645,6 +849,12 @@ void sbro_apply_early_exit(int64_t n_beta, int64_t n_u, int32_t threshold, doubl
     }
 }
 
+/* FastPower.fastpower as the controller uses it (tests compare it against the device) */
+void sbro_fastpow(const double* x, const double* y, int64_t n, double* out)
+{
+    for (int64_t i = 0; i < n; i++) out[i] = sbr_fastpow(x[i], y[i]);
+}
+
 /* detmath exports (tests compare them against numpy and against the device) */
 void sbro_detmath(const double* x, const double* y, int64_t n, double* e, double* l, double* pw)
 {
@@ -676,6 +886,25 @@ static void rhs_hetero(void* ctx, double t, const double* I, double* du, int* oo
     for (int k = 0; k < h->K; k++) du[k] = ((1.0 - I[k]) * h->betas[k]) * w;
 }
 
+/* ForwardDiff jacobian of rhs_hetero: with b_k = (1 − I_k)·β_k (partials −β_k
+ * in slot k) and ω (partials dist_j), the product rule gives
+ * J_kj = dist_j·b_k (j ≠ k; the −0.0 partial adds nothing) and
+ * J_kk = (−β_k)·ω + dist_k·b_k; autonomous: ∂f/∂t = 0 */
+static void jac_hetero(void* ctx, double t, const double* I, double* J, double* dT, int* oob)
+{
+    (void)t; (void)oob;
+    const hetero_ctx* h = (const hetero_ctx*)ctx;
+    const int K = h->K;
+    double w = h->dist[0] * I[0];
+    for (int j = 1; j < K; j++) w = w + h->dist[j] * I[j];
+    for (int k = 0; k < K; k++) {
+        const double bk = (1.0 - I[k]) * h->betas[k];
+        for (int j = 0; j < K; j++) J[k * K + j] = h->dist[j] * bk;
+        J[k * K + k] = (-h->betas[k]) * w + h->dist[k] * bk;
+        dT[k] = 0.0;
+    }
+}
+
 int64_t sbro_learn_hetero(const double* betas, const double* dist, int32_t K, double t1, double x0, double* t_out,
                           double* G_out, int64_t cap, int64_t* stats)
 {
@@ -684,15 +913,16 @@ int64_t sbro_learn_hetero(const double* betas, const double* dist, int32_t K, do
     double x0v[MAXK];
     for (int k = 0; k < K; k++) x0v[k] = x0;
     hetero_ctx hc = {K, betas, dist};
+    const ode_sys_t S = {rhs_hetero, K <= MAXJ ? jac_hetero : NULL, &hc};
     const double e = 2.220446049250313e-16;
-    if (K < 1 || K > MAXK || tsit5_solve(rhs_hetero, &hc, K, 0.0, t1, x0v, e, e, SBR_DEFAULT_ODE_MAXITERS, &kn, &st)) {
+    if (K < 1 || K > MAXK || ode_solve(&S, K, 0.0, t1, x0v, e, e, SBR_DEFAULT_ODE_MAXITERS, &kn, &st)) {
         knots_free(&kn);
         return -1;
     }
     int64_t n = kn.n;
     if (stats) {
         stats[0] = st.naccept; stats[1] = st.nreject; stats[2] = st.status; stats[3] = n;
-        memcpy(&stats[4], &st.t_switch, 8);
+        memcpy(&stats[4], &st.t_switch, 8); stats[5] = st.nswitch; stats[6] = st.nstiff;
     }
     if (n > cap) n = -n;
     else {
@@ -824,8 +1054,9 @@ int sbro_sweep_hetero(int32_t K, const double* betas, const double* dist, const 
         double x0v[MAXK];
         for (int k = 0; k < K; k++) x0v[k] = x0;
         hetero_ctx hc = {K, bk, dist};
+        const ode_sys_t S = {rhs_hetero, K <= MAXJ ? jac_hetero : NULL, &hc};
         const double e = 2.220446049250313e-16;
-        if (tsit5_solve(rhs_hetero, &hc, K, 0.0, t_end[c], x0v, e, e, SBR_DEFAULT_ODE_MAXITERS, &kn, &st)) { err |= 1; continue; }
+        if (ode_solve(&S, K, 0.0, t_end[c], x0v, e, e, SBR_DEFAULT_ODE_MAXITERS, &kn, &st)) { err |= 1; continue; }
         int64_t n = kn.n;
         if (nknots) nknots[c] = n;
         /* compute_pdf_hetero: pdf_k = (1 − I_k) β_k ω at the knots */
@@ -907,6 +1138,17 @@ static void rhs_social(void* ctx, double t, const double* x, double* dx, int* oo
     dx[0] = ((1.0 - x[0]) * s->beta) * aw;
 }
 
+/* ForwardDiff: J = ((−1)·β)·AW_old(t); ∂f/∂t = ((1 − I)·β)·AW_old'(t) with the
+ * interpolant's dual-number slope (interp_dx) */
+static void jac_social(void* ctx, double t, const double* x, double* J, double* dT, int* oob)
+{
+    const social_ctx* s = (const social_ctx*)ctx;
+    const double aw = interp_s(s->t, s->v, 1, s->n, t, oob);
+    const double awp = interp_dx(s->t, s->v, 1, s->n, t, oob);
+    J[0] = ((-1.0) * s->beta) * aw;
+    dT[0] = ((1.0 - x[0]) * s->beta) * awp;
+}
+
 /* One (β, u) point of solve_equilibrium_social_learning (social_learning_solver.jl:63-263).
  * tspan = (0, η) (:79); cmp = range(0, η, length=n_cmp) supplied by the caller
  * (:103).  Returns the last inner SolvedModel's fields (:262) like the
@@ -931,8 +1173,9 @@ static void social_point(double beta, double eta, double x0, double u, double p,
     /* initial guess: baseline SI learning on (0, η); AW_old = G on its knots (:89-94) */
     knots_t old = {0};
     ode_stats_t st;
+    ode_sys_t S0;
     double x0v = x0, bb = beta;
-    if (tsit5_solve(rhs_logistic, &bb, 1, 0.0, eta, &x0v, e, e, SBR_DEFAULT_ODE_MAXITERS, &old, &st)) {
+    if (ode_solve(sys_logistic(&bb, &S0), 1, 0.0, eta, &x0v, e, e, SBR_DEFAULT_ODE_MAXITERS, &old, &st)) {
         out->status = SBR_ODE_FAILED; knots_free(&old); return;
     }
     ode_bits |= st.status & (SBR_ODE_MAXITERS | SBR_STIFF_SWITCH | SBR_ODE_FAILED | SBR_OOB);
@@ -944,8 +1187,9 @@ static void social_point(double beta, double eta, double x0, double u, double p,
         /* (a) learning from withdrawals: tspan (0, η), eps tolerances (:128-130) */
         knots_t kn = {0};
         social_ctx sc = {beta, old.t, old.x, old.n};
+        const ode_sys_t S = {rhs_social, jac_social, &sc};
         x0v = x0;
-        if (tsit5_solve(rhs_social, &sc, 1, 0.0, eta, &x0v, e, e, SBR_DEFAULT_ODE_MAXITERS, &kn, &st)) {
+        if (ode_solve(&S, 1, 0.0, eta, &x0v, e, e, SBR_DEFAULT_ODE_MAXITERS, &kn, &st)) {
             out->status = SBR_ODE_FAILED; knots_free(&kn); break;
         }
         s_acc += st.naccept; s_rej += st.nreject;
@@ -1151,6 +1395,20 @@ static void rhs_value(void* ctx, double t, const double* V, double* dV, int* oob
     dV[0] = (h + c->delta) * (1.0 - V[0]) + re;
 }
 
+/* ForwardDiff: max(x, 0.0) on a Dual keeps x (and its partials) iff 0 < x
+ * (isless), else the constant 0.0; J = −(h + δ) + (r | 0),
+ * ∂f/∂τ̄ = h'·(1 − V) + (−h' | 0) with h' the HR interpolant's slope */
+static void jac_value(void* ctx, double t, const double* V, double* J, double* dT, int* oob)
+{
+    const vf_ctx* c = (const vf_ctx*)ctx;
+    const double h = INTERP(c->tau, c->hr, c->n, t, oob);
+    const double hp = interp_dx(c->tau, c->hr, 1, c->n, t, oob);
+    const double x = (c->u + c->r * V[0]) - h;
+    const int keep = (x != x) || (x > 0.0);
+    J[0] = (h + c->delta) * (-1.0) + (keep ? c->r : 0.0);
+    dT[0] = hp * (1.0 - V[0]) + (keep ? -hp : 0.0);
+}
+
 typedef struct {
     const double* grid; /* saveat = the HR grid */
     int64_t n, next;
@@ -1159,13 +1417,24 @@ typedef struct {
 
 /* savevalues! with saveat: every pending point ≤ t, interpolated at
  * Θ = (s − tprev)/dt unless it is t itself (then the step's u) */
+/* Rosenbrock23's dense output (_ode_interpolant, @muladd):
+ * y0 + dt·(c1·k1 + c2·k2), c1 = Θ(1 − Θ)/(1 − 2d), c2 = Θ(Θ − 2d)/(1 − 2d) */
+static double ros23_dense(double th, double dt, double y0, const double* const* k)
+{
+    const double omd = 1.0 - 2.0 * ROS23_D;
+    const double c1 = (th * (1.0 - th)) / omd;
+    const double c2 = (th * fma(-2.0, ROS23_D, th)) / omd;
+    return fma(dt, fma(c1, k[0][0], c2 * k[1][0]), y0);
+}
+
 static void saveat_step(void* ctx, double tprev, double t, double dt, const double* y0, const double* y1,
-                        const double* const* k)
+                        const double* const* k, int stiff)
 {
     saveat_t* s = (saveat_t*)ctx;
     while (s->next < s->n && s->grid[s->next] <= t) {
         const double ts = s->grid[s->next];
-        s->V[s->next++] = (ts != t) ? tsit5_dense((ts - tprev) / dt, dt, y0[0], k) : y1[0];
+        const double th = (ts - tprev) / dt;
+        s->V[s->next++] = (ts != t) ? (stiff ? ros23_dense(th, dt, y0[0], k) : tsit5_dense(th, dt, y0[0], k)) : y1[0];
     }
 }
 
@@ -1179,7 +1448,8 @@ static int64_t value_function(const hazard_t* h, double delta, double r, double 
     saveat_t sv = {h->tau, h->n, 1, V};
     V[0] = V0; /* save_start: τ̄_1 = 0 = tspan[1] */
     const double eps = 2.220446049250313e-16;
-    tsit5_solve_cb(rhs_value, &c, 1, 0.0, h->tau[h->n - 1], &V0, eps, eps, maxiters, NULL, st, saveat_step, &sv);
+    const ode_sys_t S = {rhs_value, jac_value, &c};
+    ode_solve_cb(&S, 1, 0.0, h->tau[h->n - 1], &V0, eps, eps, maxiters, NULL, st, saveat_step, &sv);
     return sv.next;
 }
 
@@ -1256,8 +1526,9 @@ int sbro_sweep_interest(const double* beta, const double* eta, const double* t_e
         const double eps = 2.220446049250313e-16;
         knots_t kn = {0};
         ode_stats_t st;
+        ode_sys_t S;
         double bt = beta[b];
-        if (tsit5_solve(rhs_logistic, &bt, 1, 0.0, t_end[b], &x0, eps, eps, SBR_DEFAULT_ODE_MAXITERS, &kn, &st)) {
+        if (ode_solve(sys_logistic(&bt, &S), 1, 0.0, t_end[b], &x0, eps, eps, SBR_DEFAULT_ODE_MAXITERS, &kn, &st)) {
             rc |= 1;
             continue;
         }
@@ -1293,7 +1564,8 @@ int64_t sbro_interest_point(double beta, double eta, double t_end, double x0, do
     const double eps = 2.220446049250313e-16;
     knots_t kn = {0};
     ode_stats_t st;
-    if (tsit5_solve(rhs_logistic, &beta, 1, 0.0, t_end, &x0, eps, eps, SBR_DEFAULT_ODE_MAXITERS, &kn, &st)) return -1;
+    ode_sys_t S;
+    if (ode_solve(sys_logistic(&beta, &S), 1, 0.0, t_end, &x0, eps, eps, SBR_DEFAULT_ODE_MAXITERS, &kn, &st)) return -1;
     double* g = (double*)malloc((size_t)kn.n * sizeof(double));
     for (int64_t i = 0; i < kn.n; i++) g[i] = (beta * kn.x[i]) * (1.0 - kn.x[i]);
     hazard_t h;

@@ -18,6 +18,7 @@
 // Bit-exact against oracle/sbr_oracle.c (see sbr_device.h).
 #include "sbr_device.h"
 #include "sbr_kernels.h"
+#include "sbr_ode.h"
 #include "sbr_scan.h"
 
 namespace sbr {
@@ -47,33 +48,6 @@ __global__ __launch_bounds__(64) void learn_logistic_kernel(const double* __rest
         L.n_knots[b] = 0; L.n_tau[b] = 0; L.n_le[b] = 0; L.n_accept[b] = 0; L.n_reject[b] = 0;
         return;
     }
-    const double x0 = a.x0, rtol = a.rtol, atol = a.atol;
-    const double dtmax = T1 - T0;
-    const double dtmin = sbr_jl_eps(dmax(fabs(T0), fabs(T1)));
-
-    // ---- ode_determine_initdt ----
-    const double sk = fma(fabs(x0), rtol, atol);
-    const double d0 = fabs(x0 / sk);
-    double k1 = (BETA * x0) * (1.0 - x0);
-    const double d1 = fabs(k1 / sk);
-    double dt0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * (d0 / d1);
-    dt0 = dmin(dt0, dtmax);
-    double dt;
-    if (dt0 < 10.0 * DBL_EPS) {
-        dt = dmax(1e-6, dtmin);
-    } else {
-        const double u1 = fma(dt0, k1, x0);
-        const double f1 = (BETA * u1) * (1.0 - u1);
-        if (k1 == f1) {
-            dt = dmax(dtmin, 100.0 * dt0);
-        } else {
-            const double d2 = fabs((f1 - k1) / sk) / dt0;
-            const double md = dmax(d1, d2);
-            const double dt1 = (md <= 1e-15) ? dmax(1e-6, dt0 * 1e-3) : sbr_pow_pos(0.01 / md, 1.0 / 6.0);
-            dt = dmax(dtmin, dmin(dmin(100.0 * dt0, dt1), dtmax));
-        }
-    }
-
     // ---- knot sink: store (t, G); the hazard stage runs afterwards in parallel ----
     double tlast = 0.0, bound = -INFINITY;
     bool past = false, done = false;
@@ -89,71 +63,21 @@ __global__ __launch_bounds__(64) void learn_logistic_kernel(const double* __rest
         n++;
         if (a.stop_after_eta && past && t >= bound) done = true;
     };
-
-    const double LOG_QOLDMIN = sbr_log(CTL_QOLDMIN);
-    const double snap = 100.0 * sbr_jl_eps(T1); // fixed_t_for_floatingpoint_error!: t < t_end
-    double t = T0, x = x0, qold = CTL_QOLDMIN, lqold = LOG_QOLDMIN;
-    AutoSwitch as;
-    const ConstDiv by_gamma(CTL_GAMMA);
-    int naccept = 0, nreject = 0;
-    push(t, x);
-    int64_t iter = 0;
-    while (t < T1 && !done) {
-        if (++iter > a.maxiters) { st |= SBR_ODE_MAXITERS; break; }
-        dt = dmin(dtmax, dt);
-        dt = dmax(dt, dtmin);
-        dt = dmin(dt, T1 - t);
-
-        const double a21 = dt * A21;
-        double tmp = fma(a21, k1, x);
-        const double k2 = (BETA * tmp) * (1.0 - tmp);
-        tmp = fma(dt, fma(A31, k1, A32 * k2), x);
-        const double k3 = (BETA * tmp) * (1.0 - tmp);
-        tmp = fma(dt, fma(A41, k1, fma(A42, k2, A43 * k3)), x);
-        const double k4 = (BETA * tmp) * (1.0 - tmp);
-        tmp = fma(dt, fma(A51, k1, fma(A52, k2, fma(A53, k3, A54 * k4))), x);
-        const double k5 = (BETA * tmp) * (1.0 - tmp);
-        const double tmp6 = fma(dt, fma(A61, k1, fma(A62, k2, fma(A63, k3, fma(A64, k4, A65 * k5)))), x);
-        const double k6 = (BETA * tmp6) * (1.0 - tmp6);
-        const double u =
-            fma(dt, fma(A71, k1, fma(A72, k2, fma(A73, k3, fma(A74, k4, fma(A75, k5, A76 * k6))))), x);
-        const double k7 = (BETA * u) * (1.0 - u);
-        const double eigr = fabs((k7 - k6) / (u - tmp6));
-        const double eig = (eigr != eigr) ? (double)NAN : eigr;
-        const double ut =
-            dt * fma(BT1, k1, fma(BT2, k2, fma(BT3, k3, fma(BT4, k4, fma(BT5, k5, fma(BT6, k6, BT7 * k7))))));
-        const double EEst = fabs(ut / fma(dmax(fabs(x), fabs(u)), rtol, atol));
-        // stepsize_controller!(PIController) with log(qold) carried over from the
-        // step that set qold: same operations as pi_q (sbr_pow_pos = exp(y·log x)).
-        double q, le = 0.0;
-        if (EEst == 0.0) {
-            q = CTL_INV_QMAX;
-        } else {
-            le = sbr_log(EEst);
-            q = sbr_exp(CTL_BETA1 * le - CTL_BETA2 * lqold);
-            q = dmax(CTL_INV_QMAX, dmin(CTL_INV_QMIN, by_gamma(q)));
+    struct Sink {
+        decltype(push)& p;
+        bool& done;
+        __device__ __forceinline__ bool start(double t, double x) { p(t, x); return !done; }
+        __device__ __forceinline__ bool accept(double, double tn, double, double, double y1, const StepK&, bool)
+        {
+            p(tn, y1);
+            return !done;
         }
-        if (EEst <= 1.0) {
-            naccept++;
-            const double dtnew = dt / q;
-            qold = dmax(EEst, CTL_QOLDMIN);
-            lqold = (qold == EEst) ? le : LOG_QOLDMIN;
-            double tn = t + dt;
-            if (fabs(tn - T1) < snap) tn = T1;
-            t = tn;
-            x = u;
-            k1 = k7;
-            dt = dmax(dmin(dtmax, dtnew), dtmin);
-            push(t, x);
-        } else {
-            nreject++;
-            const double q11 = sbr_exp(CTL_BETA1 * le);
-            dt = dt / dmin(CTL_INV_QMIN, by_gamma(q11));
-        }
-        if (!(dt > 0.0) || !isfinite(dt)) { st |= SBR_ODE_FAILED; break; }
-        as.update(eig, dt);
-    }
-    if (as.switched) st |= SBR_STIFF_SWITCH;
+    } sink{push, done};
+    LogisticSys f{BETA};
+    OdeOut o;
+    ode_scalar(f, sink, T1, a.x0, a.rtol, a.atol, a.maxiters, o);
+    st |= o.status;
+    const int naccept = (int)o.naccept, nreject = (int)o.nreject;
     L.n_knots[b] = n;
     L.status[b] = st;
     L.n_accept[b] = naccept;
@@ -644,12 +568,35 @@ struct ValueRhs {
         const int j = (tau[jb] <= t) ? ssl_gallop(tau, ntau, jb, t) : ssl_range(tau, 0, jb, t);
         return lerp_at(tau, H, ntau, j, t);
     }
-    __device__ __forceinline__ double operator()(double t, double V)
+    __device__ __forceinline__ double eval(double t, double V)
     {
         const double h = hr(t);
         const double x = (u + r * V) - h;
         const double re = (x != x) ? x : (x > 0.0 ? x : 0.0); // Julia max(x, 0.0)
         return (h + delta) * (1.0 - V) + re;
+    }
+    __device__ __forceinline__ void prepare(double, double) {}
+    __device__ __forceinline__ double stage(int, double ts, double V) { return eval(ts, V); }
+    // ForwardDiff (oracle jac_value): max(x, 0.0) on a Dual keeps x iff 0 < x (or NaN);
+    // J = −(h + δ) + (r | 0), ∂f/∂τ̄ = h'·(1 − V) + (−h' | 0), h' the HR interpolant's slope
+    __device__ __forceinline__ void jac(double t, double V, double& J, double& dT)
+    {
+        double h = (double)NAN, hp = (double)NAN;
+        if (ntau < 2 || !(t >= tlo && t <= thi)) {
+            oob = true;
+        } else {
+            int j = (tau[jb] <= t) ? ssl_gallop(tau, ntau, jb, t) : ssl_range(tau, 0, jb, t);
+            j = j > ntau - 2 ? ntau - 2 : (j < 0 ? 0 : j);
+            const double t0 = tau[j], t1 = tau[j + 1], h0 = H[j], h1 = H[j + 1];
+            const double d = (t - t0) / (t1 - t0);
+            h = h0 * (1.0 - d) + h1 * d;
+            const double rr = 1.0 / (t1 - t0);
+            hp = h0 * (-rr) + h1 * rr;
+        }
+        const double x = (u + r * V) - h;
+        const bool keep = (x != x) || (x > 0.0);
+        J = (h + delta) * (-1.0) + (keep ? r : 0.0);
+        dT = hp * (1.0 - V) + (keep ? -hp : 0.0);
     }
     __device__ __forceinline__ void accepted(double t)
     {
@@ -722,98 +669,6 @@ struct SaveScan {
     }
 };
 
-// Tsit5 (oracle tsit5_solve_cb, m = 1) with the accepted-step hook on_step(tprev, t, dt,
-// uprev, u, k1..k7) that OrdinaryDiffEq's savevalues! sees.
-template <class Rhs, class OnStep>
-__device__ __forceinline__ void tsit5_hooked(Rhs& f, OnStep& on_step, double T1, double x0, double rtol,
-                                             double atol, int64_t maxiters, uint32_t& status, int64_t& nsteps)
-{
-    const double T0 = 0.0;
-    const double dtmax = T1 - T0;
-    const double dtmin = sbr_jl_eps(dmax(fabs(T0), fabs(T1)));
-    const double sk = fma(fabs(x0), rtol, atol);
-    const double d0 = fabs(x0 / sk);
-    double k1 = f(T0, x0);
-    const double d1 = fabs(k1 / sk);
-    double dt0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * (d0 / d1);
-    dt0 = dmin(dt0, dtmax);
-    double dt;
-    if (dt0 < 10.0 * DBL_EPS) {
-        dt = dmax(1e-6, dtmin);
-    } else {
-        const double u1 = fma(dt0, k1, x0);
-        const double f1 = f(T0 + dt0, u1);
-        if (k1 == f1) {
-            dt = dmax(dtmin, 100.0 * dt0);
-        } else {
-            const double d2 = fabs((f1 - k1) / sk) / dt0;
-            const double md = dmax(d1, d2);
-            const double dt1 = (md <= 1e-15) ? dmax(1e-6, dt0 * 1e-3) : sbr_pow_pos(0.01 / md, 1.0 / 6.0);
-            dt = dmax(dtmin, dmin(dmin(100.0 * dt0, dt1), dtmax));
-        }
-    }
-    const double LOG_QOLDMIN = sbr_log(CTL_QOLDMIN);
-    const double snap = 100.0 * sbr_jl_eps(T1);
-    double t = T0, x = x0, lqold = LOG_QOLDMIN;
-    AutoSwitch as;
-    const ConstDiv by_gamma(CTL_GAMMA);
-    int64_t iter = 0, nacc = 0, nrej = 0;
-    while (t < T1) {
-        if (++iter > maxiters) { status |= SBR_ODE_MAXITERS; break; }
-        dt = dmin(dtmax, dt);
-        dt = dmax(dt, dtmin);
-        dt = dmin(dt, T1 - t);
-        double tmp = fma(dt * A21, k1, x);
-        const double k2 = f(fma(C1, dt, t), tmp);
-        tmp = fma(dt, fma(A31, k1, A32 * k2), x);
-        const double k3 = f(fma(C2, dt, t), tmp);
-        tmp = fma(dt, fma(A41, k1, fma(A42, k2, A43 * k3)), x);
-        const double k4 = f(fma(C3, dt, t), tmp);
-        tmp = fma(dt, fma(A51, k1, fma(A52, k2, fma(A53, k3, A54 * k4))), x);
-        const double k5 = f(fma(C4, dt, t), tmp);
-        const double tmp6 = fma(dt, fma(A61, k1, fma(A62, k2, fma(A63, k3, fma(A64, k4, A65 * k5)))), x);
-        const double k6 = f(t + dt, tmp6);
-        const double u =
-            fma(dt, fma(A71, k1, fma(A72, k2, fma(A73, k3, fma(A74, k4, fma(A75, k5, A76 * k6))))), x);
-        const double k7 = f(t + dt, u);
-        const double eigr = fabs((k7 - k6) / (u - tmp6));
-        const double eig = (eigr != eigr) ? (double)NAN : eigr;
-        const double ut =
-            dt * fma(BT1, k1, fma(BT2, k2, fma(BT3, k3, fma(BT4, k4, fma(BT5, k5, fma(BT6, k6, BT7 * k7))))));
-        const double EEst = fabs(ut / fma(dmax(fabs(x), fabs(u)), rtol, atol));
-        double q, le = 0.0;
-        if (EEst == 0.0) {
-            q = CTL_INV_QMAX;
-        } else {
-            le = sbr_log(EEst);
-            q = sbr_exp(CTL_BETA1 * le - CTL_BETA2 * lqold);
-            q = dmax(CTL_INV_QMAX, dmin(CTL_INV_QMIN, by_gamma(q)));
-        }
-        if (EEst <= 1.0) {
-            nacc++;
-            const double dtnew = dt / q;
-            const double qold = dmax(EEst, CTL_QOLDMIN);
-            lqold = (qold == EEst) ? le : LOG_QOLDMIN;
-            double tn = t + dt;
-            if (fabs(tn - T1) < snap) tn = T1;
-            on_step(t, tn, dt, x, u, k1, k2, k3, k4, k5, k6, k7);
-            t = tn;
-            x = u;
-            k1 = k7;
-            dt = dmax(dmin(dtmax, dtnew), dtmin);
-            f.accepted(t);
-        } else {
-            nrej++;
-            const double q11 = sbr_exp(CTL_BETA1 * le);
-            dt = dt / dmin(CTL_INV_QMIN, by_gamma(q11));
-        }
-        if (!(dt > 0.0) || !isfinite(dt)) { status |= SBR_ODE_FAILED; break; }
-        as.update(eig, dt);
-    }
-    if (as.switched) status |= SBR_STIFF_SWITCH;
-    nsteps = nacc + nrej;
-}
-
 // solve_equilibrium_interest (interest_rate_solver.jl:51-150) for one u with r > 0:
 // V on the HR grid, optimal_buffer on h − rV, then the baseline's compute_ξ / AW.
 template <class P>
@@ -831,15 +686,31 @@ __device__ __forceinline__ void solve_interest_point(P T, P G, P H, const Summ& 
     const double V0 = (u + ia.delta) / (ia.r + ia.delta);
     SaveScan<P> sv{tau, H, ntau, ia.r, u, ia.v_path};
     sv.init(V0);
-    auto on_step = [&](double tprev, double tn, double dt, double y0, double y1, double k1, double k2, double k3,
-                       double k4, double k5, double k6, double k7) {
-        while (sv.next < ntau && tau[sv.next] <= tn) {
-            const double ts = tau[sv.next];
-            sv.save(ts != tn ? tsit5_dense((ts - tprev) / dt, dt, y0, k1, k2, k3, k4, k5, k6, k7) : y1);
+    // savevalues! with saveat = the HR grid: each pending grid point ≤ the new t is the
+    // step's dense output at Θ = (s − tprev)/dt (Tsit5's or Rosenbrock23's), or u itself at t
+    struct Saver {
+        SaveScan<P>& sv;
+        const TauView<P>& tau;
+        int ntau;
+        __device__ __forceinline__ bool start(double, double) { return true; }
+        __device__ __forceinline__ bool accept(double tprev, double tn, double dt, double y0, double y1,
+                                               const StepK& K, bool)
+        {
+            while (sv.next < ntau && tau[sv.next] <= tn) {
+                const double ts = tau[sv.next];
+                const double th = (ts - tprev) / dt;
+                sv.save(ts != tn ? (K.stiff ? ros23_dense(th, dt, y0, K.k[0], K.k[1])
+                                            : tsit5_dense(th, dt, y0, K.k[0], K.k[1], K.k[2], K.k[3], K.k[4],
+                                                          K.k[5], K.k[6]))
+                                 : y1);
+            }
+            return true;
         }
-    };
-    uint32_t vbits = 0;
-    tsit5_hooked(f, on_step, ntau > 0 ? tau[ntau - 1] : 0.0, V0, ia.rtol, ia.atol, ia.maxiters, vbits, nsteps);
+    } saver{sv, tau, ntau};
+    OdeOut vo;
+    ode_scalar(f, saver, ntau > 0 ? tau[ntau - 1] : 0.0, V0, ia.rtol, ia.atol, ia.maxiters, vo);
+    uint32_t vbits = vo.status;
+    nsteps = vo.naccept + vo.nreject;
     if (ia.v_count) *ia.v_count = sv.next;
     if (f.oob) vbits |= SBR_OOB;
     const uint32_t bits = lbits | (vbits & (SBR_ODE_MAXITERS | SBR_STIFF_SWITCH | SBR_ODE_FAILED));
@@ -898,7 +769,11 @@ __global__ __launch_bounds__(BLOCK, INTEREST ? 1 : SBR_EQ_MINW) void equilibrium
     double* pmc = hmin + nsum;
     double* smc = pmc + nsum8;
     __shared__ int eq_next;
-    if (threadIdx.x == 0) eq_next = 0;
+    __shared__ int s_nonmono;
+    __shared__ double s_thalf;
+    // every shared flag is initialised before the first barrier: lanes >= nq set
+    // s_nonmono right after it, so a later store by thread 0 could clear their flag
+    if (threadIdx.x == 0) { eq_next = 0; s_nonmono = 0; s_thalf = NAN; }
     if (fits) {
         for (int i = threadIdx.x; i < n; i += BLOCK) { sT[i] = gT[i]; sG[i] = gG[i]; }
         if (INTEREST)
@@ -906,9 +781,6 @@ __global__ __launch_bounds__(BLOCK, INTEREST ? 1 : SBR_EQ_MINW) void equilibrium
     }
     __syncthreads();
     Summ S{nullptr, nullptr, nullptr, nullptr, false, (double)NAN};
-    __shared__ int s_nonmono;
-    __shared__ double s_thalf;
-    if (threadIdx.x == 0) { s_nonmono = 0; s_thalf = NAN; }
     if (fits && !a.exhaustive) {
         const int nbh = (ntau + 63) >> 6, nbg = (n + 7) >> 3;
         // HR summaries: 8 lanes per 64-entry block, 8 independent loads each (HR is read from

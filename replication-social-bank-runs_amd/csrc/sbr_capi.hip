@@ -41,13 +41,18 @@ struct sbr_ctx {
     // learning of the next kLearnSlots-1 batches (latency-bound: 32 waves each) runs
     // concurrently with the equilibrium of the current one
     static constexpr int kLearnSlots = SBR_LEARN_SLOTS;
+    // the hetero batch pipeline alternates two of these slots' streams/events
+    static_assert(kLearnSlots >= 2, "SBR_LEARN_SLOTS must be >= 2 (hetero batch pipeline)");
     size_t ws_beta[kLearnSlots] = {}, ws_cap[kLearnSlots] = {};
     sbr::LearnBufs LW[kLearnSlots]{};
     int last_slot = 0;
     hipStream_t lstream[kLearnSlots] = {};
     hipEvent_t ev_in = nullptr, ev_learned[kLearnSlots] = {}, ev_eq[kLearnSlots] = {};
-    // fork/join fences between HIP's null stream and `stream` (NullFence)
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    // fork/join fences between HIP's null stream and `stream`, and the end of the last call
+    // (whatever stream it ran on) that every call waits for (CallFence)
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_last = nullptr;
+    hipStream_t last_stream = nullptr;
+    bool have_last = false;
     // hetero learning workspace; H2 is the second slot of a pipelined hetero batch
     size_t hs_col = 0, hs_cap = 0, hs_K = 0;
     sbr::HeteroBufs H{};
@@ -112,29 +117,60 @@ int fail(sbr_ctx* c, int code, const char* what, hipError_t e = hipSuccess)
         if (_e != hipSuccess) return fail((ctx), (code), #expr, _e); \
     } while (0)
 
-// A NULL stream argument of the *_dev entry points names HIP's null stream (torch's
-// default stream).  The work itself runs on the context's non-blocking stream, fenced to
-// the null stream on both sides: it starts after, and null-stream work enqueued after the
-// call starts after it, without putting the kernels on the null stream's queue.
-struct NullFence {
+// Every entry point runs inside a CallFence:
+//  * it is ordered after the previous call on this context, whatever stream that one used
+//    (a *_dev call on a caller stream X followed by a host-pointer call on the private
+//    stream would otherwise let the learning kernel rewrite LW[0] while X still reads it);
+//  * a NULL stream argument of a *_dev entry point names HIP's null stream (torch's default
+//    stream): the work runs on the context's non-blocking stream, fenced to the null stream
+//    on both sides (it starts after earlier null-stream work, and null-stream work enqueued
+//    after the call starts after it) without putting the kernels on the null stream's queue.
+// Fence failures are reported (SBR_EDEVICE), never dropped.
+struct CallFence {
     sbr_ctx* c;
-    bool on;
-    NullFence(sbr_ctx* c_, void* stream) : c(c_), on(stream == nullptr)
+    bool null_stream;
+    hipStream_t s;
+    CallFence(sbr_ctx* c_, void* stream, bool dev)
+        : c(c_), null_stream(dev && stream == nullptr), s(dev && stream ? (hipStream_t)stream : c_->stream)
     {
-        if (on) {
-            (void)hipEventRecord(c->ev_fork, nullptr);
-            (void)hipStreamWaitEvent(c->stream, c->ev_fork, 0);
-        }
     }
-    ~NullFence()
+    int begin()
     {
-        if (on) {
-            (void)hipEventRecord(c->ev_join, c->stream);
-            (void)hipStreamWaitEvent(nullptr, c->ev_join, 0);
+        if (null_stream) {
+            HIP_TRY(c, hipEventRecord(c->ev_fork, nullptr), SBR_EDEVICE);
+            HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_fork, 0), SBR_EDEVICE);
         }
+        if (c->have_last && c->last_stream != s) HIP_TRY(c, hipStreamWaitEvent(s, c->ev_last, 0), SBR_EDEVICE);
+        return SBR_OK;
     }
-    hipStream_t get(void* stream) const { return on ? c->stream : (hipStream_t)stream; }
+    int end(int rc)
+    {
+        // recorded after a failure too: later calls still order after whatever was enqueued
+        hipError_t e = hipEventRecord(c->ev_last, s);
+        if (e == hipSuccess) {
+            c->have_last = true;
+            c->last_stream = s;
+        }
+        if (null_stream && e == hipSuccess) {
+            e = hipEventRecord(c->ev_join, c->stream);
+            if (e == hipSuccess) e = hipStreamWaitEvent(nullptr, c->ev_join, 0);
+        }
+        if (rc == SBR_OK && e != hipSuccess) return fail(c, SBR_EDEVICE, "stream fence", e);
+        return rc;
+    }
 };
+
+// run body(stream) inside a CallFence (dev: `stream` is a caller stream or NULL = null stream;
+// host-pointer entry points pass dev = false and run on the private stream)
+template <class F>
+int fenced(sbr_ctx* c, void* stream, bool dev, F&& body)
+{
+    CallFence f(c, stream, dev);
+    int rc = f.begin();
+    if (rc) return rc;
+    rc = body(f.s);
+    return f.end(rc);
+}
 
 void free_learn(sbr_ctx* c, int slot)
 {
@@ -419,7 +455,8 @@ int sbr_init(int device, sbr_ctx** out)
     c->device = device;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fork, SBR_SYNC_EVENT_FLAGS) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_join, SBR_SYNC_EVENT_FLAGS) != hipSuccess) {
+        hipEventCreateWithFlags(&c->ev_join, SBR_SYNC_EVENT_FLAGS) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_last, SBR_SYNC_EVENT_FLAGS) != hipSuccess) {
         delete c;
         return SBR_EDEVICE;
     }
@@ -454,6 +491,7 @@ int sbr_free(sbr_ctx* c)
     if (c->ev_in) (void)hipEventDestroy(c->ev_in);
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+    if (c->ev_last) (void)hipEventDestroy(c->ev_last);
     for (int k = 0; k < sbr_ctx::kLearnSlots; k++) {
         if (c->ev_learned[k]) (void)hipEventDestroy(c->ev_learned[k]);
         if (c->ev_eq[k]) (void)hipEventDestroy(c->ev_eq[k]);
@@ -479,9 +517,9 @@ int sbr_sweep_baseline_dev(sbr_ctx* c, void* stream, const double* beta, const d
     if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
     sbr_opts o = resolve(opts);
     sbr::ResultSoA r{out->xi, out->tau_in_unc, out->tau_out_unc, out->aw_max, out->tol, out->status, out->iters};
-    NullFence fence(c, stream); // NULL = HIP null stream (torch default stream)
-    hipStream_t s = fence.get(stream);
-    return run_baseline(c, s, beta, eta, t_end, x0, u, n_beta, n_u, p, kappa, lambda, o, r, nullptr);
+    return fenced(c, stream, true, [&](hipStream_t s) {
+        return run_baseline(c, s, beta, eta, t_end, x0, u, n_beta, n_u, p, kappa, lambda, o, r, nullptr);
+    });
 }
 
 // hetero equilibrium LDS slab (doubles): knot times + per-group HR summaries of one column,
@@ -526,40 +564,40 @@ int sbr_sweep_baseline_batch_dev(sbr_ctx* c, void* stream, int64_t n_batch, cons
         int rc = ensure_pipe_streams(c);
         if (rc) return rc;
     }
-    NullFence fence(c, stream); // NULL = HIP null stream (torch default stream)
-    hipStream_t s = fence.get(stream);
-    const size_t np = (size_t)n_beta * (size_t)n_u;
-    sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, p, lambda, o.ode_maxiters, (int32_t)n_beta, 1, 0};
-    // inputs are ready once prior work on the caller's stream is
-    HIP_TRY(c, hipEventRecord(c->ev_in, s), SBR_EDEVICE);
-    for (int k = 0; k < nslot; k++) HIP_TRY(c, hipStreamWaitEvent(c->lstream[k], c->ev_in, 0), SBR_EDEVICE);
-    for (int64_t k = 0; k < n_batch; k++) {
-        const int slot = (int)(k % nslot);
-        hipStream_t es = s; // one equilibrium stream (two alternating: 15% slower, r01_ab27)
-        hipStream_t ls = c->lstream[slot];
-        const double* bk = beta + k * n_beta;
-        const double* ek = eta + k * n_beta;
-        const double* tk = t_end + k * n_beta;
-        // the slot's previous reader (equilibrium of batch k - nslot) must be done
-        if (k >= nslot) HIP_TRY(c, hipStreamWaitEvent(ls, c->ev_eq[slot], 0), SBR_EDEVICE);
-        hipEvent_t t0 = tstart(c, ls);
-        HIP_TRY(c, sbr::launch_learn_logistic(bk, ek, tk, la, c->LW[slot], ls), SBR_EDEVICE);
-        tend(c, ls, 0, t0);
-        HIP_TRY(c, hipEventRecord(c->ev_learned[slot], ls), SBR_EDEVICE);
-        HIP_TRY(c, hipStreamWaitEvent(es, c->ev_learned[slot], 0), SBR_EDEVICE);
-        sbr::ResultSoA r{out->xi ? out->xi + k * np : nullptr,
-                         out->tau_in_unc ? out->tau_in_unc + k * np : nullptr,
-                         out->tau_out_unc ? out->tau_out_unc + k * np : nullptr,
-                         out->aw_max ? out->aw_max + k * np : nullptr,
-                         out->tol ? out->tol + k * np : nullptr,
-                         out->status ? out->status + k * np : nullptr,
-                         out->iters ? out->iters + k * np : nullptr};
-        int rc = launch_eq(c, es, c->LW[slot], ek, tk, u, n_beta, n_u, kappa, o, r, nullptr);
-        if (rc) return rc;
-        HIP_TRY(c, hipEventRecord(c->ev_eq[slot], es), SBR_EDEVICE);
-        c->last_slot = slot;
-    }
-    return SBR_OK;
+    return fenced(c, stream, true, [&](hipStream_t s) -> int {
+        const size_t np = (size_t)n_beta * (size_t)n_u;
+        sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, p, lambda, o.ode_maxiters, (int32_t)n_beta, 1, 0};
+        // inputs are ready once prior work on the caller's stream is
+        HIP_TRY(c, hipEventRecord(c->ev_in, s), SBR_EDEVICE);
+        for (int k = 0; k < nslot; k++) HIP_TRY(c, hipStreamWaitEvent(c->lstream[k], c->ev_in, 0), SBR_EDEVICE);
+        for (int64_t k = 0; k < n_batch; k++) {
+            const int slot = (int)(k % nslot);
+            hipStream_t es = s; // one equilibrium stream (two alternating: 15% slower, r01_ab27)
+            hipStream_t ls = c->lstream[slot];
+            const double* bk = beta + k * n_beta;
+            const double* ek = eta + k * n_beta;
+            const double* tk = t_end + k * n_beta;
+            // the slot's previous reader (equilibrium of batch k - nslot) must be done
+            if (k >= nslot) HIP_TRY(c, hipStreamWaitEvent(ls, c->ev_eq[slot], 0), SBR_EDEVICE);
+            hipEvent_t t0 = tstart(c, ls);
+            HIP_TRY(c, sbr::launch_learn_logistic(bk, ek, tk, la, c->LW[slot], ls), SBR_EDEVICE);
+            tend(c, ls, 0, t0);
+            HIP_TRY(c, hipEventRecord(c->ev_learned[slot], ls), SBR_EDEVICE);
+            HIP_TRY(c, hipStreamWaitEvent(es, c->ev_learned[slot], 0), SBR_EDEVICE);
+            sbr::ResultSoA r{out->xi ? out->xi + k * np : nullptr,
+                             out->tau_in_unc ? out->tau_in_unc + k * np : nullptr,
+                             out->tau_out_unc ? out->tau_out_unc + k * np : nullptr,
+                             out->aw_max ? out->aw_max + k * np : nullptr,
+                             out->tol ? out->tol + k * np : nullptr,
+                             out->status ? out->status + k * np : nullptr,
+                             out->iters ? out->iters + k * np : nullptr};
+            int rc = launch_eq(c, es, c->LW[slot], ek, tk, u, n_beta, n_u, kappa, o, r, nullptr);
+            if (rc) return rc;
+            HIP_TRY(c, hipEventRecord(c->ev_eq[slot], es), SBR_EDEVICE);
+            c->last_slot = slot;
+        }
+        return SBR_OK;
+    });
 }
 
 int sbr_sweep_baseline(sbr_ctx* c, const double* beta, const double* eta, const double* t_end, double x0,
@@ -589,22 +627,23 @@ int sbr_sweep_baseline(sbr_ctx* c, const double* beta, const double* eta, const 
     double* dres = (double*)(base + ((in_bytes + 255) & ~(size_t)255));
     sbr::ResultSoA r{dres, dres + np, dres + 2 * np, dres + 3 * np, dres + 4 * np, (uint32_t*)(dres + 5 * np),
                      (int32_t*)((uint32_t*)(dres + 5 * np) + np)};
-    hipStream_t s = c->stream;
-    HIP_TRY(c, hipMemcpyAsync(dbeta, beta, n_beta * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
-    HIP_TRY(c, hipMemcpyAsync(deta, eta, n_beta * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
-    HIP_TRY(c, hipMemcpyAsync(dtend, t_end, n_beta * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
-    HIP_TRY(c, hipMemcpyAsync(du, u, n_u * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
-    rc = run_baseline(c, s, dbeta, deta, dtend, x0, du, n_beta, n_u, p, kappa, lambda, o, r, nullptr);
-    if (rc) return rc;
-    double* hs[5] = {out->xi, out->tau_in_unc, out->tau_out_unc, out->aw_max, out->tol};
-    for (int k = 0; k < 5; k++)
-        if (hs[k]) HIP_TRY(c, hipMemcpyAsync(hs[k], dres + k * np, np * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
-    if (out->status) HIP_TRY(c, hipMemcpyAsync(out->status, r.status, np * 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
-    if (out->iters) HIP_TRY(c, hipMemcpyAsync(out->iters, r.iters, np * 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
-    HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
-    if (o.early_exit_nan_run > 0 && out->status && out->xi && out->aw_max && out->tol)
-        sbr_apply_early_exit(n_beta, n_u, o.early_exit_nan_run, out);
-    return SBR_OK;
+    return fenced(c, nullptr, false, [&](hipStream_t s) -> int {
+        HIP_TRY(c, hipMemcpyAsync(dbeta, beta, n_beta * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+        HIP_TRY(c, hipMemcpyAsync(deta, eta, n_beta * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+        HIP_TRY(c, hipMemcpyAsync(dtend, t_end, n_beta * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+        HIP_TRY(c, hipMemcpyAsync(du, u, n_u * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+        rc = run_baseline(c, s, dbeta, deta, dtend, x0, du, n_beta, n_u, p, kappa, lambda, o, r, nullptr);
+        if (rc) return rc;
+        double* hs[5] = {out->xi, out->tau_in_unc, out->tau_out_unc, out->aw_max, out->tol};
+        for (int k = 0; k < 5; k++)
+            if (hs[k]) HIP_TRY(c, hipMemcpyAsync(hs[k], dres + k * np, np * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        if (out->status) HIP_TRY(c, hipMemcpyAsync(out->status, r.status, np * 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        if (out->iters) HIP_TRY(c, hipMemcpyAsync(out->iters, r.iters, np * 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
+        if (o.early_exit_nan_run > 0 && out->status && out->xi && out->aw_max && out->tol)
+            sbr_apply_early_exit(n_beta, n_u, o.early_exit_nan_run, out);
+        return SBR_OK;
+    });
 }
 
 int sbr_sweep_interest_dev(sbr_ctx* c, void* stream, const double* beta, const double* eta, const double* t_end,
@@ -620,9 +659,9 @@ int sbr_sweep_interest_dev(sbr_ctx* c, void* stream, const double* beta, const d
     if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
     sbr_opts o = resolve(opts);
     sbr::ResultSoA rs{out->xi, out->tau_in_unc, out->tau_out_unc, out->aw_max, out->tol, out->status, out->iters};
-    NullFence fence(c, stream); // NULL = HIP null stream (torch default stream)
-    hipStream_t s = fence.get(stream);
-    return run_interest(c, s, beta, eta, t_end, x0, u, n_beta, n_u, p, kappa, lambda, r, delta, o, rs, rk_steps);
+    return fenced(c, stream, true, [&](hipStream_t s) {
+        return run_interest(c, s, beta, eta, t_end, x0, u, n_beta, n_u, p, kappa, lambda, r, delta, o, rs, rk_steps);
+    });
 }
 
 int sbr_sweep_interest(sbr_ctx* c, const double* beta, const double* eta, const double* t_end, double x0,
@@ -654,21 +693,22 @@ int sbr_sweep_interest(sbr_ctx* c, const double* beta, const double* eta, const 
     int64_t* dsteps = (int64_t*)(dres + 5 * np);
     sbr::ResultSoA rs{dres, dres + np, dres + 2 * np, dres + 3 * np, dres + 4 * np, (uint32_t*)(dsteps + np),
                       (int32_t*)((uint32_t*)(dsteps + np) + np)};
-    hipStream_t s = c->stream;
-    HIP_TRY(c, hipMemcpyAsync(dbeta, beta, n_beta * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
-    HIP_TRY(c, hipMemcpyAsync(deta, eta, n_beta * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
-    HIP_TRY(c, hipMemcpyAsync(dtend, t_end, n_beta * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
-    HIP_TRY(c, hipMemcpyAsync(du, u, n_u * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
-    rc = run_interest(c, s, dbeta, deta, dtend, x0, du, n_beta, n_u, p, kappa, lambda, r, delta, o, rs, dsteps);
-    if (rc) return rc;
-    double* hs[5] = {out->xi, out->tau_in_unc, out->tau_out_unc, out->aw_max, out->tol};
-    for (int k = 0; k < 5; k++)
-        if (hs[k]) HIP_TRY(c, hipMemcpyAsync(hs[k], dres + k * np, np * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
-    if (out->status) HIP_TRY(c, hipMemcpyAsync(out->status, rs.status, np * 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
-    if (out->iters) HIP_TRY(c, hipMemcpyAsync(out->iters, rs.iters, np * 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
-    if (rk_steps) HIP_TRY(c, hipMemcpyAsync(rk_steps, dsteps, np * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
-    HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
-    return SBR_OK;
+    return fenced(c, nullptr, false, [&](hipStream_t s) -> int {
+        HIP_TRY(c, hipMemcpyAsync(dbeta, beta, n_beta * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+        HIP_TRY(c, hipMemcpyAsync(deta, eta, n_beta * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+        HIP_TRY(c, hipMemcpyAsync(dtend, t_end, n_beta * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+        HIP_TRY(c, hipMemcpyAsync(du, u, n_u * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+        rc = run_interest(c, s, dbeta, deta, dtend, x0, du, n_beta, n_u, p, kappa, lambda, r, delta, o, rs, dsteps);
+        if (rc) return rc;
+        double* hs[5] = {out->xi, out->tau_in_unc, out->tau_out_unc, out->aw_max, out->tol};
+        for (int k = 0; k < 5; k++)
+            if (hs[k]) HIP_TRY(c, hipMemcpyAsync(hs[k], dres + k * np, np * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        if (out->status) HIP_TRY(c, hipMemcpyAsync(out->status, rs.status, np * 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        if (out->iters) HIP_TRY(c, hipMemcpyAsync(out->iters, rs.iters, np * 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        if (rk_steps) HIP_TRY(c, hipMemcpyAsync(rk_steps, dsteps, np * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
+        return SBR_OK;
+    });
 }
 
 int sbr_interest_point_paths(sbr_ctx* c, double beta, double eta, double t_end, double x0, double u, double p,
@@ -687,40 +727,41 @@ int sbr_interest_point_paths(sbr_ctx* c, double beta, double eta, double t_end, 
     if (rc) return rc;
     double* d = (double*)c->stage;
     double hin[4] = {beta, eta, t_end, u};
-    hipStream_t s = c->stream;
-    HIP_TRY(c, hipMemcpyAsync(d, hin, 32, hipMemcpyHostToDevice, s), SBR_EDEVICE);
-    double* dres = d + 4;
-    uint32_t* dst = (uint32_t*)(dres + 5);
-    int32_t* dnv = (int32_t*)(dres + 6);
-    double* dpath = dres + 7;
-    double* dv = dpath + kc;
-    HIP_TRY(c, hipMemsetAsync(dnv, 0, 4, s), SBR_EDEVICE);
-    sbr::ResultSoA rs{dres, dres + 1, dres + 2, dres + 3, dres + 4, dst, nullptr};
-    rc = run_interest(c, s, d, d + 1, d + 2, x0, d + 3, 1, 1, p, kappa, lambda, r, delta, o, rs, nullptr, dpath,
-                      r > 0.0 ? dv : nullptr, dnv);
-    if (rc) return rc;
-    HIP_TRY(c, hipMemcpyAsync(res, dres, 40, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
-    HIP_TRY(c, hipMemcpyAsync(status, dst, 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
-    int32_t nt = 0, nle = 0, nv = 0;
-    HIP_TRY(c, hipMemcpyAsync(&nt, c->LW[0].n_tau, 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
-    HIP_TRY(c, hipMemcpyAsync(&nle, c->LW[0].n_le, 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
-    HIP_TRY(c, hipMemcpyAsync(&nv, dnv, 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
-    HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
-    if (r <= 0.0) nv = 0;
-    if (n_tau) *n_tau = nt;
-    if (n_v) *n_v = nv;
-    if (nt > cap) return fail(c, SBR_EARG, "path capacity too small");
-    if (tau) {
-        HIP_TRY(c, hipMemcpy(tau, c->LW[0].t, (size_t)nle * 8, hipMemcpyDeviceToHost), SBR_EDEVICE);
-        if (nt > nle) tau[nle] = eta;
-    }
-    if (hr) HIP_TRY(c, hipMemcpy(hr, c->LW[0].hr, (size_t)nt * 8, hipMemcpyDeviceToHost), SBR_EDEVICE);
-    if (V && nv > 0) HIP_TRY(c, hipMemcpy(V, dv, (size_t)nv * 8, hipMemcpyDeviceToHost), SBR_EDEVICE);
-    if (aw_cum) {
-        if (*status & SBR_RUN) HIP_TRY(c, hipMemcpy(aw_cum, dpath, (size_t)nt * 8, hipMemcpyDeviceToHost), SBR_EDEVICE);
-        else for (int i = 0; i < nt; i++) aw_cum[i] = NAN;
-    }
-    return SBR_OK;
+    return fenced(c, nullptr, false, [&](hipStream_t s) -> int {
+        HIP_TRY(c, hipMemcpyAsync(d, hin, 32, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+        double* dres = d + 4;
+        uint32_t* dst = (uint32_t*)(dres + 5);
+        int32_t* dnv = (int32_t*)(dres + 6);
+        double* dpath = dres + 7;
+        double* dv = dpath + kc;
+        HIP_TRY(c, hipMemsetAsync(dnv, 0, 4, s), SBR_EDEVICE);
+        sbr::ResultSoA rs{dres, dres + 1, dres + 2, dres + 3, dres + 4, dst, nullptr};
+        rc = run_interest(c, s, d, d + 1, d + 2, x0, d + 3, 1, 1, p, kappa, lambda, r, delta, o, rs, nullptr, dpath,
+                          r > 0.0 ? dv : nullptr, dnv);
+        if (rc) return rc;
+        HIP_TRY(c, hipMemcpyAsync(res, dres, 40, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        HIP_TRY(c, hipMemcpyAsync(status, dst, 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        int32_t nt = 0, nle = 0, nv = 0;
+        HIP_TRY(c, hipMemcpyAsync(&nt, c->LW[0].n_tau, 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        HIP_TRY(c, hipMemcpyAsync(&nle, c->LW[0].n_le, 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        HIP_TRY(c, hipMemcpyAsync(&nv, dnv, 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
+        if (r <= 0.0) nv = 0;
+        if (n_tau) *n_tau = nt;
+        if (n_v) *n_v = nv;
+        if (nt > cap) return fail(c, SBR_EARG, "path capacity too small");
+        if (tau) {
+            HIP_TRY(c, hipMemcpy(tau, c->LW[0].t, (size_t)nle * 8, hipMemcpyDeviceToHost), SBR_EDEVICE);
+            if (nt > nle) tau[nle] = eta;
+        }
+        if (hr) HIP_TRY(c, hipMemcpy(hr, c->LW[0].hr, (size_t)nt * 8, hipMemcpyDeviceToHost), SBR_EDEVICE);
+        if (V && nv > 0) HIP_TRY(c, hipMemcpy(V, dv, (size_t)nv * 8, hipMemcpyDeviceToHost), SBR_EDEVICE);
+        if (aw_cum) {
+            if (*status & SBR_RUN) HIP_TRY(c, hipMemcpy(aw_cum, dpath, (size_t)nt * 8, hipMemcpyDeviceToHost), SBR_EDEVICE);
+            else for (int i = 0; i < nt; i++) aw_cum[i] = NAN;
+        }
+        return SBR_OK;
+    });
 }
 
 int sbr_learn_baseline(sbr_ctx* c, const double* beta, const double* eta, const double* t_end, double x0,
@@ -738,21 +779,22 @@ int sbr_learn_baseline(sbr_ctx* c, const double* beta, const double* eta, const 
     double* dbeta = (double*)c->stage;
     double* deta = dbeta + n_beta;
     double* dtend = deta + n_beta;
-    hipStream_t s = c->stream;
-    HIP_TRY(c, hipMemcpyAsync(dbeta, beta, n_beta * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
-    HIP_TRY(c, hipMemcpyAsync(deta, eta, n_beta * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
-    HIP_TRY(c, hipMemcpyAsync(dtend, t_end, n_beta * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
-    sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, 0.5, 1.0, o.ode_maxiters, (int32_t)n_beta, stop_after_eta, 0};
-    HIP_TRY(c, sbr::launch_learn_logistic(dbeta, deta, dtend, la, c->LW[0], s), SBR_EDEVICE);
-    const size_t w = (size_t)o.knot_capacity;
-    if (t_out)
-        HIP_TRY(c, hipMemcpy2DAsync(t_out, cap * 8, c->LW[0].t, w * 8, w * 8, n_beta, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
-    if (G_out)
-        HIP_TRY(c, hipMemcpy2DAsync(G_out, cap * 8, c->LW[0].G, w * 8, w * 8, n_beta, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
-    if (n_knots) HIP_TRY(c, hipMemcpyAsync(n_knots, c->LW[0].n_knots, n_beta * 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
-    if (status) HIP_TRY(c, hipMemcpyAsync(status, c->LW[0].status, n_beta * 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
-    HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
-    return SBR_OK;
+    return fenced(c, nullptr, false, [&](hipStream_t s) -> int {
+        HIP_TRY(c, hipMemcpyAsync(dbeta, beta, n_beta * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+        HIP_TRY(c, hipMemcpyAsync(deta, eta, n_beta * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+        HIP_TRY(c, hipMemcpyAsync(dtend, t_end, n_beta * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+        sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, 0.5, 1.0, o.ode_maxiters, (int32_t)n_beta, stop_after_eta, 0};
+        HIP_TRY(c, sbr::launch_learn_logistic(dbeta, deta, dtend, la, c->LW[0], s), SBR_EDEVICE);
+        const size_t w = (size_t)o.knot_capacity;
+        if (t_out)
+            HIP_TRY(c, hipMemcpy2DAsync(t_out, cap * 8, c->LW[0].t, w * 8, w * 8, n_beta, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        if (G_out)
+            HIP_TRY(c, hipMemcpy2DAsync(G_out, cap * 8, c->LW[0].G, w * 8, w * 8, n_beta, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        if (n_knots) HIP_TRY(c, hipMemcpyAsync(n_knots, c->LW[0].n_knots, n_beta * 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        if (status) HIP_TRY(c, hipMemcpyAsync(status, c->LW[0].status, n_beta * 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
+        return SBR_OK;
+    });
 }
 
 int sbr_solve_point_paths(sbr_ctx* c, double beta, double eta, double t_end, double x0, double u, double p,
@@ -769,34 +811,35 @@ int sbr_solve_point_paths(sbr_ctx* c, double beta, double eta, double t_end, dou
     if (rc) return rc;
     double* d = (double*)c->stage;
     double hin[4] = {beta, eta, t_end, u};
-    hipStream_t s = c->stream;
-    HIP_TRY(c, hipMemcpyAsync(d, hin, 32, hipMemcpyHostToDevice, s), SBR_EDEVICE);
-    double* dres = d + 4;
-    uint32_t* dst = (uint32_t*)(dres + 5);
-    double* dpath = dres + 6 + 1;
-    sbr::ResultSoA r{dres, dres + 1, dres + 2, dres + 3, dres + 4, dst, nullptr};
-    rc = run_baseline(c, s, d, d + 1, d + 2, x0, d + 3, 1, 1, p, kappa, lambda, o, r, dpath);
-    if (rc) return rc;
-    HIP_TRY(c, hipMemcpyAsync(res, dres, 40, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
-    HIP_TRY(c, hipMemcpyAsync(status, dst, 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
-    int32_t nt = 0, nle = 0, nk = 0;
-    HIP_TRY(c, hipMemcpyAsync(&nt, c->LW[0].n_tau, 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
-    HIP_TRY(c, hipMemcpyAsync(&nle, c->LW[0].n_le, 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
-    HIP_TRY(c, hipMemcpyAsync(&nk, c->LW[0].n_knots, 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
-    HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
-    if (n_tau) *n_tau = nt;
-    if (nt > cap) return fail(c, SBR_EARG, "path capacity too small");
-    if (tau) {
-        HIP_TRY(c, hipMemcpy(tau, c->LW[0].t, (size_t)nle * 8, hipMemcpyDeviceToHost), SBR_EDEVICE);
-        if (nt > nle) tau[nle] = eta;
-    }
-    if (hr) HIP_TRY(c, hipMemcpy(hr, c->LW[0].hr, (size_t)nt * 8, hipMemcpyDeviceToHost), SBR_EDEVICE);
-    if (aw_cum) {
-        if (*status & SBR_RUN) HIP_TRY(c, hipMemcpy(aw_cum, dpath, (size_t)nt * 8, hipMemcpyDeviceToHost), SBR_EDEVICE);
-        else for (int i = 0; i < nt; i++) aw_cum[i] = NAN;
-    }
-    (void)nk;
-    return SBR_OK;
+    return fenced(c, nullptr, false, [&](hipStream_t s) -> int {
+        HIP_TRY(c, hipMemcpyAsync(d, hin, 32, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+        double* dres = d + 4;
+        uint32_t* dst = (uint32_t*)(dres + 5);
+        double* dpath = dres + 6 + 1;
+        sbr::ResultSoA r{dres, dres + 1, dres + 2, dres + 3, dres + 4, dst, nullptr};
+        rc = run_baseline(c, s, d, d + 1, d + 2, x0, d + 3, 1, 1, p, kappa, lambda, o, r, dpath);
+        if (rc) return rc;
+        HIP_TRY(c, hipMemcpyAsync(res, dres, 40, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        HIP_TRY(c, hipMemcpyAsync(status, dst, 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        int32_t nt = 0, nle = 0, nk = 0;
+        HIP_TRY(c, hipMemcpyAsync(&nt, c->LW[0].n_tau, 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        HIP_TRY(c, hipMemcpyAsync(&nle, c->LW[0].n_le, 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        HIP_TRY(c, hipMemcpyAsync(&nk, c->LW[0].n_knots, 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
+        if (n_tau) *n_tau = nt;
+        if (nt > cap) return fail(c, SBR_EARG, "path capacity too small");
+        if (tau) {
+            HIP_TRY(c, hipMemcpy(tau, c->LW[0].t, (size_t)nle * 8, hipMemcpyDeviceToHost), SBR_EDEVICE);
+            if (nt > nle) tau[nle] = eta;
+        }
+        if (hr) HIP_TRY(c, hipMemcpy(hr, c->LW[0].hr, (size_t)nt * 8, hipMemcpyDeviceToHost), SBR_EDEVICE);
+        if (aw_cum) {
+            if (*status & SBR_RUN) HIP_TRY(c, hipMemcpy(aw_cum, dpath, (size_t)nt * 8, hipMemcpyDeviceToHost), SBR_EDEVICE);
+            else for (int i = 0; i < nt; i++) aw_cum[i] = NAN;
+        }
+        (void)nk;
+        return SBR_OK;
+    });
 }
 
 int sbr_timing_enable(sbr_ctx* c, int on)
@@ -846,6 +889,20 @@ int sbr_learn_stats(sbr_ctx* c, int64_t n_beta, int32_t* n_knots, int32_t* n_tau
     return SBR_OK;
 }
 
+int sbr_hetero_learn_stats(sbr_ctx* c, int64_t n_col, int32_t* n_knots, int32_t* n_tau, int32_t* n_accept,
+                           int32_t* n_reject, uint32_t* status)
+{
+    if (!c || n_col <= 0 || (size_t)n_col > c->hs_col) return SBR_EARG;
+    if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
+    HIP_TRY(c, hipDeviceSynchronize(), SBR_EDEVICE);
+    const sbr::HeteroBufs& H = c->H;
+    struct { int32_t* h; void* d; } cp[] = {{n_knots, H.n_knots}, {n_tau, H.n_tau}, {n_accept, H.n_accept},
+                                           {n_reject, H.n_reject}, {(int32_t*)status, H.status}};
+    for (auto& x : cp)
+        if (x.h) HIP_TRY(c, hipMemcpy(x.h, x.d, (size_t)n_col * 4, hipMemcpyDeviceToHost), SBR_EDEVICE);
+    return SBR_OK;
+}
+
 int sbr_sweep_hetero_dev(sbr_ctx* c, void* stream, int32_t K, const double* betas, const double* dist,
                          const double* eta, const double* t_end, double x0, const double* u, int64_t n_col,
                          int64_t n_u, double p, double kappa, double lambda, const sbr_opts* opts,
@@ -859,19 +916,19 @@ int sbr_sweep_hetero_dev(sbr_ctx* c, void* stream, int32_t K, const double* beta
     sbr_opts o = resolve(opts);
     int rc = ensure_hetero(c, (size_t)n_col, (size_t)o.knot_capacity, (size_t)K);
     if (rc) return rc;
-    NullFence fence(c, stream); // NULL = HIP null stream (torch default stream)
-    hipStream_t s = fence.get(stream);
-    sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, p, lambda, o.ode_maxiters, (int32_t)n_col, 0, 0};
-    sbr::HeteroEqArgs ea{kappa, 1e-12, (int32_t)n_u, o.hetero_max_iters, het_lds(c),
-                         (o.flags & SBR_FLAG_EXHAUSTIVE) ? 1 : 0, (o.flags >> 8) & 7, c->het_aw_path};
-    sbr::ResultSoA r{out->xi, nullptr, nullptr, out->aw_max, out->tol, out->status, out->iters};
-    hipEvent_t t0 = tstart(c, s);
-    HIP_TRY(c, sbr::launch_hetero(K, betas, dist, eta, t_end, u, la, ea, c->H, r, tau_in, tau_out, s, 0), SBR_EDEVICE);
-    tend(c, s, 0, t0);
-    t0 = tstart(c, s);
-    HIP_TRY(c, sbr::launch_hetero(K, betas, dist, eta, t_end, u, la, ea, c->H, r, tau_in, tau_out, s, 1), SBR_EDEVICE);
-    tend(c, s, 1, t0);
-    return SBR_OK;
+    return fenced(c, stream, true, [&](hipStream_t s) -> int {
+        sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, p, lambda, o.ode_maxiters, (int32_t)n_col, 0, 0};
+        sbr::HeteroEqArgs ea{kappa, 1e-12, (int32_t)n_u, o.hetero_max_iters, het_lds(c),
+                             (o.flags & SBR_FLAG_EXHAUSTIVE) ? 1 : 0, (o.flags >> 8) & 7, c->het_aw_path};
+        sbr::ResultSoA r{out->xi, nullptr, nullptr, out->aw_max, out->tol, out->status, out->iters};
+        hipEvent_t t0 = tstart(c, s);
+        HIP_TRY(c, sbr::launch_hetero(K, betas, dist, eta, t_end, u, la, ea, c->H, r, tau_in, tau_out, s, 0), SBR_EDEVICE);
+        tend(c, s, 0, t0);
+        t0 = tstart(c, s);
+        HIP_TRY(c, sbr::launch_hetero(K, betas, dist, eta, t_end, u, la, ea, c->H, r, tau_in, tau_out, s, 1), SBR_EDEVICE);
+        tend(c, s, 1, t0);
+        return SBR_OK;
+    });
 }
 
 int sbr_sweep_hetero_batch_dev(sbr_ctx* c, void* stream, int64_t n_batch, int32_t K, const double* betas,
@@ -892,38 +949,38 @@ int sbr_sweep_hetero_batch_dev(sbr_ctx* c, void* stream, int64_t n_batch, int32_
     if (!rc && n_batch > 1) rc = ensure_hetero_bufs(c, c->H2, c->hs2_col, c->hs2_cap, c->hs2_K, (size_t)n_col, cap, (size_t)K);
     if (!rc) rc = ensure_pipe_streams(c);
     if (rc) return rc;
-    NullFence fence(c, stream); // NULL = HIP null stream (torch default stream)
-    hipStream_t s = fence.get(stream);
-    sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, p, lambda, o.ode_maxiters, (int32_t)n_col, 0, 0};
-    sbr::HeteroEqArgs ea{kappa, 1e-12, (int32_t)n_u, o.hetero_max_iters, het_lds(c),
-                         (o.flags & SBR_FLAG_EXHAUSTIVE) ? 1 : 0, (o.flags >> 8) & 7, nullptr};
-    const size_t np = (size_t)n_col * (size_t)n_u;
-    HIP_TRY(c, hipEventRecord(c->ev_in, s), SBR_EDEVICE);
-    for (int k = 0; k < 2; k++) HIP_TRY(c, hipStreamWaitEvent(c->lstream[k], c->ev_in, 0), SBR_EDEVICE);
-    for (int64_t k = 0; k < n_batch; k++) {
-        const int slot = (int)(k & 1);
-        hipStream_t ls = c->lstream[slot];
-        const sbr::HeteroBufs& H = slot ? c->H2 : c->H;
-        const double* bk = betas + k * n_col * K;
-        const double* ek = eta + k * n_col;
-        const double* tk = t_end + k * n_col;
-        // the slot's previous reader (equilibrium of batch k - 2) must be done
-        if (k >= 2) HIP_TRY(c, hipStreamWaitEvent(ls, c->ev_eq[slot], 0), SBR_EDEVICE);
-        hipEvent_t t0 = tstart(c, ls);
-        sbr::ResultSoA r{out->xi + k * np, nullptr, nullptr, out->aw_max + k * np, out->tol + k * np,
-                         out->status + k * np, out->iters ? out->iters + k * np : nullptr};
-        double* ti = tau_in ? tau_in + k * np * K : nullptr;
-        double* to = tau_out ? tau_out + k * np * K : nullptr;
-        HIP_TRY(c, sbr::launch_hetero(K, bk, dist, ek, tk, u, la, ea, H, r, ti, to, ls, 0), SBR_EDEVICE);
-        tend(c, ls, 0, t0);
-        HIP_TRY(c, hipEventRecord(c->ev_learned[slot], ls), SBR_EDEVICE);
-        HIP_TRY(c, hipStreamWaitEvent(s, c->ev_learned[slot], 0), SBR_EDEVICE);
-        t0 = tstart(c, s);
-        HIP_TRY(c, sbr::launch_hetero(K, bk, dist, ek, tk, u, la, ea, H, r, ti, to, s, 1), SBR_EDEVICE);
-        tend(c, s, 1, t0);
-        HIP_TRY(c, hipEventRecord(c->ev_eq[slot], s), SBR_EDEVICE);
-    }
-    return SBR_OK;
+    return fenced(c, stream, true, [&](hipStream_t s) -> int {
+        sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, p, lambda, o.ode_maxiters, (int32_t)n_col, 0, 0};
+        sbr::HeteroEqArgs ea{kappa, 1e-12, (int32_t)n_u, o.hetero_max_iters, het_lds(c),
+                             (o.flags & SBR_FLAG_EXHAUSTIVE) ? 1 : 0, (o.flags >> 8) & 7, nullptr};
+        const size_t np = (size_t)n_col * (size_t)n_u;
+        HIP_TRY(c, hipEventRecord(c->ev_in, s), SBR_EDEVICE);
+        for (int k = 0; k < 2; k++) HIP_TRY(c, hipStreamWaitEvent(c->lstream[k], c->ev_in, 0), SBR_EDEVICE);
+        for (int64_t k = 0; k < n_batch; k++) {
+            const int slot = (int)(k & 1);
+            hipStream_t ls = c->lstream[slot];
+            const sbr::HeteroBufs& H = slot ? c->H2 : c->H;
+            const double* bk = betas + k * n_col * K;
+            const double* ek = eta + k * n_col;
+            const double* tk = t_end + k * n_col;
+            // the slot's previous reader (equilibrium of batch k - 2) must be done
+            if (k >= 2) HIP_TRY(c, hipStreamWaitEvent(ls, c->ev_eq[slot], 0), SBR_EDEVICE);
+            hipEvent_t t0 = tstart(c, ls);
+            sbr::ResultSoA r{out->xi + k * np, nullptr, nullptr, out->aw_max + k * np, out->tol + k * np,
+                             out->status + k * np, out->iters ? out->iters + k * np : nullptr};
+            double* ti = tau_in ? tau_in + k * np * K : nullptr;
+            double* to = tau_out ? tau_out + k * np * K : nullptr;
+            HIP_TRY(c, sbr::launch_hetero(K, bk, dist, ek, tk, u, la, ea, H, r, ti, to, ls, 0), SBR_EDEVICE);
+            tend(c, ls, 0, t0);
+            HIP_TRY(c, hipEventRecord(c->ev_learned[slot], ls), SBR_EDEVICE);
+            HIP_TRY(c, hipStreamWaitEvent(s, c->ev_learned[slot], 0), SBR_EDEVICE);
+            t0 = tstart(c, s);
+            HIP_TRY(c, sbr::launch_hetero(K, bk, dist, ek, tk, u, la, ea, H, r, ti, to, s, 1), SBR_EDEVICE);
+            tend(c, s, 1, t0);
+            HIP_TRY(c, hipEventRecord(c->ev_eq[slot], s), SBR_EDEVICE);
+        }
+        return SBR_OK;
+    });
 }
 
 int sbr_hetero_point_paths(sbr_ctx* c, int32_t K, const double* betas, const double* dist, double eta, double t_end,
@@ -954,32 +1011,33 @@ int sbr_hetero_point_paths(sbr_ctx* c, int32_t K, const double* betas, const dou
     double* dtin = dres + 4;
     double* dtout = dtin + K;
     double* dpath = dtout + K;
-    hipStream_t s = c->stream;
-    const double hin[3] = {eta, t_end, u};
-    HIP_TRY(c, hipMemcpyAsync(dbeta, betas, (size_t)K * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
-    HIP_TRY(c, hipMemcpyAsync(ddist, dist, (size_t)K * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
-    HIP_TRY(c, hipMemcpyAsync(deta, hin, 24, hipMemcpyHostToDevice, s), SBR_EDEVICE);
-    sbr_result_soa r{dres, nullptr, nullptr, dres + 1, dres + 2, dst, nullptr};
-    c->het_aw_path = dpath;
-    rc = sbr_sweep_hetero_dev(c, s, K, dbeta, ddist, deta, dtend, x0, du, 1, 1, p, kappa, lambda, &o, &r, dtin, dtout);
-    c->het_aw_path = nullptr;
-    if (rc) return rc;
-    int32_t n = 0;
-    HIP_TRY(c, hipMemcpyAsync(res, dres, 24, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
-    HIP_TRY(c, hipMemcpyAsync(status, dst, 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
-    if (tau_in) HIP_TRY(c, hipMemcpyAsync(tau_in, dtin, (size_t)K * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
-    if (tau_out) HIP_TRY(c, hipMemcpyAsync(tau_out, dtout, (size_t)K * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
-    HIP_TRY(c, hipMemcpyAsync(&n, c->H.n_knots, 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
-    HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
-    if (n_knots) *n_knots = n;
-    if (n > cap) return fail(c, SBR_EARG, "path capacity too small");
-    if (t) HIP_TRY(c, hipMemcpy(t, c->H.t, (size_t)n * 8, hipMemcpyDeviceToHost), SBR_EDEVICE);
-    if (G) HIP_TRY(c, hipMemcpy(G, c->H.G, (size_t)n * K * 8, hipMemcpyDeviceToHost), SBR_EDEVICE);
-    if (aw_total) {
-        if (*status & SBR_RUN) HIP_TRY(c, hipMemcpy(aw_total, dpath, (size_t)n * 8, hipMemcpyDeviceToHost), SBR_EDEVICE);
-        else for (int i = 0; i < n; i++) aw_total[i] = NAN;
-    }
-    return SBR_OK;
+    return fenced(c, nullptr, false, [&](hipStream_t s) -> int {
+        const double hin[3] = {eta, t_end, u};
+        HIP_TRY(c, hipMemcpyAsync(dbeta, betas, (size_t)K * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+        HIP_TRY(c, hipMemcpyAsync(ddist, dist, (size_t)K * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+        HIP_TRY(c, hipMemcpyAsync(deta, hin, 24, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+        sbr_result_soa r{dres, nullptr, nullptr, dres + 1, dres + 2, dst, nullptr};
+        c->het_aw_path = dpath;
+        rc = sbr_sweep_hetero_dev(c, s, K, dbeta, ddist, deta, dtend, x0, du, 1, 1, p, kappa, lambda, &o, &r, dtin, dtout);
+        c->het_aw_path = nullptr;
+        if (rc) return rc;
+        int32_t n = 0;
+        HIP_TRY(c, hipMemcpyAsync(res, dres, 24, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        HIP_TRY(c, hipMemcpyAsync(status, dst, 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        if (tau_in) HIP_TRY(c, hipMemcpyAsync(tau_in, dtin, (size_t)K * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        if (tau_out) HIP_TRY(c, hipMemcpyAsync(tau_out, dtout, (size_t)K * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        HIP_TRY(c, hipMemcpyAsync(&n, c->H.n_knots, 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
+        if (n_knots) *n_knots = n;
+        if (n > cap) return fail(c, SBR_EARG, "path capacity too small");
+        if (t) HIP_TRY(c, hipMemcpy(t, c->H.t, (size_t)n * 8, hipMemcpyDeviceToHost), SBR_EDEVICE);
+        if (G) HIP_TRY(c, hipMemcpy(G, c->H.G, (size_t)n * K * 8, hipMemcpyDeviceToHost), SBR_EDEVICE);
+        if (aw_total) {
+            if (*status & SBR_RUN) HIP_TRY(c, hipMemcpy(aw_total, dpath, (size_t)n * 8, hipMemcpyDeviceToHost), SBR_EDEVICE);
+            else for (int i = 0; i < n; i++) aw_total[i] = NAN;
+        }
+        return SBR_OK;
+    });
 }
 
 int sbr_sweep_hetero(sbr_ctx* c, int32_t K, const double* betas, const double* dist, const double* eta,
@@ -1017,25 +1075,26 @@ int sbr_sweep_hetero(sbr_ctx* c, int32_t K, const double* betas, const double* d
     int32_t* dit = (int32_t*)(dst + np);
     double* dtin = (double*)(dit + np);
     double* dtout = dtin + np * K;
-    hipStream_t s = c->stream;
-    HIP_TRY(c, hipMemcpyAsync(dbeta, betas, (size_t)n_col * K * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
-    HIP_TRY(c, hipMemcpyAsync(ddist, dist, (size_t)K * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
-    HIP_TRY(c, hipMemcpyAsync(deta, eta, (size_t)n_col * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
-    HIP_TRY(c, hipMemcpyAsync(dtend, t_end, (size_t)n_col * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
-    HIP_TRY(c, hipMemcpyAsync(du, u, (size_t)n_u * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
-    sbr_result_soa r{dxi, nullptr, nullptr, daw, dtol, dst, dit};
-    rc = sbr_sweep_hetero_dev(c, s, K, dbeta, ddist, deta, dtend, x0, du, n_col, n_u, p, kappa, lambda, opts, &r,
-                              tau_in ? dtin : nullptr, tau_out ? dtout : nullptr);
-    if (rc) return rc;
-    if (out->xi) HIP_TRY(c, hipMemcpyAsync(out->xi, dxi, np * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
-    if (out->aw_max) HIP_TRY(c, hipMemcpyAsync(out->aw_max, daw, np * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
-    if (out->tol) HIP_TRY(c, hipMemcpyAsync(out->tol, dtol, np * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
-    if (out->status) HIP_TRY(c, hipMemcpyAsync(out->status, dst, np * 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
-    if (out->iters) HIP_TRY(c, hipMemcpyAsync(out->iters, dit, np * 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
-    if (tau_in) HIP_TRY(c, hipMemcpyAsync(tau_in, dtin, np * K * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
-    if (tau_out) HIP_TRY(c, hipMemcpyAsync(tau_out, dtout, np * K * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
-    HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
-    return SBR_OK;
+    return fenced(c, nullptr, false, [&](hipStream_t s) -> int {
+        HIP_TRY(c, hipMemcpyAsync(dbeta, betas, (size_t)n_col * K * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+        HIP_TRY(c, hipMemcpyAsync(ddist, dist, (size_t)K * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+        HIP_TRY(c, hipMemcpyAsync(deta, eta, (size_t)n_col * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+        HIP_TRY(c, hipMemcpyAsync(dtend, t_end, (size_t)n_col * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+        HIP_TRY(c, hipMemcpyAsync(du, u, (size_t)n_u * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+        sbr_result_soa r{dxi, nullptr, nullptr, daw, dtol, dst, dit};
+        rc = sbr_sweep_hetero_dev(c, s, K, dbeta, ddist, deta, dtend, x0, du, n_col, n_u, p, kappa, lambda, opts, &r,
+                                  tau_in ? dtin : nullptr, tau_out ? dtout : nullptr);
+        if (rc) return rc;
+        if (out->xi) HIP_TRY(c, hipMemcpyAsync(out->xi, dxi, np * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        if (out->aw_max) HIP_TRY(c, hipMemcpyAsync(out->aw_max, daw, np * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        if (out->tol) HIP_TRY(c, hipMemcpyAsync(out->tol, dtol, np * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        if (out->status) HIP_TRY(c, hipMemcpyAsync(out->status, dst, np * 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        if (out->iters) HIP_TRY(c, hipMemcpyAsync(out->iters, dit, np * 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        if (tau_in) HIP_TRY(c, hipMemcpyAsync(tau_in, dtin, np * K * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        if (tau_out) HIP_TRY(c, hipMemcpyAsync(tau_out, dtout, np * K * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
+        return SBR_OK;
+    });
 }
 
 int sbr_social_prof_read(sbr_ctx* c, int64_t* out8)
@@ -1267,10 +1326,10 @@ int sbr_sweep_social_dev(sbr_ctx* c, void* stream, const double* beta, const dou
     if (rc) return rc;
     if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
     sbr_opts o = resolve(opts);
-    NullFence fence(c, stream); // NULL = HIP null stream (torch default stream)
-    hipStream_t s = fence.get(stream);
-    return run_social(c, s, beta, eta, x0, u, n_beta, n_u, p, kappa, lambda, cmp_grid, n_cmp, tol, max_iter, o, out,
-                      fp_iters, rk_steps, 0);
+    return fenced(c, stream, true, [&](hipStream_t s) {
+        return run_social(c, s, beta, eta, x0, u, n_beta, n_u, p, kappa, lambda, cmp_grid, n_cmp, tol, max_iter, o,
+                          out, fp_iters, rk_steps, 0);
+    });
 }
 
 int sbr_social_point_paths(sbr_ctx* c, double beta, double eta, double x0, double u, double p, double kappa,
@@ -1338,23 +1397,24 @@ int sbr_sweep_social(sbr_ctx* c, const double* beta, const double* eta, double x
     int32_t* dit = (int32_t*)(dst + np);
     int32_t* dfp = dit + np;
     int64_t* dsteps = (int64_t*)(dfp + 2 * np);
-    hipStream_t s = c->stream;
-    HIP_TRY(c, hipMemcpyAsync(dbeta, beta, (size_t)n_beta * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
-    HIP_TRY(c, hipMemcpyAsync(deta, eta, (size_t)n_beta * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
-    HIP_TRY(c, hipMemcpyAsync(du, u, (size_t)n_u * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
-    HIP_TRY(c, hipMemcpyAsync(dcmp, cmp_grid, (size_t)n_beta * n_cmp * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
-    sbr_result_soa r{dxi, dtin, dtout, daw, dtol, dst, dit};
-    rc = run_social(c, s, dbeta, deta, x0, du, n_beta, n_u, p, kappa, lambda, dcmp, n_cmp, tol, max_iter, o, &r, dfp,
-                    dsteps, 8);
-    if (rc) return rc;
-    struct { void* h; const void* dv; size_t b; } cp[] = {
-        {out->xi, dxi, np * 8}, {out->tau_in_unc, dtin, np * 8}, {out->tau_out_unc, dtout, np * 8},
-        {out->aw_max, daw, np * 8}, {out->tol, dtol, np * 8}, {out->status, dst, np * 4},
-        {out->iters, dit, np * 4}, {fp_iters, dfp, np * 4}, {rk_steps, dsteps, np * 8}};
-    for (auto& x : cp)
-        if (x.h) HIP_TRY(c, hipMemcpyAsync(x.h, x.dv, x.b, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
-    HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
-    return SBR_OK;
+    return fenced(c, nullptr, false, [&](hipStream_t s) -> int {
+        HIP_TRY(c, hipMemcpyAsync(dbeta, beta, (size_t)n_beta * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+        HIP_TRY(c, hipMemcpyAsync(deta, eta, (size_t)n_beta * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+        HIP_TRY(c, hipMemcpyAsync(du, u, (size_t)n_u * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+        HIP_TRY(c, hipMemcpyAsync(dcmp, cmp_grid, (size_t)n_beta * n_cmp * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+        sbr_result_soa r{dxi, dtin, dtout, daw, dtol, dst, dit};
+        rc = run_social(c, s, dbeta, deta, x0, du, n_beta, n_u, p, kappa, lambda, dcmp, n_cmp, tol, max_iter, o, &r, dfp,
+                        dsteps, 8);
+        if (rc) return rc;
+        struct { void* h; const void* dv; size_t b; } cp[] = {
+            {out->xi, dxi, np * 8}, {out->tau_in_unc, dtin, np * 8}, {out->tau_out_unc, dtout, np * 8},
+            {out->aw_max, daw, np * 8}, {out->tol, dtol, np * 8}, {out->status, dst, np * 4},
+            {out->iters, dit, np * 4}, {fp_iters, dfp, np * 4}, {rk_steps, dsteps, np * 8}};
+        for (auto& x : cp)
+            if (x.h) HIP_TRY(c, hipMemcpyAsync(x.h, x.dv, x.b, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
+        return SBR_OK;
+    });
 }
 
 int sbr_device_info(sbr_ctx* c, int32_t* lds_bytes_per_block, int32_t* lds_knot_capacity, int32_t* cu_count)
@@ -1402,7 +1462,32 @@ __global__ void detmath_kernel(const double* x, const double* y, int n, double* 
     l[i] = sbr_log(x[i]);
     pw[i] = sbr_pow_pos(x[i], y[i]);
 }
+
+__global__ void fastpow_kernel(const double* x, const double* y, int n, double* out)
+{
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    out[i] = sbr_fastpow(x[i], y[i]);
+}
 }  // namespace
+
+extern "C" int sbr_selftest_fastpow(sbr_ctx* c, const double* x, const double* y, int n, double* out)
+{
+    if (!c || n <= 0 || !x || !y || !out) return SBR_EARG;
+    if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
+    int rc = ensure_stage(c, (size_t)n * 3 * 8);
+    if (rc) return rc;
+    return fenced(c, nullptr, false, [&](hipStream_t s) -> int {
+        double* d = (double*)c->stage;
+        HIP_TRY(c, hipMemcpyAsync(d, x, n * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+        HIP_TRY(c, hipMemcpyAsync(d + n, y, n * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+        hipLaunchKernelGGL(fastpow_kernel, dim3((n + 255) / 256), dim3(256), 0, s, d, d + n, n, d + 2 * n);
+        HIP_TRY(c, hipGetLastError(), SBR_EDEVICE);
+        HIP_TRY(c, hipMemcpyAsync(out, d + 2 * n, n * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
+        return SBR_OK;
+    });
+}
 
 extern "C" int sbr_selftest_detmath(sbr_ctx* c, const double* x, const double* y, int n, double* e, double* l,
                                     double* pw)
@@ -1412,15 +1497,16 @@ extern "C" int sbr_selftest_detmath(sbr_ctx* c, const double* x, const double* y
     int rc = ensure_stage(c, (size_t)n * 5 * 8);
     if (rc) return rc;
     double* d = (double*)c->stage;
-    hipStream_t s = c->stream;
-    HIP_TRY(c, hipMemcpyAsync(d, x, n * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
-    HIP_TRY(c, hipMemcpyAsync(d + n, y, n * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
-    hipLaunchKernelGGL(detmath_kernel, dim3((n + 255) / 256), dim3(256), 0, s, d, d + n, n, d + 2 * n, d + 3 * n,
-                       d + 4 * n);
-    HIP_TRY(c, hipGetLastError(), SBR_EDEVICE);
-    HIP_TRY(c, hipMemcpyAsync(e, d + 2 * n, n * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
-    HIP_TRY(c, hipMemcpyAsync(l, d + 3 * n, n * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
-    HIP_TRY(c, hipMemcpyAsync(pw, d + 4 * n, n * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
-    HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
-    return SBR_OK;
+    return fenced(c, nullptr, false, [&](hipStream_t s) -> int {
+        HIP_TRY(c, hipMemcpyAsync(d, x, n * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+        HIP_TRY(c, hipMemcpyAsync(d + n, y, n * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+        hipLaunchKernelGGL(detmath_kernel, dim3((n + 255) / 256), dim3(256), 0, s, d, d + n, n, d + 2 * n, d + 3 * n,
+                           d + 4 * n);
+        HIP_TRY(c, hipGetLastError(), SBR_EDEVICE);
+        HIP_TRY(c, hipMemcpyAsync(e, d + 2 * n, n * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        HIP_TRY(c, hipMemcpyAsync(l, d + 3 * n, n * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        HIP_TRY(c, hipMemcpyAsync(pw, d + 4 * n, n * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
+        return SBR_OK;
+    });
 }

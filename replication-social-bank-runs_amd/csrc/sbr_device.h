@@ -31,13 +31,13 @@ constexpr double A71 = 0.09646076681806523, A72 = 0.01, A73 = 0.4798896504144996
 constexpr double BT1 = -0.00178001105222577714, BT2 = -0.0008164344596567469, BT3 = 0.007880878010261995,
                  BT4 = -0.1447110071732629, BT5 = 0.5823571654525552, BT6 = -0.45808210592918697,
                  BT7 = 0.015151515151515152;
-constexpr double TSIT5_STABILITY = 3.5068469938049235;
+constexpr double TSIT5_STABILITY = 3.5068; // alg_stability_size(::Tsit5)
 
 // ---- PI controller defaults (OrdinaryDiffEqCore, 5th-order method) -------
 constexpr double CTL_BETA1 = 0.14, CTL_BETA2 = 0.08, CTL_INV_QMIN = 5.0, CTL_INV_QMAX = 0.1, CTL_GAMMA = 0.9,
                  CTL_QOLDMIN = 1e-4;
 constexpr double AUTOSWITCH_TOL = 0.9;
-constexpr int AUTOSWITCH_MAXSTIFF = 10;
+constexpr int AUTOSWITCH_MAXSTIFF = 10, AUTOSWITCH_MAXNONSTIFF = 3;
 constexpr double DBL_EPS = 2.220446049250313e-16;
 
 // The bisection's collapse test `abs(d) < 2·eps(d)` (solver.jl:440) in one
@@ -86,17 +86,34 @@ struct ConstDiv {
     }
 };
 
+// AutoSwitch (OrdinaryDiffEqCore composite_algs: maxstiffstep 10, maxnonstiffstep 3,
+// stifftol = nonstifftol = 9/10, dtfac 2): in every loopheader!, is_stiff =
+// |eigen_est·dt / stability(Tsit5)| > 9/10; successive positives count up, negatives
+// down; > 10 switches Tsit5 → Rosenbrock23 (dt ×2), < −3 switches back (dt ÷2).
+// choose() returns true when the algorithm changes.
 struct AutoSwitch {
     int count = 0;
-    bool switched = false;
+    bool stiff = false;
+    int nswitch = 0;
     ConstDiv by_stab{TSIT5_STABILITY};
-    __device__ __forceinline__ void update(double eig, double dt)
+    __device__ __forceinline__ bool choose(double eig, double& dt)
     {
-        double stiffness = fabs(by_stab(eig * dt));
-        bool st = stiffness > AUTOSWITCH_TOL;
-        if (st) count = count < 0 ? 1 : count + 1;
-        else count = count > 0 ? -1 : count - 1;
-        if (count > AUTOSWITCH_MAXSTIFF) switched = true;
+        const double stiffness = fabs(by_stab(eig * dt));
+        const bool st = stiffness > AUTOSWITCH_TOL; // NaN -> false
+        count = st ? (count < 0 ? 1 : count + 1) : (count > 0 ? -1 : count - 1);
+        if (!stiff && count > AUTOSWITCH_MAXSTIFF) {
+            dt = dt * 2.0;
+            stiff = true;
+            nswitch++;
+            return true;
+        }
+        if (stiff && count < -AUTOSWITCH_MAXNONSTIFF) {
+            dt = dt / 2.0;
+            stiff = false;
+            nswitch++;
+            return true;
+        }
+        return false;
     }
 };
 

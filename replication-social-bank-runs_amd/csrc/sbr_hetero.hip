@@ -17,6 +17,7 @@
 // Bit-exact against oracle/sbr_oracle.c (sbro_sweep_hetero).
 #include "sbr_device.h"
 #include "sbr_kernels.h"
+#include "sbr_ode.h"
 #include "sbr_scan.h"
 
 namespace sbr {
@@ -47,6 +48,102 @@ __device__ __forceinline__ double rms(const double* v)
     for (int i = 0; i < K; i++) s = s + v[i] * v[i];
     return sqrt(s / (double)K);
 }
+
+// ForwardDiff jacobian of rhs (oracle jac_hetero): b_k = (1 − I_k)·β_k,
+// J_kj = dist_j·b_k (j ≠ k), J_kk = (−β_k)·ω + dist_k·b_k; autonomous (∂f/∂t = 0)
+template <int K>
+__device__ __forceinline__ void jac(const double* __restrict__ dist, const double* b, const double* I, double* J)
+{
+    const double w = omega<K>(dist, I);
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const double bk = (1.0 - I[k]) * b[k];
+#pragma unroll
+        for (int j = 0; j < K; j++) J[k * K + j] = (j == k) ? (-b[k]) * w + dist[k] * bk : dist[j] * bk;
+    }
+}
+
+// opnorm(J, Inf) (NaN-propagating max of the row sums): Rosenbrock23's eigen_est
+template <int K>
+__device__ __forceinline__ double opnorm_inf(const double* J)
+{
+    double nrm = 0.0;
+#pragma unroll
+    for (int i = 0; i < K; i++) {
+        double s = 0.0;
+#pragma unroll
+        for (int j = 0; j < K; j++) s = s + fabs(J[i * K + j]);
+        nrm = (nrm != nrm || s != s) ? (double)NAN : (s > nrm ? s : nrm);
+    }
+    return nrm;
+}
+
+// K×K LU in registers (oracle lu_factor / lu_solve): generic_lufact! with RowMaximum
+// pivoting, then getrs (row interchanges, unit-lower and upper column sweeps in fma,
+// division by the pivots).  Row interchanges are selects so every index is static.
+template <int K>
+struct RegLU {
+    double A[K * K];
+    int piv[K];
+    __device__ __forceinline__ void factor()
+    {
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            int kp = k;
+            double amax = fabs(A[k * K + k]), pv = A[k * K + k];
+#pragma unroll
+            for (int i = k + 1; i < K; i++) {
+                const double ai = fabs(A[i * K + k]);
+                if (ai > amax) { kp = i; amax = ai; pv = A[i * K + k]; }
+            }
+            piv[k] = kp;
+            if (pv != 0.0) {
+#pragma unroll
+                for (int i = k + 1; i < K; i++) {
+                    const bool sw = kp == i;
+#pragma unroll
+                    for (int j = 0; j < K; j++) {
+                        const double a = A[k * K + j], c = A[i * K + j];
+                        A[k * K + j] = sw ? c : a;
+                        A[i * K + j] = sw ? a : c;
+                    }
+                }
+                const double inv = 1.0 / A[k * K + k];
+#pragma unroll
+                for (int i = k + 1; i < K; i++) A[i * K + k] = A[i * K + k] * inv;
+            }
+#pragma unroll
+            for (int j = k + 1; j < K; j++)
+#pragma unroll
+                for (int i = k + 1; i < K; i++) A[i * K + j] = A[i * K + j] - A[i * K + k] * A[k * K + j];
+        }
+    }
+    __device__ __forceinline__ void solve(double* b) const
+    {
+#pragma unroll
+        for (int k = 0; k < K; k++)
+#pragma unroll
+            for (int i = k + 1; i < K; i++) {
+                const bool sw = piv[k] == i;
+                const double x = b[k], y = b[i];
+                b[k] = sw ? y : x;
+                b[i] = sw ? x : y;
+            }
+#pragma unroll
+        for (int j = 0; j < K; j++) {
+            const double a = -b[j];
+#pragma unroll
+            for (int i = j + 1; i < K; i++) b[i] = fma(a, A[i * K + j], b[i]);
+        }
+#pragma unroll
+        for (int j = K - 1; j >= 0; j--) {
+            b[j] = b[j] / A[j * K + j];
+            const double a = -b[j];
+#pragma unroll
+            for (int i = 0; i < j; i++) b[i] = fma(a, A[i * K + j], b[i]);
+        }
+    }
+};
 
 template <int K>
 __global__ __launch_bounds__(64) void learn_hetero_kernel(const double* __restrict__ betas,
@@ -88,7 +185,7 @@ __global__ __launch_bounds__(64) void learn_hetero_kernel(const double* __restri
 #pragma unroll
     for (int k = 0; k < K; k++) buf[k] = k1[k] / sk[k];
     const double d1 = rms<K>(buf);
-    double dt0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * (d0 / d1);
+    double dt0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : (d0 / d1) / 100.0;
     dt0 = dmin(dt0, dtmax);
     double dt;
     if (dt0 < 10.0 * DBL_EPS) {
@@ -159,71 +256,107 @@ __global__ __launch_bounds__(64) void learn_hetero_kernel(const double* __restri
         n++;
     };
 
-    const double LOG_QOLDMIN = sbr_log(CTL_QOLDMIN);
     const double snap = 100.0 * sbr_jl_eps(T1);
-    double t = T0, qold = CTL_QOLDMIN, lqold = LOG_QOLDMIN;
+    double t = T0;
+    double eig = 1.0; // integrator.eigen_est at init
+    PIControl pc;
     AutoSwitch as;
-    const ConstDiv by_gamma(CTL_GAMMA);
     int naccept = 0, nreject = 0;
     push(t, x);
     int64_t iter = 0;
     while (t < T1 && !done) {
         if (++iter > a.maxiters) { st |= SBR_ODE_MAXITERS; break; }
+        if (as.choose(eig, dt)) rhs<K>(dist, b, x, k1); // initialize!: fsalfirst = f(uprev, t)
         dt = dmin(dtmax, dt);
         dt = dmax(dt, dtmin);
         dt = dmin(dt, T1 - t);
-        const double a21 = dt * A21;
+        if (dt <= dtmin && t + dt < T1) { st |= SBR_ODE_FAILED; break; } // DtLessThanMin
+        double EEst;
+        if (as.stiff) {
+            // ---- Rosenbrock23 (perform_step!, Rosenbrock23Cache, @muladd); k7 <- fsallast ----
+            const double dtg = dt * ROS23_D;
+            const double invdtg = 1.0 / dtg, neginvdtg = -(1.0 / dtg);
+            const double dto2 = dt / 2.0, dto6 = dt / 6.0;
+            RegLU<K> W;
+            jac<K>(dist, b, x, W.A);
+            eig = opnorm_inf<K>(W.A);
 #pragma unroll
-        for (int k = 0; k < K; k++) tmp[k] = fma(a21, k1[k], x[k]);
-        rhs<K>(dist, b, tmp, k2);
+            for (int k = 0; k < K; k++) W.A[k * K + k] = fma(-1.0, invdtg, W.A[k * K + k]);
+            W.factor();
+            double* s1 = k2; // Tsit5's stage arrays are free in a stiff step
+            double* s2 = k3;
+            double* f1 = k4;
+            double* r = k5;
 #pragma unroll
-        for (int k = 0; k < K; k++) tmp[k] = fma(dt, fma(A31, k1[k], A32 * k2[k]), x[k]);
-        rhs<K>(dist, b, tmp, k3);
+            for (int k = 0; k < K; k++) r[k] = k1[k] + dtg * 0.0; // fsalfirst + dt·d·∂f/∂t
+            W.solve(r);
 #pragma unroll
-        for (int k = 0; k < K; k++) tmp[k] = fma(dt, fma(A41, k1[k], fma(A42, k2[k], A43 * k3[k])), x[k]);
-        rhs<K>(dist, b, tmp, k4);
+            for (int k = 0; k < K; k++) { s1[k] = r[k] * neginvdtg; tmp[k] = fma(dto2, s1[k], x[k]); }
+            rhs<K>(dist, b, tmp, f1);
 #pragma unroll
-        for (int k = 0; k < K; k++)
-            tmp[k] = fma(dt, fma(A51, k1[k], fma(A52, k2[k], fma(A53, k3[k], A54 * k4[k]))), x[k]);
-        rhs<K>(dist, b, tmp, k5);
+            for (int k = 0; k < K; k++) r[k] = f1[k] - s1[k];
+            W.solve(r);
 #pragma unroll
-        for (int k = 0; k < K; k++)
-            tmp6[k] = fma(dt, fma(A61, k1[k], fma(A62, k2[k], fma(A63, k3[k], fma(A64, k4[k], A65 * k5[k])))), x[k]);
-        rhs<K>(dist, b, tmp6, k6);
+            for (int k = 0; k < K; k++) { s2[k] = fma(r[k], neginvdtg, s1[k]); u[k] = fma(dt, s2[k], x[k]); }
+            rhs<K>(dist, b, u, k7);
 #pragma unroll
-        for (int k = 0; k < K; k++)
-            u[k] = fma(dt, fma(A71, k1[k], fma(A72, k2[k], fma(A73, k3[k], fma(A74, k4[k], fma(A75, k5[k], A76 * k6[k]))))),
-                       x[k]);
-        rhs<K>(dist, b, u, k7);
-        double eig = 0.0;
-        bool eig_nan = false;
+            for (int k = 0; k < K; k++)
+                r[k] = fma(dt, 0.0, fma(-2.0, s1[k] - k1[k], fma(-ROS23_C32, s2[k] - f1[k], k7[k])));
+            W.solve(r);
 #pragma unroll
-        for (int k = 0; k < K; k++) {
-            const double r = fabs((k7[k] - k6[k]) / (u[k] - tmp6[k]));
-            if (r != r) eig_nan = true;
-            else if (r > eig) eig = r;
-        }
-        if (eig_nan) eig = NAN;
-#pragma unroll
-        for (int k = 0; k < K; k++) {
-            const double ut = dt * fma(BT1, k1[k], fma(BT2, k2[k], fma(BT3, k3[k], fma(BT4, k4[k],
-                                       fma(BT5, k5[k], fma(BT6, k6[k], BT7 * k7[k]))))));
-            buf[k] = ut / fma(dmax(fabs(x[k]), fabs(u[k])), rtol, atol);
-        }
-        const double EEst = rms<K>(buf);
-        double q, le = 0.0;
-        if (EEst == 0.0) {
-            q = CTL_INV_QMAX;
+            for (int k = 0; k < K; k++) {
+                const double s3 = r[k] * neginvdtg;
+                const double ut = dto6 * (fma(-2.0, s2[k], s1[k]) + s3);
+                buf[k] = ut / fma(dmax(fabs(x[k]), fabs(u[k])), rtol, atol);
+            }
+            EEst = rms<K>(buf);
         } else {
-            le = sbr_log(EEst);
-            q = sbr_exp(CTL_BETA1 * le - CTL_BETA2 * lqold);
-            q = dmax(CTL_INV_QMAX, dmin(CTL_INV_QMIN, by_gamma(q)));
+            const double a21 = dt * A21;
+#pragma unroll
+            for (int k = 0; k < K; k++) tmp[k] = fma(a21, k1[k], x[k]);
+            rhs<K>(dist, b, tmp, k2);
+#pragma unroll
+            for (int k = 0; k < K; k++) tmp[k] = fma(dt, fma(A31, k1[k], A32 * k2[k]), x[k]);
+            rhs<K>(dist, b, tmp, k3);
+#pragma unroll
+            for (int k = 0; k < K; k++) tmp[k] = fma(dt, fma(A41, k1[k], fma(A42, k2[k], A43 * k3[k])), x[k]);
+            rhs<K>(dist, b, tmp, k4);
+#pragma unroll
+            for (int k = 0; k < K; k++)
+                tmp[k] = fma(dt, fma(A51, k1[k], fma(A52, k2[k], fma(A53, k3[k], A54 * k4[k]))), x[k]);
+            rhs<K>(dist, b, tmp, k5);
+#pragma unroll
+            for (int k = 0; k < K; k++)
+                tmp6[k] = fma(dt, fma(A61, k1[k], fma(A62, k2[k], fma(A63, k3[k], fma(A64, k4[k], A65 * k5[k])))), x[k]);
+            rhs<K>(dist, b, tmp6, k6);
+#pragma unroll
+            for (int k = 0; k < K; k++)
+                u[k] = fma(dt, fma(A71, k1[k], fma(A72, k2[k], fma(A73, k3[k], fma(A74, k4[k], fma(A75, k5[k], A76 * k6[k]))))),
+                           x[k]);
+            rhs<K>(dist, b, u, k7);
+            double e = 0.0;
+            bool e_nan = false;
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+                const double rr = fabs((k7[k] - k6[k]) / (u[k] - tmp6[k]));
+                if (rr != rr) e_nan = true;
+                else if (rr > e) e = rr;
+            }
+            eig = e_nan ? (double)NAN : e;
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+                const double ut = dt * fma(BT1, k1[k], fma(BT2, k2[k], fma(BT3, k3[k], fma(BT4, k4[k],
+                                           fma(BT5, k5[k], fma(BT6, k6[k], BT7 * k7[k]))))));
+                buf[k] = ut / fma(dmax(fabs(x[k]), fabs(u[k])), rtol, atol);
+            }
+            EEst = rms<K>(buf);
         }
+        if (EEst != EEst) { st |= SBR_ODE_FAILED; break; } // NaN trial state (ReturnCode.Unstable)
+        const double q = pc.q(EEst);
         if (EEst <= 1.0) {
             naccept++;
             const double dtnew = dt / q;
-            qold = dmax(EEst, CTL_QOLDMIN);
-            lqold = (qold == EEst) ? le : LOG_QOLDMIN;
+            pc.accept(EEst);
             double tn = t + dt;
             if (fabs(tn - T1) < snap) tn = T1;
             t = tn;
@@ -233,13 +366,11 @@ __global__ __launch_bounds__(64) void learn_hetero_kernel(const double* __restri
             push(t, x);
         } else {
             nreject++;
-            const double q11 = sbr_exp(CTL_BETA1 * le);
-            dt = dt / dmin(CTL_INV_QMIN, by_gamma(q11));
+            dt = dt / pc.reject_div();
         }
         if (!(dt > 0.0) || !isfinite(dt)) { st |= SBR_ODE_FAILED; break; }
-        as.update(eig, dt);
     }
-    if (as.switched) st |= SBR_STIFF_SWITCH;
+    if (as.nswitch > 0) st |= SBR_STIFF_SWITCH;
     int n_le = m;
     if (past) {
         n_le = m - 1;

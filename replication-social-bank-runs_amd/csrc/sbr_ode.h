@@ -1,0 +1,237 @@
+// sbr_ode.h — OrdinaryDiffEq's AutoTsit5(Rosenbrock23()) at reltol = abstol =
+// eps() on the device: one lane integrates one ODE.  The reference solves every
+// learning / value-function ODE with it (learning.jl:51,
+// heterogeneity_learning.jl:74, social_learning_dynamics.jl:71,
+// value_function_solver.jl:105; OrdinaryDiffEqCore 1.34.0, OrdinaryDiffEqTsit5
+// 1.5.0, OrdinaryDiffEqRosenbrock 1.18.1 — not vendored, restated in
+// oracle/sbr_oracle.c, which these routines match bit for bit):
+//
+//   * ode_determine_initdt (Tsit5 current at init);
+//   * per loop iteration (loopheader!): AutoSwitch's stiffness test on the
+//     last eigen_est and the proposed dt — 11 successive positives switch to
+//     Rosenbrock23 (dt ×2), 4 successive negatives switch back (dt ÷2); the
+//     new algorithm re-evaluates fsalfirst = f(uprev, t);
+//   * Tsit5 (eigen_est = |(k7 − k6)/(u − g6)|) or Rosenbrock23 (eigen_est =
+//     ‖J‖_∞, W = J − I/(dt·d), three linear solves);
+//   * the PI controller with FastPower.fastpower (Float32) for EEst^β1 and
+//     qold^β2, accept / reject, tstop clipping and the 100·eps snap.
+//
+// Scalar systems (baseline learning, social forced ODE, interest value function)
+// use ode_scalar; the K-group hetero system has its own loop (sbr_hetero.hip)
+// on the same PIControl / AutoSwitch / Rosenbrock23 pieces.
+#pragma once
+
+#include "sbr_device.h"
+
+namespace sbr {
+
+// Rosenbrock23Tableau: c32 = 6 + sqrt(2), d = 1/(2 + sqrt(2))
+constexpr double ROS23_C32 = 0x1.da827999fcef3p+2;
+constexpr double ROS23_D = 0x1.2bec333018867p-2;
+
+// PIController (OrdinaryDiffEqCore controllers.jl) with FastPower.fastpower:
+//   q11 = fastpower(EEst, β1); q = clamp(q11 / fastpower(qold, β2) / γ, 1/qmax, 1/qmin)
+//   accept: dtnew = dt / q, qold = max(EEst, qoldinit); reject: dt /= min(1/qmin, q11/γ)
+// fastpower(qold, β2) is refreshed only when qold changes.
+struct PIControl {
+    double qold = CTL_QOLDMIN;
+    double qold_b2;
+    double q11 = 0.0;
+    ConstDiv by_gamma{CTL_GAMMA};
+    __device__ __forceinline__ PIControl() : qold_b2(sbr_fastpow(CTL_QOLDMIN, CTL_BETA2)) {}
+    __device__ __forceinline__ double q(double EEst)
+    {
+        if (EEst == 0.0) return CTL_INV_QMAX;
+        q11 = sbr_fastpow(EEst, CTL_BETA1);
+        const double qq = q11 / qold_b2;
+        return dmax(CTL_INV_QMAX, dmin(CTL_INV_QMIN, by_gamma(qq)));
+    }
+    __device__ __forceinline__ void accept(double EEst)
+    {
+        const double qn = dmax(EEst, CTL_QOLDMIN);
+        if (qn != qold) {
+            qold = qn;
+            qold_b2 = sbr_fastpow(qn, CTL_BETA2);
+        }
+    }
+    __device__ __forceinline__ double reject_div() const { return dmin(CTL_INV_QMIN, by_gamma(q11)); }
+};
+
+// Rosenbrock23's dense output (_ode_interpolant, @muladd):
+// y0 + dt·(c1·k1 + c2·k2), c1 = Θ(1 − Θ)/(1 − 2d), c2 = Θ(Θ − 2d)/(1 − 2d)
+__device__ __forceinline__ double ros23_dense(double th, double dt, double y0, double k1, double k2)
+{
+    const double omd = 1.0 - 2.0 * ROS23_D;
+    const double c1 = (th * (1.0 - th)) / omd;
+    const double c2 = (th * fma(-2.0, ROS23_D, th)) / omd;
+    return fma(dt, fma(c1, k1, c2 * k2), y0);
+}
+
+// the stages of an accepted step, for dense output (stiff: k[0], k[1] = Rosenbrock23's k1, k2)
+struct StepK {
+    double k[7];
+    bool stiff;
+};
+
+struct OdeOut {
+    int64_t naccept = 0, nreject = 0;
+    int32_t nswitch = 0;
+    uint32_t status = 0;
+};
+
+// dx/dt = βx(1 − x) (learning.jl:45-48) with ForwardDiff's ∂f/∂x through (β·x)·(1 − x):
+// β·(1 − x) + (−1)·(β·x); autonomous, ∂f/∂t = 0
+struct LogisticSys {
+    double beta;
+    __device__ __forceinline__ double eval(double, double x) const { return (beta * x) * (1.0 - x); }
+    __device__ __forceinline__ void prepare(double, double) const {}
+    __device__ __forceinline__ double stage(int, double, double x) const { return (beta * x) * (1.0 - x); }
+    __device__ __forceinline__ void jac(double, double x, double& J, double& dT) const
+    {
+        J = beta * (1.0 - x) + (-1.0) * (beta * x);
+        dT = 0.0;
+    }
+    __device__ __forceinline__ void accepted(double) const {}
+};
+
+// ode_determine_initdt for a scalar ODE (order 5: dt₁ = (0.01/max(d₁,d₂))^(1/6));
+// returns dt, sets k1 = f(T0, x0)
+template <class Sys>
+__device__ __forceinline__ double initdt_scalar(Sys& f, double T0, double T1, double x0, double rtol, double atol,
+                                                double& k1)
+{
+    const double dtmax = T1 - T0;
+    const double dtmin = sbr_jl_eps(dmax(fabs(T0), fabs(T1)));
+    const double sk = fma(fabs(x0), rtol, atol);
+    const double d0 = fabs(x0 / sk);
+    k1 = f.eval(T0, x0);
+    const double d1 = fabs(k1 / sk);
+    double dt0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : (d0 / d1) / 100.0;
+    dt0 = dmin(dt0, dtmax);
+    double dt;
+    if (dt0 < 10.0 * DBL_EPS) {
+        dt = dmax(1e-6, dtmin);
+    } else {
+        const double u1 = fma(dt0, k1, x0);
+        const double f1 = f.eval(T0 + dt0, u1);
+        if (k1 == f1) {
+            dt = dmax(dtmin, 100.0 * dt0);
+        } else {
+            const double d2 = fabs((f1 - k1) / sk) / dt0;
+            const double md = dmax(d1, d2);
+            const double dt1 = (md <= 1e-15) ? dmax(1e-6, dt0 * 1e-3) : sbr_pow_pos(0.01 / md, 1.0 / 6.0);
+            dt = dmax(dtmin, dmin(dmin(100.0 * dt0, dt1), dtmax));
+        }
+    }
+    return dt;
+}
+
+// Scalar AutoTsit5(Rosenbrock23()) on (0, T1) from x0.  Sys provides
+//   double eval(double t, double x)                       f at any (t, x)
+//   void   prepare(double t, double dt)                   before the Tsit5 stages of a step
+//   double stage(int s, double ts, double x)              Tsit5 stage s = 1..6 (k2..k7) at time ts
+//   void   jac(double t, double x, double& J, double& dT) ForwardDiff ∂f/∂x, ∂f/∂t
+//   void   accepted(double t)                             after an accepted step
+// Sink provides
+//   bool start(double t0, double x0)                      the first knot; false = stop
+//   bool accept(double tprev, double tn, double dt, double y0, double y1, const StepK& k, bool exact)
+//        exact: tn == tprev + dt (no snap to T1); false = stop
+template <class Sys, class Sink>
+__device__ __forceinline__ void ode_scalar(Sys& f, Sink& sink, double T1, double x0, double rtol, double atol,
+                                           int64_t maxiters, OdeOut& o)
+{
+    const double T0 = 0.0;
+    const double dtmax = T1 - T0;
+    const double dtmin = sbr_jl_eps(dmax(fabs(T0), fabs(T1)));
+    double k1;
+    double dt = initdt_scalar(f, T0, T1, x0, rtol, atol, k1);
+    const double snap = 100.0 * sbr_jl_eps(T1);
+    double t = T0, x = x0;
+    double eig = 1.0; // integrator.eigen_est = 1/oneunit(t) at init
+    PIControl pc;
+    AutoSwitch as;
+    if (!sink.start(t, x)) return;
+    int64_t iter = 0;
+    while (t < T1) {
+        if (++iter > maxiters) { o.status |= SBR_ODE_MAXITERS; break; }
+        if (as.choose(eig, dt)) k1 = f.eval(t, x); // initialize!: fsalfirst = f(uprev, t)
+        dt = dmin(dtmax, dt);
+        dt = dmax(dt, dtmin);
+        dt = dmin(dt, T1 - t);
+        if (dt <= dtmin && t + dt < T1) { o.status |= SBR_ODE_FAILED; break; } // DtLessThanMin
+        StepK K;
+        double u, fnew, EEst;
+        if (as.stiff) {
+            // ---- Rosenbrock23 (perform_step!, @muladd), 1×1 W: the solves are divisions ----
+            K.stiff = true;
+            double J, dT;
+            f.jac(t, x, J, dT);
+            eig = fabs(J);
+            const double dtg = dt * ROS23_D;
+            const double invdtg = 1.0 / dtg, neginvdtg = -(1.0 / dtg);
+            const double dto2 = dt / 2.0, dto6 = dt / 6.0;
+            const double W = fma(-1.0, invdtg, J);
+            const double r1 = k1 + dtg * dT;
+            const double s1 = (r1 / W) * neginvdtg;
+            const double tmp = fma(dto2, s1, x);
+            const double f1 = f.eval(t + dto2, tmp);
+            const double s2 = fma((f1 - s1) / W, neginvdtg, s1);
+            u = fma(dt, s2, x);
+            fnew = f.eval(t + dt, u);
+            const double r3 = fma(dt, dT, fma(-2.0, s1 - k1, fma(-ROS23_C32, s2 - f1, fnew)));
+            const double s3 = (r3 / W) * neginvdtg;
+            const double ut = dto6 * (fma(-2.0, s2, s1) + s3);
+            EEst = fabs(ut / fma(dmax(fabs(x), fabs(u)), rtol, atol));
+            K.k[0] = s1;
+            K.k[1] = s2;
+        } else {
+            // ---- Tsit5 (perform_step!, Tsit5ConstantCache, @muladd) ----
+            K.stiff = false;
+            f.prepare(t, dt);
+            double tmp = fma(dt * A21, k1, x);
+            const double k2 = f.stage(1, fma(C1, dt, t), tmp);
+            tmp = fma(dt, fma(A31, k1, A32 * k2), x);
+            const double k3 = f.stage(2, fma(C2, dt, t), tmp);
+            tmp = fma(dt, fma(A41, k1, fma(A42, k2, A43 * k3)), x);
+            const double k4 = f.stage(3, fma(C3, dt, t), tmp);
+            tmp = fma(dt, fma(A51, k1, fma(A52, k2, fma(A53, k3, A54 * k4))), x);
+            const double k5 = f.stage(4, fma(C4, dt, t), tmp);
+            const double tmp6 = fma(dt, fma(A61, k1, fma(A62, k2, fma(A63, k3, fma(A64, k4, A65 * k5)))), x);
+            const double k6 = f.stage(5, t + dt, tmp6);
+            u = fma(dt, fma(A71, k1, fma(A72, k2, fma(A73, k3, fma(A74, k4, fma(A75, k5, A76 * k6))))), x);
+            const double k7 = f.stage(6, t + dt, u);
+            const double eigr = fabs((k7 - k6) / (u - tmp6));
+            eig = (eigr != eigr) ? (double)NAN : eigr;
+            const double ut =
+                dt * fma(BT1, k1, fma(BT2, k2, fma(BT3, k3, fma(BT4, k4, fma(BT5, k5, fma(BT6, k6, BT7 * k7))))));
+            EEst = fabs(ut / fma(dmax(fabs(x), fabs(u)), rtol, atol));
+            fnew = k7;
+            K.k[0] = k1; K.k[1] = k2; K.k[2] = k3; K.k[3] = k4; K.k[4] = k5; K.k[5] = k6; K.k[6] = k7;
+        }
+        if (EEst != EEst) { o.status |= SBR_ODE_FAILED; break; } // NaN trial state (ReturnCode.Unstable)
+        const double q = pc.q(EEst);
+        if (EEst <= 1.0) {
+            o.naccept++;
+            const double dtnew = dt / q;
+            pc.accept(EEst);
+            const double tdt = t + dt;
+            double tn = tdt;
+            if (fabs(tn - T1) < snap) tn = T1;
+            const double tprev = t, xprev = x, dstep = dt;
+            t = tn;
+            x = u;
+            k1 = fnew;
+            dt = dmax(dmin(dtmax, dtnew), dtmin);
+            if (!sink.accept(tprev, tn, dstep, xprev, u, K, tn == tdt)) break;
+            f.accepted(t);
+        } else {
+            o.nreject++;
+            dt = dt / pc.reject_div();
+        }
+        if (!(dt > 0.0) || !isfinite(dt)) { o.status |= SBR_ODE_FAILED; break; }
+    }
+    o.nswitch = as.nswitch;
+    if (as.nswitch > 0) o.status |= SBR_STIFF_SWITCH;
+}
+
+}  // namespace sbr

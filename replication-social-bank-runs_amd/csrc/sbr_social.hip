@@ -26,6 +26,7 @@
 // -ffp-contract=off, fma() where the oracle has it, shared sbr_exp/sbr_log).
 #include "sbr_device.h"
 #include "sbr_kernels.h"
+#include "sbr_ode.h"
 
 namespace sbr {
 
@@ -179,114 +180,6 @@ __device__ bool promote(const SocialArgs& a, int l, int64_t g, int iter, BView T
     return true;
 }
 
-// ---------------------------------------------------------------------------
-// Tsit5 on one scalar ODE (oracle tsit5_solve with m = 1): initial dt of
-// ode_determine_initdt, PI control, tstop clipping / snap, AutoSwitch test.
-// Rhs: double f(double t, double x)  (may set oob through its own state);
-// Sink: bool push(double t, double x, bool exact_last_stage) — false = stop.
-// ---------------------------------------------------------------------------
-struct OdeOut {
-    int64_t naccept = 0, nreject = 0;
-    uint32_t status = 0;
-};
-
-template <class Rhs, class Sink>
-__device__ __forceinline__ void tsit5_scalar(Rhs& f, Sink& push, double T1, double x0, double rtol, double atol,
-                                             int64_t maxiters, OdeOut& o)
-{
-    const double T0 = 0.0;
-    const double dtmax = T1 - T0;
-    const double dtmin = sbr_jl_eps(dmax(fabs(T0), fabs(T1)));
-    // ---- ode_determine_initdt ----
-    const double sk = fma(fabs(x0), rtol, atol);
-    const double d0 = fabs(x0 / sk);
-    double k1 = f(T0, x0);
-    const double d1 = fabs(k1 / sk);
-    double dt0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * (d0 / d1);
-    dt0 = dmin(dt0, dtmax);
-    double dt;
-    if (dt0 < 10.0 * DBL_EPS) {
-        dt = dmax(1e-6, dtmin);
-    } else {
-        const double u1 = fma(dt0, k1, x0);
-        const double f1 = f(T0 + dt0, u1);
-        if (k1 == f1) {
-            dt = dmax(dtmin, 100.0 * dt0);
-        } else {
-            const double d2 = fabs((f1 - k1) / sk) / dt0;
-            const double md = dmax(d1, d2);
-            const double dt1 = (md <= 1e-15) ? dmax(1e-6, dt0 * 1e-3) : sbr_pow_pos(0.01 / md, 1.0 / 6.0);
-            dt = dmax(dtmin, dmin(dmin(100.0 * dt0, dt1), dtmax));
-        }
-    }
-    const double LOG_QOLDMIN = sbr_log(CTL_QOLDMIN);
-    const double snap = 100.0 * sbr_jl_eps(T1);
-    double t = T0, x = x0, lqold = LOG_QOLDMIN;
-    AutoSwitch as;
-    const ConstDiv by_gamma(CTL_GAMMA);
-    if (!push(t, x, false)) return; // (the last RHS call was at T0 + dt0, not T0)
-    int64_t iter = 0;
-    while (t < T1) {
-        if (++iter > maxiters) { o.status |= SBR_ODE_MAXITERS; break; }
-        dt = dmin(dtmax, dt);
-        dt = dmax(dt, dtmin);
-        dt = dmin(dt, T1 - t);
-        double tmp = fma(dt * A21, k1, x);
-        const double k2 = f(fma(C1, dt, t), tmp);
-        tmp = fma(dt, fma(A31, k1, A32 * k2), x);
-        const double k3 = f(fma(C2, dt, t), tmp);
-        tmp = fma(dt, fma(A41, k1, fma(A42, k2, A43 * k3)), x);
-        const double k4 = f(fma(C3, dt, t), tmp);
-        tmp = fma(dt, fma(A51, k1, fma(A52, k2, fma(A53, k3, A54 * k4))), x);
-        const double k5 = f(fma(C4, dt, t), tmp);
-        const double tmp6 = fma(dt, fma(A61, k1, fma(A62, k2, fma(A63, k3, fma(A64, k4, A65 * k5)))), x);
-        const double k6 = f(t + dt, tmp6);
-        const double u =
-            fma(dt, fma(A71, k1, fma(A72, k2, fma(A73, k3, fma(A74, k4, fma(A75, k5, A76 * k6))))), x);
-        const double k7 = f(t + dt, u);
-        const double eigr = fabs((k7 - k6) / (u - tmp6));
-        const double eig = (eigr != eigr) ? (double)NAN : eigr;
-        const double ut =
-            dt * fma(BT1, k1, fma(BT2, k2, fma(BT3, k3, fma(BT4, k4, fma(BT5, k5, fma(BT6, k6, BT7 * k7))))));
-        const double EEst = fabs(ut / fma(dmax(fabs(x), fabs(u)), rtol, atol));
-        double q, le = 0.0;
-        if (EEst == 0.0) {
-            q = CTL_INV_QMAX;
-        } else {
-            le = sbr_log(EEst);
-            q = sbr_exp(CTL_BETA1 * le - CTL_BETA2 * lqold);
-            q = dmax(CTL_INV_QMAX, dmin(CTL_INV_QMIN, by_gamma(q)));
-        }
-        if (EEst <= 1.0) {
-            o.naccept++;
-            const double dtnew = dt / q;
-            const double qold = dmax(EEst, CTL_QOLDMIN);
-            lqold = (qold == EEst) ? le : LOG_QOLDMIN;
-            const double tdt = t + dt;
-            double tn = tdt;
-            if (fabs(tn - T1) < snap) tn = T1;
-            t = tn;
-            x = u;
-            k1 = k7;
-            dt = dmax(dmin(dtmax, dtnew), dtmin);
-            if (!push(t, x, tn == tdt)) return;
-        } else {
-            o.nreject++;
-            const double q11 = sbr_exp(CTL_BETA1 * le);
-            dt = dt / dmin(CTL_INV_QMIN, by_gamma(q11));
-        }
-        if (!(dt > 0.0) || !isfinite(dt)) { o.status |= SBR_ODE_FAILED; break; }
-        as.update(eig, dt);
-    }
-    if (as.switched) o.status |= SBR_STIFF_SWITCH;
-}
-
-// dx/dt = βx(1 − x) (learning.jl:45-48)
-struct LogisticRhs {
-    double beta;
-    __device__ __forceinline__ double operator()(double, double x) const { return (beta * x) * (1.0 - x); }
-};
-
 // dG/dt = (1 − G) β AW_old(t) (social_learning_dynamics.jl:61-67).  All stage
 // times of a step (t + c_i·dt, t + dt) are known when the step starts, so the
 // five AW_old lookups are done up front (prepare): brackets from the register
@@ -350,111 +243,35 @@ struct SocialRhs {
         last_aw = aw[4];
     }
     // stage s = 1..6 (k2..k7): times C1..C4, then t + dt twice
-    __device__ __forceinline__ double stage(int s, double x) const
+    __device__ __forceinline__ double stage(int s, double, double x) const
     {
         return ((1.0 - x) * beta) * aw[s < 5 ? s - 1 : 4];
+    }
+    // ForwardDiff (oracle jac_social): J = ((−1)·β)·AW_old(t), ∂f/∂t = ((1 − G)·β)·AW_old'(t)
+    // with the interpolant's dual-number slope v_j·(−1/Δ) + v_{j+1}·(1/Δ) on t's bracket
+    __device__ __forceinline__ void jac(double t, double x, double& J, double& dT)
+    {
+        if (n < 2 || !(t >= tfirst && t <= tlast)) {
+            oob = true;
+            J = (double)NAN;
+            dT = (double)NAN;
+            return;
+        }
+        int j = w.find(t);
+        j = j > n - 2 ? n - 2 : (j < 0 ? 0 : j);
+        const double t0 = to[j], t1 = to[j + 1], v0 = vo[j], v1 = vo[j + 1];
+        const double d = (t - t0) / (t1 - t0);
+        const double a = v0 * (1.0 - d) + v1 * d;
+        const double rr = 1.0 / (t1 - t0);
+        const double ap = v0 * (-rr) + v1 * rr;
+        J = ((-1.0) * beta) * a;
+        dT = ((1.0 - x) * beta) * ap;
     }
     __device__ __forceinline__ void accepted(double t)
     {
         if (n >= 2 && t >= tfirst && t <= tlast) (void)w.find_advance(t);
     }
 };
-
-// Tsit5 loop for the social ODE: tsit5_scalar with the stage lookups batched
-// by SocialRhs::prepare (same arithmetic, same order of the RK operations).
-template <class Sink>
-__device__ __forceinline__ void tsit5_social(SocialRhs& f, Sink& push, double T1, double x0, double rtol,
-                                             double atol, int64_t maxiters, OdeOut& o)
-{
-    const double T0 = 0.0;
-    const double dtmax = T1 - T0;
-    const double dtmin = sbr_jl_eps(dmax(fabs(T0), fabs(T1)));
-    const double sk = fma(fabs(x0), rtol, atol);
-    const double d0 = fabs(x0 / sk);
-    double k1 = f.eval(T0, x0);
-    const double aw0 = f.last_aw;
-    const double d1 = fabs(k1 / sk);
-    double dt0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * (d0 / d1);
-    dt0 = dmin(dt0, dtmax);
-    double dt;
-    if (dt0 < 10.0 * DBL_EPS) {
-        dt = dmax(1e-6, dtmin);
-    } else {
-        const double u1 = fma(dt0, k1, x0);
-        const double f1 = f.eval(T0 + dt0, u1);
-        if (k1 == f1) {
-            dt = dmax(dtmin, 100.0 * dt0);
-        } else {
-            const double d2 = fabs((f1 - k1) / sk) / dt0;
-            const double md = dmax(d1, d2);
-            const double dt1 = (md <= 1e-15) ? dmax(1e-6, dt0 * 1e-3) : sbr_pow_pos(0.01 / md, 1.0 / 6.0);
-            dt = dmax(dtmin, dmin(dmin(100.0 * dt0, dt1), dtmax));
-        }
-    }
-    const double LOG_QOLDMIN = sbr_log(CTL_QOLDMIN);
-    const double snap = 100.0 * sbr_jl_eps(T1);
-    double t = T0, x = x0, lqold = LOG_QOLDMIN;
-    AutoSwitch as;
-    const ConstDiv by_gamma(CTL_GAMMA);
-    if (!push(t, x, aw0)) return;
-    int64_t iter = 0;
-    while (t < T1) {
-        if (++iter > maxiters) { o.status |= SBR_ODE_MAXITERS; break; }
-        dt = dmin(dtmax, dt);
-        dt = dmax(dt, dtmin);
-        dt = dmin(dt, T1 - t);
-        f.prepare(t, dt);
-        double tmp = fma(dt * A21, k1, x);
-        const double k2 = f.stage(1, tmp);
-        tmp = fma(dt, fma(A31, k1, A32 * k2), x);
-        const double k3 = f.stage(2, tmp);
-        tmp = fma(dt, fma(A41, k1, fma(A42, k2, A43 * k3)), x);
-        const double k4 = f.stage(3, tmp);
-        tmp = fma(dt, fma(A51, k1, fma(A52, k2, fma(A53, k3, A54 * k4))), x);
-        const double k5 = f.stage(4, tmp);
-        const double tmp6 = fma(dt, fma(A61, k1, fma(A62, k2, fma(A63, k3, fma(A64, k4, A65 * k5)))), x);
-        const double k6 = f.stage(5, tmp6);
-        const double u =
-            fma(dt, fma(A71, k1, fma(A72, k2, fma(A73, k3, fma(A74, k4, fma(A75, k5, A76 * k6))))), x);
-        const double k7 = f.stage(6, u);
-        const double eigr = fabs((k7 - k6) / (u - tmp6));
-        const double eig = (eigr != eigr) ? (double)NAN : eigr;
-        const double ut =
-            dt * fma(BT1, k1, fma(BT2, k2, fma(BT3, k3, fma(BT4, k4, fma(BT5, k5, fma(BT6, k6, BT7 * k7))))));
-        const double EEst = fabs(ut / fma(dmax(fabs(x), fabs(u)), rtol, atol));
-        double q, le = 0.0;
-        if (EEst == 0.0) {
-            q = CTL_INV_QMAX;
-        } else {
-            le = sbr_log(EEst);
-            q = sbr_exp(CTL_BETA1 * le - CTL_BETA2 * lqold);
-            q = dmax(CTL_INV_QMAX, dmin(CTL_INV_QMIN, by_gamma(q)));
-        }
-        if (EEst <= 1.0) {
-            o.naccept++;
-            const double dtnew = dt / q;
-            const double qold = dmax(EEst, CTL_QOLDMIN);
-            lqold = (qold == EEst) ? le : LOG_QOLDMIN;
-            const double tdt = t + dt;
-            double tn = tdt;
-            if (fabs(tn - T1) < snap) tn = T1;
-            t = tn;
-            x = u;
-            k1 = k7;
-            dt = dmax(dmin(dtmax, dtnew), dtmin);
-            // AW_old at the new knot: the t + dt stage lookup unless snapped to T1
-            if (!push(t, x, tn == tdt ? f.last_aw : f.lookup(t))) return;
-            f.accepted(t);
-        } else {
-            o.nreject++;
-            const double q11 = sbr_exp(CTL_BETA1 * le);
-            dt = dt / dmin(CTL_INV_QMIN, by_gamma(q11));
-        }
-        if (!(dt > 0.0) || !isfinite(dt)) { o.status |= SBR_ODE_FAILED; break; }
-        as.update(eig, dt);
-    }
-    if (as.switched) o.status |= SBR_STIFF_SWITCH;
-}
 
 }  // namespace
 
@@ -472,16 +289,28 @@ __global__ __launch_bounds__(64) void social_init_kernel(SocialArgs a)
     BView V = buf(a, l, 1);
     int n = 0;
     uint32_t st = 0;
-    LogisticRhs f{BETA};
-    auto push = [&](double t, double x, bool) {
-        if (n >= a.cap) { st |= SBR_KNOT_OVERFLOW; return false; }
-        T[n] = t;
-        V[n] = x;
-        n++;
-        return true;
-    };
+    LogisticSys f{BETA};
+    struct Sink {
+        BView T, V;
+        int& n;
+        int cap;
+        uint32_t& st;
+        __device__ __forceinline__ bool push(double t, double x)
+        {
+            if (n >= cap) { st |= SBR_KNOT_OVERFLOW; return false; }
+            T[n] = t;
+            V[n] = x;
+            n++;
+            return true;
+        }
+        __device__ __forceinline__ bool start(double t, double x) { return push(t, x); }
+        __device__ __forceinline__ bool accept(double, double tn, double, double, double y1, const StepK&, bool)
+        {
+            return push(tn, y1);
+        }
+    } sink{T, V, n, a.cap, st};
     OdeOut o;
-    tsit5_scalar(f, push, ETA, a.x0, a.rtol, a.atol, a.maxiters, o);
+    ode_scalar(f, sink, ETA, a.x0, a.rtol, a.atol, a.maxiters, o);
     st |= o.status & (SBR_ODE_MAXITERS | SBR_STIFF_SWITCH | SBR_ODE_FAILED);
     a.n_old[l] = n;
     a.slots[l] = 0u | (1u << 3) | (2u << 6) | (3u << 9) | (4u << 12);
@@ -552,16 +381,31 @@ __device__ __forceinline__ bool social_iterate(const SocialArgs& a, int l, int i
     f.init(BETA, TO, VO, n_old);
     int n = 0;
     bool overflow = false;
-    auto push = [&](double t, double x, double aw) {
-        if (n >= a.cap) { overflow = true; return false; }
-        T[n] = t;
-        Gv[n] = x;
-        AWO[n] = aw;
-        n++;
-        return true;
-    };
+    // knots (t, G) and AW_{n−1} at each knot: the t + dt stage lookup unless the step
+    // was snapped to T1 (the first knot: AW_{n−1}(0))
+    struct Sink {
+        SocialRhs& f;
+        BView T, Gv, AWO;
+        int& n;
+        int cap;
+        bool& overflow;
+        __device__ __forceinline__ bool push(double t, double x, double aw)
+        {
+            if (n >= cap) { overflow = true; return false; }
+            T[n] = t;
+            Gv[n] = x;
+            AWO[n] = aw;
+            n++;
+            return true;
+        }
+        __device__ __forceinline__ bool start(double t, double x) { return push(t, x, f.lookup(t)); }
+        __device__ __forceinline__ bool accept(double, double tn, double, double, double y1, const StepK&, bool exact)
+        {
+            return push(tn, y1, exact ? f.last_aw : f.lookup(tn));
+        }
+    } sink{f, T, Gv, AWO, n, a.cap, overflow};
     OdeOut o;
-    tsit5_social(f, push, ETA, a.x0, a.rtol, a.atol, a.maxiters, o);
+    ode_scalar(f, sink, ETA, a.x0, a.rtol, a.atol, a.maxiters, o);
     stamp(1);
     if (PR) { PR[6] += f.slow; PR[7] += o.naccept + o.nreject; }
     if (f.oob) o.status |= SBR_OOB;

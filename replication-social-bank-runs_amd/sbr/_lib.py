@@ -89,6 +89,8 @@ _SIGS = {
     "sbr_timing_enable": (ctypes.c_int, [_P, ctypes.c_int]),
     "sbr_timing_read": (ctypes.c_int, [_P, _P, _P, _P, _P]),
     "sbr_learn_stats": (ctypes.c_int, [_P, _I64, _P, _P, _P, _P, _P]),
+    "sbr_hetero_learn_stats": (ctypes.c_int, [_P, _I64, _P, _P, _P, _P, _P]),
+    "sbr_selftest_fastpow": (ctypes.c_int, [_P, _P, _P, ctypes.c_int, _P]),
     "sbr_device_info": (ctypes.c_int, [_P, _P, _P, _P]),
     "sbr_sweep_hetero": (ctypes.c_int, [_P, _I32, _P, _P, _P, _P, _D, _P, _I64, _I64, _D, _D, _D, _P, _P, _P, _P]),
     "sbr_sweep_hetero_dev": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P, _P, _D, _P, _I64, _I64, _D, _D, _D, _P, _P, _P,

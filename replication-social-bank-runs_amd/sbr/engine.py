@@ -39,6 +39,40 @@ def _ptr(a: np.ndarray | None):
     return None if a is None else a.ctypes.data_as(_P)
 
 
+_F64, _I32, _I64 = "float64", "int32", "int64"
+
+
+def _dptr(t, name: str, kind: str, numel: int | None = None, optional: bool = False):
+    """data_ptr() of a device tensor handed to a *_dev entry point, after the checks the
+    kernels cannot make: a contiguous CUDA tensor of the right dtype holding at least
+    ``numel`` elements.  Anything else raises ArgumentError (never a silent OOB access)."""
+    if t is None:
+        if optional:
+            return None
+        raise ArgumentError(f"{name}: a device tensor is required")
+    import torch
+    want = {_F64: (torch.float64,), _I32: (torch.int32, getattr(torch, "uint32", torch.int32)),
+            _I64: (torch.int64,)}[kind]
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise ArgumentError(f"{name}: expected a CUDA tensor")
+    if t.dtype not in want:
+        raise ArgumentError(f"{name}: expected dtype {kind}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ArgumentError(f"{name}: tensor must be contiguous")
+    if numel is not None and t.numel() < numel:
+        raise ArgumentError(f"{name}: needs at least {numel} elements, has {t.numel()}")
+    return t.data_ptr()
+
+
+def _out_ptrs(out: dict, fields, n: int, required=()):
+    """SoA result pointers from ``out`` (missing / None entries are NULL unless required)."""
+    ptrs = []
+    for k in fields:
+        kind = _I32 if k in ("status", "iters", "fp_iters") else (_I64 if k == "rk_steps" else _F64)
+        ptrs.append(_dptr(out.get(k), f"out[{k!r}]", kind, n, optional=k not in required))
+    return ptrs
+
+
 class Engine:
     """One libsbr context on one HIP device."""
 
@@ -91,12 +125,13 @@ class Engine:
         ``out`` holds preallocated tensors xi/tau_in_unc/tau_out_unc/aw_max/tol
         (float64), status (int32 viewed as uint32) and optional iters (int32)."""
         nb, nu = beta.numel(), u.numel()
-        soa = _lib.ResultSoA(*[(out[k].data_ptr() if out.get(k) is not None else None)
-                               for k in (*RESULT_FIELDS, "status", "iters")])
+        soa = _lib.ResultSoA(*_out_ptrs(out, (*RESULT_FIELDS, "status", "iters"), nb * nu,
+                                        required=(*RESULT_FIELDS, "status")))
         opts = _lib.default_opts(early_exit_nan_run=0, bisect_max_iters=max_iters, knot_capacity=knot_capacity,
                                  flags=(_lib.SBR_FLAG_EXHAUSTIVE if exhaustive else 0) | flags)
-        rc = self._L.sbr_sweep_baseline_dev(self._ctx, stream, beta.data_ptr(), eta.data_ptr(), t_end.data_ptr(),
-                                            x0, u.data_ptr(), nb, nu, p, kappa, lam, ctypes.byref(opts),
+        rc = self._L.sbr_sweep_baseline_dev(self._ctx, stream, _dptr(beta, "beta", _F64),
+                                            _dptr(eta, "eta", _F64, nb), _dptr(t_end, "t_end", _F64, nb),
+                                            x0, _dptr(u, "u", _F64), nb, nu, p, kappa, lam, ctypes.byref(opts),
                                             ctypes.byref(soa))
         check(rc, self._ctx, "sbr_sweep_baseline_dev")
 
@@ -109,12 +144,13 @@ class Engine:
         nu = u.numel()
         if tuple(eta.shape) != (nbat, nb) or tuple(t_end.shape) != (nbat, nb):
             raise ArgumentError("eta and t_end must be [n_batch, n_beta] like beta")
-        soa = _lib.ResultSoA(*[(out[k].data_ptr() if out.get(k) is not None else None)
-                               for k in (*RESULT_FIELDS, "status", "iters")])
+        soa = _lib.ResultSoA(*_out_ptrs(out, (*RESULT_FIELDS, "status", "iters"), nbat * nb * nu,
+                                        required=(*RESULT_FIELDS, "status")))
         opts = _lib.default_opts(early_exit_nan_run=0, bisect_max_iters=max_iters, knot_capacity=knot_capacity,
                                  flags=flags)
-        rc = self._L.sbr_sweep_baseline_batch_dev(self._ctx, stream, nbat, beta.data_ptr(), eta.data_ptr(),
-                                                  t_end.data_ptr(), x0, u.data_ptr(), nb, nu, p, kappa, lam,
+        rc = self._L.sbr_sweep_baseline_batch_dev(self._ctx, stream, nbat, _dptr(beta, "beta", _F64),
+                                                  _dptr(eta, "eta", _F64), _dptr(t_end, "t_end", _F64), x0,
+                                                  _dptr(u, "u", _F64), nb, nu, p, kappa, lam,
                                                   ctypes.byref(opts), ctypes.byref(soa))
         check(rc, self._ctx, "sbr_sweep_baseline_batch_dev")
 
@@ -182,13 +218,14 @@ class Engine:
                          stream: int | None = None, knot_capacity: int = 16384, flags: int = 0):
         """Device-pointer hetero sweep on torch tensors (no host sync)."""
         n_col, nu = eta.numel(), u.numel()
-        soa = _lib.ResultSoA(out["xi"].data_ptr(), None, None, out["aw_max"].data_ptr(), out["tol"].data_ptr(),
-                             out["status"].data_ptr(), out["iters"].data_ptr() if out.get("iters") is not None
-                             else None)
+        xi, aw, tl, st, it = _out_ptrs(out, ("xi", "aw_max", "tol", "status", "iters"), n_col * nu,
+                                       required=("xi", "aw_max", "tol", "status"))
+        soa = _lib.ResultSoA(xi, None, None, aw, tl, st, it)
         opts = _lib.default_opts(knot_capacity=knot_capacity, flags=flags)
-        rc = self._L.sbr_sweep_hetero_dev(self._ctx, stream, K, betas.data_ptr(), dist.data_ptr(), eta.data_ptr(),
-                                          t_end.data_ptr(), x0, u.data_ptr(), n_col, nu, p, kappa, lam,
-                                          ctypes.byref(opts), ctypes.byref(soa), None, None)
+        rc = self._L.sbr_sweep_hetero_dev(self._ctx, stream, K, _dptr(betas, "betas", _F64, n_col * K),
+                                          _dptr(dist, "dist", _F64, K), _dptr(eta, "eta", _F64),
+                                          _dptr(t_end, "t_end", _F64, n_col), x0, _dptr(u, "u", _F64), n_col, nu, p,
+                                          kappa, lam, ctypes.byref(opts), ctypes.byref(soa), None, None)
         check(rc, self._ctx, "sbr_sweep_hetero_dev")
 
     def sweep_hetero_batch_dev(self, K, betas, dist, eta, t_end, u, p, kappa, lam, x0, out: dict,
@@ -200,12 +237,13 @@ class Engine:
         nu = u.numel()
         if tuple(betas.shape) != (nbat, n_col, K) or tuple(t_end.shape) != (nbat, n_col):
             raise ArgumentError("betas must be [n_batch, n_col, K] and t_end [n_batch, n_col]")
-        soa = _lib.ResultSoA(out["xi"].data_ptr(), None, None, out["aw_max"].data_ptr(), out["tol"].data_ptr(),
-                             out["status"].data_ptr(), out["iters"].data_ptr() if out.get("iters") is not None
-                             else None)
+        xi, aw, tl, st, it = _out_ptrs(out, ("xi", "aw_max", "tol", "status", "iters"), nbat * n_col * nu,
+                                       required=("xi", "aw_max", "tol", "status"))
+        soa = _lib.ResultSoA(xi, None, None, aw, tl, st, it)
         opts = _lib.default_opts(knot_capacity=knot_capacity, flags=flags)
-        rc = self._L.sbr_sweep_hetero_batch_dev(self._ctx, stream, nbat, K, betas.data_ptr(), dist.data_ptr(),
-                                                eta.data_ptr(), t_end.data_ptr(), x0, u.data_ptr(), n_col, nu, p,
+        rc = self._L.sbr_sweep_hetero_batch_dev(self._ctx, stream, nbat, K, _dptr(betas, "betas", _F64),
+                                                _dptr(dist, "dist", _F64, K), _dptr(eta, "eta", _F64),
+                                                _dptr(t_end, "t_end", _F64), x0, _dptr(u, "u", _F64), n_col, nu, p,
                                                 kappa, lam, ctypes.byref(opts), ctypes.byref(soa), None, None)
         check(rc, self._ctx, "sbr_sweep_hetero_batch_dev")
 
@@ -244,16 +282,15 @@ class Engine:
                          stream: int | None = None, knot_capacity: int = 0, flags: int = 0):
         """Device-pointer social sweep on torch tensors (enqueue only)."""
         nb, nu = beta.numel(), u.numel()
-        soa = _lib.ResultSoA(*[out[k].data_ptr() if out.get(k) is not None else None
-                               for k in ("xi", "tau_in_unc", "tau_out_unc", "aw_max", "tol", "status", "iters")])
+        soa = _lib.ResultSoA(*_out_ptrs(out, (*RESULT_FIELDS, "status", "iters"), nb * nu,
+                                        required=(*RESULT_FIELDS, "status")))
         opts = _lib.default_opts(pad=knot_capacity, flags=flags)
-        fp = out.get("fp_iters")
-        rk = out.get("rk_steps")
-        rc = self._L.sbr_sweep_social_dev(self._ctx, stream, beta.data_ptr(), eta.data_ptr(), x0, u.data_ptr(), nb, nu,
-                                          p, kappa, lam, cmp.data_ptr(), cmp.shape[-1], tol, max_iter,
-                                          ctypes.byref(opts), ctypes.byref(soa),
-                                          fp.data_ptr() if fp is not None else None,
-                                          rk.data_ptr() if rk is not None else None)
+        fp, rk = _out_ptrs(out, ("fp_iters", "rk_steps"), nb * nu)
+        n_cmp = cmp.shape[-1]
+        rc = self._L.sbr_sweep_social_dev(self._ctx, stream, _dptr(beta, "beta", _F64), _dptr(eta, "eta", _F64, nb),
+                                          x0, _dptr(u, "u", _F64), nb, nu, p, kappa, lam,
+                                          _dptr(cmp, "cmp", _F64, nb * n_cmp), n_cmp, tol, max_iter,
+                                          ctypes.byref(opts), ctypes.byref(soa), fp, rk)
         check(rc, self._ctx, "sbr_sweep_social_dev")
 
     def sweep_interest(self, beta, eta, t_end, u, p, kappa, lam, r, delta, x0=1e-4, max_iters: int = 100,
@@ -340,13 +377,13 @@ class Engine:
                            stream: int | None = None, max_iters: int = 100, knot_capacity: int = 65536):
         """Device-pointer interest sweep on torch tensors (enqueue only)."""
         nb, nu = beta.numel(), u.numel()
-        soa = _lib.ResultSoA(*[(out[k].data_ptr() if out.get(k) is not None else None)
-                               for k in (*RESULT_FIELDS, "status", "iters")])
+        soa = _lib.ResultSoA(*_out_ptrs(out, (*RESULT_FIELDS, "status", "iters"), nb * nu,
+                                        required=(*RESULT_FIELDS, "status")))
         opts = _lib.default_opts(early_exit_nan_run=0, bisect_max_iters=max_iters, knot_capacity=knot_capacity)
-        rk = out.get("rk_steps")
-        rc = self._L.sbr_sweep_interest_dev(self._ctx, stream, beta.data_ptr(), eta.data_ptr(), t_end.data_ptr(), x0,
-                                            u.data_ptr(), nb, nu, p, kappa, lam, r, delta, ctypes.byref(opts),
-                                            ctypes.byref(soa), rk.data_ptr() if rk is not None else None)
+        (rk,) = _out_ptrs(out, ("rk_steps",), nb * nu)
+        rc = self._L.sbr_sweep_interest_dev(self._ctx, stream, _dptr(beta, "beta", _F64), _dptr(eta, "eta", _F64, nb),
+                                            _dptr(t_end, "t_end", _F64, nb), x0, _dptr(u, "u", _F64), nb, nu, p,
+                                            kappa, lam, r, delta, ctypes.byref(opts), ctypes.byref(soa), rk)
         check(rc, self._ctx, "sbr_sweep_interest_dev")
 
     def social_prof_read(self) -> list[int]:
@@ -383,6 +420,23 @@ class Engine:
         check(self._L.sbr_learn_stats(self._ctx, n_beta, *[_ptr(out[k]) for k in
                                                          ("n_knots", "n_tau", "n_accept", "n_reject", "status")]),
               self._ctx, "sbr_learn_stats")
+        return out
+
+    def hetero_learn_stats(self, n_col: int) -> dict:
+        out = {k: np.zeros(n_col, np.int32) for k in ("n_knots", "n_tau", "n_accept", "n_reject")}
+        out["status"] = np.zeros(n_col, np.uint32)
+        check(self._L.sbr_hetero_learn_stats(self._ctx, n_col, *[_ptr(out[k]) for k in
+                                                                ("n_knots", "n_tau", "n_accept", "n_reject",
+                                                                 "status")]),
+              self._ctx, "sbr_hetero_learn_stats")
+        return out
+
+    def selftest_fastpow(self, x, y):
+        x = np.ascontiguousarray(x, np.float64)
+        y = np.ascontiguousarray(y, np.float64)
+        out = np.empty(len(x))
+        check(self._L.sbr_selftest_fastpow(self._ctx, _ptr(x), _ptr(y), len(x), _ptr(out)), self._ctx,
+              "sbr_selftest_fastpow")
         return out
 
     def selftest_detmath(self, x, y):

@@ -62,11 +62,13 @@ def test_social_no_run_and_oob_paths(engine, oracle):
     assert np.all(g["status"] & sbr.STATUS["SBR_NO_RUN_HR_BELOW_U"])
     beta = 1.0 / sbr.julia_range("0.01", "2", 512)
     u = sbr.julia_range("0.001", "1", 512)
-    for b, uu in ((beta[20], u[3]), (beta[0], u[2])):
+    # (found by scanning the oracle over small u: tools/social_oob_scan.py)
+    for b, uu, failed in ((beta[40], u[6], False), (beta[0], u[2], True)):
         g, o = _both(engine, oracle, [b], [uu])
         _compare(g, o)
         assert g["status"][0, 0] & sbr.STATUS["SBR_OOB"]
         assert g["status"][0, 0] & sbr.STATUS["SBR_SOCIAL_NOT_CONVERGED"]
+        assert bool(g["status"][0, 0] & sbr.STATUS["SBR_ODE_FAILED"]) == failed
 
 
 def test_social_config5_subgrid_capped(engine, oracle):
@@ -127,7 +129,7 @@ def test_social_point_paths_bitwise(engine, oracle):
     beta = 1.0 / sbr.julia_range("0.01", "2", 512)
     u = sbr.julia_range("0.001", "1", 512)
     cmp = sbr.julia_range(0.0, ETA, 1000)
-    for b, uu in ((0.9, 0.5), (beta[20], u[3])):
+    for b, uu in ((0.9, 0.5), (beta[40], u[6])):
         g = engine.social_point_paths(b, ETA, uu, P, KAPPA, LAM, cmp=cmp)
         o = oracle.social_point(b, ETA, uu, P, KAPPA, LAM, cmp)
         assert g["status"] == o["status"] and g["fp_iters"] == o["fp_iters"], (b, uu)

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Aggregate rocprofv3 --pmc passes (tools/pmc.sh) into a per-kernel table.
 
-Usage: python tools/pmc_summary.py gpurun_out/pmc profiles/r01_v3_pmc.txt [profiles/traffic_latest.json [workload]]
+Usage: python tools/pmc_summary.py gpurun_out/pmc profiles/r01_v3_pmc.txt [profiles/traffic_latest.json [workload
+       [profiles/pmc_latest.json]]]
 
 Every counter is averaged per dispatch of a kernel (summed over the device).
 The optional JSON holds HBM traffic per launch of the equilibrium kernel for
@@ -71,6 +72,17 @@ def main():
                 t["hbm_bytes_per_launch"] = t["read_bytes"] + t["write_bytes"]
                 with open(out_json, "w") as f:
                     json.dump(t, f, indent=1)
+    # per-kernel counter averages + the libsbr.so they were collected on (bench.py's
+    # roofline.frac_executed uses them only for that exact binary)
+    if len(sys.argv) > 5:
+        import hashlib
+        lib = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "replication-social-bank-runs_amd", "lib",
+                           "libsbr.so")
+        sha = hashlib.sha256(open(lib, "rb").read()).hexdigest()[:16]
+        pm = {"workload": sys.argv[4], "source": out_txt, "libsbr_sha16": sha,
+              "kernels": {short(k): per[k] for k in kernels}}
+        with open(sys.argv[5], "w") as f:
+            json.dump(pm, f, indent=1)
 
 
 if __name__ == "__main__":
