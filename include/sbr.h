@@ -86,6 +86,26 @@ int sbr_free(sbr_ctx* ctx);
 const char* sbr_last_error(const sbr_ctx* ctx);
 
 /*
+ * n-device context (SURVEY.md §8(b) `sbr_init(n_gpus, …)`, §8(e)): n_gpus HIP devices
+ * (`devices` lists their ids, NULL = 0 .. n_gpus-1), one single-device context per
+ * device, an RCCL communicator over them (librccl.so.1, loaded at run time).  The
+ * host-pointer sweeps — sbr_sweep_baseline, sbr_sweep_hetero, sbr_sweep_social,
+ * sbr_sweep_interest — on such a context deal the parameter columns cyclically
+ * (column i to device i mod n_gpus), solve every shard on its GPU from one host thread
+ * per GPU, gather the result arrays to device 0 over RCCL (xGMI) and return them in
+ * the single-device layout: bit-identical to a one-GPU sweep (per-point results do not
+ * depend on the partitioning).  Single-point, learning-only and diagnostic calls run on
+ * device 0; the device-pointer (*_dev) entry points need a single-device context:
+ * sbr_multi_child(ctx, rank).  A call is synchronous; contexts are independent, so
+ * distinct contexts may be used from distinct threads.
+ */
+int sbr_init_multi(int n_gpus, const int* devices, sbr_ctx** ctx);
+/* number of devices of a context (1 for sbr_init's) */
+int sbr_multi_size(const sbr_ctx* ctx);
+/* the single-device context of rank `rank` (rank 0 of a single-device context is itself) */
+sbr_ctx* sbr_multi_child(sbr_ctx* ctx, int rank);
+
+/*
  * Baseline β×u sweep — replaces the Fig 4/Fig 5 loops of
  * scripts/1_baseline.jl:151-192 and :224-267, i.e. for each β
  *     lr = solve_learning(LearningParameters(β, (0, t_end[i]), x0))   learning.jl:109

@@ -179,14 +179,15 @@ SBR_HD float sbr_fastlog2f(float x)
     return fexp + (signif * (a * signif + b)) / (signif + c);
 }
 
-/* Base.Math.exp_impl_fast(x::Float32, Val(2)) (MAX_EXP = 128, SUBNORM_EXP = 150) */
+/* Base.Math.exp_impl_fast(x::Float32, Val(2)) (MAX_EXP = 128, SUBNORM_EXP = 150).
+ * Branch-free: the kernel runs on a clamped argument and the out-of-range / NaN
+ * results are selected at the end (NaN in -> NaN out, as Julia's NaN * 2^N). */
 SBR_HD float sbr_exp2f_jl(float x)
 {
-    const float inf = sbr_bitsf(0x7f800000u);
-    if (x >= 128.0f) return inf;
-    if (x <= -150.0f) return 0.0f;
-    const float nf = __builtin_rintf(x); /* round(x), ties to even */
-    const float r0 = __builtin_fmaf(nf, -1.0f, x);
+    const int over = x >= 128.0f, under = x <= -150.0f, nan_ = x != x;
+    const float xs = (over | under | nan_) ? 0.0f : x;
+    const float nf = __builtin_rintf(xs); /* round(x), ties to even */
+    const float r0 = __builtin_fmaf(nf, -1.0f, xs);
     const float r = __builtin_fmaf(nf, 0.0f, r0);
     float p = 1.5316464e-5f; /* expb_kernel(Val(2), ::Float32): evalpoly = Horner in muladd */
     p = __builtin_fmaf(r, p, 0.00015469732f);
@@ -198,7 +199,8 @@ SBR_HD float sbr_exp2f_jl(float x)
     p = __builtin_fmaf(r, p, 1.0f);
     const int32_t n = (int32_t)nf;
     const float twopk = sbr_bitsf((uint32_t)(n + 127) << 23);
-    return twopk * p;
+    const float res = twopk * p;
+    return over ? sbr_bitsf(0x7f800000u) : (under ? 0.0f : (nan_ ? x : res));
 }
 
 /* FastPower.fastpower(x, y) for Float64 x, y */

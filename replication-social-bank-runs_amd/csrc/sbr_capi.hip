@@ -15,6 +15,7 @@
 #include "../../include/sbr.h"
 #include "../../include/sbr_detmath.h"
 #include "sbr_kernels.h"
+#include "sbr_multi.h"
 
 // Event flags. Timing events only time (no system-scope cache writeback/invalidate when they
 // complete); dependency events between this device's queues release to device scope.
@@ -34,6 +35,9 @@
 
 struct sbr_ctx {
     int device = 0;
+    // n-device context (sbr_init_multi): the per-device contexts, RCCL communicator and
+    // rank buffers live in `multi`; the host-pointer sweeps fan out over them
+    sbr_multi* multi = nullptr;
     hipStream_t stream = nullptr;
     std::string err;
     // learning workspaces: slot 0 for single sweeps; a pipelined batch rotates through
@@ -428,7 +432,42 @@ int run_interest(sbr_ctx* c, hipStream_t s, const double* beta, const double* et
 // value_function_solver.jl:67-69)
 bool interest_valid(double r, double delta) { return r >= 0.0 && delta > 0.0 && r < delta; }
 
+int multi_sweep_social(sbr_ctx* c, const double* beta, const double* eta, double x0, const double* u, int64_t n_beta,
+                       int64_t n_u, double p, double kappa, double lambda, const double* cmp_grid, int32_t n_cmp,
+                       double tol, int32_t max_iter, const sbr_opts& o, sbr_result_soa* out, int32_t* fp_iters,
+                       int64_t* rk_steps);
+int multi_sweep_hetero(sbr_ctx* c, int32_t K, const double* betas, const double* dist, const double* eta,
+                       const double* t_end, double x0, const double* u, int64_t n_col, int64_t n_u, double p,
+                       double kappa, double lambda, const sbr_opts& o, sbr_result_soa* out, double* tau_in,
+                       double* tau_out);
+int multi_sweep_interest(sbr_ctx* c, const double* beta, const double* eta, const double* t_end, double x0,
+                         const double* u, int64_t n_beta, int64_t n_u, double p, double kappa, double lambda, double r_,
+                         double delta, const sbr_opts& o, sbr_result_soa* out, int64_t* rk_steps);
+int multi_sweep_baseline(sbr_ctx* c, const double* beta, const double* eta, const double* t_end, double x0,
+                         const double* u, int64_t n_beta, int64_t n_u, double p, double kappa, double lambda,
+                         const sbr_opts& o, sbr_result_soa* out);
+
 }  // namespace
+
+// device-pointer entry points address one GPU's HBM: they need a single-device context
+#define SBR_SINGLE_DEVICE(c)                                                                                \
+    do {                                                                                                    \
+        if ((c) && (c)->multi)                                                                              \
+            return fail((c), SBR_EARG, "device-pointer entry points need a single-device context "          \
+                                       "(sbr_multi_child)");                                                \
+    } while (0)
+// single-point / diagnostic entry points on an n-device context run on its rank 0
+#define SBR_ON_RANK0(c, call)                                                                               \
+    do {                                                                                                    \
+        if ((c) && (c)->multi) {                                                                            \
+            sbr_ctx* const c0_ = sbr_multi_child((c), 0);                                                   \
+            sbr_ctx* const parent_ = (c);                                                                   \
+            sbr_ctx* c = c0_;                                                                               \
+            const int rc_ = (call);                                                                         \
+            parent_->err = rc_ ? std::string(sbr_last_error(c0_)) : std::string();                          \
+            return rc_;                                                                                     \
+        }                                                                                                   \
+    } while (0)
 
 extern "C" {
 
@@ -473,9 +512,41 @@ int sbr_init(int device, sbr_ctx** out)
     return SBR_OK;
 }
 
+int sbr_init_multi(int n_gpus, const int* devices, sbr_ctx** out)
+{
+    if (!out) return SBR_EARG;
+    *out = nullptr;
+    if (n_gpus <= 0) return SBR_EARG;
+    sbr_ctx* c = new sbr_ctx();
+    std::vector<sbr_ctx*> kids;
+    std::string err;
+    const int rc = sbr_multi_impl::create(n_gpus, devices, &c->multi, kids, err);
+    if (rc != SBR_OK) {
+        delete c;
+        return rc;
+    }
+    c->device = kids[0]->device;
+    *out = c;
+    return SBR_OK;
+}
+
+int sbr_multi_size(const sbr_ctx* c) { return c ? sbr_multi_impl::size(c->multi) : 0; }
+
+sbr_ctx* sbr_multi_child(sbr_ctx* c, int rank)
+{
+    if (!c) return nullptr;
+    if (!c->multi) return rank == 0 ? c : nullptr;
+    return sbr_multi_impl::child(c->multi, rank);
+}
+
 int sbr_free(sbr_ctx* c)
 {
     if (!c) return SBR_OK;
+    if (c->multi) {
+        sbr_multi_impl::destroy(c->multi);
+        delete c;
+        return SBR_OK;
+    }
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     for (hipStream_t ls : c->lstream)
@@ -504,12 +575,18 @@ int sbr_free(sbr_ctx* c)
     return SBR_OK;
 }
 
-const char* sbr_last_error(const sbr_ctx* c) { return c ? c->err.c_str() : "null context"; }
+const char* sbr_last_error(const sbr_ctx* c)
+{
+    if (!c) return "null context";
+    if (c->multi && c->err.empty()) return sbr_multi_impl::last_error(c->multi);
+    return c->err.c_str();
+}
 
 int sbr_sweep_baseline_dev(sbr_ctx* c, void* stream, const double* beta, const double* eta, const double* t_end,
                            double x0, const double* u, int64_t n_beta, int64_t n_u, double p, double kappa,
                            double lambda, const sbr_opts* opts, sbr_result_soa* out)
 {
+    SBR_SINGLE_DEVICE(c);
     if (!c || !out || !out->xi || !out->tau_in_unc || !out->tau_out_unc || !out->aw_max || !out->tol || !out->status)
         return SBR_EARG;
     if (n_beta <= 0 || n_u <= 0 || n_beta > (1 << 30) || n_u > (1 << 30)) return fail(c, SBR_EARG, "grid size");
@@ -548,6 +625,7 @@ int sbr_sweep_baseline_batch_dev(sbr_ctx* c, void* stream, int64_t n_batch, cons
                                  const double* t_end, double x0, const double* u, int64_t n_beta, int64_t n_u,
                                  double p, double kappa, double lambda, const sbr_opts* opts, sbr_result_soa* out)
 {
+    SBR_SINGLE_DEVICE(c);
     if (!c || !out || !beta || !eta || !t_end || !u) return SBR_EARG;
     if (!out->xi || !out->tau_in_unc || !out->tau_out_unc || !out->aw_max || !out->tol || !out->status) return SBR_EARG;
     if (n_batch <= 0 || n_beta <= 0 || n_u <= 0 || n_beta > (1 << 30) || n_u > (1 << 30))
@@ -612,6 +690,7 @@ int sbr_sweep_baseline(sbr_ctx* c, const double* beta, const double* eta, const 
             return fail(c, SBR_EARG, "ArgumentError: beta/eta/t_end must be positive");
     for (int64_t j = 0; j < n_u; j++)
         if (!(u[j] >= 0.0)) return fail(c, SBR_EARG, "ArgumentError: u must be non-negative");
+    if (c->multi) return multi_sweep_baseline(c, beta, eta, t_end, x0, u, n_beta, n_u, p, kappa, lambda, resolve(opts), out);
     if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
     sbr_opts o = resolve(opts);
     const size_t np = (size_t)n_beta * (size_t)n_u;
@@ -651,6 +730,7 @@ int sbr_sweep_interest_dev(sbr_ctx* c, void* stream, const double* beta, const d
                            double lambda, double r, double delta, const sbr_opts* opts, sbr_result_soa* out,
                            int64_t* rk_steps)
 {
+    SBR_SINGLE_DEVICE(c);
     if (!c || !out || !out->xi || !out->tau_in_unc || !out->tau_out_unc || !out->aw_max || !out->tol || !out->status)
         return SBR_EARG;
     if (n_beta <= 0 || n_u <= 0 || n_beta > (1 << 30) || n_u > (1 << 30)) return fail(c, SBR_EARG, "grid size");
@@ -677,6 +757,9 @@ int sbr_sweep_interest(sbr_ctx* c, const double* beta, const double* eta, const 
             return fail(c, SBR_EARG, "ArgumentError: beta/eta/t_end must be positive");
     for (int64_t j = 0; j < n_u; j++)
         if (!(u[j] >= 0.0)) return fail(c, SBR_EARG, "ArgumentError: u must be non-negative");
+    if (c->multi)
+        return multi_sweep_interest(c, beta, eta, t_end, x0, u, n_beta, n_u, p, kappa, lambda, r, delta, resolve(opts),
+                                    out, rk_steps);
     if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
     sbr_opts o = resolve(opts);
     const size_t np = (size_t)n_beta * (size_t)n_u;
@@ -716,6 +799,7 @@ int sbr_interest_point_paths(sbr_ctx* c, double beta, double eta, double t_end, 
                              uint32_t* status, double* tau, double* hr, double* V, double* aw_cum, int64_t cap,
                              int64_t* n_tau, int64_t* n_v)
 {
+    SBR_ON_RANK0(c, sbr_interest_point_paths(c, beta, eta, t_end, x0, u, p, kappa, lambda, r, delta, opts, res, status, tau, hr, V, aw_cum, cap, n_tau, n_v));
     if (!c || !res || !status) return SBR_EARG;
     if (!scalars_valid(x0, p, kappa, lambda) || !(beta > 0) || !(eta > 0) || !(t_end > 0) || !(u >= 0))
         return fail(c, SBR_EARG, "ArgumentError");
@@ -768,6 +852,7 @@ int sbr_learn_baseline(sbr_ctx* c, const double* beta, const double* eta, const 
                        int64_t n_beta, int32_t stop_after_eta, const sbr_opts* opts, double* t_out, double* G_out,
                        int64_t cap, int32_t* n_knots, uint32_t* status)
 {
+    SBR_ON_RANK0(c, sbr_learn_baseline(c, beta, eta, t_end, x0, n_beta, stop_after_eta, opts, t_out, G_out, cap, n_knots, status));
     if (!c || !beta || !eta || !t_end || n_beta <= 0 || cap <= 0) return SBR_EARG;
     if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
     sbr_opts o = resolve(opts);
@@ -801,6 +886,7 @@ int sbr_solve_point_paths(sbr_ctx* c, double beta, double eta, double t_end, dou
                           double kappa, double lambda, const sbr_opts* opts, double* res, uint32_t* status,
                           double* tau, double* hr, double* aw_cum, int64_t cap, int64_t* n_tau)
 {
+    SBR_ON_RANK0(c, sbr_solve_point_paths(c, beta, eta, t_end, x0, u, p, kappa, lambda, opts, res, status, tau, hr, aw_cum, cap, n_tau));
     if (!c || !res || !status) return SBR_EARG;
     if (!scalars_valid(x0, p, kappa, lambda) || !(beta > 0) || !(eta > 0) || !(t_end > 0) || !(u >= 0))
         return fail(c, SBR_EARG, "ArgumentError");
@@ -844,6 +930,7 @@ int sbr_solve_point_paths(sbr_ctx* c, double beta, double eta, double t_end, dou
 
 int sbr_timing_enable(sbr_ctx* c, int on)
 {
+    SBR_ON_RANK0(c, sbr_timing_enable(c, on));
     if (!c) return SBR_EARG;
     c->timing = on != 0;
     c->ev_used = 0;
@@ -853,6 +940,7 @@ int sbr_timing_enable(sbr_ctx* c, int on)
 
 int sbr_timing_read(sbr_ctx* c, void* stream, double* learn_ms, double* eq_ms, int32_t* n_calls)
 {
+    SBR_ON_RANK0(c, sbr_timing_read(c, stream, learn_ms, eq_ms, n_calls));
     if (!c) return SBR_EARG;
     hipStream_t s = (hipStream_t)stream; // NULL = HIP null stream
     HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
@@ -878,6 +966,7 @@ int sbr_timing_read(sbr_ctx* c, void* stream, double* learn_ms, double* eq_ms, i
 int sbr_learn_stats(sbr_ctx* c, int64_t n_beta, int32_t* n_knots, int32_t* n_tau, int32_t* n_accept,
                     int32_t* n_reject, uint32_t* status)
 {
+    SBR_ON_RANK0(c, sbr_learn_stats(c, n_beta, n_knots, n_tau, n_accept, n_reject, status));
     if (!c || n_beta <= 0 || (size_t)n_beta > c->ws_beta[c->last_slot]) return SBR_EARG;
     if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
     HIP_TRY(c, hipDeviceSynchronize(), SBR_EDEVICE);
@@ -892,6 +981,7 @@ int sbr_learn_stats(sbr_ctx* c, int64_t n_beta, int32_t* n_knots, int32_t* n_tau
 int sbr_hetero_learn_stats(sbr_ctx* c, int64_t n_col, int32_t* n_knots, int32_t* n_tau, int32_t* n_accept,
                            int32_t* n_reject, uint32_t* status)
 {
+    SBR_ON_RANK0(c, sbr_hetero_learn_stats(c, n_col, n_knots, n_tau, n_accept, n_reject, status));
     if (!c || n_col <= 0 || (size_t)n_col > c->hs_col) return SBR_EARG;
     if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
     HIP_TRY(c, hipDeviceSynchronize(), SBR_EDEVICE);
@@ -908,6 +998,7 @@ int sbr_sweep_hetero_dev(sbr_ctx* c, void* stream, int32_t K, const double* beta
                          int64_t n_u, double p, double kappa, double lambda, const sbr_opts* opts,
                          sbr_result_soa* out, double* tau_in, double* tau_out)
 {
+    SBR_SINGLE_DEVICE(c);
     if (!c || !out || !out->xi || !out->aw_max || !out->tol || !out->status) return SBR_EARG;
     if (K != 1 && K != 2 && K != 3 && K != 4 && K != 8) return fail(c, SBR_EARG, "K must be 1, 2, 3, 4 or 8");
     if (n_col <= 0 || n_u <= 0 || n_col > (1 << 30) || n_u > (1 << 30)) return fail(c, SBR_EARG, "grid size");
@@ -936,6 +1027,7 @@ int sbr_sweep_hetero_batch_dev(sbr_ctx* c, void* stream, int64_t n_batch, int32_
                                int64_t n_col, int64_t n_u, double p, double kappa, double lambda, const sbr_opts* opts,
                                sbr_result_soa* out, double* tau_in, double* tau_out)
 {
+    SBR_SINGLE_DEVICE(c);
     if (!c || !out || !out->xi || !out->aw_max || !out->tol || !out->status || !betas || !dist || !eta || !t_end || !u)
         return SBR_EARG;
     if (K != 1 && K != 2 && K != 3 && K != 4 && K != 8) return fail(c, SBR_EARG, "K must be 1, 2, 3, 4 or 8");
@@ -988,6 +1080,7 @@ int sbr_hetero_point_paths(sbr_ctx* c, int32_t K, const double* betas, const dou
                            double* res, uint32_t* status, double* tau_in, double* tau_out, double* t, double* G,
                            double* aw_total, int64_t cap, int64_t* n_knots)
 {
+    SBR_ON_RANK0(c, sbr_hetero_point_paths(c, K, betas, dist, eta, t_end, x0, u, p, kappa, lambda, opts, res, status, tau_in, tau_out, t, G, aw_total, cap, n_knots));
     if (!c || !res || !status || !betas || !dist) return SBR_EARG;
     if (K != 1 && K != 2 && K != 3 && K != 4 && K != 8) return fail(c, SBR_EARG, "K must be 1, 2, 3, 4 or 8");
     double dsum = 0.0;
@@ -1060,6 +1153,11 @@ int sbr_sweep_hetero(sbr_ctx* c, int32_t K, const double* betas, const double* d
         if (!(eta[i] > 0.0) || !(t_end[i] > 0.0)) return fail(c, SBR_EARG, "ArgumentError: eta/t_end");
     for (int64_t j = 0; j < n_u; j++)
         if (!(u[j] >= 0.0)) return fail(c, SBR_EARG, "ArgumentError: u must be non-negative");
+    if (c->multi) {
+        if (K != 1 && K != 2 && K != 3 && K != 4 && K != 8) return fail(c, SBR_EARG, "K must be 1, 2, 3, 4 or 8");
+        return multi_sweep_hetero(c, K, betas, dist, eta, t_end, x0, u, n_col, n_u, p, kappa, lambda, resolve(opts),
+                                  out, tau_in, tau_out);
+    }
     if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
     const size_t np = (size_t)n_col * (size_t)n_u;
     const size_t in_d = (size_t)n_col * K + K + 2 * (size_t)n_col + (size_t)n_u;
@@ -1099,6 +1197,7 @@ int sbr_sweep_hetero(sbr_ctx* c, int32_t K, const double* betas, const double* d
 
 int sbr_social_prof_read(sbr_ctx* c, int64_t* out8)
 {
+    SBR_ON_RANK0(c, sbr_social_prof_read(c, out8));
     if (!c || !out8) return SBR_EARG;
     for (int k = 0; k < 8; k++) out8[k] = k < (int)c->so_prof_acc.size() ? c->so_prof_acc[k] : 0;
     return SBR_OK;
@@ -1106,6 +1205,7 @@ int sbr_social_prof_read(sbr_ctx* c, int64_t* out8)
 
 int sbr_social_overflow_stats(sbr_ctx* c, int64_t* promoted, int64_t* rerun)
 {
+    SBR_ON_RANK0(c, sbr_social_overflow_stats(c, promoted, rerun));
     if (!c) return SBR_EARG;
     if (promoted) *promoted = c->so_promoted;
     if (rerun) *rerun = c->so_rerun;
@@ -1115,6 +1215,7 @@ int sbr_social_overflow_stats(sbr_ctx* c, int64_t* promoted, int64_t* rerun)
 int sbr_set_social_workspace(sbr_ctx* c, int64_t bytes)
 {
     if (!c || bytes < 0) return SBR_EARG;
+    for (int r = 0; c->multi && r < sbr_multi_size(c); r++) (void)sbr_set_social_workspace(sbr_multi_child(c, r), bytes);
     c->so_budget = bytes;
     return SBR_OK;
 }
@@ -1322,6 +1423,7 @@ int sbr_sweep_social_dev(sbr_ctx* c, void* stream, const double* beta, const dou
                          int32_t n_cmp, double tol, int32_t max_iter, const sbr_opts* opts, sbr_result_soa* out,
                          int32_t* fp_iters, int64_t* rk_steps)
 {
+    SBR_SINGLE_DEVICE(c);
     int rc = social_checks(c, beta, eta, u, n_beta, n_u, x0, p, kappa, lambda, cmp_grid, n_cmp, tol, max_iter, out);
     if (rc) return rc;
     if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
@@ -1337,6 +1439,7 @@ int sbr_social_point_paths(sbr_ctx* c, double beta, double eta, double x0, doubl
                            const sbr_opts* opts, double* res, uint32_t* status, int32_t* fp_iters, double* t,
                            double* G, int64_t cap, int64_t* n_knots)
 {
+    SBR_ON_RANK0(c, sbr_social_point_paths(c, beta, eta, x0, u, p, kappa, lambda, cmp_grid, n_cmp, tol, max_iter, opts, res, status, fp_iters, t, G, cap, n_knots));
     if (!c || !res || !status || !t || !G || cap <= 0 || cap > (int64_t(1) << 30)) return SBR_EARG;
     double* d = nullptr;
     const size_t kc = (size_t)cap;
@@ -1382,6 +1485,9 @@ int sbr_sweep_social(sbr_ctx* c, const double* beta, const double* eta, double x
         if (!(beta[i] > 0.0) || !(eta[i] > 0.0)) return fail(c, SBR_EARG, "ArgumentError: beta/eta must be positive");
     for (int64_t j = 0; j < n_u; j++)
         if (!(u[j] >= 0.0)) return fail(c, SBR_EARG, "ArgumentError: u must be non-negative");
+    if (c->multi)
+        return multi_sweep_social(c, beta, eta, x0, u, n_beta, n_u, p, kappa, lambda, cmp_grid, n_cmp, tol, max_iter,
+                                  resolve(opts), out, fp_iters, rk_steps);
     if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
     sbr_opts o = resolve(opts);
     const size_t np = (size_t)(n_beta * n_u);
@@ -1419,6 +1525,7 @@ int sbr_sweep_social(sbr_ctx* c, const double* beta, const double* eta, double x
 
 int sbr_device_info(sbr_ctx* c, int32_t* lds_bytes_per_block, int32_t* lds_knot_capacity, int32_t* cu_count)
 {
+    SBR_ON_RANK0(c, sbr_device_info(c, lds_bytes_per_block, lds_knot_capacity, cu_count));
     if (!c) return SBR_EARG;
     int cus = 0;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
@@ -1473,6 +1580,7 @@ __global__ void fastpow_kernel(const double* x, const double* y, int n, double* 
 
 extern "C" int sbr_selftest_fastpow(sbr_ctx* c, const double* x, const double* y, int n, double* out)
 {
+    SBR_ON_RANK0(c, sbr_selftest_fastpow(c, x, y, n, out));
     if (!c || n <= 0 || !x || !y || !out) return SBR_EARG;
     if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
     int rc = ensure_stage(c, (size_t)n * 3 * 8);
@@ -1492,6 +1600,7 @@ extern "C" int sbr_selftest_fastpow(sbr_ctx* c, const double* x, const double* y
 extern "C" int sbr_selftest_detmath(sbr_ctx* c, const double* x, const double* y, int n, double* e, double* l,
                                     double* pw)
 {
+    SBR_ON_RANK0(c, sbr_selftest_detmath(c, x, y, n, e, l, pw));
     if (!c || n <= 0) return SBR_EARG;
     if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
     int rc = ensure_stage(c, (size_t)n * 5 * 8);
@@ -1510,3 +1619,145 @@ extern "C" int sbr_selftest_detmath(sbr_ctx* c, const double* x, const double* y
         return SBR_OK;
     });
 }
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// n-device contexts: the host-pointer sweeps fan out over the ranks (sbr_multi.hip).
+// Inputs of column i go to rank i mod N; each rank runs the single-device *_dev
+// entry point on its GPU; the packed results come back over RCCL.
+// ---------------------------------------------------------------------------
+using sbr_multi_impl::FieldSpec;
+
+// the rank's columns r, r+N, … of a per-column array with `w` values per column
+void gather_cols(const double* src, int64_t w, int r, int N, int64_t nc, double* dst)
+{
+    for (int64_t k = 0; k < nc; k++) memcpy(dst + k * w, src + (r + k * (int64_t)N) * w, (size_t)w * 8);
+}
+
+int stage_host(void* dev, const std::vector<double>& h)
+{
+    return hipMemcpy(dev, h.data(), h.size() * 8, hipMemcpyHostToDevice) == hipSuccess ? SBR_OK : SBR_EDEVICE;
+}
+
+int multi_sweep_baseline(sbr_ctx* c, const double* beta, const double* eta, const double* t_end, double x0,
+                         const double* u, int64_t n_beta, int64_t n_u, double p, double kappa, double lambda,
+                         const sbr_opts& o, sbr_result_soa* out)
+{
+    const int N = sbr_multi_impl::size(c->multi);
+    const int64_t cmax = (n_beta + N - 1) / N;
+    std::vector<FieldSpec> fs = {{out->xi, 8, 1},  {out->tau_in_unc, 8, 1}, {out->tau_out_unc, 8, 1},
+                                 {out->aw_max, 8, 1}, {out->tol, 8, 1},      {out->status, 4, 1},
+                                 {out->iters, 4, 1}};
+    auto stage = [&](int r, int64_t nc, void* in, hipStream_t) -> int {
+        std::vector<double> h(3 * nc + n_u);
+        gather_cols(beta, 1, r, N, nc, h.data());
+        gather_cols(eta, 1, r, N, nc, h.data() + nc);
+        gather_cols(t_end, 1, r, N, nc, h.data() + 2 * nc);
+        memcpy(h.data() + 3 * nc, u, (size_t)n_u * 8);
+        return stage_host(in, h);
+    };
+    auto run = [&](int, int64_t nc, sbr_ctx* kid, hipStream_t s, void* in, const std::vector<void*>& f) -> int {
+        const double* d = (const double*)in;
+        sbr_result_soa ro{(double*)f[0], (double*)f[1], (double*)f[2], (double*)f[3], (double*)f[4],
+                          (uint32_t*)f[5], (int32_t*)f[6]};
+        return sbr_sweep_baseline_dev(kid, s, d, d + nc, d + 2 * nc, x0, d + 3 * nc, nc, n_u, p, kappa, lambda, &o,
+                                      &ro);
+    };
+    int rc = sbr_multi_impl::run_sharded(c->multi, n_beta, n_u, fs, (size_t)(3 * cmax + n_u) * 8, stage, run);
+    if (rc) return fail(c, rc, sbr_multi_impl::last_error(c->multi));
+    if (o.early_exit_nan_run > 0 && out->status && out->xi && out->aw_max && out->tol)
+        sbr_apply_early_exit(n_beta, n_u, o.early_exit_nan_run, out);
+    return SBR_OK;
+}
+
+int multi_sweep_interest(sbr_ctx* c, const double* beta, const double* eta, const double* t_end, double x0,
+                         const double* u, int64_t n_beta, int64_t n_u, double p, double kappa, double lambda, double r_,
+                         double delta, const sbr_opts& o, sbr_result_soa* out, int64_t* rk_steps)
+{
+    const int N = sbr_multi_impl::size(c->multi);
+    const int64_t cmax = (n_beta + N - 1) / N;
+    std::vector<FieldSpec> fs = {{out->xi, 8, 1},  {out->tau_in_unc, 8, 1}, {out->tau_out_unc, 8, 1},
+                                 {out->aw_max, 8, 1}, {out->tol, 8, 1},      {out->status, 4, 1},
+                                 {out->iters, 4, 1},  {rk_steps, 8, 1}};
+    auto stage = [&](int r, int64_t nc, void* in, hipStream_t) -> int {
+        std::vector<double> h(3 * nc + n_u);
+        gather_cols(beta, 1, r, N, nc, h.data());
+        gather_cols(eta, 1, r, N, nc, h.data() + nc);
+        gather_cols(t_end, 1, r, N, nc, h.data() + 2 * nc);
+        memcpy(h.data() + 3 * nc, u, (size_t)n_u * 8);
+        return stage_host(in, h);
+    };
+    auto run = [&](int, int64_t nc, sbr_ctx* kid, hipStream_t s, void* in, const std::vector<void*>& f) -> int {
+        const double* d = (const double*)in;
+        sbr_result_soa ro{(double*)f[0], (double*)f[1], (double*)f[2], (double*)f[3], (double*)f[4],
+                          (uint32_t*)f[5], (int32_t*)f[6]};
+        return sbr_sweep_interest_dev(kid, s, d, d + nc, d + 2 * nc, x0, d + 3 * nc, nc, n_u, p, kappa, lambda, r_,
+                                      delta, &o, &ro, (int64_t*)f[7]);
+    };
+    int rc = sbr_multi_impl::run_sharded(c->multi, n_beta, n_u, fs, (size_t)(3 * cmax + n_u) * 8, stage, run);
+    return rc ? fail(c, rc, sbr_multi_impl::last_error(c->multi)) : SBR_OK;
+}
+
+int multi_sweep_hetero(sbr_ctx* c, int32_t K, const double* betas, const double* dist, const double* eta,
+                       const double* t_end, double x0, const double* u, int64_t n_col, int64_t n_u, double p,
+                       double kappa, double lambda, const sbr_opts& o, sbr_result_soa* out, double* tau_in,
+                       double* tau_out)
+{
+    const int N = sbr_multi_impl::size(c->multi);
+    const int64_t cmax = (n_col + N - 1) / N;
+    std::vector<FieldSpec> fs = {{out->xi, 8, 1},    {out->aw_max, 8, 1}, {out->tol, 8, 1},
+                                 {out->status, 4, 1}, {out->iters, 4, 1},  {tau_in, 8, (size_t)K},
+                                 {tau_out, 8, (size_t)K}};
+    auto stage = [&](int r, int64_t nc, void* in, hipStream_t) -> int {
+        std::vector<double> h(nc * K + K + 2 * nc + n_u);
+        gather_cols(betas, K, r, N, nc, h.data());
+        memcpy(h.data() + nc * K, dist, (size_t)K * 8);
+        gather_cols(eta, 1, r, N, nc, h.data() + nc * K + K);
+        gather_cols(t_end, 1, r, N, nc, h.data() + nc * K + K + nc);
+        memcpy(h.data() + nc * K + K + 2 * nc, u, (size_t)n_u * 8);
+        return stage_host(in, h);
+    };
+    auto run = [&](int, int64_t nc, sbr_ctx* kid, hipStream_t s, void* in, const std::vector<void*>& f) -> int {
+        const double* d = (const double*)in;
+        const double *db = d, *dd = d + nc * K, *de = dd + K, *dt = de + nc, *du = dt + nc;
+        sbr_result_soa ro{(double*)f[0], nullptr, nullptr, (double*)f[1], (double*)f[2], (uint32_t*)f[3],
+                          (int32_t*)f[4]};
+        return sbr_sweep_hetero_dev(kid, s, K, db, dd, de, dt, x0, du, nc, n_u, p, kappa, lambda, &o, &ro,
+                                    (double*)f[5], (double*)f[6]);
+    };
+    int rc = sbr_multi_impl::run_sharded(c->multi, n_col, n_u, fs, (size_t)(cmax * K + K + 2 * cmax + n_u) * 8,
+                                         stage, run);
+    return rc ? fail(c, rc, sbr_multi_impl::last_error(c->multi)) : SBR_OK;
+}
+
+int multi_sweep_social(sbr_ctx* c, const double* beta, const double* eta, double x0, const double* u, int64_t n_beta,
+                       int64_t n_u, double p, double kappa, double lambda, const double* cmp_grid, int32_t n_cmp,
+                       double tol, int32_t max_iter, const sbr_opts& o, sbr_result_soa* out, int32_t* fp_iters,
+                       int64_t* rk_steps)
+{
+    const int N = sbr_multi_impl::size(c->multi);
+    const int64_t cmax = (n_beta + N - 1) / N;
+    std::vector<FieldSpec> fs = {{out->xi, 8, 1},  {out->tau_in_unc, 8, 1}, {out->tau_out_unc, 8, 1},
+                                 {out->aw_max, 8, 1}, {out->tol, 8, 1},      {out->status, 4, 1},
+                                 {out->iters, 4, 1},  {fp_iters, 4, 1},      {rk_steps, 8, 1}};
+    auto stage = [&](int r, int64_t nc, void* in, hipStream_t) -> int {
+        std::vector<double> h(2 * nc + n_u + nc * n_cmp);
+        gather_cols(beta, 1, r, N, nc, h.data());
+        gather_cols(eta, 1, r, N, nc, h.data() + nc);
+        memcpy(h.data() + 2 * nc, u, (size_t)n_u * 8);
+        gather_cols(cmp_grid, n_cmp, r, N, nc, h.data() + 2 * nc + n_u);
+        return stage_host(in, h);
+    };
+    auto run = [&](int, int64_t nc, sbr_ctx* kid, hipStream_t s, void* in, const std::vector<void*>& f) -> int {
+        const double* d = (const double*)in;
+        sbr_result_soa ro{(double*)f[0], (double*)f[1], (double*)f[2], (double*)f[3], (double*)f[4],
+                          (uint32_t*)f[5], (int32_t*)f[6]};
+        return sbr_sweep_social_dev(kid, s, d, d + nc, x0, d + 2 * nc, nc, n_u, p, kappa, lambda, d + 2 * nc + n_u,
+                                    n_cmp, tol, max_iter, &o, &ro, (int32_t*)f[7], (int64_t*)f[8]);
+    };
+    int rc = sbr_multi_impl::run_sharded(c->multi, n_beta, n_u, fs, (size_t)(2 * cmax + n_u + cmax * n_cmp) * 8,
+                                         stage, run);
+    return rc ? fail(c, rc, sbr_multi_impl::last_error(c->multi)) : SBR_OK;
+}
+}  // namespace

@@ -352,21 +352,20 @@ __global__ __launch_bounds__(64) void learn_hetero_kernel(const double* __restri
             EEst = rms<K>(buf);
         }
         if (EEst != EEst) { st |= SBR_ODE_FAILED; break; } // NaN trial state (ReturnCode.Unstable)
-        const double q = pc.q(EEst);
-        if (EEst <= 1.0) {
+        bool acc;
+        const double dtn = pc.next_dt(EEst, dt, dtmax, dtmin, acc);
+        if (acc) {
             naccept++;
-            const double dtnew = dt / q;
-            pc.accept(EEst);
             double tn = t + dt;
             if (fabs(tn - T1) < snap) tn = T1;
             t = tn;
 #pragma unroll
             for (int k = 0; k < K; k++) { x[k] = u[k]; k1[k] = k7[k]; }
-            dt = dmax(dmin(dtmax, dtnew), dtmin);
+            dt = dtn;
             push(t, x);
         } else {
             nreject++;
-            dt = dt / pc.reject_div();
+            dt = dtn;
         }
         if (!(dt > 0.0) || !isfinite(dt)) { st |= SBR_ODE_FAILED; break; }
     }

@@ -1,0 +1,39 @@
+// sbr_multi.h — internal interface of the multi-GPU fan-out (sbr_multi.hip) used by
+// the C-ABI entry points of sbr_capi.hip.  Not part of the public ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "../../include/sbr.h"
+
+struct sbr_multi;
+
+namespace sbr_multi_impl {
+
+// one result array of the caller: n_col·n_u·per_pt elements of esz bytes, u-fastest
+// per column (host == nullptr: computed but not returned)
+struct FieldSpec {
+    void* host;
+    size_t esz;
+    size_t per_pt;
+};
+
+// stage(rank, n_cols_of_rank, device_in, stream): copy the rank's inputs into device_in
+using StageFn = std::function<int(int, int64_t, void*, hipStream_t)>;
+// run(rank, n_cols_of_rank, child_ctx, stream, device_in, device_field_ptrs): enqueue the sweep
+using RunFn = std::function<int(int, int64_t, sbr_ctx*, hipStream_t, void*, const std::vector<void*>&)>;
+
+int create(int n_gpus, const int* devices, sbr_multi** out, std::vector<sbr_ctx*>& kids, std::string& err);
+void destroy(sbr_multi* m);
+int size(const sbr_multi* m);
+sbr_ctx* child(sbr_multi* m, int rank);
+const char* last_error(const sbr_multi* m);
+int run_sharded(sbr_multi* m, int64_t n_col, int64_t n_u, const std::vector<FieldSpec>& fields, size_t in_bytes,
+                const StageFn& stage, const RunFn& run);
+
+}  // namespace sbr_multi_impl

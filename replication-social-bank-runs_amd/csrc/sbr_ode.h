@@ -32,29 +32,41 @@ constexpr double ROS23_D = 0x1.2bec333018867p-2;
 // PIController (OrdinaryDiffEqCore controllers.jl) with FastPower.fastpower:
 //   q11 = fastpower(EEst, β1); q = clamp(q11 / fastpower(qold, β2) / γ, 1/qmax, 1/qmin)
 //   accept: dtnew = dt / q, qold = max(EEst, qoldinit); reject: dt /= min(1/qmin, q11/γ)
-// fastpower(qold, β2) is refreshed only when qold changes.
+// Evaluated for the latency of one lane's serial chain, bit-identical to the oracle:
+//  * fastpower(EEst, β1) and the next fastpower(qold, β2) share fastlog2(Float32(EEst))
+//    (qold = EEst whenever EEst > qoldinit) and their exp2s run side by side;
+//  * q11 / fastpower(qold, β2) divides by a reciprocal refined when qold was set
+//    (div_rcp: the IEEE quotient for these operand ranges, q11 ∈ [2^-21, 2^18]);
+//  * the accept and reject step sizes are both formed, then selected.
 struct PIControl {
-    double qold = CTL_QOLDMIN;
-    double qold_b2;
+    double qold_b2; // fastpower(qold, β2)
+    double r_b2;    // its refined reciprocal
+    double qb2_min; // fastpower(qoldinit, β2)
     double q11 = 0.0;
     ConstDiv by_gamma{CTL_GAMMA};
-    __device__ __forceinline__ PIControl() : qold_b2(sbr_fastpow(CTL_QOLDMIN, CTL_BETA2)) {}
-    __device__ __forceinline__ double q(double EEst)
+    __device__ __forceinline__ PIControl()
+        : qold_b2(sbr_fastpow(CTL_QOLDMIN, CTL_BETA2)), r_b2(rcp_refined(qold_b2)), qb2_min(qold_b2)
     {
-        if (EEst == 0.0) return CTL_INV_QMAX;
-        q11 = sbr_fastpow(EEst, CTL_BETA1);
-        const double qq = q11 / qold_b2;
-        return dmax(CTL_INV_QMAX, dmin(CTL_INV_QMIN, by_gamma(qq)));
     }
-    __device__ __forceinline__ void accept(double EEst)
+    // one controller pass: returns the next dt; `accept` = EEst <= 1 (EEst not NaN)
+    __device__ __forceinline__ double next_dt(double EEst, double dt, double dtmax, double dtmin, bool& accept)
     {
-        const double qn = dmax(EEst, CTL_QOLDMIN);
-        if (qn != qold) {
-            qold = qn;
-            qold_b2 = sbr_fastpow(qn, CTL_BETA2);
+        const float L = sbr_fastlog2f((float)EEst);
+        const double p1 = (double)sbr_exp2f_jl((float)CTL_BETA1 * L); // fastpower(EEst, β1)
+        const double p2 = (double)sbr_exp2f_jl((float)CTL_BETA2 * L); // fastpower(EEst, β2)
+        const bool zero = EEst == 0.0;
+        const double qq = by_gamma(div_rcp(p1, qold_b2, r_b2));
+        const double q = zero ? CTL_INV_QMAX : dmax(CTL_INV_QMAX, dmin(CTL_INV_QMIN, qq));
+        q11 = zero ? q11 : p1;
+        accept = EEst <= 1.0;
+        const double dt_acc = dmax(dmin(dtmax, dt / q), dtmin);
+        const double dt_rej = dt / dmin(CTL_INV_QMIN, by_gamma(q11));
+        if (accept) { // qold = max(EEst, qoldinit)
+            qold_b2 = EEst > CTL_QOLDMIN ? p2 : qb2_min;
+            r_b2 = rcp_refined(qold_b2);
         }
+        return accept ? dt_acc : dt_rej;
     }
-    __device__ __forceinline__ double reject_div() const { return dmin(CTL_INV_QMIN, by_gamma(q11)); }
 };
 
 // Rosenbrock23's dense output (_ode_interpolant, @muladd):
@@ -209,11 +221,10 @@ __device__ __forceinline__ void ode_scalar(Sys& f, Sink& sink, double T1, double
             K.k[0] = k1; K.k[1] = k2; K.k[2] = k3; K.k[3] = k4; K.k[4] = k5; K.k[5] = k6; K.k[6] = k7;
         }
         if (EEst != EEst) { o.status |= SBR_ODE_FAILED; break; } // NaN trial state (ReturnCode.Unstable)
-        const double q = pc.q(EEst);
-        if (EEst <= 1.0) {
+        bool acc;
+        const double dtn = pc.next_dt(EEst, dt, dtmax, dtmin, acc);
+        if (acc) {
             o.naccept++;
-            const double dtnew = dt / q;
-            pc.accept(EEst);
             const double tdt = t + dt;
             double tn = tdt;
             if (fabs(tn - T1) < snap) tn = T1;
@@ -221,12 +232,12 @@ __device__ __forceinline__ void ode_scalar(Sys& f, Sink& sink, double T1, double
             t = tn;
             x = u;
             k1 = fnew;
-            dt = dmax(dmin(dtmax, dtnew), dtmin);
+            dt = dtn;
             if (!sink.accept(tprev, tn, dstep, xprev, u, K, tn == tdt)) break;
             f.accepted(t);
         } else {
             o.nreject++;
-            dt = dt / pc.reject_div();
+            dt = dtn;
         }
         if (!(dt > 0.0) || !isfinite(dt)) { o.status |= SBR_ODE_FAILED; break; }
     }

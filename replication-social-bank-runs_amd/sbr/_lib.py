@@ -76,6 +76,9 @@ globals().update(STATUS)
 _SIGS = {
     "sbr_default_opts": (None, [_P]),
     "sbr_init": (ctypes.c_int, [ctypes.c_int, _P]),
+    "sbr_init_multi": (ctypes.c_int, [ctypes.c_int, _P, _P]),
+    "sbr_multi_size": (ctypes.c_int, [_P]),
+    "sbr_multi_child": (_P, [_P, ctypes.c_int]),
     "sbr_free": (ctypes.c_int, [_P]),
     "sbr_last_error": (ctypes.c_char_p, [_P]),
     "sbr_sweep_baseline": (ctypes.c_int, [_P, _P, _P, _P, _D, _P, _I64, _I64, _D, _D, _D, _P, _P]),

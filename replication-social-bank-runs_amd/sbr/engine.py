@@ -74,19 +74,34 @@ def _out_ptrs(out: dict, fields, n: int, required=()):
 
 
 class Engine:
-    """One libsbr context on one HIP device."""
+    """One libsbr context: one HIP device (``device``), or — with ``n_gpus`` /
+    ``devices`` — an n-device context whose host-pointer sweeps fan out over the GPUs
+    inside libsbr (one host thread per GPU, RCCL gather; sbr_init_multi)."""
 
-    def __init__(self, device: int | None = None):
-        if device is None:
-            device = int(os.environ.get("LOCAL_RANK", "0"))
-        self.device = device
+    def __init__(self, device: int | None = None, n_gpus: int | None = None, devices=None):
         L = _lib.load()
         ctx = _P()
-        rc = L.sbr_init(device, ctypes.byref(ctx))
-        if rc != 0:
-            raise SBRNativeError(f"sbr_init(device={device}) failed ({rc}): no usable HIP device")
+        if n_gpus is not None or devices is not None:
+            devs = None if devices is None else (ctypes.c_int * len(devices))(*devices)
+            n = len(devices) if devices is not None else int(n_gpus)
+            rc = L.sbr_init_multi(n, devs, ctypes.byref(ctx))
+            if rc != 0:
+                raise SBRNativeError(f"sbr_init_multi(n_gpus={n}) failed ({rc})")
+            self.device = devices[0] if devices is not None else 0
+        else:
+            if device is None:
+                device = int(os.environ.get("LOCAL_RANK", "0"))
+            self.device = device
+            rc = L.sbr_init(device, ctypes.byref(ctx))
+            if rc != 0:
+                raise SBRNativeError(f"sbr_init(device={device}) failed ({rc}): no usable HIP device")
         self._ctx = ctx
         self._L = L
+
+    @property
+    def n_gpus(self) -> int:
+        """Devices this context sweeps over (sbr_multi_size)."""
+        return int(self._L.sbr_multi_size(self._ctx))
 
     def close(self):
         if getattr(self, "_ctx", None):

@@ -136,3 +136,18 @@ def test_social_point_paths_bitwise(engine, oracle):
         for k in ("xi", "tau_in_unc", "tau_out_unc", "aw_max", "tol", "t", "G"):
             x, y = np.atleast_1d(g[k]), np.atleast_1d(o[k])
             assert x.shape == y.shape and np.array_equal(x, y, equal_nan=True), (b, uu, k)
+
+
+def test_social_config5_sample_full_workload(engine, golden):
+    """BASELINE config 5 at its stated workload (tol 1e-4, max_iter 500) on an 8 β × 4 u
+    sample of the 512² axes, incl. the corner β = 100, u = 0.001: bit for bit against the
+    oracle's fixed points (tests/golden/config5_sample.npz, tools/make_config5_sample.py)."""
+    gold = golden("config5_sample.npz")
+    cmp = np.stack([sbr.julia_range(0.0, ETA, 1000)] * len(gold["beta"]))
+    g = engine.sweep_social(gold["beta"], ETA, gold["u"], P, KAPPA, LAM, cmp=cmp, tol=1e-4, max_iter=500)
+    for k in FIELDS:
+        assert_bitwise(g[k], gold[k], k)
+    assert_bitwise(g["status"], gold["status"], "status")
+    assert_bitwise(g["iters"], gold["iters"], "bisection iterations")
+    assert_bitwise(g["fp_iters"], gold["fp_iters"], "fixed-point iterations")
+    assert (g["status"] & sbr.STATUS["SBR_RUN"]).any() and (g["status"] & sbr.STATUS["SBR_OOB"]).any()

@@ -183,3 +183,39 @@ def test_hetero_batch_ordered_on_torch_default_stream(engine):
     ref = engine.sweep_hetero(g.betas, g.dist, g.eta, g.t_end, g.u, g.p, g.kappa, g.lam, g.x0, with_groups=False)
     assert np.array_equal(st.cpu().numpy().view(np.uint32), ref["status"].ravel())
     assert np.array_equal(aw.cpu().numpy(), ref["aw_max"].ravel(), equal_nan=True)
+
+
+@pytest.mark.gpu
+def test_hetero_config4_full_properties_and_strided_columns(engine, oracle):
+    """BASELINE config 4 at its stated size (K = 8, 1024 × 1024 = 1,048,576 equilibria) on
+    the GPU: every learning column switches to Rosenbrock23 (AutoSwitch, handled); size-
+    independent properties over the whole grid; 16 strided columns (every 64th, all 1024 u)
+    bit for bit against the oracle's sweep_hetero."""
+    g = sbr.hetero_config4(1024, 1024, 8)
+    r = engine.sweep_hetero(g.betas, g.dist, g.eta, g.t_end, g.u, g.p, g.kappa, g.lam, g.x0, with_groups=False)
+    st = r["status"]
+    run = (st & sbr.STATUS["SBR_RUN"]) > 0
+    # every column's AutoSwitch moves to Rosenbrock23 at least once (the stiff branch runs)
+    assert ((st & sbr.STATUS["SBR_STIFF_SWITCH"]) > 0).all()
+    assert not (st & (sbr.STATUS["SBR_ODE_FAILED"] | sbr.STATUS["SBR_ODE_MAXITERS"] | sbr.STATUS["SBR_KNOT_OVERFLOW"]
+                      | sbr.STATUS["SBR_OOB"] | sbr.STATUS["SBR_ENGINE_TRUNC"])).any()
+    # SolvedModel conventions: ξ / AW_max finite exactly on run points, tol Inf off them
+    assert np.isfinite(r["xi"][run]).all() and np.isnan(r["xi"][~run]).all()
+    assert np.isfinite(r["aw_max"][run]).all() and np.isnan(r["aw_max"][~run]).all()
+    assert (r["tol"][run] <= 1e-12).all()
+    no_trivial = (st & sbr.STATUS["SBR_NO_RUN_HR_BELOW_U"]) > 0
+    assert (r["tol"][no_trivial] == 0.0).all() and np.isinf(r["tol"][~run & ~no_trivial]).all()
+    # AW(ξ*) = κ within the bisection tolerance, so the path maximum is at least κ
+    assert (r["aw_max"][run] >= g.kappa - 1e-12).all()
+    assert 0.5 < run.mean() < 1.0
+    # 16 strided columns, every u, bit for bit
+    sub = g.subset(np.arange(0, 1024, 64))
+    o = oracle.sweep_hetero(sub.betas, sub.dist, sub.eta, sub.t_end, sub.u, sub.p, sub.kappa, sub.lam, sub.x0,
+                            nthreads=16)
+    for f in ("xi", "aw_max", "tol", "status", "iters"):
+        a, b = r[f][::64], o[f]
+        same = (a == b) | (np.isnan(a) & np.isnan(b)) if a.dtype.kind == "f" else (a == b)
+        assert same.all(), (f, int((~same).sum()))
+    # the learning of a strided column: knots bit for bit, Rosenbrock23 steps taken
+    t_o, G_o, info = oracle.learn_hetero(g.betas[512], g.dist, g.t_end[512])
+    assert info["nswitch"] > 0 and info["nstiff"] > 0
