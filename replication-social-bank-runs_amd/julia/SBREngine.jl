@@ -45,17 +45,27 @@ struct ResultSoA       # sbr_result_soa
     iters::Ptr{Int32}
 end
 
+"""
+    Context(device = 0)            one MI355X
+    Context(; n_gpus = 8)          n GPUs of the node: the sweeps below fan out inside libsbr
+                                   (one host thread per GPU, β columns dealt cyclically, RCCL
+                                   gather of the results to GPU 0) — same results as one GPU
+"""
 mutable struct Context
     ptr::Ptr{Cvoid}
-    function Context(device::Integer = 0)
+    function Context(device::Integer = 0; n_gpus::Union{Nothing, Integer} = nothing)
         r = Ref{Ptr{Cvoid}}(C_NULL)
-        rc = ccall((:sbr_init, libsbr), Cint, (Cint, Ptr{Ptr{Cvoid}}), device, r)
+        rc = n_gpus === nothing ?
+             ccall((:sbr_init, libsbr), Cint, (Cint, Ptr{Ptr{Cvoid}}), device, r) :
+             ccall((:sbr_init_multi, libsbr), Cint, (Cint, Ptr{Cint}, Ptr{Ptr{Cvoid}}), n_gpus, C_NULL, r)
         rc == 0 || error("sbr_init failed ($rc): no usable MI355X")
         ctx = new(r[])
         finalizer(c -> ccall((:sbr_free, libsbr), Cint, (Ptr{Cvoid},), c.ptr), ctx)
         return ctx
     end
 end
+
+n_gpus(ctx::Context) = Int(ccall((:sbr_multi_size, libsbr), Cint, (Ptr{Cvoid},), ctx.ptr))
 
 function check(ctx::Context, rc)
     rc == 0 && return
@@ -92,6 +102,27 @@ function solve_equilibrium_grid(ctx::Context, β_vals, u_vals; η = 15.0, tspan_
         check(ctx, rc)
     end
     return (max_AW_matrix = aw, ξ = xi, τ_bar_IN_UNC = tin, τ_bar_OUT_UNC = tout, status = st)
+end
+
+"""
+    learn(ctx, β, tspan_end, x0; cap = 1 << 16)
+
+`solve_SIhomogeneous` (learning.jl:41-54) on the GPU: the knot grid `t` and CDF values `G`
+of the adaptive AutoTsit5(Rosenbrock23()) solution on (0, tspan_end), and the status bits.
+"""
+function learn(ctx::Context, β, tspan_end, x0; cap = 1 << 16)
+    t = Vector{Float64}(undef, cap); G = similar(t); nk = Ref{Int32}(0); st = Ref{UInt32}(0)
+    b = Float64[β]; e = Float64[tspan_end]; te = Float64[tspan_end]
+    opts = Ref(Opts(; early_exit = 0))
+    GC.@preserve t G b e te begin
+        rc = ccall((:sbr_learn_baseline, libsbr), Cint,
+                   (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Float64, Int64, Int32, Ref{Opts},
+                    Ptr{Float64}, Ptr{Float64}, Int64, Ref{Int32}, Ref{UInt32}),
+                   ctx.ptr, b, e, te, x0, 1, Int32(0), opts, t, G, cap, nk, st)
+        check(ctx, rc)
+    end
+    n = Int(nk[])
+    return t[1:n], G[1:n], st[]
 end
 
 """

@@ -1,0 +1,142 @@
+"""The Julia binding (replication-social-bank-runs_amd/julia/SBREngine.jl + SBRDropIn.jl)
+cannot run here (no Julia in the image), so its contract with include/sbr.h is checked
+statically: the `struct Opts` / `struct ResultSoA` mirrors have the C structs' field
+offsets and sizes (a C program compiled against sbr.h prints offsetof / sizeof), the
+ctypes mirror agrees, every ccall'd symbol is declared in sbr.h and exported by libsbr,
+and every ccall passes as many arguments as the C prototype takes."""
+import ctypes
+import re
+import subprocess
+from pathlib import Path
+
+import pytest
+
+REPO = Path(__file__).resolve().parent.parent
+JL = REPO / "replication-social-bank-runs_amd" / "julia"
+HEADER = REPO / "include" / "sbr.h"
+
+# Julia isbits field types → (size, alignment) of the C layout Julia uses for them
+JL_TYPES = {"Float64": (8, 8), "Int64": (8, 8), "Int32": (4, 4), "UInt32": (4, 4)}
+
+
+def jl_struct_fields(name):
+    src = (JL / "SBREngine.jl").read_text()
+    m = re.search(r"^struct %s\b.*?\n(.*?)^end" % name, src, re.S | re.M)
+    assert m, name
+    fields = []
+    for line in m.group(1).splitlines():
+        line = line.split("#")[0].strip()
+        if not line:
+            continue
+        f, t = line.split("::")
+        t = t.strip()
+        fields.append((f.strip(), (8, 8) if t.startswith("Ptr{") else JL_TYPES[t]))
+    return fields
+
+
+def jl_layout(fields):
+    off, out, align = 0, {}, 1
+    for f, (sz, al) in fields:
+        off = (off + al - 1) // al * al
+        out[f] = off
+        off += sz
+        align = max(align, al)
+    return out, (off + align - 1) // align * align
+
+
+@pytest.fixture(scope="module")
+def c_layout(tmp_path_factory):
+    d = tmp_path_factory.mktemp("layout")
+    prog = d / "layout.c"
+    fields = {"sbr_opts": [f for f, _ in jl_struct_fields("Opts")],
+              "sbr_result_soa": [f for f, _ in jl_struct_fields("ResultSoA")]}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void) {"]
+    for st, fs in fields.items():
+        lines.append(f'printf("{st} sizeof %zu\\n", sizeof({st}));')
+        for f in fs:
+            lines.append(f'printf("{st} {f} %zu\\n", offsetof({st}, {f}));')
+    lines.append("return 0; }")
+    prog.write_text("\n".join(lines))
+    exe = d / "layout"
+    subprocess.run(["gcc", "-std=c11", "-o", str(exe), str(prog)], check=True)
+    out = {}
+    for line in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.splitlines():
+        st, f, v = line.split()
+        out[(st, f)] = int(v)
+    return out
+
+
+@pytest.mark.parametrize("jl_name, c_name", [("Opts", "sbr_opts"), ("ResultSoA", "sbr_result_soa")])
+def test_julia_struct_layout_matches_header(c_layout, jl_name, c_name):
+    offs, size = jl_layout(jl_struct_fields(jl_name))
+    assert size == c_layout[(c_name, "sizeof")]
+    for f, o in offs.items():
+        assert o == c_layout[(c_name, f)], (jl_name, f)
+
+
+def test_ctypes_mirror_matches_header(c_layout):
+    from sbr import _lib
+
+    for cls, c_name in ((_lib.Opts, "sbr_opts"), (_lib.ResultSoA, "sbr_result_soa")):
+        assert ctypes.sizeof(cls) == c_layout[(c_name, "sizeof")]
+        for f, _ in cls._fields_:
+            assert getattr(cls, f).offset == c_layout[(c_name, f)], (c_name, f)
+
+
+def _prototypes():
+    src = re.sub(r"/\*.*?\*/", "", HEADER.read_text(), flags=re.S)
+    protos = {}
+    for m in re.finditer(r"\b(?:int|void|const char\*|sbr_ctx\*)\s+(sbr_\w+)\s*\(([^)]*)\)\s*;", src):
+        args = [a for a in m.group(2).split(",") if a.strip() and a.strip() != "void"]
+        protos[m.group(1)] = len(args)
+    return protos
+
+
+def _ccalls():
+    calls = []
+    for f in JL.glob("*.jl"):
+        src = f.read_text()
+        for m in re.finditer(r"ccall\(\(:(\w+), libsbr\),\s*\w+(?:\{\w+\})?,\s*\(", src):
+            # the argument-type tuple: balance parentheses from the match end
+            i, depth = m.end(), 1
+            while depth:
+                depth += {"(": 1, ")": -1}.get(src[i], 0)
+                i += 1
+            types = src[m.end():i - 1]
+            n = len([t for t in re.split(r",(?![^{]*\})", types) if t.strip()])
+            calls.append((f.name, m.group(1), n))
+    return calls
+
+
+def test_julia_ccalls_match_prototypes():
+    protos = _prototypes()
+    calls = _ccalls()
+    assert len(calls) >= 10
+    for fname, sym, n in calls:
+        assert sym in protos, (fname, sym)
+        assert n == protos[sym], (fname, sym, n, protos[sym])
+
+
+def test_ccalled_symbols_are_exported():
+    from sbr import _lib
+
+    L = _lib.load()
+    for _, sym, _ in _ccalls():
+        assert hasattr(L, sym), sym
+
+
+def test_dropin_defines_the_reference_call_surface():
+    """SBRDropIn.jl defines what scripts/1_baseline.jl and plotting.jl call (learning.jl /
+    solver.jl names) with the reference's SolvedModel / LearningResults fields."""
+    src = (JL / "SBRDropIn.jl").read_text()
+    for fn in ("solve_learning", "solve_equilibrium_baseline", "get_AW_functions!", "get_AW", "hazard_rate",
+               "compute_pdf_symbolic_baseline"):
+        assert re.search(r"^function %s\(" % re.escape(fn), src, re.M), fn
+    for st, fields in (("LearningResults", ("params", "learning_cdf", "learning_pdf", "grid", "solve_time",
+                                            "ode_solution")),
+                       ("SolvedModel", ("ξ", "τ_bar_IN_UNC", "τ_bar_OUT_UNC", "HR", "bankrun", "τ_IN", "τ_OUT",
+                                        "model_params", "learning_results", "converged", "solve_time", "tolerance",
+                                        "aw"))):
+        body = re.search(r"^struct %s\b(.*?)^end" % st, src, re.S | re.M).group(1)
+        declared = re.findall(r"^\s+(\w+)::", body, re.M)
+        assert tuple(declared[:len(fields)]) == fields, (st, declared)
