@@ -48,35 +48,45 @@ __global__ __launch_bounds__(64) void learn_logistic_kernel(const double* __rest
         L.n_knots[b] = 0; L.n_tau[b] = 0; L.n_le[b] = 0; L.n_accept[b] = 0; L.n_reject[b] = 0;
         return;
     }
-    // ---- knot sink: store (t, G); the hazard stage runs afterwards in parallel ----
-    double tlast = 0.0, bound = -INFINITY;
-    bool past = false, done = false;
-    int jstar = -1;
-    auto push = [&](double t, double x) {
-        if (n >= L.cap) { st |= SBR_KNOT_OVERFLOW; done = true; return; }
-        T[n] = t;
-        Gv[n] = x;
-        if (!past && t > ETA) { past = true; jstar = n; }
-        // furthest point any lookup of the equilibrium stage can reach
-        if (n >= 1 && (jstar < 0 || n <= jstar)) bound = dmax(bound, t + (t - tlast));
-        tlast = t;
-        n++;
-        if (a.stop_after_eta && past && t >= bound) done = true;
-    };
+    // ---- knot sink: store (t, G); the hazard stage runs afterwards in parallel.  Branch-free:
+    // every attempted step writes its candidate knot at the fill index n (a rejected one is
+    // overwritten by the next accepted step) and the counters advance by select ----
     struct Sink {
-        decltype(push)& p;
-        bool& done;
-        __device__ __forceinline__ bool start(double t, double x) { p(t, x); return !done; }
-        __device__ __forceinline__ bool accept(double, double tn, double, double, double y1, const StepK&, bool)
+        double* __restrict__ T;
+        double* __restrict__ Gv;
+        int n, cap, jstar;
+        double tlast, bound, eta;
+        bool past, done, stop_after_eta;
+        uint32_t& st;
+        __device__ __forceinline__ bool push(bool acc, double t, double x)
         {
-            p(tn, y1);
+            const bool room = n < cap;
+            const int w = room ? n : cap - 1;
+            if (room) { T[w] = t; Gv[w] = x; } // a rejected candidate is overwritten later
+            const bool pushed = acc && room;
+            if (acc && !room) { st |= SBR_KNOT_OVERFLOW; done = true; }
+            const bool newpast = pushed && !past && t > eta;
+            jstar = newpast ? n : jstar;
+            past = past || newpast;
+            // furthest point any lookup of the equilibrium stage can reach
+            const bool upd = pushed && n >= 1 && (jstar < 0 || n <= jstar);
+            bound = upd ? dmax(bound, t + (t - tlast)) : bound;
+            tlast = pushed ? t : tlast;
+            n += pushed ? 1 : 0;
+            done = done || (pushed && stop_after_eta && past && t >= bound);
             return !done;
         }
-    } sink{push, done};
+        __device__ __forceinline__ bool start(double t, double x) { return push(true, t, x); }
+        __device__ __forceinline__ bool step(bool acc, double, double tn, double, double, double y1, const StepK&, bool)
+        {
+            return push(acc, tn, y1);
+        }
+    } sink{T, Gv, 0, L.cap, -1, 0.0, -INFINITY, ETA, false, false, a.stop_after_eta != 0, st};
     LogisticSys f{BETA};
     OdeOut o;
     ode_scalar(f, sink, T1, a.x0, a.rtol, a.atol, a.maxiters, o);
     st |= o.status;
+    n = sink.n;
     const int naccept = (int)o.naccept, nreject = (int)o.nreject;
     L.n_knots[b] = n;
     L.status[b] = st;
@@ -602,6 +612,7 @@ struct ValueRhs {
     {
         if (ntau >= 2 && t >= tlo && t <= thi) jb = ssl_gallop(tau, ntau, jb, t);
     }
+    static constexpr bool kCheapEval = false;
 };
 
 // The value function saved on the HR grid (saveat) streamed into optimal_buffer
@@ -693,10 +704,10 @@ __device__ __forceinline__ void solve_interest_point(P T, P G, P H, const Summ& 
         const TauView<P>& tau;
         int ntau;
         __device__ __forceinline__ bool start(double, double) { return true; }
-        __device__ __forceinline__ bool accept(double tprev, double tn, double dt, double y0, double y1,
-                                               const StepK& K, bool)
+        __device__ __forceinline__ bool step(bool acc, double tprev, double tn, double dt, double y0, double y1,
+                                             const StepK& K, bool)
         {
-            while (sv.next < ntau && tau[sv.next] <= tn) {
+            while (acc && sv.next < ntau && tau[sv.next] <= tn) {
                 const double ts = tau[sv.next];
                 const double th = (ts - tprev) / dt;
                 sv.save(ts != tn ? (K.stiff ? ros23_dense(th, dt, y0, K.k[0], K.k[1])

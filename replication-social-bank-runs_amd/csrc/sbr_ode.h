@@ -104,6 +104,7 @@ struct LogisticSys {
         dT = 0.0;
     }
     __device__ __forceinline__ void accepted(double) const {}
+    static constexpr bool kCheapEval = true;
 };
 
 // ode_determine_initdt for a scalar ODE (order 5: dt₁ = (0.01/max(d₁,d₂))^(1/6));
@@ -144,10 +145,16 @@ __device__ __forceinline__ double initdt_scalar(Sys& f, double T0, double T1, do
 //   double stage(int s, double ts, double x)              Tsit5 stage s = 1..6 (k2..k7) at time ts
 //   void   jac(double t, double x, double& J, double& dT) ForwardDiff ∂f/∂x, ∂f/∂t
 //   void   accepted(double t)                             after an accepted step
+//   static constexpr bool kCheapEval                      eval is a few flops (no lookups)
 // Sink provides
 //   bool start(double t0, double x0)                      the first knot; false = stop
-//   bool accept(double tprev, double tn, double dt, double y0, double y1, const StepK& k, bool exact)
-//        exact: tn == tprev + dt (no snap to T1); false = stop
+//   bool step(bool acc, double tprev, double tn, double dt, double y0, double y1, const StepK& k, bool exact)
+//        called after EVERY attempted step (acc: accepted — the sink must ignore rejected
+//        ones); exact: tn == tprev + dt (no snap to T1); false = stop.
+// The 64 lanes of a wave integrate 64 different ODEs whose steps are accepted and
+// rejected independently, so the step bookkeeping is branch-free (state updates by
+// select, knots written unconditionally at the fill index): a divergent accept / reject
+// branch would run both sides and serialise exec-mask updates on the lane's chain.
 template <class Sys, class Sink>
 __device__ __forceinline__ void ode_scalar(Sys& f, Sink& sink, double T1, double x0, double rtol, double atol,
                                            int64_t maxiters, OdeOut& o)
@@ -166,7 +173,14 @@ __device__ __forceinline__ void ode_scalar(Sys& f, Sink& sink, double T1, double
     int64_t iter = 0;
     while (t < T1) {
         if (++iter > maxiters) { o.status |= SBR_ODE_MAXITERS; break; }
-        if (as.choose(eig, dt)) k1 = f.eval(t, x); // initialize!: fsalfirst = f(uprev, t)
+        // initialize! of the new algorithm: fsalfirst = f(uprev, t)
+        if (Sys::kCheapEval) {
+            const bool sw = as.choose(eig, dt);
+            const double fe = f.eval(t, x);
+            k1 = sw ? fe : k1;
+        } else if (as.choose(eig, dt)) {
+            k1 = f.eval(t, x);
+        }
         dt = dmin(dtmax, dt);
         dt = dmax(dt, dtmin);
         dt = dmin(dt, T1 - t);
@@ -223,22 +237,17 @@ __device__ __forceinline__ void ode_scalar(Sys& f, Sink& sink, double T1, double
         if (EEst != EEst) { o.status |= SBR_ODE_FAILED; break; } // NaN trial state (ReturnCode.Unstable)
         bool acc;
         const double dtn = pc.next_dt(EEst, dt, dtmax, dtmin, acc);
-        if (acc) {
-            o.naccept++;
-            const double tdt = t + dt;
-            double tn = tdt;
-            if (fabs(tn - T1) < snap) tn = T1;
-            const double tprev = t, xprev = x, dstep = dt;
-            t = tn;
-            x = u;
-            k1 = fnew;
-            dt = dtn;
-            if (!sink.accept(tprev, tn, dstep, xprev, u, K, tn == tdt)) break;
-            f.accepted(t);
-        } else {
-            o.nreject++;
-            dt = dtn;
-        }
+        const double tdt = t + dt;
+        const double tn = fabs(tdt - T1) < snap ? T1 : tdt; // fixed_t_for_floatingpoint_error!
+        const bool go = sink.step(acc, t, tn, dt, x, u, K, tn == tdt);
+        if (acc) f.accepted(tn);
+        t = acc ? tn : t;
+        x = acc ? u : x;
+        k1 = acc ? fnew : k1;
+        dt = dtn;
+        o.naccept += acc ? 1 : 0;
+        o.nreject += acc ? 0 : 1;
+        if (!go) break;
         if (!(dt > 0.0) || !isfinite(dt)) { o.status |= SBR_ODE_FAILED; break; }
     }
     o.nswitch = as.nswitch;

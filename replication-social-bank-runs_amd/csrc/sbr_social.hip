@@ -271,6 +271,7 @@ struct SocialRhs {
     {
         if (n >= 2 && t >= tfirst && t <= tlast) (void)w.find_advance(t);
     }
+    static constexpr bool kCheapEval = false;
 };
 
 }  // namespace
@@ -304,9 +305,9 @@ __global__ __launch_bounds__(64) void social_init_kernel(SocialArgs a)
             return true;
         }
         __device__ __forceinline__ bool start(double t, double x) { return push(t, x); }
-        __device__ __forceinline__ bool accept(double, double tn, double, double, double y1, const StepK&, bool)
+        __device__ __forceinline__ bool step(bool acc, double, double tn, double, double, double y1, const StepK&, bool)
         {
-            return push(tn, y1);
+            return acc ? push(tn, y1) : true;
         }
     } sink{T, V, n, a.cap, st};
     OdeOut o;
@@ -399,8 +400,10 @@ __device__ __forceinline__ bool social_iterate(const SocialArgs& a, int l, int i
             return true;
         }
         __device__ __forceinline__ bool start(double t, double x) { return push(t, x, f.lookup(t)); }
-        __device__ __forceinline__ bool accept(double, double tn, double, double, double y1, const StepK&, bool exact)
+        __device__ __forceinline__ bool step(bool acc, double, double tn, double, double, double y1, const StepK&,
+                                             bool exact)
         {
+            if (!acc) return true;
             return push(tn, y1, exact ? f.last_aw : f.lookup(tn));
         }
     } sink{f, T, Gv, AWO, n, a.cap, overflow};
