@@ -200,7 +200,12 @@ SBR_HD float sbr_exp2f_jl(float x)
     const int32_t n = (int32_t)nf;
     const float twopk = sbr_bitsf((uint32_t)(n + 127) << 23);
     const float res = twopk * p;
-    return over ? sbr_bitsf(0x7f800000u) : (under ? 0.0f : (nan_ ? x : res));
+    /* one select per case on computed values (no conditional arms to branch over) */
+    const float inf = sbr_bitsf(0x7f800000u);
+    float out = nan_ ? x : res;
+    out = under ? 0.0f : out;
+    out = over ? inf : out;
+    return out;
 }
 
 /* FastPower.fastpower(x, y) for Float64 x, y */

@@ -63,17 +63,20 @@ __global__ __launch_bounds__(64) void learn_logistic_kernel(const double* __rest
             const bool room = n < cap;
             const int w = room ? n : cap - 1;
             if (room) { T[w] = t; Gv[w] = x; } // a rejected candidate is overwritten later
-            const bool pushed = acc && room;
-            if (acc && !room) { st |= SBR_KNOT_OVERFLOW; done = true; }
-            const bool newpast = pushed && !past && t > eta;
+            // bitwise (not short-circuit) logic: selects, no branches
+            const bool pushed = acc & room;
+            const bool over = acc & !room;
+            st |= over ? SBR_KNOT_OVERFLOW : 0u;
+            const bool newpast = pushed & !past & (t > eta);
             jstar = newpast ? n : jstar;
-            past = past || newpast;
+            past = past | newpast;
             // furthest point any lookup of the equilibrium stage can reach
-            const bool upd = pushed && n >= 1 && (jstar < 0 || n <= jstar);
-            bound = upd ? dmax(bound, t + (t - tlast)) : bound;
+            const bool upd = pushed & (n >= 1) & ((jstar < 0) | (n <= jstar));
+            const double reach = dmax(bound, t + (t - tlast));
+            bound = upd ? reach : bound;
             tlast = pushed ? t : tlast;
             n += pushed ? 1 : 0;
-            done = done || (pushed && stop_after_eta && past && t >= bound);
+            done = done | over | (pushed & stop_after_eta & past & (t >= bound));
             return !done;
         }
         __device__ __forceinline__ bool start(double t, double x) { return push(true, t, x); }

@@ -99,23 +99,20 @@ struct AutoSwitch {
     // so the test is |fl(eigen_est·dt)| >= STIFF_THRESHOLD, the least double passing it
     // (tools/stiff_threshold.py; NaN fails both forms)
     static constexpr double STIFF_THRESHOLD = 0x1.93fbbd7b2031ep+1;
+    // branch-free (select / toggle): the lanes of a wave switch at different steps
     __device__ __forceinline__ bool choose(double eig, double& dt)
     {
         const bool st = fabs(eig * dt) >= STIFF_THRESHOLD;
-        count = st ? (count < 0 ? 1 : count + 1) : (count > 0 ? -1 : count - 1);
-        if (!stiff && count > AUTOSWITCH_MAXSTIFF) {
-            dt = dt * 2.0;
-            stiff = true;
-            nswitch++;
-            return true;
-        }
-        if (stiff && count < -AUTOSWITCH_MAXNONSTIFF) {
-            dt = dt / 2.0;
-            stiff = false;
-            nswitch++;
-            return true;
-        }
-        return false;
+        const int cs = count < 0 ? 1 : count + 1, cn = count > 0 ? -1 : count - 1;
+        count = st ? cs : cn;
+        const bool up = !stiff && count > AUTOSWITCH_MAXSTIFF;
+        const bool down = stiff && count < -AUTOSWITCH_MAXNONSTIFF;
+        const double dt2 = dt * 2.0, dth = dt * 0.5; // dt·0.5 == dt/2 exactly
+        dt = down ? dth : dt;
+        dt = up ? dt2 : dt;
+        stiff = stiff != (up || down);
+        nswitch += (up || down) ? 1 : 0;
+        return up || down;
     }
 };
 

@@ -48,24 +48,31 @@ struct PIControl {
         : qold_b2(sbr_fastpow(CTL_QOLDMIN, CTL_BETA2)), r_b2(rcp_refined(qold_b2)), qb2_min(qold_b2)
     {
     }
-    // one controller pass: returns the next dt; `accept` = EEst <= 1 (EEst not NaN)
-    __device__ __forceinline__ double next_dt(double EEst, double dt, double dtmax, double dtmin, bool& accept)
+    // one controller pass: returns the next dt; `accept` = ok && EEst <= 1 (EEst not NaN).
+    // ok = false turns the pass into a no-op on the controller state (a step that the
+    // caller discards).  One division: the accept (dt/q) and reject (dt/min(1/qmin, q11/γ))
+    // denominators are selected first.
+    __device__ __forceinline__ double next_dt(double EEst, double dt, double dtmax, double dtmin, bool& accept,
+                                              bool ok = true)
     {
         const float L = sbr_fastlog2f((float)EEst);
         const double p1 = (double)sbr_exp2f_jl((float)CTL_BETA1 * L); // fastpower(EEst, β1)
         const double p2 = (double)sbr_exp2f_jl((float)CTL_BETA2 * L); // fastpower(EEst, β2)
         const bool zero = EEst == 0.0;
         const double qq = by_gamma(div_rcp(p1, qold_b2, r_b2));
-        const double q = zero ? CTL_INV_QMAX : dmax(CTL_INV_QMAX, dmin(CTL_INV_QMIN, qq));
+        const double qc = dmax(CTL_INV_QMAX, dmin(CTL_INV_QMIN, qq));
+        const double q = zero ? CTL_INV_QMAX : qc;
         q11 = zero ? q11 : p1;
-        accept = EEst <= 1.0;
-        const double dt_acc = dmax(dmin(dtmax, dt / q), dtmin);
-        const double dt_rej = dt / dmin(CTL_INV_QMIN, by_gamma(q11));
-        if (accept) { // qold = max(EEst, qoldinit)
-            qold_b2 = EEst > CTL_QOLDMIN ? p2 : qb2_min;
-            r_b2 = rcp_refined(qold_b2);
-        }
-        return accept ? dt_acc : dt_rej;
+        accept = ok & (EEst <= 1.0);
+        const double qrej = dmin(CTL_INV_QMIN, by_gamma(q11));
+        const double quot = dt / (accept ? q : qrej);
+        // qold = max(EEst, qoldinit) on accept
+        const double nb2 = EEst > CTL_QOLDMIN ? p2 : qb2_min;
+        const double nr = rcp_refined(nb2);
+        qold_b2 = accept ? nb2 : qold_b2;
+        r_b2 = accept ? nr : r_b2;
+        const double dta = dmax(dmin(dtmax, quot), dtmin);
+        return accept ? dta : quot;
     }
 };
 
@@ -170,9 +177,16 @@ __device__ __forceinline__ void ode_scalar(Sys& f, Sink& sink, double T1, double
     PIControl pc;
     AutoSwitch as;
     if (!sink.start(t, x)) return;
+    if (!(t < T1)) return;
+    if (maxiters < 1) { o.status |= SBR_ODE_MAXITERS; return; }
+    // One loop exit, tested at the bottom: the reference's early exits (DtLessThanMin before
+    // the step, a NaN trial state after it) compute the step and discard it (ok = false: no
+    // knot, no controller / state update, not counted), and the maxiters test of the next
+    // loopheader is made at the end of this iteration.  A divergent multi-exit loop costs
+    // every lane the exit-mask bookkeeping of all exits on every step.
     int64_t iter = 0;
-    while (t < T1) {
-        if (++iter > maxiters) { o.status |= SBR_ODE_MAXITERS; break; }
+    for (;;) {
+        ++iter;
         // initialize! of the new algorithm: fsalfirst = f(uprev, t)
         if (Sys::kCheapEval) {
             const bool sw = as.choose(eig, dt);
@@ -184,7 +198,7 @@ __device__ __forceinline__ void ode_scalar(Sys& f, Sink& sink, double T1, double
         dt = dmin(dtmax, dt);
         dt = dmax(dt, dtmin);
         dt = dmin(dt, T1 - t);
-        if (dt <= dtmin && t + dt < T1) { o.status |= SBR_ODE_FAILED; break; } // DtLessThanMin
+        const bool dtfail = (dt <= dtmin) & (t + dt < T1); // DtLessThanMin
         StepK K;
         double u, fnew, EEst;
         if (as.stiff) {
@@ -192,7 +206,6 @@ __device__ __forceinline__ void ode_scalar(Sys& f, Sink& sink, double T1, double
             K.stiff = true;
             double J, dT;
             f.jac(t, x, J, dT);
-            eig = fabs(J);
             const double dtg = dt * ROS23_D;
             const double invdtg = 1.0 / dtg, neginvdtg = -(1.0 / dtg);
             const double dto2 = dt / 2.0, dto6 = dt / 6.0;
@@ -210,6 +223,7 @@ __device__ __forceinline__ void ode_scalar(Sys& f, Sink& sink, double T1, double
             EEst = fabs(ut / fma(dmax(fabs(x), fabs(u)), rtol, atol));
             K.k[0] = s1;
             K.k[1] = s2;
+            eig = fabs(J);
         } else {
             // ---- Tsit5 (perform_step!, Tsit5ConstantCache, @muladd) ----
             K.stiff = false;
@@ -227,16 +241,17 @@ __device__ __forceinline__ void ode_scalar(Sys& f, Sink& sink, double T1, double
             u = fma(dt, fma(A71, k1, fma(A72, k2, fma(A73, k3, fma(A74, k4, fma(A75, k5, A76 * k6))))), x);
             const double k7 = f.stage(6, t + dt, u);
             const double eigr = fabs((k7 - k6) / (u - tmp6));
-            eig = (eigr != eigr) ? (double)NAN : eigr;
             const double ut =
                 dt * fma(BT1, k1, fma(BT2, k2, fma(BT3, k3, fma(BT4, k4, fma(BT5, k5, fma(BT6, k6, BT7 * k7))))));
             EEst = fabs(ut / fma(dmax(fabs(x), fabs(u)), rtol, atol));
             fnew = k7;
             K.k[0] = k1; K.k[1] = k2; K.k[2] = k3; K.k[3] = k4; K.k[4] = k5; K.k[5] = k6; K.k[6] = k7;
+            eig = (eigr != eigr) ? (double)NAN : eigr;
         }
-        if (EEst != EEst) { o.status |= SBR_ODE_FAILED; break; } // NaN trial state (ReturnCode.Unstable)
+        const bool nan = EEst != EEst; // NaN trial state (ReturnCode.Unstable)
+        const bool ok = (!dtfail) & (!nan);
         bool acc;
-        const double dtn = pc.next_dt(EEst, dt, dtmax, dtmin, acc);
+        const double dtn = pc.next_dt(EEst, dt, dtmax, dtmin, acc, ok);
         const double tdt = t + dt;
         const double tn = fabs(tdt - T1) < snap ? T1 : tdt; // fixed_t_for_floatingpoint_error!
         const bool go = sink.step(acc, t, tn, dt, x, u, K, tn == tdt);
@@ -244,11 +259,16 @@ __device__ __forceinline__ void ode_scalar(Sys& f, Sink& sink, double T1, double
         t = acc ? tn : t;
         x = acc ? u : x;
         k1 = acc ? fnew : k1;
-        dt = dtn;
+        dt = ok ? dtn : dt;
         o.naccept += acc ? 1 : 0;
-        o.nreject += acc ? 0 : 1;
-        if (!go) break;
-        if (!(dt > 0.0) || !isfinite(dt)) { o.status |= SBR_ODE_FAILED; break; }
+        o.nreject += (ok & !acc) ? 1 : 0;
+        // bitwise (not short-circuit) logic: no branches for the compiler to form
+        const bool badt = ok & go & !((dt > 0.0) & (fabs(dt) < (double)INFINITY));
+        const bool more = t < T1;
+        const bool maxit = ok & go & !badt & more & (iter >= maxiters);
+        o.status |= ((!ok) | badt) ? SBR_ODE_FAILED : 0u;
+        o.status |= maxit ? SBR_ODE_MAXITERS : 0u;
+        if ((!ok) | (!go) | badt | (!more) | maxit) break;
     }
     o.nswitch = as.nswitch;
     if (as.nswitch > 0) o.status |= SBR_STIFF_SWITCH;
