@@ -166,17 +166,38 @@ SBR_HD double sbr_exp10(double y) { return sbr_exp(y * SBR_LN10); }
 SBR_HD uint32_t sbr_fbits(float x) { uint32_t u; __builtin_memcpy(&u, &x, 4); return u; }
 SBR_HD float sbr_bitsf(uint32_t u) { float x; __builtin_memcpy(&x, &u, 4); return x; }
 
+/* n / d in IEEE single precision for d in [1, 4) and n = 0 or 2^-100 < |n| < 2^100: on
+ * gfx950 the hardware division sequence the compiler emits for `/` (v_rcp_f32, one
+ * Newton step on the reciprocal, q = n·r, two fma remainder corrections) without its
+ * v_div_scale / v_div_fmas scaling and v_div_fixup special-case steps, which are
+ * identities for these operands — the same correctly rounded quotient, bit for bit,
+ * in 8 dependent operations instead of 11; the host divides. */
+SBR_HD float sbr_fdiv_mid(float n, float d)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    const float r0 = __builtin_amdgcn_rcpf(d);
+    const float r = __builtin_fmaf(__builtin_fmaf(-d, r0, 1.0f), r0, r0);
+    float q = n * r;
+    q = __builtin_fmaf(__builtin_fmaf(-d, q, n), r, q);
+    return __builtin_fmaf(__builtin_fmaf(-d, q, n), r, q);
+#else
+    return n / d;
+#endif
+}
+
 SBR_HD float sbr_fastlog2f(float x)
 {
     const float a = 0.338953f, b = 2.198599f, c = 1.523692f;
     const uint32_t ux1i = sbr_fbits(x);
     const uint32_t e = (ux1i & 0x7F800000u) >> 23;
-    const int greater = (ux1i & 0x00400000u) != 0u; /* significand > 1.5 */
-    /* greater: halve the significand (exponent 0x3f000000) and compensate with 126 */
-    const float signif0 = sbr_bitsf((ux1i & 0x007FFFFFu) | (greater ? 0x3f000000u : 0x3f800000u));
-    const float fexp = (float)e - (greater ? 126.0f : 127.0f);
+    const uint32_t g = (ux1i >> 22) & 1u; /* significand > 1.5 */
+    /* g: halve the significand (exponent 0x3f000000 instead of 0x3f800000) and
+     * compensate with 126 instead of 127 (integer forms of the same selects) */
+    const float signif0 = sbr_bitsf(((ux1i & 0x007FFFFFu) | 0x3f800000u) - (g << 23));
+    const float fexp = (float)((int32_t)e - 127 + (int32_t)g);
     const float signif = signif0 - 1.0f;
-    return fexp + (signif * (a * signif + b)) / (signif + c);
+    /* signif in [-0.25, 0.5): the divisor signif + c is in [1.27, 2.03) */
+    return fexp + sbr_fdiv_mid(signif * (a * signif + b), signif + c);
 }
 
 /* Base.Math.exp_impl_fast(x::Float32, Val(2)) (MAX_EXP = 128, SUBNORM_EXP = 150).
@@ -185,7 +206,9 @@ SBR_HD float sbr_fastlog2f(float x)
 SBR_HD float sbr_exp2f_jl(float x)
 {
     const int over = x >= 128.0f, under = x <= -150.0f, nan_ = x != x;
-    const float xs = (over | under | nan_) ? 0.0f : x;
+    /* the kernel's argument clamped into [-150, 128] (NaN -> -150): out-of-range and NaN
+     * results are selected at the end, the clamp only keeps the exponent arithmetic defined */
+    const float xs = __builtin_fminf(__builtin_fmaxf(x, -150.0f), 128.0f);
     const float nf = __builtin_rintf(xs); /* round(x), ties to even */
     const float r0 = __builtin_fmaf(nf, -1.0f, xs);
     const float r = __builtin_fmaf(nf, 0.0f, r0);

@@ -54,9 +54,9 @@ __global__ __launch_bounds__(64) void learn_logistic_kernel(const double* __rest
     struct Sink {
         double* __restrict__ T;
         double* __restrict__ Gv;
-        int n, cap, jstar;
+        int n, cap;
         double tlast, bound, eta;
-        bool past, done, stop_after_eta;
+        int past, done, stop_after_eta; // 0 / 1 (ints: loop-carried bools cost mask conversions)
         uint32_t& st;
         __device__ __forceinline__ bool push(bool acc, double t, double x)
         {
@@ -67,24 +67,24 @@ __global__ __launch_bounds__(64) void learn_logistic_kernel(const double* __rest
             const bool pushed = acc & room;
             const bool over = acc & !room;
             st |= over ? SBR_KNOT_OVERFLOW : 0u;
-            const bool newpast = pushed & !past & (t > eta);
-            jstar = newpast ? n : jstar;
-            past = past | newpast;
-            // furthest point any lookup of the equilibrium stage can reach
-            const bool upd = pushed & (n >= 1) & ((jstar < 0) | (n <= jstar));
+            // furthest point any lookup of the equilibrium stage can reach (DESIGN.md
+            // §Truncation): max of t_j + (t_j − t_{j−1}) over the knots j ≥ 1 up to and
+            // including the first knot past η
+            const bool upd = pushed & (n >= 1) & (past == 0);
             const double reach = dmax(bound, t + (t - tlast));
             bound = upd ? reach : bound;
+            past |= (pushed & (t > eta)) ? 1 : 0;
             tlast = pushed ? t : tlast;
             n += pushed ? 1 : 0;
-            done = done | over | (pushed & stop_after_eta & past & (t >= bound));
-            return !done;
+            done |= (over | (pushed & (stop_after_eta != 0) & (past != 0) & (t >= bound))) ? 1 : 0;
+            return done == 0;
         }
         __device__ __forceinline__ bool start(double t, double x) { return push(true, t, x); }
         __device__ __forceinline__ bool step(bool acc, double, double tn, double, double, double y1, const StepK&, bool)
         {
             return push(acc, tn, y1);
         }
-    } sink{T, Gv, 0, L.cap, -1, 0.0, -INFINITY, ETA, false, false, a.stop_after_eta != 0, st};
+    } sink{T, Gv, 0, L.cap, 0.0, -INFINITY, ETA, 0, 0, a.stop_after_eta != 0 ? 1 : 0, st};
     LogisticSys f{BETA};
     OdeOut o;
     ode_scalar(f, sink, T1, a.x0, a.rtol, a.atol, a.maxiters, o);
@@ -615,7 +615,7 @@ struct ValueRhs {
     {
         if (ntau >= 2 && t >= tlo && t <= thi) jb = ssl_gallop(tau, ntau, jb, t);
     }
-    static constexpr bool kCheapEval = false;
+    static constexpr bool kFsalExact = false;
 };
 
 // The value function saved on the HR grid (saveat) streamed into optimal_buffer

@@ -348,6 +348,8 @@ sbr_opts resolve(const sbr_opts* o)
         r = *o;
         if (r.knot_capacity <= 0) r.knot_capacity = kDefaultCap;
         if (r.ode_maxiters <= 0) r.ode_maxiters = SBR_DEFAULT_ODE_MAXITERS;
+        // the device ODE loops count a solve's steps in int32 (sbr_ode.h OdeOut)
+        if (r.ode_maxiters > INT32_MAX) r.ode_maxiters = INT32_MAX;
         if (r.bisect_max_iters <= 0) r.bisect_max_iters = 100;
         if (r.hetero_max_iters <= 0) r.hetero_max_iters = 500;
     }

@@ -48,6 +48,12 @@ __device__ __forceinline__ bool collapsed(double d) { return fabs(d) <= 4.940656
 
 __device__ __forceinline__ double dmin(double a, double b) { return a < b ? a : b; }
 __device__ __forceinline__ double dmax(double a, double b) { return a > b ? a : b; }
+// One v_min_f64 / v_max_f64 (IEEE minNum / maxNum) instead of a compare and two
+// selects: the same value as dmin / dmax whenever neither operand is NaN and they
+// are not zeros of opposite sign — the ODE step-size clamps, whose operands (dt, the
+// controller's q) are positive and finite on every step that is kept.
+__device__ __forceinline__ double vmin(double a, double b) { return __builtin_fmin(a, b); }
+__device__ __forceinline__ double vmax(double a, double b) { return __builtin_fmax(a, b); }
 
 // a / b for a fixed b by the same IEEE-754 division sequence the compiler
 // emits for `/` (v_div_scale, v_rcp_f64, two Newton steps, q = a·r, one fma
@@ -84,6 +90,8 @@ struct ConstDiv {
         const double q = div_rcp(a, b, r);
         return a == (double)INFINITY ? (double)INFINITY : q;
     }
+    // a known finite (the +Inf select dropped)
+    __device__ __forceinline__ double finite(double a) const { return div_rcp(a, b, r); }
 };
 
 // AutoSwitch (OrdinaryDiffEqCore composite_algs: maxstiffstep 10, maxnonstiffstep 3,
@@ -93,7 +101,7 @@ struct ConstDiv {
 // choose() returns true when the algorithm changes.
 struct AutoSwitch {
     int count = 0;
-    bool stiff = false;
+    int stiff = 0; // 0 / 1 (an int: loop-carried bools cost mask conversions every step)
     int nswitch = 0;
     // |eigen_est·dt / 3.5068| > 9/10 without the division: x ↦ fl(x / 3.5068) is monotone,
     // so the test is |fl(eigen_est·dt)| >= STIFF_THRESHOLD, the least double passing it
@@ -105,14 +113,14 @@ struct AutoSwitch {
         const bool st = fabs(eig * dt) >= STIFF_THRESHOLD;
         const int cs = count < 0 ? 1 : count + 1, cn = count > 0 ? -1 : count - 1;
         count = st ? cs : cn;
-        const bool up = !stiff && count > AUTOSWITCH_MAXSTIFF;
-        const bool down = stiff && count < -AUTOSWITCH_MAXNONSTIFF;
+        const bool up = (stiff == 0) & (count > AUTOSWITCH_MAXSTIFF);
+        const bool down = (stiff != 0) & (count < -AUTOSWITCH_MAXNONSTIFF);
         const double dt2 = dt * 2.0, dth = dt * 0.5; // dt·0.5 == dt/2 exactly
         dt = down ? dth : dt;
         dt = up ? dt2 : dt;
-        stiff = stiff != (up || down);
-        nswitch += (up || down) ? 1 : 0;
-        return up || down;
+        stiff ^= (up | down) ? 1 : 0;
+        nswitch += (up | down) ? 1 : 0;
+        return up | down;
     }
 };
 

@@ -59,19 +59,23 @@ struct PIControl {
         const double p1 = (double)sbr_exp2f_jl((float)CTL_BETA1 * L); // fastpower(EEst, β1)
         const double p2 = (double)sbr_exp2f_jl((float)CTL_BETA2 * L); // fastpower(EEst, β2)
         const bool zero = EEst == 0.0;
-        const double qq = by_gamma(div_rcp(p1, qold_b2, r_b2));
-        const double qc = dmax(CTL_INV_QMAX, dmin(CTL_INV_QMIN, qq));
+        // p1, q11 = fastpower(·, β1) ∈ [2^-18, 2^18]: finite, so the +Inf select of by_gamma is dropped
+        const double qq = by_gamma.finite(div_rcp(p1, qold_b2, r_b2));
+        const double qc = vmax(CTL_INV_QMAX, vmin(CTL_INV_QMIN, qq));
         const double q = zero ? CTL_INV_QMAX : qc;
         q11 = zero ? q11 : p1;
         accept = ok & (EEst <= 1.0);
-        const double qrej = dmin(CTL_INV_QMIN, by_gamma(q11));
-        const double quot = dt / (accept ? q : qrej);
+        const double qrej = vmin(CTL_INV_QMIN, by_gamma.finite(q11));
+        // dt / den with den in [1/qmax, 1/qmin] and dt in [dtmin, dtmax]: the division
+        // sequence without its identity scaling steps (div_rcp), the IEEE quotient
+        const double den = accept ? q : qrej;
+        const double quot = div_rcp(dt, den, rcp_refined(den));
         // qold = max(EEst, qoldinit) on accept
         const double nb2 = EEst > CTL_QOLDMIN ? p2 : qb2_min;
         const double nr = rcp_refined(nb2);
         qold_b2 = accept ? nb2 : qold_b2;
         r_b2 = accept ? nr : r_b2;
-        const double dta = dmax(dmin(dtmax, quot), dtmin);
+        const double dta = vmax(vmin(dtmax, quot), dtmin);
         return accept ? dta : quot;
     }
 };
@@ -93,7 +97,7 @@ struct StepK {
 };
 
 struct OdeOut {
-    int64_t naccept = 0, nreject = 0;
+    int32_t naccept = 0, nreject = 0; // per solve (maxiters is clamped to INT32_MAX by the C API)
     int32_t nswitch = 0;
     uint32_t status = 0;
 };
@@ -111,7 +115,10 @@ struct LogisticSys {
         dT = 0.0;
     }
     __device__ __forceinline__ void accepted(double) const {}
-    static constexpr bool kCheapEval = true;
+    // k1 (FSAL: k7 of the last Tsit5 step, or Rosenbrock23's f(t+dt, u)) is bit for bit
+    // the f(t, x) that initialize! re-evaluates after a switch: the same expression on the
+    // same x (autonomous), so the re-evaluation is skipped
+    static constexpr bool kFsalExact = true;
 };
 
 // ode_determine_initdt for a scalar ODE (order 5: dt₁ = (0.01/max(d₁,d₂))^(1/6));
@@ -146,13 +153,51 @@ __device__ __forceinline__ double initdt_scalar(Sys& f, double T0, double T1, do
     return dt;
 }
 
+// The Tsit5 tableau held in VGPRs for the scalar loop: as literals the compiler keeps
+// re-materialising the 64-bit constants it cannot hold in SGPRs (two s_mov_b32 each,
+// every step, issued by the lone wave in series with its VALU work).
+struct Tsit5Regs {
+    double a31, a32, a41, a42, a43, a51, a52, a53, a54, a61, a62, a63, a64, a65, a71, a72, a73, a74, a75, a76, bt1, bt2, bt3, bt4, bt5, bt6, bt7;
+    __device__ __forceinline__ Tsit5Regs()
+        : a31(A31), a32(A32), a41(A41), a42(A42), a43(A43), a51(A51), a52(A52), a53(A53), a54(A54), a61(A61), a62(A62), a63(A63), a64(A64), a65(A65), a71(A71), a72(A72), a73(A73), a74(A74), a75(A75), a76(A76), bt1(BT1), bt2(BT2), bt3(BT3), bt4(BT4), bt5(BT5), bt6(BT6), bt7(BT7)
+    {
+        asm volatile("" : "+v"(a31));
+        asm volatile("" : "+v"(a32));
+        asm volatile("" : "+v"(a41));
+        asm volatile("" : "+v"(a42));
+        asm volatile("" : "+v"(a43));
+        asm volatile("" : "+v"(a51));
+        asm volatile("" : "+v"(a52));
+        asm volatile("" : "+v"(a53));
+        asm volatile("" : "+v"(a54));
+        asm volatile("" : "+v"(a61));
+        asm volatile("" : "+v"(a62));
+        asm volatile("" : "+v"(a63));
+        asm volatile("" : "+v"(a64));
+        asm volatile("" : "+v"(a65));
+        asm volatile("" : "+v"(a71));
+        asm volatile("" : "+v"(a72));
+        asm volatile("" : "+v"(a73));
+        asm volatile("" : "+v"(a74));
+        asm volatile("" : "+v"(a75));
+        asm volatile("" : "+v"(a76));
+        asm volatile("" : "+v"(bt1));
+        asm volatile("" : "+v"(bt2));
+        asm volatile("" : "+v"(bt3));
+        asm volatile("" : "+v"(bt4));
+        asm volatile("" : "+v"(bt5));
+        asm volatile("" : "+v"(bt6));
+        asm volatile("" : "+v"(bt7));
+    }
+};
+
 // Scalar AutoTsit5(Rosenbrock23()) on (0, T1) from x0.  Sys provides
 //   double eval(double t, double x)                       f at any (t, x)
 //   void   prepare(double t, double dt)                   before the Tsit5 stages of a step
 //   double stage(int s, double ts, double x)              Tsit5 stage s = 1..6 (k2..k7) at time ts
 //   void   jac(double t, double x, double& J, double& dT) ForwardDiff ∂f/∂x, ∂f/∂t
 //   void   accepted(double t)                             after an accepted step
-//   static constexpr bool kCheapEval                      eval is a few flops (no lookups)
+//   static constexpr bool kFsalExact                      f(t, x) == the carried k1 bit for bit
 // Sink provides
 //   bool start(double t0, double x0)                      the first knot; false = stop
 //   bool step(bool acc, double tprev, double tn, double dt, double y0, double y1, const StepK& k, bool exact)
@@ -176,6 +221,7 @@ __device__ __forceinline__ void ode_scalar(Sys& f, Sink& sink, double T1, double
     double eig = 1.0; // integrator.eigen_est = 1/oneunit(t) at init
     PIControl pc;
     AutoSwitch as;
+    const Tsit5Regs cf;
     if (!sink.start(t, x)) return;
     if (!(t < T1)) return;
     if (maxiters < 1) { o.status |= SBR_ODE_MAXITERS; return; }
@@ -185,19 +231,18 @@ __device__ __forceinline__ void ode_scalar(Sys& f, Sink& sink, double T1, double
     // loopheader is made at the end of this iteration.  A divergent multi-exit loop costs
     // every lane the exit-mask bookkeeping of all exits on every step.
     int64_t iter = 0;
+    uint32_t why = 0; // status bits of the exit (an int, not loop-carried bools)
     for (;;) {
         ++iter;
         // initialize! of the new algorithm: fsalfirst = f(uprev, t)
-        if (Sys::kCheapEval) {
-            const bool sw = as.choose(eig, dt);
-            const double fe = f.eval(t, x);
-            k1 = sw ? fe : k1;
+        if (Sys::kFsalExact) {
+            (void)as.choose(eig, dt);
         } else if (as.choose(eig, dt)) {
             k1 = f.eval(t, x);
         }
-        dt = dmin(dtmax, dt);
-        dt = dmax(dt, dtmin);
-        dt = dmin(dt, T1 - t);
+        dt = vmin(dtmax, dt);
+        dt = vmax(dt, dtmin);
+        dt = vmin(dt, T1 - t);
         const bool dtfail = (dt <= dtmin) & (t + dt < T1); // DtLessThanMin
         StepK K;
         double u, fnew, EEst;
@@ -230,19 +275,19 @@ __device__ __forceinline__ void ode_scalar(Sys& f, Sink& sink, double T1, double
             f.prepare(t, dt);
             double tmp = fma(dt * A21, k1, x);
             const double k2 = f.stage(1, fma(C1, dt, t), tmp);
-            tmp = fma(dt, fma(A31, k1, A32 * k2), x);
+            tmp = fma(dt, fma(cf.a31, k1, cf.a32 * k2), x);
             const double k3 = f.stage(2, fma(C2, dt, t), tmp);
-            tmp = fma(dt, fma(A41, k1, fma(A42, k2, A43 * k3)), x);
+            tmp = fma(dt, fma(cf.a41, k1, fma(cf.a42, k2, cf.a43 * k3)), x);
             const double k4 = f.stage(3, fma(C3, dt, t), tmp);
-            tmp = fma(dt, fma(A51, k1, fma(A52, k2, fma(A53, k3, A54 * k4))), x);
+            tmp = fma(dt, fma(cf.a51, k1, fma(cf.a52, k2, fma(cf.a53, k3, cf.a54 * k4))), x);
             const double k5 = f.stage(4, fma(C4, dt, t), tmp);
-            const double tmp6 = fma(dt, fma(A61, k1, fma(A62, k2, fma(A63, k3, fma(A64, k4, A65 * k5)))), x);
+            const double tmp6 = fma(dt, fma(cf.a61, k1, fma(cf.a62, k2, fma(cf.a63, k3, fma(cf.a64, k4, cf.a65 * k5)))), x);
             const double k6 = f.stage(5, t + dt, tmp6);
-            u = fma(dt, fma(A71, k1, fma(A72, k2, fma(A73, k3, fma(A74, k4, fma(A75, k5, A76 * k6))))), x);
+            u = fma(dt, fma(cf.a71, k1, fma(cf.a72, k2, fma(cf.a73, k3, fma(cf.a74, k4, fma(cf.a75, k5, cf.a76 * k6))))), x);
             const double k7 = f.stage(6, t + dt, u);
             const double eigr = fabs((k7 - k6) / (u - tmp6));
             const double ut =
-                dt * fma(BT1, k1, fma(BT2, k2, fma(BT3, k3, fma(BT4, k4, fma(BT5, k5, fma(BT6, k6, BT7 * k7))))));
+                dt * fma(cf.bt1, k1, fma(cf.bt2, k2, fma(cf.bt3, k3, fma(cf.bt4, k4, fma(cf.bt5, k5, fma(cf.bt6, k6, cf.bt7 * k7))))));
             EEst = fabs(ut / fma(dmax(fabs(x), fabs(u)), rtol, atol));
             fnew = k7;
             K.k[0] = k1; K.k[1] = k2; K.k[2] = k3; K.k[3] = k4; K.k[4] = k5; K.k[5] = k6; K.k[6] = k7;
@@ -262,14 +307,16 @@ __device__ __forceinline__ void ode_scalar(Sys& f, Sink& sink, double T1, double
         dt = ok ? dtn : dt;
         o.naccept += acc ? 1 : 0;
         o.nreject += (ok & !acc) ? 1 : 0;
-        // bitwise (not short-circuit) logic: no branches for the compiler to form
+        // bitwise (not short-circuit) logic: no branches for the compiler to form; the
+        // exit reason is turned into status bits once, after the loop
         const bool badt = ok & go & !((dt > 0.0) & (fabs(dt) < (double)INFINITY));
         const bool more = t < T1;
         const bool maxit = ok & go & !badt & more & (iter >= maxiters);
-        o.status |= ((!ok) | badt) ? SBR_ODE_FAILED : 0u;
-        o.status |= maxit ? SBR_ODE_MAXITERS : 0u;
-        if ((!ok) | (!go) | badt | (!more) | maxit) break;
+        const bool fail = (!ok) | badt;
+        why = (fail ? SBR_ODE_FAILED : 0u) | (maxit ? SBR_ODE_MAXITERS : 0u);
+        if (fail | (!go) | (!more) | maxit) break;
     }
+    o.status |= why;
     o.nswitch = as.nswitch;
     if (as.nswitch > 0) o.status |= SBR_STIFF_SWITCH;
 }

@@ -271,7 +271,7 @@ struct SocialRhs {
     {
         if (n >= 2 && t >= tfirst && t <= tlast) (void)w.find_advance(t);
     }
-    static constexpr bool kCheapEval = false;
+    static constexpr bool kFsalExact = false;
 };
 
 }  // namespace
