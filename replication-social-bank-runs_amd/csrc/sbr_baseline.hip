@@ -54,7 +54,7 @@ __global__ __launch_bounds__(64) void learn_logistic_kernel(const double* __rest
     struct Sink {
         double* __restrict__ T;
         double* __restrict__ Gv;
-        int n, cap;
+        int n, cap, m; // m: knots ≤ η (the hazard stage's τ̄ prefix), set at the first knot past η
         double tlast, bound, eta;
         int past, done, stop_after_eta; // 0 / 1 (ints: loop-carried bools cost mask conversions)
         uint32_t& st;
@@ -73,7 +73,9 @@ __global__ __launch_bounds__(64) void learn_logistic_kernel(const double* __rest
             const bool upd = pushed & (n >= 1) & (past == 0);
             const double reach = dmax(bound, t + (t - tlast));
             bound = upd ? reach : bound;
-            past |= (pushed & (t > eta)) ? 1 : 0;
+            const bool cross = pushed & (past == 0) & (t > eta);
+            m = cross ? n : m;
+            past |= cross ? 1 : 0;
             tlast = pushed ? t : tlast;
             n += pushed ? 1 : 0;
             done |= (over | (pushed & (stop_after_eta != 0) & (past != 0) & (t >= bound))) ? 1 : 0;
@@ -84,7 +86,7 @@ __global__ __launch_bounds__(64) void learn_logistic_kernel(const double* __rest
         {
             return push(acc, tn, y1);
         }
-    } sink{T, Gv, 0, L.cap, 0.0, -INFINITY, ETA, 0, 0, a.stop_after_eta != 0 ? 1 : 0, st};
+    } sink{T, Gv, 0, L.cap, -1, 0.0, -INFINITY, ETA, 0, 0, a.stop_after_eta != 0 ? 1 : 0, st};
     LogisticSys f{BETA};
     OdeOut o;
     ode_scalar(f, sink, T1, a.x0, a.rtol, a.atol, a.maxiters, o);
@@ -92,6 +94,7 @@ __global__ __launch_bounds__(64) void learn_logistic_kernel(const double* __rest
     n = sink.n;
     const int naccept = (int)o.naccept, nreject = (int)o.nreject;
     L.n_knots[b] = n;
+    L.n_le[b] = sink.m < 0 ? n : sink.m; // every knot ≤ η when none passed it
     L.status[b] = st;
     L.n_accept[b] = naccept;
     L.n_reject[b] = nreject;
@@ -110,23 +113,79 @@ __global__ __launch_bounds__(64) void learn_logistic_kernel(const double* __rest
 #define SBR_EQ_MINW 6 // waves per SIMD the baseline equilibrium kernel must fit (two 12-wave blocks per CU)
 #endif
 constexpr int HZ_BLOCK = 256;
-constexpr int HZ_CHUNK = 16;
+constexpr int HZ_LDS = 1024; // τ̄ knots per LDS chunk of the hazard kernel
+constexpr int HZ_REG = 16;   // τ̄ knots per thread held in registers (ntau <= 4096: one pass over HBM)
 constexpr int EQ_TILE = 4096;  // u values per equilibrium block (one block per β column up to this)
 #ifndef SBR_AW_WIN
 #define SBR_AW_WIN 6
 #endif
 constexpr int kAwWin = SBR_AW_WIN; // 8-blocks each side of the predicted AW peak evaluated first
 
+// I_k = I_{k-1} + term_k over s_I[0, cn) in place, left to right (the reference's rounding
+// order), by the 64 lanes of one wave: lane l holds terms [16l, 16l + 16) in registers and
+// the running integral passes from lane to lane — in round r only lane r adds (16 dependent
+// adds), then v_readlane broadcasts its I.  The chain is the adds plus one broadcast per 16
+// terms; a one-lane scan out of LDS waits on an LDS round trip every few terms instead.
+// Call with all 64 lanes of the wave active; I must be wave-uniform (and is on return).
+constexpr int HZ_LANE = HZ_LDS / 64; // terms per lane (16)
+__device__ __forceinline__ double hz_bcast(double x, int lane)
+{
+    const uint64_t u = sbr_dbits(x);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, lane);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), lane);
+    return sbr_bitsd(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ void hz_scan_wave(double* s_I, int cn, double& I)
+{
+    const int lane = threadIdx.x & 63, base = lane * HZ_LANE;
+    double v[HZ_LANE];
+#pragma unroll
+    for (int j = 0; j < HZ_LANE; j++) v[j] = base + j < cn ? s_I[base + j] : 0.0;
+    const int rounds = (cn + HZ_LANE - 1) / HZ_LANE;
+    double acc = I;
+    for (int r = 0; r < rounds; r++) {
+        if (lane == r) {
+            // the tail past cn adds +0.0, which leaves I (>= +0) unchanged
+#pragma unroll
+            for (int j = 0; j < HZ_LANE; j++) { acc = acc + v[j]; v[j] = acc; }
+        }
+        acc = hz_bcast(acc, r);
+    }
+    I = acc;
+#pragma unroll
+    for (int j = 0; j < HZ_LANE; j++)
+        if (base + j < cn) s_I[base + j] = v[j];
+}
+
+#ifdef SBR_HZ_PROF // per-block phase cycles of the hazard kernel (tools/ubench_hazard.hip)
+__device__ long long g_hzprof[8192 * 6];
+#define HZ_T0 long long hz_tp = __builtin_amdgcn_s_memtime()
+#define HZ_STAMP(ph)                                                                                  \
+    do {                                                                                              \
+        const long long hz_now = __builtin_amdgcn_s_memtime();                                        \
+        if (threadIdx.x == 0) g_hzprof[(size_t)blockIdx.x * 6 + (ph)] += hz_now - hz_tp;              \
+        hz_tp = hz_now;                                                                               \
+    } while (0)
+#else
+#define HZ_T0
+#define HZ_STAMP(ph)
+#endif
 __global__ __launch_bounds__(HZ_BLOCK) void hazard_kernel(const double* __restrict__ beta,
                                                           const double* __restrict__ eta, LearnArgs a, LearnBufs L)
 {
-    // Trapezoid terms, then I, go to the column's HBM scratch row (L2-resident
-    // while the block runs): no LDS, so hazard blocks of the next batch can share
-    // CUs with an equilibrium kernel that holds all of their LDS.
-    __shared__ int s_m;
+    // The τ̄ grid in chunks of HZ_LDS knots: e_i·g_i and the trapezoid terms are formed in
+    // parallel into LDS, one thread adds the terms left to right (the reference's rounding
+    // order) out of LDS, and the partial integrals I_i are parked in the HR row; a last
+    // parallel pass turns them into HR_i.  24 KiB of LDS per block, so hazard blocks of the
+    // next batch still fit beside two equilibrium blocks on a CU.
+    __shared__ double s_eg[HZ_LDS + 1]; // s_eg[k + 1] = e·g of knot c0 + k; s_eg[0] that of knot c0 − 1
+    __shared__ double s_t[HZ_LDS + 1];  // τ̄ likewise
+    __shared__ double s_I[HZ_LDS];
+    __shared__ double s_Ieta;
 #ifndef SBR_HZ_NOPRIO
     __builtin_amdgcn_s_setprio(3);
 #endif
+    HZ_T0;
     const int b = blockIdx.x;
     const int n = L.n_knots[b];
     const uint32_t st = L.status[b];
@@ -136,17 +195,7 @@ __global__ __launch_bounds__(HZ_BLOCK) void hazard_kernel(const double* __restri
     const double* __restrict__ Gv = L.G + row;
     double* __restrict__ H = L.hr + row;
     const double BETA = beta[b], ETA = eta[b], p = a.p, lam = a.lam;
-    if (threadIdx.x == 0) { // m = #knots ≤ η (sorted: searchsortedlast + 1)
-        int lo = 0, hi = n;
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (T[mid] <= ETA) lo = mid + 1;
-            else hi = mid;
-        }
-        s_m = lo;
-    }
-    __syncthreads();
-    const int m = s_m;
+    const int m = L.n_le[b]; // #knots ≤ η (searchsortedlast + 1), counted by the learning kernel
     bool oob = false, push;
     if (m < n) {
         push = (m == 0) || T[m - 1] != ETA; // solver.jl:159
@@ -156,7 +205,6 @@ __global__ __launch_bounds__(HZ_BLOCK) void hazard_kernel(const double* __restri
         oob = push;                           // no knot beyond η to interpolate pdf(η)
     }
     const int ntau = m + (push ? 1 : 0);
-    double* __restrict__ term = L.hrI + row;
     if (oob) {
         if (threadIdx.x == 0) {
             L.status[b] = st | SBR_OOB;
@@ -165,7 +213,6 @@ __global__ __launch_bounds__(HZ_BLOCK) void hazard_kernel(const double* __restri
         }
         return;
     }
-    // e_i and the numerator (p·E_i)·pdf_i; the trapezoid term of i pairs e_{i-1}, e_i
     auto pdf_at = [&](int i) -> double {
         if (i < m) { const double x = Gv[i]; return (BETA * x) * (1.0 - x); }
         // η on bracket [m-1, m]
@@ -175,44 +222,130 @@ __global__ __launch_bounds__(HZ_BLOCK) void hazard_kernel(const double* __restri
         return g0 * (1.0 - d) + g1 * d;
     };
     auto tau_at = [&](int i) -> double { return i < m ? T[i] : ETA; };
-    for (int i = threadIdx.x; i < ntau; i += HZ_BLOCK) {
-        const double ti = tau_at(i);
-        const double E = sbr_exp(lam * ti);
-        const double g = pdf_at(i);
-        H[i] = (p * E) * g;
-        if (i > 0) {
-            const double tp = tau_at(i - 1);
-            const double ep = sbr_exp(lam * tp) * pdf_at(i - 1);
-            term[i] = (0.5 * (ep + E * g)) * (ti - tp);
-        } else {
-            term[0] = 0.0;
+    // Global reads are batched (unrolled loops, every load of a batch in flight before the
+    // first use): the knots were written by another XCD's learning wave, so each one costs an
+    // L2 miss, and one dependent miss per knot per thread would dominate the kernel.
+    HZ_STAMP(0);
+    if (ntau <= HZ_BLOCK * HZ_REG) {
+        // Every τ̄ knot of the column in registers (thread tid owns knots tid + 256·j): one
+        // batch of global loads, the chunks fed to LDS from registers, I_i read back into
+        // registers, HR written once.
+        double tv[HZ_REG], egv[HZ_REG], numv[HZ_REG], iv[HZ_REG], gk[HZ_REG];
+        // loads first, unconditionally (indices clamped into the knots ≤ η), so that all of
+        // them are in flight at once; τ̄ = η and its interpolated pdf are selected after
+        const double pdf_eta = m < n ? pdf_at(m) : 0.0; // m == n: η is a knot, not pushed
+#pragma unroll
+        for (int j = 0; j < HZ_REG; j++) {
+            const int i = threadIdx.x + HZ_BLOCK * j;
+            const int ic = i < m ? i : m - 1;
+            tv[j] = T[ic];
+            gk[j] = Gv[ic];
         }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) { // I_i = I_{i-1} + term_i, left to right (solver.jl:173-175)
-        // The chain of adds is inherently serial (reassociating would change the
-        // rounding); load HZ_CHUNK terms per round so only the adds are dependent.
+#pragma unroll
+        for (int j = 0; j < HZ_REG; j++) {
+            const int i = threadIdx.x + HZ_BLOCK * j;
+            const double x = gk[j];
+            const double ti = i < m ? tv[j] : ETA;
+            const double g = i < m ? (BETA * x) * (1.0 - x) : pdf_eta;
+            const double E = sbr_exp(lam * ti);
+            tv[j] = ti;
+            egv[j] = E * g;        // e_i = exp(λτ̄_i)·pdf_i
+            numv[j] = (p * E) * g; // the HR numerator (p·exp(λτ̄_i))·pdf_i
+            iv[j] = 0.0;
+        }
         double I = 0.0;
-        int i0 = 1;
-        for (; i0 + HZ_CHUNK <= ntau; i0 += HZ_CHUNK) {
-            double v[HZ_CHUNK];
+        constexpr int RPC = HZ_LDS / HZ_BLOCK; // register slots per LDS chunk
 #pragma unroll
-            for (int k = 0; k < HZ_CHUNK; k++) v[k] = term[i0 + k];
+        for (int c = 0; c < HZ_REG / RPC; c++) {
+            const int c0 = c * HZ_LDS;
+            if (c0 < ntau) { // uniform
+                const int cn = ntau - c0 < HZ_LDS ? ntau - c0 : HZ_LDS;
 #pragma unroll
-            for (int k = 0; k < HZ_CHUNK; k++) { I = I + v[k]; v[k] = I; }
+                for (int r = 0; r < RPC; r++) {
+                    const int k = threadIdx.x + HZ_BLOCK * r;
+                    s_t[k + 1] = tv[c * RPC + r];
+                    s_eg[k + 1] = egv[c * RPC + r];
+                }
+                if (c > 0 && threadIdx.x == HZ_BLOCK - 1) { // knot c0 − 1 is this thread's last slot
+                    s_t[0] = tv[c * RPC - 1];
+                    s_eg[0] = egv[c * RPC - 1];
+                }
+                __syncthreads();
+                HZ_STAMP(1);
+                for (int k = threadIdx.x; k < cn; k += HZ_BLOCK)
+                    s_I[k] = c0 + k == 0 ? 0.0 : (0.5 * (s_eg[k] + s_eg[k + 1])) * (s_t[k + 1] - s_t[k]);
+                __syncthreads();
+                HZ_STAMP(2);
+                if (threadIdx.x < 64) hz_scan_wave(s_I, cn, I);
+                __syncthreads();
+                HZ_STAMP(3);
 #pragma unroll
-            for (int k = 0; k < HZ_CHUNK; k++) term[i0 + k] = v[k];
+                for (int r = 0; r < RPC; r++) {
+                    const int k = threadIdx.x + HZ_BLOCK * r;
+                    if (k < cn) iv[c * RPC + r] = s_I[k];
+                }
+                __syncthreads(); // the chunk's LDS is reused
+                HZ_STAMP(4);
+            }
         }
-        for (int i = i0; i < ntau; i++) {
-            I = I + term[i];
-            term[i] = I;
+        if (threadIdx.x == 0) {
+            s_Ieta = I;
+            L.n_tau[b] = ntau;
+            L.n_le[b] = m;
         }
+        __syncthreads();
+        const double Ieta = s_Ieta, omp = 1.0 - p;
+#pragma unroll
+        for (int j = 0; j < HZ_REG; j++) {
+            const int i = threadIdx.x + HZ_BLOCK * j;
+            if (i < ntau) H[i] = numv[j] / ((p * iv[j]) + (omp * Ieta));
+        }
+        HZ_STAMP(5);
+        return;
+    }
+    double I = 0.0, egprev = 0.0, tprev = 0.0; // thread 0: running integral; the chunk's last e·g, τ̄
+    for (int c0 = 0; c0 < ntau; c0 += HZ_LDS) {
+        const int cn = ntau - c0 < HZ_LDS ? ntau - c0 : HZ_LDS;
+        if (threadIdx.x == 0) { s_eg[0] = egprev; s_t[0] = tprev; }
+#pragma unroll 4
+        for (int k = threadIdx.x; k < cn; k += HZ_BLOCK) {
+            const int i = c0 + k;
+            const double ti = tau_at(i);
+            s_t[k + 1] = ti;
+            s_eg[k + 1] = sbr_exp(lam * ti) * pdf_at(i); // e_i = exp(λτ̄_i)·pdf_i
+        }
+        __syncthreads();
+        HZ_STAMP(1);
+        // trapezoid term of i pairs e_{i-1}, e_i (solver.jl:173-175); term_0 = 0
+        for (int k = threadIdx.x; k < cn; k += HZ_BLOCK)
+            s_I[k] = c0 + k == 0 ? 0.0 : (0.5 * (s_eg[k] + s_eg[k + 1])) * (s_t[k + 1] - s_t[k]);
+        __syncthreads();
+        HZ_STAMP(2);
+        if (threadIdx.x < 64) hz_scan_wave(s_I, cn, I); // I_i = I_{i-1} + term_i, left to right
+        if (threadIdx.x == 0) {
+            egprev = s_eg[cn];
+            tprev = s_t[cn];
+        }
+        __syncthreads();
+        HZ_STAMP(3);
+        for (int k = threadIdx.x; k < cn; k += HZ_BLOCK) H[c0 + k] = s_I[k]; // I_i parked in the HR row
+        __syncthreads(); // the chunk's LDS is reused
+        HZ_STAMP(4);
+    }
+    if (threadIdx.x == 0) {
+        s_Ieta = I;
         L.n_tau[b] = ntau;
         L.n_le[b] = m;
     }
     __syncthreads();
-    const double Ieta = term[ntau - 1], omp = 1.0 - p;
-    for (int i = threadIdx.x; i < ntau; i += HZ_BLOCK) H[i] = H[i] / ((p * term[i]) + (omp * Ieta));
+    // HR_i = (p·exp(λτ̄_i))·pdf_i / (p·I_i + (1 − p)·I_η); each thread reads back the I_i it parked
+    const double Ieta = s_Ieta, omp = 1.0 - p;
+#pragma unroll 4
+    for (int i = threadIdx.x; i < ntau; i += HZ_BLOCK) {
+        const double E = sbr_exp(lam * tau_at(i));
+        H[i] = ((p * E) * pdf_at(i)) / ((p * H[i]) + (omp * Ieta));
+    }
+    HZ_STAMP(5);
 }
 
 // ============================================================================

@@ -195,7 +195,7 @@ int ensure_learn(sbr_ctx* c, size_t n_beta, size_t cap, int slot = 0)
     HIP_TRY(c, hipMalloc(&L.t, slab), SBR_ENOMEM);
     HIP_TRY(c, hipMalloc(&L.G, slab), SBR_ENOMEM);
     HIP_TRY(c, hipMalloc(&L.hr, slab), SBR_ENOMEM);
-    HIP_TRY(c, hipMalloc(&L.hrI, slab), SBR_ENOMEM);
+    L.hrI = nullptr; // the hazard kernel scans in LDS (no HBM scratch row)
     HIP_TRY(c, hipMalloc(&L.n_knots, n_beta * 4), SBR_ENOMEM);
     HIP_TRY(c, hipMalloc(&L.n_tau, n_beta * 4), SBR_ENOMEM);
     HIP_TRY(c, hipMalloc(&L.n_le, n_beta * 4), SBR_ENOMEM);
@@ -395,6 +395,42 @@ int launch_eq(sbr_ctx* c, hipStream_t s, const sbr::LearnBufs& L, const double* 
     return SBR_OK;
 }
 
+// highest-priority learning streams + events of the pipelined batch sweeps
+int ensure_pipe_streams(sbr_ctx* c)
+{
+    if (c->lstream[0]) return SBR_OK;
+    int lo = 0, hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&lo, &hi); // hi = greatest priority
+    for (int k = 0; k < sbr_ctx::kLearnSlots; k++) {
+        HIP_TRY(c, hipStreamCreateWithPriority(&c->lstream[k], hipStreamNonBlocking, SBR_LEARN_PRIO_HI ? hi : lo), SBR_EDEVICE);
+        HIP_TRY(c, hipEventCreateWithFlags(&c->ev_learned[k], SBR_SYNC_EVENT_FLAGS), SBR_EDEVICE);
+        HIP_TRY(c, hipEventCreateWithFlags(&c->ev_eq[k], SBR_SYNC_EVENT_FLAGS), SBR_EDEVICE);
+    }
+    HIP_TRY(c, hipEventCreateWithFlags(&c->ev_in, SBR_SYNC_EVENT_FLAGS), SBR_EDEVICE);
+    return SBR_OK;
+}
+
+// the learning buffers / results of columns [c0, ...) of a sweep (row views)
+sbr::LearnBufs learn_rows(const sbr::LearnBufs& L, size_t c0)
+{
+    const size_t k = c0 * (size_t)L.cap;
+    return {L.t + k,        L.G + k,        L.hr + k,     L.hrI + k,         L.n_knots + c0, L.n_tau + c0,
+            L.n_le + c0,    L.status + c0,  L.n_accept + c0, L.n_reject + c0, L.cap};
+}
+sbr::ResultSoA result_rows(const sbr::ResultSoA& r, size_t off)
+{
+    auto at = [off](auto* p) { return p ? p + off : p; };
+    return {at(r.xi), at(r.tau_in_unc), at(r.tau_out_unc), at(r.aw_max), at(r.tol), at(r.status), at(r.iters)};
+}
+
+// One sweep.  Every learning column is a serial ODE on one lane, and the launch lasts as long
+// as its slowest column (config 3: one column takes 4.4k steps where the median takes 2.9k),
+// while the equilibrium stage is a throughput kernel over the whole chip.  Wide sweeps are
+// therefore cut into kSweepChunks column chunks, each learned and solved on its own learning
+// stream: the equilibria of the chunks that finish learning early run while the slowest
+// chunk is still integrating.  Timing records: kind 0 = the learning stage of all chunks
+// (fork to the last chunk learned), kind 1 = the equilibrium tail after it.
+constexpr int kSweepChunks = sbr_ctx::kLearnSlots;
 int run_baseline(sbr_ctx* c, hipStream_t s, const double* beta, const double* eta, const double* t_end, double x0,
                  const double* u, int64_t n_beta, int64_t n_u, double p, double kappa, double lambda,
                  const sbr_opts& o, const sbr::ResultSoA& out, double* aw_path)
@@ -403,10 +439,52 @@ int run_baseline(sbr_ctx* c, hipStream_t s, const double* beta, const double* et
     if (rc) return rc;
     c->last_slot = 0;
     sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, p, lambda, o.ode_maxiters, (int32_t)n_beta, 1, 0};
+    if (aw_path || n_beta < 64 * kSweepChunks) {
+        hipEvent_t t0 = tstart(c, s);
+        HIP_TRY(c, sbr::launch_learn_logistic(beta, eta, t_end, la, c->LW[0], s), SBR_EDEVICE);
+        tend(c, s, 0, t0);
+        return launch_eq(c, s, c->LW[0], eta, t_end, u, n_beta, n_u, kappa, o, out, aw_path);
+    }
+    rc = ensure_pipe_streams(c);
+    if (rc) return rc;
+    // chunk boundaries on whole waves (64 columns), halving towards the front: the last chunk
+    // gets half of the columns, the others 1/4, 1/8, ...  The longest learning columns of a
+    // β-descending grid (Fig 5: large β, outliers of up to 1.5x the median steps) sit in the
+    // front chunks, whose equilibria, last to start, then fill one round of workgroups.
+    const int64_t waves = (n_beta + 63) / 64;
+    int64_t lo[kSweepChunks + 1];
+    lo[0] = 0;
+    lo[kSweepChunks] = n_beta;
+    for (int k = kSweepChunks - 1; k >= 1; k--) {
+        const int64_t wk = waves >> (kSweepChunks - k); // waves before chunk k
+        lo[k] = std::min<int64_t>(n_beta, std::max<int64_t>(wk * 64, (int64_t)k * 64));
+    }
+    HIP_TRY(c, hipEventRecord(c->ev_in, s), SBR_EDEVICE);
     hipEvent_t t0 = tstart(c, s);
-    HIP_TRY(c, sbr::launch_learn_logistic(beta, eta, t_end, la, c->LW[0], s), SBR_EDEVICE);
+    for (int k = 0; k < kSweepChunks; k++) {
+        hipStream_t ls = c->lstream[k];
+        const int64_t c0 = lo[k], nb = lo[k + 1] - lo[k];
+        HIP_TRY(c, hipStreamWaitEvent(ls, c->ev_in, 0), SBR_EDEVICE);
+        if (nb <= 0) continue;
+        sbr::LearnArgs lk = la;
+        lk.n_beta = (int32_t)nb;
+        const sbr::LearnBufs Lk = learn_rows(c->LW[0], (size_t)c0);
+        HIP_TRY(c, sbr::launch_learn_logistic(beta + c0, eta + c0, t_end + c0, lk, Lk, ls), SBR_EDEVICE);
+        HIP_TRY(c, hipEventRecord(c->ev_learned[k], ls), SBR_EDEVICE);
+        sbr::EqArgs ea{kappa, (int32_t)n_u, o.bisect_max_iters, c->lds_cap_b, nullptr,
+                       (o.flags & SBR_FLAG_EXHAUSTIVE) ? 1 : 0, (o.flags >> 8) & 7};
+        HIP_TRY(c, sbr::launch_equilibrium(Lk, eta + c0, t_end + c0, u, ea, result_rows(out, (size_t)(c0 * n_u)),
+                                           (int)nb, ls), SBR_EDEVICE);
+        HIP_TRY(c, hipEventRecord(c->ev_eq[k], ls), SBR_EDEVICE);
+    }
+    for (int k = 0; k < kSweepChunks; k++)
+        if (lo[k + 1] > lo[k]) HIP_TRY(c, hipStreamWaitEvent(s, c->ev_learned[k], 0), SBR_EDEVICE);
+    hipEvent_t t1 = tstart(c, s);
     tend(c, s, 0, t0);
-    return launch_eq(c, s, c->LW[0], eta, t_end, u, n_beta, n_u, kappa, o, out, aw_path);
+    for (int k = 0; k < kSweepChunks; k++)
+        if (lo[k + 1] > lo[k]) HIP_TRY(c, hipStreamWaitEvent(s, c->ev_eq[k], 0), SBR_EDEVICE);
+    tend(c, s, 1, t1);
+    return SBR_OK;
 }
 
 int run_interest(sbr_ctx* c, hipStream_t s, const double* beta, const double* eta, const double* t_end, double x0,
@@ -608,20 +686,6 @@ int sbr_sweep_baseline_dev(sbr_ctx* c, void* stream, const double* beta, const d
 #endif
 static int het_lds(const sbr_ctx* c) { return c->lds_cap * 3 < SBR_HET_LDS ? c->lds_cap * 3 : SBR_HET_LDS; }
 
-// highest-priority learning streams + events of the pipelined batch sweeps
-int ensure_pipe_streams(sbr_ctx* c)
-{
-    if (c->lstream[0]) return SBR_OK;
-    int lo = 0, hi = 0;
-    (void)hipDeviceGetStreamPriorityRange(&lo, &hi); // hi = greatest priority
-    for (int k = 0; k < sbr_ctx::kLearnSlots; k++) {
-        HIP_TRY(c, hipStreamCreateWithPriority(&c->lstream[k], hipStreamNonBlocking, SBR_LEARN_PRIO_HI ? hi : lo), SBR_EDEVICE);
-        HIP_TRY(c, hipEventCreateWithFlags(&c->ev_learned[k], SBR_SYNC_EVENT_FLAGS), SBR_EDEVICE);
-        HIP_TRY(c, hipEventCreateWithFlags(&c->ev_eq[k], SBR_SYNC_EVENT_FLAGS), SBR_EDEVICE);
-    }
-    HIP_TRY(c, hipEventCreateWithFlags(&c->ev_in, SBR_SYNC_EVENT_FLAGS), SBR_EDEVICE);
-    return SBR_OK;
-}
 
 int sbr_sweep_baseline_batch_dev(sbr_ctx* c, void* stream, int64_t n_batch, const double* beta, const double* eta,
                                  const double* t_end, double x0, const double* u, int64_t n_beta, int64_t n_u,
