@@ -274,15 +274,23 @@ def main():
             "parallelism": f"beta-column shards x{world}",
             "pipelined": pipe,
         },
-        "kernel_ms_per_step": {"learn_logistic": learn_ms / max(ncalls, 1), "equilibrium": eq_ms / max(ncalls, 1)},
+        # pipelined: per-launch kernel times (HIP events around each launch on its stream);
+        # single sweep: libsbr cuts the grid into column chunks whose kernels overlap, so the
+        # events give the learning stage's wall time and the equilibrium tail after it
+        "kernel_ms_per_step": ({"learn_logistic": learn_ms / max(ncalls, 1), "equilibrium": eq_ms / max(ncalls, 1)}
+                               if pipe else
+                               {"learning_stage_wall": learn_ms / max(ncalls, 1),
+                                "equilibrium_tail_after_learning": eq_ms / max(ncalls, 1)}),
         "flops_per_step": {"equilibrium": f_eq, "learn": f_learn},
         "work_per_step": {"run_points": int(run.sum()), "bisect_iters": int(iters.sum()),
                           "aw_knots_run": int((run * n_tau[:, None]).sum()),
                           "rk_steps": int((ls["n_accept"] + ls["n_reject"]).sum())},
-        "roofline": roofline("equilibrium_kernel", f_eq, eq_s, traffic,
-                             executed_fp64("equilibrium_kernel<", f"fig5_{n}x{n}")),
+        "roofline": (roofline("equilibrium_kernel", f_eq, eq_s, traffic,
+                              executed_fp64("equilibrium_kernel<", f"fig5_{n}x{n}")) if pipe else None),
         "libsbr_sha16": lib_sha(),
     }
+    if not pipe:
+        res["roofline_note"] = "single-sweep mode: chunked kernels overlap; the roofline line is the pipelined default run's"
     if a.phases:
         res["eq_phase_ms"] = phase_breakdown(eng, beta[0], eta[0], t_end[0], u, p, kappa, lam, x0,
                                              {k: v[0] for k, v in out.items()}, stream, dev)
@@ -679,24 +687,35 @@ def main_social(a):
 
 def phase_breakdown(eng, beta, eta, t_end, u, p, kappa, lam, x0, out, stream, dev, reps=3):
     """Equilibrium-kernel time when every point stops after the crossing scan,
-    after the bisection, and in full; plus AW blocks evaluated per run point."""
+    after the bisection, and in full; plus AW blocks evaluated per run point.  Runs
+    through the batch entry point with one grid: its timing events bracket the
+    equilibrium launch itself (a single sweep is chunked, see kernel_ms_per_step)."""
     from sbr import _lib
     res = {}
+    b2, e2, t2 = beta[None, :], eta[None, :], t_end[None, :]
+    o2 = {k: v[None, :] for k, v in out.items()}
+
+    class _One:  # sweep_baseline_dev-shaped adapter over the one-grid batch call
+        @staticmethod
+        def sweep_baseline_dev(beta, eta, t_end, u, p, kappa, lam, x0, out, stream=None, exhaustive=False, flags=0):
+            fl = flags | (_lib.SBR_FLAG_EXHAUSTIVE if exhaustive else 0)
+            eng.sweep_baseline_batch_dev(b2, e2, t2, u, p, kappa, lam, x0, o2, stream=stream, flags=fl)
+    eng_one = _One()
     for name, fl in (("buffer", _lib.SBR_FLAG_DIAG_STOP_AFTER_BUFFER), ("bisect", _lib.SBR_FLAG_DIAG_STOP_AFTER_BISECT),
                      ("full", 0), ("full_exhaustive_aw", -1)):
         kw = dict(exhaustive=True) if fl == -1 else dict(flags=fl)
-        eng.sweep_baseline_dev(beta, eta, t_end, u, p, kappa, lam, x0, out, stream=stream, **kw)
+        eng_one.sweep_baseline_dev(beta, eta, t_end, u, p, kappa, lam, x0, out, stream=stream, **kw)
         torch.cuda.synchronize(dev)
         eng.timing_read(stream)
         eng.timing_enable(True)
         for _ in range(reps):
-            eng.sweep_baseline_dev(beta, eta, t_end, u, p, kappa, lam, x0, out, stream=stream, **kw)
+            eng_one.sweep_baseline_dev(beta, eta, t_end, u, p, kappa, lam, x0, out, stream=stream, **kw)
         torch.cuda.synchronize(dev)
         _, eq_ms, nc = eng.timing_read(stream)
         eng.timing_enable(False)
         res[name] = eq_ms / max(nc, 1)
-    eng.sweep_baseline_dev(beta, eta, t_end, u, p, kappa, lam, x0, out, stream=stream,
-                           flags=_lib.SBR_FLAG_DIAG_COUNT_AW_BLOCKS)
+    eng_one.sweep_baseline_dev(beta, eta, t_end, u, p, kappa, lam, x0, out, stream=stream,
+                               flags=_lib.SBR_FLAG_DIAG_COUNT_AW_BLOCKS)
     torch.cuda.synchronize(dev)
     st = out["status"].cpu().numpy().view(np.uint32)
     nb = out["iters"].cpu().numpy()[(st & sbr.STATUS["SBR_RUN"]) > 0]

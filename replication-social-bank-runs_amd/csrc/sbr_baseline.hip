@@ -26,15 +26,20 @@ namespace sbr {
 // ============================================================================
 // Learning kernel
 // ============================================================================
-__global__ __launch_bounds__(64) void learn_logistic_kernel(const double* __restrict__ beta,
+#ifndef SBR_LEARN_BLOCK
+#define SBR_LEARN_BLOCK 64
+#endif
+__global__ __launch_bounds__(SBR_LEARN_BLOCK) void learn_logistic_kernel(const double* __restrict__ beta,
                                                             const double* __restrict__ eta,
                                                             const double* __restrict__ t_end, LearnArgs a,
                                                             LearnBufs L)
 {
     // latency-bound (one serial ODE per lane): take issue priority over co-resident
     // equilibrium waves of a previous batch
+#ifndef SBR_LEARN_NOPRIO
     __builtin_amdgcn_s_setprio(3);
-    const int b = blockIdx.x * 64 + threadIdx.x;
+#endif
+    const int b = blockIdx.x * SBR_LEARN_BLOCK + threadIdx.x;
     if (b >= a.n_beta) return;
     const double BETA = beta[b], ETA = eta[b], T1 = t_end[b], T0 = 0.0;
     const size_t row = (size_t)b * (size_t)L.cap;
@@ -749,6 +754,7 @@ struct ValueRhs {
         if (ntau >= 2 && t >= tlo && t <= thi) jb = ssl_gallop(tau, ntau, jb, t);
     }
     static constexpr bool kFsalExact = false;
+    static constexpr bool kPinTableau = false;
 };
 
 // The value function saved on the HR grid (saveat) streamed into optimal_buffer
@@ -1060,8 +1066,8 @@ __global__ __launch_bounds__(BLOCK, INTEREST ? 1 : SBR_EQ_MINW) void equilibrium
 hipError_t launch_learn_logistic(const double* beta, const double* eta, const double* t_end, const LearnArgs& a,
                                  const LearnBufs& L, hipStream_t s)
 {
-    dim3 grid((a.n_beta + 63) / 64);
-    hipLaunchKernelGGL(learn_logistic_kernel, grid, dim3(64), 0, s, beta, eta, t_end, a, L);
+    dim3 grid((a.n_beta + SBR_LEARN_BLOCK - 1) / SBR_LEARN_BLOCK);
+    hipLaunchKernelGGL(learn_logistic_kernel, grid, dim3(SBR_LEARN_BLOCK), 0, s, beta, eta, t_end, a, L);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(hazard_kernel, dim3(a.n_beta), dim3(HZ_BLOCK), 0, s, beta,

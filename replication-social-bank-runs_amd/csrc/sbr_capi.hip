@@ -717,7 +717,11 @@ int sbr_sweep_baseline_batch_dev(sbr_ctx* c, void* stream, int64_t n_batch, cons
         for (int64_t k = 0; k < n_batch; k++) {
             const int slot = (int)(k % nslot);
             hipStream_t es = s; // one equilibrium stream (two alternating: 15% slower, r01_ab27)
+#ifdef SBR_AB_PIPE_SERIAL // A/B only: learning on the equilibrium stream (no overlap)
+            hipStream_t ls = s;
+#else
             hipStream_t ls = c->lstream[slot];
+#endif
             const double* bk = beta + k * n_beta;
             const double* ek = eta + k * n_beta;
             const double* tk = t_end + k * n_beta;

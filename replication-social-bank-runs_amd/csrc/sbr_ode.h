@@ -119,6 +119,7 @@ struct LogisticSys {
     // the f(t, x) that initialize! re-evaluates after a switch: the same expression on the
     // same x (autonomous), so the re-evaluation is skipped
     static constexpr bool kFsalExact = true;
+    static constexpr bool kPinTableau = true;
 };
 
 // ode_determine_initdt for a scalar ODE (order 5: dt₁ = (0.01/max(d₁,d₂))^(1/6));
@@ -191,6 +192,42 @@ struct Tsit5Regs {
     }
 };
 
+// Literal tableau (no VGPRs held): for right-hand sides that need the registers more
+// (lookup-heavy social / value-function RHS, which run near the 256-VGPR ceiling).
+struct Tsit5Lits {
+    static constexpr double a31 = A31;
+    static constexpr double a32 = A32;
+    static constexpr double a41 = A41;
+    static constexpr double a42 = A42;
+    static constexpr double a43 = A43;
+    static constexpr double a51 = A51;
+    static constexpr double a52 = A52;
+    static constexpr double a53 = A53;
+    static constexpr double a54 = A54;
+    static constexpr double a61 = A61;
+    static constexpr double a62 = A62;
+    static constexpr double a63 = A63;
+    static constexpr double a64 = A64;
+    static constexpr double a65 = A65;
+    static constexpr double a71 = A71;
+    static constexpr double a72 = A72;
+    static constexpr double a73 = A73;
+    static constexpr double a74 = A74;
+    static constexpr double a75 = A75;
+    static constexpr double a76 = A76;
+    static constexpr double bt1 = BT1;
+    static constexpr double bt2 = BT2;
+    static constexpr double bt3 = BT3;
+    static constexpr double bt4 = BT4;
+    static constexpr double bt5 = BT5;
+    static constexpr double bt6 = BT6;
+    static constexpr double bt7 = BT7;
+};
+template <bool PIN>
+struct Tsit5Tab : Tsit5Regs {};
+template <>
+struct Tsit5Tab<false> : Tsit5Lits {};
+
 // Scalar AutoTsit5(Rosenbrock23()) on (0, T1) from x0.  Sys provides
 //   double eval(double t, double x)                       f at any (t, x)
 //   void   prepare(double t, double dt)                   before the Tsit5 stages of a step
@@ -198,6 +235,7 @@ struct Tsit5Regs {
 //   void   jac(double t, double x, double& J, double& dT) ForwardDiff ∂f/∂x, ∂f/∂t
 //   void   accepted(double t)                             after an accepted step
 //   static constexpr bool kFsalExact                      f(t, x) == the carried k1 bit for bit
+//   static constexpr bool kPinTableau                     hold the Tsit5 tableau in VGPRs (Tsit5Regs)
 // Sink provides
 //   bool start(double t0, double x0)                      the first knot; false = stop
 //   bool step(bool acc, double tprev, double tn, double dt, double y0, double y1, const StepK& k, bool exact)
@@ -221,7 +259,7 @@ __device__ __forceinline__ void ode_scalar(Sys& f, Sink& sink, double T1, double
     double eig = 1.0; // integrator.eigen_est = 1/oneunit(t) at init
     PIControl pc;
     AutoSwitch as;
-    const Tsit5Regs cf;
+    const Tsit5Tab<Sys::kPinTableau> cf;
     if (!sink.start(t, x)) return;
     if (!(t < T1)) return;
     if (maxiters < 1) { o.status |= SBR_ODE_MAXITERS; return; }

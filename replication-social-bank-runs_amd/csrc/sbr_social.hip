@@ -272,6 +272,7 @@ struct SocialRhs {
         if (n >= 2 && t >= tfirst && t <= tlast) (void)w.find_advance(t);
     }
     static constexpr bool kFsalExact = false;
+    static constexpr bool kPinTableau = false;
 };
 
 }  // namespace
