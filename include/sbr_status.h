@@ -24,7 +24,7 @@
 #define SBR_SKIPPED_EARLY_EXIT  0x0100u /* 5-consecutive-NaN rule (1_baseline.jl:236-244)      */
 #define SBR_ODE_MAXITERS        0x0200u /* integrator hit maxiters (default 1e6, see below)    */
 #define SBR_ARG_INVALID         0x0400u /* parameter validation failed (model.jl:31-35,71-76)  */
-#define SBR_STIFF_SWITCH        0x0800u /* AutoSwitch would have moved to Rosenbrock23         */
+#define SBR_STIFF_SWITCH        0x0800u /* AutoSwitch moved to Rosenbrock23 (handled, info)   */
 #define SBR_SOCIAL_NOT_CONVERGED 0x1000u /* fixed point hit max_iter / stopped (social :390)   */
 #define SBR_KNOT_OVERFLOW       0x2000u /* engine knot capacity exceeded (engine limit)        */
 #define SBR_ODE_FAILED          0x4000u /* non-finite step size / state                        */

@@ -9,14 +9,17 @@
  *   learning   src/baseline/learning.jl:41-54 (solve_SIhomogeneous),
  *              :161-173 (compute_pdf_symbolic_baseline)
  *   ODE solver OrdinaryDiffEq 6.102.1 AutoTsit5(Rosenbrock23()) (Manifest.toml
- *              :1493-1497, Tsit5 1.5.0 :1679-1683) — NOT vendored in the
- *              reference; restated from the published Tsit5 method
- *              (Tsitouras 2011 tableau), OrdinaryDiffEq's PI controller
- *              defaults (beta1=7/50, beta2=2/25, qmin=1/5, qmax=10,
- *              gamma=9/10, qoldinit=1e-4), its Hairer-style initial dt and its
- *              save_everystep knot semantics.  The AutoSwitch stiffness test
- *              is evaluated and reported (SBR_STIFF_SWITCH) but Rosenbrock23 is
- *              not restated: on every configured grid the test never fires.
+ *              :1493-1497, Tsit5 1.5.0 :1679-1683, Rosenbrock 1.18.1
+ *              :1643-1647) — NOT vendored in the reference; restated from the
+ *              published methods: Tsit5 (Tsitouras 2011 tableau), Rosenbrock23
+ *              (W-method, generic_lufact!/getrs, its error estimate and dense
+ *              output), AutoSwitch's switch / switch-back (maxstiffstep 10,
+ *              maxnonstiffstep 3, tolerances 9/10, dtfac 2), the PI controller
+ *              (beta1=7/50, beta2=2/25, qmin=1/5, qmax=10, gamma=9/10,
+ *              qoldinit=1e-4) with FastPower 1.1.3 fastpower (Manifest.toml
+ *              :675-678), the Hairer-style initial dt and save_everystep
+ *              knot semantics.  SBR_STIFF_SWITCH reports that the stiff
+ *              branch ran (handled).
  *   hazard     src/baseline/solver.jl:153-185
  *   buffers    src/baseline/solver.jl:211-264
  *   bisection  src/baseline/solver.jl:308-376
