@@ -267,9 +267,26 @@ struct SocialRhs {
         J = ((-1.0) * beta) * a;
         dT = ((1.0 - x) * beta) * ap;
     }
+    // After an accepted step, touch AW_{n−1}'s knot 32 ahead (two 16-knot lines of the lane's
+    // wave-blocked buffer): those lines were written a whole iterate ago and live in HBM, so
+    // every stage lookup would otherwise wait on an HBM round trip; the touch brings them into
+    // L2 while the intervening steps run.  The loaded values are consumed one step later (an
+    // impossible-value compare into the `slow` diagnostic), so the wait for them falls where
+    // they have long arrived.
+    double pf_t = 0.0, pf_v = 0.0;
     __device__ __forceinline__ void accepted(double t)
     {
-        if (n >= 2 && t >= tfirst && t <= tlast) (void)w.find_advance(t);
+        if (n >= 2 && t >= tfirst && t <= tlast) {
+            const int j = w.find_advance(t);
+#ifndef SBR_SOCIAL_NO_PREFETCH
+            slow += (pf_t == -1.0 || pf_v == -2.0) ? 1 : 0;
+            const int q = j + 32 < n ? j + 32 : n - 1;
+            pf_t = to[q];
+            pf_v = vo[q];
+#else
+            (void)j;
+#endif
+        }
     }
     static constexpr bool kFsalExact = false;
     static constexpr bool kPinTableau = false;
