@@ -680,9 +680,10 @@ int sbr_sweep_baseline_dev(sbr_ctx* c, void* stream, const double* beta, const d
 }
 
 // hetero equilibrium LDS slab (doubles): knot times + per-group HR summaries of one column,
-// capped so that SBR_HET_MINW workgroups share a CU (config 4: n <= 4.8k knots)
+// capped so that SBR_HET_MINW = 2 workgroups share a CU's 160 KB (2 x (79.5 KB + the kernel's
+// static LDS)); config 4 with Rosenbrock23 after the switch: n <= 7.9k knots
 #ifndef SBR_HET_LDS
-#define SBR_HET_LDS 7168
+#define SBR_HET_LDS 10176
 #endif
 static int het_lds(const sbr_ctx* c) { return c->lds_cap * 3 < SBR_HET_LDS ? c->lds_cap * 3 : SBR_HET_LDS; }
 

@@ -407,6 +407,365 @@ __global__ __launch_bounds__(64) void learn_hetero_kernel(const double* __restri
 }
 
 // ---------------------------------------------------------------------------
+// learn_hetero_wave_kernel<K>: one wave per column, lane k = group k
+// ---------------------------------------------------------------------------
+// The same AutoTsit5(Rosenbrock23()) solve as learn_hetero_kernel, bit for bit, laid out
+// for the lone wave's serial chain instead of 64 columns per wave:
+//  * lane k holds component k of every stage vector and row k of W; the couplings (ω, the
+//    RMS error norm, the eigen estimates, the LU's pivot column and pivot row, the
+//    substitutions) read the other lanes' values with v_readlane into SGPRs and fold them
+//    in the oracle's order, so every sum and max is the same left fold;
+//  * the step control (t, dt, controller, AutoSwitch, knot counters) is wave-uniform: no
+//    divergence between the columns' Tsit5 and Rosenbrock23 phases (with 64 columns per
+//    wave both branches ran whenever the columns disagreed);
+//  * a row interchange is a uniform branch taken only when the pivot leaves the diagonal.
+// Lanes >= K shadow component K-1's arithmetic and never store or get read.
+#ifndef SBR_HET_LEARN_WAVE
+#define SBR_HET_LEARN_WAVE 1 // 0: learn_hetero_kernel (one lane per column, A/B)
+#endif
+__device__ __forceinline__ double wave_bcast(double v, int l)
+{
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+    return __hiloint2double(hi, lo);
+}
+
+template <int K>
+struct WaveRow {
+    const int lane; // row / component index of this lane (lanes >= K: K - 1's shadow)
+    const int kk;
+    const double bk, dk; // β_k, dist_k
+    const double* __restrict__ dist;
+    __device__ __forceinline__ WaveRow(int l, const double* __restrict__ betas_c, const double* __restrict__ d)
+        : lane(l), kk(l < K ? l : K - 1), bk(betas_c[kk]), dk(d[kk]), dist(d)
+    {
+    }
+    // ω = dist_0·I_0 + dist_1·I_1 + … (rhs_hetero's left fold; each product formed in its lane)
+    __device__ __forceinline__ double omega(double I) const
+    {
+        const double pr = dk * I;
+        double w = wave_bcast(pr, 0);
+#pragma unroll
+        for (int j = 1; j < K; j++) w = w + wave_bcast(pr, j);
+        return w;
+    }
+    __device__ __forceinline__ double rhs(double I) const { return ((1.0 - I) * bk) * omega(I); }
+    // sqrt(Σ v_k² / K), the sum from 0.0 in component order
+    __device__ __forceinline__ double rms(double v) const
+    {
+        if (K == 1) return wave_bcast(fabs(v), 0);
+        const double sq = v * v;
+        double s = 0.0;
+#pragma unroll
+        for (int i = 0; i < K; i++) s = s + wave_bcast(sq, i);
+        return sqrt(s / (double)K);
+    }
+};
+
+// Row-distributed K×K LU (RegLU's operation sequence): lane i holds row i of A.
+template <int K>
+struct WaveLU {
+    double A[K];
+    int piv[K]; // wave-uniform
+    __device__ __forceinline__ void factor(int lane)
+    {
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            double pv = wave_bcast(A[k], k);
+            double amax = fabs(pv);
+            int kp = k;
+#pragma unroll
+            for (int i = k + 1; i < K; i++) {
+                const double ai = wave_bcast(A[k], i);
+                if (fabs(ai) > amax) { kp = i; amax = fabs(ai); pv = ai; }
+            }
+            piv[k] = kp;
+            if (pv != 0.0) {
+                if (kp != k) {
+#pragma unroll
+                    for (int j = 0; j < K; j++) {
+                        const double vk = wave_bcast(A[j], k), vp = wave_bcast(A[j], kp);
+                        A[j] = lane == k ? vp : (lane == kp ? vk : A[j]);
+                    }
+                }
+                const double inv = 1.0 / pv; // A[k][k] after the interchange
+                const double sc = A[k] * inv;
+                A[k] = lane > k ? sc : A[k];
+            }
+#pragma unroll
+            for (int j = k + 1; j < K; j++) {
+                const double akj = wave_bcast(A[j], k);
+                const double v = A[j] - A[k] * akj;
+                A[j] = lane > k ? v : A[j];
+            }
+        }
+    }
+    // b: this lane's component of the right-hand side, overwritten with the solution's
+    __device__ __forceinline__ void solve(double& b, int lane) const
+    {
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const int kp = piv[k];
+            if (kp != k) {
+                const double x = wave_bcast(b, k), y = wave_bcast(b, kp);
+                b = lane == k ? y : (lane == kp ? x : b);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < K; j++) {
+            const double a = -wave_bcast(b, j);
+            const double v = fma(a, A[j], b);
+            b = lane > j ? v : b;
+        }
+#pragma unroll
+        for (int j = K - 1; j >= 0; j--) {
+            const double bj = wave_bcast(b / A[j], j); // lane j: b_j / A[j][j]
+            b = lane == j ? bj : b;
+            const double v = fma(-bj, A[j], b);
+            b = lane < j ? v : b;
+        }
+    }
+};
+
+template <int K>
+__global__ __launch_bounds__(64) void learn_hetero_wave_kernel(const double* __restrict__ betas,
+                                                               const double* __restrict__ dist,
+                                                               const double* __restrict__ eta,
+                                                               const double* __restrict__ t_end, LearnArgs a,
+                                                               HeteroBufs L)
+{
+    const int c = blockIdx.x;
+    const int lane = threadIdx.x;
+    const bool act = lane < K;
+    const WaveRow<K> R(lane, betas + (size_t)c * K, dist);
+    const double ETA = eta[c], T1 = t_end[c], T0 = 0.0;
+    const size_t cap = (size_t)L.cap;
+    double* __restrict__ T = L.t + (size_t)c * cap;
+    double* __restrict__ Gv = L.G + (size_t)c * cap * K;
+    double* __restrict__ H = L.hr + ((size_t)c * K + R.kk) * cap;
+    double* __restrict__ HI = L.hrI + ((size_t)c * K + R.kk) * cap;
+    uint32_t st = 0;
+    bool argok = ETA > 0.0 && T1 > T0;
+#pragma unroll
+    for (int k = 0; k < K; k++) argok = argok && (wave_bcast(R.bk, k) > 0.0);
+    if (!argok) {
+        if (lane == 0) {
+            L.status[c] = SBR_ARG_INVALID;
+            L.n_knots[c] = 0; L.n_tau[c] = 0; L.n_le[c] = 0; L.n_accept[c] = 0; L.n_reject[c] = 0;
+        }
+        return;
+    }
+    const double x0 = a.x0, rtol = a.rtol, atol = a.atol, p = a.p, lam = a.lam;
+    const double dtmax = T1 - T0;
+    const double dtmin = sbr_jl_eps(dmax(fabs(T0), fabs(T1)));
+    double x, k1, k2, k3, k4, k5, k6, k7, tmp, tmp6, u;
+
+    // ---- ode_determine_initdt ----
+    x = x0;
+    const double sk = fma(fabs(x0), rtol, atol);
+    const double d0 = R.rms(x0 / sk);
+    k1 = R.rhs(x);
+    const double d1 = R.rms(k1 / sk);
+    double dt0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : (d0 / d1) / 100.0;
+    dt0 = dmin(dt0, dtmax);
+    double dt;
+    if (dt0 < 10.0 * DBL_EPS) {
+        dt = dmax(1e-6, dtmin);
+    } else {
+        u = fma(dt0, k1, x0);
+        k7 = R.rhs(u);
+        bool same = true;
+#pragma unroll
+        for (int k = 0; k < K; k++) same = same && (__builtin_amdgcn_readlane((int)(k1 == k7), k) != 0);
+        if (same) {
+            dt = dmax(dtmin, 100.0 * dt0);
+        } else {
+            const double d2 = R.rms((k7 - k1) / sk) / dt0;
+            const double md = dmax(d1, d2);
+            const double dt1 = (md <= 1e-15) ? dmax(1e-6, dt0 * 1e-3) : sbr_pow_pos(0.01 / md, 1.0 / 6.0);
+            dt = dmax(dtmin, dmin(dmin(100.0 * dt0, dt1), dtmax));
+        }
+    }
+
+    // ---- knot sink: (t, G_k) + this lane's streamed hazard terms; g = f(t, x)_k is the
+    // FSAL value of the step that produced the knot (the same expression on the same x) ----
+    int n = 0, m = 0;
+    double tprev = 0.0, Ik = 0.0, eprev = 0.0, gprev = 0.0;
+    bool past = false, done = false;
+    auto push = [&](double t, double xs, double g) {
+        if (n >= L.cap) { st |= SBR_KNOT_OVERFLOW; done = true; return; }
+        if (lane == 0) T[n] = t;
+        if (act) Gv[(size_t)n * K + lane] = xs;
+        if (!past) {
+            if (t <= ETA) {
+                const double E = sbr_exp(lam * t);
+                const double e = E * g;
+                Ik = (m == 0) ? 0.0 : Ik + (0.5 * (eprev + e)) * (t - tprev);
+                if (act) { H[m] = (p * E) * g; HI[m] = Ik; }
+                eprev = e;
+                gprev = g;
+                m++;
+                tprev = t;
+            } else {
+                past = true; // η always appended (explicit grid): pdf(η) on bracket [n-1, n]
+                const double d = (ETA - tprev) / (t - tprev);
+                const double E = sbr_exp(lam * ETA);
+                const double pe = gprev * (1.0 - d) + g * d;
+                const double e = E * pe;
+                Ik = Ik + (0.5 * (eprev + e)) * (ETA - tprev);
+                if (act) { H[m] = (p * E) * pe; HI[m] = Ik; }
+                m++;
+            }
+        }
+        n++;
+    };
+
+    const double snap = 100.0 * sbr_jl_eps(T1);
+    double t = T0;
+    double eig = 1.0; // integrator.eigen_est at init
+    PIControl pc;
+    AutoSwitch as;
+    int naccept = 0, nreject = 0;
+    push(t, x, k1);
+    int64_t iter = 0;
+    while (t < T1 && !done) {
+        if (++iter > a.maxiters) { st |= SBR_ODE_MAXITERS; break; }
+        (void)as.choose(eig, dt); // initialize!: fsalfirst = f(uprev, t) == k1 bit for bit (autonomous)
+        dt = dmin(dtmax, dt);
+        dt = dmax(dt, dtmin);
+        dt = dmin(dt, T1 - t);
+        if (dt <= dtmin && t + dt < T1) { st |= SBR_ODE_FAILED; break; } // DtLessThanMin
+        double EEst;
+        if (as.stiff) {
+            // ---- Rosenbrock23 (perform_step!, Rosenbrock23Cache, @muladd); k7 <- fsallast ----
+            const double dtg = dt * ROS23_D;
+            const double invdtg = 1.0 / dtg, neginvdtg = -(1.0 / dtg);
+            const double dto2 = dt / 2.0, dto6 = dt / 6.0;
+            WaveLU<K> W;
+            {
+                // ForwardDiff jacobian row k: J_kj = dist_j·b_k, J_kk = (−β_k)·ω + dist_k·b_k
+                const double w = R.omega(x);
+                const double bkx = (1.0 - x) * R.bk;
+                const double dg = (-R.bk) * w + R.dk * bkx;
+                double s = 0.0;
+#pragma unroll
+                for (int j = 0; j < K; j++) {
+                    W.A[j] = (j == lane) ? dg : dist[j] * bkx;
+                    s = s + fabs(W.A[j]);
+                }
+                // opnorm(J, Inf): NaN-propagating max of the row sums, in row order
+                double nrm = 0.0;
+#pragma unroll
+                for (int i = 0; i < K; i++) {
+                    const double si = wave_bcast(s, i);
+                    nrm = (nrm != nrm || si != si) ? (double)NAN : (si > nrm ? si : nrm);
+                }
+                eig = nrm;
+#pragma unroll
+                for (int j = 0; j < K; j++) W.A[j] = (j == lane) ? fma(-1.0, invdtg, W.A[j]) : W.A[j];
+            }
+            W.factor(lane);
+            double r = k1 + dtg * 0.0; // fsalfirst + dt·d·∂f/∂t
+            W.solve(r, lane);
+            const double s1 = r * neginvdtg;
+            tmp = fma(dto2, s1, x);
+            const double f1 = R.rhs(tmp);
+            r = f1 - s1;
+            W.solve(r, lane);
+            const double s2 = fma(r, neginvdtg, s1);
+            u = fma(dt, s2, x);
+            k7 = R.rhs(u);
+            r = fma(dt, 0.0, fma(-2.0, s1 - k1, fma(-ROS23_C32, s2 - f1, k7)));
+            W.solve(r, lane);
+            const double s3 = r * neginvdtg;
+            const double ut = dto6 * (fma(-2.0, s2, s1) + s3);
+            EEst = R.rms(ut / fma(dmax(fabs(x), fabs(u)), rtol, atol));
+        } else {
+            const double a21 = dt * A21;
+            tmp = fma(a21, k1, x);
+            k2 = R.rhs(tmp);
+            tmp = fma(dt, fma(A31, k1, A32 * k2), x);
+            k3 = R.rhs(tmp);
+            tmp = fma(dt, fma(A41, k1, fma(A42, k2, A43 * k3)), x);
+            k4 = R.rhs(tmp);
+            tmp = fma(dt, fma(A51, k1, fma(A52, k2, fma(A53, k3, A54 * k4))), x);
+            k5 = R.rhs(tmp);
+            tmp6 = fma(dt, fma(A61, k1, fma(A62, k2, fma(A63, k3, fma(A64, k4, A65 * k5)))), x);
+            k6 = R.rhs(tmp6);
+            u = fma(dt, fma(A71, k1, fma(A72, k2, fma(A73, k3, fma(A74, k4, fma(A75, k5, A76 * k6))))), x);
+            k7 = R.rhs(u);
+            const double rr = fabs((k7 - k6) / (u - tmp6));
+            double e = 0.0;
+            bool e_nan = false;
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+                const double v = wave_bcast(rr, k);
+                if (v != v) e_nan = true;
+                else if (v > e) e = v;
+            }
+            eig = e_nan ? (double)NAN : e;
+            const double ut = dt * fma(BT1, k1, fma(BT2, k2, fma(BT3, k3, fma(BT4, k4,
+                                       fma(BT5, k5, fma(BT6, k6, BT7 * k7))))));
+            EEst = R.rms(ut / fma(dmax(fabs(x), fabs(u)), rtol, atol));
+        }
+        if (EEst != EEst) { st |= SBR_ODE_FAILED; break; } // NaN trial state (ReturnCode.Unstable)
+        bool acc;
+        const double dtn = pc.next_dt(EEst, dt, dtmax, dtmin, acc);
+        if (acc) {
+            naccept++;
+            double tn = t + dt;
+            if (fabs(tn - T1) < snap) tn = T1;
+            t = tn;
+            x = u;
+            k1 = k7;
+            dt = dtn;
+            push(t, x, k1);
+        } else {
+            nreject++;
+            dt = dtn;
+        }
+        if (!(dt > 0.0) || !isfinite(dt)) { st |= SBR_ODE_FAILED; break; }
+    }
+    if (as.nswitch > 0) st |= SBR_STIFF_SWITCH;
+    int n_le = m;
+    if (past) {
+        n_le = m - 1;
+    } else if (!(st & SBR_KNOT_OVERFLOW)) {
+        // no knot beyond η: pdf(η) exists only if the last knot is η itself
+        if (n >= 2 && tprev == ETA) {
+            const double E = sbr_exp(lam * ETA);
+            // bracket clamps to [n-2, n-1] with δ = 1: gprev*(1-1) ... = g_{n-1}
+            const double pe = 0.0 + gprev * 1.0;
+            if (act) { H[m] = (p * E) * pe; HI[m] = Ik; }
+            m++;
+        } else {
+            st |= SBR_OOB;
+        }
+    }
+    if (m > 0 && !(st & SBR_OOB)) {
+        // normalisation hr = p·e^{λτ̄}g / (p·I(τ̄) + (1 − p)·I(η)), all 64 lanes over each group's row
+        __threadfence_block();
+        const double omp = 1.0 - p;
+        double* __restrict__ Hc = L.hr + (size_t)c * K * cap;
+        const double* __restrict__ HIc = L.hrI + (size_t)c * K * cap;
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const double Ieta = HIc[(size_t)k * cap + m - 1];
+            for (int i = lane; i < m; i += 64)
+                Hc[(size_t)k * cap + i] = Hc[(size_t)k * cap + i] / ((p * HIc[(size_t)k * cap + i]) + (omp * Ieta));
+        }
+    }
+    if (lane == 0) {
+        L.n_knots[c] = n;
+        L.n_tau[c] = m;
+        L.n_le[c] = n_le;
+        L.status[c] = st;
+        L.n_accept[c] = naccept;
+        L.n_reject[c] = nreject;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // per-point solve
 // ---------------------------------------------------------------------------
 template <int K, class PT>
@@ -895,8 +1254,12 @@ static hipError_t launch_hetero_k(const double* betas, const double* dist, const
                                   const ResultSoA& out, double* tin, double* tout, hipStream_t s, int phase)
 {
     if (phase == 0) {
+#if SBR_HET_LEARN_WAVE
+        hipLaunchKernelGGL(learn_hetero_wave_kernel<K>, dim3(la.n_beta), dim3(64), 0, s, betas, dist, eta, t_end, la, L);
+#else
         hipLaunchKernelGGL(learn_hetero_kernel<K>, dim3((la.n_beta + 63) / 64), dim3(64), 0, s, betas, dist, eta,
                            t_end, la, L);
+#endif
         return hipGetLastError();
     }
     const size_t lds = (size_t)ea.lds_cap * sizeof(double);
