@@ -58,30 +58,38 @@ def lib_sha() -> str:
     return hashlib.sha256(sbr._lib.LIB_PATH.read_bytes()).hexdigest()[:16]
 
 
-def executed_fp64(kernel_prefix: str, workload: str):
-    """Executed FP64 flops per launch of a kernel from the committed PMC summary
-    (tools/pmc_summary.py), only when it was collected on this very libsbr.so:
-    64·(ADD + MUL + TRANS) + 128·FMA over SQ_INSTS_VALU_*_F64 (wave instructions, every
-    lane counted as active, i.e. an upper bound).  None when unavailable."""
+def pmc_of(kernel_prefix: str, workload: str):
+    """(executed FP64 flops, HBM bytes) per launch of a kernel from the committed PMC summary
+    (tools/pmc_summary.py -> profiles/pmc_latest.json), only when the counters were collected
+    on this kernel's machine code (sbr.provenance.kernel_code_sha over libsbr.so) and
+    workload; (None, None) otherwise.  Executed flops: 64·(ADD + MUL + TRANS) + 128·FMA over
+    SQ_INSTS_VALU_*_F64 (wave instructions, every lane counted as active: an upper bound).
+    Bytes: FETCH_SIZE×2 (gfx950) + WRITE_SIZE, MI355X_MICROARCH.md's correction."""
+    from sbr import provenance
     try:
-        pm = json.loads(PMC_SUMMARY.read_text())
+        pm = json.loads(PMC_SUMMARY.read_text())["workloads"][workload]["kernels"]
     except Exception:
-        return None
-    if pm.get("libsbr_sha16") != lib_sha() or pm.get("workload") != workload:
-        return None
-    for k, c in pm.get("kernels", {}).items():
-        if k.startswith(kernel_prefix) and "SQ_INSTS_VALU_FMA_F64" in c:
-            return (64 * (c.get("SQ_INSTS_VALU_ADD_F64", 0) + c.get("SQ_INSTS_VALU_MUL_F64", 0)
-                          + c.get("SQ_INSTS_VALU_TRANS_F64", 0)) + 128 * c["SQ_INSTS_VALU_FMA_F64"])
-    return None
+        return None, None
+    for k, c in pm.items():
+        if not k.startswith(kernel_prefix):
+            continue
+        if c.get("code_sha16") is None or c["code_sha16"] != provenance.kernel_code_sha(k):
+            return None, None
+        ex = None
+        if "SQ_INSTS_VALU_FMA_F64" in c:
+            ex = (64 * (c.get("SQ_INSTS_VALU_ADD_F64", 0) + c.get("SQ_INSTS_VALU_MUL_F64", 0)
+                        + c.get("SQ_INSTS_VALU_TRANS_F64", 0)) + 128 * c["SQ_INSTS_VALU_FMA_F64"])
+        return ex, c.get("hbm_bytes_per_launch")
+    return None, None
 
 
-def roofline(kernel: str, flops: float, secs: float, traffic=None, executed=None, limiter="latency") -> dict:
+def roofline(kernel: str, flops: float, secs: float, pmc=(None, None), limiter="latency") -> dict:
     """roofline block for `kernel`: algorithmic flops per launch / average launch time.
     The roof the metric is priced against is the FP64 vector peak (no dense
     contraction: no MFMA; ≈10⁴ flop/B: not HBM); `bound` names what limits the kernel
     in practice (PMC: dependent search / division chains, wait and issue stalls)."""
     ach = flops / secs / 1e12 if secs > 0 else 0.0
+    executed, traffic = pmc
     r = {"bound": limiter, "roof": "valu_fp64", "kernel": kernel, "achieved": ach, "peak": FP64_VALU_PEAK_TFLOPS,
          "unit": "TFLOP/s", "frac": ach / FP64_VALU_PEAK_TFLOPS, "traffic": traffic,
          "flops_per_launch": flops, "flop_convention": "SURVEY.md §8(d)"}
@@ -130,7 +138,6 @@ def parse():
     ap.add_argument("--cpu-stride", type=int, default=2, help="cpu_baseline samples every k-th β column")
     ap.add_argument("--phases", action="store_true",
                     help="also time the equilibrium kernel stopped after each stage (diagnostic flags)")
-    ap.add_argument("--traffic", default=str(REPO / "profiles" / "traffic_latest.json"))
     ap.add_argument("--workload", choices=("baseline", "social", "hetero", "interest"), default="baseline",
                     help="baseline: BASELINE config 3 (the metric); social: config 5 per-GPU share; "
                          "hetero: config 4 (K = 8, 1024x1024 per GPU); interest: the interest-rate "
@@ -244,16 +251,6 @@ def main():
 
     total_pts = nb * nu * world
     value = total_pts * a.steps / elapsed
-    traffic = None
-    tp = Path(a.traffic)
-    if tp.exists():
-        try:
-            tj = json.loads(tp.read_text())
-            if tj.get("workload") == f"fig5_{n}x{n}" and tj.get("kernel", "").startswith("equilibrium_kernel"):
-                traffic = tj.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
-
     res = {
         "metric": "equilibria solved/sec on β×u grid (FP64)",
         "value": value,
@@ -285,8 +282,8 @@ def main():
         "work_per_step": {"run_points": int(run.sum()), "bisect_iters": int(iters.sum()),
                           "aw_knots_run": int((run * n_tau[:, None]).sum()),
                           "rk_steps": int((ls["n_accept"] + ls["n_reject"]).sum())},
-        "roofline": (roofline("equilibrium_kernel", f_eq, eq_s, traffic,
-                              executed_fp64("equilibrium_kernel<", f"fig5_{n}x{n}")) if pipe else None),
+        "roofline": (roofline("equilibrium_kernel", f_eq, eq_s, pmc_of("equilibrium_kernel<", f"fig5_{n}x{n}"))
+                     if pipe else None),
         "libsbr_sha16": lib_sha(),
     }
     if not pipe:
@@ -405,8 +402,8 @@ def main_hetero(a):
         "stiff_switch_fraction": float(((st & sbr.STATUS["SBR_STIFF_SWITCH"]) > 0).mean()),
         "stiff_switch": "handled (Rosenbrock23 restated, DESIGN.md §2)",
         "learn_steps_per_column": float((hs["n_accept"] + hs["n_reject"]).mean()),
-        "roofline": roofline("equilibrium_hetero_kernel", f_eq_h, eq_ms / max(ncalls, 1) / 1e3, None,
-                             executed_fp64("equilibrium_hetero_kernel<", f"hetero_K8_{n}x{n}")),
+        "roofline": roofline("equilibrium_hetero_kernel", f_eq_h, eq_ms / max(ncalls, 1) / 1e3,
+                             pmc_of("equilibrium_hetero_kernel<", f"hetero_K8_{n}x{n}")),
         "libsbr_sha16": lib_sha(),
     }
     if a.phases:
@@ -531,8 +528,8 @@ def main_interest(a):
         "value_fn_rk_steps_per_point": float(steps.mean()),
         "run_fraction": float(((st & sbr.STATUS["SBR_RUN"]) > 0).mean()),
         "stiff_switch_fraction": float(((st & sbr.STATUS["SBR_STIFF_SWITCH"]) > 0).mean()),
-        "roofline": roofline("equilibrium_kernel<*, true> (interest)", f_eq_i, eq_ms / max(ncalls, 1) / 1e3, None,
-                             executed_fp64("equilibrium_kernel<512, true>", f"interest_fig5_{n}x{n}")),
+        "roofline": roofline("equilibrium_kernel<*, true> (interest)", f_eq_i, eq_ms / max(ncalls, 1) / 1e3,
+                             pmc_of("equilibrium_kernel<512, true>", f"interest_fig5_{n}x{n}")),
         "libsbr_sha16": lib_sha(),
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

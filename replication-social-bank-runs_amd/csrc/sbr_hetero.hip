@@ -1127,6 +1127,9 @@ __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const d
     st_o = SBR_RUN | SBR_CONVERGED | lbits;
 }
 
+#ifndef SBR_HET_XCD
+#define SBR_HET_XCD 1
+#endif
 template <int K, int BLOCK>
 #ifndef SBR_HET_MINW
 #define SBR_HET_MINW 2 // waves per SIMD: two 4-wave workgroups per CU (LDS slab: SBR_HET_LDS in sbr_capi.hip)
@@ -1139,7 +1142,19 @@ __global__ __launch_bounds__(BLOCK, SBR_HET_MINW) void equilibrium_hetero_kernel
                                                                    double* __restrict__ tout_out)
 {
     extern __shared__ double smem[];
+#if SBR_HET_XCD
+    // XCD-aware tile order (1-D grid): workgroup w runs on XCD w mod 8, so the u-tiles of one
+    // column are given to consecutive workgroups of the same XCD — they share that XCD's L2
+    // copy of the column's G and HR rows instead of fetching four copies into four L2s.
+    const int ntile = (a.n_u + BLOCK - 1) / BLOCK;
+    const int wid = blockIdx.x, xcd = wid & 7, seq = wid >> 3;
+    const int c = (seq / ntile) * 8 + xcd;
+    const int tile = seq - (seq / ntile) * ntile;
+    if (c >= a.n_col) return;
+#else
     const int c = blockIdx.y;
+    const int tile = blockIdx.x;
+#endif
     const int n = L.n_knots[c];
     const uint32_t lst = L.status[c];
     const size_t cap = (size_t)L.cap;
@@ -1209,7 +1224,7 @@ __global__ __launch_bounds__(BLOCK, SBR_HET_MINW) void equilibrium_hetero_kernel
 #pragma unroll
     for (int k = 0; k < K; k++)
         env = env + dist[k] * (2.0 * ((double)s_dcnt[k] * __longlong_as_double((long long)s_dmax[k])));
-    const int j = blockIdx.x * BLOCK + threadIdx.x;
+    const int j = tile * BLOCK + threadIdx.x;
     if (j >= a.n_u) return;
     double dl[K];
 #pragma unroll
@@ -1250,7 +1265,7 @@ __global__ __launch_bounds__(BLOCK, SBR_HET_MINW) void equilibrium_hetero_kernel
 
 template <int K>
 static hipError_t launch_hetero_k(const double* betas, const double* dist, const double* eta, const double* t_end,
-                                  const double* u, const LearnArgs& la, const HeteroEqArgs& ea, const HeteroBufs& L,
+                                  const double* u, const LearnArgs& la, const HeteroEqArgs& ea_in, const HeteroBufs& L,
                                   const ResultSoA& out, double* tin, double* tout, hipStream_t s, int phase)
 {
     if (phase == 0) {
@@ -1262,7 +1277,19 @@ static hipError_t launch_hetero_k(const double* betas, const double* dist, const
 #endif
         return hipGetLastError();
     }
-    const size_t lds = (size_t)ea.lds_cap * sizeof(double);
+    const size_t lds = (size_t)ea_in.lds_cap * sizeof(double);
+    HeteroEqArgs ea = ea_in;
+    ea.n_col = la.n_beta;
+#if SBR_HET_XCD
+    const unsigned ncol8 = (unsigned)((la.n_beta + 7) / 8) * 8;
+    if (ea.n_u >= 256) {
+        hipLaunchKernelGGL((equilibrium_hetero_kernel<K, 256>), dim3(((ea.n_u + 255) / 256) * ncol8), dim3(256), lds, s,
+                           L, dist, eta, t_end, u, ea, out, tin, tout);
+    } else {
+        hipLaunchKernelGGL((equilibrium_hetero_kernel<K, 64>), dim3(((ea.n_u + 63) / 64) * ncol8), dim3(64), lds, s,
+                           L, dist, eta, t_end, u, ea, out, tin, tout);
+    }
+#else
     if (ea.n_u >= 256) {
         hipLaunchKernelGGL((equilibrium_hetero_kernel<K, 256>), dim3((ea.n_u + 255) / 256, la.n_beta), dim3(256), lds, s,
                            L, dist, eta, t_end, u, ea, out, tin, tout);
@@ -1270,6 +1297,7 @@ static hipError_t launch_hetero_k(const double* betas, const double* dist, const
         hipLaunchKernelGGL((equilibrium_hetero_kernel<K, 64>), dim3((ea.n_u + 63) / 64, la.n_beta), dim3(64), lds, s,
                            L, dist, eta, t_end, u, ea, out, tin, tout);
     }
+#endif
     return hipGetLastError();
 }
 

@@ -79,6 +79,7 @@ struct HeteroEqArgs {
     int32_t exhaustive; // 1: evaluate AW over every knot (no branch and bound)
     int32_t diag;       // SBR_FLAG_DIAG_* bits >> 8 (timing breakdown only)
     double* aw_path;    // single-point mode (n_u = 1): AW_total on the learning knots (may be null)
+    int32_t n_col;      // set by the launcher (XCD-aware 1-D grid)
 };
 
 // Promotion pool of the social sweep: a point whose iterate outgrows the knot

@@ -74,3 +74,17 @@ def test_social_entry_points_validate_arguments():
     rc = L.sbr_sweep_social(None, None, None, 1e-4, None, 1, 1, 0.5, 0.5, 0.5, None, 1000, 1e-4, 10, None,
                             ctypes.byref(soa), None, None)
     assert rc == sbr._lib.SBR_EARG
+
+
+def test_kernel_code_provenance():
+    """bench.py folds PMC counters into its roofline line only for the machine code they
+    were collected on: the per-kernel code sha read from libsbr.so's gfx950 code object."""
+    from sbr import provenance
+
+    shas = {k: provenance.kernel_code_sha(k) for k in ("equilibrium_kernel<768, false>",
+                                                       "equilibrium_hetero_kernel<8, 256>", "hazard_kernel",
+                                                       "learn_logistic_kernel")}
+    assert all(s is not None and len(s) == 16 for s in shas.values()), shas
+    assert len(set(shas.values())) == len(shas)
+    assert provenance.kernel_code_sha("no_such_kernel") is None
+    assert provenance.kernel_base("void sbr::equilibrium_kernel<768, false>(sbr::LearnBufs)") == "equilibrium_kernel"

@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # PMC counter passes on a short bench run (one counter group per rocprofv3 run).
 set -u
-OUT=gpurun_out/pmc
+OUT=${PMC_OUT:-gpurun_out/pmc}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 timeout -k 5 60 rocprofv3 -L > "$OUT/counters_list.txt" 2>&1 || true

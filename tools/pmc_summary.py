@@ -1,13 +1,13 @@
 #!/usr/bin/env python3
 """Aggregate rocprofv3 --pmc passes (tools/pmc.sh) into a per-kernel table.
 
-Usage: python tools/pmc_summary.py gpurun_out/pmc profiles/r01_v3_pmc.txt [profiles/traffic_latest.json [workload
-       [profiles/pmc_latest.json]]]
+Usage: python tools/pmc_summary.py gpurun_out/pmc profiles/rNN_pmc.txt [workload [profiles/pmc_latest.json]]
 
 Every counter is averaged per dispatch of a kernel (summed over the device).
-The optional JSON holds HBM traffic per launch of the equilibrium kernel for
-bench.py's roofline.traffic, corrected as MI355X_MICROARCH.md's HBM section
-prescribes: FETCH_SIZE (KiB) doubled on gfx950, WRITE_SIZE (KiB) as is.
+The optional JSON (merged per workload) holds every kernel's counters, its HBM
+traffic per launch corrected as MI355X_MICROARCH.md's HBM section prescribes
+(FETCH_SIZE (KiB) doubled on gfx950, WRITE_SIZE (KiB) as is) and the sha of the
+kernel's machine code, for bench.py's roofline.traffic / frac_executed.
 """
 import csv
 import glob
@@ -34,7 +34,8 @@ def short(name):
 
 def main():
     pmc_dir, out_txt = sys.argv[1], sys.argv[2]
-    out_json = sys.argv[3] if len(sys.argv) > 3 else None
+    workload = sys.argv[3] if len(sys.argv) > 3 else "fig5_2048x2048"
+    out_json = sys.argv[4] if len(sys.argv) > 4 else None
     vals = load(pmc_dir)
     kernels = sorted({k for k, _ in vals if not k.startswith("__amd")})
     lines = ["# per-dispatch averages of rocprofv3 --pmc passes (%s)" % pmc_dir]
@@ -61,27 +62,30 @@ def main():
     with open(out_txt, "w") as f:
         f.write("\n".join(lines) + "\n")
     print("\n".join(lines))
+    # per-kernel counter averages, each tagged with the sha of the kernel's gfx950 code in
+    # libsbr.so (sbr.provenance): bench.py folds a kernel's counters into its roofline line
+    # (traffic, frac_executed) only while that machine code is unchanged.  Merged per workload.
     if out_json:
-        eq = [k for k in kernels if "equilibrium_kernel" in k and "hetero" not in k]
-        if eq:
-            c = per[eq[0]]
-            if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
-                t = {"kernel": short(eq[0]), "workload": sys.argv[4] if len(sys.argv) > 4 else "fig5_2048x2048",
-                     "source": out_txt,
-                     "read_bytes": 2 * c["FETCH_SIZE"] * 1024, "write_bytes": c["WRITE_SIZE"] * 1024}
-                t["hbm_bytes_per_launch"] = t["read_bytes"] + t["write_bytes"]
-                with open(out_json, "w") as f:
-                    json.dump(t, f, indent=1)
-    # per-kernel counter averages + the libsbr.so they were collected on (bench.py's
-    # roofline.frac_executed uses them only for that exact binary)
-    if len(sys.argv) > 5:
-        import hashlib
-        lib = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "replication-social-bank-runs_amd", "lib",
-                           "libsbr.so")
-        sha = hashlib.sha256(open(lib, "rb").read()).hexdigest()[:16]
-        pm = {"workload": sys.argv[4], "source": out_txt, "libsbr_sha16": sha,
-              "kernels": {short(k): per[k] for k in kernels}}
-        with open(sys.argv[5], "w") as f:
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
+                                        "replication-social-bank-runs_amd"))
+        from sbr import provenance as P
+        try:
+            pm = json.load(open(out_json))
+        except Exception:
+            pm = {}
+        if "workloads" not in pm:
+            pm = {"workloads": {}}
+        ks = {}
+        for k in kernels:
+            d = dict(per[k])
+            d["code_sha16"] = P.kernel_code_sha(short(k)) if "sbr::" in k else None
+            if "FETCH_SIZE" in d and "WRITE_SIZE" in d:  # MI355X_MICROARCH.md: FETCH_SIZE (KiB) x2 on gfx950
+                d["hbm_read_bytes"] = 2 * d["FETCH_SIZE"] * 1024
+                d["hbm_write_bytes"] = d["WRITE_SIZE"] * 1024
+                d["hbm_bytes_per_launch"] = d["hbm_read_bytes"] + d["hbm_write_bytes"]
+            ks[short(k)] = d
+        pm["workloads"][workload] = {"source": out_txt, "kernels": ks}
+        with open(out_json, "w") as f:
             json.dump(pm, f, indent=1)
 
 
