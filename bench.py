@@ -18,7 +18,8 @@ cannot overlap anything, so the default 50 steps amortise that pipeline fill to
 N GPUs (torchrun, one process per GPU, RCCL): weak scaling — rank r owns the β
 columns r, r+N, r+2N, … of a 2048·N-column grid (same u axis), so per-GPU work is
 fixed; each step ends with an RCCL gather of the result tensor (AW_max + status) to
-rank 0 over xGMI.  value = all ranks' equilibria × steps / max-over-ranks time.
+rank 0 over xGMI, issued on its own stream once that step's results exist
+(sbr_batch_wait) so that it overlaps the later steps' sweeps.  value = all ranks' equilibria × steps / max-over-ranks time.
 """
 from __future__ import annotations
 
@@ -199,6 +200,10 @@ def main():
         dist.gather(out["aw_max"][k], g_aw, dst=0)
         dist.gather(out["status"][k], g_st, dst=0)
 
+    # the gather of step k runs on its own stream as soon as step k's results exist
+    # (sbr_batch_wait), overlapped with the sweeps of the later steps
+    comm = torch.cuda.Stream(dev) if gather and pipe else None
+
     def run_steps(n):
         """n steps: pipelined, one batch call of n grids (learning of step k+1
         overlaps the equilibrium of step k); else one sweep call per step."""
@@ -209,7 +214,9 @@ def main():
                                          {k: v[:n] for k, v in out.items()}, stream=stream)
             for k in range(n):
                 if gather:
-                    gather_batch(k)
+                    eng.batch_wait(comm.cuda_stream, k)
+                    with torch.cuda.stream(comm):
+                        gather_batch(k)
         else:
             one = {k: v[0] for k, v in out.items()}
             for _ in range(n):

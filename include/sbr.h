@@ -144,6 +144,16 @@ int sbr_sweep_baseline_batch_dev(sbr_ctx* ctx, void* stream, int64_t n_batch, co
                                  const sbr_opts* opts, sbr_result_soa* out);
 
 /*
+ * Make `stream` wait (device side, no host sync) until grid k of the last
+ * sbr_sweep_baseline_batch_dev call on this context has its results, while the
+ * later grids of the batch are still being swept: the caller can ship grid k's
+ * results (e.g. an RCCL gather to rank 0, the collection of the result matrix
+ * in scripts/1_baseline.jl:224-267) overlapped with the rest of the batch.
+ * SBR_EARG if k is not a grid of that call.
+ */
+int sbr_batch_wait(sbr_ctx* ctx, void* stream, int64_t k);
+
+/*
  * Learning only — solve_learning (learning.jl:109-124) for n_beta β at once.
  * Writes, per β, the knot grid t and CDF values G of the adaptive ODE
  * solution (row i at [i*cap .. i*cap + n_knots[i]) ); g = βG(1−G) is implied

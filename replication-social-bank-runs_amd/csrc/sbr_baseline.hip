@@ -120,7 +120,13 @@ __global__ __launch_bounds__(SBR_LEARN_BLOCK) void learn_logistic_kernel(const d
 constexpr int HZ_BLOCK = 256;
 constexpr int HZ_LDS = 1024; // τ̄ knots per LDS chunk of the hazard kernel
 constexpr int HZ_REG = 16;   // τ̄ knots per thread held in registers (ntau <= 4096: one pass over HBM)
-constexpr int EQ_TILE = 4096;  // u values per equilibrium block (one block per β column up to this)
+#ifndef SBR_EQ_TILE
+#define SBR_EQ_TILE 4096
+#endif
+constexpr int EQ_TILE = SBR_EQ_TILE;  // u values per equilibrium block (one block per β column up to this)
+#ifndef SBR_EQ_REVERSE
+#define SBR_EQ_REVERSE 0 // A/B: dispatch the β columns last to first
+#endif
 #ifndef SBR_AW_WIN
 #define SBR_AW_WIN 6
 #endif
@@ -899,7 +905,7 @@ __global__ __launch_bounds__(BLOCK, INTEREST ? 1 : SBR_EQ_MINW) void equilibrium
                                                             ResultSoA out)
 {
     extern __shared__ double smem[];
-    const int b = blockIdx.y;
+    const int b = SBR_EQ_REVERSE ? (int)(gridDim.y - 1 - blockIdx.y) : (int)blockIdx.y;
     const int n = L.n_knots[b], ntau = L.n_tau[b], nle = L.n_le[b];
     const uint32_t lst = L.status[b];
     const size_t row = (size_t)b * (size_t)L.cap;

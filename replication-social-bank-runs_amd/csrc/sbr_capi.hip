@@ -94,6 +94,8 @@ struct sbr_ctx {
     // kernel timing (HIP event pairs on the launching stream), opt-in via sbr_timing_enable
     bool timing = false;
     std::vector<hipEvent_t> ev_pool;
+    std::vector<hipEvent_t> ev_grid; // per grid of the last baseline batch: results complete
+    int64_t n_grid = 0;
     size_t ev_used = 0;
     struct TRec {
         int kind; // 0 learning (+ hazard), 1 equilibrium
@@ -650,6 +652,7 @@ int sbr_free(sbr_ctx* c)
     }
     if (c->stage) (void)hipFree(c->stage);
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->ev_grid) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(c->stream);
     delete c;
     return SBR_OK;
@@ -709,6 +712,12 @@ int sbr_sweep_baseline_batch_dev(sbr_ctx* c, void* stream, int64_t n_batch, cons
         int rc = ensure_pipe_streams(c);
         if (rc) return rc;
     }
+    while ((int64_t)c->ev_grid.size() < n_batch) {
+        hipEvent_t e = nullptr;
+        HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming), SBR_EDEVICE);
+        c->ev_grid.push_back(e);
+    }
+    c->n_grid = 0;
     return fenced(c, stream, true, [&](hipStream_t s) -> int {
         const size_t np = (size_t)n_beta * (size_t)n_u;
         sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, p, lambda, o.ode_maxiters, (int32_t)n_beta, 1, 0};
@@ -743,10 +752,22 @@ int sbr_sweep_baseline_batch_dev(sbr_ctx* c, void* stream, int64_t n_batch, cons
             int rc = launch_eq(c, es, c->LW[slot], ek, tk, u, n_beta, n_u, kappa, o, r, nullptr);
             if (rc) return rc;
             HIP_TRY(c, hipEventRecord(c->ev_eq[slot], es), SBR_EDEVICE);
+            HIP_TRY(c, hipEventRecord(c->ev_grid[k], es), SBR_EDEVICE);
+            c->n_grid = k + 1;
             c->last_slot = slot;
         }
         return SBR_OK;
     });
+}
+
+int sbr_batch_wait(sbr_ctx* c, void* stream, int64_t k)
+{
+    SBR_SINGLE_DEVICE(c);
+    if (!c) return SBR_EARG;
+    if (k < 0 || k >= c->n_grid) return fail(c, SBR_EARG, "sbr_batch_wait: no such grid in the last batch");
+    if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
+    HIP_TRY(c, hipStreamWaitEvent((hipStream_t)stream, c->ev_grid[k], 0), SBR_EDEVICE);
+    return SBR_OK;
 }
 
 int sbr_sweep_baseline(sbr_ctx* c, const double* beta, const double* eta, const double* t_end, double x0,

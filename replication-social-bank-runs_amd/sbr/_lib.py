@@ -85,6 +85,7 @@ _SIGS = {
     "sbr_sweep_baseline_dev": (ctypes.c_int, [_P, _P, _P, _P, _P, _D, _P, _I64, _I64, _D, _D, _D, _P, _P]),
     "sbr_sweep_baseline_batch_dev": (ctypes.c_int, [_P, _P, _I64, _P, _P, _P, _D, _P, _I64, _I64, _D, _D, _D, _P,
                                                     _P]),
+    "sbr_batch_wait": (ctypes.c_int, [_P, _P, _I64]),
     "sbr_learn_baseline": (ctypes.c_int, [_P, _P, _P, _P, _D, _I64, _I32, _P, _P, _P, _I64, _P, _P]),
     "sbr_solve_point_paths": (ctypes.c_int, [_P, _D, _D, _D, _D, _D, _D, _D, _D, _P, _P, _P, _P, _P, _P, _I64, _P]),
     "sbr_apply_early_exit": (None, [_I64, _I64, _I32, _P]),

@@ -169,6 +169,11 @@ class Engine:
                                                   ctypes.byref(opts), ctypes.byref(soa))
         check(rc, self._ctx, "sbr_sweep_baseline_batch_dev")
 
+    def batch_wait(self, stream: int | None, k: int):
+        """Make ``stream`` wait until grid ``k`` of the last batch call has its results
+        (sbr_batch_wait): ship grid k while the rest of the batch is still being swept."""
+        check(self._L.sbr_batch_wait(self._ctx, stream, int(k)), self._ctx, "sbr_batch_wait")
+
     def learn_baseline(self, beta, eta, t_end, x0=1e-4, stop_after_eta=False, cap=65536):
         beta = np.ascontiguousarray(beta, np.float64)
         nb = len(beta)

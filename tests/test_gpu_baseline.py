@@ -194,7 +194,18 @@ def test_pipelined_batches_equal_single_sweeps(engine):
     # enqueued behind the call on torch's default stream, no host synchronisation between:
     # must see every batch complete (whichever equilibrium stream ran it)
     snap = {f: out[f].clone() for f in ("aw_max", "status")}
+    # grid k shipped from a side stream ordered only by sbr_batch_wait (bench.py's gathers)
+    side = torch.cuda.Stream(dev)
+    early = []
+    for k in range(nbat):
+        engine.batch_wait(side.cuda_stream, k)
+        with torch.cuda.stream(side):
+            early.append(out["aw_max"][k].clone())
+    with pytest.raises(sbr.ArgumentError):
+        engine.batch_wait(side.cuda_stream, nbat)
     torch.cuda.synchronize(dev)
+    for k in range(nbat):
+        assert torch.equal(early[k].view(torch.int64), out["aw_max"][k].view(torch.int64)), k
     for f in snap:
         assert torch.equal(snap[f].view(torch.int64) if f == "aw_max" else snap[f],
                            out[f].view(torch.int64) if f == "aw_max" else out[f]), f
