@@ -433,6 +433,9 @@ sbr::ResultSoA result_rows(const sbr::ResultSoA& r, size_t off)
 // chunk is still integrating.  Timing records: kind 0 = the learning stage of all chunks
 // (fork to the last chunk learned), kind 1 = the equilibrium tail after it.
 constexpr int kSweepChunks = sbr_ctx::kLearnSlots;
+#ifndef SBR_SWEEP_FRONT
+#define SBR_SWEEP_FRONT 32 // 0: halving chunks only (A/B: 4.44 -> 4.25 ms per config-3 sweep)
+#endif
 int run_baseline(sbr_ctx* c, hipStream_t s, const double* beta, const double* eta, const double* t_end, double x0,
                  const double* u, int64_t n_beta, int64_t n_u, double p, double kappa, double lambda,
                  const sbr_opts& o, const sbr::ResultSoA& out, double* aw_path)
@@ -461,6 +464,11 @@ int run_baseline(sbr_ctx* c, hipStream_t s, const double* beta, const double* et
         const int64_t wk = waves >> (kSweepChunks - k); // waves before chunk k
         lo[k] = std::min<int64_t>(n_beta, std::max<int64_t>(wk * 64, (int64_t)k * 64));
     }
+#if SBR_SWEEP_FRONT
+    // A/B: the front chunk is 1/SBR_SWEEP_FRONT of the waves (the Fig 5 grid's outliers sit in
+    // its first wave: 1.25x the steps of the next slowest)
+    lo[1] = std::min<int64_t>(lo[2] - 64, std::max<int64_t>(64, (waves / SBR_SWEEP_FRONT) * 64));
+#endif
     HIP_TRY(c, hipEventRecord(c->ev_in, s), SBR_EDEVICE);
     hipEvent_t t0 = tstart(c, s);
     for (int k = 0; k < kSweepChunks; k++) {
@@ -590,6 +598,9 @@ int sbr_init(int device, sbr_ctx** out)
     c->lds_cap = (int)(((long)(smem - 1024) * 64) / (8 * (3 * 64 + 2 + 16)));
     // baseline equilibrium kernel: t, G (2·64) + summaries per 64 knots, two workgroups per CU
     c->lds_cap_b = (int)(((long)(smem / 2 - 1024) * 64) / (8 * (2 * 64 + 2 + 16)));
+#ifdef SBR_EQ_LDS_KNOTS
+    c->lds_cap_b = std::min(c->lds_cap_b, (int)SBR_EQ_LDS_KNOTS);
+#endif
     *out = c;
     return SBR_OK;
 }
