@@ -155,6 +155,32 @@ def test_fig5_5000_run_mask(engine, golden):
     assert run.sum() == 8736564
 
 
+@pytest.mark.parametrize("case", ["single_point", "ragged_extremes", "eta_past_tend", "short_eta_per_column"])
+def test_edge_grids_bitwise(engine, oracle, case):
+    """Edge shapes and parameter extremes, every field, status bit and bisection count
+    equal to the oracle: a 1 × 1 grid; 6 × 65 (partial waves and tiles) with β from 1e-3 to
+    3e4 and u from 0 to 1.5 (no-run, run and u > every HR value); η beyond tspan on one
+    column (the reference's BoundsError); per-column η and t_end."""
+    if case == "single_point":
+        g = sbr.BaselineGrid([1.0], [0.05], 15.0, 30.0)
+    elif case == "ragged_extremes":
+        g = sbr.BaselineGrid([1e-3, 0.2, 7.3, 250.0, 1e4, 3e4], sbr.julia_range("0.0", "1.5", 65), 15.0, 30.0)
+    elif case == "eta_past_tend":
+        g = sbr.BaselineGrid([0.5, 2.0, 2.0], sbr.julia_range("0.001", "1", 97), np.array([40.0, 15.0, 30.0]),
+                             np.array([30.0, 30.0, 30.0]))
+    else:
+        g = sbr.BaselineGrid([0.7, 1.3, 4.0, 12.0, 40.0], sbr.julia_range("0.001", "1", 130),
+                             np.array([0.5, 3.0, 9.0, 15.0, 20.0]), np.array([1.0, 10.0, 18.0, 30.0, 60.0]))
+    a = engine.sweep_baseline(g)
+    o = _oracle_sweep(oracle, g)
+    for f in FIELDS:
+        assert_bitwise(a[f], o[f], f"{case} {f}")
+    assert np.array_equal(a["status"], o["status"]), case
+    assert np.array_equal(a["iters"], o["iters"]), case
+    if case == "eta_past_tend":
+        assert (a["status"][0] & sbr.STATUS["SBR_OOB"]).all()
+
+
 def test_blocked_scan_and_pruned_aw_equal_exhaustive(engine):
     """Block-summary crossing scan + branch-and-bound AW_max give exactly the
     exhaustive per-knot results (a different search, the same arithmetic)."""
