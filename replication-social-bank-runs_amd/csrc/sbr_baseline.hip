@@ -40,29 +40,38 @@ __global__ __launch_bounds__(SBR_LEARN_BLOCK) void learn_logistic_kernel(const d
     __builtin_amdgcn_s_setprio(3);
 #endif
     const int b = blockIdx.x * SBR_LEARN_BLOCK + threadIdx.x;
-    if (b >= a.n_beta) return;
-    const double BETA = beta[b], ETA = eta[b], T1 = t_end[b], T0 = 0.0;
-    const size_t row = (size_t)b * (size_t)L.cap;
+    const bool live = b < a.n_beta;
+    const double BETA = live ? beta[b] : 1.0, ETA = live ? eta[b] : 1.0, T1 = live ? t_end[b] : 1.0, T0 = 0.0;
+    const size_t row = (size_t)(live ? b : 0) * (size_t)L.cap;
     double* __restrict__ T = L.t + row;
     double* __restrict__ Gv = L.G + row;
     uint32_t st = 0;
-    int n = 0;
+    const bool fuse = a.fuse_hazard != 0; // wave-uniform
 
-    if (!(BETA > 0.0) || !(T1 > T0) || !(ETA > 0.0)) { // LearningParameters / EconomicParameters checks
+    if (live && (!(BETA > 0.0) || !(T1 > T0) || !(ETA > 0.0))) { // LearningParameters / EconomicParameters checks
         L.status[b] = SBR_ARG_INVALID;
         L.n_knots[b] = 0; L.n_tau[b] = 0; L.n_le[b] = 0; L.n_accept[b] = 0; L.n_reject[b] = 0;
-        return;
-    }
-    // ---- knot sink: store (t, G); the hazard stage runs afterwards in parallel.  Branch-free:
-    // every attempted step writes its candidate knot at the fill index n (a rejected one is
-    // overwritten by the next accepted step) and the counters advance by select ----
+    } else if (live) {
+    // ---- knot sink: store (t, G).  Branch-free: every attempted step writes its candidate
+    // knot at the fill index n (a rejected one is overwritten by the next accepted step) and the
+    // counters advance by select.  Fused hazard (a.fuse_hazard, the pipelined batch): each
+    // accepted knot ≤ η is also a τ̄ entry of hazard_rate (solver.jl:153-185) — its numerator
+    // (p·e^{λτ̄})·g and the running trapezoid integral I are formed as the knot is accepted
+    // (g = βG(1−G), the sequential sum in the reference's order), the η entry at the first
+    // knot past η; the normalisation by p·I + (1−p)·I_η is hazard_norm_kernel's.  The same
+    // operations as hazard_kernel, so the same bits. ----
     struct Sink {
         double* __restrict__ T;
         double* __restrict__ Gv;
+        double* __restrict__ H;
+        double* __restrict__ HI;
         int n, cap, m; // m: knots ≤ η (the hazard stage's τ̄ prefix), set at the first knot past η
         double tlast, bound, eta;
         int past, done, stop_after_eta; // 0 / 1 (ints: loop-carried bools cost mask conversions)
         uint32_t& st;
+        int fuse, hm;            // hm: τ̄ entries written
+        double beta, lam, p;
+        double hI, he, ht, hg;   // I, e and τ̄ of the last τ̄ entry, pdf of the last knot ≤ η
         __device__ __forceinline__ bool push(bool acc, double t, double x)
         {
             const bool room = n < cap;
@@ -79,6 +88,30 @@ __global__ __launch_bounds__(SBR_LEARN_BLOCK) void learn_logistic_kernel(const d
             const double reach = dmax(bound, t + (t - tlast));
             bound = upd ? reach : bound;
             const bool cross = pushed & (past == 0) & (t > eta);
+            if (fuse) {
+                const double g = (beta * x) * (1.0 - x);
+                const bool le = pushed & (past == 0) & (t <= eta);
+                const double E = sbr_exp(lam * t);
+                const double e = E * g;
+                const double In = hm == 0 ? 0.0 : hI + (0.5 * (he + e)) * (t - ht);
+                if (le) { H[n] = (p * E) * g; HI[n] = In; }
+                hI = le ? In : hI;
+                he = le ? e : he;
+                ht = le ? t : ht;
+                hg = le ? g : hg;
+                hm += le ? 1 : 0;
+                if (cross && ht != eta) {
+                    // τ̄ = η on bracket [m-1, m]: pdf interpolated, pushed unless η is a knot
+                    const double d = (eta - ht) / (t - ht);
+                    const double pe = hg * (1.0 - d) + g * d;
+                    const double E2 = sbr_exp(lam * eta);
+                    const double e2 = E2 * pe;
+                    hI = hI + (0.5 * (he + e2)) * (eta - ht);
+                    H[hm] = (p * E2) * pe;
+                    HI[hm] = hI;
+                    hm++;
+                }
+            }
             m = cross ? n : m;
             past |= cross ? 1 : 0;
             tlast = pushed ? t : tlast;
@@ -91,18 +124,61 @@ __global__ __launch_bounds__(SBR_LEARN_BLOCK) void learn_logistic_kernel(const d
         {
             return push(acc, tn, y1);
         }
-    } sink{T, Gv, 0, L.cap, -1, 0.0, -INFINITY, ETA, 0, 0, a.stop_after_eta != 0 ? 1 : 0, st};
+    } sink{T, Gv, fuse ? L.hr + row : nullptr, fuse ? L.hrI + row : nullptr, 0, L.cap, -1, 0.0, -INFINITY, ETA,
+           0, 0, a.stop_after_eta != 0 ? 1 : 0, st, fuse ? 1 : 0, 0, BETA, a.lam, a.p, 0.0, 0.0, 0.0, 0.0};
     LogisticSys f{BETA};
     OdeOut o;
     ode_scalar(f, sink, T1, a.x0, a.rtol, a.atol, a.maxiters, o);
     st |= o.status;
-    n = sink.n;
-    const int naccept = (int)o.naccept, nreject = (int)o.nreject;
+    const int n = sink.n;
+    int n_le = sink.m < 0 ? n : sink.m; // every knot ≤ η when none passed it
+    int n_tau = 0;
+    if (fuse) {
+        // hazard_kernel's η rule: with no knot past η, pdf(η) exists only if η is the last knot
+        if (sink.m < 0 && sink.ht != ETA) {
+            st |= SBR_OOB;
+            n_le = 0;
+        } else {
+            n_tau = sink.hm;
+        }
+    }
     L.n_knots[b] = n;
-    L.n_le[b] = sink.m < 0 ? n : sink.m; // every knot ≤ η when none passed it
+    L.n_le[b] = n_le;
+    if (fuse) L.n_tau[b] = n_tau;
     L.status[b] = st;
-    L.n_accept[b] = naccept;
-    L.n_reject[b] = nreject;
+    L.n_accept[b] = (int)o.naccept;
+    L.n_reject[b] = (int)o.nreject;
+    }
+}
+
+// Fused hazard, second half: HR_i = num_i / (p·I_i + (1 − p)·I_η) over every τ̄ entry the
+// learning kernel streamed (num_i in the HR row, I_i in the hrI row; I_η = the last I).  Fully
+// parallel and HBM-streaming (≈20 µs per 2048-column grid) — unlike hazard_kernel, whose
+// workgroups hold CU slots for the length of a serial scan while equilibria are running.
+constexpr int HN_BLOCK = 256, HN_UNROLL = 4;
+__global__ __launch_bounds__(HN_BLOCK) void hazard_norm_kernel(LearnArgs a, LearnBufs L)
+{
+    const int b = blockIdx.x;
+    const int nt = L.n_tau[b];
+    if (nt <= 0) return;
+    const size_t row = (size_t)b * (size_t)L.cap;
+    double* __restrict__ H = L.hr + row;
+    const double* __restrict__ HI = L.hrI + row;
+    const double p = a.p, omp = 1.0 - p, ie = HI[nt - 1];
+    for (int i0 = threadIdx.x; i0 < nt; i0 += HN_BLOCK * HN_UNROLL) {
+        double h[HN_UNROLL], q[HN_UNROLL];
+#pragma unroll
+        for (int k = 0; k < HN_UNROLL; k++) {
+            const int i = i0 + k * HN_BLOCK;
+            h[k] = i < nt ? H[i] : 0.0;
+            q[k] = i < nt ? HI[i] : 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < HN_UNROLL; k++) {
+            const int i = i0 + k * HN_BLOCK;
+            if (i < nt) H[i] = h[k] / ((p * q[k]) + (omp * ie));
+        }
+    }
 }
 
 // ============================================================================
@@ -1076,6 +1152,10 @@ hipError_t launch_learn_logistic(const double* beta, const double* eta, const do
     hipLaunchKernelGGL(learn_logistic_kernel, grid, dim3(SBR_LEARN_BLOCK), 0, s, beta, eta, t_end, a, L);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
+    if (a.fuse_hazard) {
+        hipLaunchKernelGGL(hazard_norm_kernel, dim3(a.n_beta), dim3(HN_BLOCK), 0, s, a, L);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(hazard_kernel, dim3(a.n_beta), dim3(HZ_BLOCK), 0, s, beta,
                        eta, a, L);
     return hipGetLastError();

@@ -30,7 +30,10 @@
 #define SBR_LEARN_PRIO_HI 1 // learning streams at the greatest stream priority
 #endif
 #ifndef SBR_LEARN_SLOTS
-#define SBR_LEARN_SLOTS 3
+#define SBR_LEARN_SLOTS 4 // learning workspaces of the pipelined batch
+#endif
+#ifndef SBR_LEARN_STREAMS
+#define SBR_LEARN_STREAMS 3 // learning streams (with the context stream: within GPU_MAX_HW_QUEUES = 4)
 #endif
 
 struct sbr_ctx {
@@ -44,13 +47,17 @@ struct sbr_ctx {
     // kLearnSlots slots, each learned on its own highest-priority stream, so the
     // learning of the next kLearnSlots-1 batches (latency-bound: 32 waves each) runs
     // concurrently with the equilibrium of the current one
+    // (workspace slots and streams are separate counts: grid k learns into slot k mod
+    // kLearnSlots on stream k mod kLearnStreams)
     static constexpr int kLearnSlots = SBR_LEARN_SLOTS;
-    // the hetero batch pipeline alternates two of these slots' streams/events
-    static_assert(kLearnSlots >= 2, "SBR_LEARN_SLOTS must be >= 2 (hetero batch pipeline)");
+    static constexpr int kLearnStreams = SBR_LEARN_STREAMS;
+    // the hetero batch pipeline alternates two of these slots' streams/events; single sweeps
+    // run their column chunks on the streams with slot events 0..kLearnStreams-1
+    static_assert(kLearnStreams >= 2 && kLearnSlots >= kLearnStreams, "SBR_LEARN_SLOTS >= SBR_LEARN_STREAMS >= 2");
     size_t ws_beta[kLearnSlots] = {}, ws_cap[kLearnSlots] = {};
     sbr::LearnBufs LW[kLearnSlots]{};
     int last_slot = 0;
-    hipStream_t lstream[kLearnSlots] = {};
+    hipStream_t lstream[kLearnStreams] = {};
     hipEvent_t ev_in = nullptr, ev_learned[kLearnSlots] = {}, ev_eq[kLearnSlots] = {};
     // fork/join fences between HIP's null stream and `stream`, and the end of the last call
     // (whatever stream it ran on) that every call waits for (CallFence)
@@ -188,16 +195,17 @@ void free_learn(sbr_ctx* c, int slot)
     c->ws_beta[slot] = c->ws_cap[slot] = 0;
 }
 
-int ensure_learn(sbr_ctx* c, size_t n_beta, size_t cap, int slot = 0)
+int ensure_learn(sbr_ctx* c, size_t n_beta, size_t cap, int slot = 0, bool hri = false)
 {
-    if (n_beta <= c->ws_beta[slot] && cap == c->ws_cap[slot]) return SBR_OK;
+    if (n_beta <= c->ws_beta[slot] && cap == c->ws_cap[slot] && (!hri || c->LW[slot].hrI)) return SBR_OK;
     free_learn(c, slot);
     sbr::LearnBufs& L = c->LW[slot];
     const size_t slab = n_beta * cap * sizeof(double);
     HIP_TRY(c, hipMalloc(&L.t, slab), SBR_ENOMEM);
     HIP_TRY(c, hipMalloc(&L.G, slab), SBR_ENOMEM);
     HIP_TRY(c, hipMalloc(&L.hr, slab), SBR_ENOMEM);
-    L.hrI = nullptr; // the hazard kernel scans in LDS (no HBM scratch row)
+    L.hrI = nullptr; // the hazard kernel scans in LDS; the fused hazard (batch) parks I here
+    if (hri) HIP_TRY(c, hipMalloc(&L.hrI, slab), SBR_ENOMEM);
     HIP_TRY(c, hipMalloc(&L.n_knots, n_beta * 4), SBR_ENOMEM);
     HIP_TRY(c, hipMalloc(&L.n_tau, n_beta * 4), SBR_ENOMEM);
     HIP_TRY(c, hipMalloc(&L.n_le, n_beta * 4), SBR_ENOMEM);
@@ -403,8 +411,9 @@ int ensure_pipe_streams(sbr_ctx* c)
     if (c->lstream[0]) return SBR_OK;
     int lo = 0, hi = 0;
     (void)hipDeviceGetStreamPriorityRange(&lo, &hi); // hi = greatest priority
-    for (int k = 0; k < sbr_ctx::kLearnSlots; k++) {
+    for (int k = 0; k < sbr_ctx::kLearnStreams; k++)
         HIP_TRY(c, hipStreamCreateWithPriority(&c->lstream[k], hipStreamNonBlocking, SBR_LEARN_PRIO_HI ? hi : lo), SBR_EDEVICE);
+    for (int k = 0; k < sbr_ctx::kLearnSlots; k++) {
         HIP_TRY(c, hipEventCreateWithFlags(&c->ev_learned[k], SBR_SYNC_EVENT_FLAGS), SBR_EDEVICE);
         HIP_TRY(c, hipEventCreateWithFlags(&c->ev_eq[k], SBR_SYNC_EVENT_FLAGS), SBR_EDEVICE);
     }
@@ -432,7 +441,12 @@ sbr::ResultSoA result_rows(const sbr::ResultSoA& r, size_t off)
 // stream: the equilibria of the chunks that finish learning early run while the slowest
 // chunk is still integrating.  Timing records: kind 0 = the learning stage of all chunks
 // (fork to the last chunk learned), kind 1 = the equilibrium tail after it.
-constexpr int kSweepChunks = sbr_ctx::kLearnSlots;
+constexpr int kSweepChunks = sbr_ctx::kLearnStreams;
+// pipelined batch: hazard_rate streamed by the learning kernel (no separate hazard launch
+// competing with the equilibrium kernel for CU slots); single sweeps keep the hazard kernel
+#ifndef SBR_FUSE_HAZARD
+#define SBR_FUSE_HAZARD 1
+#endif
 #ifndef SBR_SWEEP_FRONT
 #define SBR_SWEEP_FRONT 32 // 0: halving chunks only (A/B: 4.44 -> 4.25 ms per config-3 sweep)
 #endif
@@ -659,8 +673,9 @@ int sbr_free(sbr_ctx* c)
     for (int k = 0; k < sbr_ctx::kLearnSlots; k++) {
         if (c->ev_learned[k]) (void)hipEventDestroy(c->ev_learned[k]);
         if (c->ev_eq[k]) (void)hipEventDestroy(c->ev_eq[k]);
-        if (c->lstream[k]) (void)hipStreamDestroy(c->lstream[k]);
     }
+    for (int k = 0; k < sbr_ctx::kLearnStreams; k++)
+        if (c->lstream[k]) (void)hipStreamDestroy(c->lstream[k]);
     if (c->stage) (void)hipFree(c->stage);
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->ev_grid) (void)hipEventDestroy(e);
@@ -716,7 +731,7 @@ int sbr_sweep_baseline_batch_dev(sbr_ctx* c, void* stream, int64_t n_batch, cons
     sbr_opts o = resolve(opts);
     const int nslot = sbr_ctx::kLearnSlots;
     for (int k = 0; k < nslot && k < n_batch; k++) {
-        int rc = ensure_learn(c, (size_t)n_beta, (size_t)o.knot_capacity, k);
+        int rc = ensure_learn(c, (size_t)n_beta, (size_t)o.knot_capacity, k, SBR_FUSE_HAZARD != 0);
         if (rc) return rc;
     }
     {
@@ -731,17 +746,18 @@ int sbr_sweep_baseline_batch_dev(sbr_ctx* c, void* stream, int64_t n_batch, cons
     c->n_grid = 0;
     return fenced(c, stream, true, [&](hipStream_t s) -> int {
         const size_t np = (size_t)n_beta * (size_t)n_u;
-        sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, p, lambda, o.ode_maxiters, (int32_t)n_beta, 1, 0};
+        sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, p, lambda, o.ode_maxiters, (int32_t)n_beta, 1,
+                          SBR_FUSE_HAZARD};
         // inputs are ready once prior work on the caller's stream is
         HIP_TRY(c, hipEventRecord(c->ev_in, s), SBR_EDEVICE);
-        for (int k = 0; k < nslot; k++) HIP_TRY(c, hipStreamWaitEvent(c->lstream[k], c->ev_in, 0), SBR_EDEVICE);
+        for (int k = 0; k < sbr_ctx::kLearnStreams; k++) HIP_TRY(c, hipStreamWaitEvent(c->lstream[k], c->ev_in, 0), SBR_EDEVICE);
         for (int64_t k = 0; k < n_batch; k++) {
             const int slot = (int)(k % nslot);
             hipStream_t es = s; // one equilibrium stream (two alternating: 15% slower, r01_ab27)
 #ifdef SBR_AB_PIPE_SERIAL // A/B only: learning on the equilibrium stream (no overlap)
             hipStream_t ls = s;
 #else
-            hipStream_t ls = c->lstream[slot];
+            hipStream_t ls = c->lstream[k % sbr_ctx::kLearnStreams];
 #endif
             const double* bk = beta + k * n_beta;
             const double* ek = eta + k * n_beta;

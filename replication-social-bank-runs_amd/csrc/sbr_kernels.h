@@ -26,7 +26,7 @@ struct LearnArgs {
     int64_t maxiters;
     int32_t n_beta;
     int32_t stop_after_eta;
-    int32_t pad;
+    int32_t fuse_hazard; // learn_logistic_kernel: stream hazard_rate with the knots (needs hrI)
 };
 
 struct EqArgs {

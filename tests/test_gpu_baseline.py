@@ -208,6 +208,8 @@ def test_pipelined_batches_equal_single_sweeps(engine):
     base = sbr.fig5_grid(384)
     betas = np.stack([base.beta, base.beta[::-1], base.beta * 0.5, base.beta])
     etas = np.stack([np.full(384, 15.0), np.full(384, 10.0), np.full(384, 15.0), np.full(384, 7.5)])
+    etas[1, :7] = 40.0  # η past tspan: the hazard stage's BoundsError (fused into learning in the batch)
+    etas[2, 7:9] = 30.0  # η == t_end: the last knot is η itself
     tends = np.stack([np.full(384, 30.0), np.full(384, 30.0), np.full(384, 20.0), np.full(384, 30.0)])
     nbat, nb, nu = betas.shape[0], betas.shape[1], len(base.u)
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)

@@ -1,13 +1,13 @@
 #!/usr/bin/env bash
 # A/B of libsbr variants on one workload (+ optional parity subset first):
-#   TAG=x TESTS="-k hetero" VARIANTS="noxcd" BENCH_ARGS="--workload hetero --phases" bash tools/gpu_r02_ab.sh
+#   TAG=x TESTK="hetero" VARIANTS="noxcd" BENCH_ARGS="--workload hetero --phases" bash tools/gpu_r02_ab.sh
 set -u
 cd "${GRAFT_REPO_ROOT:-.}"
 OUT=gpurun_out/${TAG:-ab}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-if [ -n "${TESTS:-}" ]; then
-  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 170 --timeout-method thread $TESTS > "$OUT/pytest.log" 2>&1
+if [ -n "${TESTK:-}" ]; then
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 170 --timeout-method thread -k "$TESTK" > "$OUT/pytest.log" 2>&1
   rc=$?; tail -3 "$OUT/pytest.log"; [ $rc -ne 0 ] && exit $rc
 fi
 for v in base ${VARIANTS:-}; do
