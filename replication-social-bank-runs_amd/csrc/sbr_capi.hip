@@ -765,7 +765,11 @@ int sbr_sweep_baseline_batch_dev(sbr_ctx* c, void* stream, int64_t n_batch, cons
             // the slot's previous reader (equilibrium of batch k - nslot) must be done
             if (k >= nslot) HIP_TRY(c, hipStreamWaitEvent(ls, c->ev_eq[slot], 0), SBR_EDEVICE);
             hipEvent_t t0 = tstart(c, ls);
-            HIP_TRY(c, sbr::launch_learn_logistic(bk, ek, tk, la, c->LW[slot], ls), SBR_EDEVICE);
+            // the first grid's learning is the pipeline fill (nothing to overlap it with): the
+            // two-kernel hazard is shorter there; later grids stream it (off the critical path)
+            sbr::LearnArgs lk = la;
+            if (k == 0) lk.fuse_hazard = 0;
+            HIP_TRY(c, sbr::launch_learn_logistic(bk, ek, tk, lk, c->LW[slot], ls), SBR_EDEVICE);
             tend(c, ls, 0, t0);
             HIP_TRY(c, hipEventRecord(c->ev_learned[slot], ls), SBR_EDEVICE);
             HIP_TRY(c, hipStreamWaitEvent(es, c->ev_learned[slot], 0), SBR_EDEVICE);
