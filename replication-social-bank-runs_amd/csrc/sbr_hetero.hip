@@ -1130,6 +1130,9 @@ __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const d
 #ifndef SBR_HET_XCD
 #define SBR_HET_XCD 1
 #endif
+#ifndef SBR_HET_EQ_PRIO
+#define SBR_HET_EQ_PRIO 2 // equilibrium waves ahead of the co-resident learning waves (config-4 step 49.7 -> 47.9 ms)
+#endif
 template <int K, int BLOCK>
 #ifndef SBR_HET_MINW
 #define SBR_HET_MINW 2 // waves per SIMD: two 4-wave workgroups per CU (LDS slab: SBR_HET_LDS in sbr_capi.hip)
@@ -1142,6 +1145,9 @@ __global__ __launch_bounds__(BLOCK, SBR_HET_MINW) void equilibrium_hetero_kernel
                                                                    double* __restrict__ tout_out)
 {
     extern __shared__ double smem[];
+#if SBR_HET_EQ_PRIO
+    __builtin_amdgcn_s_setprio(SBR_HET_EQ_PRIO); // A/B: issue priority over co-resident learning waves
+#endif
 #if SBR_HET_XCD
     // XCD-aware tile order (1-D grid): workgroup w runs on XCD w mod 8, so the u-tiles of one
     // column are given to consecutive workgroups of the same XCD — they share that XCD's L2
