@@ -203,6 +203,9 @@ constexpr int EQ_TILE = SBR_EQ_TILE;  // u values per equilibrium block (one blo
 #ifndef SBR_EQ_REVERSE
 #define SBR_EQ_REVERSE 0 // A/B: dispatch the β columns last to first
 #endif
+#ifndef SBR_EQ_PRIO
+#define SBR_EQ_PRIO 0
+#endif
 #ifndef SBR_AW_WIN
 #define SBR_AW_WIN 6
 #endif
@@ -981,6 +984,9 @@ __global__ __launch_bounds__(BLOCK, INTEREST ? 1 : SBR_EQ_MINW) void equilibrium
                                                             ResultSoA out)
 {
     extern __shared__ double smem[];
+#if SBR_EQ_PRIO
+    __builtin_amdgcn_s_setprio(SBR_EQ_PRIO); // A/B: issue priority over co-resident learning waves
+#endif
     const int b = SBR_EQ_REVERSE ? (int)(gridDim.y - 1 - blockIdx.y) : (int)blockIdx.y;
     const int n = L.n_knots[b], ntau = L.n_tau[b], nle = L.n_le[b];
     const uint32_t lst = L.status[b];
