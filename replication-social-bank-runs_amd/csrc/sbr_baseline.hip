@@ -206,8 +206,11 @@ constexpr int EQ_TILE = SBR_EQ_TILE;  // u values per equilibrium block (one blo
 #ifndef SBR_EQ_PRIO
 #define SBR_EQ_PRIO 0
 #endif
+#ifndef SBR_AW_SLOPE
+#define SBR_AW_SLOPE 0 // A/B: slope bounds (one exact knot + slope tables) before evaluating an 8-block (bit-exact, slower: r02_slope)
+#endif
 #ifndef SBR_AW_WIN
-#define SBR_AW_WIN 6
+#define SBR_AW_WIN (SBR_AW_SLOPE ? 1 : 6)
 #endif
 constexpr int kAwWin = SBR_AW_WIN; // 8-blocks each side of the predicted AW peak evaluated first
 
@@ -467,6 +470,10 @@ struct Summ {
     const double* smc;
     bool mono; // G nondecreasing over the knots (no NaN): prefix max / suffix min are knot values
     double t_half; // time where G crosses 1/2 (lerp inverse), NaN if it does not: AW peak predictor
+    // mono only (they reuse pmc/smc): per 8-interval block, the largest / smallest knot-interval
+    // slope (G[k+1] − G[k]) / (t[k+1] − t[k]), widened by 1e-12 relative
+    const double* smax;
+    const double* smin;
 };
 
 template <class P>
@@ -630,6 +637,9 @@ __device__ __forceinline__ void solve_from_buffers(P T, P G, P H, const Summ& S,
     auto brk_a = [&](int i) { ra_j = ssl_near(T, n, ra_j + (i - ra_i), xa_of(i)); ra_i = i; return ra_j; };
     auto brk_b = [&](int i) { rb_j = ssl_near(T, n, rb_j + (i - rb_i), xb_of(i)); rb_i = i; return rb_j; };
     // exact AW_cum(τ̄_i) for i in [i0, i1), folded into the NaN-propagating max
+#if SBR_AW_SLOPE
+    double last_v = NAN;
+#endif
     auto eval_range = [&](int i0, int i1) {
         // The brackets of a(τ̄_i) and b(τ̄_i) only move forward with i: keep each bracket's
         // two knots (t, G) in registers and slide them, so a knot costs the LDS loads of
@@ -662,6 +672,9 @@ __device__ __forceinline__ void solve_from_buffers(P T, P G, P H, const Summ& S,
             if ((diag & 4) && ((i & 7) == 0 || i == i0)) nblk_eval++;
             if (aw_path) aw_path[i] = v;
             if (mx == mx && (v != v || v > mx)) mx = v;
+#if SBR_AW_SLOPE
+            last_v = v;
+#endif
         }
         ra_j = ka; ra_i = i1 - 1;
         rb_j = kb; rb_i = i1 - 1;
@@ -693,6 +706,31 @@ __device__ __forceinline__ void solve_from_buffers(P T, P G, P H, const Summ& S,
                 return ((ub_out - lb_in) + G0) + 1e-14;
             };
             auto end_of = [&](int i0, int w) { return i0 + w < ntau ? i0 + w : ntau; };
+#if SBR_AW_SLOPE
+            // Slope bound of AW_cum over knots [i0, ie) once AW_cum(τ̄_i0) = v0 is known exactly:
+            // G is piecewise linear, so G(b_i) − G(b_i0) ≤ Smax_b·(b_i − b_i0) and
+            // G(a_i) − G(a_i0) ≥ Smin_a·(a_i − a_i0) with the slope extremes over the knot
+            // intervals the arguments cross; b_i − b_i0 and a_i − a_i0 are both τ̄_i − τ̄_i0 up to
+            // the rounding of the shifted arguments (ε ≤ 8 ulp of their magnitude), so
+            // AW_cum(τ̄_i) ≤ v0 + max(0, Smax_b − Smin_a)·(a_ie−1 − a_i0) + Smax_b·ε (+ a margin
+            // for the interpolation roundings).  Near the maximum the two slopes nearly cancel
+            // (the peak is where g(b) = g(a)), so this is far tighter there than the
+            // knot-value bound; requires a_i0, b_i0 ≥ 0 (no masked term) and a monotone G.
+            auto slope_ub = [&](int i0, int ie, double v0) -> double {
+                const double ta0 = tau(i0), ta1 = tau(ie - 1);
+                const double av0 = (ta0 - xi) + icc, av1 = (ta1 - xi) + icc;
+                const double bv1 = (ta1 - xi) + occ;
+                int ka0 = brk_a(i0), ka1 = brk_a(ie - 1), kb0 = brk_b(i0), kb1 = brk_b(ie - 1);
+                ka0 = ka0 < n - 2 ? ka0 : n - 2; ka1 = ka1 < n - 2 ? ka1 : n - 2;
+                kb0 = kb0 < n - 2 ? kb0 : n - 2; kb1 = kb1 < n - 2 ? kb1 : n - 2;
+                double smx = 0.0, smn = INFINITY;
+                for (int g = kb0 >> 3; g <= (kb1 >> 3); g++) smx = dmax(smx, S.smax[g]);
+                for (int g = ka0 >> 3; g <= (ka1 >> 3); g++) smn = dmin(smn, S.smin[g]);
+                const double mag = fabs(ta1) + fabs(xi) + fabs(icc) + fabs(occ) + fabs(bv1);
+                const double eps = mag * 4e-15;
+                return ((v0 + (dmax(0.0, smx - smn) * (av1 - av0)) * (1.0 + 1e-12)) + smx * eps) + 1e-14;
+            };
+#endif
             // pass 1: a first running maximum.  For a logistic-shaped CDF the continuous
             // maximiser of G(τ − s_out) − G(τ − s_in) sits where G(τ − s_out) + G(τ − s_in) = 1,
             // i.e. at τ* = t_half + (s_in + s_out)/2: evaluate the 8-blocks around it
@@ -737,6 +775,14 @@ __device__ __forceinline__ void solve_from_buffers(P T, P G, P H, const Summ& S,
                     for (int i0 = k0; i0 < ke && !flag && mx == mx; i0 += 8) {
                         const int ie = end_of(i0, 8);
                         if (i0 == b8 || (i0 >= w0 && ie <= w1) || ub_rng(i0, ie - 1) <= mx) continue;
+#if SBR_AW_SLOPE
+                        if (S.smax && ie - i0 > 1 && ((tau(i0) - xi) + icc) >= 0.0 && ((tau(i0) - xi) + occ) >= 0.0) {
+                            eval_range(i0, i0 + 1);
+                            if (flag || mx != mx || slope_ub(i0, ie, last_v) <= mx) continue;
+                            eval_range(i0 + 1, ie);
+                            continue;
+                        }
+#endif
                         eval_range(i0, ie);
                     }
                 }
@@ -1021,7 +1067,7 @@ __global__ __launch_bounds__(BLOCK, INTEREST ? 1 : SBR_EQ_MINW) void equilibrium
             for (int i = threadIdx.x; i < ntau; i += BLOCK) sH[i] = gH[i];
     }
     __syncthreads();
-    Summ S{nullptr, nullptr, nullptr, nullptr, false, (double)NAN};
+    Summ S{nullptr, nullptr, nullptr, nullptr, false, (double)NAN, nullptr, nullptr};
     if (fits && !a.exhaustive) {
         const int nbh = (ntau + 63) >> 6, nbg = (n + 7) >> 3;
         // HR summaries: 8 lanes per 64-entry block, 8 independent loads each (HR is read from
@@ -1070,6 +1116,22 @@ __global__ __launch_bounds__(BLOCK, INTEREST ? 1 : SBR_EQ_MINW) void equilibrium
             }
         }
         __syncthreads();
+#if SBR_AW_SLOPE
+        // monotone G: the prefix/suffix tables are unused — the same slots hold the per-block
+        // slope extremes for the AW slope bounds
+        if (!s_nonmono)
+            for (int g = threadIdx.x; g < nbg; g += BLOCK) {
+                double mx = 0.0, mn = INFINITY;
+                const int e = (g << 3) + 8 < n - 1 ? (g << 3) + 8 : n - 1;
+                for (int k = g << 3; k < e; k++) {
+                    const double sl = (sG[k + 1] - sG[k]) / (sT[k + 1] - sT[k]);
+                    mx = sl > mx ? sl : mx;
+                    mn = sl < mn ? sl : mn;
+                }
+                pmc[g] = mx * (1.0 + 1e-12);
+                smc[g] = mn * (1.0 - 1e-12);
+            }
+#endif
         // prefix max / suffix min over blocks (NaN-propagating), two waves at once
         if (threadIdx.x == 0) {
             // t_half: first knot interval with G[k] <= 1/2 < G[k+1] (heuristic only)
@@ -1095,7 +1157,8 @@ __global__ __launch_bounds__(BLOCK, INTEREST ? 1 : SBR_EQ_MINW) void equilibrium
             }
         }
         __syncthreads();
-        S = Summ{hmax, hmin, pmc, smc, s_nonmono == 0, s_thalf};
+        S = Summ{hmax, hmin, pmc, smc, s_nonmono == 0, s_thalf, SBR_AW_SLOPE && s_nonmono == 0 ? pmc : nullptr,
+                 SBR_AW_SLOPE && s_nonmono == 0 ? smc : nullptr};
     }
     // Points are handed out to waves 64 at a time from an LDS counter, so a
     // wave that drew cheap no-run points goes back for more instead of idling
