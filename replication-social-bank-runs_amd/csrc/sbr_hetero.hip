@@ -423,6 +423,9 @@ __global__ __launch_bounds__(64) void learn_hetero_kernel(const double* __restri
 #ifndef SBR_HET_LEARN_WAVE
 #define SBR_HET_LEARN_WAVE 1 // 0: learn_hetero_kernel (one lane per column, A/B)
 #endif
+#ifndef SBR_HET_DIVRCP
+#define SBR_HET_DIVRCP 0 // LU back substitutions by refined pivot reciprocals (A/B)
+#endif
 __device__ __forceinline__ double wave_bcast(double v, int l)
 {
     const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
@@ -499,7 +502,27 @@ struct WaveLU {
                 A[j] = lane > k ? v : A[j];
             }
         }
+#if SBR_HET_DIVRCP
+        // this lane's pivot U_ll and its refined reciprocal, for the back substitutions
+        double dg = A[0];
+#pragma unroll
+        for (int j = 1; j < K; j++) dg = j == lane ? A[j] : dg;
+        rdiag = rcp_refined(dg);
+        okd = in_div_range(dg) ? 1 : 0;
+#endif
     }
+#if SBR_HET_DIVRCP
+    double rdiag;
+    int okd;
+    // |x| in [2^-400, 2^400]: with both operands there the division sequence needs no scaling
+    // and its intermediates neither overflow nor underflow, so div_rcp (the compiler's IEEE
+    // sequence without its identity scale / fixup steps) is the correctly rounded quotient
+    static __device__ __forceinline__ bool in_div_range(double x)
+    {
+        const double ax = fabs(x);
+        return ax >= 0x1p-400 && ax <= 0x1p400;
+    }
+#endif
     // b: this lane's component of the right-hand side, overwritten with the solution's
     __device__ __forceinline__ void solve(double& b, int lane) const
     {
@@ -519,7 +542,17 @@ struct WaveLU {
         }
 #pragma unroll
         for (int j = K - 1; j >= 0; j--) {
+#if SBR_HET_DIVRCP
+            // lane j: b_j / U_jj, by the refined reciprocal when both operands are in range
+            // (wave-uniform choice on lane j's operands), else the IEEE division
+            const int fast = __builtin_amdgcn_readlane((okd & (b == 0.0 || in_div_range(b))) ? 1 : 0, j);
+            double q;
+            if (fast) q = div_rcp(b, A[j], rdiag);
+            else q = b / A[j];
+            const double bj = wave_bcast(q, j);
+#else
             const double bj = wave_bcast(b / A[j], j); // lane j: b_j / A[j][j]
+#endif
             b = lane == j ? bj : b;
             const double v = fma(-bj, A[j], b);
             b = lane < j ? v : b;

@@ -7,8 +7,11 @@ OUT=gpurun_out/${TAG:-ab}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 if [ -n "${TESTK:-}" ]; then
+  # TESTLIB=<variant>: run the parity subset against that build (bit-exactness of a candidate)
+  if [ -n "${TESTLIB:-}" ]; then export SBR_LIB=replication-social-bank-runs_amd/lib_var/$TESTLIB/libsbr.so; fi
   timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 170 --timeout-method thread -k "$TESTK" > "$OUT/pytest.log" 2>&1
   rc=$?; tail -3 "$OUT/pytest.log"; [ $rc -ne 0 ] && exit $rc
+  unset SBR_LIB
 fi
 for v in base ${VARIANTS:-}; do
   if [ "$v" = base ]; then lib=replication-social-bank-runs_amd/lib/libsbr.so; else lib=replication-social-bank-runs_amd/lib_var/$v/libsbr.so; fi
