@@ -1349,7 +1349,10 @@ namespace {
 constexpr int kSocialDefaultCap = 98304;  // ≈1.4× the typical longest iterate on config 5 (≈70k knots)
 constexpr int kSocialMaxCap = 1 << 22;    // overflow retries grow 4× per pass up to this
 constexpr int64_t kPoolSlots = 256;       // promotion pool slots (points that outgrow the capacity)
-constexpr int kSocialInner = 16;          // fixed-point iterates per launch (compaction in between)
+#ifndef SBR_SOCIAL_INNER
+#define SBR_SOCIAL_INNER 16
+#endif
+constexpr int kSocialInner = SBR_SOCIAL_INNER; // fixed-point iterates per launch (compaction in between)
 
 int social_checks(sbr_ctx* c, const double* beta, const double* eta, const double* u, int64_t n_beta, int64_t n_u,
                   double x0, double p, double kappa, double lambda, const double* cmp, int32_t n_cmp, double tol,

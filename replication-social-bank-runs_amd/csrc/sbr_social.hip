@@ -728,18 +728,30 @@ __device__ __forceinline__ bool social_iterate(const SocialArgs& a, int l, int i
 // picked up here or by the next launch; either way it redoes that iterate).
 // args[0]: the main worklist's arguments, args[1]: the pool's (n_pts = 0: none),
 // in device memory so that the wave-uniform choice between them stays scalar loads.
+#ifndef SBR_SOCIAL_WAVES
+#define SBR_SOCIAL_WAVES 1024 // A/B: 0 = dense waves (64 worklist entries each, the round-1 layout)
+#endif
+// Main blocks (one wave each) spread the live worklist over all `nbs` of them: L = ⌈live/nbs⌉
+// consecutive entries per wave (L ≤ 64), lanes ≥ L idle.  A fixed-point lane's RK step is a
+// serial chain whose memory side grows with the wave's active lanes (each lane streams its own
+// knot lines: a wave load touches one line per active lane), so as points retire the
+// survivors run in ever sparser waves, down to one per wave — and with nbs = one wave per
+// SIMD the bulk uses every SIMD instead of half of them.
 __global__ __launch_bounds__(64) void social_iter_kernel(const SocialArgs* __restrict__ args, int iter_arg,
                                                          int n_inner, const int32_t* __restrict__ work,
-                                                         const int32_t* __restrict__ count)
+                                                         const int32_t* __restrict__ count, int nbs)
 {
     const SocialArgs& sa = args[0];
     const SocialArgs& pa = args[1];
-    const int nbs = (sa.n_pts + 63) >> 6;
     const bool in_pool = (int)blockIdx.x >= nbs;
     int l, iter;
     if (!in_pool) {
-        const int w = blockIdx.x * 64 + threadIdx.x;
-        if (w >= *count) return;
+        const int cnt = *count;
+        int L = SBR_SOCIAL_WAVES ? (cnt + nbs - 1) / nbs : 64;
+        L = L < 1 ? 1 : (L > 64 ? 64 : L);
+        if ((int)threadIdx.x >= L) return;
+        const int w = blockIdx.x * L + threadIdx.x;
+        if (w >= cnt) return;
         l = work[w];
         if (!sa.live[l]) return; // retired by the init kernel (knot overflow)
         iter = iter_arg;
@@ -808,8 +820,13 @@ hipError_t launch_social_iter(const SocialArgs& a, const SocialArgs& p, const So
                               int n_inner, const int32_t* work, const int32_t* count, int32_t* work_out,
                               int32_t* count_out, hipStream_t s)
 {
-    hipLaunchKernelGGL(social_iter_kernel, dim3((a.n_pts + 63) / 64 + (p.n_pts + 63) / 64), dim3(64), 0, s,
-                       args_dev, iter, n_inner, work, count);
+    // main blocks: one wave per SIMD of the MI355X (4 × 256), at least one wave per 64 points
+    // and no more than one per point
+    int nbs = (a.n_pts + 63) / 64;
+    nbs = nbs > SBR_SOCIAL_WAVES ? nbs : SBR_SOCIAL_WAVES;
+    nbs = nbs < a.n_pts ? nbs : (a.n_pts > 0 ? a.n_pts : 1);
+    hipLaunchKernelGGL(social_iter_kernel, dim3(nbs + (p.n_pts + 63) / 64), dim3(64), 0, s, args_dev, iter, n_inner,
+                       work, count, nbs);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(social_compact_kernel, dim3(1), dim3(CMP_BLOCK), 0, s, work, count, a.live, work_out,
