@@ -29,6 +29,9 @@ namespace sbr {
 #ifndef SBR_LEARN_BLOCK
 #define SBR_LEARN_BLOCK 64
 #endif
+#ifndef SBR_LEARN_LANES
+#define SBR_LEARN_LANES 64 // columns per wave of learn_logistic_kernel
+#endif
 __global__ __launch_bounds__(SBR_LEARN_BLOCK) void learn_logistic_kernel(const double* __restrict__ beta,
                                                             const double* __restrict__ eta,
                                                             const double* __restrict__ t_end, LearnArgs a,
@@ -39,8 +42,11 @@ __global__ __launch_bounds__(SBR_LEARN_BLOCK) void learn_logistic_kernel(const d
 #ifndef SBR_LEARN_NOPRIO
     __builtin_amdgcn_s_setprio(3);
 #endif
-    const int b = blockIdx.x * SBR_LEARN_BLOCK + threadIdx.x;
-    const bool live = b < a.n_beta;
+    // SBR_LEARN_LANES columns per wave (lanes beyond idle): a knot store or load of the wave
+    // touches one row per active lane
+    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    const int b = (blockIdx.x * (SBR_LEARN_BLOCK / 64) + wv) * SBR_LEARN_LANES + ln;
+    const bool live = ln < SBR_LEARN_LANES && b < a.n_beta;
     const double BETA = live ? beta[b] : 1.0, ETA = live ? eta[b] : 1.0, T1 = live ? t_end[b] : 1.0, T0 = 0.0;
     const size_t row = (size_t)(live ? b : 0) * (size_t)L.cap;
     double* __restrict__ T = L.t + row;
@@ -1217,7 +1223,8 @@ __global__ __launch_bounds__(BLOCK, INTEREST ? 1 : SBR_EQ_MINW) void equilibrium
 hipError_t launch_learn_logistic(const double* beta, const double* eta, const double* t_end, const LearnArgs& a,
                                  const LearnBufs& L, hipStream_t s)
 {
-    dim3 grid((a.n_beta + SBR_LEARN_BLOCK - 1) / SBR_LEARN_BLOCK);
+    constexpr int per_block = (SBR_LEARN_BLOCK / 64) * SBR_LEARN_LANES;
+    dim3 grid((a.n_beta + per_block - 1) / per_block);
     hipLaunchKernelGGL(learn_logistic_kernel, grid, dim3(SBR_LEARN_BLOCK), 0, s, beta, eta, t_end, a, L);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
