@@ -428,6 +428,9 @@ __global__ __launch_bounds__(64) void learn_hetero_kernel(const double* __restri
 #endif
 __device__ __forceinline__ double wave_bcast(double v, int l)
 {
+#if SBR_HET_BCAST_SHFL // A/B: through the LDS crossbar into VGPRs instead of SGPRs
+    return __shfl(v, l, 64);
+#endif
     const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
     const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
     return __hiloint2double(hi, lo);
