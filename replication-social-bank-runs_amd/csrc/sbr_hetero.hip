@@ -1166,6 +1166,9 @@ __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const d
 #ifndef SBR_HET_XCD
 #define SBR_HET_XCD 1
 #endif
+#ifndef SBR_HET_BLOCK
+#define SBR_HET_BLOCK 256 // u points per hetero equilibrium workgroup (A/B: 512)
+#endif
 #ifndef SBR_HET_EQ_PRIO
 #define SBR_HET_EQ_PRIO 2 // equilibrium waves ahead of the co-resident learning waves (config-4 step 49.7 -> 47.9 ms)
 #endif
@@ -1324,8 +1327,9 @@ static hipError_t launch_hetero_k(const double* betas, const double* dist, const
     ea.n_col = la.n_beta;
 #if SBR_HET_XCD
     const unsigned ncol8 = (unsigned)((la.n_beta + 7) / 8) * 8;
-    if (ea.n_u >= 256) {
-        hipLaunchKernelGGL((equilibrium_hetero_kernel<K, 256>), dim3(((ea.n_u + 255) / 256) * ncol8), dim3(256), lds, s,
+    if (ea.n_u >= SBR_HET_BLOCK) {
+        hipLaunchKernelGGL((equilibrium_hetero_kernel<K, SBR_HET_BLOCK>), dim3(((ea.n_u + SBR_HET_BLOCK - 1) / SBR_HET_BLOCK) * ncol8),
+                           dim3(SBR_HET_BLOCK), lds, s,
                            L, dist, eta, t_end, u, ea, out, tin, tout);
     } else {
         hipLaunchKernelGGL((equilibrium_hetero_kernel<K, 64>), dim3(((ea.n_u + 63) / 64) * ncol8), dim3(64), lds, s,
