@@ -180,6 +180,9 @@ __device__ bool promote(const SocialArgs& a, int l, int64_t g, int iter, BView T
     return true;
 }
 
+#ifndef SBR_SOCIAL_PF
+#define SBR_SOCIAL_PF 32 // knots ahead of the step that `accepted` touches (A/B)
+#endif
 // dG/dt = (1 − G) β AW_old(t) (social_learning_dynamics.jl:61-67).  All stage
 // times of a step (t + c_i·dt, t + dt) are known when the step starts, so the
 // five AW_old lookups are done up front (prepare): brackets from the register
@@ -280,7 +283,7 @@ struct SocialRhs {
             const int j = w.find_advance(t);
 #ifndef SBR_SOCIAL_NO_PREFETCH
             slow += (pf_t == -1.0 || pf_v == -2.0) ? 1 : 0;
-            const int q = j + 32 < n ? j + 32 : n - 1;
+            const int q = j + SBR_SOCIAL_PF < n ? j + SBR_SOCIAL_PF : n - 1;
             pf_t = to[q];
             pf_v = vo[q];
 #else
