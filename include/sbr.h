@@ -187,6 +187,18 @@ int sbr_solve_point_paths(sbr_ctx* ctx, double beta, double eta, double t_end, d
  * buffers go to tau_in/tau_out ([n_col*n_u][K], may be NULL).  The caller
  * resolves η = η_bar / Σ dist·βs per column (heterogeneity_model.jl:131-132).
  */
+/*
+ * Heterogeneity learning only — solve_SInetwork_hetero (heterogeneity_learning.jl:49-94) for
+ * n_col columns at once (column c: group rates betas[c*K .. c*K+K), tspan = (0, t_end[c])):
+ * the shared knot grid t (row c at [c*cap ..]) and the group CDFs G (row c at [c*cap*K ..],
+ * knot-major: G[c][i][k]) of the AutoTsit5(Rosenbrock23()) solution at eps() tolerance, run to
+ * t_end like the reference; the PDFs follow from compute_pdf_hetero (:114-134).  Validation
+ * mirrors LearningParametersHetero (heterogeneity_model.jl:33-41).  Host pointers; synchronous.
+ */
+int sbr_learn_hetero(sbr_ctx* ctx, int32_t K, const double* betas, const double* dist, const double* t_end, double x0,
+                     int64_t n_col, const sbr_opts* opts, double* t_out, double* G_out, int64_t cap, int32_t* n_knots,
+                     uint32_t* status);
+
 int sbr_sweep_hetero(sbr_ctx* ctx, int32_t K, const double* betas, const double* dist, const double* eta,
                      const double* t_end, double x0, const double* u, int64_t n_col, int64_t n_u, double p,
                      double kappa, double lambda, const sbr_opts* opts, sbr_result_soa* out, double* tau_in,
@@ -261,12 +273,15 @@ int sbr_sweep_social_dev(sbr_ctx* ctx, void* stream, const double* beta, const d
 /* One social-learning fixed point with the learning knots t[n], G[n] of the
  * returned SolvedModel (the last inner equilibrium, social_learning_solver.jl:262)
  * — with ξ, τ̄_IN, τ̄_OUT they rebuild the AW curves scripts/4_social_learning.jl
- * plots (get_AW on τ̄ = knots ≤ η (+ η)).  res = {ξ, τ̄_IN, τ̄_OUT, AW_max, tol};
- * t / G hold `cap` doubles; SBR_EARG if the knots do not fit. */
+ * plots (get_AW on τ̄ = knots ≤ η (+ η)).  aw_old (may be NULL) receives
+ * AW_{n-1}(t_i), the forcing that drove that iterate, so that the caller rebuilds
+ * its learning_pdf = (1 − G)·β·AW_{n-1} (compute_pdf_social_learning,
+ * social_learning_dynamics.jl:98-114) and HR.  res = {ξ, τ̄_IN, τ̄_OUT, AW_max, tol};
+ * t / G / aw_old hold `cap` doubles; SBR_EARG if the knots do not fit. */
 int sbr_social_point_paths(sbr_ctx* ctx, double beta, double eta, double x0, double u, double p, double kappa,
                            double lambda, const double* cmp_grid, int32_t n_cmp, double tol, int32_t max_iter,
                            const sbr_opts* opts, double* res, uint32_t* status, int32_t* fp_iters, double* t,
-                           double* G, int64_t cap, int64_t* n_knots);
+                           double* G, double* aw_old, int64_t cap, int64_t* n_knots);
 /* Workspace budget in bytes for social sweeps (0 = 60 % of free HBM at call time). */
 int sbr_set_social_workspace(sbr_ctx* ctx, int64_t bytes);
 /* Diagnostics: sums over the points of the last social sweep run with

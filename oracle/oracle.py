@@ -237,23 +237,25 @@ def sweep_social(beta, eta, u, p, kappa, lam, cmp, x0=1e-4, tol=1e-4, max_iter=5
 
 def social_point(beta, eta, u, p, kappa, lam, cmp, x0=1e-4, tol=1e-4, max_iter=500, cap=1 << 18):
     """One solve_equilibrium_social_learning point with the last iterate's
-    learning knots (t, G) and HR grid τ̄ (to rebuild the plotted AW paths)."""
+    learning knots (t, G), AW_{n-1} at those knots and HR grid τ̄ (to rebuild the plotted
+    AW paths and the SolvedModel's learning_pdf / HR)."""
     L = lib()
     L.sbro_social_point.restype = _I64
-    L.sbro_social_point.argtypes = [_D, _D, _D, _D, _D, _D, _D, _P, _I32, _D, _I32, _P, _P, _P, _P, _P, _P, _I64, _P]
+    L.sbro_social_point.argtypes = [_D, _D, _D, _D, _D, _D, _D, _P, _I32, _D, _I32, _P, _P, _P, _P, _P, _P, _P, _I64,
+                                    _P]
     cmp = np.ascontiguousarray(cmp, np.float64)
     res = np.zeros(5)
     st = np.zeros(1, np.uint32)
     fi = np.zeros(1, np.int32)
-    t, G, tau = np.empty(cap), np.empty(cap), np.empty(cap)
+    t, G, tau, awo = np.empty(cap), np.empty(cap), np.empty(cap), np.empty(cap)
     ntau = np.zeros(1, np.int64)
     n = L.sbro_social_point(beta, eta, x0, u, p, kappa, lam, _ptr(cmp), len(cmp), tol, max_iter, _ptr(res), _ptr(st),
-                            _ptr(fi), _ptr(t), _ptr(G), _ptr(tau), cap, _ptr(ntau))
+                            _ptr(fi), _ptr(t), _ptr(G), _ptr(tau), _ptr(awo), cap, _ptr(ntau))
     if n < 0:
         raise RuntimeError(f"oracle social path buffer too small ({-n} needed)")
     k = int(ntau[0])
     return dict(xi=res[0], tau_in_unc=res[1], tau_out_unc=res[2], aw_max=res[3], tol=res[4], status=int(st[0]),
-                fp_iters=int(fi[0]), t=t[:n].copy(), G=G[:n].copy(), hr_tau=tau[:k].copy())
+                fp_iters=int(fi[0]), t=t[:n].copy(), G=G[:n].copy(), hr_tau=tau[:k].copy(), aw_old=awo[:n].copy())
 
 
 def sweep_interest(beta, eta, t_end, u, p, kappa, lam, r, delta, x0=1e-4, max_iters=100, nthreads=0):

@@ -1160,6 +1160,7 @@ static void jac_social(void* ctx, double t, const double* x, double* J, double* 
  * steps, Σ rejected steps, max knots over iterates}. */
 typedef struct {
     double *t, *G, *tau; /* last iterate's learning knots and HR grid (caller-allocated, cap each) */
+    double* awo;         /* AW_{n-1} at those knots: the forcing of learning_pdf (may be NULL) */
     int64_t cap, n, n_tau;
 } social_paths_t;
 
@@ -1226,6 +1227,7 @@ static void social_point(double beta, double eta, double x0, double u, double p,
                 memcpy(paths->t, kn.t, (size_t)n * sizeof(double));
                 memcpy(paths->G, kn.x, (size_t)n * sizeof(double));
                 memcpy(paths->tau, h.tau, (size_t)h.n * sizeof(double));
+                if (paths->awo) memcpy(paths->awo, awo, (size_t)n * sizeof(double));
             }
         }
         if (r.status & SBR_OOB) { stop_oob = 1; }
@@ -1315,9 +1317,9 @@ int sbro_sweep_social(const double* beta, const double* eta, double x0, const do
 int64_t sbro_social_point(double beta, double eta, double x0, double u, double p, double kappa, double lambda,
                           const double* cmp, int32_t n_cmp, double tol, int32_t max_iter, double* res,
                           uint32_t* status, int32_t* fp_iters, double* t_out, double* G_out, double* tau_out,
-                          int64_t cap, int64_t* n_tau)
+                          double* awo_out, int64_t cap, int64_t* n_tau)
 {
-    social_paths_t sp = {t_out, G_out, tau_out, cap, 0, 0};
+    social_paths_t sp = {t_out, G_out, tau_out, awo_out, cap, 0, 0};
     point_t r;
     social_point(beta, eta, x0, u, p, kappa, lambda, cmp, n_cmp, tol, max_iter, 100, &r, fp_iters, NULL, &sp);
     res[0] = r.xi; res[1] = r.tin; res[2] = r.tout; res[3] = r.aw_max; res[4] = r.tol;

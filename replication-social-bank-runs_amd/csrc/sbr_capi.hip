@@ -83,7 +83,7 @@ struct sbr_ctx {
     int64_t *pl_steps = nullptr, *pl_pts = nullptr;
     int32_t* so_count_host = nullptr; // pinned
     double* het_aw_path = nullptr;      // set only inside sbr_hetero_point_paths
-    double *so_path_t = nullptr, *so_path_G = nullptr; // set only inside sbr_social_point_paths
+    double *so_path_t = nullptr, *so_path_G = nullptr, *so_path_aw = nullptr; // set only inside sbr_social_point_paths
     int32_t* so_path_n = nullptr;
     int32_t so_path_cap = 0;
     sbr::SocialArgs* so_args_dev = nullptr;  // {main, pool} arguments of the iterate kernel
@@ -1116,6 +1116,60 @@ int sbr_hetero_learn_stats(sbr_ctx* c, int64_t n_col, int32_t* n_knots, int32_t*
     return SBR_OK;
 }
 
+int sbr_learn_hetero(sbr_ctx* c, int32_t K, const double* betas, const double* dist, const double* t_end, double x0,
+                     int64_t n_col, const sbr_opts* opts, double* t_out, double* G_out, int64_t cap, int32_t* n_knots,
+                     uint32_t* status)
+{
+    SBR_ON_RANK0(c, sbr_learn_hetero(c, K, betas, dist, t_end, x0, n_col, opts, t_out, G_out, cap, n_knots, status));
+    if (!c || !betas || !dist || !t_end || n_col <= 0 || n_col > (1 << 30) || cap <= 0) return SBR_EARG;
+    if (K != 1 && K != 2 && K != 3 && K != 4 && K != 8) return fail(c, SBR_EARG, "K must be 1, 2, 3, 4 or 8");
+    // LearningParametersHetero checks (heterogeneity_model.jl:33-41)
+    double dsum = 0.0;
+    for (int k = 0; k < K; k++) {
+        if (!(dist[k] >= 0.0)) return fail(c, SBR_EARG, "ArgumentError: distribution weights must be non-negative");
+        dsum = dsum + dist[k];
+    }
+    if (!(fabs(dsum - 1.0) < 1e-10)) return fail(c, SBR_EARG, "ArgumentError: distribution must sum to 1");
+    for (int64_t i = 0; i < n_col * K; i++)
+        if (!(betas[i] > 0.0)) return fail(c, SBR_EARG, "ArgumentError: all learning rates must be positive");
+    for (int64_t i = 0; i < n_col; i++)
+        if (!(t_end[i] > 0.0)) return fail(c, SBR_EARG, "ArgumentError: End time must be greater than start time");
+    if (!(x0 >= 0.0)) return fail(c, SBR_EARG, "ArgumentError: Initial condition must be non-negative");
+    if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
+    sbr_opts o = resolve(opts);
+    if (cap < o.knot_capacity) o.knot_capacity = (int32_t)cap;
+    int rc = ensure_hetero(c, (size_t)n_col, (size_t)o.knot_capacity, (size_t)K);
+    if (rc) return rc;
+    rc = ensure_stage(c, ((size_t)n_col * K + K + (size_t)n_col) * 8 + 256);
+    if (rc) return rc;
+    double* dbeta = (double*)c->stage;
+    double* ddist = dbeta + (size_t)n_col * K;
+    double* dtend = ddist + K;
+    return fenced(c, nullptr, false, [&](hipStream_t s) -> int {
+        HIP_TRY(c, hipMemcpyAsync(dbeta, betas, (size_t)n_col * K * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+        HIP_TRY(c, hipMemcpyAsync(ddist, dist, (size_t)K * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+        HIP_TRY(c, hipMemcpyAsync(dtend, t_end, (size_t)n_col * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+        // the knot grid runs to t_end whatever η is (the learning stage of a sweep streams
+        // the hazard for η alongside; here η = t_end only sizes that unused stream)
+        sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, 0.5, 1.0, o.ode_maxiters, (int32_t)n_col, 0, 0};
+        sbr::HeteroEqArgs ea{0.5, 1e-12, 1, o.hetero_max_iters, het_lds(c), 0, 0, nullptr};
+        sbr::ResultSoA r{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+        HIP_TRY(c, sbr::launch_hetero(K, dbeta, ddist, dtend, dtend, nullptr, la, ea, c->H, r, nullptr, nullptr, s, 0),
+                SBR_EDEVICE);
+        const size_t w = (size_t)o.knot_capacity;
+        if (t_out)
+            HIP_TRY(c, hipMemcpy2DAsync(t_out, (size_t)cap * 8, c->H.t, w * 8, w * 8, (size_t)n_col, hipMemcpyDeviceToHost, s),
+                    SBR_EDEVICE);
+        if (G_out)
+            HIP_TRY(c, hipMemcpy2DAsync(G_out, (size_t)cap * K * 8, c->H.G, w * K * 8, w * K * 8, (size_t)n_col,
+                                        hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        if (n_knots) HIP_TRY(c, hipMemcpyAsync(n_knots, c->H.n_knots, (size_t)n_col * 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        if (status) HIP_TRY(c, hipMemcpyAsync(status, c->H.status, (size_t)n_col * 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
+        return SBR_OK;
+    });
+}
+
 int sbr_sweep_hetero_dev(sbr_ctx* c, void* stream, int32_t K, const double* betas, const double* dist,
                          const double* eta, const double* t_end, double x0, const double* u, int64_t n_col,
                          int64_t n_u, double p, double kappa, double lambda, const sbr_opts* opts,
@@ -1430,7 +1484,8 @@ int run_social_pass(sbr_ctx* c, hipStream_t s, const double* beta, const double*
         a.fp_iters = fp_iters;
         a.steps_out = rk_steps;
         a.prof = prof ? c->so_prof : nullptr;
-        a.path_t = c->so_path_t; a.path_G = c->so_path_G; a.path_n = c->so_path_n; a.path_cap = c->so_path_cap;
+        a.path_t = c->so_path_t; a.path_G = c->so_path_G; a.path_aw = c->so_path_aw; a.path_n = c->so_path_n;
+        a.path_cap = c->so_path_cap;
         a.pool = sbr::SocialPool{};
         sbr::SocialArgs b{}; // the pool's own arguments (n_pts = 0: no pool blocks)
         if (nslots > 0) {
@@ -1563,16 +1618,17 @@ int sbr_sweep_social_dev(sbr_ctx* c, void* stream, const double* beta, const dou
 int sbr_social_point_paths(sbr_ctx* c, double beta, double eta, double x0, double u, double p, double kappa,
                            double lambda, const double* cmp_grid, int32_t n_cmp, double tol, int32_t max_iter,
                            const sbr_opts* opts, double* res, uint32_t* status, int32_t* fp_iters, double* t,
-                           double* G, int64_t cap, int64_t* n_knots)
+                           double* G, double* aw_old, int64_t cap, int64_t* n_knots)
 {
-    SBR_ON_RANK0(c, sbr_social_point_paths(c, beta, eta, x0, u, p, kappa, lambda, cmp_grid, n_cmp, tol, max_iter, opts, res, status, fp_iters, t, G, cap, n_knots));
+    SBR_ON_RANK0(c, sbr_social_point_paths(c, beta, eta, x0, u, p, kappa, lambda, cmp_grid, n_cmp, tol, max_iter, opts, res, status, fp_iters, t, G, aw_old, cap, n_knots));
     if (!c || !res || !status || !t || !G || cap <= 0 || cap > (int64_t(1) << 30)) return SBR_EARG;
     double* d = nullptr;
     const size_t kc = (size_t)cap;
-    HIP_TRY(c, hipMalloc(&d, (2 * kc + 8) * 8), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&d, (3 * kc + 8) * 8), SBR_ENOMEM);
     c->so_path_t = d;
     c->so_path_G = d + kc;
-    c->so_path_n = (int32_t*)(d + 2 * kc);
+    c->so_path_aw = aw_old ? d + 2 * kc : nullptr;
+    c->so_path_n = (int32_t*)(d + 3 * kc);
     c->so_path_cap = (int32_t)cap;
     hipError_t e = hipMemset(c->so_path_n, 0, 4);
     double xi, tin, tout, aw, tl;
@@ -1581,15 +1637,16 @@ int sbr_social_point_paths(sbr_ctx* c, double beta, double eta, double x0, doubl
     int rc = e == hipSuccess ? sbr_sweep_social(c, &beta, &eta, x0, &u, 1, 1, p, kappa, lambda, cmp_grid, n_cmp, tol,
                                                 max_iter, opts, &out, fp_iters, &steps)
                              : fail(c, SBR_EDEVICE, "hipMemset", e);
-    c->so_path_t = c->so_path_G = nullptr;
+    c->so_path_t = c->so_path_G = c->so_path_aw = nullptr;
     c->so_path_n = nullptr;
     c->so_path_cap = 0;
     int32_t n = 0;
     if (rc == SBR_OK) {
-        e = hipMemcpy(&n, d + 2 * kc, 4, hipMemcpyDeviceToHost);
+        e = hipMemcpy(&n, d + 3 * kc, 4, hipMemcpyDeviceToHost);
         const int64_t m = n < 0 ? 0 : n;
         if (e == hipSuccess && m > 0) e = hipMemcpy(t, d, (size_t)m * 8, hipMemcpyDeviceToHost);
         if (e == hipSuccess && m > 0) e = hipMemcpy(G, d + kc, (size_t)m * 8, hipMemcpyDeviceToHost);
+        if (e == hipSuccess && m > 0 && aw_old) e = hipMemcpy(aw_old, d + 2 * kc, (size_t)m * 8, hipMemcpyDeviceToHost);
         if (e != hipSuccess) rc = fail(c, SBR_EDEVICE, "social path copy", e);
     }
     (void)hipFree(d);

@@ -143,6 +143,7 @@ struct SocialArgs {
     // returned SolvedModel's are the last written); path_n = knots (−knots if > path_cap)
     double* path_t;
     double* path_G;
+    double* path_aw;     // AW_{n-1} at the knots (the forcing of compute_pdf_social_learning), may be null
     int32_t* path_n;
     int32_t path_cap;
 };

@@ -453,6 +453,8 @@ __device__ __forceinline__ bool social_iterate(const SocialArgs& a, int l, int i
         stop_oob = true; // previous iterate's SolvedModel stays in `out`
     } else {
         have_r = true;
+        if (a.path_aw && n <= a.path_cap) // before the damping below overwrites AW_{n-1}(t_i)
+            for (int i = 0; i < n; i++) a.path_aw[i] = AWO[i];
         // ---- hazard_rate (solver.jl:153-185) on τ̄ = knots (t_n = η, else the η
         // append needs pdf(η) past the grid: BoundsError) ----
         const bool h_oob = !(n >= 2 && T[n - 1] == ETA);

@@ -2,8 +2,7 @@
 SBRDropIn.jl — drop-in replacement for src/baseline/learning.jl + src/baseline/solver.jl
 backed by libsbr (the MI355X engine), with the reference's names, structs and semantics.
 
-scripts/1_baseline.jl (and the extension scripts, which re-include the baseline) switch
-with one line each: keep
+scripts/1_baseline.jl switches with one line: keep
 
     include(joinpath(@__DIR__, "..", "src", "baseline", "model.jl"))       # parameter structs
 
@@ -24,6 +23,10 @@ Then Figs 1–3 run unchanged:
   * `hazard_rate`, `get_AW`                 → host restatements of solver.jl:153-185, 495-532,
     kept for plot_hazard_rate_decomposition / plot_equilibrium (plotting.jl:62-210), which
     call them on interpolants; they are presentation code, not the sweep path.
+The extension scripts add their own drop-in on top of this one (they call these too):
+SBRDropInHetero.jl (scripts/2_heterogeneity.jl), SBRDropInInterest.jl
+(scripts/3_interest_rates.jl), SBRDropInSocial.jl (scripts/4_social_learning.jl); see
+INTEGRATION.md for the include lines of each script.
 The Fig 4 / Fig 5 loops can keep calling these per point, or call
 `SBREngine.solve_equilibrium_grid` once per grid (one ccall per grid, all GPUs of a
 `SBREngine.Context(; n_gpus = 8)`).
@@ -164,13 +167,15 @@ function get_AW(ξ, τ_bar_IN_UNC, τ_bar_OUT_UNC, HR, learning_cdf)
     return LinearInterpolation(t_grid, AW_cum), LinearInterpolation(t_grid, AW_OUT), LinearInterpolation(t_grid, AW_IN)
 end
 
-# solver.jl:553-576 — AW_cum and AW_max from the engine, AW_OUT / AW_IN rebuilt on the host
+# solver.jl:553-576 — AW_cum and AW_max from the engine (when the solve returned its path),
+# AW_OUT / AW_IN rebuilt on the host
 function get_AW_functions!(result::SolvedModel)
     result.aw[] !== nothing && return result.aw[]
     result.bankrun || return result.aw[]
-    _, AW_OUT_func, AW_IN_func = get_AW(result.ξ, result.τ_bar_IN_UNC, result.τ_bar_OUT_UNC, result.HR,
-                                        result.learning_results.learning_cdf)
-    AW_cum_func = LinearInterpolation(result.HR.itp.knots[1], result.aw_cum_engine)
+    AW_cum_host, AW_OUT_func, AW_IN_func = get_AW(result.ξ, result.τ_bar_IN_UNC, result.τ_bar_OUT_UNC, result.HR,
+                                                  result.learning_results.learning_cdf)
+    AW_cum_func = isempty(result.aw_cum_engine) ? AW_cum_host :
+                  LinearInterpolation(result.HR.itp.knots[1], result.aw_cum_engine)
     result.aw[] = (AW_cum = AW_cum_func, AW_OUT = AW_OUT_func, AW_IN = AW_IN_func,
                    AW_max = maximum(AW_cum_func.itp.coefs))
     return result.aw[]

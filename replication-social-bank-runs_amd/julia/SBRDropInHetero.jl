@@ -1,0 +1,107 @@
+#=
+SBRDropInHetero.jl — drop-in replacement for
+src/extensions/heterogeneity/heterogeneity_learning.jl + heterogeneity_solver.jl, backed by
+libsbr (the MI355X engine), with the reference's names, argument lists and result structs.
+
+scripts/2_heterogeneity.jl switches by include (INTEGRATION.md §"Extension scripts"):
+keep model.jl, plotting.jl and heterogeneity_model.jl (parameter structs and the
+LearningResultsHetero / SolvedModelHetero result structs, heterogeneity_model.jl:195-294),
+replace learning.jl + solver.jl by SBRDropIn.jl and heterogeneity_learning.jl +
+heterogeneity_solver.jl by this file.  Then :59, :67 and :76 run unchanged:
+
+  * `solve_SInetwork_hetero(lp)` → LearningResultsHetero (heterogeneity_learning.jl:49-94):
+    the shared knot grid and the K group CDFs of the coupled AutoTsit5(Rosenbrock23()) solve
+    at eps() (sbr_learn_hetero), the PDFs by compute_pdf_hetero (:114-134);
+  * `solve_equilibrium_hetero(lr, econ; verbose)` → SolvedModelHetero
+    (heterogeneity_solver.jl:241-293): per-group buffers, ξ of compute_ξ_hetero with its
+    validity check, bankrun / converged / tolerance — one GPU solve through
+    sbr_hetero_point_paths (bit-identical to a sweep point); HRs as the reference builds
+    them (hazard_rate per group on the learning grid, :255);
+  * `get_AW_functions_hetero!(result)` → (AW_cum, AW_OUT_groups, AW_IN_groups, AW_groups,
+    AW_max) (:386-402 / get_AW_hetero :316-375): AW_cum and AW_max are the engine's AW_total
+    path, the per-group curves are rebuilt from the group CDFs.
+
+A β×u (or βs-column × u) grid is one call: `SBREngine.solve_equilibrium_hetero_grid`.
+
+NOT EXECUTED IN THIS REPOSITORY (no Julia in the image): the same entry points run through
+the Python binding (sbr.learn_hetero / hetero_point_paths, tests/test_hetero.py), and
+tests/test_julia_shim.py checks this file's call surface against the reference's
+(tests/golden/julia_surface.json, made by tools/extract_julia_surface.py).
+=#
+using Interpolations
+
+# heterogeneity_learning.jl:114-134 — g_k = (1 − G_k)·β_k·ω with ω = Σ_j dist_j G_j, on the knots
+function compute_pdf_hetero(βs, dist, learning_cdfs, t_values)
+    Gm = reduce(hcat, [cdf.(t_values) for cdf in learning_cdfs])   # n × K
+    ω = Gm * dist
+    return Any[LinearInterpolation(t_values, (1 .- Gm[:, k]) .* βs[k] .* ω) for k in eachindex(βs)]
+end
+
+# heterogeneity_learning.jl:49-94
+function solve_SInetwork_hetero(params::LearningParametersHetero; tol = eps())
+    solve_start = time()
+    tol == eps() || throw(ArgumentError("the engine integrates at reltol = abstol = eps()"))
+    params.tspan[1] == 0 || throw(ArgumentError("the engine integrates from t = 0"))
+    t, Gm, _ = SBREngine.learn_hetero(sbr_context(), params.βs, params.dist, params.tspan[2], params.x0)
+    cdfs = Any[LinearInterpolation(t, Gm[:, k]) for k in eachindex(params.βs)]
+    pdfs = compute_pdf_hetero(params.βs, params.dist, cdfs, t)
+    return LearningResultsHetero(params, cdfs, pdfs, t, time() - solve_start, nothing)
+end
+
+# the per-group withdrawal curves of get_AW_hetero (heterogeneity_solver.jl:335-362) on the grid
+function _hetero_group_curves(ξ, τ_bar_IN_UNCs, τ_bar_OUT_UNCs, learning_cdfs, t_grid)
+    shifted(cdf, τ) = (s = t_grid .- ξ .+ min(τ, ξ); ifelse.(s .>= 0, cdf.(max.(s, 0)), 0.0))
+    outs, ins, nets = Any[], Any[], Any[]
+    for k in eachindex(learning_cdfs)
+        o = shifted(learning_cdfs[k], τ_bar_OUT_UNCs[k])
+        i = shifted(learning_cdfs[k], τ_bar_IN_UNCs[k])
+        push!(outs, LinearInterpolation(t_grid, o)); push!(ins, LinearInterpolation(t_grid, i))
+        push!(nets, LinearInterpolation(t_grid, o .- i))
+    end
+    return outs, ins, nets
+end
+
+# heterogeneity_solver.jl:316-375 (host restatement; the engine's AW_total is used when present)
+function get_AW_hetero(result::SolvedModelHetero, AW_total = nothing)
+    result.bankrun || return nothing
+    lr = result.learning_results
+    t_grid = lr.grid
+    dist = result.model_params.learning.dist
+    outs, ins, nets = _hetero_group_curves(result.ξ, result.τ_bar_IN_UNCs, result.τ_bar_OUT_UNCs,
+                                           lr.learning_cdfs, t_grid)
+    if AW_total === nothing
+        AW_total = zeros(length(t_grid))
+        for k in eachindex(dist)
+            AW_total .+= dist[k] .* nets[k].itp.coefs
+        end
+    end
+    return (AW_cum = LinearInterpolation(t_grid, AW_total), AW_OUT_groups = outs, AW_IN_groups = ins,
+            AW_groups = nets, AW_max = maximum(AW_total))
+end
+
+# heterogeneity_solver.jl:241-293 — one GPU solve (hazards, buffers, compute_ξ_hetero, validity, AW path)
+function solve_equilibrium_hetero(lr_hetero::LearningResultsHetero, econ::EconomicParameters; verbose = false)
+    solve_start = time()
+    lp = lr_hetero.params
+    r = SBREngine.solve_hetero_point_paths(sbr_context(), lp.βs, lp.dist, econ.u; η = econ.η, tspan_end = lp.tspan[2],
+                                           x0 = lp.x0, p = econ.p, κ = econ.κ, λ = econ.λ)
+    (r.status & SBREngine.SBR_OOB) != 0 && throw(BoundsError(lr_hetero.learning_cdfs[1], econ.η))
+    length(r.t) == length(lr_hetero.grid) || error("engine knot grid differs from lr_hetero.grid")
+    HRs = Any[hazard_rate(econ.p, econ.λ, lr_hetero.learning_pdfs[k], econ.η; grid = lr_hetero.grid)
+              for k in eachindex(lp.βs)]
+    bankrun = (r.status & SBREngine.SBR_RUN) != 0
+    converged = (r.status & SBREngine.SBR_CONVERGED) != 0
+    result = SolvedModelHetero(r.ξ, r.τ_bar_IN_UNCs, r.τ_bar_OUT_UNCs, HRs, bankrun, econ, lr_hetero, converged,
+                               time() - solve_start, r.tolerance)
+    bankrun && (result.aw[] = get_AW_hetero(result, r.AW_total))
+    verbose && println(bankrun ? "Converged: ξ = $(result.ξ), tolerance = $(result.tolerance)" :
+                                 "No valid run equilibrium exists (status 0x$(string(r.status, base = 16)))")
+    return result
+end
+
+# heterogeneity_solver.jl:386-402
+function get_AW_functions_hetero!(result::SolvedModelHetero)
+    result.aw[] !== nothing && return result.aw[]
+    result.aw[] = result.bankrun ? get_AW_hetero(result) : nothing
+    return result.aw[]
+end

@@ -271,27 +271,52 @@ end
     solve_social_point_paths(ctx, β, u; η, x0 = 1e-4, p = 0.99, κ = 0.25, λ = 0.25, tol = 1e-4, max_iter = 500)
 
 `solve_equilibrium_social_learning` for one point with the learning knots `t`, `G` of the
-returned `SolvedModel`; `LinearInterpolation(t, G)` is its `learning_cdf`, from which `get_AW`
-rebuilds the curves of `scripts/4_social_learning.jl` (HR grid τ̄ = knots ≤ η, plus η).
+returned `SolvedModel` and `AW_old` = AW_{n-1}(t) (the forcing that drove that iterate);
+`LinearInterpolation(t, G)` is its `learning_cdf`, `(1 .- G) .* β .* AW_old` its
+`learning_pdf` (compute_pdf_social_learning), from which `hazard_rate` and `get_AW` rebuild
+the curves of `scripts/4_social_learning.jl` (HR grid τ̄ = knots ≤ η, plus η).
 """
 function solve_social_point_paths(ctx::Context, β, u; η, x0 = 1e-4, p = 0.99, κ = 0.25, λ = 0.25, tol = 1e-4,
                                   max_iter = 500, cap = 1 << 20)
     cmp = collect(range(0.0, Float64(η), length = 1000))
     res = zeros(Float64, 5); st = Ref{UInt32}(0); fp = Ref{Int32}(0); nk = Ref{Int64}(0)
-    t = Vector{Float64}(undef, cap); G = similar(t)
+    t = Vector{Float64}(undef, cap); G = similar(t); awo = similar(t)
     opts = Ref(Opts(; early_exit = 0))
-    GC.@preserve cmp res t G begin
+    GC.@preserve cmp res t G awo begin
         rc = ccall((:sbr_social_point_paths, libsbr), Cint,
                    (Ptr{Cvoid}, Float64, Float64, Float64, Float64, Float64, Float64, Float64, Ptr{Float64}, Int32,
                     Float64, Int32, Ref{Opts}, Ptr{Float64}, Ref{UInt32}, Ref{Int32}, Ptr{Float64}, Ptr{Float64},
-                    Int64, Ref{Int64}),
+                    Ptr{Float64}, Int64, Ref{Int64}),
                    ctx.ptr, β, η, x0, u, p, κ, λ, cmp, Int32(1000), tol, Int32(max_iter), opts, res, st, fp, t, G,
-                   cap, nk)
+                   awo, cap, nk)
         check(ctx, rc)
     end
     k = nk[]
     return (ξ = res[1], τ_bar_IN_UNC = res[2], τ_bar_OUT_UNC = res[3], AW_max = res[4], tolerance = res[5],
-            status = st[], fp_iters = fp[], t = t[1:k], G = G[1:k])
+            status = st[], fp_iters = fp[], t = t[1:k], G = G[1:k], AW_old = awo[1:k])
+end
+
+"""
+    learn_hetero(ctx, βs, dist, tspan_end, x0; cap = 1 << 14)
+
+`solve_SInetwork_hetero` (heterogeneity_learning.jl:49-94) on the GPU: the shared knot grid
+`t` and the group CDFs `G` (n × K) of the coupled AutoTsit5(Rosenbrock23()) solve at eps()
+on (0, tspan_end), and the status bits.
+"""
+function learn_hetero(ctx::Context, βs, dist, tspan_end, x0; cap = 1 << 14)
+    b = collect(Float64, βs); d = collect(Float64, dist); K = length(d)
+    t = Vector{Float64}(undef, cap); G = Vector{Float64}(undef, cap * K)
+    nk = Ref{Int32}(0); st = Ref{UInt32}(0); te = Float64[tspan_end]
+    opts = Ref(Opts(; early_exit = 0))
+    GC.@preserve b d t G te begin
+        rc = ccall((:sbr_learn_hetero, libsbr), Cint,
+                   (Ptr{Cvoid}, Int32, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Float64, Int64, Ref{Opts},
+                    Ptr{Float64}, Ptr{Float64}, Int64, Ref{Int32}, Ref{UInt32}),
+                   ctx.ptr, Int32(K), b, d, te, x0, 1, opts, t, G, cap, nk, st)
+        check(ctx, rc)
+    end
+    n = Int(nk[])
+    return t[1:n], permutedims(reshape(G[1:n*K], K, n)), st[]
 end
 
 """

@@ -109,7 +109,8 @@ _SIGS = {
     "sbr_social_prof_read": (ctypes.c_int, [_P, _P]),
     "sbr_social_overflow_stats": (ctypes.c_int, [_P, _P, _P]),
     "sbr_social_point_paths": (ctypes.c_int, [_P, _D, _D, _D, _D, _D, _D, _D, _P, ctypes.c_int32, _D,
-                                              ctypes.c_int32, _P, _P, _P, _P, _P, _P, _I64, _P]),
+                                              ctypes.c_int32, _P, _P, _P, _P, _P, _P, _P, _I64, _P]),
+    "sbr_learn_hetero": (ctypes.c_int, [_P, _I32, _P, _P, _P, _D, _I64, _P, _P, _P, _I64, _P, _P]),
     "sbr_hetero_point_paths": (ctypes.c_int, [_P, ctypes.c_int32, _P, _P, _D, _D, _D, _D, _D, _D, _D, _P, _P, _P,
                                               _P, _P, _P, _P, _P, _I64, _P]),
     "sbr_interest_point_paths": (ctypes.c_int, [_P, _D, _D, _D, _D, _D, _D, _D, _D, _D, _D, _P, _P, _P, _P, _P, _P,

@@ -339,23 +339,41 @@ class Engine:
     def social_point_paths(self, beta, eta, u, p, kappa, lam, cmp=None, x0=1e-4, tol=1e-4, max_iter=500,
                            cap=1 << 20) -> dict:
         """One social-learning fixed point with the learning knots (t, G) of the returned
-        SolvedModel — what scripts/4_social_learning.jl plots (AW curves rebuilt from them)."""
+        SolvedModel and AW_{n-1} at those knots (the forcing of its learning_pdf,
+        social_learning_dynamics.jl:98-114) — what scripts/4_social_learning.jl plots."""
         if cmp is None:
             cmp = julia_range(0.0, float(eta), 1000)
         cmp = np.ascontiguousarray(cmp, np.float64)
         res = np.zeros(5)
         st = np.zeros(1, np.uint32)
         fp = np.zeros(1, np.int32)
-        t, G = np.empty(cap), np.empty(cap)
+        t, G, awo = np.empty(cap), np.empty(cap), np.empty(cap)
         nk = ctypes.c_int64()
         opts = _lib.default_opts()
         rc = self._L.sbr_social_point_paths(self._ctx, beta, eta, x0, u, p, kappa, lam, _ptr(cmp), len(cmp), tol,
                                             max_iter, ctypes.byref(opts), _ptr(res), _ptr(st), _ptr(fp), _ptr(t),
-                                            _ptr(G), cap, ctypes.byref(nk))
+                                            _ptr(G), _ptr(awo), cap, ctypes.byref(nk))
         check(rc, self._ctx, "sbr_social_point_paths")
         n = nk.value
         return dict(xi=res[0], tau_in_unc=res[1], tau_out_unc=res[2], aw_max=res[3], tol=res[4], status=int(st[0]),
-                    fp_iters=int(fp[0]), t=t[:n].copy(), G=G[:n].copy())
+                    fp_iters=int(fp[0]), t=t[:n].copy(), G=G[:n].copy(), aw_old=awo[:n].copy())
+
+    def learn_hetero(self, betas, dist, t_end, x0=1e-4, cap=16384) -> dict:
+        """solve_SInetwork_hetero (heterogeneity_learning.jl:49-94) for n_col columns: the shared
+        knot grid t [n_col, cap] and group CDFs G [n_col, cap, K] (row c valid to n_knots[c])."""
+        dist = np.ascontiguousarray(dist, np.float64)
+        K = len(dist)
+        betas = np.ascontiguousarray(np.atleast_2d(betas), np.float64)
+        nc = betas.shape[0]
+        assert betas.shape[1] == K
+        t_end = np.ascontiguousarray(np.broadcast_to(t_end, (nc,)), np.float64)
+        t, G = np.empty((nc, cap)), np.empty((nc, cap, K))
+        nk, st = np.zeros(nc, np.int32), np.zeros(nc, np.uint32)
+        opts = _lib.default_opts(early_exit_nan_run=0, knot_capacity=cap)
+        rc = self._L.sbr_learn_hetero(self._ctx, K, _ptr(betas), _ptr(dist), _ptr(t_end), x0, nc, ctypes.byref(opts),
+                                      _ptr(t), _ptr(G), cap, _ptr(nk), _ptr(st))
+        check(rc, self._ctx, "sbr_learn_hetero")
+        return dict(t=t, G=G, n_knots=nk, status=st)
 
     def hetero_point_paths(self, betas, dist, eta, t_end, u, p, kappa, lam, x0=1e-4, cap=65536) -> dict:
         """One heterogeneity equilibrium with learning knots t, group CDFs G [n, K], the

@@ -133,7 +133,7 @@ def test_social_point_paths_bitwise(engine, oracle):
         g = engine.social_point_paths(b, ETA, uu, P, KAPPA, LAM, cmp=cmp)
         o = oracle.social_point(b, ETA, uu, P, KAPPA, LAM, cmp)
         assert g["status"] == o["status"] and g["fp_iters"] == o["fp_iters"], (b, uu)
-        for k in ("xi", "tau_in_unc", "tau_out_unc", "aw_max", "tol", "t", "G"):
+        for k in ("xi", "tau_in_unc", "tau_out_unc", "aw_max", "tol", "t", "G", "aw_old"):
             x, y = np.atleast_1d(g[k]), np.atleast_1d(o[k])
             assert x.shape == y.shape and np.array_equal(x, y, equal_nan=True), (b, uu, k)
 

@@ -107,6 +107,23 @@ def test_hetero_point_paths_bitwise(engine, oracle):
             assert np.max(a["aw_total"]) == a["aw_max"]
 
 
+@pytest.mark.gpu
+def test_learn_hetero_bitwise(engine, oracle):
+    """sbr_learn_hetero (solve_SInetwork_hetero, run to t_end like the reference) == the
+    oracle's knots and group CDFs, on the script column and two config-4 columns (one of
+    which switches to Rosenbrock23)."""
+    g = sbr.hetero_script_grid()
+    c4 = sbr.hetero_config4(4, 4)
+    cols = [(g.betas[0], g.dist, g.t_end[0])] + [(c4.betas[i], c4.dist, c4.t_end[i]) for i in (0, 3)]
+    for betas, dist, t_end in cols:
+        a = engine.learn_hetero(np.atleast_2d(betas), dist, t_end)
+        t, G, st = oracle.learn_hetero(betas, dist, t_end)
+        n = int(a["n_knots"][0])
+        assert n == len(t), (betas, n, len(t))
+        assert np.array_equal(a["t"][0, :n], t) and np.array_equal(a["G"][0, :n], G)
+        assert int(a["status"][0]) & ~sbr.STATUS["SBR_STIFF_SWITCH"] == st["status"] & ~sbr.STATUS["SBR_STIFF_SWITCH"]
+
+
 def test_hetero_point_paths_oracle_figure(oracle, golden):
     """The oracle's path output reproduces the script figure's AW_total maximum."""
     g = sbr.hetero_script_grid()

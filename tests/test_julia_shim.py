@@ -140,3 +140,93 @@ def test_dropin_defines_the_reference_call_surface():
         body = re.search(r"^struct %s\b(.*?)^end" % st, src, re.S | re.M).group(1)
         declared = re.findall(r"^\s+(\w+)::", body, re.M)
         assert tuple(declared[:len(fields)]) == fields, (st, declared)
+
+
+# --------------------------------------------------------------------------------------
+# The extension drop-ins: every script switches by include.  The reference
+# surface per script (calls, arities, returns, fields read) comes from the reference's own
+# files via tools/extract_julia_surface.py → tests/golden/julia_surface.json.
+import json  # noqa: E402
+import sys  # noqa: E402
+
+sys.path.insert(0, str(Path(__file__).resolve().parent))
+import jl_surface as JS  # noqa: E402
+
+SURFACE = json.loads((REPO / "tests" / "golden" / "julia_surface.json").read_text())["scripts"]
+
+
+def _dropin_defs(files):
+    defs, structs, full = {}, {}, {}
+    for f in files:
+        src = (JL / f).read_text()
+        for name, meths in JS.functions(src).items():
+            full.setdefault(name, []).extend(meths)
+        structs.update(JS.structs(src))
+    return full, structs
+
+
+@pytest.mark.parametrize("script", sorted(SURFACE))
+def test_dropins_define_every_called_function_with_reference_arity(script):
+    s = SURFACE[script]
+    defs, _ = _dropin_defs(s["dropins"])
+    assert s["calls"], script
+    for c in s["calls"]:
+        meths = defs.get(c["fn"])
+        assert meths, f"{script}: {c['fn']} (called at {c['file']}:{c['line']}) is not defined by {s['dropins']}"
+        ok = any(m["required"] <= c["npos"] <= (m["max"] if m["max"] is not None else 1 << 30)
+                 and (m["varkw"] or set(c["kwargs"]) <= set(m["kwargs"])) for m in meths)
+        assert ok, (script, c, [(m["required"], m["max"], m["kwargs"]) for m in meths])
+        # and with the reference's own signature (positional range and keywords)
+        for r in s["defs"][c["fn"]]:
+            if r["required"] <= c["npos"] <= (r["max"] if r["max"] is not None else 1 << 30):
+                assert any(m["required"] == r["required"] and m["max"] == r["max"]
+                           and set(r["kwargs"]) <= set(m["kwargs"]) for m in meths), (script, c["fn"], r)
+
+
+@pytest.mark.parametrize("script", sorted(SURFACE))
+def test_dropins_return_the_reference_result_types(script):
+    s = SURFACE[script]
+    defs, structs = _dropin_defs(s["dropins"])
+    names = set(structs) | set(s["structs_kept"]) | set(s["structs_replaced"])
+    for fn, kind in s["returns"].items():
+        if kind is None:  # an interpolant (hazard_rate)
+            continue
+        mine = JS.return_kind(fn, defs, names)
+        assert mine == kind, (script, fn, mine, kind)
+
+
+@pytest.mark.parametrize("script", sorted(SURFACE))
+def test_dropins_provide_every_field_the_scripts_and_plotting_read(script):
+    s = SURFACE[script]
+    defs, structs = _dropin_defs(s["dropins"])
+    # structs the replaced files defined: the drop-ins define them with the reference's fields, in order
+    for name, st in s["structs_replaced"].items():
+        assert name in structs, (script, name, st["file"])
+        assert structs[name][:len(st["fields"])] == st["fields"], (script, name, structs[name], st["fields"])
+
+    def fields_of(kind):
+        if "namedtuple" in kind:
+            return kind["namedtuple"]
+        n = kind["struct"]
+        return structs[n] if n in structs else s["structs_kept"][n]["fields"]
+
+    for r in s["field_reads"]:
+        kind = s["returns"][r["fn"]]
+        assert kind is not None, r
+        assert r["field"] in fields_of(kind), (script, r)
+    for f in s["plotting_solvedmodel_reads"]:
+        assert f in structs["SolvedModel"], (script, f)
+
+
+def test_surface_fixture_matches_reference_when_present():
+    """The fixture is what tools/extract_julia_surface.py reads from /root/reference today
+    (skipped where the reference is absent, e.g. on the GPU box)."""
+    if not Path("/root/reference/scripts").is_dir():
+        pytest.skip("reference not present")
+    import subprocess as sp
+
+    before = (REPO / "tests" / "golden" / "julia_surface.json").read_text()
+    out = sp.run([sys.executable, str(REPO / "tools" / "extract_julia_surface.py")], capture_output=True, text=True)
+    assert out.returncode == 0, out.stderr
+    after = (REPO / "tests" / "golden" / "julia_surface.json").read_text()
+    assert before == after
