@@ -17,9 +17,13 @@ cannot overlap anything, so the default 50 steps amortise that pipeline fill to
 
 N GPUs (torchrun, one process per GPU, RCCL): weak scaling — rank r owns the β
 columns r, r+N, r+2N, … of a 2048·N-column grid (same u axis), so per-GPU work is
-fixed; each step ends with an RCCL gather of the result tensor (AW_max + status) to
-rank 0 over xGMI, issued on its own stream once that step's results exist
-(sbr_batch_wait) so that it overlaps the later steps' sweeps.  value = all ranks' equilibria × steps / max-over-ranks time.
+fixed.  Every step's full result SoA (ξ, τ̄_IN, τ̄_OUT, AW_max, tol, status, bisection
+iterations: 48 B per point) is collected over RCCL/xGMI: step k's grid on rank k mod N,
+N consecutive steps by one all-to-all per field (sbr.distributed.StepCollector: every
+link carries a share in both directions; a gather of every step to rank 0 would be
+capped by rank 0's inbound links), issued on its own stream once those steps' results
+exist (sbr_batch_wait) so that it overlaps the later steps' sweeps.  value = all ranks'
+equilibria × steps / max-over-ranks time.
 """
 from __future__ import annotations
 
@@ -39,6 +43,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 import sbr  # noqa: E402
+from sbr import distributed as D  # noqa: E402
 
 FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X FP64 vector, AMD spec (256 CU x 128 FLOP/clk x 2.4 GHz)
 
@@ -187,20 +192,13 @@ def main():
     out["status"] = torch.empty(nbat, nb * nu, dtype=torch.int32, device=dev)
     out["iters"] = torch.empty(nbat, nb * nu, dtype=torch.int32, device=dev)
     gather = world > 1 and not a.no_gather
-    if gather and rank == 0:
-        g_aw = [torch.empty(nb * nu, dtype=torch.float64, device=dev) for _ in range(world)]
-        g_st = [torch.empty(nb * nu, dtype=torch.int32, device=dev) for _ in range(world)]
-    else:
-        g_aw = g_st = None
+    # the full SoA of every step, collected on rank k mod N (all-to-all per window of N steps)
+    col = D.StepCollector(out, world, rank) if gather else None
 
     eng = sbr.Engine(local)
     stream = torch.cuda.current_stream(dev).cuda_stream
 
-    def gather_batch(k):
-        dist.gather(out["aw_max"][k], g_aw, dst=0)
-        dist.gather(out["status"][k], g_st, dst=0)
-
-    # the gather of step k runs on its own stream as soon as step k's results exist
+    # a window's collection runs on its own stream as soon as its last step's results exist
     # (sbr_batch_wait), overlapped with the sweeps of the later steps
     comm = torch.cuda.Stream(dev) if gather and pipe else None
 
@@ -212,17 +210,17 @@ def main():
         if pipe:
             eng.sweep_baseline_batch_dev(beta[:n], eta[:n], t_end[:n], u, p, kappa, lam, x0,
                                          {k: v[:n] for k, v in out.items()}, stream=stream)
-            for k in range(n):
-                if gather:
-                    eng.batch_wait(comm.cuda_stream, k)
+            if gather:
+                for k0, m in col.windows(n):
+                    eng.batch_wait(comm.cuda_stream, k0 + m - 1)
                     with torch.cuda.stream(comm):
-                        gather_batch(k)
+                        col.collect(k0, m)
         else:
             one = {k: v[0] for k, v in out.items()}
-            for _ in range(n):
+            for k in range(n):
                 eng.sweep_baseline_dev(beta[0], eta[0], t_end[0], u, p, kappa, lam, x0, one, stream=stream)
                 if gather:
-                    gather_batch(0)
+                    col.collect(k, 1, row0=0)
 
     run_steps(a.warmup)
     torch.cuda.synchronize(dev)
@@ -274,7 +272,9 @@ def main():
         "config": {
             "workload": f"fig5_beta_u_sweep_{n}x{n}_per_gpu (BASELINE config 3)",
             "n_beta_per_gpu": nb, "n_u": nu, "eta": 15.0, "t_end": 30.0, "p": p, "kappa": kappa,
-            "lambda": lam, "x0": x0, "early_exit": False, "gather": gather,
+            "lambda": lam, "x0": x0, "early_exit": False,
+            "collect": ("full SoA (48 B/pt) of every step on rank k mod N, all-to-all per N steps"
+                        if gather else None),
             "parallelism": f"beta-column shards x{world}",
             "pipelined": pipe,
         },
@@ -335,8 +335,6 @@ def main_hetero(a):
     eng = sbr.Engine(local)
     stream = torch.cuda.current_stream(dev).cuda_stream
     gather = world > 1 and not a.no_gather
-    g_aw = [torch.empty(nb * nu, dtype=torch.float64, device=dev) for _ in range(world)] if gather and rank == 0 \
-        else None
 
     pipe = not a.no_pipeline
     nbat = max(a.steps, a.warmup, 1) if pipe else 1
@@ -345,6 +343,8 @@ def main_hetero(a):
         betas_b = betas.unsqueeze(0).repeat(nbat, 1, 1).contiguous()
         eta_b = eta.unsqueeze(0).repeat(nbat, 1).contiguous()
         t_end_b = t_end.unsqueeze(0).repeat(nbat, 1).contiguous()
+    # every step's result SoA (ξ, AW_max, tol, status, iterations) on rank k mod N
+    col = D.StepCollector(out_b if pipe else {k: v[None] for k, v in out.items()}, world, rank) if gather else None
 
     def run_steps(m):
         """m steps: pipelined, one batch call of m grids (learning of step k+1 overlaps the
@@ -354,15 +354,15 @@ def main_hetero(a):
         if pipe:
             eng.sweep_hetero_batch_dev(K, betas_b[:m], distw, eta_b[:m], t_end_b[:m], u, g.p, g.kappa, g.lam, g.x0,
                                        {k: v[:m] for k, v in out_b.items()}, stream=stream)
-            for k in range(m):
-                if gather:
-                    dist.gather(out_b["aw_max"][k], g_aw, dst=0)
+            if gather:
+                for k0, mm in col.windows(m):
+                    col.collect(k0, mm)
             out["status"].copy_(out_b["status"][m - 1])
         else:
-            for _ in range(m):
+            for k in range(m):
                 eng.sweep_hetero_dev(K, betas, distw, eta, t_end, u, g.p, g.kappa, g.lam, g.x0, out, stream=stream)
                 if gather:
-                    dist.gather(out["aw_max"], g_aw, dst=0)
+                    col.collect(k, 1, row0=0)
 
     run_steps(a.warmup)
     torch.cuda.synchronize(dev)
@@ -482,13 +482,14 @@ def main_interest(a):
     eng = sbr.Engine(local)
     stream = torch.cuda.current_stream(dev).cuda_stream
     gather = world > 1 and not a.no_gather
-    g_aw = [torch.empty(nb * nu, dtype=torch.float64, device=dev) for _ in range(world)] if gather and rank == 0 \
-        else None
+    col = D.StepCollector({k: v[None] for k, v in out.items()}, world, rank) if gather else None
+    n_done = [0]
 
     def step():
         eng.sweep_interest_dev(beta, eta, t_end, u, p, kappa, lam, r_, delta, x0, out, stream=stream)
-        if gather:
-            dist.gather(out["aw_max"], g_aw, dst=0)
+        if gather:  # the step's full result SoA on rank (step mod N)
+            col.collect(n_done[0], 1, row0=0)
+        n_done[0] += 1
 
     for _ in range(a.warmup):
         step()
@@ -597,16 +598,17 @@ def main_social(a):
     eng = sbr.Engine(local)
     stream = torch.cuda.current_stream(dev).cuda_stream
     gather = world > 1 and not a.no_gather
-    g_aw = [torch.empty(nb * nu, dtype=torch.float64, device=dev) for _ in range(world)] if gather and rank == 0 \
-        else None
+    col = D.StepCollector({k: v[None] for k, v in out.items()}, world, rank) if gather else None
+    n_done = [0]
 
     flags = sbr._lib.SBR_FLAG_DIAG_SOCIAL_PROF if a.social_prof else 0
 
     def step():
         eng.sweep_social_dev(beta, eta, u, p, kappa, lam, cmp, x0, out, tol=tol, max_iter=a.social_max_iter,
                              stream=stream, flags=flags)
-        if gather:
-            dist.gather(out["aw_max"], g_aw, dst=0)
+        if gather:  # the step's full result SoA on rank (step mod N)
+            col.collect(n_done[0], 1, row0=0)
+        n_done[0] += 1
 
     for _ in range(a.warmup):
         step()

@@ -334,7 +334,10 @@ void sbr_apply_early_exit(int64_t n_beta, int64_t n_u, int32_t threshold, sbr_re
  * learning and equilibrium kernels of every baseline sweep call while
  * enabled; sbr_timing_read synchronises `stream` (NULL = the HIP null stream),
  * returns the summed milliseconds per kernel and the number of calls, and
- * resets the accumulators. */
+ * resets the accumulators.  This and the other per-device diagnostics below
+ * (sbr_learn_stats, sbr_hetero_learn_stats, sbr_social_prof_read,
+ * sbr_social_overflow_stats) return SBR_EARG on an n-device context: call them
+ * on sbr_multi_child(ctx, rank). */
 int sbr_timing_enable(sbr_ctx* ctx, int on);
 int sbr_timing_read(sbr_ctx* ctx, void* stream, double* learn_ms, double* eq_ms, int32_t* n_calls);
 
@@ -351,6 +354,18 @@ int sbr_hetero_learn_stats(sbr_ctx* ctx, int64_t n_col, int32_t* n_knots, int32_
 /* Device facts the engine sized itself with: LDS bytes per workgroup, knots
  * staged in LDS per β column, compute units. */
 int sbr_device_info(sbr_ctx* ctx, int32_t* lds_bytes_per_block, int32_t* lds_knot_capacity, int32_t* cu_count);
+
+/* Diagnostics of the n-device data movement without GPUs: the same
+ * plan, cyclic column deal, per-rank packing, gather to rank 0 and strided scatter as an
+ * sbr_init_multi sweep (csrc/sbr_shard.h), with a host loopback in place of RCCL and the
+ * caller's `compute` in place of each rank's GPU sweep.  compute(user, rank, n_cols,
+ * col_ids, fields) fills, for the grid columns col_ids[0..n_cols), field f at fields[f] as
+ * [n_cols][n_u][per_pt[f]] elements of esz[f] bytes; the scattered results land in
+ * host_out[f] (n_col·n_u·per_pt[f] elements, u-fastest per column, NULL = dropped). */
+typedef int (*sbr_shard_compute_fn)(void* user, int32_t rank, int64_t n_cols, const int64_t* col_ids,
+                                    void* const* fields);
+int sbr_shard_host_run(int32_t n_ranks, int64_t n_col, int64_t n_u, int32_t n_fields, const int64_t* esz,
+                       const int64_t* per_pt, void* const* host_out, sbr_shard_compute_fn compute, void* user);
 
 /* Diagnostics: sbr_exp / sbr_log / sbr_pow_pos (include/sbr_detmath.h)
  * evaluated on the device, for host/device bit-equality tests. */

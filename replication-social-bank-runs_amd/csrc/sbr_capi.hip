@@ -560,6 +560,14 @@ int multi_sweep_baseline(sbr_ctx* c, const double* beta, const double* eta, cons
             return fail((c), SBR_EARG, "device-pointer entry points need a single-device context "          \
                                        "(sbr_multi_child)");                                                \
     } while (0)
+// per-device diagnostics (timings, learning statistics, social counters) describe one
+// device's last sweep: on an n-device context they would report rank 0's shard as if it
+// were the grid, so they are refused there — ask the rank's child context instead
+#define SBR_PER_DEVICE_DIAG(c)                                                                              \
+    do {                                                                                                    \
+        if ((c) && (c)->multi)                                                                              \
+            return fail((c), SBR_EARG, "per-device diagnostic: call it on sbr_multi_child(ctx, rank)");    \
+    } while (0)
 // single-point / diagnostic entry points on an n-device context run on its rank 0
 #define SBR_ON_RANK0(c, call)                                                                               \
     do {                                                                                                    \
@@ -572,6 +580,8 @@ int multi_sweep_baseline(sbr_ctx* c, const double* beta, const double* eta, cons
             return rc_;                                                                                     \
         }                                                                                                   \
     } while (0)
+
+hipStream_t sbr_ctx_stream(sbr_ctx* c) { return c ? c->stream : nullptr; }
 
 extern "C" {
 
@@ -686,9 +696,9 @@ int sbr_free(sbr_ctx* c)
 
 const char* sbr_last_error(const sbr_ctx* c)
 {
-    if (!c) return "null context";
-    if (c->multi && c->err.empty()) return sbr_multi_impl::last_error(c->multi);
-    return c->err.c_str();
+    // an n-device sweep's failure is copied into c->err by fail(); no fallback to the
+    // multi layer's message, which would resurface after a later success
+    return c ? c->err.c_str() : "null context";
 }
 
 int sbr_sweep_baseline_dev(sbr_ctx* c, void* stream, const double* beta, const double* eta, const double* t_end,
@@ -1053,7 +1063,7 @@ int sbr_solve_point_paths(sbr_ctx* c, double beta, double eta, double t_end, dou
 
 int sbr_timing_enable(sbr_ctx* c, int on)
 {
-    SBR_ON_RANK0(c, sbr_timing_enable(c, on));
+    SBR_PER_DEVICE_DIAG(c);
     if (!c) return SBR_EARG;
     c->timing = on != 0;
     c->ev_used = 0;
@@ -1063,7 +1073,7 @@ int sbr_timing_enable(sbr_ctx* c, int on)
 
 int sbr_timing_read(sbr_ctx* c, void* stream, double* learn_ms, double* eq_ms, int32_t* n_calls)
 {
-    SBR_ON_RANK0(c, sbr_timing_read(c, stream, learn_ms, eq_ms, n_calls));
+    SBR_PER_DEVICE_DIAG(c);
     if (!c) return SBR_EARG;
     hipStream_t s = (hipStream_t)stream; // NULL = HIP null stream
     HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
@@ -1089,7 +1099,7 @@ int sbr_timing_read(sbr_ctx* c, void* stream, double* learn_ms, double* eq_ms, i
 int sbr_learn_stats(sbr_ctx* c, int64_t n_beta, int32_t* n_knots, int32_t* n_tau, int32_t* n_accept,
                     int32_t* n_reject, uint32_t* status)
 {
-    SBR_ON_RANK0(c, sbr_learn_stats(c, n_beta, n_knots, n_tau, n_accept, n_reject, status));
+    SBR_PER_DEVICE_DIAG(c);
     if (!c || n_beta <= 0 || (size_t)n_beta > c->ws_beta[c->last_slot]) return SBR_EARG;
     if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
     HIP_TRY(c, hipDeviceSynchronize(), SBR_EDEVICE);
@@ -1104,7 +1114,7 @@ int sbr_learn_stats(sbr_ctx* c, int64_t n_beta, int32_t* n_knots, int32_t* n_tau
 int sbr_hetero_learn_stats(sbr_ctx* c, int64_t n_col, int32_t* n_knots, int32_t* n_tau, int32_t* n_accept,
                            int32_t* n_reject, uint32_t* status)
 {
-    SBR_ON_RANK0(c, sbr_hetero_learn_stats(c, n_col, n_knots, n_tau, n_accept, n_reject, status));
+    SBR_PER_DEVICE_DIAG(c);
     if (!c || n_col <= 0 || (size_t)n_col > c->hs_col) return SBR_EARG;
     if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
     HIP_TRY(c, hipDeviceSynchronize(), SBR_EDEVICE);
@@ -1374,7 +1384,7 @@ int sbr_sweep_hetero(sbr_ctx* c, int32_t K, const double* betas, const double* d
 
 int sbr_social_prof_read(sbr_ctx* c, int64_t* out8)
 {
-    SBR_ON_RANK0(c, sbr_social_prof_read(c, out8));
+    SBR_PER_DEVICE_DIAG(c);
     if (!c || !out8) return SBR_EARG;
     for (int k = 0; k < 8; k++) out8[k] = k < (int)c->so_prof_acc.size() ? c->so_prof_acc[k] : 0;
     return SBR_OK;
@@ -1382,7 +1392,7 @@ int sbr_social_prof_read(sbr_ctx* c, int64_t* out8)
 
 int sbr_social_overflow_stats(sbr_ctx* c, int64_t* promoted, int64_t* rerun)
 {
-    SBR_ON_RANK0(c, sbr_social_overflow_stats(c, promoted, rerun));
+    SBR_PER_DEVICE_DIAG(c);
     if (!c) return SBR_EARG;
     if (promoted) *promoted = c->so_promoted;
     if (rerun) *rerun = c->so_rerun;
@@ -1813,10 +1823,7 @@ namespace {
 using sbr_multi_impl::FieldSpec;
 
 // the rank's columns r, r+N, … of a per-column array with `w` values per column
-void gather_cols(const double* src, int64_t w, int r, int N, int64_t nc, double* dst)
-{
-    for (int64_t k = 0; k < nc; k++) memcpy(dst + k * w, src + (r + k * (int64_t)N) * w, (size_t)w * 8);
-}
+constexpr auto gather_cols = sbr_shard::deal_cols;
 
 int stage_host(void* dev, const std::vector<double>& h)
 {

@@ -10,18 +10,16 @@
 #include <vector>
 
 #include "../../include/sbr.h"
+#include "sbr_shard.h"
 
 struct sbr_multi;
 
+// the private stream of a single-device context (sbr_capi.hip): a rank's sweeps run on it
+hipStream_t sbr_ctx_stream(sbr_ctx* c);
+
 namespace sbr_multi_impl {
 
-// one result array of the caller: n_col·n_u·per_pt elements of esz bytes, u-fastest
-// per column (host == nullptr: computed but not returned)
-struct FieldSpec {
-    void* host;
-    size_t esz;
-    size_t per_pt;
-};
+using FieldSpec = sbr_shard::Field;
 
 // stage(rank, n_cols_of_rank, device_in, stream): copy the rank's inputs into device_in
 using StageFn = std::function<int(int, int64_t, void*, hipStream_t)>;

@@ -2,23 +2,29 @@
 // contract, §8(e) partitioning): an n-device context holds one single-device
 // context per GPU; every host-pointer sweep on it
 //   1. deals the β (or parameter) columns cyclically — column i to rank i mod N,
-//      which balances the β-dependent knot counts and run lengths;
+//      which balances the β-dependent knot counts and run lengths (sbr_shard.h);
 //   2. runs each shard on its own GPU from its own host thread (the single-device
-//      *_dev entry points on a per-rank stream, inputs staged into that GPU's HBM);
-//   3. after every shard has finished (no collective is entered unless all ranks
-//      succeeded, so a failing rank cannot leave the others blocked), gathers the
-//      packed result blocks to rank 0 with RCCL point-to-point (ncclSend/ncclRecv over
-//      xGMI) — the only communication of the path;
-//   4. rank 0 scatters the blocks into the caller's u-fastest arrays (strided
-//      copies: column i of the grid is block row i / N of rank i mod N).
-// Per-point results do not depend on the partitioning, so a multi-GPU sweep is
-// bit-identical to a single-device one.  librccl.so.1 is loaded at run time
-// (reusing an already-loaded copy, e.g. torch's), so libsbr has no link-time
-// dependency on it.
+//      *_dev entry points on that child context's own stream, inputs staged into that
+//      GPU's HBM);
+//   3. after every shard has finished, and after every fallible per-rank step of the
+//      gather (device selection, rank 0's gather buffer, its local copy) has succeeded,
+//      gathers the packed result blocks to rank 0 with RCCL point-to-point
+//      (ncclSend/ncclRecv over xGMI, posted as one group over all communicators from one
+//      thread) — the only communication of the path.  If the group or a stream fails
+//      after posting, every communicator is aborted (ncclCommAbort: no rank stays blocked)
+//      and rebuilt on the next call;
+//   4. rank 0 scatters the blocks into the caller's u-fastest arrays (strided copies:
+//      column i of the grid is block row i / N of rank i mod N).
+// Steps 1, 3 and 4 are sbr_shard.h's, shared with the host loopback of
+// sbr_shard_host_run (the CPU tests' N = 2, 3, 8 layouts).  Per-point results do not
+// depend on the partitioning, so a multi-GPU sweep is bit-identical to a single-device
+// one.  librccl.so.1 is loaded at run time (reusing an already-loaded copy, e.g.
+// torch's), so libsbr has no link-time dependency on it.
 #include <dlfcn.h>
 #include <math.h>
 #include <string.h>
 
+#include <chrono>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -28,6 +34,7 @@
 
 #include "../../include/sbr.h"
 #include "sbr_multi.h"
+#include "sbr_shard.h"
 
 namespace {
 
@@ -36,6 +43,7 @@ struct Rccl {
     std::string err;
     decltype(&ncclCommInitAll) CommInitAll = nullptr;
     decltype(&ncclCommDestroy) CommDestroy = nullptr;
+    decltype(&ncclCommAbort) CommAbort = nullptr;
     decltype(&ncclSend) Send = nullptr;
     decltype(&ncclRecv) Recv = nullptr;
     decltype(&ncclGroupStart) GroupStart = nullptr;
@@ -59,12 +67,13 @@ const Rccl& rccl()
         }
         r.CommInitAll = (decltype(r.CommInitAll))dlsym(h, "ncclCommInitAll");
         r.CommDestroy = (decltype(r.CommDestroy))dlsym(h, "ncclCommDestroy");
+        r.CommAbort = (decltype(r.CommAbort))dlsym(h, "ncclCommAbort");
         r.Send = (decltype(r.Send))dlsym(h, "ncclSend");
         r.Recv = (decltype(r.Recv))dlsym(h, "ncclRecv");
         r.GroupStart = (decltype(r.GroupStart))dlsym(h, "ncclGroupStart");
         r.GroupEnd = (decltype(r.GroupEnd))dlsym(h, "ncclGroupEnd");
         r.GetErrorString = (decltype(r.GetErrorString))dlsym(h, "ncclGetErrorString");
-        r.ok = r.CommInitAll && r.CommDestroy && r.Send && r.Recv && r.GroupStart && r.GroupEnd && r.GetErrorString;
+        r.ok = r.CommInitAll && r.CommDestroy && r.CommAbort && r.Send && r.Recv && r.GroupStart && r.GroupEnd && r.GetErrorString;
         if (!r.ok) r.err = "librccl.so.1 lacks a required symbol";
     });
     return r;
@@ -74,7 +83,7 @@ const Rccl& rccl()
 struct Rank {
     int device = 0;
     sbr_ctx* kid = nullptr;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr; // the child context's own stream (sbr_ctx_stream)
     ncclComm_t comm = nullptr;
     void* in = nullptr;     // staged inputs
     size_t in_bytes = 0;
@@ -100,7 +109,113 @@ int grow(void** p, size_t* have, size_t need)
 struct sbr_multi {
     std::vector<Rank> ranks;
     std::string err;
+    bool comms_ok = false; // false after an abort: rebuilt by the next gather
 };
+
+namespace {
+
+int init_comms(sbr_multi* m, std::string& err)
+{
+    const Rccl& R = rccl();
+    const int n = (int)m->ranks.size();
+    std::vector<ncclComm_t> comms(n);
+    std::vector<int> dl(n);
+    for (int r = 0; r < n; r++) dl[r] = m->ranks[r].device;
+    const ncclResult_t nr = R.CommInitAll(comms.data(), n, dl.data());
+    if (nr != ncclSuccess) {
+        err = std::string("ncclCommInitAll: ") + R.GetErrorString(nr);
+        return SBR_EDEVICE;
+    }
+    for (int r = 0; r < n; r++) m->ranks[r].comm = comms[r];
+    m->comms_ok = true;
+    return SBR_OK;
+}
+
+void abort_comms(sbr_multi* m)
+{
+    const Rccl& R = rccl();
+    for (Rank& k : m->ranks) {
+        if (k.comm) (void)R.CommAbort(k.comm);
+        k.comm = nullptr;
+    }
+    m->comms_ok = false;
+}
+
+// RCCL transport of the gather: one group over every rank's communicator, posted from one
+// thread; any failure after a send or receive was posted aborts every communicator, so that
+// no stream is left waiting for a peer.
+struct RcclTransport : sbr_shard::Transport {
+    sbr_multi* m;
+    const Rccl& R;
+    std::string err;
+    bool posted = false, failed = false;
+    explicit RcclTransport(sbr_multi* m_) : m(m_), R(rccl()) {}
+    int bad(const char* what, ncclResult_t nr)
+    {
+        failed = true;
+        err = std::string(what) + ": " + R.GetErrorString(nr);
+        return SBR_EDEVICE;
+    }
+    int begin() override
+    {
+        const ncclResult_t nr = R.GroupStart();
+        return nr == ncclSuccess ? SBR_OK : bad("ncclGroupStart", nr);
+    }
+    int local_copy(void* dst, const void* src, size_t bytes) override
+    {
+        Rank& k0 = m->ranks[0];
+        if (hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, k0.stream) != hipSuccess) {
+            failed = true;
+            err = "gather: rank 0 local copy";
+            return SBR_EDEVICE;
+        }
+        return SBR_OK;
+    }
+    int recv(int from, void* dst, size_t bytes) override
+    {
+        posted = true;
+        const ncclResult_t nr = R.Recv(dst, bytes, ncclUint8, from, m->ranks[0].comm, m->ranks[0].stream);
+        return nr == ncclSuccess ? SBR_OK : bad("ncclRecv", nr);
+    }
+    int send(int from, const void* src, size_t bytes) override
+    {
+        posted = true;
+        Rank& k = m->ranks[from];
+        const ncclResult_t nr = R.Send(src, bytes, ncclUint8, 0, k.comm, k.stream);
+        return nr == ncclSuccess ? SBR_OK : bad("ncclSend", nr);
+    }
+    int end() override
+    {
+        const ncclResult_t nr = R.GroupEnd();
+        return nr == ncclSuccess ? SBR_OK : bad("ncclGroupEnd", nr);
+    }
+    int wait() override
+    {
+        // poll every rank's stream; on the first failure (or one already seen while
+        // posting) abort all communicators, then drain the streams (aborted kernels exit)
+        if (failed && posted) abort_comms(m);
+        std::vector<char> done(m->ranks.size(), 0);
+        size_t left = m->ranks.size();
+        while (left) {
+            for (size_t r = 0; r < m->ranks.size(); r++) {
+                if (done[r]) continue;
+                const hipError_t e = hipStreamQuery(m->ranks[r].stream);
+                if (e == hipErrorNotReady) continue;
+                done[r] = 1;
+                left--;
+                if (e != hipSuccess && !failed) {
+                    failed = true;
+                    err = std::string("gather: rank ") + std::to_string(r) + ": " + hipGetErrorString(e);
+                    if (posted) abort_comms(m);
+                }
+            }
+            if (left) std::this_thread::sleep_for(std::chrono::microseconds(20));
+        }
+        return failed ? SBR_EDEVICE : SBR_OK;
+    }
+};
+
+}  // namespace
 
 namespace sbr_multi_impl {
 
@@ -123,26 +238,21 @@ int create(int n_gpus, const int* devices, sbr_multi** out, std::vector<sbr_ctx*
     if (!R.ok) { err = R.err; return SBR_EDEVICE; }
     sbr_multi* m = new sbr_multi();
     m->ranks.resize(n_gpus);
-    std::vector<ncclComm_t> comms(n_gpus);
-    ncclResult_t nr = R.CommInitAll(comms.data(), n_gpus, dl.data());
-    if (nr != ncclSuccess) {
-        err = std::string("ncclCommInitAll: ") + R.GetErrorString(nr);
+    for (int r = 0; r < n_gpus; r++) m->ranks[r].device = dl[r];
+    int rc = init_comms(m, err);
+    if (rc != SBR_OK) {
         delete m;
-        return SBR_EDEVICE;
+        return rc;
     }
     for (int r = 0; r < n_gpus; r++) {
         Rank& k = m->ranks[r];
-        k.device = dl[r];
-        k.comm = comms[r];
-        int rc = sbr_init(dl[r], &k.kid);
-        if (rc == SBR_OK && (hipSetDevice(dl[r]) != hipSuccess ||
-                             hipStreamCreateWithFlags(&k.stream, hipStreamNonBlocking) != hipSuccess))
-            rc = SBR_EDEVICE;
+        rc = sbr_init(dl[r], &k.kid);
         if (rc != SBR_OK) {
             err = "per-device context";
             destroy(m);
             return rc;
         }
+        k.stream = sbr_ctx_stream(k.kid);
         kids.push_back(k.kid);
     }
     *out = m;
@@ -159,8 +269,7 @@ void destroy(sbr_multi* m)
         if (k.comm && R.ok) (void)R.CommDestroy(k.comm);
         for (void* p : {k.in, k.out, k.gather})
             if (p) (void)hipFree(p);
-        if (k.stream) (void)hipStreamDestroy(k.stream);
-        if (k.kid) (void)sbr_free(k.kid);
+        if (k.kid) (void)sbr_free(k.kid); // owns k.stream
     }
     delete m;
 }
@@ -171,47 +280,37 @@ sbr_ctx* child(sbr_multi* m, int r) { return (m && r >= 0 && r < (int)m->ranks.s
 
 const char* last_error(const sbr_multi* m) { return m ? m->err.c_str() : ""; }
 
-// One sweep over the ranks.  For rank r with cols_r columns:
+// One sweep over the ranks (plan, deal, pack, gather, scatter: sbr_shard.h).  For rank r
+// with cols_r columns:
 //   stage(r, cols_r, in_dev, stream) -> int   stages its inputs into in_dev (device)
-//   run(r, kid, stream, in_dev, out_fields)    enqueues the single-device sweep, writing
+//   run(r, cols_r, kid, stream, in_dev, out_fields)  enqueues the single-device sweep, writing
 //                                              field f of the block at out_fields[f]
-// Fields: result arrays of n_col·n_u·per_pt elements of esz bytes, u-fastest per column
-// (host == nullptr: not requested, still computed if the kernel needs a buffer).
-int run_sharded(sbr_multi* m, int64_t n_col, int64_t n_u, const std::vector<FieldSpec>& fields, size_t in_bytes,
-                const StageFn& stage, const RunFn& run)
+int run_sharded(sbr_multi* m, int64_t n_col, int64_t n_u, const std::vector<sbr_shard::Field>& fields,
+                size_t in_bytes, const StageFn& stage, const RunFn& run)
 {
+    m->err.clear();
     const int N = (int)m->ranks.size();
-    const Rccl& R = rccl();
+    const sbr_shard::Plan plan = sbr_shard::make_plan(N, n_col, n_u, fields);
     std::vector<int> rcs(N, SBR_OK);
     std::vector<std::string> errs(N);
-    std::vector<int64_t> cols(N), off(N + 1, 0);
-    for (int r = 0; r < N; r++) cols[r] = n_col > r ? (n_col - r + N - 1) / N : 0;
-    size_t per_col = 0; // packed bytes per column
-    for (const FieldSpec& f : fields) per_col += (size_t)n_u * f.per_pt * f.esz;
-    for (int r = 0; r < N; r++) off[r + 1] = off[r] + cols[r];
 
-    // phase 1: every shard on its GPU, to completion
+    // phase 1: every shard on its GPU, to completion (no collective is entered unless all succeed)
     {
         std::vector<std::thread> th;
         for (int r = 0; r < N; r++)
             th.emplace_back([&, r] {
                 Rank& k = m->ranks[r];
-                if (cols[r] == 0) return;
+                if (plan.cols[r] == 0) return;
                 if (hipSetDevice(k.device) != hipSuccess) { rcs[r] = SBR_EDEVICE; errs[r] = "hipSetDevice"; return; }
-                if (grow(&k.in, &k.in_bytes, in_bytes + 256) ||
-                    grow(&k.out, &k.out_bytes, (size_t)cols[r] * per_col + 256)) {
+                if (grow(&k.in, &k.in_bytes, in_bytes + 256) || grow(&k.out, &k.out_bytes, plan.block_bytes(r) + 256)) {
                     rcs[r] = SBR_ENOMEM;
                     errs[r] = "rank buffers";
                     return;
                 }
-                int rc = stage(r, cols[r], k.in, k.stream);
+                int rc = stage(r, plan.cols[r], k.in, k.stream);
                 std::vector<void*> fp;
-                size_t o = 0;
-                for (const FieldSpec& f : fields) {
-                    fp.push_back((char*)k.out + o);
-                    o += (size_t)cols[r] * n_u * f.per_pt * f.esz;
-                }
-                if (rc == SBR_OK) rc = run(r, cols[r], k.kid, k.stream, k.in, fp);
+                for (size_t o : sbr_shard::field_offsets(plan, r, fields)) fp.push_back((char*)k.out + o);
+                if (rc == SBR_OK) rc = run(r, plan.cols[r], k.kid, k.stream, k.in, fp);
                 if (rc == SBR_OK && hipStreamSynchronize(k.stream) != hipSuccess) rc = SBR_EDEVICE;
                 if (rc != SBR_OK) { rcs[r] = rc; errs[r] = sbr_last_error(k.kid); }
             });
@@ -223,60 +322,70 @@ int run_sharded(sbr_multi* m, int64_t n_col, int64_t n_u, const std::vector<Fiel
             return rcs[r];
         }
 
-    // phase 2: RCCL gather of the packed blocks to rank 0, then rank 0 scatters to the host
-    {
-        Rank& k0 = m->ranks[0];
-        if (hipSetDevice(k0.device) != hipSuccess) { m->err = "hipSetDevice"; return SBR_EDEVICE; }
-        if (grow(&k0.gather, &k0.gather_bytes, (size_t)n_col * per_col + 256)) { m->err = "gather buffer"; return SBR_ENOMEM; }
-        std::vector<std::thread> th;
-        for (int r = 0; r < N; r++)
-            th.emplace_back([&, r] {
-                Rank& k = m->ranks[r];
-                if (hipSetDevice(k.device) != hipSuccess) { rcs[r] = SBR_EDEVICE; errs[r] = "hipSetDevice"; return; }
-                ncclResult_t nr = ncclSuccess;
-                if (r == 0) {
-                    if (cols[0] > 0 &&
-                        hipMemcpyAsync(k.gather, k.out, (size_t)cols[0] * per_col, hipMemcpyDeviceToDevice, k.stream) !=
-                            hipSuccess) {
-                        rcs[r] = SBR_EDEVICE; errs[r] = "gather copy"; return;
-                    }
-                    nr = R.GroupStart();
-                    for (int q = 1; q < N && nr == ncclSuccess; q++)
-                        if (cols[q] > 0)
-                            nr = R.Recv((char*)k.gather + (size_t)off[q] * per_col, (size_t)cols[q] * per_col, ncclUint8,
-                                        q, k.comm, k.stream);
-                    const ncclResult_t ne = R.GroupEnd();
-                    if (nr == ncclSuccess) nr = ne;
-                } else if (cols[r] > 0) {
-                    nr = R.Send(k.out, (size_t)cols[r] * per_col, ncclUint8, 0, k.comm, k.stream);
-                }
-                if (nr != ncclSuccess) { rcs[r] = SBR_EDEVICE; errs[r] = std::string("rccl: ") + R.GetErrorString(nr); return; }
-                if (hipStreamSynchronize(k.stream) != hipSuccess) { rcs[r] = SBR_EDEVICE; errs[r] = "gather sync"; }
-            });
-        for (auto& t : th) t.join();
-        for (int r = 0; r < N; r++)
-            if (rcs[r] != SBR_OK) {
-                m->err = "rank " + std::to_string(r) + ": " + errs[r];
-                return rcs[r];
-            }
-        // scatter: block row c of rank r is grid column r + c·N
-        for (int r = 0; r < N; r++) {
-            if (cols[r] == 0) continue;
-            const char* blk = (const char*)k0.gather + (size_t)off[r] * per_col;
-            size_t o = 0;
-            for (const FieldSpec& f : fields) {
-                const size_t row = (size_t)n_u * f.per_pt * f.esz;
-                if (f.host) {
-                    hipError_t e = hipMemcpy2DAsync((char*)f.host + (size_t)r * row, (size_t)N * row, blk + o, row, row,
-                                                    (size_t)cols[r], hipMemcpyDeviceToHost, k0.stream);
-                    if (e != hipSuccess) { m->err = "result copy"; return SBR_EDEVICE; }
-                }
-                o += (size_t)cols[r] * row;
-            }
-        }
-        if (hipStreamSynchronize(k0.stream) != hipSuccess) { m->err = "result sync"; return SBR_EDEVICE; }
+    // phase 2, pre-checks: everything fallible before a send or receive is posted
+    Rank& k0 = m->ranks[0];
+    for (int r = 0; r < N; r++)
+        if (hipSetDevice(m->ranks[r].device) != hipSuccess) { m->err = "hipSetDevice"; return SBR_EDEVICE; }
+    if (hipSetDevice(k0.device) != hipSuccess) { m->err = "hipSetDevice"; return SBR_EDEVICE; }
+    if (grow(&k0.gather, &k0.gather_bytes, plan.gather_bytes() + 256)) { m->err = "gather buffer"; return SBR_ENOMEM; }
+    if (N > 1 && !m->comms_ok) {
+        int rc = init_comms(m, m->err);
+        if (rc) return rc;
+        (void)hipSetDevice(k0.device);
     }
+    // phase 2: the RCCL gather of the packed blocks to rank 0 …
+    {
+        RcclTransport tr(m);
+        std::vector<const void*> blocks;
+        for (const Rank& k : m->ranks) blocks.push_back(k.out);
+        const int rc = sbr_shard::gather(plan, tr, blocks, k0.gather);
+        if (rc) { m->err = tr.err.empty() ? "gather" : tr.err; return rc; }
+    }
+    // … and the strided scatter into the caller's arrays
+    if (hipSetDevice(k0.device) != hipSuccess) { m->err = "hipSetDevice"; return SBR_EDEVICE; }
+    const int rc = sbr_shard::scatter(plan, fields, k0.gather,
+                                      [&](void* d, size_t dp, const void* src, size_t sp, size_t w, size_t h) {
+                                          return hipMemcpy2DAsync(d, dp, src, sp, w, h, hipMemcpyDeviceToHost,
+                                                                  k0.stream) == hipSuccess ? 0 : SBR_EDEVICE;
+                                      });
+    if (rc) { m->err = "result copy"; return rc; }
+    if (hipStreamSynchronize(k0.stream) != hipSuccess) { m->err = "result sync"; return SBR_EDEVICE; }
     return SBR_OK;
 }
 
 }  // namespace sbr_multi_impl
+
+// ---------------------------------------------------------------------------
+// sbr_shard_host_run: the same plan / deal / pack / gather / scatter on host memory with the
+// loopback transport, the per-rank sweep supplied by the caller (tests: the CPU oracle).
+// ---------------------------------------------------------------------------
+extern "C" int sbr_shard_host_run(int32_t n_ranks, int64_t n_col, int64_t n_u, int32_t n_fields, const int64_t* esz,
+                                  const int64_t* per_pt, void* const* host_out, sbr_shard_compute_fn compute, void* user)
+{
+    if (n_ranks <= 0 || n_col <= 0 || n_u <= 0 || n_fields <= 0 || !esz || !per_pt || !host_out || !compute)
+        return SBR_EARG;
+    std::vector<sbr_shard::Field> fields;
+    for (int f = 0; f < n_fields; f++) {
+        if (esz[f] <= 0 || per_pt[f] <= 0) return SBR_EARG;
+        fields.push_back({host_out[f], (size_t)esz[f], (size_t)per_pt[f]});
+    }
+    const sbr_shard::Plan plan = sbr_shard::make_plan(n_ranks, n_col, n_u, fields);
+    std::vector<std::vector<char>> blocks(n_ranks);
+    std::vector<const void*> bp(n_ranks, nullptr);
+    for (int r = 0; r < n_ranks; r++) {
+        blocks[r].assign(plan.block_bytes(r) + 1, 0);
+        bp[r] = blocks[r].data();
+        if (plan.cols[r] == 0) continue;
+        std::vector<int64_t> ids(plan.cols[r]);
+        for (int64_t c = 0; c < plan.cols[r]; c++) ids[c] = sbr_shard::global_col(r, c, n_ranks);
+        std::vector<void*> fp;
+        for (size_t o : sbr_shard::field_offsets(plan, r, fields)) fp.push_back(blocks[r].data() + o);
+        const int rc = compute(user, r, plan.cols[r], ids.data(), fp.data());
+        if (rc) return rc;
+    }
+    std::vector<char> gathered(plan.gather_bytes() + 1, 0);
+    sbr_shard::LoopbackTransport tr;
+    int rc = sbr_shard::gather(plan, tr, bp, gathered.data());
+    if (rc) return SBR_EARG;
+    return sbr_shard::scatter(plan, fields, gathered.data(), sbr_shard::host_copy2d);
+}

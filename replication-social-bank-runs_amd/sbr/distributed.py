@@ -156,3 +156,60 @@ def sweep_interest_sharded(beta, eta, t_end, u, p, kappa, lam, r, delta, x0=1e-4
     if world == 1:
         return local
     return gather_columns(local, len(beta), len(u), world, rank, _device(device), root)
+
+
+class StepCollector:
+    """Collect the full result SoA of every step of a weak-scaled sweep, each step's grid on
+    one rank: step k — every rank's column shard of it — lands on rank k mod N (the
+    grid's "root").  A window of up to N consecutive steps k0 … k0+m−1 with distinct roots
+    is collected by one all-to-all per field (rank q sends its shard of step k to rank
+    k mod N), so every xGMI link carries its share in both directions.  A gather of every
+    step to rank 0 is capped by rank 0's inbound links instead: at config 3 each rank
+    produces ≈201 MB of results per ≈1.9 ms step, and 7 of those per step exceed the
+    ≈0.54 TB/s that one MI355X's 7 links take in.
+
+    fields: {name: tensor [n_steps, n_pts]} (this rank's shard of every step, one row per
+    step; any dtype the backend moves).  After collect(k0, m), rank (k mod N) holds, for
+    every field, ranks 0…N−1's shards of step k in ``recv[name][q]`` (q = source rank).
+    """
+
+    def __init__(self, fields: dict, world: int, rank: int):
+        self.fields, self.world, self.rank = fields, world, rank
+        self.n_pts = {f: t.shape[1] for f, t in fields.items()}
+        self.recv = {f: torch.empty(world, t.shape[1], dtype=t.dtype, device=t.device) for f, t in fields.items()}
+        self._empty = {f: torch.empty(0, dtype=t.dtype, device=t.device) for f, t in fields.items()}
+        self.last_roots: list[int] = []
+
+    def window_roots(self, k0: int, m: int) -> list[int]:
+        roots = [(k0 + i) % self.world for i in range(m)]
+        if m > self.world or len(set(roots)) != m:
+            raise ValueError("a window holds at most one step per root")
+        return roots
+
+    def collect(self, k0: int, m: int = 1, row0: int | None = None) -> None:
+        """Steps k0 … k0+m−1 are complete on every rank; move them to their roots.  Their
+        shards are rows row0 … row0+m−1 of each field (default row0 = k0; a caller that
+        reuses one row per step passes row0 = 0, m = 1).  The window must be contiguous in
+        root order (k0 mod N + m ≤ N), so that the shards to send are one contiguous slice
+        of each field."""
+        roots = self.window_roots(k0, m)
+        first = roots[0]
+        if first + m > self.world:
+            raise ValueError("window wraps past rank N-1: split it")
+        self.last_roots = roots
+        r0 = k0 if row0 is None else row0
+        for f, t in self.fields.items():
+            n = self.n_pts[f]
+            src = t[r0:r0 + m].reshape(-1)
+            in_splits = [n if first <= r < first + m else 0 for r in range(self.world)]
+            is_root = first <= self.rank < first + m
+            out = self.recv[f].view(-1) if is_root else self._empty[f]
+            dist.all_to_all_single(out, src, [n] * self.world if is_root else [0] * self.world, in_splits)
+
+    def windows(self, n_steps: int):
+        """(k0, m) windows covering steps 0 … n_steps−1, each within one round of N roots."""
+        k = 0
+        while k < n_steps:
+            m = min(self.world - k % self.world, n_steps - k)
+            yield k, m
+            k += m

@@ -123,3 +123,49 @@ def test_shard_columns_partition():
         allc = np.sort(np.concatenate(parts))
         assert np.array_equal(allc, np.arange(n))
         assert max(len(p) for p in parts) == D.max_shard(n, w)
+
+
+def _worker_collect(rank, world, port, out_path):
+    """Every step's full result SoA on its root (rank k mod N) via StepCollector."""
+    import torch
+    import torch.distributed as dist
+
+    sys.path.insert(0, os.path.join(REPO, "replication-social-bank-runs_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n_steps, n_pts = 7, 11
+    # rank r's shard of step k: values that encode (field, step, rank, point)
+    base = torch.arange(n_steps * n_pts, dtype=torch.float64).view(n_steps, n_pts)
+    fields = {"xi": base + 1000.0 * rank, "status": (base * 3 + rank).to(torch.int32),
+              "rk_steps": (base * 7 + 100000 * rank).to(torch.int64)}
+    col = D.StepCollector(fields, world, rank)
+    got = {}
+    for k0, m in col.windows(n_steps):
+        col.collect(k0, m)
+        for i, root in enumerate(col.last_roots):
+            if root == rank:
+                got[k0 + i] = {f: col.recv[f].clone().numpy() for f in fields}
+    np.savez(out_path + f".{rank}.npz", **{f"{k}_{f}": v for k, d in got.items() for f, v in d.items()})
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_step_collector_round_robin_roots(tmp_path, world):
+    out = str(tmp_path / "col")
+    mp.spawn(_worker_collect, args=(world, _free_port(), out), nprocs=world, join=True)
+    n_steps, n_pts = 7, 11
+    base = np.arange(n_steps * n_pts, dtype=np.float64).reshape(n_steps, n_pts)
+    seen = set()
+    for r in range(world):
+        d = np.load(out + f".{r}.npz")
+        for key in d.files:
+            k, f = key.split("_", 1)
+            k = int(k)
+            assert k % world == r  # step k is collected on rank k mod N
+            seen.add(k)
+            for q in range(world):
+                exp = {"xi": base[k] + 1000.0 * q, "status": (base[k] * 3 + q).astype(np.int32),
+                       "rk_steps": (base[k] * 7 + 100000 * q).astype(np.int64)}[f]
+                assert np.array_equal(d[key][q], exp), (k, f, q)
+    assert seen == set(range(n_steps))
