@@ -140,6 +140,8 @@ def parse():
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="one sbr_sweep_baseline_dev call per step (no learning/equilibrium overlap across steps)")
+    ap.add_argument("--ready", action="store_true",
+                    help="--no-pipeline: the per-column readiness schedule (SBR_FLAG_READY_SWEEP) instead of chunks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-stride", type=int, default=2, help="cpu_baseline samples every k-th β column")
     ap.add_argument("--phases", action="store_true",
@@ -218,7 +220,8 @@ def main():
         else:
             one = {k: v[0] for k, v in out.items()}
             for k in range(n):
-                eng.sweep_baseline_dev(beta[0], eta[0], t_end[0], u, p, kappa, lam, x0, one, stream=stream)
+                eng.sweep_baseline_dev(beta[0], eta[0], t_end[0], u, p, kappa, lam, x0, one, stream=stream,
+                                       flags=sbr._lib.SBR_FLAG_READY_SWEEP if a.ready else 0)
                 if gather:
                     col.collect(k, 1, row0=0)
 
@@ -277,6 +280,7 @@ def main():
                         if gather else None),
             "parallelism": f"beta-column shards x{world}",
             "pipelined": pipe,
+            "single_sweep_schedule": None if pipe else ("per-column readiness" if a.ready else "chunked"),
         },
         # pipelined: per-launch kernel times (HIP events around each launch on its stream);
         # single sweep: libsbr cuts the grid into column chunks whose kernels overlap, so the
@@ -284,7 +288,10 @@ def main():
         "kernel_ms_per_step": ({"learn_logistic": learn_ms / max(ncalls, 1), "equilibrium": eq_ms / max(ncalls, 1)}
                                if pipe else
                                {"learning_stage_wall": learn_ms / max(ncalls, 1),
-                                "equilibrium_tail_after_learning": eq_ms / max(ncalls, 1)}),
+                                "equilibrium_tail_after_learning": eq_ms / max(ncalls, 1)}
+                               if not a.ready else
+                               {"learn_logistic": learn_ms / max(ncalls, 1),
+                                "eq_ready_concurrent": eq_ms / max(ncalls, 1)}),
         "flops_per_step": {"equilibrium": f_eq, "learn": f_learn},
         "work_per_step": {"run_points": int(run.sum()), "bisect_iters": int(iters.sum()),
                           "aw_knots_run": int((run * n_tau[:, None]).sum()),

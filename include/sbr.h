@@ -55,6 +55,12 @@ typedef struct {
 /* Evaluate every τ̄ knot of the crossing scan and of the AW path (no block
  * summaries / branch-and-bound).  Same results; for A/B timing and checks. */
 #define SBR_FLAG_EXHAUSTIVE 0x1
+/* Single sweeps (sbr_sweep_baseline[_dev]): per-column readiness instead of the default
+ * three-chunk schedule — the learning kernel publishes each column the moment its lane has
+ * solved it, and one equilibrium workgroup per column (on CUs the learning waves do not
+ * use) runs its hazard and equilibria.  Same results; slower on the configs (the columns'
+ * learning ends late and the equilibria lose the learning CUs), kept for A/B. */
+#define SBR_FLAG_READY_SWEEP 0x2
 /* Diagnostics (timing breakdown only — results are NOT the reference's):
  * stop every point after the crossing scan / after the ξ bisection, or
  * report the number of 64-knot AW blocks evaluated in `iters` instead of

@@ -29,6 +29,14 @@ namespace sbr {
 #ifndef SBR_LEARN_BLOCK
 #define SBR_LEARN_BLOCK 64
 #endif
+
+// readiness sweeps: column b is complete (knots, counters, status written by this lane) —
+// release it to the equilibrium workgroups (agent scope: they run on other CUs / XCDs)
+__device__ __forceinline__ void publish_column(const LearnArgs& a, int b)
+{
+    const int k = atomicAdd(a.ready_tail, 1);
+    __hip_atomic_store(a.ready_q + k, b + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
 #ifndef SBR_LEARN_LANES
 #define SBR_LEARN_LANES 64 // columns per wave of learn_logistic_kernel
 #endif
@@ -57,6 +65,7 @@ __global__ __launch_bounds__(SBR_LEARN_BLOCK) void learn_logistic_kernel(const d
     if (live && (!(BETA > 0.0) || !(T1 > T0) || !(ETA > 0.0))) { // LearningParameters / EconomicParameters checks
         L.status[b] = SBR_ARG_INVALID;
         L.n_knots[b] = 0; L.n_tau[b] = 0; L.n_le[b] = 0; L.n_accept[b] = 0; L.n_reject[b] = 0;
+        if (a.ready_q) publish_column(a, b);
     } else if (live) {
     // ---- knot sink: store (t, G).  Branch-free: every attempted step writes its candidate
     // knot at the fill index n (a rejected one is overwritten by the next accepted step) and the
@@ -130,30 +139,40 @@ __global__ __launch_bounds__(SBR_LEARN_BLOCK) void learn_logistic_kernel(const d
         {
             return push(acc, tn, y1);
         }
+        // the column is learned: counters and status, then (readiness sweeps) its
+        // publication — called by ode_scalar the moment this lane's solve ends, while the
+        // other columns of the wave may still be integrating
+        const LearnBufs* Lp;
+        const LearnArgs* ap;
+        int b;
+        __device__ __forceinline__ void finish(const OdeOut& o)
+        {
+            st |= o.status;
+            int n_le = m < 0 ? n : m; // every knot ≤ η when none passed it
+            int n_tau = 0;
+            if (fuse) {
+                // hazard_kernel's η rule: with no knot past η, pdf(η) exists only if η is the last knot
+                if (m < 0 && ht != eta) {
+                    st |= SBR_OOB;
+                    n_le = 0;
+                } else {
+                    n_tau = hm;
+                }
+            }
+            Lp->n_knots[b] = n;
+            Lp->n_le[b] = n_le;
+            if (fuse) Lp->n_tau[b] = n_tau;
+            Lp->status[b] = st;
+            Lp->n_accept[b] = (int)o.naccept;
+            Lp->n_reject[b] = (int)o.nreject;
+            if (ap->ready_q) publish_column(*ap, b);
+        }
     } sink{T, Gv, fuse ? L.hr + row : nullptr, fuse ? L.hrI + row : nullptr, 0, L.cap, -1, 0.0, -INFINITY, ETA,
-           0, 0, a.stop_after_eta != 0 ? 1 : 0, st, fuse ? 1 : 0, 0, BETA, a.lam, a.p, 0.0, 0.0, 0.0, 0.0};
+           0, 0, a.stop_after_eta != 0 ? 1 : 0, st, fuse ? 1 : 0, 0, BETA, a.lam, a.p, 0.0, 0.0, 0.0, 0.0,
+           &L, &a, b};
     LogisticSys f{BETA};
     OdeOut o;
     ode_scalar(f, sink, T1, a.x0, a.rtol, a.atol, a.maxiters, o);
-    st |= o.status;
-    const int n = sink.n;
-    int n_le = sink.m < 0 ? n : sink.m; // every knot ≤ η when none passed it
-    int n_tau = 0;
-    if (fuse) {
-        // hazard_kernel's η rule: with no knot past η, pdf(η) exists only if η is the last knot
-        if (sink.m < 0 && sink.ht != ETA) {
-            st |= SBR_OOB;
-            n_le = 0;
-        } else {
-            n_tau = sink.hm;
-        }
-    }
-    L.n_knots[b] = n;
-    L.n_le[b] = n_le;
-    if (fuse) L.n_tau[b] = n_tau;
-    L.status[b] = st;
-    L.n_accept[b] = (int)o.naccept;
-    L.n_reject[b] = (int)o.nreject;
     }
 }
 
@@ -269,23 +288,21 @@ __device__ long long g_hzprof[8192 * 6];
 #define HZ_T0
 #define HZ_STAMP(ph)
 #endif
-__global__ __launch_bounds__(HZ_BLOCK) void hazard_kernel(const double* __restrict__ beta,
-                                                          const double* __restrict__ eta, LearnArgs a, LearnBufs L)
+// hazard_rate of column b by one workgroup of NT >= HZ_BLOCK threads (threads past HZ_BLOCK
+// only take part in the barriers): the τ̄ grid in chunks of HZ_LDS knots, e_i·g_i and the
+// trapezoid terms formed in parallel into LDS, one wave adds the terms left to right (the
+// reference's rounding order), and a last parallel pass turns the partial integrals into
+// HR_i.  LDS scratch: s_eg, s_t [HZ_LDS + 1], s_I [HZ_LDS], s_Ieta [1].  Every early
+// return is uniform over the workgroup.
+template <int NT, bool REGS = true>
+__device__ __forceinline__ void hazard_column(const int b, const double BETA, const double ETA, const LearnArgs& a,
+                                              const LearnBufs& L, double* s_eg, double* s_t, double* s_I,
+                                              double* s_Ieta)
 {
-    // The τ̄ grid in chunks of HZ_LDS knots: e_i·g_i and the trapezoid terms are formed in
-    // parallel into LDS, one thread adds the terms left to right (the reference's rounding
-    // order) out of LDS, and the partial integrals I_i are parked in the HR row; a last
-    // parallel pass turns them into HR_i.  24 KiB of LDS per block, so hazard blocks of the
-    // next batch still fit beside two equilibrium blocks on a CU.
-    __shared__ double s_eg[HZ_LDS + 1]; // s_eg[k + 1] = e·g of knot c0 + k; s_eg[0] that of knot c0 − 1
-    __shared__ double s_t[HZ_LDS + 1];  // τ̄ likewise
-    __shared__ double s_I[HZ_LDS];
-    __shared__ double s_Ieta;
-#ifndef SBR_HZ_NOPRIO
-    __builtin_amdgcn_s_setprio(3);
-#endif
+    static_assert(NT >= HZ_BLOCK, "hazard_column needs HZ_BLOCK threads");
+    const int tid = threadIdx.x;
+    const bool act = tid < HZ_BLOCK;
     HZ_T0;
-    const int b = blockIdx.x;
     const int n = L.n_knots[b];
     const uint32_t st = L.status[b];
     if (st & SBR_ARG_INVALID) return; // learn kernel already wrote the row
@@ -293,7 +310,7 @@ __global__ __launch_bounds__(HZ_BLOCK) void hazard_kernel(const double* __restri
     const double* __restrict__ T = L.t + row;
     const double* __restrict__ Gv = L.G + row;
     double* __restrict__ H = L.hr + row;
-    const double BETA = beta[b], ETA = eta[b], p = a.p, lam = a.lam;
+    const double p = a.p, lam = a.lam;
     const int m = L.n_le[b]; // #knots ≤ η (searchsortedlast + 1), counted by the learning kernel
     bool oob = false, push;
     if (m < n) {
@@ -305,7 +322,7 @@ __global__ __launch_bounds__(HZ_BLOCK) void hazard_kernel(const double* __restri
     }
     const int ntau = m + (push ? 1 : 0);
     if (oob) {
-        if (threadIdx.x == 0) {
+        if (tid == 0) {
             L.status[b] = st | SBR_OOB;
             L.n_tau[b] = 0;
             L.n_le[b] = 0;
@@ -325,32 +342,34 @@ __global__ __launch_bounds__(HZ_BLOCK) void hazard_kernel(const double* __restri
     // first use): the knots were written by another XCD's learning wave, so each one costs an
     // L2 miss, and one dependent miss per knot per thread would dominate the kernel.
     HZ_STAMP(0);
-    if (ntau <= HZ_BLOCK * HZ_REG) {
+    if (REGS && ntau <= HZ_BLOCK * HZ_REG) {
         // Every τ̄ knot of the column in registers (thread tid owns knots tid + 256·j): one
         // batch of global loads, the chunks fed to LDS from registers, I_i read back into
         // registers, HR written once.
         double tv[HZ_REG], egv[HZ_REG], numv[HZ_REG], iv[HZ_REG], gk[HZ_REG];
-        // loads first, unconditionally (indices clamped into the knots ≤ η), so that all of
-        // them are in flight at once; τ̄ = η and its interpolated pdf are selected after
-        const double pdf_eta = m < n ? pdf_at(m) : 0.0; // m == n: η is a knot, not pushed
+        if (act) {
+            // loads first, unconditionally (indices clamped into the knots ≤ η), so that all of
+            // them are in flight at once; τ̄ = η and its interpolated pdf are selected after
+            const double pdf_eta = m < n ? pdf_at(m) : 0.0; // m == n: η is a knot, not pushed
 #pragma unroll
-        for (int j = 0; j < HZ_REG; j++) {
-            const int i = threadIdx.x + HZ_BLOCK * j;
-            const int ic = i < m ? i : m - 1;
-            tv[j] = T[ic];
-            gk[j] = Gv[ic];
-        }
+            for (int j = 0; j < HZ_REG; j++) {
+                const int i = tid + HZ_BLOCK * j;
+                const int ic = i < m ? i : m - 1;
+                tv[j] = T[ic];
+                gk[j] = Gv[ic];
+            }
 #pragma unroll
-        for (int j = 0; j < HZ_REG; j++) {
-            const int i = threadIdx.x + HZ_BLOCK * j;
-            const double x = gk[j];
-            const double ti = i < m ? tv[j] : ETA;
-            const double g = i < m ? (BETA * x) * (1.0 - x) : pdf_eta;
-            const double E = sbr_exp(lam * ti);
-            tv[j] = ti;
-            egv[j] = E * g;        // e_i = exp(λτ̄_i)·pdf_i
-            numv[j] = (p * E) * g; // the HR numerator (p·exp(λτ̄_i))·pdf_i
-            iv[j] = 0.0;
+            for (int j = 0; j < HZ_REG; j++) {
+                const int i = tid + HZ_BLOCK * j;
+                const double x = gk[j];
+                const double ti = i < m ? tv[j] : ETA;
+                const double g = i < m ? (BETA * x) * (1.0 - x) : pdf_eta;
+                const double E = sbr_exp(lam * ti);
+                tv[j] = ti;
+                egv[j] = E * g;        // e_i = exp(λτ̄_i)·pdf_i
+                numv[j] = (p * E) * g; // the HR numerator (p·exp(λτ̄_i))·pdf_i
+                iv[j] = 0.0;
+            }
         }
         double I = 0.0;
         constexpr int RPC = HZ_LDS / HZ_BLOCK; // register slots per LDS chunk
@@ -359,45 +378,52 @@ __global__ __launch_bounds__(HZ_BLOCK) void hazard_kernel(const double* __restri
             const int c0 = c * HZ_LDS;
             if (c0 < ntau) { // uniform
                 const int cn = ntau - c0 < HZ_LDS ? ntau - c0 : HZ_LDS;
+                if (act) {
 #pragma unroll
-                for (int r = 0; r < RPC; r++) {
-                    const int k = threadIdx.x + HZ_BLOCK * r;
-                    s_t[k + 1] = tv[c * RPC + r];
-                    s_eg[k + 1] = egv[c * RPC + r];
-                }
-                if (c > 0 && threadIdx.x == HZ_BLOCK - 1) { // knot c0 − 1 is this thread's last slot
-                    s_t[0] = tv[c * RPC - 1];
-                    s_eg[0] = egv[c * RPC - 1];
+                    for (int r = 0; r < RPC; r++) {
+                        const int k = tid + HZ_BLOCK * r;
+                        s_t[k + 1] = tv[c * RPC + r];
+                        s_eg[k + 1] = egv[c * RPC + r];
+                    }
+                    if (c > 0 && tid == HZ_BLOCK - 1) { // knot c0 − 1 is this thread's last slot
+                        s_t[0] = tv[c * RPC - 1];
+                        s_eg[0] = egv[c * RPC - 1];
+                    }
                 }
                 __syncthreads();
                 HZ_STAMP(1);
-                for (int k = threadIdx.x; k < cn; k += HZ_BLOCK)
-                    s_I[k] = c0 + k == 0 ? 0.0 : (0.5 * (s_eg[k] + s_eg[k + 1])) * (s_t[k + 1] - s_t[k]);
+                if (act)
+                    for (int k = tid; k < cn; k += HZ_BLOCK)
+                        s_I[k] = c0 + k == 0 ? 0.0 : (0.5 * (s_eg[k] + s_eg[k + 1])) * (s_t[k + 1] - s_t[k]);
                 __syncthreads();
                 HZ_STAMP(2);
-                if (threadIdx.x < 64) hz_scan_wave(s_I, cn, I);
+                if (tid < 64) hz_scan_wave(s_I, cn, I);
                 __syncthreads();
                 HZ_STAMP(3);
+                if (act) {
 #pragma unroll
-                for (int r = 0; r < RPC; r++) {
-                    const int k = threadIdx.x + HZ_BLOCK * r;
-                    if (k < cn) iv[c * RPC + r] = s_I[k];
+                    for (int r = 0; r < RPC; r++) {
+                        const int k = tid + HZ_BLOCK * r;
+                        if (k < cn) iv[c * RPC + r] = s_I[k];
+                    }
                 }
                 __syncthreads(); // the chunk's LDS is reused
                 HZ_STAMP(4);
             }
         }
-        if (threadIdx.x == 0) {
-            s_Ieta = I;
+        if (tid == 0) {
+            s_Ieta[0] = I;
             L.n_tau[b] = ntau;
             L.n_le[b] = m;
         }
         __syncthreads();
-        const double Ieta = s_Ieta, omp = 1.0 - p;
+        const double Ieta = s_Ieta[0], omp = 1.0 - p;
+        if (act) {
 #pragma unroll
-        for (int j = 0; j < HZ_REG; j++) {
-            const int i = threadIdx.x + HZ_BLOCK * j;
-            if (i < ntau) H[i] = numv[j] / ((p * iv[j]) + (omp * Ieta));
+            for (int j = 0; j < HZ_REG; j++) {
+                const int i = tid + HZ_BLOCK * j;
+                if (i < ntau) H[i] = numv[j] / ((p * iv[j]) + (omp * Ieta));
+            }
         }
         HZ_STAMP(5);
         return;
@@ -405,46 +431,68 @@ __global__ __launch_bounds__(HZ_BLOCK) void hazard_kernel(const double* __restri
     double I = 0.0, egprev = 0.0, tprev = 0.0; // thread 0: running integral; the chunk's last e·g, τ̄
     for (int c0 = 0; c0 < ntau; c0 += HZ_LDS) {
         const int cn = ntau - c0 < HZ_LDS ? ntau - c0 : HZ_LDS;
-        if (threadIdx.x == 0) { s_eg[0] = egprev; s_t[0] = tprev; }
+        if (tid == 0) { s_eg[0] = egprev; s_t[0] = tprev; }
+        if (act) {
 #pragma unroll 4
-        for (int k = threadIdx.x; k < cn; k += HZ_BLOCK) {
-            const int i = c0 + k;
-            const double ti = tau_at(i);
-            s_t[k + 1] = ti;
-            s_eg[k + 1] = sbr_exp(lam * ti) * pdf_at(i); // e_i = exp(λτ̄_i)·pdf_i
+            for (int k = tid; k < cn; k += HZ_BLOCK) {
+                const int i = c0 + k;
+                const double ti = tau_at(i);
+                s_t[k + 1] = ti;
+                s_eg[k + 1] = sbr_exp(lam * ti) * pdf_at(i); // e_i = exp(λτ̄_i)·pdf_i
+            }
         }
         __syncthreads();
         HZ_STAMP(1);
         // trapezoid term of i pairs e_{i-1}, e_i (solver.jl:173-175); term_0 = 0
-        for (int k = threadIdx.x; k < cn; k += HZ_BLOCK)
-            s_I[k] = c0 + k == 0 ? 0.0 : (0.5 * (s_eg[k] + s_eg[k + 1])) * (s_t[k + 1] - s_t[k]);
+        if (act)
+            for (int k = tid; k < cn; k += HZ_BLOCK)
+                s_I[k] = c0 + k == 0 ? 0.0 : (0.5 * (s_eg[k] + s_eg[k + 1])) * (s_t[k + 1] - s_t[k]);
         __syncthreads();
         HZ_STAMP(2);
-        if (threadIdx.x < 64) hz_scan_wave(s_I, cn, I); // I_i = I_{i-1} + term_i, left to right
-        if (threadIdx.x == 0) {
+        if (tid < 64) hz_scan_wave(s_I, cn, I); // I_i = I_{i-1} + term_i, left to right
+        if (tid == 0) {
             egprev = s_eg[cn];
             tprev = s_t[cn];
         }
         __syncthreads();
         HZ_STAMP(3);
-        for (int k = threadIdx.x; k < cn; k += HZ_BLOCK) H[c0 + k] = s_I[k]; // I_i parked in the HR row
+        if (act)
+            for (int k = tid; k < cn; k += HZ_BLOCK) H[c0 + k] = s_I[k]; // I_i parked in the HR row
         __syncthreads(); // the chunk's LDS is reused
         HZ_STAMP(4);
     }
-    if (threadIdx.x == 0) {
-        s_Ieta = I;
+    if (tid == 0) {
+        s_Ieta[0] = I;
         L.n_tau[b] = ntau;
         L.n_le[b] = m;
     }
     __syncthreads();
     // HR_i = (p·exp(λτ̄_i))·pdf_i / (p·I_i + (1 − p)·I_η); each thread reads back the I_i it parked
-    const double Ieta = s_Ieta, omp = 1.0 - p;
+    const double Ieta = s_Ieta[0], omp = 1.0 - p;
+    if (act) {
 #pragma unroll 4
-    for (int i = threadIdx.x; i < ntau; i += HZ_BLOCK) {
-        const double E = sbr_exp(lam * tau_at(i));
-        H[i] = ((p * E) * pdf_at(i)) / ((p * H[i]) + (omp * Ieta));
+        for (int i = tid; i < ntau; i += HZ_BLOCK) {
+            const double E = sbr_exp(lam * tau_at(i));
+            H[i] = ((p * E) * pdf_at(i)) / ((p * H[i]) + (omp * Ieta));
+        }
     }
     HZ_STAMP(5);
+}
+
+__global__ __launch_bounds__(HZ_BLOCK) void hazard_kernel(const double* __restrict__ beta,
+                                                          const double* __restrict__ eta, LearnArgs a, LearnBufs L)
+{
+    // 24 KiB of LDS per block, so hazard blocks of the next batch still fit beside two
+    // equilibrium blocks on a CU
+    __shared__ double s_eg[HZ_LDS + 1]; // s_eg[k + 1] = e·g of knot c0 + k; s_eg[0] that of knot c0 − 1
+    __shared__ double s_t[HZ_LDS + 1];  // τ̄ likewise
+    __shared__ double s_I[HZ_LDS];
+    __shared__ double s_Ieta;
+#ifndef SBR_HZ_NOPRIO
+    __builtin_amdgcn_s_setprio(3);
+#endif
+    const int b = blockIdx.x;
+    hazard_column<HZ_BLOCK>(b, beta[b], eta[b], a, L, s_eg, s_t, s_I, &s_Ieta);
 }
 
 // ============================================================================
@@ -1029,17 +1077,15 @@ __device__ __forceinline__ void solve_interest_point(P T, P G, P H, const Summ& 
                        tout);
 }
 
+// The equilibria of u values [j0, j1) of column b by one workgroup of BLOCK threads (smem:
+// the dynamic LDS slab of launch_equilibrium's size).  Starts and ends uniformly; the caller
+// puts a barrier between two calls on the same workgroup (the LDS slab and flags are reused).
 template <int BLOCK, bool INTEREST>
-__global__ __launch_bounds__(BLOCK, INTEREST ? 1 : SBR_EQ_MINW) void equilibrium_kernel(LearnBufs L, const double* __restrict__ eta,
-                                                            const double* __restrict__ t_end,
-                                                            const double* __restrict__ u, EqArgs a, InterestArgs ia,
-                                                            ResultSoA out)
+__device__ __forceinline__ void eq_column(const int b, const int j0, const int j1, const LearnBufs& L,
+                                          const double* __restrict__ eta, const double* __restrict__ t_end,
+                                          const double* __restrict__ u, const EqArgs& a, const InterestArgs& ia,
+                                          const ResultSoA& out, double* smem)
 {
-    extern __shared__ double smem[];
-#if SBR_EQ_PRIO
-    __builtin_amdgcn_s_setprio(SBR_EQ_PRIO); // A/B: issue priority over co-resident learning waves
-#endif
-    const int b = SBR_EQ_REVERSE ? (int)(gridDim.y - 1 - blockIdx.y) : (int)blockIdx.y;
     const int n = L.n_knots[b], ntau = L.n_tau[b], nle = L.n_le[b];
     const uint32_t lst = L.status[b];
     const size_t row = (size_t)b * (size_t)L.cap;
@@ -1171,8 +1217,6 @@ __global__ __launch_bounds__(BLOCK, INTEREST ? 1 : SBR_EQ_MINW) void equilibrium
     // at the end of the block while the run points (bisection + AW_max) of its
     // neighbours finish.  Consecutive u in one wave keep its lanes on similar
     // control paths (runs form a prefix in u on the paper's grids).
-    const int j0 = blockIdx.x * EQ_TILE;
-    const int j1 = j0 + EQ_TILE < a.n_u ? j0 + EQ_TILE : a.n_u;
     const int lane = threadIdx.x & 63;
     const double ETA = eta[b], T1 = t_end[b];
     const uint32_t lbits = lst & (SBR_ODE_MAXITERS | SBR_STIFF_SWITCH | SBR_ODE_FAILED | SBR_KNOT_OVERFLOW);
@@ -1217,6 +1261,93 @@ __global__ __launch_bounds__(BLOCK, INTEREST ? 1 : SBR_EQ_MINW) void equilibrium
     }
 }
 
+template <int BLOCK, bool INTEREST>
+__global__ __launch_bounds__(BLOCK, INTEREST ? 1 : SBR_EQ_MINW) void equilibrium_kernel(LearnBufs L, const double* __restrict__ eta,
+                                                            const double* __restrict__ t_end,
+                                                            const double* __restrict__ u, EqArgs a, InterestArgs ia,
+                                                            ResultSoA out)
+{
+    extern __shared__ double smem[];
+#if SBR_EQ_PRIO
+    __builtin_amdgcn_s_setprio(SBR_EQ_PRIO); // A/B: issue priority over co-resident learning waves
+#endif
+    const int b = SBR_EQ_REVERSE ? (int)(gridDim.y - 1 - blockIdx.y) : (int)blockIdx.y;
+    const int j0 = blockIdx.x * EQ_TILE;
+    const int j1 = j0 + EQ_TILE < a.n_u ? j0 + EQ_TILE : a.n_u;
+    eq_column<BLOCK, INTEREST>(b, j0, j1, L, eta, t_end, u, a, ia, out, smem);
+}
+
+// ============================================================================
+// Readiness sweep, equilibrium side: workgroups take (column, u-tile) items in the order the
+// learning kernel publishes the columns (ReadyArgs), so that a column's equilibria start as
+// soon as its own ODE is solved instead of after the slowest column of the grid.  The
+// tile-0 taker runs the column's hazard_rate first.
+// ============================================================================
+// poll *p (acquire) until it is set; 0 after `limit` polls or once another workgroup has
+// given up (*err set): a stuck schedule drains in one timeout, not one per workgroup
+__device__ __forceinline__ int ready_wait(const int32_t* p, const int32_t* err, int limit)
+{
+    int v = 0;
+    for (int k = 0; k < limit; k++) {
+#ifdef SBR_READY_RELAXED // A/B only (timing of the cache maintenance): no acquire
+        v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+        v = __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+#endif
+        if (v) break;
+        if ((k & 63) == 63 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+        __builtin_amdgcn_s_sleep(8);
+    }
+    return v;
+}
+
+// One workgroup per item, n_items in the grid: a workgroup draws its item ticket when it
+// starts (tickets follow the publication order, so resident workgroups wait for the columns
+// that come next), rather than persistent workgroups looping over items — a loop around the
+// equilibrium body lets the compiler hoist its invariants and spill the 80-VGPR budget.
+__global__ __launch_bounds__(SBR_EQ_WIDE, SBR_EQ_MINW) void eq_ready_kernel(LearnBufs L, const double* __restrict__ beta,
+                                                                            const double* __restrict__ eta,
+                                                                            const double* __restrict__ t_end,
+                                                                            const double* __restrict__ u, LearnArgs la,
+                                                                            EqArgs a, ReadyArgs ra, ResultSoA out)
+{
+    extern __shared__ double smem[];
+    __shared__ int s_col, s_tile;
+    const InterestArgs none{0.0, 1.0, 0.0, 0.0, 0, nullptr, nullptr, nullptr};
+    if (threadIdx.x == 0) {
+        const int it = atomicAdd(ra.head, 1);
+        int col = -1, tile = 0;
+        if (it < ra.n_items) {
+            const int slot = it / ra.tiles;
+            tile = it - slot * ra.tiles;
+            const int v = ready_wait(ra.q + slot, ra.head + 1, ra.spin_limit);
+            col = v ? v - 1 : -2;
+            if (col >= 0 && tile > 0 && !ready_wait(ra.hz_flag + col, ra.head + 1, ra.spin_limit)) col = -2;
+        }
+        s_col = col;
+        s_tile = tile;
+    }
+    __syncthreads();
+    const int col = __builtin_amdgcn_readfirstlane(s_col), tile = __builtin_amdgcn_readfirstlane(s_tile);
+    if (col == -1) return;
+    if (col == -2) { // gave up waiting (a bug guard): the grid still drains
+        if (threadIdx.x == 0) atomicOr(ra.head + 1, 1);
+        return;
+    }
+    if (tile == 0) {
+        // (the LDS-chunked path: the register-resident one needs 5 × 16 doubles per thread,
+        // which the equilibrium's 80-VGPR budget would spill)
+        hazard_column<SBR_EQ_WIDE, false>(col, beta[col], eta[col], la, L, smem, smem + (HZ_LDS + 1),
+                                          smem + 2 * (HZ_LDS + 1), smem + 3 * HZ_LDS + 2);
+        __syncthreads();
+        if (threadIdx.x == 0 && ra.tiles > 1)
+            __hip_atomic_store(ra.hz_flag + col, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const int j0 = tile * ra.tile_u;
+    const int j1 = j0 + ra.tile_u < a.n_u ? j0 + ra.tile_u : a.n_u;
+    eq_column<SBR_EQ_WIDE, false>(col, j0, j1, L, eta, t_end, u, a, none, out, smem);
+}
+
 // ============================================================================
 // launchers
 // ============================================================================
@@ -1228,6 +1359,7 @@ hipError_t launch_learn_logistic(const double* beta, const double* eta, const do
     hipLaunchKernelGGL(learn_logistic_kernel, grid, dim3(SBR_LEARN_BLOCK), 0, s, beta, eta, t_end, a, L);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
+    if (a.ready_q) return hipSuccess; // readiness sweep: eq_ready_kernel runs each column's hazard
     if (a.fuse_hazard) {
         hipLaunchKernelGGL(hazard_norm_kernel, dim3(a.n_beta), dim3(HN_BLOCK), 0, s, a, L);
         return hipGetLastError();
@@ -1254,6 +1386,19 @@ hipError_t launch_equilibrium(const LearnBufs& L, const double* eta, const doubl
         hipLaunchKernelGGL((equilibrium_kernel<256, false>), grid, dim3(256), lds, s, L, eta, t_end, u, a, none, out);
     else
         hipLaunchKernelGGL((equilibrium_kernel<64, false>), grid, dim3(64), lds, s, L, eta, t_end, u, a, none, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_eq_ready(const LearnBufs& L, const double* beta, const double* eta, const double* t_end,
+                           const double* u, const LearnArgs& la, const EqArgs& a, const ReadyArgs& ra,
+                           const ResultSoA& out, int n_blocks, hipStream_t s)
+{
+    size_t lds = ((size_t)2 * a.lds_cap + 2 * ((a.lds_cap >> 6) + 1) + 2 * ((a.lds_cap >> 3) + 1)) * sizeof(double);
+    const size_t hz = (size_t)(3 * HZ_LDS + 3) * sizeof(double); // hazard scratch shares the slab
+    if (lds < hz) lds = hz;
+    (void)n_blocks; // one workgroup per item
+    hipLaunchKernelGGL(eq_ready_kernel, dim3(ra.n_items), dim3(SBR_EQ_WIDE), lds, s, L, beta, eta, t_end, u, la, a, ra,
+                       out);
     return hipGetLastError();
 }
 

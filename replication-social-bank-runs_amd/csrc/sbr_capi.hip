@@ -109,6 +109,15 @@ struct sbr_ctx {
         hipEvent_t a, b;
     };
     std::vector<TRec> trec;
+    // readiness schedule of single sweeps: the learning kernel and the equilibrium workgroups
+    // on streams with disjoint CU masks (hipExtStreamCreateWithCUMask), and the publication
+    // queue [head, err, tail, pad, q[n_beta], hz_flag[n_beta]]
+    hipStream_t rs_learn = nullptr, rs_eq = nullptr;
+    int rs_state = 0; // 0 untried, 1 available, -1 unavailable (chunked schedule instead)
+    bool rs_used = false; // the last run_baseline took the readiness schedule
+    int32_t* rq = nullptr;
+    size_t rq_cap = 0;
+    hipEvent_t ev_rin = nullptr, ev_rq = nullptr, ev_rl = nullptr, ev_re = nullptr;
 };
 
 namespace {
@@ -450,6 +459,85 @@ constexpr int kSweepChunks = sbr_ctx::kLearnStreams;
 #ifndef SBR_SWEEP_FRONT
 #define SBR_SWEEP_FRONT 32 // 0: halving chunks only (A/B: 4.44 -> 4.25 ms per config-3 sweep)
 #endif
+#ifndef SBR_READY_LEARN_CUS
+#define SBR_READY_LEARN_CUS 64 // CUs reserved for the learning waves (8 / 16 / 32 / 64: 13.3 / 9.2 / 3.5 / 3.0 ms of learning)
+#endif
+#ifndef SBR_READY_TILE_U
+#define SBR_READY_TILE_U 4096 // u values per equilibrium workgroup (768: three tiles of a config-3 column, 6.7 vs 5.5 ms)
+#endif
+#ifndef SBR_READY_SPIN
+#define SBR_READY_SPIN (1 << 24) // polls (≈ 0.5 µs each) before a waiting workgroup gives up: a bug guard
+#endif
+
+// the streams with disjoint CU masks and the queue of a readiness sweep
+int ensure_ready(sbr_ctx* c, size_t n_beta)
+{
+    if (c->rs_state == 0) {
+        c->rs_state = -1;
+        int ncu = 0;
+        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device);
+        if (ncu >= 4 * SBR_READY_LEARN_CUS) {
+            std::vector<uint32_t> ml((size_t)(ncu + 31) / 32, 0u), me(ml.size(), 0u);
+            for (int i = 0; i < ncu; i++) (i < SBR_READY_LEARN_CUS ? ml : me)[(size_t)i / 32] |= 1u << (i % 32);
+            if (hipExtStreamCreateWithCUMask(&c->rs_learn, (uint32_t)ml.size(), ml.data()) == hipSuccess &&
+                hipExtStreamCreateWithCUMask(&c->rs_eq, (uint32_t)me.size(), me.data()) == hipSuccess &&
+                hipEventCreateWithFlags(&c->ev_rin, SBR_SYNC_EVENT_FLAGS) == hipSuccess &&
+                hipEventCreateWithFlags(&c->ev_rq, SBR_SYNC_EVENT_FLAGS) == hipSuccess &&
+                hipEventCreateWithFlags(&c->ev_rl, SBR_SYNC_EVENT_FLAGS) == hipSuccess &&
+                hipEventCreateWithFlags(&c->ev_re, SBR_SYNC_EVENT_FLAGS) == hipSuccess)
+                c->rs_state = 1;
+        }
+    }
+    if (c->rs_state != 1) return SBR_EDEVICE;
+    const size_t need = 4 + 2 * n_beta;
+    if (need > c->rq_cap) {
+        if (c->rq) (void)hipFree(c->rq);
+        c->rq = nullptr;
+        c->rq_cap = 0;
+        HIP_TRY(c, hipMalloc(&c->rq, need * 4), SBR_ENOMEM);
+        c->rq_cap = need;
+    }
+    return SBR_OK;
+}
+
+// One sweep, readiness schedule (SBR_FLAG_READY_SWEEP): the learning kernel publishes every
+// column the moment its lane has solved it (release), and one equilibrium workgroup per
+// (column, u-tile) — in publication order, on the CUs the learning waves do not use — runs
+// the column's hazard (tile 0) and equilibria (acquire).  Measured on config 3 it is slower
+// than the chunked schedule (5.5 vs 4.3 ms): most columns' learning ends late (≈2.8k steps of
+// a ≈4.4k-step maximum), so the equilibria cannot start much earlier, and they lose the
+// learning CUs.  Timing records: kind 0 = the learning kernel, kind 1 = the equilibrium
+// kernel (concurrent).
+int run_baseline_ready(sbr_ctx* c, hipStream_t s, const double* beta, const double* eta, const double* t_end,
+                       const double* u, int64_t n_beta, int64_t n_u, double kappa, const sbr_opts& o,
+                       sbr::LearnArgs la, const sbr::ResultSoA& out)
+{
+    const int tiles = (int)((n_u + SBR_READY_TILE_U - 1) / SBR_READY_TILE_U);
+    int32_t* q = c->rq;
+    HIP_TRY(c, hipEventRecord(c->ev_rin, s), SBR_EDEVICE);
+    HIP_TRY(c, hipStreamWaitEvent(c->rs_learn, c->ev_rin, 0), SBR_EDEVICE);
+    HIP_TRY(c, hipMemsetAsync(q, 0, (4 + 2 * (size_t)n_beta) * 4, c->rs_learn), SBR_EDEVICE);
+    HIP_TRY(c, hipEventRecord(c->ev_rq, c->rs_learn), SBR_EDEVICE);
+    HIP_TRY(c, hipStreamWaitEvent(c->rs_eq, c->ev_rq, 0), SBR_EDEVICE);
+    la.fuse_hazard = 0;
+    la.ready_tail = q + 2;
+    la.ready_q = q + 4;
+    hipEvent_t t0 = tstart(c, c->rs_learn);
+    HIP_TRY(c, sbr::launch_learn_logistic(beta, eta, t_end, la, c->LW[0], c->rs_learn), SBR_EDEVICE);
+    tend(c, c->rs_learn, 0, t0);
+    sbr::EqArgs ea{kappa, (int32_t)n_u, o.bisect_max_iters, c->lds_cap_b, nullptr,
+                   (o.flags & SBR_FLAG_EXHAUSTIVE) ? 1 : 0, (o.flags >> 8) & 7};
+    sbr::ReadyArgs ra{q, q + 4, q + 4 + n_beta, (int32_t)(n_beta * tiles), tiles, SBR_READY_TILE_U, SBR_READY_SPIN};
+    hipEvent_t t1 = tstart(c, c->rs_eq);
+    HIP_TRY(c, sbr::launch_eq_ready(c->LW[0], beta, eta, t_end, u, la, ea, ra, out, 0, c->rs_eq), SBR_EDEVICE);
+    tend(c, c->rs_eq, 1, t1);
+    HIP_TRY(c, hipEventRecord(c->ev_rl, c->rs_learn), SBR_EDEVICE);
+    HIP_TRY(c, hipEventRecord(c->ev_re, c->rs_eq), SBR_EDEVICE);
+    HIP_TRY(c, hipStreamWaitEvent(s, c->ev_rl, 0), SBR_EDEVICE);
+    HIP_TRY(c, hipStreamWaitEvent(s, c->ev_re, 0), SBR_EDEVICE);
+    return SBR_OK;
+}
+
 int run_baseline(sbr_ctx* c, hipStream_t s, const double* beta, const double* eta, const double* t_end, double x0,
                  const double* u, int64_t n_beta, int64_t n_u, double p, double kappa, double lambda,
                  const sbr_opts& o, const sbr::ResultSoA& out, double* aw_path)
@@ -458,6 +546,10 @@ int run_baseline(sbr_ctx* c, hipStream_t s, const double* beta, const double* et
     if (rc) return rc;
     c->last_slot = 0;
     sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, p, lambda, o.ode_maxiters, (int32_t)n_beta, 1, 0};
+    // per-column readiness on request (SBR_FLAG_READY_SWEEP): see above
+    c->rs_used = !aw_path && n_beta >= 64 && (o.flags & SBR_FLAG_READY_SWEEP) &&
+                 ensure_ready(c, (size_t)n_beta) == SBR_OK;
+    if (c->rs_used) return run_baseline_ready(c, s, beta, eta, t_end, u, n_beta, n_u, kappa, o, la, out);
     if (aw_path || n_beta < 64 * kSweepChunks) {
         hipEvent_t t0 = tstart(c, s);
         HIP_TRY(c, sbr::launch_learn_logistic(beta, eta, t_end, la, c->LW[0], s), SBR_EDEVICE);
@@ -686,6 +778,11 @@ int sbr_free(sbr_ctx* c)
     }
     for (int k = 0; k < sbr_ctx::kLearnStreams; k++)
         if (c->lstream[k]) (void)hipStreamDestroy(c->lstream[k]);
+    for (hipStream_t rs : {c->rs_learn, c->rs_eq})
+        if (rs) { (void)hipStreamSynchronize(rs); (void)hipStreamDestroy(rs); }
+    for (hipEvent_t e : {c->ev_rin, c->ev_rq, c->ev_rl, c->ev_re})
+        if (e) (void)hipEventDestroy(e);
+    if (c->rq) (void)hipFree(c->rq);
     if (c->stage) (void)hipFree(c->stage);
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->ev_grid) (void)hipEventDestroy(e);
@@ -851,7 +948,10 @@ int sbr_sweep_baseline(sbr_ctx* c, const double* beta, const double* eta, const 
             if (hs[k]) HIP_TRY(c, hipMemcpyAsync(hs[k], dres + k * np, np * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
         if (out->status) HIP_TRY(c, hipMemcpyAsync(out->status, r.status, np * 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
         if (out->iters) HIP_TRY(c, hipMemcpyAsync(out->iters, r.iters, np * 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        int32_t gave_up = 0;
+        if (c->rs_used) HIP_TRY(c, hipMemcpyAsync(&gave_up, c->rq + 1, 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
         HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
+        if (gave_up) return fail(c, SBR_EDEVICE, "readiness schedule: an equilibrium workgroup timed out");
         if (o.early_exit_nan_run > 0 && out->status && out->xi && out->aw_max && out->tol)
             sbr_apply_early_exit(n_beta, n_u, o.early_exit_nan_run, out);
         return SBR_OK;
@@ -1082,6 +1182,8 @@ int sbr_timing_read(sbr_ctx* c, void* stream, double* learn_ms, double* eq_ms, i
     int32_t n = 0;
     for (hipStream_t ls : c->lstream)
         if (ls) HIP_TRY(c, hipStreamSynchronize(ls), SBR_EDEVICE);
+    for (hipStream_t rs : {c->rs_learn, c->rs_eq})
+        if (rs) HIP_TRY(c, hipStreamSynchronize(rs), SBR_EDEVICE);
     for (const auto& r : c->trec) {
         float t = 0.f;
         HIP_TRY(c, hipEventElapsedTime(&t, r.a, r.b), SBR_EDEVICE);

@@ -27,6 +27,26 @@ struct LearnArgs {
     int32_t n_beta;
     int32_t stop_after_eta;
     int32_t fuse_hazard; // learn_logistic_kernel: stream hazard_rate with the knots (needs hrI)
+    // per-column readiness (single sweeps, null otherwise): the lane that finishes column b
+    // takes slot k = atomicAdd(ready_tail, 1) and release-stores b + 1 into ready_q[k]
+    int32_t* ready_tail;
+    int32_t* ready_q;
+};
+
+// The equilibrium side of a readiness sweep (eq_ready_kernel): one workgroup per item, each
+// drawing its ticket it = atomicAdd(head, 1) < n_items when it starts; item it is tile it % tiles of the column
+// published in ready_q[it / tiles] (acquire, spinning until it appears).  The tile-0 taker
+// computes the column's hazard_rate and release-stores hz_flag[b] = 1; the other tiles
+// acquire it before reading HR.  A wait longer than spin_limit polls gives up (status
+// head[1] = 1, the tile's points unwritten): every workgroup reaches the exit.
+struct ReadyArgs {
+    int32_t* head;
+    const int32_t* q;
+    int32_t* hz_flag;
+    int32_t n_items;
+    int32_t tiles;
+    int32_t tile_u;
+    int32_t spin_limit;
 };
 
 struct EqArgs {
@@ -164,6 +184,12 @@ hipError_t launch_learn_logistic(const double* beta, const double* eta, const do
                                  const LearnBufs& L, hipStream_t s);
 hipError_t launch_equilibrium(const LearnBufs& L, const double* eta, const double* t_end, const double* u,
                               const EqArgs& a, const ResultSoA& out, int n_beta, hipStream_t s);
+// the equilibrium side of a readiness sweep: one workgroup per item (hazard + equilibria
+// of each column as soon as the learning kernel publishes it); the learning side is
+// launch_learn_logistic with la.ready_q set and la.fuse_hazard = 0, without its hazard launch
+hipError_t launch_eq_ready(const LearnBufs& L, const double* beta, const double* eta, const double* t_end,
+                           const double* u, const LearnArgs& la, const EqArgs& a, const ReadyArgs& ra,
+                           const ResultSoA& out, int n_blocks, hipStream_t s);
 // solve_equilibrium_interest per (β, u) on the same learning buffers
 hipError_t launch_interest(const LearnBufs& L, const double* eta, const double* t_end, const double* u,
                            const EqArgs& a, const InterestArgs& ia, const ResultSoA& out, int n_beta, hipStream_t s);

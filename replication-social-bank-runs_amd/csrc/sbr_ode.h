@@ -21,6 +21,9 @@
 // on the same PIControl / AutoSwitch / Rosenbrock23 pieces.
 #pragma once
 
+#include <type_traits>
+#include <utility>
+
 #include "sbr_device.h"
 
 namespace sbr {
@@ -101,6 +104,19 @@ struct OdeOut {
     int32_t nswitch = 0;
     uint32_t status = 0;
 };
+
+// Optional Sink::finish(const OdeOut&): called by the lane at the moment its solve ends (inside
+// the step loop, with o final), so that a lane can publish its results while the other lanes
+// of its wave are still integrating (the learning kernel's per-column readiness).
+template <class S, class = void>
+struct has_finish : std::false_type {};
+template <class S>
+struct has_finish<S, decltype(std::declval<S&>().finish(std::declval<const OdeOut&>()), void())> : std::true_type {};
+template <class S>
+__device__ __forceinline__ void sink_finish(S& s, const OdeOut& o)
+{
+    if constexpr (has_finish<S>::value) s.finish(o);
+}
 
 // dx/dt = βx(1 − x) (learning.jl:45-48) with ForwardDiff's ∂f/∂x through (β·x)·(1 − x):
 // β·(1 − x) + (−1)·(β·x); autonomous, ∂f/∂t = 0
@@ -260,9 +276,9 @@ __device__ __forceinline__ void ode_scalar(Sys& f, Sink& sink, double T1, double
     PIControl pc;
     AutoSwitch as;
     const Tsit5Tab<Sys::kPinTableau> cf;
-    if (!sink.start(t, x)) return;
-    if (!(t < T1)) return;
-    if (maxiters < 1) { o.status |= SBR_ODE_MAXITERS; return; }
+    if (!sink.start(t, x)) { sink_finish(sink, o); return; }
+    if (!(t < T1)) { sink_finish(sink, o); return; }
+    if (maxiters < 1) { o.status |= SBR_ODE_MAXITERS; sink_finish(sink, o); return; }
     // One loop exit, tested at the bottom: the reference's early exits (DtLessThanMin before
     // the step, a NaN trial state after it) compute the step and discard it (ok = false: no
     // knot, no controller / state update, not counted), and the maxiters test of the next
@@ -352,7 +368,15 @@ __device__ __forceinline__ void ode_scalar(Sys& f, Sink& sink, double T1, double
         const bool maxit = ok & go & !badt & more & (iter >= maxiters);
         const bool fail = (!ok) | badt;
         why = (fail ? SBR_ODE_FAILED : 0u) | (maxit ? SBR_ODE_MAXITERS : 0u);
-        if (fail | (!go) | (!more) | maxit) break;
+        if (fail | (!go) | (!more) | maxit) {
+            if constexpr (has_finish<Sink>::value) {
+                o.status |= why;
+                o.nswitch = as.nswitch;
+                if (as.nswitch > 0) o.status |= SBR_STIFF_SWITCH;
+                sink.finish(o);
+            }
+            break;
+        }
     }
     o.status |= why;
     o.nswitch = as.nswitch;

@@ -116,7 +116,8 @@ class Engine:
 
     # ------------------------------------------------------------------ sweeps
     def sweep_baseline(self, grid: BaselineGrid, early_exit: int = 0, max_iters: int = 100,
-                       knot_capacity: int = 65536, with_iters: bool = True, exhaustive: bool = False) -> dict:
+                       knot_capacity: int = 65536, with_iters: bool = True, exhaustive: bool = False,
+                       flags: int = 0) -> dict:
         """Every (β, u) of ``grid`` through learning → HR → buffers → bisection
         → AW_max.  Returns [n_beta, n_u] arrays (row i = β_i).  ``early_exit=5``
         applies the reference's 5-consecutive-no-run rule as a post-pass."""
@@ -126,7 +127,8 @@ class Engine:
         out["iters"] = np.empty(nb * nu, np.int32) if with_iters else None
         soa = _lib.ResultSoA(*[_ptr(out[k]) for k in (*RESULT_FIELDS, "status", "iters")])
         opts = _lib.default_opts(early_exit_nan_run=early_exit, bisect_max_iters=max_iters,
-                                 knot_capacity=knot_capacity, flags=_lib.SBR_FLAG_EXHAUSTIVE if exhaustive else 0)
+                                 knot_capacity=knot_capacity,
+                                 flags=flags | (_lib.SBR_FLAG_EXHAUSTIVE if exhaustive else 0))
         rc = self._L.sbr_sweep_baseline(self._ctx, _ptr(grid.beta), _ptr(grid.eta), _ptr(grid.t_end), grid.x0,
                                         _ptr(grid.u), nb, nu, grid.p, grid.kappa, grid.lam, ctypes.byref(opts),
                                         ctypes.byref(soa))

@@ -246,3 +246,29 @@ def test_pipelined_batches_equal_single_sweeps(engine):
         st = out["status"][k].cpu().numpy().view(np.uint32).reshape(nb, nu)
         assert np.array_equal(st, ref["status"])
         assert np.array_equal(out["iters"][k].cpu().numpy().reshape(nb, nu), ref["iters"])
+
+
+@pytest.mark.parametrize("n_u", [50, 2000])
+def test_readiness_schedule_equals_chunked(engine, n_u):
+    """The per-column readiness schedule (SBR_FLAG_READY_SWEEP: the learning kernel publishes
+    each column the moment its lane solves it; equilibrium workgroups on other CUs take
+    (column, u-tile) items in publication order, tile 0 running the column's hazard) gives
+    exactly the default three-chunk schedule's results — incl. BoundsError columns (η past
+    tspan), η == t_end, and one or several u-tiles per column."""
+    base = sbr.fig5_grid(384, n_u=n_u)
+    eta = np.full(384, 15.0)
+    tend = np.full(384, 30.0)
+    eta[:5] = 40.0   # η past tspan: the hazard's BoundsError
+    eta[100:103] = 30.0  # η == t_end: η is the last knot
+    tend[200:210] = 20.0
+    g = sbr.BaselineGrid(base.beta, base.u, eta, tend)
+    a = engine.sweep_baseline(g, flags=sbr._lib.SBR_FLAG_READY_SWEEP)
+    b = engine.sweep_baseline(g)
+    for f in FIELDS:
+        assert_bitwise(a[f], b[f], f)
+    assert np.array_equal(a["status"], b["status"])
+    assert np.array_equal(a["iters"], b["iters"])
+    assert (a["status"][:5] & sbr.STATUS["SBR_OOB"]).all()
+    # and repeatedly (the publication queue is reset per call)
+    c = engine.sweep_baseline(g, flags=sbr._lib.SBR_FLAG_READY_SWEEP)
+    assert np.array_equal(c["status"], a["status"]) and np.array_equal(c["aw_max"], a["aw_max"], equal_nan=True)

@@ -1,0 +1,33 @@
+#!/usr/bin/env bash
+# Round-3 GPU steps: STEPS selects a subset (in order); each GPU step has its own time limit
+# and the first failure ends the script.  TESTK narrows the pytest step (-k expression).
+set -u
+cd "${GRAFT_REPO_ROOT:-.}"
+OUT=gpurun_out/${TAG:-r03}
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+( while true; do date +%T >> "$OUT/heartbeat.log"; sleep 30; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
+run() { # name timeout cmd...
+  local name=$1 to=$2; shift 2
+  timeout -k 10 "$to" "$@" > "$OUT/$name.out" 2> "$OUT/$name.err"
+  local rc=$?
+  echo "$name rc=$rc" | tee -a "$OUT/steps.log"
+  tail -c 1500 "$OUT/$name.out"; echo
+  if [ $rc -ne 0 ]; then tail -20 "$OUT/$name.err"; exit $rc; fi
+}
+for s in ${STEPS:-tests smoke bench single}; do
+  case $s in
+    tests) run tests 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${TESTK:+-k "$TESTK"} ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 300 python -u bench.py ;;
+    single) run single 300 python -u bench.py --no-pipeline --steps 20 --warmup 2 --no-cpu-baseline ;;
+    ready) run ready 300 python -u bench.py --no-pipeline --ready --steps 20 --warmup 2 --no-cpu-baseline ;;
+    prof) run prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
+    profsingle) run profsingle 300 rocprofv3 --kernel-trace --stats -d "$OUT/profsingle" -o run --output-format csv -- python3 bench.py --no-pipeline --steps 20 --warmup 2 --no-cpu-baseline ;;
+    hetero) run hetero 600 python -u bench.py --workload hetero --steps 10 --warmup 2 --phases ;;
+    interest) run interest 600 python -u bench.py --workload interest --steps 3 --warmup 1 ;;
+    social) run social 600 python -u bench.py --workload social --steps 1 --warmup 0 ;;
+  esac
+done
