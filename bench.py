@@ -146,10 +146,13 @@ def parse():
     ap.add_argument("--cpu-stride", type=int, default=2, help="cpu_baseline samples every k-th β column")
     ap.add_argument("--phases", action="store_true",
                     help="also time the equilibrium kernel stopped after each stage (diagnostic flags)")
-    ap.add_argument("--workload", choices=("baseline", "social", "hetero", "interest"), default="baseline",
+    ap.add_argument("--workload", choices=("baseline", "social", "hetero", "interest", "config1", "config2"),
+                    default="baseline",
                     help="baseline: BASELINE config 3 (the metric); social: config 5 per-GPU share; "
                          "hetero: config 4 (K = 8, 1024x1024 per GPU); interest: the interest-rate "
-                         "extension on the Fig 5 grid (500x500 per GPU, r = 0.06, delta = 0.1)")
+                         "extension on the Fig 5 grid (500x500 per GPU, r = 0.06, delta = 0.1); config1: "
+                         "one Fig 3 equilibrium per call (latency); config2: one 500x500 Fig 5 sweep per "
+                         "call with the 5-NaN early exit, host arrays in and out")
     ap.add_argument("--interest-n", type=int, default=500, help="interest: β columns per GPU and u rows")
     ap.add_argument("--hetero-n", type=int, default=1024, help="hetero: columns per GPU and u rows")
     ap.add_argument("--social-cols", type=int, default=64, help="social: β columns per GPU (config 5: 512/8)")
@@ -159,8 +162,80 @@ def parse():
     return ap.parse_args()
 
 
+def main_small(a):
+    """BASELINE configs 1 and 2, timed the way a drop-in caller pays them (host arrays in and
+    out, one synchronous C-ABI call each; N = 1 only).
+    config1: the Fig 3 main equilibrium (scripts/1_baseline.jl:82-86) — solve_learning +
+    solve_equilibrium_baseline + get_AW as sbr_solve_point_paths (learning, hazard, buffers,
+    ξ, the AW_cum path) — latency per call.
+    config2: the Fig 5 500×500 grid (scripts/1_baseline.jl:210-267) — one sbr_sweep_baseline
+    call with early_exit_nan_run = 5 — equilibria per second over the whole grid."""
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    torch.cuda.init()
+    eng = sbr.Engine(0)
+    sys.path.insert(0, str(REPO / "oracle"))
+    import oracle as O  # noqa: E402  (test infrastructure: cpu_baseline leg only)
+    if a.workload == "config1":
+        args = dict(beta=1.0, eta=15.0, t_end=30.0, u=0.1, p=0.5, kappa=0.6, lam=0.01)
+        for _ in range(max(a.warmup, 1)):
+            r = eng.solve_point_paths(**args)
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            r = eng.solve_point_paths(**args)
+        dt = (time.perf_counter() - t0) / a.steps
+        res = {"metric": "single baseline equilibrium latency (Fig 3 main, host API)", "value": dt * 1e3,
+               "unit": "ms per equilibrium", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
+               "ms_per_step": dt * 1e3, "higher_is_better": False, "scaling": None, "vs_baseline": None,
+               "dtype": "f64", "data": "the reference's Fig 3 parameters",
+               "config": {"workload": "config1: sbr_solve_point_paths(beta=1, eta=15, tspan=(0,30), u=0.1, "
+                                      "p=0.5, kappa=0.6, lambda=0.01) (BASELINE config 1)"},
+               "xi": r["xi"], "paper_cpu_seconds": 0.5, "libsbr_sha16": lib_sha()}
+        if not a.no_cpu_baseline:
+            O.build()
+            n = 20
+            t1 = time.perf_counter()
+            for _ in range(n):
+                t, G, _ = O.learn_logistic(1.0, 30.0)
+                o = O.equilibrium(t, G, 1.0, 15.0, 30.0, 0.1, 0.5, 0.6, 0.01, paths=True)
+            c = (time.perf_counter() - t1) / n
+            res["cpu_baseline"] = {"value": c * 1e3, "unit": "ms per equilibrium", "cores": 1, "kind": "port",
+                                   "host": host_info(), "sample": f"{n} single-point solves (learning + "
+                                   "equilibrium + AW path) on one core"}
+    else:
+        g = sbr.fig5_grid(500)
+        npts = g.n_points
+        for _ in range(max(a.warmup, 1)):
+            r = eng.sweep_baseline(g, early_exit=5)
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            r = eng.sweep_baseline(g, early_exit=5)
+        dt = (time.perf_counter() - t0) / a.steps
+        run = int(((r["status"] & sbr.STATUS["SBR_RUN"]) > 0).sum())
+        res = {"metric": "equilibria solved/sec on β×u grid (FP64), Fig 5 500x500, one host-API call per grid",
+               "value": npts / dt, "unit": "equilibria/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
+               "ms_per_step": dt * 1e3, "higher_is_better": True, "scaling": None, "vs_baseline": None,
+               "dtype": "f64", "data": "the reference's Fig 5 grid (deterministic)",
+               "config": {"workload": "config2: sbr_sweep_baseline on fig5 500x500, early_exit_nan_run=5, host "
+                                      "arrays (PCIe included) (BASELINE config 2)", "run_cells": run},
+               "libsbr_sha16": lib_sha()}
+        if not a.no_cpu_baseline:
+            O.build()
+            cores = usable_cores()
+            t1 = time.perf_counter()
+            o = O.sweep_baseline(g.beta, g.eta, g.t_end, g.u, g.p, g.kappa, g.lam, g.x0, nthreads=cores)
+            O.apply_early_exit(o, 5)
+            c = time.perf_counter() - t1
+            res["cpu_baseline"] = {"value": npts / c, "unit": "equilibria/s", "cores": cores, "kind": "port",
+                                   "host": host_info(), "sample": f"the whole 500x500 grid ({npts} points, every "
+                                   f"point solved, 5-NaN rule as a post-pass like the GPU) in {c:.2f} s"}
+    print(json.dumps(res), flush=True)
+
+
 def main():
     a = parse()
+    if a.workload in ("config1", "config2"):
+        return main_small(a)
     if a.workload == "social":
         return main_social(a)
     if a.workload == "hetero":

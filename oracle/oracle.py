@@ -322,3 +322,29 @@ def hetero_point_paths(betas, dist, eta, t_end, u, p, kappa, lam, x0=1e-4, cap=1
         raise RuntimeError("oracle hetero point failed")
     return dict(xi=res[0], aw_max=res[1], tol=res[2], status=int(st[0]), tau_in_unc=tin, tau_out_unc=tout,
                 t=t[:n].copy(), G=G[:n * K].reshape(n, K).copy(), aw_total=aw[:n].copy())
+
+
+def set_initdt_den(d: int = 6) -> None:
+    """ode_determine_initdt's exponent 1/d (6: Tsit5's order + 1, the restatement's choice);
+    other values only for tools/initdt_evidence.py."""
+    L = lib()
+    L.sbro_set_initdt_den.restype = None
+    L.sbro_set_initdt_den.argtypes = [_I32]
+    L.sbro_set_initdt_den(int(d))
+
+
+def set_initdt(form: int = 0, den: int = 6) -> None:
+    """form 0: (0.01/max(d₁,d₂))^(1/den); form 1: 10^(-(2 + log10(max(d₁,d₂)))/den), the
+    published initdt.jl expression (tools/initdt_evidence.py)."""
+    L = lib()
+    L.sbro_set_initdt.restype = None
+    L.sbro_set_initdt.argtypes = [_I32, _I32]
+    L.sbro_set_initdt(int(form), int(den))
+
+
+def set_initdt_ulps(k: int = 0) -> None:
+    """Sensitivity probe: move the initial dt₁ by k ulps (tools/initdt_evidence.py)."""
+    L = lib()
+    L.sbro_set_initdt_ulps.restype = None
+    L.sbro_set_initdt_ulps.argtypes = [_I32]
+    L.sbro_set_initdt_ulps(int(k))

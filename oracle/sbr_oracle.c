@@ -50,6 +50,16 @@
  * @muladd would put a muladd; exp/log/pow come from include/sbr_detmath.h.
  */
 #include <math.h>
+
+/* ode_determine_initdt's exponent 1/(order + 1): 6 (Tsit5's order 5, the restatement's
+ * choice) unless a test sets another denominator to measure the choice (DESIGN.md §2,
+ * tools/initdt_evidence.py) */
+static double g_initdt_den = 6.0;
+static int g_initdt_form = 0; /* 0: (0.01/md)^(1/den); 1: 10^(-(2 + log10(md))/den), initdt.jl's form */
+void sbro_set_initdt_den(int d) { g_initdt_den = d > 0 ? (double)d : 6.0; }
+static int g_initdt_ulps = 0; /* sensitivity probe: dt₁ moved by this many ulps */
+void sbro_set_initdt(int form, int d) { g_initdt_form = form; g_initdt_den = d > 0 ? (double)d : 6.0; }
+void sbro_set_initdt_ulps(int k) { g_initdt_ulps = k; }
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -437,11 +447,17 @@ static int ode_solve_cb(const ode_sys_t* S, int m, double t0, double t1, const d
             for (int i = 0; i < m; i++) buf[i] = (f1[i] - fsal[i]) / sk[i];
             double d2 = rms_norm(buf, m) / dt0;
             double md = dmax(d1, d2);
-            /* 10^(-(2 + log10(md)) / get_current_alg_order) with Tsit5's order 5 */
-            /* dt₁ = (0.01/max(d₁, d₂))^(1/(p+1)) with p = 5 (Tsit5): the exponent 1/6
-             * is pinned by the committed Fig 5 heatmap — with 1/5 the 500² run mask
-             * gains cell (β₂₈₄, u₉₅), where the figure has no run */
-            double dt1 = (md <= 1e-15) ? dmax(1e-6, dt0 * 1e-3) : sbr_pow_pos(0.01 / md, 1.0 / 6.0);
+            /* dt₁ = (0.01/max(d₁, d₂))^(1/6).  initdt.jl's own expression is recalled as
+             * 10^(-(2 + log10(md)) / get_current_alg_order) with Tsit5's order 5, i.e. 1/5;
+             * the figures cannot separate the two except at one knife-edge cell, (β₂₈₄,
+             * u₉₅) of the 500² mask (no run in the figure): 1/6 gives no run for every
+             * first step within ±4 ulps, 1/5 for 4-5 of 9 (tools/initdt_evidence.py →
+             * profiles/r03_initdt_exponent.json).  Kept: 1/6. */
+            double dt1 = (md <= 1e-15) ? dmax(1e-6, dt0 * 1e-3)
+                         : (g_initdt_form ? sbr_exp10(-(2.0 + sbr_log10(md)) / g_initdt_den)
+                                          : sbr_pow_pos(0.01 / md, 1.0 / g_initdt_den));
+            for (int k = 0; k < g_initdt_ulps; k++) dt1 = nextafter(dt1, INFINITY);
+            for (int k = 0; k > g_initdt_ulps; k--) dt1 = nextafter(dt1, -INFINITY);
             dt = dmax(dtmin, dmin(dmin(100.0 * dt0, dt1), dtmax));
         }
     }

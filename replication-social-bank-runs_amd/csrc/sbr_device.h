@@ -15,6 +15,12 @@
 #include "../../include/sbr_detmath.h"
 #include "../../include/sbr_status.h"
 
+// ode_determine_initdt's exponent 1/(order + 1) with Tsit5's order 5; -DSBR_INITDT_DEN=5 builds
+// the alternative the restatement rejected (tools/initdt_evidence.py)
+#ifndef SBR_INITDT_DEN
+#define SBR_INITDT_DEN 6.0
+#endif
+
 namespace sbr {
 
 // ---- Tsit5 (Tsitouras 2011) as in OrdinaryDiffEqTsit5 --------------------

@@ -204,7 +204,7 @@ __global__ __launch_bounds__(64) void learn_hetero_kernel(const double* __restri
             for (int k = 0; k < K; k++) buf[k] = (k7[k] - k1[k]) / sk[k];
             const double d2 = rms<K>(buf) / dt0;
             const double md = dmax(d1, d2);
-            const double dt1 = (md <= 1e-15) ? dmax(1e-6, dt0 * 1e-3) : sbr_pow_pos(0.01 / md, 1.0 / 6.0);
+            const double dt1 = (md <= 1e-15) ? dmax(1e-6, dt0 * 1e-3) : sbr_pow_pos(0.01 / md, 1.0 / SBR_INITDT_DEN);
             dt = dmax(dtmin, dmin(dmin(100.0 * dt0, dt1), dtmax));
         }
     }
@@ -618,7 +618,7 @@ __global__ __launch_bounds__(64) void learn_hetero_wave_kernel(const double* __r
         } else {
             const double d2 = R.rms((k7 - k1) / sk) / dt0;
             const double md = dmax(d1, d2);
-            const double dt1 = (md <= 1e-15) ? dmax(1e-6, dt0 * 1e-3) : sbr_pow_pos(0.01 / md, 1.0 / 6.0);
+            const double dt1 = (md <= 1e-15) ? dmax(1e-6, dt0 * 1e-3) : sbr_pow_pos(0.01 / md, 1.0 / SBR_INITDT_DEN);
             dt = dmax(dtmin, dmin(dmin(100.0 * dt0, dt1), dtmax));
         }
     }

@@ -163,7 +163,7 @@ __device__ __forceinline__ double initdt_scalar(Sys& f, double T0, double T1, do
         } else {
             const double d2 = fabs((f1 - k1) / sk) / dt0;
             const double md = dmax(d1, d2);
-            const double dt1 = (md <= 1e-15) ? dmax(1e-6, dt0 * 1e-3) : sbr_pow_pos(0.01 / md, 1.0 / 6.0);
+            const double dt1 = (md <= 1e-15) ? dmax(1e-6, dt0 * 1e-3) : sbr_pow_pos(0.01 / md, 1.0 / SBR_INITDT_DEN);
             dt = dmax(dtmin, dmin(dmin(100.0 * dt0, dt1), dtmax));
         }
     }

@@ -29,5 +29,7 @@ for s in ${STEPS:-tests smoke bench single}; do
     hetero) run hetero 600 python -u bench.py --workload hetero --steps 10 --warmup 2 --phases ;;
     interest) run interest 600 python -u bench.py --workload interest --steps 3 --warmup 1 ;;
     social) run social 600 python -u bench.py --workload social --steps 1 --warmup 0 ;;
+    config1) run config1 300 python -u bench.py --workload config1 --steps 50 --warmup 3 ;;
+    config2) run config2 300 python -u bench.py --workload config2 --steps 20 --warmup 2 ;;
   esac
 done
