@@ -775,7 +775,7 @@ def main_social(a):
 
 def phase_breakdown(eng, beta, eta, t_end, u, p, kappa, lam, x0, out, stream, dev, reps=3):
     """Equilibrium-kernel time when every point stops after the crossing scan,
-    after the bisection, and in full; plus AW blocks evaluated per run point.  Runs
+    after the bisection, and in full; plus AW knots evaluated exactly per run point.  Runs
     through the batch entry point with one grid: its timing events bracket the
     equilibrium launch itself (a single sweep is chunked, see kernel_ms_per_step)."""
     from sbr import _lib
@@ -807,7 +807,7 @@ def phase_breakdown(eng, beta, eta, t_end, u, p, kappa, lam, x0, out, stream, de
     torch.cuda.synchronize(dev)
     st = out["status"].cpu().numpy().view(np.uint32)
     nb = out["iters"].cpu().numpy()[(st & sbr.STATUS["SBR_RUN"]) > 0]
-    res["aw_blocks_per_run_point"] = float(nb.mean()) if nb.size else 0.0
+    res["aw_knots_evaluated_per_run_point"] = float(nb.mean()) if nb.size else 0.0
     res["run_points"] = int(nb.size)
     return res
 

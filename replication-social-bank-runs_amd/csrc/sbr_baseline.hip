@@ -231,13 +231,16 @@ constexpr int EQ_TILE = SBR_EQ_TILE;  // u values per equilibrium block (one blo
 #ifndef SBR_EQ_PRIO
 #define SBR_EQ_PRIO 0
 #endif
-#ifndef SBR_AW_SLOPE
-#define SBR_AW_SLOPE 0 // A/B: slope bounds (one exact knot + slope tables) before evaluating an 8-block (bit-exact, slower: r02_slope)
-#endif
 #ifndef SBR_AW_WIN
-#define SBR_AW_WIN (SBR_AW_SLOPE ? 1 : 6)
+#define SBR_AW_WIN 6
+#endif
+#ifndef SBR_AW_SCAN
+#define SBR_AW_SCAN 1 // AW_max by the outward scan from the predicted peak (aw_scan) where its bounds hold
 #endif
 constexpr int kAwWin = SBR_AW_WIN; // 8-blocks each side of the predicted AW peak evaluated first
+#ifndef SBR_BISECT_FAST
+#define SBR_BISECT_FAST 1 // single-interval bisection steps decided by the line's estimate (solve_from_buffers)
+#endif
 
 // I_k = I_{k-1} + term_k over s_I[0, cn) in place, left to right (the reference's rounding
 // order), by the 64 lanes of one wave: lane l holds terms [16l, 16l + 16) in registers and
@@ -524,10 +527,9 @@ struct Summ {
     const double* smc;
     bool mono; // G nondecreasing over the knots (no NaN): prefix max / suffix min are knot values
     double t_half; // time where G crosses 1/2 (lerp inverse), NaN if it does not: AW peak predictor
-    // mono only (they reuse pmc/smc): per 8-interval block, the largest / smallest knot-interval
-    // slope (G[k+1] − G[k]) / (t[k+1] − t[k]), widened by 1e-12 relative
-    const double* smax;
-    const double* smin;
+    // aw_scan's preconditions: mono, 0 <= G[0], G[n−1] <= 2 (the 1e-14 rounding margin) and
+    // t[k+2] − t[k] > 1e-15·t[n−1] (a shifted τ̄ argument stays below the knot after next)
+    bool scan;
 };
 
 template <class P>
@@ -536,6 +538,142 @@ __device__ __forceinline__ void solve_from_buffers(P T, P G, P H, const Summ& S,
                                                    const double u, const double kappa, const int max_iters,
                                                    const uint32_t lbits, PointResult& r, double* __restrict__ aw_path,
                                                    const int diag, const double tin, const double tout);
+
+// smallest k in [0, hi] with key(k) >= x, for a nondecreasing key with key(hi) >= x: gallop
+// down from hi, then bisect
+template <class F>
+__device__ __forceinline__ int first_ge_down(F key, int hi, double x)
+{
+    int top = hi, lo = hi - 1, step = 1; // key(top) >= x; answer in (lo, top]
+    while (lo >= 0 && key(lo) >= x) {
+        top = lo;
+        step <<= 1;
+        lo = top - step;
+    }
+    if (lo < -1) lo = -1;
+    while (top - lo > 1) {
+        const int mid = (lo + top) >> 1;
+        if (key(mid) >= x) top = mid;
+        else lo = mid;
+    }
+    return top;
+}
+
+// AW_max (solver.jl:553-576) over τ̄ knots [0, ntau) by an outward scan from the predicted
+// peak knot c, for a nondecreasing G with Summ::scan's preconditions.  AW_cum(τ̄_i) =
+// AW_OUT(b_i) − AW_IN(a_i) + G(0) with a_i = (τ̄_i − ξ) + icc ≤ b_i = (τ̄_i − ξ) + occ ≤ τ̄_i + ulp,
+// both nondecreasing in i, so
+//   right of the last evaluated knot i:  AW_OUT(b_j) ≤ G[j + 2] and AW_IN(a_j) ≥ AW_IN(a_i);
+//   left of it:                         AW_OUT(b_j) ≤ AW_OUT(b_i) and AW_IN(a_j) ≥ G[bracket(a_j)].
+// A knot is evaluated exactly (the same operations as eval_range) only where these bounds
+// (+ the 1e-14 rounding margin) do not already put it at or below the running maximum; runs
+// of knots the bounds dismiss are skipped with one search in G (right) or in G and τ̄ (left).
+// The maximum equals the exhaustive one bit for bit (G has no NaN here).
+template <class P>
+__device__ __forceinline__ void aw_scan(P T, P G, const int n, const int ntau, const int nle, const double ETA,
+                                        const double xi, const double icc, const double occ, const double G0,
+                                        const int c, double& mx, int& nev)
+{
+    auto tau = [&](int i) -> double { return i < nle ? T[i] : ETA; };
+    auto av_of = [&](int i) -> double { return (tau(i) - xi) + icc; };
+    // a(τ̄_i)'s bracket window: k = min(searchsortedlast(t, x), n − 2), its two knots (t, G)
+    int ka;
+    double ta0, ta1, ga0, ga1;
+    auto seek = [&](int hint, double x) {
+        ka = ssl_near(T, n, hint, x);
+        ka = ka < n - 2 ? ka : n - 2;
+        ta0 = T[ka]; ta1 = T[ka + 1]; ga0 = G[ka]; ga1 = G[ka + 1];
+    };
+    auto fwd = [&](double x) {
+        while (ka < n - 2 && ta1 <= x) { ka++; ta0 = ta1; ga0 = ga1; ta1 = T[ka + 1]; ga1 = G[ka + 1]; }
+    };
+    auto bwd = [&](double x) {
+        while (ka > 0 && ta0 > x) { ka--; ta1 = ta0; ga1 = ga0; ta0 = T[ka]; ga0 = G[ka]; }
+    };
+    // exact AW_cum(τ̄_i) with the a window at a_i's bracket; b's bracket is searched from i
+    double awin = 0.0, awout = 0.0;
+    auto exact = [&](int i, double av, double xa) -> double {
+        const double bv = (tau(i) - xi) + occ;
+        const double xb = bv > 0 ? bv : 0.0;
+        int kb = ssl_near(T, n, i, xb);
+        kb = kb < n - 2 ? kb : n - 2;
+        const double tb0 = T[kb], tb1 = T[kb + 1], gb0 = G[kb], gb1 = G[kb + 1];
+        const double da = (xa - ta0) / (ta1 - ta0);
+        const double gi = ga0 * (1.0 - da) + ga1 * da;
+        double go;
+        if (xb == tb0) go = gb0 * 1.0 + gb1 * 0.0;
+        else { const double db = (xb - tb0) / (tb1 - tb0); go = gb0 * (1.0 - db) + gb1 * db; }
+        awin = av >= 0 ? gi : 0.0;
+        awout = bv >= 0 ? go : 0.0;
+        nev++;
+        return (awout - awin) + G0;
+    };
+    // knot c
+    {
+        const double av = av_of(c), xa = av > 0 ? av : 0.0;
+        seek(c, xa);
+        const double v = exact(c, av, xa);
+        if (v > mx) mx = v;
+    }
+    const int kc = ka;
+    const double ub_left = awout;
+    // right of c
+    double LA = awin; // lower bound of AW_IN(a_j) for every j >= i
+    for (int i = c + 1; i < ntau;) {
+        const double av = av_of(i), xa = av > 0 ? av : 0.0;
+        fwd(xa);
+        const double lb = av >= 0 ? ga0 : 0.0;
+        LA = LA > lb ? LA : lb;
+        const double V = ((mx - G0) + LA) - 1e-14;
+        const int k2 = i + 2 < n - 1 ? i + 2 : n - 1;
+        if (G[k2] > V) {
+            const double v = exact(i, av, xa);
+            if (v > mx) mx = v;
+            LA = awin;
+            i++;
+            continue;
+        }
+        // every knot j with G[min(j + 2, n − 1)] <= V is at or below mx: skip to the first other
+        const int kl = ssl_gallop(G, n, k2, V);
+        if (kl >= n - 1) break;
+        const int inext = kl - 1; // G[kl + 1] > V
+        const double an = av_of(inext);
+        seek(ka + (inext - i), an > 0 ? an : 0.0);
+        i = inext;
+    }
+    // left of c
+    double UB = ub_left; // upper bound of AW_OUT(b_j) for every j <= i
+    {
+        const double av = av_of(c);
+        seek(kc, av > 0 ? av : 0.0);
+    }
+    for (int i = c - 1; i >= 0;) {
+        const int k2 = i + 2 < n - 1 ? i + 2 : n - 1;
+        const double g2 = G[k2] > 0.0 ? G[k2] : 0.0;
+        UB = UB < g2 ? UB : g2;
+        const double Vp = ((UB + G0) + 1e-14) - mx;
+        if (!(Vp > 0.0)) break; // AW_IN(a_j) >= 0 for every j: all pruned
+        const double av = av_of(i), xa = av > 0 ? av : 0.0;
+        bwd(xa);
+        const double lb = av >= 0 ? ga0 : 0.0;
+        if (!(lb >= Vp)) {
+            const double v = exact(i, av, xa);
+            if (v > mx) mx = v;
+            UB = UB < awout ? UB : awout;
+            i--;
+            continue;
+        }
+        // knots j <= i with a_j >= t[k*] (k* = first knot with G >= Vp) are pruned
+        const int ks = first_ge_down([&](int k) { return G[k]; }, ka, Vp);
+        const double tk = T[ks];
+        const int j = first_ge_down(av_of, i, tk);
+        if (j == 0) break;
+        const int inext = j - 1;
+        const double an = av_of(inext);
+        seek(ks, an > 0 ? an : 0.0);
+        i = inext;
+    }
+}
 
 template <class P>
 __device__ __forceinline__ void solve_point(P T, P G, P H, const Summ& S, const int n, const int ntau,
@@ -627,12 +765,35 @@ __device__ __forceinline__ void solve_from_buffers(P T, P G, P H, const Summ& S,
     double c_ic_x = NAN, c_ic_v = 0.0;
     uint32_t s = SBR_NO_RUN_MAXITER;
     double xi = NAN, tolr = INFINITY;
+#if SBR_BISECT_FAST
+    // Single-interval bisection.  Once the bracket is one knot interval [t0, t1) (jlo == jhi),
+    // G(ξ) there is the line g0·(1 − δ) + g1·δ, and the error AW − κ of a midpoint is
+    // e0 + s·(x − t0) up to a few ulps of the operands.  Every midpoint whose estimate is
+    // farther than `lim` from zero has the sign of its estimate and is no terminal iterate
+    // (|AW − κ| > tol): it moves xmin or xmax without the search, the lerp and its division.
+    // Only the last few midpoints (|err| ≲ 1e-13) run the exact iteration below.  The
+    // exact iteration's other effects are constant over the interval (ic = tin, oc = ξ,
+    // ε = t1 − t0, the BoundsError tests of ξ + ε and tin + ε pass), checked on entry.
+    // ea = s·x + c (c = e0 − s·t0, |s·t0| ≤ 16: the rounding of c and of the fma stays ≈1e-14, far
+    // inside lim); f_s = NaN until the interval is reached: every comparison fails and the exact
+    // iteration runs.  Lanes of a wave move through the same trips, the decided ones skipping
+    // the exact body.
+    double f_s = NAN, f_c = 0.0;
+    const double f_lim = tolerance + 1e-13;
+#endif
     for (int iter = 1; iter <= max_iters; iter++) {
         r.iters = iter;
         const double dd = xmin - xmax;
         if (collapsed(dd)) { s = SBR_NO_RUN_COLLAPSE; break; }
         if (iter == max_iters - 1) { s = SBR_NO_RUN_MAXITER; break; }
         const double xo = xnew;
+#if SBR_BISECT_FAST
+        {
+            const double ea = fma(f_s, xo, f_c);
+            if (ea < -f_lim) { xmin = xo; xnew = 0.5 * (xo + xmax); continue; }
+            if (ea > f_lim) { xmax = xo; xnew = 0.5 * (xo + xmin); continue; }
+        }
+#endif
         const double ic = dmin(tin, xo), oc = dmin(tout, xo);
         const int j = ssl_range(T, jlo, jhi, xo); // t[jlo] <= ξmin <= xo <= ξmax < t[jhi+1]
         // G(oc)
@@ -671,6 +832,20 @@ __device__ __forceinline__ void solve_from_buffers(P T, P G, P H, const Summ& S,
         } else {
             xmin = xo; jlo = j; xnew = 0.5 * (xo + xmax);
         }
+#if SBR_BISECT_FAST
+        if (f_s != f_s && jlo == jhi && ic == tin && tin <= xmin && xmax <= tout && xmax + eps <= thi) {
+            // j + 1 < n and ξ + ε, tin + ε in range were tested by this iteration
+            const double t0 = T[j], g0 = G[j], g1 = G[j + 1];
+            const double mag = dmax(dmax(fabs(g0), fabs(g1)), dmax(fabs(Gic), fabs(kappa)));
+            if (mag <= 4.0 && eps > 0.0) { // finite, moderate operands (NaN fails): rounding ≤ 1e-14
+                const double sl = (g1 - g0) / eps, st = sl * t0;
+                if (fabs(st) <= 16.0) { // |c| ≤ 28: its rounding stays ≈1e-14
+                    f_s = sl;
+                    f_c = ((g0 - Gic) - kappa) - st;
+                }
+            }
+        }
+#endif
     }
     if (flag) { r.status = flag | lbits; return; }
     if (s != SBR_RUN) { r.status = s | lbits; return; }
@@ -691,9 +866,6 @@ __device__ __forceinline__ void solve_from_buffers(P T, P G, P H, const Summ& S,
     auto brk_a = [&](int i) { ra_j = ssl_near(T, n, ra_j + (i - ra_i), xa_of(i)); ra_i = i; return ra_j; };
     auto brk_b = [&](int i) { rb_j = ssl_near(T, n, rb_j + (i - rb_i), xb_of(i)); rb_i = i; return rb_j; };
     // exact AW_cum(τ̄_i) for i in [i0, i1), folded into the NaN-propagating max
-#if SBR_AW_SLOPE
-    double last_v = NAN;
-#endif
     auto eval_range = [&](int i0, int i1) {
         // The brackets of a(τ̄_i) and b(τ̄_i) only move forward with i: keep each bracket's
         // two knots (t, G) in registers and slide them, so a knot costs the LDS loads of
@@ -723,12 +895,9 @@ __device__ __forceinline__ void solve_from_buffers(P T, P G, P H, const Summ& S,
             const double awin = av >= 0 ? gi : 0.0;
             const double awout = bv >= 0 ? go : 0.0;
             const double v = (awout - awin) + G0;
-            if ((diag & 4) && ((i & 7) == 0 || i == i0)) nblk_eval++;
+            if (diag & 4) nblk_eval++;
             if (aw_path) aw_path[i] = v;
             if (mx == mx && (v != v || v > mx)) mx = v;
-#if SBR_AW_SLOPE
-            last_v = v;
-#endif
         }
         ra_j = ka; ra_i = i1 - 1;
         rb_j = kb; rb_i = i1 - 1;
@@ -760,40 +929,22 @@ __device__ __forceinline__ void solve_from_buffers(P T, P G, P H, const Summ& S,
                 return ((ub_out - lb_in) + G0) + 1e-14;
             };
             auto end_of = [&](int i0, int w) { return i0 + w < ntau ? i0 + w : ntau; };
-#if SBR_AW_SLOPE
-            // Slope bound of AW_cum over knots [i0, ie) once AW_cum(τ̄_i0) = v0 is known exactly:
-            // G is piecewise linear, so G(b_i) − G(b_i0) ≤ Smax_b·(b_i − b_i0) and
-            // G(a_i) − G(a_i0) ≥ Smin_a·(a_i − a_i0) with the slope extremes over the knot
-            // intervals the arguments cross; b_i − b_i0 and a_i − a_i0 are both τ̄_i − τ̄_i0 up to
-            // the rounding of the shifted arguments (ε ≤ 8 ulp of their magnitude), so
-            // AW_cum(τ̄_i) ≤ v0 + max(0, Smax_b − Smin_a)·(a_ie−1 − a_i0) + Smax_b·ε (+ a margin
-            // for the interpolation roundings).  Near the maximum the two slopes nearly cancel
-            // (the peak is where g(b) = g(a)), so this is far tighter there than the
-            // knot-value bound; requires a_i0, b_i0 ≥ 0 (no masked term) and a monotone G.
-            auto slope_ub = [&](int i0, int ie, double v0) -> double {
-                const double ta0 = tau(i0), ta1 = tau(ie - 1);
-                const double av0 = (ta0 - xi) + icc, av1 = (ta1 - xi) + icc;
-                const double bv1 = (ta1 - xi) + occ;
-                int ka0 = brk_a(i0), ka1 = brk_a(ie - 1), kb0 = brk_b(i0), kb1 = brk_b(ie - 1);
-                ka0 = ka0 < n - 2 ? ka0 : n - 2; ka1 = ka1 < n - 2 ? ka1 : n - 2;
-                kb0 = kb0 < n - 2 ? kb0 : n - 2; kb1 = kb1 < n - 2 ? kb1 : n - 2;
-                double smx = 0.0, smn = INFINITY;
-                for (int g = kb0 >> 3; g <= (kb1 >> 3); g++) smx = dmax(smx, S.smax[g]);
-                for (int g = ka0 >> 3; g <= (ka1 >> 3); g++) smn = dmin(smn, S.smin[g]);
-                const double mag = fabs(ta1) + fabs(xi) + fabs(icc) + fabs(occ) + fabs(bv1);
-                const double eps = mag * 4e-15;
-                return ((v0 + (dmax(0.0, smx - smn) * (av1 - av0)) * (1.0 + 1e-12)) + smx * eps) + 1e-14;
-            };
-#endif
             // pass 1: a first running maximum.  For a logistic-shaped CDF the continuous
             // maximiser of G(τ − s_out) − G(τ − s_in) sits where G(τ − s_out) + G(τ − s_in) = 1,
             // i.e. at τ* = t_half + (s_in + s_out)/2: evaluate the 8-blocks around it
             // (a heuristic — exactness comes from pass 2's bounds).  Otherwise descend the
             // bound hierarchy to the most promising 8-block.
-            int b8 = -1, w0 = 0, w1 = 0;
             const double tstar = S.t_half + 0.5 * ((xi - icc) + (xi - occ));
-            if (tstar == tstar && tstar >= tau(0) && tstar <= tau(ntau - 1)) {
-                const int ic = ssl_range(T, 0, (nle > 0 ? nle : 1) - 1, tstar < T[0] ? T[0] : tstar);
+            const bool predicted = tstar == tstar && tstar >= tau(0) && tstar <= tau(ntau - 1);
+            const int ic = predicted ? ssl_range(T, 0, (nle > 0 ? nle : 1) - 1, tstar < T[0] ? T[0] : tstar) : 0;
+#if SBR_AW_SCAN
+            if (S.scan && predicted) {
+                aw_scan(T, G, n, ntau, nle, ETA, xi, icc, occ, G0, ic < ntau ? ic : ntau - 1, mx, nblk_eval);
+            } else
+#endif
+            {
+            int b8 = -1, w0 = 0, w1 = 0;
+            if (predicted) {
                 const int c8 = (ic < ntau ? ic : ntau - 1) & ~7;
                 w0 = c8 - 8 * kAwWin > 0 ? c8 - 8 * kAwWin : 0;
                 w1 = end_of(c8, 8 * (kAwWin + 1));
@@ -829,17 +980,10 @@ __device__ __forceinline__ void solve_from_buffers(P T, P G, P H, const Summ& S,
                     for (int i0 = k0; i0 < ke && !flag && mx == mx; i0 += 8) {
                         const int ie = end_of(i0, 8);
                         if (i0 == b8 || (i0 >= w0 && ie <= w1) || ub_rng(i0, ie - 1) <= mx) continue;
-#if SBR_AW_SLOPE
-                        if (S.smax && ie - i0 > 1 && ((tau(i0) - xi) + icc) >= 0.0 && ((tau(i0) - xi) + occ) >= 0.0) {
-                            eval_range(i0, i0 + 1);
-                            if (flag || mx != mx || slope_ub(i0, ie, last_v) <= mx) continue;
-                            eval_range(i0 + 1, ie);
-                            continue;
-                        }
-#endif
                         eval_range(i0, ie);
                     }
                 }
+            }
             }
         }
     }
@@ -1109,17 +1253,18 @@ __device__ __forceinline__ void eq_column(const int b, const int j0, const int j
     double* smc = pmc + nsum8;
     __shared__ int eq_next;
     __shared__ int s_nonmono;
+    __shared__ int s_noscan;
     __shared__ double s_thalf;
     // every shared flag is initialised before the first barrier: lanes >= nq set
     // s_nonmono right after it, so a later store by thread 0 could clear their flag
-    if (threadIdx.x == 0) { eq_next = 0; s_nonmono = 0; s_thalf = NAN; }
+    if (threadIdx.x == 0) { eq_next = 0; s_nonmono = 0; s_noscan = 0; s_thalf = NAN; }
     if (fits) {
         for (int i = threadIdx.x; i < n; i += BLOCK) { sT[i] = gT[i]; sG[i] = gG[i]; }
         if (INTEREST)
             for (int i = threadIdx.x; i < ntau; i += BLOCK) sH[i] = gH[i];
     }
     __syncthreads();
-    Summ S{nullptr, nullptr, nullptr, nullptr, false, (double)NAN, nullptr, nullptr};
+    Summ S{nullptr, nullptr, nullptr, nullptr, false, (double)NAN, false};
     if (fits && !a.exhaustive) {
         const int nbh = (ntau + 63) >> 6, nbg = (n + 7) >> 3;
         // HR summaries: 8 lanes per 64-entry block, 8 independent loads each (HR is read from
@@ -1163,27 +1308,16 @@ __device__ __forceinline__ void eq_column(const int b, const int j0, const int j
                     prev = v;
                 }
                 if (!mono) s_nonmono = 1;
+                // aw_scan's knot separation (Summ::scan)
+                const double sep = 1e-15 * sT[n - 1];
+                bool far = true;
+                for (int i = g << 3; i < e; i++) far &= i + 2 >= n || sT[i + 2] - sT[i] > sep;
+                if (!far) s_noscan = 1;
                 pmc[g] = mx; // block max for now
                 smc[g] = mn; // block min for now
             }
         }
         __syncthreads();
-#if SBR_AW_SLOPE
-        // monotone G: the prefix/suffix tables are unused — the same slots hold the per-block
-        // slope extremes for the AW slope bounds
-        if (!s_nonmono)
-            for (int g = threadIdx.x; g < nbg; g += BLOCK) {
-                double mx = 0.0, mn = INFINITY;
-                const int e = (g << 3) + 8 < n - 1 ? (g << 3) + 8 : n - 1;
-                for (int k = g << 3; k < e; k++) {
-                    const double sl = (sG[k + 1] - sG[k]) / (sT[k + 1] - sT[k]);
-                    mx = sl > mx ? sl : mx;
-                    mn = sl < mn ? sl : mn;
-                }
-                pmc[g] = mx * (1.0 + 1e-12);
-                smc[g] = mn * (1.0 - 1e-12);
-            }
-#endif
         // prefix max / suffix min over blocks (NaN-propagating), two waves at once
         if (threadIdx.x == 0) {
             // t_half: first knot interval with G[k] <= 1/2 < G[k+1] (heuristic only)
@@ -1209,8 +1343,8 @@ __device__ __forceinline__ void eq_column(const int b, const int j0, const int j
             }
         }
         __syncthreads();
-        S = Summ{hmax, hmin, pmc, smc, s_nonmono == 0, s_thalf, SBR_AW_SLOPE && s_nonmono == 0 ? pmc : nullptr,
-                 SBR_AW_SLOPE && s_nonmono == 0 ? smc : nullptr};
+        S = Summ{hmax, hmin, pmc, smc, s_nonmono == 0, s_thalf,
+                 s_nonmono == 0 && !s_noscan && sG[0] >= 0.0 && sG[n - 1] <= 2.0};
     }
     // Points are handed out to waves 64 at a time from an LDS counter, so a
     // wave that drew cheap no-run points goes back for more instead of idling
@@ -1261,6 +1395,14 @@ __device__ __forceinline__ void eq_column(const int b, const int j0, const int j
     }
 }
 
+#ifdef SBR_EQ_WGTIME
+// diagnostic build only (tools/wgtime.py): per-workgroup start / end (100 MHz realtime clock)
+// and hardware ids of the last equilibrium_kernel launch
+constexpr size_t kWgTimeMax = 65536;
+__device__ unsigned long long g_wgtime[2 * kWgTimeMax];
+__device__ unsigned int g_wghw[2 * kWgTimeMax];
+#endif
+
 template <int BLOCK, bool INTEREST>
 __global__ __launch_bounds__(BLOCK, INTEREST ? 1 : SBR_EQ_MINW) void equilibrium_kernel(LearnBufs L, const double* __restrict__ eta,
                                                             const double* __restrict__ t_end,
@@ -1274,7 +1416,21 @@ __global__ __launch_bounds__(BLOCK, INTEREST ? 1 : SBR_EQ_MINW) void equilibrium
     const int b = SBR_EQ_REVERSE ? (int)(gridDim.y - 1 - blockIdx.y) : (int)blockIdx.y;
     const int j0 = blockIdx.x * EQ_TILE;
     const int j1 = j0 + EQ_TILE < a.n_u ? j0 + EQ_TILE : a.n_u;
+#ifdef SBR_EQ_WGTIME
+    const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
+#endif
     eq_column<BLOCK, INTEREST>(b, j0, j1, L, eta, t_end, u, a, ia, out, smem);
+#ifdef SBR_EQ_WGTIME
+    __syncthreads();
+    const size_t wg = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
+    if (threadIdx.x == 0 && wg < kWgTimeMax) {
+        g_wgtime[2 * wg] = wt0;
+        g_wgtime[2 * wg + 1] = __builtin_amdgcn_s_memrealtime();
+        // HW_ID (SE / CU / SIMD of wave 0) and XCC_ID: where the workgroup ran
+        g_wghw[2 * wg] = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));
+        g_wghw[2 * wg + 1] = __builtin_amdgcn_s_getreg((20) | (0 << 6) | (31 << 11));
+    }
+#endif
 }
 
 // ============================================================================
@@ -1423,3 +1579,14 @@ hipError_t launch_interest(const LearnBufs& L, const double* eta, const double* 
 }
 
 }  // namespace sbr
+
+#ifdef SBR_EQ_WGTIME
+// diagnostic build only: copy the workgroup timeline of the last equilibrium launch (n entries)
+extern "C" int sbr_diag_wgtime_read(unsigned long long* t2, unsigned int* hw2, int n)
+{
+    if (n < 0 || (size_t)n > sbr::kWgTimeMax) return -1;
+    if (hipMemcpyFromSymbol(t2, HIP_SYMBOL(sbr::g_wgtime), sizeof(unsigned long long) * 2 * n) != hipSuccess) return -2;
+    if (hipMemcpyFromSymbol(hw2, HIP_SYMBOL(sbr::g_wghw), sizeof(unsigned int) * 2 * n) != hipSuccess) return -2;
+    return 0;
+}
+#endif

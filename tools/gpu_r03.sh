@@ -30,6 +30,11 @@ for s in ${STEPS:-tests smoke bench single}; do
     interest) run interest 600 python -u bench.py --workload interest --steps 3 --warmup 1 ;;
     social) run social 600 python -u bench.py --workload social --steps 1 --warmup 0 ;;
     config1) run config1 300 python -u bench.py --workload config1 --steps 50 --warmup 3 ;;
+    phases) run phases 300 python -u bench.py --phases --steps 10 --warmup 2 --no-cpu-baseline ;;
+    wgtime) run wgtime 300 env SBR_LIB=replication-social-bank-runs_amd/lib_var/wgtime/libsbr.so WG_OUT=$OUT/wgtime.npz python -u tools/wgtime.py ;;
+    phasevars) for v in ${VARS:-}; do run phases_$v 300 env SBR_LIB=replication-social-bank-runs_amd/lib_var/$v/libsbr.so python -u bench.py --phases --steps 10 --warmup 2 --no-cpu-baseline; done ;;
+    pmc) PMC_OUT=$OUT/pmc bash tools/pmc.sh > "$OUT/pmc.out" 2>&1; echo "pmc rc=$?" | tee -a "$OUT/steps.log" ;;
+    pmcphase) for fl in 0x100 0x200 0; do run pmcph_$fl 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY --output-format csv -d "$OUT/pmcph_$fl" -o pass -- python3 tools/eq_diag_run.py $fl; done ;;
     config2) run config2 300 python -u bench.py --workload config2 --steps 20 --warmup 2 ;;
   esac
 done
