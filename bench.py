@@ -371,7 +371,7 @@ def main():
         "work_per_step": {"run_points": int(run.sum()), "bisect_iters": int(iters.sum()),
                           "aw_knots_run": int((run * n_tau[:, None]).sum()),
                           "rk_steps": int((ls["n_accept"] + ls["n_reject"]).sum())},
-        "roofline": (roofline("equilibrium_kernel", f_eq, eq_s, pmc_of("equilibrium_kernel<", f"fig5_{n}x{n}"))
+        "roofline": (roofline("equilibrium_kernel", f_eq, eq_s, pmc_of("equilibrium_kernel<768, false, 1>", f"fig5_{n}x{n}"))
                      if pipe else None),
         "libsbr_sha16": lib_sha(),
     }
@@ -619,7 +619,7 @@ def main_interest(a):
         "run_fraction": float(((st & sbr.STATUS["SBR_RUN"]) > 0).mean()),
         "stiff_switch_fraction": float(((st & sbr.STATUS["SBR_STIFF_SWITCH"]) > 0).mean()),
         "roofline": roofline("equilibrium_kernel<*, true> (interest)", f_eq_i, eq_ms / max(ncalls, 1) / 1e3,
-                             pmc_of("equilibrium_kernel<512, true>", f"interest_fig5_{n}x{n}")),
+                             pmc_of("equilibrium_kernel<512, true, 1>", f"interest_fig5_{n}x{n}")),
         "libsbr_sha16": lib_sha(),
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

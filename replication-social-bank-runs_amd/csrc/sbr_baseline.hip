@@ -1224,7 +1224,7 @@ __device__ __forceinline__ void solve_interest_point(P T, P G, P H, const Summ& 
 // The equilibria of u values [j0, j1) of column b by one workgroup of BLOCK threads (smem:
 // the dynamic LDS slab of launch_equilibrium's size).  Starts and ends uniformly; the caller
 // puts a barrier between two calls on the same workgroup (the LDS slab and flags are reused).
-template <int BLOCK, bool INTEREST>
+template <int BLOCK, bool INTEREST, int MODE = 0>
 __device__ __forceinline__ void eq_column(const int b, const int j0, const int j1, const LearnBufs& L,
                                           const double* __restrict__ eta, const double* __restrict__ t_end,
                                           const double* __restrict__ u, const EqArgs& a, const InterestArgs& ia,
@@ -1241,6 +1241,10 @@ __device__ __forceinline__ void eq_column(const int b, const int j0, const int j
     // interest mode stages HR too (its value functions look it up every RK stage).
     constexpr int NS = INTEREST ? 3 : 2;
     const bool fits = n <= a.lds_cap && (!INTEREST || ntau <= a.lds_cap);
+    // MODE 1: the columns whose knots fit the LDS slab, MODE 2: the others, MODE 0: both.  The
+    // sweeps launch 1 then 2, so the hot kernel carries no copy of the global-memory path (half
+    // the machine code, no VGPR spills); a MODE-2 workgroup of a fitting column exits at once.
+    if ((MODE == 1 && !fits) || (MODE == 2 && fits)) return;
     double* sT = smem;
     double* sG = smem + a.lds_cap;
     double* sH = INTEREST ? smem + 2 * a.lds_cap : nullptr;
@@ -1371,16 +1375,16 @@ __device__ __forceinline__ void eq_column(const int b, const int j0, const int j
             r.tin = NAN; r.tout = NAN;
             r.status = ((lst & SBR_ARG_INVALID) || !(uj >= 0.0)) ? SBR_ARG_INVALID : (SBR_OOB | lbits);
         } else if (INTEREST && ia.r > 0.0) {
-            if (fits)
+            if (MODE != 2 && fits)
                 solve_interest_point(sT, sG, sH, S, n, ntau, nle, ETA, T1, trunc, uj, a.kappa, a.max_iters, lbits, ia,
                                      r, vsteps, a.aw_path, a.diag);
-            else
+            else if (MODE != 1)
                 solve_interest_point(gT, gG, gH, S, n, ntau, nle, ETA, T1, trunc, uj, a.kappa, a.max_iters, lbits, ia,
                                      r, vsteps, a.aw_path, a.diag);
-        } else if (fits) {
+        } else if (MODE != 2 && fits) {
             solve_point((const double*)sT, (const double*)sG, cH, S, n, ntau, nle, ETA, T1, trunc, uj, a.kappa,
                         a.max_iters, lbits, r, a.aw_path, a.diag);
-        } else {
+        } else if (MODE != 1) {
             solve_point(gT, gG, gH, S, n, ntau, nle, ETA, T1, trunc, uj, a.kappa, a.max_iters, lbits, r, a.aw_path, a.diag);
         }
         const size_t o = (size_t)b * (size_t)a.n_u + j;
@@ -1403,7 +1407,7 @@ __device__ unsigned long long g_wgtime[2 * kWgTimeMax];
 __device__ unsigned int g_wghw[2 * kWgTimeMax];
 #endif
 
-template <int BLOCK, bool INTEREST>
+template <int BLOCK, bool INTEREST, int MODE>
 __global__ __launch_bounds__(BLOCK, INTEREST ? 1 : SBR_EQ_MINW) void equilibrium_kernel(LearnBufs L, const double* __restrict__ eta,
                                                             const double* __restrict__ t_end,
                                                             const double* __restrict__ u, EqArgs a, InterestArgs ia,
@@ -1419,7 +1423,7 @@ __global__ __launch_bounds__(BLOCK, INTEREST ? 1 : SBR_EQ_MINW) void equilibrium
 #ifdef SBR_EQ_WGTIME
     const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
 #endif
-    eq_column<BLOCK, INTEREST>(b, j0, j1, L, eta, t_end, u, a, ia, out, smem);
+    eq_column<BLOCK, INTEREST, MODE>(b, j0, j1, L, eta, t_end, u, a, ia, out, smem);
 #ifdef SBR_EQ_WGTIME
     __syncthreads();
     const size_t wg = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
@@ -1535,13 +1539,18 @@ hipError_t launch_equilibrium(const LearnBufs& L, const double* eta, const doubl
     const int w = a.n_u < EQ_TILE ? a.n_u : EQ_TILE;
     dim3 grid(tiles, n_beta);
     const InterestArgs none{0.0, 1.0, 0.0, 0.0, 0, nullptr, nullptr, nullptr};
+    // the LDS-resident columns, then (a workgroup per column, exiting at once where it fits, no
+    // LDS slab) the columns beyond the slab on the global-memory path
+    auto go = [&](auto k1, auto k2, int bs) {
+        hipLaunchKernelGGL(k1, grid, dim3(bs), lds, s, L, eta, t_end, u, a, none, out);
+        hipLaunchKernelGGL(k2, grid, dim3(bs), 0, s, L, eta, t_end, u, a, none, out);
+    };
     if (w > 256)
-        hipLaunchKernelGGL((equilibrium_kernel<SBR_EQ_WIDE, false>), grid, dim3(SBR_EQ_WIDE), lds, s, L, eta, t_end, u, a,
-                           none, out);
+        go(equilibrium_kernel<SBR_EQ_WIDE, false, 1>, equilibrium_kernel<SBR_EQ_WIDE, false, 2>, SBR_EQ_WIDE);
     else if (w > 64)
-        hipLaunchKernelGGL((equilibrium_kernel<256, false>), grid, dim3(256), lds, s, L, eta, t_end, u, a, none, out);
+        go(equilibrium_kernel<256, false, 1>, equilibrium_kernel<256, false, 2>, 256);
     else
-        hipLaunchKernelGGL((equilibrium_kernel<64, false>), grid, dim3(64), lds, s, L, eta, t_end, u, a, none, out);
+        go(equilibrium_kernel<64, false, 1>, equilibrium_kernel<64, false, 2>, 64);
     return hipGetLastError();
 }
 
@@ -1567,14 +1576,18 @@ hipError_t launch_interest(const LearnBufs& L, const double* eta, const double* 
     const int tiles = (a.n_u + EQ_TILE - 1) / EQ_TILE;
     const int w = a.n_u < EQ_TILE ? a.n_u : EQ_TILE;
     dim3 grid(tiles, n_beta);
+    auto go = [&](auto k1, auto k2, int bs) {
+        hipLaunchKernelGGL(k1, grid, dim3(bs), lds, s, L, eta, t_end, u, a, ia, out);
+        hipLaunchKernelGGL(k2, grid, dim3(bs), 0, s, L, eta, t_end, u, a, ia, out);
+    };
     if (w > 512)
-        hipLaunchKernelGGL((equilibrium_kernel<1024, true>), grid, dim3(1024), lds, s, L, eta, t_end, u, a, ia, out);
+        go(equilibrium_kernel<1024, true, 1>, equilibrium_kernel<1024, true, 2>, 1024);
     else if (w > 256)
-        hipLaunchKernelGGL((equilibrium_kernel<512, true>), grid, dim3(512), lds, s, L, eta, t_end, u, a, ia, out);
+        go(equilibrium_kernel<512, true, 1>, equilibrium_kernel<512, true, 2>, 512);
     else if (w > 64)
-        hipLaunchKernelGGL((equilibrium_kernel<256, true>), grid, dim3(256), lds, s, L, eta, t_end, u, a, ia, out);
+        go(equilibrium_kernel<256, true, 1>, equilibrium_kernel<256, true, 2>, 256);
     else
-        hipLaunchKernelGGL((equilibrium_kernel<64, true>), grid, dim3(64), lds, s, L, eta, t_end, u, a, ia, out);
+        go(equilibrium_kernel<64, true, 1>, equilibrium_kernel<64, true, 2>, 64);
     return hipGetLastError();
 }
 
