@@ -527,9 +527,12 @@ struct Summ {
     const double* smc;
     bool mono; // G nondecreasing over the knots (no NaN): prefix max / suffix min are knot values
     double t_half; // time where G crosses 1/2 (lerp inverse), NaN if it does not: AW peak predictor
-    // aw_scan's preconditions: mono, 0 <= G[0], G[n−1] <= 2 (the 1e-14 rounding margin) and
-    // t[k+2] − t[k] > 1e-15·t[n−1] (a shifted τ̄ argument stays below the knot after next)
+    // aw_scan's preconditions: no NaN in G, 0 <= G[0], G[n−1] <= 2 (the 1e-14 rounding margin),
+    // t[k+2] − t[k] > 1e-15·t[n−1] (a shifted τ̄ argument stays below the knot after next) and a
+    // drawdown bound dd <= 1e-12 (Tsit5 at eps() leaves ulp-sized decreases in the saturated tail
+    // of G on ≈20 % of the Fig 5 columns: G[k] <= G[k'] + dd for every k < k')
     bool scan;
+    double dd;
 };
 
 template <class P>
@@ -560,7 +563,8 @@ __device__ __forceinline__ int first_ge_down(F key, int hi, double x)
 }
 
 // AW_max (solver.jl:553-576) over τ̄ knots [0, ntau) by an outward scan from the predicted
-// peak knot c, for a nondecreasing G with Summ::scan's preconditions.  AW_cum(τ̄_i) =
+// peak knot c, for a G with Summ::scan's preconditions (nondecreasing up to the drawdown dd:
+// every bound below is widened by dd, and the margin is 1e-14 + 4·dd).  AW_cum(τ̄_i) =
 // AW_OUT(b_i) − AW_IN(a_i) + G(0) with a_i = (τ̄_i − ξ) + icc ≤ b_i = (τ̄_i − ξ) + occ ≤ τ̄_i + ulp,
 // both nondecreasing in i, so
 //   right of the last evaluated knot i:  AW_OUT(b_j) ≤ G[j + 2] and AW_IN(a_j) ≥ AW_IN(a_i);
@@ -572,8 +576,9 @@ __device__ __forceinline__ int first_ge_down(F key, int hi, double x)
 template <class P>
 __device__ __forceinline__ void aw_scan(P T, P G, const int n, const int ntau, const int nle, const double ETA,
                                         const double xi, const double icc, const double occ, const double G0,
-                                        const int c, double& mx, int& nev)
+                                        const double dd, const int c, double& mx, int& nev)
 {
+    const double M = 1e-14 + 4.0 * dd;
     auto tau = [&](int i) -> double { return i < nle ? T[i] : ETA; };
     auto av_of = [&](int i) -> double { return (tau(i) - xi) + icc; };
     // a(τ̄_i)'s bracket window: k = min(searchsortedlast(t, x), n − 2), its two knots (t, G)
@@ -624,7 +629,7 @@ __device__ __forceinline__ void aw_scan(P T, P G, const int n, const int ntau, c
         fwd(xa);
         const double lb = av >= 0 ? ga0 : 0.0;
         LA = LA > lb ? LA : lb;
-        const double V = ((mx - G0) + LA) - 1e-14;
+        const double V = (((mx - G0) + LA) - M) - dd; // G[k] <= V: every knot up to k is <= V + dd
         const int k2 = i + 2 < n - 1 ? i + 2 : n - 1;
         if (G[k2] > V) {
             const double v = exact(i, av, xa);
@@ -651,8 +656,8 @@ __device__ __forceinline__ void aw_scan(P T, P G, const int n, const int ntau, c
         const int k2 = i + 2 < n - 1 ? i + 2 : n - 1;
         const double g2 = G[k2] > 0.0 ? G[k2] : 0.0;
         UB = UB < g2 ? UB : g2;
-        const double Vp = ((UB + G0) + 1e-14) - mx;
-        if (!(Vp > 0.0)) break; // AW_IN(a_j) >= 0 for every j: all pruned
+        const double Vp = (((UB + G0) + M) - mx) + dd; // AW_IN(a_j) >= G[bracket(a_j)] − dd
+        if (!(Vp - dd > 0.0)) break; // AW_IN(a_j) >= 0 for every j: all pruned
         const double av = av_of(i), xa = av > 0 ? av : 0.0;
         bwd(xa);
         const double lb = av >= 0 ? ga0 : 0.0;
@@ -903,7 +908,9 @@ __device__ __forceinline__ void solve_from_buffers(P T, P G, P H, const Summ& S,
         rb_j = kb; rb_i = i1 - 1;
     };
     if (!S.pmc || aw_path) {
+#ifndef SBR_EQ_NOFALLBACK_TEST // timing A/B only (wrong results off the scan path)
         eval_range(0, ntau); // exhaustive (single-point path mode, or summaries unavailable)
+#endif
     } else {
         // Branch and bound over a 256/64/8 hierarchy of τ̄ ranges — the same maximum,
         // far fewer evaluations.  Every argument sequence is nondecreasing in i, so the
@@ -939,10 +946,14 @@ __device__ __forceinline__ void solve_from_buffers(P T, P G, P H, const Summ& S,
             const int ic = predicted ? ssl_range(T, 0, (nle > 0 ? nle : 1) - 1, tstar < T[0] ? T[0] : tstar) : 0;
 #if SBR_AW_SCAN
             if (S.scan && predicted) {
-                aw_scan(T, G, n, ntau, nle, ETA, xi, icc, occ, G0, ic < ntau ? ic : ntau - 1, mx, nblk_eval);
+                aw_scan(T, G, n, ntau, nle, ETA, xi, icc, occ, G0, S.dd, ic < ntau ? ic : ntau - 1, mx, nblk_eval);
             } else
 #endif
+#ifndef SBR_EQ_NOFALLBACK_TEST
             {
+#else
+            if (0) {
+#endif
             int b8 = -1, w0 = 0, w1 = 0;
             if (predicted) {
                 const int c8 = (ic < ntau ? ic : ntau - 1) & ~7;
@@ -1258,17 +1269,19 @@ __device__ __forceinline__ void eq_column(const int b, const int j0, const int j
     __shared__ int eq_next;
     __shared__ int s_nonmono;
     __shared__ int s_noscan;
+    __shared__ int s_ndec;                 // decreases of G between consecutive knots
+    __shared__ unsigned long long s_maxdec; // largest decrease (bits of a nonnegative double)
     __shared__ double s_thalf;
     // every shared flag is initialised before the first barrier: lanes >= nq set
     // s_nonmono right after it, so a later store by thread 0 could clear their flag
-    if (threadIdx.x == 0) { eq_next = 0; s_nonmono = 0; s_noscan = 0; s_thalf = NAN; }
+    if (threadIdx.x == 0) { eq_next = 0; s_nonmono = 0; s_noscan = 0; s_ndec = 0; s_maxdec = 0; s_thalf = NAN; }
     if (fits) {
         for (int i = threadIdx.x; i < n; i += BLOCK) { sT[i] = gT[i]; sG[i] = gG[i]; }
         if (INTEREST)
             for (int i = threadIdx.x; i < ntau; i += BLOCK) sH[i] = gH[i];
     }
     __syncthreads();
-    Summ S{nullptr, nullptr, nullptr, nullptr, false, (double)NAN, false};
+    Summ S{nullptr, nullptr, nullptr, nullptr, false, (double)NAN, false, 0.0};
     if (fits && !a.exhaustive) {
         const int nbh = (ntau + 63) >> 6, nbg = (n + 7) >> 3;
         // HR summaries: 8 lanes per 64-entry block, 8 independent loads each (HR is read from
@@ -1302,16 +1315,26 @@ __device__ __forceinline__ void eq_column(const int b, const int j0, const int j
                 double mx = -INFINITY, mn = INFINITY;
                 const int e = (g << 3) + 8 < n ? (g << 3) + 8 : n;
                 double prev = g > 0 ? sG[(g << 3) - 1] : -INFINITY;
-                bool mono = true;
+                bool mono = true, nan = false;
+                int ndec = 0;
+                double maxdec = 0.0;
                 for (int i = g << 3; i < e; i++) {
                     const double v = sG[i];
-                    if (v != v) { mx = NAN; mn = NAN; mono = false; break; }
+                    if (v != v) { mx = NAN; mn = NAN; mono = false; nan = true; break; }
                     if (v > mx) mx = v;
                     if (v < mn) mn = v;
-                    mono &= v >= prev;
+                    const bool dec = v < prev;
+                    mono &= !dec;
+                    ndec += dec ? 1 : 0;
+                    maxdec = dec && prev - v > maxdec ? prev - v : maxdec;
                     prev = v;
                 }
                 if (!mono) s_nonmono = 1;
+                if (nan) s_noscan = 1;
+                if (ndec) {
+                    atomicAdd(&s_ndec, ndec);
+                    atomicMax(&s_maxdec, (unsigned long long)sbr_dbits(maxdec));
+                }
                 // aw_scan's knot separation (Summ::scan)
                 const double sep = 1e-15 * sT[n - 1];
                 bool far = true;
@@ -1347,8 +1370,9 @@ __device__ __forceinline__ void eq_column(const int b, const int j0, const int j
             }
         }
         __syncthreads();
+        const double dd = (double)s_ndec * sbr_bitsd(s_maxdec); // ≥ the largest drawdown
         S = Summ{hmax, hmin, pmc, smc, s_nonmono == 0, s_thalf,
-                 s_nonmono == 0 && !s_noscan && sG[0] >= 0.0 && sG[n - 1] <= 2.0};
+                 !s_noscan && dd <= 1e-12 && sG[0] >= 0.0 && sG[n - 1] <= 2.0, dd};
     }
     // Points are handed out to waves 64 at a time from an LDS counter, so a
     // wave that drew cheap no-run points goes back for more instead of idling
