@@ -533,6 +533,7 @@ struct Summ {
     // of G on ≈20 % of the Fig 5 columns: G[k] <= G[k'] + dd for every k < k')
     bool scan;
     double dd;
+    bool bnb; // the branch-and-bound bounds are available (mono, or the prefix/suffix tables built)
 };
 
 template <class P>
@@ -598,9 +599,11 @@ __device__ __forceinline__ void aw_scan(P T, P G, const int n, const int ntau, c
     // exact AW_cum(τ̄_i) with the a window at a_i's bracket; b's bracket is searched from i
     double awin = 0.0, awout = 0.0;
     auto exact = [&](int i, double av, double xa) -> double {
-        const double bv = (tau(i) - xi) + occ;
+        const double ti = tau(i);
+        const double bv = (ti - xi) + occ;
         const double xb = bv > 0 ? bv : 0.0;
-        int kb = ssl_near(T, n, i, xb);
+        // b(τ̄_i) is τ̄_i = t[i] itself whenever τ̄_i − ξ is exact: bracket i, no search
+        int kb = (i < nle && xb == ti) ? i : ssl_near(T, n, i, xb);
         kb = kb < n - 2 ? kb : n - 2;
         const double tb0 = T[kb], tb1 = T[kb + 1], gb0 = G[kb], gb1 = G[kb + 1];
         const double da = (xa - ta0) / (ta1 - ta0);
@@ -907,7 +910,13 @@ __device__ __forceinline__ void solve_from_buffers(P T, P G, P H, const Summ& S,
         ra_j = ka; ra_i = i1 - 1;
         rb_j = kb; rb_i = i1 - 1;
     };
-    if (!S.pmc || aw_path) {
+    // AW peak predictor (a logistic-shaped CDF): the continuous maximiser of
+    // G(τ − s_out) − G(τ − s_in) sits where G(τ − s_out) + G(τ − s_in) = 1, i.e. at
+    // τ* = t_half + (s_in + s_out)/2
+    const double tstar = S.t_half + 0.5 * ((xi - icc) + (xi - occ));
+    const bool predicted = tstar == tstar && tstar >= tau(0) && tstar <= tau(ntau - 1);
+    const bool scan = SBR_AW_SCAN && S.scan && predicted;
+    if (!S.pmc || aw_path || !(scan || S.bnb)) {
 #ifndef SBR_EQ_NOFALLBACK_TEST // timing A/B only (wrong results off the scan path)
         eval_range(0, ntau); // exhaustive (single-point path mode, or summaries unavailable)
 #endif
@@ -941,11 +950,9 @@ __device__ __forceinline__ void solve_from_buffers(P T, P G, P H, const Summ& S,
             // i.e. at τ* = t_half + (s_in + s_out)/2: evaluate the 8-blocks around it
             // (a heuristic — exactness comes from pass 2's bounds).  Otherwise descend the
             // bound hierarchy to the most promising 8-block.
-            const double tstar = S.t_half + 0.5 * ((xi - icc) + (xi - occ));
-            const bool predicted = tstar == tstar && tstar >= tau(0) && tstar <= tau(ntau - 1);
             const int ic = predicted ? ssl_range(T, 0, (nle > 0 ? nle : 1) - 1, tstar < T[0] ? T[0] : tstar) : 0;
 #if SBR_AW_SCAN
-            if (S.scan && predicted) {
+            if (scan) {
                 aw_scan(T, G, n, ntau, nle, ETA, xi, icc, occ, G0, S.dd, ic < ntau ? ic : ntau - 1, mx, nblk_eval);
             } else
 #endif
@@ -1281,7 +1288,7 @@ __device__ __forceinline__ void eq_column(const int b, const int j0, const int j
             for (int i = threadIdx.x; i < ntau; i += BLOCK) sH[i] = gH[i];
     }
     __syncthreads();
-    Summ S{nullptr, nullptr, nullptr, nullptr, false, (double)NAN, false, 0.0};
+    Summ S{nullptr, nullptr, nullptr, nullptr, false, (double)NAN, false, 0.0, false};
     if (fits && !a.exhaustive) {
         const int nbh = (ntau + 63) >> 6, nbg = (n + 7) >> 3;
         // HR summaries: 8 lanes per 64-entry block, 8 independent loads each (HR is read from
@@ -1357,13 +1364,14 @@ __device__ __forceinline__ void eq_column(const int b, const int j0, const int j
                 }
                 s_thalf = sT[lo] + (0.5 - sG[lo]) * (sT[hi] - sT[lo]) / (sG[hi] - sG[lo]);
             }
-            // the tables are read only when G is not monotone (Summ::mono): skip the serial scans
-            if (s_nonmono)
+            // the tables are read only when G is not monotone (Summ::mono) and aw_scan's
+            // preconditions fail (the scan's points never read them): skip the serial scans
+            if (s_nonmono && s_noscan)
             for (int g = 1; g < nbg; g++) {
                 const double a0 = pmc[g - 1], b0 = pmc[g];
                 pmc[g] = (a0 != a0 || b0 != b0) ? NAN : (a0 > b0 ? a0 : b0);
             }
-        } else if (threadIdx.x == (BLOCK > 64 ? 64 : 1) && s_nonmono) {
+        } else if (threadIdx.x == (BLOCK > 64 ? 64 : 1) && s_nonmono && s_noscan) {
             for (int g = nbg - 2; g >= 0; g--) {
                 const double a0 = smc[g + 1], b0 = smc[g];
                 smc[g] = (a0 != a0 || b0 != b0) ? NAN : (a0 < b0 ? a0 : b0);
@@ -1372,7 +1380,7 @@ __device__ __forceinline__ void eq_column(const int b, const int j0, const int j
         __syncthreads();
         const double dd = (double)s_ndec * sbr_bitsd(s_maxdec); // ≥ the largest drawdown
         S = Summ{hmax, hmin, pmc, smc, s_nonmono == 0, s_thalf,
-                 !s_noscan && dd <= 1e-12 && sG[0] >= 0.0 && sG[n - 1] <= 2.0, dd};
+                 !s_noscan && dd <= 1e-12 && sG[0] >= 0.0 && sG[n - 1] <= 2.0, dd, s_nonmono == 0 || s_noscan != 0};
     }
     // Points are handed out to waves 64 at a time from an LDS counter, so a
     // wave that drew cheap no-run points goes back for more instead of idling
