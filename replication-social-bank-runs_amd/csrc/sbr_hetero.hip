@@ -1172,7 +1172,7 @@ __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const d
 #ifndef SBR_HET_EQ_PRIO
 #define SBR_HET_EQ_PRIO 2 // equilibrium waves ahead of the co-resident learning waves (config-4 step 49.7 -> 47.9 ms)
 #endif
-template <int K, int BLOCK>
+template <int K, int BLOCK, int MODE>
 #ifndef SBR_HET_MINW
 #define SBR_HET_MINW 2 // waves per SIMD: two 4-wave workgroups per CU (LDS slab: SBR_HET_LDS in sbr_capi.hip)
 #endif
@@ -1205,6 +1205,9 @@ __global__ __launch_bounds__(BLOCK, SBR_HET_MINW) void equilibrium_hetero_kernel
     const size_t cap = (size_t)L.cap;
     const double* __restrict__ gT = L.t + (size_t)c * cap;
     const bool fits = n <= a.lds_cap;
+    // MODE 1: columns whose knot times fit the LDS slab; MODE 2: the others (global-memory path,
+    // launched second without a slab); the hot launch carries one copy of the point solve
+    if ((MODE == 1 && !fits) || (MODE == 2 && fits)) return;
     __shared__ int s_nonmono;
     if (threadIdx.x == 0) s_nonmono = a.exhaustive || a.aw_path; // path mode: every knot
     if (fits)
@@ -1284,7 +1287,7 @@ __global__ __launch_bounds__(BLOCK, SBR_HET_MINW) void equilibrium_hetero_kernel
 #pragma unroll
         for (int k = 0; k < K; k++) { tin[k] = NAN; tout[k] = NAN; }
         st = ((lst & SBR_ARG_INVALID) || !(uj >= 0.0)) ? SBR_ARG_INVALID : (SBR_OOB | lbits);
-    } else if (fits) {
+    } else if constexpr (MODE == 1) {
         HCol<K, const double*> C{smem, L.G + (size_t)c * cap * K, L.hr + (size_t)c * K * cap, n, L.n_tau[c],
                                  L.n_le[c], cap, eta[c], t_end[c], sums && !a.exhaustive ? hsum : nullptr, nblk};
         solve_hetero_point<K>(C, dl, uj, a.kappa, a.max_iters, a.tolerance, lbits, xi, aw, tol, st, it, tin, tout,
@@ -1325,24 +1328,23 @@ static hipError_t launch_hetero_k(const double* betas, const double* dist, const
     const size_t lds = (size_t)ea_in.lds_cap * sizeof(double);
     HeteroEqArgs ea = ea_in;
     ea.n_col = la.n_beta;
+    // the LDS-resident columns, then (no slab, exiting at once where the knots fit) the others
+    auto go = [&](auto k1, auto k2, dim3 grid, int bs) {
+        hipLaunchKernelGGL(k1, grid, dim3(bs), lds, s, L, dist, eta, t_end, u, ea, out, tin, tout);
+        hipLaunchKernelGGL(k2, grid, dim3(bs), 0, s, L, dist, eta, t_end, u, ea, out, tin, tout);
+    };
 #if SBR_HET_XCD
     const unsigned ncol8 = (unsigned)((la.n_beta + 7) / 8) * 8;
-    if (ea.n_u >= SBR_HET_BLOCK) {
-        hipLaunchKernelGGL((equilibrium_hetero_kernel<K, SBR_HET_BLOCK>), dim3(((ea.n_u + SBR_HET_BLOCK - 1) / SBR_HET_BLOCK) * ncol8),
-                           dim3(SBR_HET_BLOCK), lds, s,
-                           L, dist, eta, t_end, u, ea, out, tin, tout);
-    } else {
-        hipLaunchKernelGGL((equilibrium_hetero_kernel<K, 64>), dim3(((ea.n_u + 63) / 64) * ncol8), dim3(64), lds, s,
-                           L, dist, eta, t_end, u, ea, out, tin, tout);
-    }
+    if (ea.n_u >= SBR_HET_BLOCK)
+        go(equilibrium_hetero_kernel<K, SBR_HET_BLOCK, 1>, equilibrium_hetero_kernel<K, SBR_HET_BLOCK, 2>,
+           dim3(((ea.n_u + SBR_HET_BLOCK - 1) / SBR_HET_BLOCK) * ncol8), SBR_HET_BLOCK);
+    else
+        go(equilibrium_hetero_kernel<K, 64, 1>, equilibrium_hetero_kernel<K, 64, 2>, dim3(((ea.n_u + 63) / 64) * ncol8), 64);
 #else
-    if (ea.n_u >= 256) {
-        hipLaunchKernelGGL((equilibrium_hetero_kernel<K, 256>), dim3((ea.n_u + 255) / 256, la.n_beta), dim3(256), lds, s,
-                           L, dist, eta, t_end, u, ea, out, tin, tout);
-    } else {
-        hipLaunchKernelGGL((equilibrium_hetero_kernel<K, 64>), dim3((ea.n_u + 63) / 64, la.n_beta), dim3(64), lds, s,
-                           L, dist, eta, t_end, u, ea, out, tin, tout);
-    }
+    if (ea.n_u >= 256)
+        go(equilibrium_hetero_kernel<K, 256, 1>, equilibrium_hetero_kernel<K, 256, 2>, dim3((ea.n_u + 255) / 256, la.n_beta), 256);
+    else
+        go(equilibrium_hetero_kernel<K, 64, 1>, equilibrium_hetero_kernel<K, 64, 2>, dim3((ea.n_u + 63) / 64, la.n_beta), 64);
 #endif
     return hipGetLastError();
 }
