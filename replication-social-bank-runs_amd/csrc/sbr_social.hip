@@ -24,6 +24,8 @@
 //
 // Bit-exact against oracle/sbr_oracle.c social_point (same operation order,
 // -ffp-contract=off, fma() where the oracle has it, shared sbr_exp/sbr_log).
+#include <type_traits>
+
 #include "sbr_device.h"
 #include "sbr_kernels.h"
 #include "sbr_ode.h"
@@ -295,6 +297,134 @@ struct SocialRhs {
     static constexpr bool kPinTableau = false;
 };
 
+#ifndef SBR_SOCIAL_COOP
+#define SBR_SOCIAL_COOP 1 // a wave left with one live point runs it on all 64 lanes (SocialRhsCoop)
+#endif
+// The same right-hand side for a wave whose 64 lanes all run ONE point (the tail of a sweep,
+// when the spread worklist leaves one live point per wave): every lane executes the identical
+// chain, and AW_{n−1}'s knots are held across the wave — lane L holds knot wb + L (time and
+// value) — so a stage lookup is a ballot over the window (the lanes whose knot time is ≤ x form
+// a prefix: the bracket is wb + popcount − 1) and four v_readlanes, instead of waiting on an
+// L2/HBM round trip per step.  The window moves forward by 32 knots when the step's time passes
+// its middle (one coalesced load per array); lookups outside it fall back to the global search.
+// Same brackets, same operands, same operations as SocialRhs: bit-identical.
+struct SocialRhsCoop {
+    double beta;
+    BView to;
+    BView vo;
+    int n;
+    double tfirst, tlast;
+    int wb;           // window base (wave-uniform)
+    double wt, wv;    // this lane's knot wb + lane (+Inf / 0 past the grid)
+    double aw[5];
+    double last_aw;
+    bool oob;
+    int slow;
+    __device__ __forceinline__ void refill(int base)
+    {
+        wb = base;
+        const int i = base + (int)(threadIdx.x & 63);
+        const int ic = i < n - 1 ? i : (n > 0 ? n - 1 : 0);
+        const double t = to[ic], v = vo[ic];
+        wt = i < n ? t : (double)INFINITY;
+        wv = i < n ? v : 0.0;
+    }
+    __device__ __forceinline__ void init(double b, BView t_, BView v_, int n_)
+    {
+        slow = 0;
+        beta = b; to = t_; vo = v_; n = n_;
+        tfirst = n > 0 ? to[0] : 0.0;
+        tlast = n > 0 ? to[n - 1] : 0.0;
+        oob = false;
+        last_aw = 0.0;
+        refill(0);
+    }
+    __device__ __forceinline__ static double lane_d(double x, int k)
+    {
+        const uint64_t u = sbr_dbits(x);
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, k);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), k);
+        return sbr_bitsd(((uint64_t)hi << 32) | lo);
+    }
+    // searchsortedlast(t, x) for t[0] <= x <= t[n−1] (wave-uniform x)
+    __device__ __forceinline__ int find(double x)
+    {
+        const int c = __popcll(__ballot(wt <= x));
+        if (c >= 1 && c < 64) return wb + c - 1;
+        slow++;
+        return c == 0 ? ssl_range(to, 0, wb, x) : ssl_gallop(to, n, wb + 63, x);
+    }
+    // lerp_at(to, vo, n, j, x) with the operands from the window where it holds them
+    __device__ __forceinline__ double lerp_j(int j, double x)
+    {
+        j = j > n - 2 ? n - 2 : j;
+        j = j < 0 ? 0 : j;
+        const int k = __builtin_amdgcn_readfirstlane(j - wb);
+        double t0, t1, v0, v1;
+        if (k >= 0 && k < 63) {
+            t0 = lane_d(wt, k); t1 = lane_d(wt, k + 1); v0 = lane_d(wv, k); v1 = lane_d(wv, k + 1);
+        } else {
+            t0 = to[j]; t1 = to[j + 1]; v0 = vo[j]; v1 = vo[j + 1];
+        }
+        const double d = (x - t0) / (t1 - t0);
+        return v0 * (1.0 - d) + v1 * d;
+    }
+    __device__ __forceinline__ double lookup(double x)
+    {
+        if (n < 2 || !(x >= tfirst && x <= tlast)) { oob = true; return (double)NAN; }
+        return lerp_j(find(x), x);
+    }
+    __device__ __forceinline__ double eval(double t, double x)
+    {
+        const double a = lookup(t);
+        last_aw = a;
+        return ((1.0 - x) * beta) * a;
+    }
+    __device__ __forceinline__ void prepare(double t, double dt)
+    {
+        const double xs[5] = {fma(C1, dt, t), fma(C2, dt, t), fma(C3, dt, t), fma(C4, dt, t), t + dt};
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            const bool in = n >= 2 && xs[k] >= tfirst && xs[k] <= tlast;
+            aw[k] = in ? lerp_j(find(xs[k]), xs[k]) : (double)NAN;
+            oob |= !in;
+        }
+        last_aw = aw[4];
+    }
+    __device__ __forceinline__ double stage(int s, double, double x) const
+    {
+        return ((1.0 - x) * beta) * aw[s < 5 ? s - 1 : 4];
+    }
+    __device__ __forceinline__ void jac(double t, double x, double& J, double& dT)
+    {
+        if (n < 2 || !(t >= tfirst && t <= tlast)) {
+            oob = true;
+            J = (double)NAN;
+            dT = (double)NAN;
+            return;
+        }
+        int j = find(t);
+        j = j > n - 2 ? n - 2 : (j < 0 ? 0 : j);
+        const double t0 = to[j], t1 = to[j + 1], v0 = vo[j], v1 = vo[j + 1];
+        const double d = (t - t0) / (t1 - t0);
+        const double a = v0 * (1.0 - d) + v1 * d;
+        const double rr = 1.0 / (t1 - t0);
+        const double ap = v0 * (-rr) + v1 * rr;
+        J = ((-1.0) * beta) * a;
+        dT = ((1.0 - x) * beta) * ap;
+    }
+    // re-anchor the window 8 knots behind the accepted time once it passes the window's middle
+    __device__ __forceinline__ void accepted(double t)
+    {
+        if (n >= 2 && t >= tfirst && t <= tlast) {
+            const int c = __popcll(__ballot(wt <= t));
+            if (c >= 40) refill(wb + c - 9);
+        }
+    }
+    static constexpr bool kFsalExact = false;
+    static constexpr bool kPinTableau = false;
+};
+
 }  // namespace
 
 // ============================================================================
@@ -364,6 +494,10 @@ __global__ __launch_bounds__(64) void social_init_kernel(SocialArgs a)
 // one fixed-point iterate of point l (local index into a's per-point state);
 // false once the point has finished or moved into the promotion pool
 // ============================================================================
+// COOP: all 64 lanes of the wave run this same point (SocialRhsCoop); every lane computes the
+// same values and stores them to the same places, and the few non-idempotent steps (the pool
+// promotion, the live counter) are taken by lane 0 alone.
+template <bool COOP>
 __device__ __forceinline__ bool social_iterate(const SocialArgs& a, int l, int iter)
 {
     const int64_t g = a.pts ? a.pts[l] : a.pt0 + l;
@@ -399,14 +533,14 @@ __device__ __forceinline__ bool social_iterate(const SocialArgs& a, int l, int i
 
     stamp(0);
     // ---- (a) learning from withdrawals on (0, η) ----
-    SocialRhs f;
+    typename std::conditional<COOP, SocialRhsCoop, SocialRhs>::type f;
     f.init(BETA, TO, VO, n_old);
     int n = 0;
     bool overflow = false;
     // knots (t, G) and AW_{n−1} at each knot: the t + dt stage lookup unless the step
     // was snapped to T1 (the first knot: AW_{n−1}(0))
     struct Sink {
-        SocialRhs& f;
+        decltype(f)& f;
         BView T, Gv, AWO;
         int& n;
         int cap;
@@ -433,7 +567,17 @@ __device__ __forceinline__ bool social_iterate(const SocialArgs& a, int l, int i
     stamp(1);
     if (PR) { PR[6] += f.slow; PR[7] += o.naccept + o.nreject; }
     if (f.oob) o.status |= SBR_OOB;
-    if (overflow && a.pool.ws && promote(a, l, g, iter, TO, VO, n_old)) return false;
+    if (overflow && a.pool.ws) {
+        bool moved;
+        if constexpr (COOP) {
+            moved = false;
+            if ((threadIdx.x & 63) == 0) moved = promote(a, l, g, iter, TO, VO, n_old);
+            moved = __builtin_amdgcn_readfirstlane(moved ? 1 : 0) != 0;
+        } else {
+            moved = promote(a, l, g, iter, TO, VO, n_old);
+        }
+        if (moved) return false;
+    }
     a.steps[l] += o.naccept + o.nreject;
     bits |= o.status & (SBR_ODE_MAXITERS | SBR_STIFF_SWITCH | SBR_ODE_FAILED);
 
@@ -708,7 +852,7 @@ __device__ __forceinline__ bool social_iterate(const SocialArgs& a, int l, int i
         if (a.fp_iters) a.fp_iters[g] = iter;
         if (a.steps_out) a.steps_out[g] = a.steps[l];
         a.live[l] = 0;
-        if (a.n_live) atomicSub(a.n_live, 1);
+        if (a.n_live && (!COOP || (threadIdx.x & 63) == 0)) atomicSub(a.n_live, 1);
         return false;
     }
     a.live[l] = 1;
@@ -754,6 +898,17 @@ __global__ __launch_bounds__(64) void social_iter_kernel(const SocialArgs* __res
         const int cnt = *count;
         int L = SBR_SOCIAL_WAVES ? (cnt + nbs - 1) / nbs : 64;
         L = L < 1 ? 1 : (L > 64 ? 64 : L);
+#if SBR_SOCIAL_COOP
+        if (L == 1) { // one point per wave: the whole wave runs it
+            const int w = blockIdx.x;
+            if (w >= cnt) return;
+            l = work[w];
+            if (!sa.live[l]) return;
+            for (int k = 0; k < n_inner; k++)
+                if (!social_iterate<true>(sa, l, iter_arg + k)) break;
+            return;
+        }
+#endif
         if ((int)threadIdx.x >= L) return;
         const int w = blockIdx.x * L + threadIdx.x;
         if (w >= cnt) return;
@@ -761,15 +916,28 @@ __global__ __launch_bounds__(64) void social_iter_kernel(const SocialArgs* __res
         if (!sa.live[l]) return; // retired by the init kernel (knot overflow)
         iter = iter_arg;
     } else {
+#if SBR_SOCIAL_COOP
+        // one pool slot per wave, run by the whole wave (the pool holds the longest fixed
+        // points — the ones whose iterates outgrew the main capacity)
+        l = (int)blockIdx.x - nbs;
+        if (l >= pa.n_pts) return;
+        if (__hip_atomic_load(pa.ready + l, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
+        if (!pa.live[l]) return;
+        iter = pa.it_cur[l];
+        for (int k = 0; k < n_inner; k++)
+            if (!social_iterate<true>(pa, l, iter + k)) break;
+        return;
+#else
         l = ((int)blockIdx.x - nbs) * 64 + threadIdx.x;
         if (l >= pa.n_pts) return;
         if (__hip_atomic_load(pa.ready + l, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
         if (!pa.live[l]) return;
         iter = pa.it_cur[l];
+#endif
     }
     const SocialArgs& a = args[in_pool ? 1 : 0];
     for (int k = 0; k < n_inner; k++)
-        if (!social_iterate(a, l, iter + k)) break;
+        if (!social_iterate<false>(a, l, iter + k)) break;
 }
 
 // ============================================================================
@@ -830,7 +998,8 @@ hipError_t launch_social_iter(const SocialArgs& a, const SocialArgs& p, const So
     int nbs = (a.n_pts + 63) / 64;
     nbs = nbs > SBR_SOCIAL_WAVES ? nbs : SBR_SOCIAL_WAVES;
     nbs = nbs < a.n_pts ? nbs : (a.n_pts > 0 ? a.n_pts : 1);
-    hipLaunchKernelGGL(social_iter_kernel, dim3(nbs + (p.n_pts + 63) / 64), dim3(64), 0, s, args_dev, iter, n_inner,
+    const int pool_waves = SBR_SOCIAL_COOP ? p.n_pts : (p.n_pts + 63) / 64;
+    hipLaunchKernelGGL(social_iter_kernel, dim3(nbs + pool_waves), dim3(64), 0, s, args_dev, iter, n_inner,
                        work, count, nbs);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;

@@ -35,6 +35,8 @@ for s in ${STEPS:-tests smoke bench single}; do
     phasevars) for v in ${VARS:-}; do run phases_$v 300 env SBR_LIB=replication-social-bank-runs_amd/lib_var/$v/libsbr.so python -u bench.py --phases --steps 10 --warmup 2 --no-cpu-baseline; done ;;
     pmc) PMC_OUT=$OUT/pmc bash tools/pmc.sh > "$OUT/pmc.out" 2>&1; echo "pmc rc=$?" | tee -a "$OUT/steps.log" ;;
     pmcphase) for fl in 0x100 0x200 0; do run pmcph_$fl 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY --output-format csv -d "$OUT/pmcph_$fl" -o pass -- python3 tools/eq_diag_run.py $fl; done ;;
+    socprobe) run socprobe 600 python -u tools/social_step_probe.py ${PROBE_ITERS:-8} && run socprobe_nocoop 600 env SBR_LIB=replication-social-bank-runs_amd/lib_var/nocoop/libsbr.so python -u tools/social_step_probe.py ${PROBE_ITERS:-8} ;;
+    socphase) run socphase 600 python -u tools/social_phase_probe.py ${PROBE_ITERS:-8} && run socphase_nocoop 600 env SBR_LIB=replication-social-bank-runs_amd/lib_var/nocoop/libsbr.so python -u tools/social_phase_probe.py ${PROBE_ITERS:-8} ;;
     config2) run config2 300 python -u bench.py --workload config2 --steps 20 --warmup 2 ;;
   esac
 done
