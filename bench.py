@@ -492,7 +492,7 @@ def main_hetero(a):
         "stiff_switch": "handled (Rosenbrock23 restated, DESIGN.md §2)",
         "learn_steps_per_column": float((hs["n_accept"] + hs["n_reject"]).mean()),
         "roofline": roofline("equilibrium_hetero_kernel", f_eq_h, eq_ms / max(ncalls, 1) / 1e3,
-                             pmc_of("equilibrium_hetero_kernel<", f"hetero_K8_{n}x{n}")),
+                             pmc_of("equilibrium_hetero_kernel<8, 256, 1>", f"hetero_K8_{n}x{n}")),
         "libsbr_sha16": lib_sha(),
     }
     if a.phases:

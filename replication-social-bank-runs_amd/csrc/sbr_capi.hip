@@ -9,6 +9,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <chrono>
 #include <string>
 #include <vector>
 
@@ -1628,16 +1629,22 @@ int run_social_pass(sbr_ctx* c, hipStream_t s, const double* beta, const double*
         // kSocialInner iterates per launch; a point promoted during a launch redoes that
         // iterate in the same or the next launch: one launch past max_iter drains the pool
         const int n_launch = (max_iter + kSocialInner - 1) / kSocialInner + (nslots > 0 ? 1 : 0);
+        static const bool trace = getenv("SBR_SOCIAL_TRACE") != nullptr;
+        const auto tr0 = std::chrono::steady_clock::now();
         for (int q = 0; q < n_launch; q++) {
             const int k = q & 1, it = 1 + q * kSocialInner;
             HIP_TRY(c, sbr::launch_social_iter(a, b, c->so_args_dev, it, kSocialInner, c->so_work[k],
                                                c->so_count + k, c->so_work[k ^ 1], c->so_count + (k ^ 1), s),
                     SBR_EDEVICE);
-            if (poll > 0 && q + 1 < n_launch) {
+            if ((poll > 0 || trace) && q + 1 < n_launch) {
                 HIP_TRY(c, hipMemcpyAsync(c->so_count_host, c->so_count, 4 * 4, hipMemcpyDeviceToHost, s),
                         SBR_EDEVICE);
                 HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
-                if (c->so_count_host[k ^ 1] == 0 && c->so_count_host[3] == 0) break;
+                if (trace) // diagnostics: the fixed point's timeline (live points after each launch)
+                    fprintf(stderr, "sbr_social_trace launch=%d t=%.3f live=%d pool_used=%d pool_live=%d\n", q,
+                                 std::chrono::duration<double>(std::chrono::steady_clock::now() - tr0).count(),
+                                 c->so_count_host[k ^ 1], c->so_count_host[2], c->so_count_host[3]);
+                if (poll > 0 && c->so_count_host[k ^ 1] == 0 && c->so_count_host[3] == 0) break;
             }
         }
         tend(c, s, 1, t0);

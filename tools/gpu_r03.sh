@@ -37,6 +37,8 @@ for s in ${STEPS:-tests smoke bench single}; do
     pmcphase) for fl in 0x100 0x200 0; do run pmcph_$fl 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY --output-format csv -d "$OUT/pmcph_$fl" -o pass -- python3 tools/eq_diag_run.py $fl; done ;;
     socprobe) run socprobe 600 python -u tools/social_step_probe.py ${PROBE_ITERS:-8} && run socprobe_nocoop 600 env SBR_LIB=replication-social-bank-runs_amd/lib_var/nocoop/libsbr.so python -u tools/social_step_probe.py ${PROBE_ITERS:-8} ;;
     socphase) run socphase 600 python -u tools/social_phase_probe.py ${PROBE_ITERS:-8} && run socphase_nocoop 600 env SBR_LIB=replication-social-bank-runs_amd/lib_var/nocoop/libsbr.so python -u tools/social_phase_probe.py ${PROBE_ITERS:-8} ;;
+    soctrace) run soctrace 600 env SBR_SOCIAL_TRACE=1 python -u bench.py --workload social --steps 1 --warmup 0 --no-cpu-baseline ;;
+    soctracevar) run soctrace_$VAR 600 env SBR_SOCIAL_TRACE=1 SBR_LIB=replication-social-bank-runs_amd/lib_var/$VAR/libsbr.so python -u bench.py --workload social --steps 1 --warmup 0 --no-cpu-baseline ;;
     config2) run config2 300 python -u bench.py --workload config2 --steps 20 --warmup 2 ;;
   esac
 done
