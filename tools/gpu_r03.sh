@@ -39,6 +39,8 @@ for s in ${STEPS:-tests smoke bench single}; do
     socphase) run socphase 600 python -u tools/social_phase_probe.py ${PROBE_ITERS:-8} && run socphase_nocoop 600 env SBR_LIB=replication-social-bank-runs_amd/lib_var/nocoop/libsbr.so python -u tools/social_phase_probe.py ${PROBE_ITERS:-8} ;;
     soctrace) run soctrace 600 env SBR_SOCIAL_TRACE=1 python -u bench.py --workload social --steps 1 --warmup 0 --no-cpu-baseline ;;
     soctracevar) run soctrace_$VAR 600 env SBR_SOCIAL_TRACE=1 SBR_LIB=replication-social-bank-runs_amd/lib_var/$VAR/libsbr.so python -u bench.py --workload social --steps 1 --warmup 0 --no-cpu-baseline ;;
+    socdump) run socdump 600 python -u bench.py --workload social --steps 1 --warmup 0 --no-cpu-baseline --social-dump $OUT/social_dump.npz ;;
+    hetvars) for v in ${VARS:-}; do run hetero_$v 600 env SBR_LIB=replication-social-bank-runs_amd/lib_var/$v/libsbr.so python -u bench.py --workload hetero --steps 10 --warmup 2 --phases --no-cpu-baseline; done ;;
     config2) run config2 300 python -u bench.py --workload config2 --steps 20 --warmup 2 ;;
   esac
 done
