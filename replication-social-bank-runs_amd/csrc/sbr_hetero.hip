@@ -832,7 +832,7 @@ __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const d
                                                    const double tolerance, const uint32_t lbits, double& xi_o,
                                                    double& aw_o, double& tol_o, uint32_t& st_o, int& it_o,
                                                    double* tin, double* tout, const bool mono, const int diag,
-                                                   double* __restrict__ aw_path, const double env)
+                                                   double* __restrict__ aw_path, const double env, const bool sep)
 {
     xi_o = NAN; aw_o = NAN; tol_o = INFINITY; it_o = 0;
     const int n = C.n;
@@ -1101,7 +1101,14 @@ __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const d
             for (int k = 0; k < K; k++) {
                 const double bv = (C.T[i1] - xi) + occ[k];
                 double hi = 0.0;
-                if (bv >= 0) {
+                if (sep && occ[k] == xi) {
+                    // b_k(t_i1) = (t_i1 − ξ) + ξ lies within an ulp of t_i1, below t[i1 + 2] (knots
+                    // 2 apart are farther apart than that, `sep`): G_k at the knot after its
+                    // bracket is G_k at a knot <= i1 + 2, no search
+                    const double g = C.g(i1 + 2 < n - 1 ? i1 + 2 : n - 1, k);
+                    hi = g > 0.0 ? g : 0.0;
+                    hb[k] = i1; // with ib = i1 below, the next hint hb + (i − ib) is i itself
+                } else if (bv >= 0) {
                     hb[k] = ssl_near(C.T, n, hb[k] + (i1 - ib), bv);
                     const double g = C.g(hb[k] + 1 < n - 1 ? hb[k] + 1 : n - 1, k);
                     hi = g > 0.0 ? g : 0.0;
@@ -1209,7 +1216,8 @@ __global__ __launch_bounds__(BLOCK, SBR_HET_MINW) void equilibrium_hetero_kernel
     // launched second without a slab); the hot launch carries one copy of the point solve
     if ((MODE == 1 && !fits) || (MODE == 2 && fits)) return;
     __shared__ int s_nonmono;
-    if (threadIdx.x == 0) s_nonmono = a.exhaustive || a.aw_path; // path mode: every knot
+    __shared__ int s_close; // two knots 2 apart closer than 1e-15·t[n−1] (the AW bounds then search)
+    if (threadIdx.x == 0) { s_nonmono = a.exhaustive || a.aw_path; s_close = 0; } // path mode: every knot
     if (fits)
         for (int i = threadIdx.x; i < n; i += BLOCK) smem[i] = gT[i];
     __syncthreads();
@@ -1238,6 +1246,12 @@ __global__ __launch_bounds__(BLOCK, SBR_HET_MINW) void equilibrium_hetero_kernel
                 else if (g1 < g0) { cnt[k]++; dm[k] = dmax(dm[k], g0 - g1); }
             }
         if (nan) s_nonmono = 1;
+        if (fits) {
+            bool close = false;
+            const double sepd = 1e-15 * smem[n - 1];
+            for (int i = threadIdx.x; i + 2 < n; i += BLOCK) close |= !(smem[i + 2] - smem[i] > sepd);
+            if (close) s_close = 1;
+        }
 #pragma unroll
         for (int k = 0; k < K; k++)
             if (cnt[k]) {
@@ -1291,12 +1305,12 @@ __global__ __launch_bounds__(BLOCK, SBR_HET_MINW) void equilibrium_hetero_kernel
         HCol<K, const double*> C{smem, L.G + (size_t)c * cap * K, L.hr + (size_t)c * K * cap, n, L.n_tau[c],
                                  L.n_le[c], cap, eta[c], t_end[c], sums && !a.exhaustive ? hsum : nullptr, nblk};
         solve_hetero_point<K>(C, dl, uj, a.kappa, a.max_iters, a.tolerance, lbits, xi, aw, tol, st, it, tin, tout,
-                              mono, a.diag, a.aw_path, env);
+                              mono, a.diag, a.aw_path, env, fits && s_close == 0);
     } else {
         HCol<K, const double*> C{gT, L.G + (size_t)c * cap * K, L.hr + (size_t)c * K * cap, n, L.n_tau[c],
                                  L.n_le[c], cap, eta[c], t_end[c], nullptr, 0};
         solve_hetero_point<K>(C, dl, uj, a.kappa, a.max_iters, a.tolerance, lbits, xi, aw, tol, st, it, tin, tout,
-                              mono, a.diag, a.aw_path, env);
+                              mono, a.diag, a.aw_path, env, fits && s_close == 0);
     }
     const size_t o = (size_t)c * (size_t)a.n_u + j;
     out.xi[o] = xi;
