@@ -143,16 +143,20 @@ def parse():
     ap.add_argument("--ready", action="store_true",
                     help="--no-pipeline: the per-column readiness schedule (SBR_FLAG_READY_SWEEP) instead of chunks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-verify", action="store_true",
+                    help="skip checking the last timed grid against the oracle (12 sampled columns)")
     ap.add_argument("--cpu-stride", type=int, default=2, help="cpu_baseline samples every k-th β column")
     ap.add_argument("--phases", action="store_true",
                     help="also time the equilibrium kernel stopped after each stage (diagnostic flags)")
-    ap.add_argument("--workload", choices=("baseline", "social", "hetero", "interest", "config1", "config2"),
+    ap.add_argument("--workload", choices=("baseline", "social", "hetero", "interest", "config1", "config2",
+                                           "dropin"),
                     default="baseline",
                     help="baseline: BASELINE config 3 (the metric); social: config 5 per-GPU share; "
                          "hetero: config 4 (K = 8, 1024x1024 per GPU); interest: the interest-rate "
                          "extension on the Fig 5 grid (500x500 per GPU, r = 0.06, delta = 0.1); config1: "
                          "one Fig 3 equilibrium per call (latency); config2: one 500x500 Fig 5 sweep per "
-                         "call with the 5-NaN early exit, host arrays in and out")
+                         "call with the 5-NaN early exit, host arrays in and out; dropin: the unchanged "
+                         "scripts' per-u loops (Fig 4, Fig 5) through the drop-in, latency per call")
     ap.add_argument("--interest-n", type=int, default=500, help="interest: β columns per GPU and u rows")
     ap.add_argument("--hetero-n", type=int, default=1024, help="hetero: columns per GPU and u rows")
     ap.add_argument("--social-cols", type=int, default=64, help="social: β columns per GPU (config 5: 512/8)")
@@ -176,6 +180,8 @@ def main_small(a):
     eng = sbr.Engine(0)
     sys.path.insert(0, str(REPO / "oracle"))
     import oracle as O  # noqa: E402  (test infrastructure: cpu_baseline leg only)
+    if a.workload == "dropin":
+        return main_dropin(a, eng, O)
     if a.workload == "config1":
         args = dict(beta=1.0, eta=15.0, t_end=30.0, u=0.1, p=0.5, kappa=0.6, lam=0.01)
         for _ in range(max(a.warmup, 1)):
@@ -232,9 +238,94 @@ def main_small(a):
     print(json.dumps(res), flush=True)
 
 
+def _unchanged_loop(lr, m, u_vals, nan_threshold=5):
+    """scripts/1_baseline.jl's per-u loop body (Fig 4 :151-192, one Fig 5 column :231-262) through
+    the Python mirror: ModelParameters(m; u=u), solve_equilibrium_baseline(lr, ·),
+    get_AW_functions!, the 5-NaN early termination.  Returns (AW_max list, calls made)."""
+    out, nan_run, calls = [], 0, 0
+    for u in u_vals:
+        if nan_run >= nan_threshold:
+            out.extend([np.nan] * (len(u_vals) - len(out)))
+            break
+        m_u = sbr.ModelParameters.modify(m, u=float(u))
+        r = sbr.solve_equilibrium_baseline(lr, m_u.economic)
+        aw = sbr.get_AW_functions(r)
+        calls += 1
+        if r.bankrun:
+            out.append(aw["AW_max"])
+            nan_run = 0
+        else:
+            out.append(np.nan)
+            nan_run += 1
+    return out, calls
+
+
+def main_dropin(a, eng, O):
+    """The reference's scripts run unchanged on the drop-in (Python mirror of SBRDropIn.jl):
+    Fig 4 = one solve_learning + 5,000 u of solve_equilibrium_baseline(lr, ·) + get_AW_functions!
+    with the 5-NaN early exit (scripts/1_baseline.jl:137-192); each call solves on lr's own knots
+    (sbr_equilibrium_on_knots: knots and HR resident, no learning ODE).  value = microseconds per
+    solve_equilibrium_baseline + get_AW_functions! call, host API (PCIe round trip included).
+    Also timed: the raw C-ABI call (Engine.equilibrium_on_knots with the paths) and the Fig 5
+    500 x 500 loop (:210-267: 500 solve_learning + the per-u calls) end to end."""
+    sbr.engine._default = eng
+    m = sbr.ModelParameters.make(beta=1.0, eta_bar=15.0, u=0.1, p=0.5, kappa=0.6, lam=0.01)
+    u4 = sbr.julia_range("0.001", "0.2", 5000)
+    lr = sbr.solve_learning(m.learning)
+    _unchanged_loop(lr, m, u4[:200])  # warm-up (first-call allocations)
+    reps = max(a.steps // 10, 1)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        aw4, calls4 = _unchanged_loop(lr, m, u4)
+    dt4 = (time.perf_counter() - t0) / reps
+    n_run4 = int(np.isfinite(aw4).sum())
+    cdf = lr.learning_cdf
+    k = 2000
+    t1 = time.perf_counter()
+    for j in range(k):
+        eng.equilibrium_on_knots(cdf.knots, cdf.coefs, 1.0, 15.0, 30.0, float(u4[j % 2700]), 0.5, 0.6, 0.01)
+    raw = (time.perf_counter() - t1) / k
+    # Fig 5 unchanged: per β, ModelParameters(m_base; β=β), solve_learning, then the u loop
+    amt = sbr.julia_range("0.0001", "1", 500)
+    u5 = sbr.julia_range("0.001", "1", 500)
+    t2 = time.perf_counter()
+    calls5, learn5, run5 = 0, 0.0, 0
+    for b in 1.0 / amt:
+        m_b = sbr.ModelParameters.modify(m, beta=float(b))
+        tl = time.perf_counter()
+        lr_b = sbr.solve_learning(m_b.learning)
+        learn5 += time.perf_counter() - tl
+        col, c = _unchanged_loop(lr_b, m_b, u5)
+        calls5 += c
+        run5 += int(np.isfinite(col).sum())
+    dt5 = time.perf_counter() - t2
+    res = {"metric": "unchanged-script drop-in latency: solve_equilibrium_baseline(lr, econ) + get_AW_functions! "
+                     "per call (Fig 4 loop, host API)",
+           "value": dt4 / calls4 * 1e6, "unit": "us per call", "n_gpus": 1, "steps": reps, "warmup": 1,
+           "ms_per_step": dt4 * 1e3, "higher_is_better": False, "scaling": None, "vs_baseline": None,
+           "dtype": "f64", "data": "the reference's Fig 4 / Fig 5 grids (deterministic)",
+           "config": {"workload": "scripts/1_baseline.jl Fig 4 loop (5000 u, 5-NaN early exit) through the Python "
+                                  "mirror on one LearningResults (sbr_equilibrium_on_knots)"},
+           "fig4": {"calls": calls4, "run_points": n_run4, "seconds": dt4},
+           "raw_capi_us_per_call": raw * 1e6,
+           "fig5_500_unchanged": {"seconds": dt5, "solve_learning_seconds": learn5, "calls": calls5,
+                                  "run_points": run5, "us_per_call": (dt5 - learn5) / max(calls5, 1) * 1e6},
+           "libsbr_sha16": lib_sha()}
+    t3 = time.perf_counter()
+    t_, G_, _ = O.learn_logistic(1.0, 30.0)
+    n = 200
+    for j in range(n):
+        O.equilibrium_paths(t_, G_, 1.0, 15.0, 30.0, float(u4[j]), 0.5, 0.6, 0.01)
+    c = (time.perf_counter() - t3 - 0.0) / n
+    res["cpu_baseline"] = {"value": c * 1e6, "unit": "us per call", "cores": 1, "kind": "port", "host": host_info(),
+                           "sample": f"{n} single-point solves on given knots (hazard + buffers + bisection + the "
+                                     "three AW paths) on one core, plus one learning solve"}
+    print(json.dumps(res), flush=True)
+
+
 def main():
     a = parse()
-    if a.workload in ("config1", "config2"):
+    if a.workload in ("config1", "config2", "dropin"):
         return main_small(a)
     if a.workload == "social":
         return main_social(a)
@@ -380,12 +471,43 @@ def main():
     if a.phases:
         res["eq_phase_ms"] = phase_breakdown(eng, beta[0], eta[0], t_end[0], u, p, kappa, lam, x0,
                                              {k: v[0] for k, v in out.items()}, stream, dev)
+    # the timed results checked against the oracle (test infrastructure, after the timed region):
+    # the cpu_baseline leg's columns (every cpu_stride-th, all u) or 12 sampled columns
+    oracle_cols = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline(beta_h, u_h, a.cpu_stride, p, kappa, lam, x0)
+        res["cpu_baseline"], oracle_cols, o_res = cpu_baseline(beta_h, u_h, a.cpu_stride, p, kappa, lam, x0)
+    elif not a.no_verify:
+        oracle_cols = np.sort(np.random.default_rng(rank).choice(nb, min(12, nb), replace=False))
+        o_res = oracle_sweep(beta_h[oracle_cols], u_h, p, kappa, lam, x0)
+    if oracle_cols is not None:
+        res["verified"] = verify_grid(out, last, nb, nu, oracle_cols, o_res)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def oracle_sweep(beta_cols, u_h, p, kappa, lam, x0, nthreads=0):
+    sys.path.insert(0, str(REPO / "oracle"))
+    import oracle as O  # noqa: E402  (test infrastructure: verification leg only)
+
+    O.build()
+    return O.sweep_baseline(beta_cols, 15.0, 30.0, u_h, p, kappa, lam, x0=x0, nthreads=nthreads or usable_cores())
+
+
+def verify_grid(out, k, nb, nu, cols, o) -> dict:
+    """Grid k of the timed run (the last timed step) against the oracle on columns `cols`:
+    every result field, status bit and bisection count, bit for bit."""
+    ok = True
+    for f in sbr.engine.RESULT_FIELDS:
+        g = out[f][k].view(nb, nu)[torch.as_tensor(cols, device=out[f].device)].cpu().numpy()
+        ok &= bool(np.all((g == o[f]) | (np.isnan(g) & np.isnan(o[f]))))
+    st = out["status"][k].view(nb, nu)[torch.as_tensor(cols, device=out["status"].device)].cpu().numpy()
+    ok &= bool(np.array_equal(st.view(np.uint32), o["status"]))
+    it = out["iters"][k].view(nb, nu)[torch.as_tensor(cols, device=out["iters"].device)].cpu().numpy()
+    ok &= bool(np.array_equal(it, o["iters"]))
+    return {"bitwise_equal_oracle": ok, "grid": "last timed step", "columns": int(len(cols)),
+            "points": int(len(cols) * nu)}
 
 
 def main_hetero(a):
@@ -822,20 +944,19 @@ def phase_breakdown(eng, beta, eta, t_end, u, p, kappa, lam, x0, out, stream, de
 
 def cpu_baseline(beta_h, u_h, stride, p, kappa, lam, x0):
     """The CPU oracle (C restatement, same algorithm, OpenMP over β columns) on a
-    bounded sample of the same workload: every `stride`-th β column, all u."""
-    sys.path.insert(0, str(REPO / "oracle"))
-    import oracle as O  # noqa: E402  (test infrastructure: cpu_baseline leg only)
-
-    O.build()
+    bounded sample of the same workload: every `stride`-th β column, all u.  Returns the
+    baseline block, the sampled column indices and the oracle's results on them."""
     cores = usable_cores()
-    cols = beta_h[::stride]
+    idx = np.arange(0, len(beta_h), stride)
+    cols = beta_h[idx]
+    oracle_sweep(cols[:1], u_h[:4], p, kappa, lam, x0, nthreads=1)  # build / load outside the clock
     t0 = time.perf_counter()
-    O.sweep_baseline(cols, 15.0, 30.0, u_h, p, kappa, lam, x0=x0, nthreads=cores)
+    o = oracle_sweep(cols, u_h, p, kappa, lam, x0, nthreads=cores)
     dt = time.perf_counter() - t0
     pts = len(cols) * len(u_h)
-    return {"value": pts / dt, "unit": "equilibria/s", "cores": cores, "kind": "port", "host": host_info(),
-            "sample": f"{len(cols)} β columns (every {stride}th of the {len(beta_h)}) x {len(u_h)} u = {pts} "
-                      f"equilibria in {dt:.2f} s"}
+    return ({"value": pts / dt, "unit": "equilibria/s", "cores": cores, "kind": "port", "host": host_info(),
+             "sample": f"{len(cols)} β columns (every {stride}th of the {len(beta_h)}) x {len(u_h)} u = {pts} "
+                       f"equilibria in {dt:.2f} s"}, idx, o)
 
 
 if __name__ == "__main__":

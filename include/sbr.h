@@ -60,7 +60,7 @@ typedef struct {
  * solved it, and one equilibrium workgroup per column (on CUs the learning waves do not
  * use) runs its hazard and equilibria.  Same results; slower on the configs (the columns'
  * learning ends late and the equilibria lose the learning CUs), kept for A/B. */
-#define SBR_FLAG_READY_SWEEP 0x2
+#define SBR_FLAG_READY_SWEEP 0x2 /* a timed-out wait marks every point SBR_ENGINE_SCHED (_dev) / SBR_EDEVICE (host) */
 /* Diagnostics (timing breakdown only — results are NOT the reference's):
  * stop every point after the crossing scan / after the ξ bisection, or
  * report the number of 64-knot AW blocks evaluated in `iters` instead of
@@ -181,6 +181,28 @@ int sbr_learn_baseline(sbr_ctx* ctx, const double* beta, const double* eta, cons
 int sbr_solve_point_paths(sbr_ctx* ctx, double beta, double eta, double t_end, double x0, double u, double p,
                           double kappa, double lambda, const sbr_opts* opts, double* res, uint32_t* status,
                           double* tau, double* hr, double* aw_cum, int64_t cap, int64_t* n_tau);
+
+/*
+ * Equilibria on the caller's learning knots — for one LearningResults `lr` and n_u values of u
+ * sharing (p, κ, λ, η):
+ *     r = solve_equilibrium_baseline(lr, EconomicParameters(u_j, p, κ, λ, η_bar, η))  solver.jl:413-462
+ *     get_AW_functions!(r)                                                        solver.jl:553-576
+ * with lr's own knot grid — t, G = the knots and values of lr.learning_cdf (learning.jl:52),
+ * beta = lr.params.β for the symbolic pdf βG(1−G) (learning.jl:161-173), t_end =
+ * lr.params.tspan[2] (optimal_buffer's no-crossing value, solver.jl:221-223, 424) — and no
+ * learning ODE: the scripts learn once per β and call this per u (1_baseline.jl:44 / :169,
+ * :227 / :248).  The knots and the u-independent hazard path stay resident on the device: a
+ * call whose t, G (compared by value), β, η, p and λ equal the previous call's uploads only u.
+ * Lookups outside [t[0], t[n−1]] are the interpolant's BoundsError (SBR_OOB); t must be sorted
+ * (SBR_EARG otherwise, like Interpolations).  Results: n_u entries per out field (host).
+ * Paths (each may be NULL; capacity cap): tau / hr = the hazard grid τ̄ and HR(τ̄) (*n_tau
+ * entries, 0 after the hazard's BoundsError); with n_u == 1, aw_cum / aw_out / aw_in =
+ * AW_cum, AW_OUT, AW_IN on τ̄ (get_AW, solver.jl:495-532; NaN without a run).  Synchronous.
+ */
+int sbr_equilibrium_on_knots(sbr_ctx* ctx, const double* t, const double* G, int64_t n_knots, double beta,
+                             double eta, double t_end, const double* u, int64_t n_u, double p, double kappa,
+                             double lambda, const sbr_opts* opts, sbr_result_soa* out, double* tau, double* hr,
+                             double* aw_cum, double* aw_out, double* aw_in, int64_t cap, int64_t* n_tau);
 
 /*
  * Heterogeneity extension sweep — for each column c (group rates
@@ -345,6 +367,11 @@ void sbr_apply_early_exit(int64_t n_beta, int64_t n_u, int32_t threshold, sbr_re
  * sbr_social_overflow_stats) return SBR_EARG on an n-device context: call them
  * on sbr_multi_child(ctx, rank). */
 int sbr_timing_enable(sbr_ctx* ctx, int on);
+/* The schedule the last single sweep (sbr_sweep_baseline[_dev]) on this device took: 1 = the
+ * per-column readiness schedule (SBR_FLAG_READY_SWEEP granted), 0 = the chunked default (also
+ * when the flag was given but the device could not run it: fewer than 256 CUs, or stream
+ * creation failed). */
+int sbr_last_schedule(sbr_ctx* ctx, int32_t* schedule);
 int sbr_timing_read(sbr_ctx* ctx, void* stream, double* learn_ms, double* eq_ms, int32_t* n_calls);
 
 /* Per-β learning statistics of the last sweep (knots stored, τ̄-grid length,

@@ -29,6 +29,8 @@
 #define SBR_KNOT_OVERFLOW       0x2000u /* engine knot capacity exceeded (engine limit)        */
 #define SBR_ODE_FAILED          0x4000u /* non-finite step size / state                        */
 #define SBR_ENGINE_TRUNC        0x8000u /* engine bug: lookup past a truncated knot grid       */
+#define SBR_ENGINE_SCHED       0x10000u /* engine bug: a readiness-schedule workgroup timed out
+                                            waiting; every point of that sweep is unsolved     */
 
 /* OrdinaryDiffEqCore __init: maxiters = anyadaptive(alg) ? 1000000 : typemax(Int).
  * Every loop iteration (accepted or rejected step) counts. */

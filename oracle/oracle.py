@@ -41,6 +41,8 @@ def lib() -> ctypes.CDLL:
         L.sbro_learn_logistic.argtypes = [_D, _D, _D, _D, _D, _D, _I64, _P, _P, _I64, _P]
         L.sbro_equilibrium.restype = None
         L.sbro_equilibrium.argtypes = [_P, _P, _I64, _D, _D, _D, _D, _D, _D, _D, _I32, _P, _P, _P, _P, _P, _P, _P]
+        L.sbro_equilibrium_paths.restype = None
+        L.sbro_equilibrium_paths.argtypes = [_P, _P, _I64, _D, _D, _D, _D, _D, _D, _D, _I32] + [_P] * 9
         L.sbro_sweep_baseline.restype = ctypes.c_int
         L.sbro_sweep_baseline.argtypes = [_P, _P, _P, _D, _P, _I64, _I64, _D, _D, _D, _I32, _I32] + [_P] * 8
         L.sbro_apply_early_exit.restype = None
@@ -91,6 +93,27 @@ def equilibrium(t, G, beta, eta, t_end, u, p, kappa, lam, max_iters=100, paths=F
     if paths:
         k = int(nhr[0])
         out.update(hr_tau=hr_tau[:k], hr=hr_v[:k], aw=aw[:k])
+    return out
+
+
+def equilibrium_paths(t, G, beta, eta, t_end, u, p, kappa, lam, max_iters=100):
+    """solve_equilibrium_baseline on caller knots with get_AW's three paths (AW_cum, AW_OUT,
+    AW_IN on the hazard grid; n_hr = 0 after the hazard's BoundsError)."""
+    t = np.ascontiguousarray(t, np.float64)
+    G = np.ascontiguousarray(G, np.float64)
+    n = len(t)
+    res = np.zeros(5)
+    st = np.zeros(1, np.uint32)
+    it = np.zeros(1, np.int32)
+    bufs = [np.full(n + 1, np.nan) for _ in range(5)]
+    nhr = np.zeros(1, np.int64)
+    lib().sbro_equilibrium_paths(_ptr(t), _ptr(G), n, beta, eta, t_end, u, p, kappa, lam, max_iters, _ptr(res),
+                                 _ptr(st), _ptr(it), *[_ptr(b) for b in bufs], _ptr(nhr))
+    k = int(nhr[0])
+    out = dict(xi=res[0], tau_in_unc=res[1], tau_out_unc=res[2], aw_max=res[3], tol=res[4], status=int(st[0]),
+               iters=int(it[0]), n_hr=k)
+    for name, b in zip(("hr_tau", "hr", "aw_cum", "aw_out", "aw_in"), bufs):
+        out[name] = b[:k]
     return out
 
 

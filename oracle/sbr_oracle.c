@@ -727,8 +727,8 @@ static uint32_t compute_xi(double tin, double tout, const double* t, const doubl
 /* ------------------------------------------------------------------------ */
 /* get_AW on the HR grid + AW_max (solver.jl:495-532, 565)                  */
 /* ------------------------------------------------------------------------ */
-static double get_aw(double xi, double tin, double tout, const double* tau, int64_t n_tau, const double* t,
-                     const double* G, int64_t n, double* aw_path, int* oob)
+static double get_aw3(double xi, double tin, double tout, const double* tau, int64_t n_tau, const double* t,
+                      const double* G, int64_t n, double* aw_path, double* aw_out_path, double* aw_in_path, int* oob)
 {
     double ic = (tin >= xi) ? xi : tin;
     double oc = (tout > xi) ? xi : tout;
@@ -743,9 +743,17 @@ static double get_aw(double xi, double tin, double tout, const double* tau, int6
         double awout = b >= 0 ? go : 0.0;
         double v = (awout - awin) + G0;
         if (aw_path) aw_path[i] = v;
+        if (aw_out_path) aw_out_path[i] = awout;
+        if (aw_in_path) aw_in_path[i] = awin;
         if (mx == mx && (v != v || v > mx)) mx = v; /* NaN-propagating max (Julia maximum) */
     }
     return mx;
+}
+
+static double get_aw(double xi, double tin, double tout, const double* tau, int64_t n_tau, const double* t,
+                     const double* G, int64_t n, double* aw_path, int* oob)
+{
+    return get_aw3(xi, tin, tout, tau, n_tau, t, G, n, aw_path, NULL, NULL, oob);
 }
 
 /* ------------------------------------------------------------------------ */
@@ -757,8 +765,9 @@ typedef struct {
     int32_t iters;
 } point_t;
 
-static void equilibrium_point(const double* t, const double* G, int64_t n, const hazard_t* h, double t_end,
-                              double u, double kappa, int32_t max_iters, point_t* r, double* aw_path)
+static void equilibrium_point3(const double* t, const double* G, int64_t n, const hazard_t* h, double t_end,
+                               double u, double kappa, int32_t max_iters, point_t* r, double* aw_path,
+                               double* aw_out_path, double* aw_in_path)
 {
     memset(r, 0, sizeof(*r));
     r->xi = NAN;
@@ -775,7 +784,7 @@ static void equilibrium_point(const double* t, const double* G, int64_t n, const
     uint32_t s = compute_xi(r->tin, r->tout, t, G, n, kappa, max_iters, &xi, &tol, &r->iters);
     if (s != SBR_RUN) { r->status = s; return; }
     int oob = 0;
-    double mx = get_aw(xi, r->tin, r->tout, h->tau, h->n, t, G, n, aw_path, &oob);
+    double mx = get_aw3(xi, r->tin, r->tout, h->tau, h->n, t, G, n, aw_path, aw_out_path, aw_in_path, &oob);
     if (oob) { r->status = SBR_OOB; return; }
     r->xi = xi;
     r->tol = tol;
@@ -783,7 +792,35 @@ static void equilibrium_point(const double* t, const double* G, int64_t n, const
     r->status = SBR_RUN | SBR_CONVERGED;
 }
 
-/* public single-point API on caller-provided knots (used by tests) */
+static void equilibrium_point(const double* t, const double* G, int64_t n, const hazard_t* h, double t_end,
+                              double u, double kappa, int32_t max_iters, point_t* r, double* aw_path)
+{
+    equilibrium_point3(t, G, n, h, t_end, u, kappa, max_iters, r, aw_path, NULL, NULL);
+}
+
+/* public single-point API on caller-provided knots (used by tests): solve_equilibrium_baseline on a
+ * LearningResults' knots (solver.jl:413-462) + get_AW's three paths (solver.jl:495-532) */
+void sbro_equilibrium_paths(const double* t, const double* G, int64_t n, double beta, double eta, double t_end,
+                            double u, double p, double kappa, double lambda, int32_t max_iters, double* res,
+                            uint32_t* status, int32_t* iters, double* hr_tau, double* hr_v, double* aw,
+                            double* aw_out, double* aw_in, int64_t* n_hr)
+{
+    double* g = (double*)malloc((size_t)n * sizeof(double));
+    for (int64_t i = 0; i < n; i++) g[i] = (beta * G[i]) * (1.0 - G[i]);
+    hazard_t h;
+    hazard_rate(t, g, n, p, lambda, eta, 0, &h);
+    point_t r;
+    equilibrium_point3(t, G, n, &h, t_end, u, kappa, max_iters, &r, aw, aw_out, aw_in);
+    res[0] = r.xi; res[1] = r.tin; res[2] = r.tout; res[3] = r.aw_max; res[4] = r.tol;
+    *status = r.status;
+    *iters = r.iters;
+    if (n_hr) *n_hr = h.oob ? 0 : h.n;
+    if (hr_tau && !h.oob) memcpy(hr_tau, h.tau, (size_t)h.n * sizeof(double));
+    if (hr_v && !h.oob) memcpy(hr_v, h.hr, (size_t)h.n * sizeof(double));
+    hazard_free(&h);
+    free(g);
+}
+
 void sbro_equilibrium(const double* t, const double* G, int64_t n, double beta, double eta, double t_end,
                       double u, double p, double kappa, double lambda, int32_t max_iters, double* res,
                       uint32_t* status, int32_t* iters, double* hr_tau, double* hr_v, double* aw, int64_t* n_hr)

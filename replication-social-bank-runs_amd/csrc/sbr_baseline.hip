@@ -1242,12 +1242,44 @@ __device__ __forceinline__ void solve_interest_point(P T, P G, P H, const Summ& 
 // The equilibria of u values [j0, j1) of column b by one workgroup of BLOCK threads (smem:
 // the dynamic LDS slab of launch_equilibrium's size).  Starts and ends uniformly; the caller
 // puts a barrier between two calls on the same workgroup (the LDS slab and flags are reused).
-template <int BLOCK, bool INTEREST, int MODE = 0>
+// get_AW (solver.jl:495-532) of a run point on the whole τ̄ grid, written by the BLOCK threads
+// of a workgroup (τ̄ entry i by thread i mod BLOCK): AW_cum, and AW_OUT / AW_IN when asked.
+// Every entry is the exhaustive path's arithmetic (eval_range: bracket k = min(searchsortedlast,
+// n − 2), the same lerp and masks), searched afresh instead of slid, so the values are the same
+// bits; the point's AW_max came from its own (scan / branch-and-bound) solve.  Called only for a
+// run point, whose every lookup was range-checked by that solve.
+template <int BLOCK, class P>
+__device__ __forceinline__ void aw_paths_coop(P T, P G, const int n, const int ntau, const int nle,
+                                              const double ETA, const double xi, const double tin,
+                                              const double tout, double* __restrict__ aw_cum,
+                                              double* __restrict__ aw_out, double* __restrict__ aw_in)
+{
+    const double icc = (tin >= xi) ? xi : tin;
+    const double occ = (tout > xi) ? xi : tout;
+    const double G0 = lerp_at(T, G, n, ssl_range(T, 0, n - 1, 0.0), 0.0);
+    for (int i = threadIdx.x; i < ntau; i += BLOCK) {
+        const double ti = i < nle ? T[i] : ETA;
+        const double av = (ti - xi) + icc;
+        const double bv = (ti - xi) + occ;
+        const double xa = av > 0 ? av : 0.0;
+        const double xb = bv > 0 ? bv : 0.0;
+        const double gi = lerp_at(T, G, n, ssl_range(T, 0, n - 1, xa), xa);
+        const double go = lerp_at(T, G, n, ssl_range(T, 0, n - 1, xb), xb);
+        const double awin = av >= 0 ? gi : 0.0;
+        const double awout = bv >= 0 ? go : 0.0;
+        aw_cum[i] = (awout - awin) + G0;
+        if (aw_out) aw_out[i] = awout;
+        if (aw_in) aw_in[i] = awin;
+    }
+}
+
+template <int BLOCK, bool INTEREST, int MODE = 0, bool PATHS = false>
 __device__ __forceinline__ void eq_column(const int b, const int j0, const int j1, const LearnBufs& L,
                                           const double* __restrict__ eta, const double* __restrict__ t_end,
                                           const double* __restrict__ u, const EqArgs& a, const InterestArgs& ia,
                                           const ResultSoA& out, double* smem)
 {
+    static_assert(!(PATHS && INTEREST), "the interest mode writes its AW path from the solving lane");
     const int n = L.n_knots[b], ntau = L.n_tau[b], nle = L.n_le[b];
     const uint32_t lst = L.status[b];
     const size_t row = (size_t)b * (size_t)L.cap;
@@ -1279,9 +1311,15 @@ __device__ __forceinline__ void eq_column(const int b, const int j0, const int j
     __shared__ int s_ndec;                 // decreases of G between consecutive knots
     __shared__ unsigned long long s_maxdec; // largest decrease (bits of a nonnegative double)
     __shared__ double s_thalf;
+    // path mode: the point j0's outcome, for the workgroup's get_AW pass after the point loop
+    __shared__ double s_pxi, s_ptin, s_ptout;
+    __shared__ uint32_t s_pst;
     // every shared flag is initialised before the first barrier: lanes >= nq set
     // s_nonmono right after it, so a later store by thread 0 could clear their flag
-    if (threadIdx.x == 0) { eq_next = 0; s_nonmono = 0; s_noscan = 0; s_ndec = 0; s_maxdec = 0; s_thalf = NAN; }
+    if (threadIdx.x == 0) {
+        eq_next = 0; s_nonmono = 0; s_noscan = 0; s_ndec = 0; s_maxdec = 0; s_thalf = NAN;
+        if (PATHS) s_pst = 0;
+    }
     if (fits) {
         for (int i = threadIdx.x; i < n; i += BLOCK) { sT[i] = gT[i]; sG[i] = gG[i]; }
         if (INTEREST)
@@ -1380,7 +1418,8 @@ __device__ __forceinline__ void eq_column(const int b, const int j0, const int j
         __syncthreads();
         const double dd = (double)s_ndec * sbr_bitsd(s_maxdec); // ≥ the largest drawdown
         S = Summ{hmax, hmin, pmc, smc, s_nonmono == 0, s_thalf,
-                 !s_noscan && dd <= 1e-12 && sG[0] >= 0.0 && sG[n - 1] <= 2.0, dd, s_nonmono == 0 || s_noscan != 0};
+                 n >= 2 && !s_noscan && dd <= 1e-12 && sG[0] >= 0.0 && sG[n - 1] <= 2.0, dd,
+                 s_nonmono == 0 || s_noscan != 0};
     }
     // Points are handed out to waves 64 at a time from an LDS counter, so a
     // wave that drew cheap no-run points goes back for more instead of idling
@@ -1391,7 +1430,7 @@ __device__ __forceinline__ void eq_column(const int b, const int j0, const int j
     const double ETA = eta[b], T1 = t_end[b];
     const uint32_t lbits = lst & (SBR_ODE_MAXITERS | SBR_STIFF_SWITCH | SBR_ODE_FAILED | SBR_KNOT_OVERFLOW);
     const bool bad_col = (lst & (SBR_ARG_INVALID | SBR_OOB)) || n < 2;
-    const bool trunc = n >= 2 && gT[n - 1] < T1;
+    const bool trunc = !a.full_grid && n >= 2 && gT[n - 1] < T1;
     for (;;) {
         int base = 0;
         if (lane == 0) base = atomicAdd(&eq_next, 64);
@@ -1415,10 +1454,12 @@ __device__ __forceinline__ void eq_column(const int b, const int j0, const int j
                                      r, vsteps, a.aw_path, a.diag);
         } else if (MODE != 2 && fits) {
             solve_point((const double*)sT, (const double*)sG, cH, S, n, ntau, nle, ETA, T1, trunc, uj, a.kappa,
-                        a.max_iters, lbits, r, a.aw_path, a.diag);
+                        a.max_iters, lbits, r, PATHS ? nullptr : a.aw_path, a.diag);
         } else if (MODE != 1) {
-            solve_point(gT, gG, gH, S, n, ntau, nle, ETA, T1, trunc, uj, a.kappa, a.max_iters, lbits, r, a.aw_path, a.diag);
+            solve_point(gT, gG, gH, S, n, ntau, nle, ETA, T1, trunc, uj, a.kappa, a.max_iters, lbits, r,
+                        PATHS ? nullptr : a.aw_path, a.diag);
         }
+        if (PATHS && j == j0) { s_pxi = r.xi; s_ptin = r.tin; s_ptout = r.tout; s_pst = r.status; }
         const size_t o = (size_t)b * (size_t)a.n_u + j;
         if (INTEREST && ia.steps) ia.steps[o] = vsteps;
         out.xi[o] = r.xi;
@@ -1428,6 +1469,17 @@ __device__ __forceinline__ void eq_column(const int b, const int j0, const int j
         out.tol[o] = r.tol;
         out.status[o] = r.status;
         if (out.iters) out.iters[o] = r.iters;
+    }
+    if constexpr (PATHS) {
+        __syncthreads();
+        if ((s_pst & SBR_RUN) && a.aw_path) {
+            if (fits)
+                aw_paths_coop<BLOCK>((const double*)sT, (const double*)sG, n, ntau, nle, ETA, s_pxi, s_ptin, s_ptout,
+                                     a.aw_path, a.aw_out_path, a.aw_in_path);
+            else
+                aw_paths_coop<BLOCK>(gT, gG, n, ntau, nle, ETA, s_pxi, s_ptin, s_ptout, a.aw_path, a.aw_out_path,
+                                     a.aw_in_path);
+        }
     }
 }
 
@@ -1439,7 +1491,7 @@ __device__ unsigned long long g_wgtime[2 * kWgTimeMax];
 __device__ unsigned int g_wghw[2 * kWgTimeMax];
 #endif
 
-template <int BLOCK, bool INTEREST, int MODE>
+template <int BLOCK, bool INTEREST, int MODE, bool PATHS = false>
 __global__ __launch_bounds__(BLOCK, INTEREST ? 1 : SBR_EQ_MINW) void equilibrium_kernel(LearnBufs L, const double* __restrict__ eta,
                                                             const double* __restrict__ t_end,
                                                             const double* __restrict__ u, EqArgs a, InterestArgs ia,
@@ -1455,7 +1507,7 @@ __global__ __launch_bounds__(BLOCK, INTEREST ? 1 : SBR_EQ_MINW) void equilibrium
 #ifdef SBR_EQ_WGTIME
     const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
 #endif
-    eq_column<BLOCK, INTEREST, MODE>(b, j0, j1, L, eta, t_end, u, a, ia, out, smem);
+    eq_column<BLOCK, INTEREST, MODE, PATHS>(b, j0, j1, L, eta, t_end, u, a, ia, out, smem);
 #ifdef SBR_EQ_WGTIME
     __syncthreads();
     const size_t wg = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
@@ -1561,8 +1613,15 @@ hipError_t launch_learn_logistic(const double* beta, const double* eta, const do
     return hipGetLastError();
 }
 
+hipError_t launch_hazard(const double* beta, const double* eta, const LearnArgs& a, const LearnBufs& L, int n_beta,
+                         hipStream_t s)
+{
+    hipLaunchKernelGGL(hazard_kernel, dim3(n_beta), dim3(HZ_BLOCK), 0, s, beta, eta, a, L);
+    return hipGetLastError();
+}
+
 hipError_t launch_equilibrium(const LearnBufs& L, const double* eta, const double* t_end, const double* u,
-                              const EqArgs& a, const ResultSoA& out, int n_beta, hipStream_t s)
+                              const EqArgs& a, const ResultSoA& out, int n_beta, hipStream_t s, int only_mode)
 {
     const size_t lds = ((size_t)2 * a.lds_cap + 2 * ((a.lds_cap >> 6) + 1) + 2 * ((a.lds_cap >> 3) + 1)) * sizeof(double);
     // one block per (β column, tile of EQ_TILE u values); block size by tile width.  Wide
@@ -1574,10 +1633,12 @@ hipError_t launch_equilibrium(const LearnBufs& L, const double* eta, const doubl
     // the LDS-resident columns, then (a workgroup per column, exiting at once where it fits, no
     // LDS slab) the columns beyond the slab on the global-memory path
     auto go = [&](auto k1, auto k2, int bs) {
-        hipLaunchKernelGGL(k1, grid, dim3(bs), lds, s, L, eta, t_end, u, a, none, out);
-        hipLaunchKernelGGL(k2, grid, dim3(bs), 0, s, L, eta, t_end, u, a, none, out);
+        if (only_mode != 2) hipLaunchKernelGGL(k1, grid, dim3(bs), lds, s, L, eta, t_end, u, a, none, out);
+        if (only_mode != 1) hipLaunchKernelGGL(k2, grid, dim3(bs), 0, s, L, eta, t_end, u, a, none, out);
     };
-    if (w > 256)
+    if (a.aw_path) // path mode (n_u == 1): one wave solves the point, then writes the paths
+        go(equilibrium_kernel<64, false, 1, true>, equilibrium_kernel<64, false, 2, true>, 64);
+    else if (w > 256)
         go(equilibrium_kernel<SBR_EQ_WIDE, false, 1>, equilibrium_kernel<SBR_EQ_WIDE, false, 2>, SBR_EQ_WIDE);
     else if (w > 64)
         go(equilibrium_kernel<256, false, 1>, equilibrium_kernel<256, false, 2>, 256);
@@ -1596,6 +1657,24 @@ hipError_t launch_eq_ready(const LearnBufs& L, const double* beta, const double*
     (void)n_blocks; // one workgroup per item
     hipLaunchKernelGGL(eq_ready_kernel, dim3(ra.n_items), dim3(SBR_EQ_WIDE), lds, s, L, beta, eta, t_end, u, la, a, ra,
                        out);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void ready_fail_kernel(const int32_t* __restrict__ gave_up, ResultSoA out,
+                                                          int64_t n_pts)
+{
+    if (__hip_atomic_load(gave_up, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n_pts; i += (int64_t)gridDim.x * 256) {
+        out.xi[i] = NAN;
+        out.aw_max[i] = NAN;
+        out.tol[i] = INFINITY;
+        out.status[i] = SBR_ENGINE_SCHED;
+    }
+}
+
+hipError_t launch_ready_fail(const int32_t* gave_up, const ResultSoA& out, int64_t n_pts, hipStream_t s)
+{
+    hipLaunchKernelGGL(ready_fail_kernel, dim3(256), dim3(256), 0, s, gave_up, out, n_pts);
     return hipGetLastError();
 }
 

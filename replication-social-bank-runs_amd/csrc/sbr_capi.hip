@@ -97,6 +97,17 @@ struct sbr_ctx {
     // host-API staging
     void* stage = nullptr;
     size_t stage_bytes = 0;
+    // sbr_equilibrium_on_knots: the caller's knot grid and its hazard path stay resident between
+    // calls, keyed by value (n, t, G and β, η, p, λ); the device block and its pinned host mirror
+    // share one layout (KnotLayout), so each transfer is one contiguous copy
+    char* kn_dev = nullptr;
+    char* kn_pin = nullptr;
+    size_t kn_cap_k = 0, kn_cap_u = 0;
+    bool kn_valid = false;
+    int64_t kn_n = 0;
+    double kn_key[4] = {};
+    std::vector<double> kn_t, kn_G, kn_hr; // host copies of the resident knots and HR
+    int32_t kn_m = 0, kn_ntau = 0;         // knots <= η; τ̄ entries (0: the hazard's BoundsError)
     int lds_cap = 0, lds_cap_b = 0;
     int lds_smem = 0;
     // kernel timing (HIP event pairs on the launching stream), opt-in via sbr_timing_enable
@@ -536,6 +547,9 @@ int run_baseline_ready(sbr_ctx* c, hipStream_t s, const double* beta, const doub
     HIP_TRY(c, hipEventRecord(c->ev_re, c->rs_eq), SBR_EDEVICE);
     HIP_TRY(c, hipStreamWaitEvent(s, c->ev_rl, 0), SBR_EDEVICE);
     HIP_TRY(c, hipStreamWaitEvent(s, c->ev_re, 0), SBR_EDEVICE);
+    // a workgroup that gave up left its tile unwritten: mark the whole sweep on the device, so a
+    // *_dev caller sees it in the results (the host-pointer entry point also returns SBR_EDEVICE)
+    HIP_TRY(c, sbr::launch_ready_fail(q + 1, out, n_beta * n_u, s), SBR_EDEVICE);
     return SBR_OK;
 }
 
@@ -785,6 +799,8 @@ int sbr_free(sbr_ctx* c)
         if (e) (void)hipEventDestroy(e);
     if (c->rq) (void)hipFree(c->rq);
     if (c->stage) (void)hipFree(c->stage);
+    if (c->kn_dev) (void)hipFree(c->kn_dev);
+    if (c->kn_pin) (void)hipHostFree(c->kn_pin);
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->ev_grid) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(c->stream);
@@ -1160,6 +1176,177 @@ int sbr_solve_point_paths(sbr_ctx* c, double beta, double eta, double t_end, dou
         (void)nk;
         return SBR_OK;
     });
+}
+
+}  // extern "C"
+
+namespace {
+
+// byte offsets of sbr_equilibrium_on_knots' device block (and of its pinned mirror) for ck knots
+// and cu u values: [counters | β, η | t, G (packed by the call's n) | HR | t_end, u | results, paths]
+struct KnotLayout {
+    size_t sc, tg, hr, u, res, bytes;
+    KnotLayout(size_t ck, size_t cu)
+    {
+        sc = 64;
+        tg = 128;
+        hr = tg + 16 * ck;
+        u = hr + 8 * (ck + 8);
+        res = u + 8 * (cu + 8);
+        bytes = res + 8 * (6 * cu + 3 * (ck + 1)) + 256;
+    }
+};
+
+int ensure_knots(sbr_ctx* c, size_t n, size_t n_u)
+{
+    if (n <= c->kn_cap_k && n_u <= c->kn_cap_u) return SBR_OK;
+    size_t ck = c->kn_cap_k > 4096 ? c->kn_cap_k : 4096, cu = c->kn_cap_u > 64 ? c->kn_cap_u : 64;
+    while (ck < n) ck *= 2;
+    while (cu < n_u) cu *= 2;
+    if (c->kn_dev) (void)hipFree(c->kn_dev);
+    if (c->kn_pin) (void)hipHostFree(c->kn_pin);
+    c->kn_dev = c->kn_pin = nullptr;
+    c->kn_cap_k = c->kn_cap_u = 0;
+    c->kn_valid = false;
+    const KnotLayout K(ck, cu);
+    HIP_TRY(c, hipMalloc(&c->kn_dev, K.bytes), SBR_ENOMEM);
+    HIP_TRY(c, hipHostMalloc(&c->kn_pin, K.bytes), SBR_ENOMEM);
+    c->kn_cap_k = ck;
+    c->kn_cap_u = cu;
+    return SBR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sbr_equilibrium_on_knots(sbr_ctx* c, const double* t, const double* G, int64_t n, double beta, double eta,
+                             double t_end, const double* u, int64_t n_u, double p, double kappa, double lambda,
+                             const sbr_opts* opts, sbr_result_soa* out, double* tau, double* hr, double* aw_cum,
+                             double* aw_out, double* aw_in, int64_t cap, int64_t* n_tau)
+{
+    SBR_ON_RANK0(c, sbr_equilibrium_on_knots(c, t, G, n, beta, eta, t_end, u, n_u, p, kappa, lambda, opts, out, tau, hr, aw_cum, aw_out, aw_in, cap, n_tau));
+    if (!c || !t || !G || !u || !out) return SBR_EARG;
+    if (n < 1 || n > (1 << 26) || n_u < 1 || n_u > (1 << 24)) return fail(c, SBR_EARG, "knot / u count");
+    if (!scalars_valid(0.0, p, kappa, lambda) || !(beta > 0) || !(eta > 0) || !(t_end > 0))
+        return fail(c, SBR_EARG, "ArgumentError: beta/eta/t_end/p/kappa/lambda");
+    for (int64_t j = 0; j < n_u; j++)
+        if (!(u[j] >= 0.0)) return fail(c, SBR_EARG, "ArgumentError: u must be non-negative");
+    // Interpolations' gridded knots must be sorted (and not NaN)
+    if (!(t[0] == t[0])) return fail(c, SBR_EARG, "ArgumentError: knots must be sorted");
+    for (int64_t i = 0; i + 1 < n; i++)
+        if (!(t[i] <= t[i + 1])) return fail(c, SBR_EARG, "ArgumentError: knots must be sorted");
+    const bool want_aw = aw_cum || aw_out || aw_in;
+    if (want_aw && n_u != 1) return fail(c, SBR_EARG, "AW paths need n_u == 1");
+    if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
+    const sbr_opts o = resolve(opts);
+    int rc = ensure_knots(c, (size_t)n, (size_t)n_u);
+    if (rc) return rc;
+    const KnotLayout K(c->kn_cap_k, c->kn_cap_u);
+    // the hazard grid as solver.jl:155-161 builds it (knots are sorted: the .<= η mask is a
+    // prefix), and its BoundsError: pdf(η) outside [t_1, t_n]
+    int64_t m = 0;
+    while (m < n && t[m] <= eta) m++;
+    const bool push = m == 0 || t[m - 1] != eta;
+    const bool hz_oob = m < n ? m == 0 : push;
+    const int64_t ntau = hz_oob ? 0 : m + (push ? 1 : 0);
+    if ((tau || hr || want_aw) && ntau > cap) return fail(c, SBR_EARG, "path capacity too small");
+    const double key[4] = {beta, eta, p, lambda};
+    const bool hit = c->kn_valid && c->kn_n == n && memcmp(c->kn_key, key, sizeof key) == 0 &&
+                     memcmp(c->kn_t.data(), t, (size_t)n * 8) == 0 && memcmp(c->kn_G.data(), G, (size_t)n * 8) == 0;
+    char* D = c->kn_dev;
+    char* H = c->kn_pin;
+    int32_t* dcnt = (int32_t*)D; // n_knots, n_tau, n_le, status, n_accept, n_reject
+    double* dsc = (double*)(D + K.sc);
+    double* dtg = (double*)(D + K.tg);
+    const sbr::LearnBufs L{dtg, dtg + n, (double*)(D + K.hr), nullptr, dcnt, dcnt + 1, dcnt + 2,
+                           (uint32_t*)(dcnt + 3), dcnt + 4, dcnt + 5, (int32_t)c->kn_cap_k};
+    double* du = (double*)(D + K.u); // [t_end, u_0 .. u_{n_u-1}]
+    double* dres = (double*)(D + K.res);
+    const size_t res_bytes = (size_t)n_u * 48 + (want_aw ? (size_t)ntau * 24 : 0);
+    if (!hit) c->kn_valid = false; // the resident copy is being replaced
+    rc = fenced(c, nullptr, false, [&](hipStream_t s) -> int {
+        if (!hit) {
+            int32_t* hc = (int32_t*)H;
+            memset(H, 0, K.tg);
+            hc[0] = (int32_t)n;
+            hc[2] = (int32_t)m;
+            double* hs = (double*)(H + K.sc);
+            hs[0] = beta;
+            hs[1] = eta;
+            memcpy(H + K.tg, t, (size_t)n * 8);
+            memcpy(H + K.tg + (size_t)n * 8, G, (size_t)n * 8);
+            HIP_TRY(c, hipMemcpyAsync(D, H, K.tg + (size_t)n * 16, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+            sbr::LearnArgs la{0.0, o.ode_reltol, o.ode_abstol, p, lambda, o.ode_maxiters, 1, 0, 0, nullptr, nullptr};
+            HIP_TRY(c, sbr::launch_hazard(dsc, dsc + 1, la, L, 1, s), SBR_EDEVICE);
+            if (ntau > 0)
+                HIP_TRY(c, hipMemcpyAsync(H + K.hr, D + K.hr, (size_t)ntau * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+            HIP_TRY(c, hipMemcpyAsync(H, D, 32, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        }
+        double* hu = (double*)(H + K.u);
+        hu[0] = t_end;
+        memcpy(hu + 1, u, (size_t)n_u * 8);
+        HIP_TRY(c, hipMemcpyAsync(du, hu, (size_t)(n_u + 1) * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+        const size_t nu = (size_t)n_u;
+        const sbr::ResultSoA r{dres, dres + nu, dres + 2 * nu, dres + 3 * nu, dres + 4 * nu, (uint32_t*)(dres + 5 * nu),
+                               (int32_t*)(dres + 5 * nu) + nu};
+        double* dpath = dres + 6 * nu;
+        sbr::EqArgs ea{kappa, (int32_t)n_u, o.bisect_max_iters, c->lds_cap_b, want_aw ? dpath : nullptr,
+                       (o.flags & SBR_FLAG_EXHAUSTIVE) ? 1 : 0, (o.flags >> 8) & 7,
+                       want_aw ? dpath + ntau : nullptr, want_aw ? dpath + 2 * ntau : nullptr, 1};
+        HIP_TRY(c, sbr::launch_equilibrium(L, dsc + 1, du, du + 1, ea, r, 1, s, n <= c->lds_cap_b ? 1 : 2),
+                SBR_EDEVICE);
+        HIP_TRY(c, hipMemcpyAsync(H + K.res, D + K.res, res_bytes, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
+        return SBR_OK;
+    });
+    if (rc) return rc;
+    if (!hit) {
+        const int32_t* hc = (const int32_t*)H;
+        // the device's hazard grid must be the one sized above (a bug guard)
+        if (hc[1] != (int32_t)ntau) return fail(c, SBR_EDEVICE, "hazard grid length mismatch");
+        c->kn_t.assign(t, t + n);
+        c->kn_G.assign(G, G + n);
+        const double* hh = (const double*)(H + K.hr);
+        c->kn_hr.assign(hh, hh + ntau);
+        memcpy(c->kn_key, key, sizeof key);
+        c->kn_n = n;
+        c->kn_m = (int32_t)m;
+        c->kn_ntau = (int32_t)ntau;
+        c->kn_valid = true;
+    }
+    const size_t nu = (size_t)n_u;
+    const double* hr_ = (const double*)(H + K.res);
+    double* hs[5] = {out->xi, out->tau_in_unc, out->tau_out_unc, out->aw_max, out->tol};
+    for (int k = 0; k < 5; k++)
+        if (hs[k]) memcpy(hs[k], hr_ + k * nu, nu * 8);
+    if (out->status) memcpy(out->status, hr_ + 5 * nu, nu * 4);
+    if (out->iters) memcpy(out->iters, (const int32_t*)(hr_ + 5 * nu) + nu, nu * 4);
+    if (n_tau) *n_tau = ntau;
+    if (tau) {
+        memcpy(tau, t, (size_t)m * 8);
+        if (ntau > m) tau[m] = eta;
+    }
+    if (hr) memcpy(hr, c->kn_hr.data(), (size_t)ntau * 8);
+    if (want_aw) {
+        const bool run = (((const uint32_t*)(hr_ + 5 * nu))[0] & SBR_RUN) != 0;
+        const double* hp = hr_ + 6 * nu;
+        double* dst[3] = {aw_cum, aw_out, aw_in};
+        for (int k = 0; k < 3; k++) {
+            if (!dst[k]) continue;
+            if (run) memcpy(dst[k], hp + k * ntau, (size_t)ntau * 8);
+            else for (int64_t i = 0; i < ntau; i++) dst[k][i] = NAN;
+        }
+    }
+    return SBR_OK;
+}
+
+int sbr_last_schedule(sbr_ctx* c, int32_t* schedule)
+{
+    SBR_PER_DEVICE_DIAG(c);
+    if (!c || !schedule) return SBR_EARG;
+    *schedule = c->rs_used ? 1 : 0;
+    return SBR_OK;
 }
 
 int sbr_timing_enable(sbr_ctx* c, int on)

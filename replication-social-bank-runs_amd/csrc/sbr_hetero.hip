@@ -1248,7 +1248,7 @@ __global__ __launch_bounds__(BLOCK, SBR_HET_MINW) void equilibrium_hetero_kernel
         if (nan) s_nonmono = 1;
         if (fits) {
             bool close = false;
-            const double sepd = 1e-15 * smem[n - 1];
+            const double sepd = n > 0 ? 1e-15 * smem[n - 1] : 0.0; // n == 0: an ARG_INVALID column
             for (int i = threadIdx.x; i + 2 < n; i += BLOCK) close |= !(smem[i + 2] - smem[i] > sepd);
             if (close) s_close = 1;
         }

@@ -57,6 +57,12 @@ struct EqArgs {
     double* aw_path;    // optional AW_cum(τ̄) output for single-point mode (n_u == 1)
     int32_t exhaustive; // 1: linear crossing scan + every AW knot (no block summaries)
     int32_t diag;       // SBR_FLAG_DIAG_* bits >> 8 (timing breakdown only)
+    // with aw_path (baseline path mode): AW_OUT(τ̄) / AW_IN(τ̄) of get_AW (solver.jl:495-532), may be null
+    double* aw_out_path;
+    double* aw_in_path;
+    // 1: the knots are the caller's whole interpolation grid (sbr_equilibrium_on_knots), never a
+    // truncated learning solve: a lookup past the last knot is the interpolant's BoundsError
+    int32_t full_grid;
 };
 
 // Interest-rate extension (sbr_baseline.hip interest mode): value function on the HR grid.
@@ -182,14 +188,25 @@ hipError_t launch_hetero(int K, const double* betas, const double* dist, const d
 
 hipError_t launch_learn_logistic(const double* beta, const double* eta, const double* t_end, const LearnArgs& a,
                                  const LearnBufs& L, hipStream_t s);
+// only_mode: 0 = the LDS-slab launch then the global-memory launch; 1 / 2 = only one of them
+// (a caller that knows every column fits the slab, or none does).  With a.aw_path (n_u == 1)
+// the path-mode kernels run: the point's solve, then get_AW's paths by the whole workgroup.
 hipError_t launch_equilibrium(const LearnBufs& L, const double* eta, const double* t_end, const double* u,
-                              const EqArgs& a, const ResultSoA& out, int n_beta, hipStream_t s);
+                              const EqArgs& a, const ResultSoA& out, int n_beta, hipStream_t s, int only_mode = 0);
+// hazard_rate (solver.jl:153-185) of n_beta columns whose knots, n_knots, n_le (#knots <= η) and
+// status are in L (the hazard stage of launch_learn_logistic on its own)
+hipError_t launch_hazard(const double* beta, const double* eta, const LearnArgs& a, const LearnBufs& L, int n_beta,
+                         hipStream_t s);
 // the equilibrium side of a readiness sweep: one workgroup per item (hazard + equilibria
 // of each column as soon as the learning kernel publishes it); the learning side is
 // launch_learn_logistic with la.ready_q set and la.fuse_hazard = 0, without its hazard launch
 hipError_t launch_eq_ready(const LearnBufs& L, const double* beta, const double* eta, const double* t_end,
                            const double* u, const LearnArgs& la, const EqArgs& a, const ReadyArgs& ra,
                            const ResultSoA& out, int n_blocks, hipStream_t s);
+// after a readiness sweep, on the stream that orders after it: if a workgroup gave up waiting
+// (*gave_up != 0), every one of the n_pts points is marked SBR_ENGINE_SCHED (ξ = AW_max = NaN,
+// tol = Inf) — the failure is visible in the results without a host synchronisation
+hipError_t launch_ready_fail(const int32_t* gave_up, const ResultSoA& out, int64_t n_pts, hipStream_t s);
 // solve_equilibrium_interest per (β, u) on the same learning buffers
 hipError_t launch_interest(const LearnBufs& L, const double* eta, const double* t_end, const double* u,
                            const EqArgs& a, const InterestArgs& ia, const ResultSoA& out, int n_beta, hipStream_t s);

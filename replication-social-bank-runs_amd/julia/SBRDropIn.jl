@@ -17,9 +17,11 @@ Then Figs 1–3 run unchanged:
     LinearInterpolations;
   * `solve_equilibrium_baseline(lr, econ)`  → SolvedModel (solver.jl:55-109, 413-462): ξ, the
     buffers, HR as a LinearInterpolation on τ̄, bankrun / converged / tolerance — one GPU
-    solve through sbr_solve_point_paths (bit-identical to a sweep point);
+    solve on `lr`'s own knots through sbr_equilibrium_on_knots (no learning ODE: the scripts
+    learn once per β, 1_baseline.jl:44 / :227, and call this per u, :169 / :248; the knots
+    and HR stay on the GPU between those calls, so each uploads only u);
   * `get_AW_functions!(result)`             → (AW_cum, AW_OUT, AW_IN, AW_max) (solver.jl:553-576):
-    AW_cum and AW_max are the engine's, AW_OUT / AW_IN are rebuilt from the CDF by `get_AW`;
+    all four from the engine (the same call returned get_AW's three paths);
   * `hazard_rate`, `get_AW`                 → host restatements of solver.jl:153-185, 495-532,
     kept for plot_hazard_rate_decomposition / plot_equilibrium (plotting.jl:62-210), which
     call them on interpolants; they are presentation code, not the sweep path.
@@ -93,10 +95,10 @@ struct SolvedModel
     solve_time::Float64
     tolerance::Float64
     aw::Ref{Union{Nothing, NamedTuple}}
-    aw_cum_engine::Vector{Float64}   # AW_cum on the HR grid from the engine (empty without a run)
+    aw_engine::Any   # the engine's (AW_cum, AW_OUT, AW_IN, AW_max) on the HR grid (nothing without a run)
 
     function SolvedModel(ξ, τ_bar_IN_UNC, τ_bar_OUT_UNC, HR, bankrun, model_params::ModelParameters,
-                         learning_results, converged, solve_time, tolerance, aw_cum_engine = Float64[])
+                         learning_results, converged, solve_time, tolerance, aw_engine = nothing)
         τ_IN = max(ξ - τ_bar_IN_UNC, 0)
         τ_OUT = max(ξ - τ_bar_OUT_UNC, 0)
         (ξ ≥ 0 || isnan(ξ)) || throw(ArgumentError("Crash time ξ must be non-negative or NaN, got ξ = $ξ"))
@@ -105,31 +107,34 @@ struct SolvedModel
         solve_time ≥ 0 || throw(ArgumentError("Solve time must be non-negative, got $solve_time"))
         tolerance ≥ 0 || throw(ArgumentError("Tolerance must be non-negative, got $tolerance"))
         new(ξ, τ_bar_IN_UNC, τ_bar_OUT_UNC, HR, bankrun, τ_IN, τ_OUT, model_params, learning_results, converged,
-            solve_time, tolerance, Ref{Union{Nothing, NamedTuple}}(nothing), aw_cum_engine)
+            solve_time, tolerance, Ref{Union{Nothing, NamedTuple}}(nothing), aw_engine)
     end
 
     function SolvedModel(ξ, τ_bar_IN_UNC, τ_bar_OUT_UNC, HR, bankrun, econ::EconomicParameters,
-                         learning_results::LearningResults, converged, solve_time, tolerance, aw_cum_engine = Float64[])
+                         learning_results::LearningResults, converged, solve_time, tolerance, aw_engine = nothing)
         model_params = ModelParameters(learning_results.params, econ)
         return SolvedModel(ξ, τ_bar_IN_UNC, τ_bar_OUT_UNC, HR, bankrun, model_params, learning_results, converged,
-                           solve_time, tolerance, aw_cum_engine)
+                           solve_time, tolerance, aw_engine)
     end
 end
 
-# solver.jl:413-462 — one point on the GPU (learning, hazard, buffers, compute_ξ, AW path)
+# solver.jl:413-462 — one point on the GPU on learning_results' own knots (hazard, buffers,
+# compute_ξ, get_AW's paths); no learning ODE
 function solve_equilibrium_baseline(learning_results::LearningResults, econ::EconomicParameters;
                                     ξ_guess = nothing, verbose = false)
     solve_start = time()
     ξ_guess === nothing || throw(ArgumentError("the engine starts the bisection at the reference's default midpoint"))
     lp = learning_results.params
-    r = SBREngine.solve_point_paths(sbr_context(), lp.β, econ.u; η = econ.η, tspan_end = lp.tspan[2], x0 = lp.x0,
-                                    p = econ.p, κ = econ.κ, λ = econ.λ)
-    (r.status & SBREngine.SBR_OOB) != 0 && throw(BoundsError(learning_results.learning_cdf, econ.η))
+    cdf = learning_results.learning_cdf
+    r = SBREngine.equilibrium_on_knots(sbr_context(), cdf.itp.knots[1], cdf.itp.coefs, lp.β, econ.u; η = econ.η,
+                                       tspan_end = lp.tspan[2], p = econ.p, κ = econ.κ, λ = econ.λ)
+    (r.status & SBREngine.SBR_OOB) != 0 && throw(BoundsError(cdf, econ.η))
     HR = LinearInterpolation(r.τ_bar, r.HR)
     bankrun = (r.status & SBREngine.SBR_RUN) != 0
     converged = (r.status & SBREngine.SBR_CONVERGED) != 0
+    aw_engine = bankrun ? (AW_cum = r.AW_cum, AW_OUT = r.AW_OUT, AW_IN = r.AW_IN, AW_max = r.AW_max) : nothing
     return SolvedModel(r.ξ, r.τ_bar_IN_UNC, r.τ_bar_OUT_UNC, HR, bankrun, econ, learning_results, converged,
-                       time() - solve_start, r.tolerance, bankrun ? r.AW_cum : Float64[])
+                       time() - solve_start, r.tolerance, aw_engine)
 end
 
 # solver.jl:153-185 (host; plotting.jl:62-132 evaluates it on the learning PDF)
@@ -167,16 +172,20 @@ function get_AW(ξ, τ_bar_IN_UNC, τ_bar_OUT_UNC, HR, learning_cdf)
     return LinearInterpolation(t_grid, AW_cum), LinearInterpolation(t_grid, AW_OUT), LinearInterpolation(t_grid, AW_IN)
 end
 
-# solver.jl:553-576 — AW_cum and AW_max from the engine (when the solve returned its path),
-# AW_OUT / AW_IN rebuilt on the host
+# solver.jl:553-576 — the engine's get_AW paths on the HR grid and its AW_max (the same maximum
+# over the knots, found by the kernel's bounded scan)
 function get_AW_functions!(result::SolvedModel)
     result.aw[] !== nothing && return result.aw[]
     result.bankrun || return result.aw[]
-    AW_cum_host, AW_OUT_func, AW_IN_func = get_AW(result.ξ, result.τ_bar_IN_UNC, result.τ_bar_OUT_UNC, result.HR,
-                                                  result.learning_results.learning_cdf)
-    AW_cum_func = isempty(result.aw_cum_engine) ? AW_cum_host :
-                  LinearInterpolation(result.HR.itp.knots[1], result.aw_cum_engine)
-    result.aw[] = (AW_cum = AW_cum_func, AW_OUT = AW_OUT_func, AW_IN = AW_IN_func,
-                   AW_max = maximum(AW_cum_func.itp.coefs))
+    a = result.aw_engine
+    if a === nothing # built without the engine's paths (SBRDropInSocial's last inner SolvedModel)
+        AW_cum, AW_OUT, AW_IN = get_AW(result.ξ, result.τ_bar_IN_UNC, result.τ_bar_OUT_UNC, result.HR,
+                                       result.learning_results.learning_cdf)
+        result.aw[] = (AW_cum = AW_cum, AW_OUT = AW_OUT, AW_IN = AW_IN, AW_max = maximum(AW_cum.itp.coefs))
+        return result.aw[]
+    end
+    τ = result.HR.itp.knots[1]
+    result.aw[] = (AW_cum = LinearInterpolation(τ, a.AW_cum), AW_OUT = LinearInterpolation(τ, a.AW_OUT),
+                   AW_IN = LinearInterpolation(τ, a.AW_IN), AW_max = a.AW_max)
     return result.aw[]
 end

@@ -151,6 +151,40 @@ function solve_point_paths(ctx::Context, β, u; η = 15.0, tspan_end = 30.0, x0 
 end
 
 """
+    equilibrium_on_knots(ctx, t, G, β, u; η, tspan_end, p, κ, λ)
+
+`solve_equilibrium_baseline(lr, econ)` + `get_AW_functions!` (src/baseline/solver.jl:413-462,
+495-576) on a LearningResults' own knot grid (`t`, `G` = `lr.learning_cdf`'s knots and values,
+`β` = `lr.params.β`, `tspan_end` = `lr.params.tspan[2]`): no learning ODE.  The knots and the
+hazard path stay on the GPU while `t`, `G`, β, η, p and λ repeat, so the scripts' per-u loops
+(1_baseline.jl:169, 248) upload only `u`.  Returns ξ, the buffers, AW_max, the tolerance, the
+status and the hazard grid τ̄ with HR(τ̄), AW_cum, AW_OUT and AW_IN on it (NaN without a run).
+"""
+function equilibrium_on_knots(ctx::Context, t::Vector{Float64}, G::Vector{Float64}, β, u; η, tspan_end,
+                              p = 0.5, κ = 0.6, λ = 0.01)
+    n = length(t)
+    length(G) == n || throw(ArgumentError("t and G must have the same length"))
+    cap = n + 1
+    res = fill(NaN, 5); st = UInt32[0]; it = Int32[0]; nt = Ref{Int64}(0)
+    τ = Vector{Float64}(undef, cap); hr = similar(τ); cum = similar(τ); awo = similar(τ); awi = similar(τ)
+    uv = Float64[u]
+    opts = Ref(Opts(; early_exit = 0))
+    GC.@preserve t G uv res st it τ hr cum awo awi begin
+        soa = Ref(ResultSoA(pointer(res, 1), pointer(res, 2), pointer(res, 3), pointer(res, 4), pointer(res, 5),
+                            pointer(st), pointer(it)))
+        rc = ccall((:sbr_equilibrium_on_knots, libsbr), Cint,
+                   (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Int64, Float64, Float64, Float64, Ptr{Float64}, Int64,
+                    Float64, Float64, Float64, Ref{Opts}, Ref{ResultSoA}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
+                    Ptr{Float64}, Ptr{Float64}, Int64, Ref{Int64}),
+                   ctx.ptr, t, G, n, β, η, tspan_end, uv, 1, p, κ, λ, opts, soa, τ, hr, cum, awo, awi, cap, nt)
+        check(ctx, rc)
+    end
+    k = nt[]
+    return (ξ = res[1], τ_bar_IN_UNC = res[2], τ_bar_OUT_UNC = res[3], AW_max = res[4], tolerance = res[5],
+            status = st[1], τ_bar = τ[1:k], HR = hr[1:k], AW_cum = cum[1:k], AW_OUT = awo[1:k], AW_IN = awi[1:k])
+end
+
+"""
     solve_equilibrium_hetero_grid(ctx, βs_cols, dist, u_vals; η, tspan_end, x0, p, κ, λ)
 
 `βs_cols` is K × n_col (column c = the group rates of one parameter column); η per column.

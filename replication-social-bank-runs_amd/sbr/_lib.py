@@ -89,9 +89,12 @@ _SIGS = {
     "sbr_batch_wait": (ctypes.c_int, [_P, _P, _I64]),
     "sbr_learn_baseline": (ctypes.c_int, [_P, _P, _P, _P, _D, _I64, _I32, _P, _P, _P, _I64, _P, _P]),
     "sbr_solve_point_paths": (ctypes.c_int, [_P, _D, _D, _D, _D, _D, _D, _D, _D, _P, _P, _P, _P, _P, _P, _I64, _P]),
+    "sbr_equilibrium_on_knots": (ctypes.c_int, [_P, _P, _P, _I64, _D, _D, _D, _P, _I64, _D, _D, _D, _P, _P, _P, _P,
+                                                _P, _P, _P, _I64, _P]),
     "sbr_apply_early_exit": (None, [_I64, _I64, _I32, _P]),
     "sbr_selftest_detmath": (ctypes.c_int, [_P, _P, _P, ctypes.c_int, _P, _P, _P]),
     "sbr_timing_enable": (ctypes.c_int, [_P, ctypes.c_int]),
+    "sbr_last_schedule": (ctypes.c_int, [_P, _P]),
     "sbr_timing_read": (ctypes.c_int, [_P, _P, _P, _P, _P]),
     "sbr_learn_stats": (ctypes.c_int, [_P, _I64, _P, _P, _P, _P, _P]),
     "sbr_hetero_learn_stats": (ctypes.c_int, [_P, _I64, _P, _P, _P, _P, _P]),

@@ -97,6 +97,7 @@ class Engine:
                 raise SBRNativeError(f"sbr_init(device={device}) failed ({rc}): no usable HIP device")
         self._ctx = ctx
         self._L = L
+        self._knot_opts = {}  # sbr_opts per bisect_max_iters of equilibrium_on_knots (per-call latency)
 
     @property
     def n_gpus(self) -> int:
@@ -205,6 +206,53 @@ class Engine:
         k = int(nt[0])
         return dict(xi=res[0], tau_in_unc=res[1], tau_out_unc=res[2], aw_max=res[3], tol=res[4],
                     status=int(st[0]), tau=tau[:k].copy(), hr=hr[:k].copy(), aw_cum=aw[:k].copy())
+
+    def equilibrium_on_knots(self, t, G, beta, eta, t_end, u, p, kappa, lam, max_iters: int = 100,
+                             paths: bool = True) -> dict:
+        """solve_equilibrium_baseline(lr, econ) + get_AW_functions!(r) (solver.jl:413-462, 553-576)
+        on the learning knots the caller holds (t, G = lr.learning_cdf's knots and values) for each
+        u — no learning ODE (sbr_equilibrium_on_knots).  The knots and the hazard path stay on the
+        GPU while (t, G, β, η, p, λ) repeat, so a per-u loop over one LearningResults uploads only
+        u.  Returns the SoA fields ([n_u] arrays); with ``paths`` (one u) also the hazard grid
+        ``tau``, ``hr`` and ``aw_cum`` / ``aw_out`` / ``aw_in`` on it (NaN without a run)."""
+        t = t if (isinstance(t, np.ndarray) and t.dtype == np.float64 and t.flags.c_contiguous) else \
+            np.ascontiguousarray(t, np.float64)
+        G = G if (isinstance(G, np.ndarray) and G.dtype == np.float64 and G.flags.c_contiguous) else \
+            np.ascontiguousarray(G, np.float64)
+        if len(G) != len(t):
+            raise ArgumentError("t and G must have the same length")
+        u = np.ascontiguousarray(np.atleast_1d(u), np.float64)
+        n, nu = len(t), len(u)
+        if paths and nu != 1:
+            raise ArgumentError("paths need a single u")
+        res = np.empty(6 * nu)  # xi, tau_in_unc, tau_out_unc, aw_max, tol, then status / iters (int32)
+        st_it = res[5 * nu:].view(np.int32)
+        base = res.ctypes.data
+        soa = _lib.ResultSoA(base, base + 8 * nu, base + 16 * nu, base + 24 * nu, base + 32 * nu, base + 40 * nu,
+                             base + 44 * nu)
+        opts = self._knot_opts.get(max_iters)
+        if opts is None:
+            opts = self._knot_opts[max_iters] = _lib.default_opts(bisect_max_iters=max_iters)
+        cap = n + 1
+        nt = ctypes.c_int64()
+        if paths:
+            pbuf = np.empty(5 * cap)
+            pb = pbuf.ctypes.data
+            pp = (pb, pb + 8 * cap, pb + 16 * cap, pb + 24 * cap, pb + 32 * cap)
+        else:
+            pp = (None,) * 5
+        rc = self._L.sbr_equilibrium_on_knots(self._ctx, t.ctypes.data, G.ctypes.data, n, beta, eta, t_end,
+                                              u.ctypes.data, nu, p, kappa, lam, ctypes.byref(opts),
+                                              ctypes.byref(soa), *pp, cap, ctypes.byref(nt))
+        check(rc, self._ctx, "sbr_equilibrium_on_knots")
+        out = dict(xi=res[:nu], tau_in_unc=res[nu:2 * nu], tau_out_unc=res[2 * nu:3 * nu],
+                   aw_max=res[3 * nu:4 * nu], tol=res[4 * nu:5 * nu], status=st_it[:nu].view(np.uint32),
+                   iters=st_it[nu:2 * nu])
+        if paths:
+            k = nt.value
+            pv = pbuf.reshape(5, cap)
+            out.update(tau=pv[0, :k], hr=pv[1, :k], aw_cum=pv[2, :k], aw_out=pv[3, :k], aw_in=pv[4, :k])
+        return out
 
     def sweep_hetero(self, betas, dist, eta, t_end, u, p, kappa, lam, x0=1e-4, knot_capacity: int = 16384,
                      with_groups: bool = True, exhaustive: bool = False) -> dict:
@@ -444,6 +492,12 @@ class Engine:
               "sbr_device_info")
         return dict(lds_bytes_per_block=a.value, lds_knot_capacity=b.value, cu_count=c.value)
 
+    def last_schedule(self) -> int:
+        """1 if the last single sweep took the per-column readiness schedule, 0 if chunked."""
+        v = ctypes.c_int32()
+        check(self._L.sbr_last_schedule(self._ctx, ctypes.byref(v)), self._ctx, "sbr_last_schedule")
+        return v.value
+
     def timing_enable(self, on: bool = True):
         check(self._L.sbr_timing_enable(self._ctx, int(on)), self._ctx, "sbr_timing_enable")
 
@@ -550,6 +604,8 @@ class SolvedModel:
     status: int
     aw_cum: np.ndarray = field(repr=False, default=None)
     aw: dict | None = field(repr=False, default=None)
+    # (AW_OUT, AW_IN, AW_max) from the engine (solve_equilibrium_baseline on the caller's knots)
+    aw_paths: tuple | None = field(repr=False, default=None)
 
     @property
     def tau_IN(self):
@@ -572,14 +628,23 @@ def solve_learning(lp: LearningParameters, engine: Engine | None = None) -> Lear
 
 def solve_equilibrium_baseline(lr: LearningResults, econ: EconomicParameters,
                                engine: Engine | None = None) -> SolvedModel:
-    """solver.jl:413-462 for one point, with the HR and AW paths (GPU)."""
+    """solver.jl:413-462 for one point on the GPU, on ``lr``'s own knots (no learning ODE: the
+    scripts learn once per β and call this per u, 1_baseline.jl:169, 248), with the HR path and
+    get_AW's three paths."""
     eng = engine or default_engine()
     lp = lr.params
-    r = eng.solve_point_paths(lp.beta, econ.eta, lp.tspan[1], econ.u, econ.p, econ.kappa, econ.lam, lp.x0)
-    st = r["status"]
+    cdf = lr.learning_cdf
+    r = eng.equilibrium_on_knots(cdf.knots, cdf.coefs, lp.beta, econ.eta, lp.tspan[1], econ.u, econ.p, econ.kappa,
+                                 econ.lam)
+    st = int(r["status"][0])
+    if st & _lib.SBR_OOB:
+        raise IndexError("BoundsError: interpolation outside the knot range (solver.jl, Interpolations Throw())")
     bankrun = bool(st & _lib.SBR_RUN)
-    return SolvedModel(r["xi"], r["tau_in_unc"], r["tau_out_unc"], LinearInterpolation(r["tau"], r["hr"]), bankrun,
-                       (lp, econ), lr, bool(st & _lib.SBR_CONVERGED), r["tol"], st, aw_cum=r["aw_cum"])
+    sm = SolvedModel(float(r["xi"][0]), float(r["tau_in_unc"][0]), float(r["tau_out_unc"][0]),
+                     LinearInterpolation(r["tau"], r["hr"]), bankrun, (lp, econ), lr, bool(st & _lib.SBR_CONVERGED),
+                     float(r["tol"][0]), st, aw_cum=r["aw_cum"],
+                     aw_paths=(r["aw_out"], r["aw_in"], float(r["aw_max"][0])))
+    return sm
 
 
 def solve_equilibrium_social_learning(model: ModelParameters, tol: float = 1e-4, max_iter: int = 250,
@@ -612,6 +677,11 @@ def get_AW_functions(result: SolvedModel):
     if not result.bankrun:
         return None
     tg = result.HR.knots
+    if result.aw_paths is not None:  # the engine's get_AW paths and AW_max
+        aw_out, aw_in, aw_max = result.aw_paths
+        result.aw = dict(AW_cum=LinearInterpolation(tg, result.aw_cum), AW_OUT=LinearInterpolation(tg, aw_out),
+                         AW_IN=LinearInterpolation(tg, aw_in), AW_max=aw_max)
+        return result.aw
     cdf = result.learning_results.learning_cdf
     xi, tin, tout = result.xi, result.tau_bar_IN_UNC, result.tau_bar_OUT_UNC
     ic = xi if tin >= xi else tin

@@ -248,13 +248,14 @@ def test_pipelined_batches_equal_single_sweeps(engine):
         assert np.array_equal(out["iters"][k].cpu().numpy().reshape(nb, nu), ref["iters"])
 
 
-@pytest.mark.parametrize("n_u", [50, 2000])
+@pytest.mark.parametrize("n_u", [50, 9000])
 def test_readiness_schedule_equals_chunked(engine, n_u):
     """The per-column readiness schedule (SBR_FLAG_READY_SWEEP: the learning kernel publishes
     each column the moment its lane solves it; equilibrium workgroups on other CUs take
     (column, u-tile) items in publication order, tile 0 running the column's hazard) gives
     exactly the default three-chunk schedule's results — incl. BoundsError columns (η past
-    tspan), η == t_end, and one or several u-tiles per column."""
+    tspan), η == t_end, and one u-tile per column (n_u = 50) or three (n_u = 9000 > 2 × 4096:
+    tiles 1 and 2 wait on the tile-0 workgroup's hazard flag).  The schedule is asserted taken."""
     base = sbr.fig5_grid(384, n_u=n_u)
     eta = np.full(384, 15.0)
     tend = np.full(384, 30.0)
@@ -263,7 +264,9 @@ def test_readiness_schedule_equals_chunked(engine, n_u):
     tend[200:210] = 20.0
     g = sbr.BaselineGrid(base.beta, base.u, eta, tend)
     a = engine.sweep_baseline(g, flags=sbr._lib.SBR_FLAG_READY_SWEEP)
+    assert engine.last_schedule() == 1  # the MI355X (256 CUs) runs the readiness schedule
     b = engine.sweep_baseline(g)
+    assert engine.last_schedule() == 0
     for f in FIELDS:
         assert_bitwise(a[f], b[f], f)
     assert np.array_equal(a["status"], b["status"])

@@ -218,15 +218,16 @@ def test_dropins_provide_every_field_the_scripts_and_plotting_read(script):
         assert f in structs["SolvedModel"], (script, f)
 
 
-def test_surface_fixture_matches_reference_when_present():
+def test_surface_fixture_matches_reference_when_present(tmp_path):
     """The fixture is what tools/extract_julia_surface.py reads from /root/reference today
-    (skipped where the reference is absent, e.g. on the GPU box)."""
+    (skipped where the reference is absent, e.g. on the GPU box).  The extractor writes to a
+    temporary file: the committed fixture is compared, never rewritten."""
     if not Path("/root/reference/scripts").is_dir():
         pytest.skip("reference not present")
     import subprocess as sp
 
-    before = (REPO / "tests" / "golden" / "julia_surface.json").read_text()
-    out = sp.run([sys.executable, str(REPO / "tools" / "extract_julia_surface.py")], capture_output=True, text=True)
+    fresh = tmp_path / "julia_surface.json"
+    out = sp.run([sys.executable, str(REPO / "tools" / "extract_julia_surface.py"), str(fresh)], capture_output=True,
+                 text=True)
     assert out.returncode == 0, out.stderr
-    after = (REPO / "tests" / "golden" / "julia_surface.json").read_text()
-    assert before == after
+    assert fresh.read_text() == (REPO / "tests" / "golden" / "julia_surface.json").read_text()

@@ -66,7 +66,7 @@ def rel(p: Path) -> str:
     return str(p.relative_to(REF))
 
 
-def main():
+def main(out: Path = OUT):
     surface = {"reference": str(REF), "scripts": {}}
     for script, dropins in DROPINS.items():
         sp = REF / script
@@ -107,10 +107,11 @@ def main():
             "dropins": dropins, "defs": defs, "calls": calls, "returns": returns, "field_reads": reads,
             "plotting_solvedmodel_reads": plot_reads, "structs_replaced": structs_r, "structs_kept": structs_k,
         }
-    OUT.write_text(json.dumps(surface, indent=1, ensure_ascii=False, sort_keys=True) + "\n")
+    out.write_text(json.dumps(surface, indent=1, ensure_ascii=False, sort_keys=True) + "\n")
     for s, d in surface["scripts"].items():
         print(s, "calls", sorted({c["fn"] for c in d["calls"]}), "returns", d["returns"])
 
 
 if __name__ == "__main__":
-    main()
+    # optional output path (default: the committed fixture tests/golden/julia_surface.json)
+    main(Path(sys.argv[1]) if len(sys.argv) > 1 else OUT)

@@ -1,0 +1,48 @@
+#!/usr/bin/env bash
+# Round-4 GPU steps: STEPS selects a subset (in order); each GPU step has its own time limit
+# and the first failure ends the script.  TESTK narrows the pytest step (-k expression).
+set -u
+cd "${GRAFT_REPO_ROOT:-.}"
+OUT=gpurun_out/${TAG:-r04}
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+( while true; do date +%T >> "$OUT/heartbeat.log"; sleep 30; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
+run() { # name timeout cmd...
+  local name=$1 to=$2; shift 2
+  timeout -k 10 "$to" "$@" > "$OUT/$name.out" 2> "$OUT/$name.err"
+  local rc=$?
+  echo "$name rc=$rc" | tee -a "$OUT/steps.log"
+  tail -c 1500 "$OUT/$name.out"; echo
+  if [ $rc -ne 0 ]; then tail -20 "$OUT/$name.err"; exit $rc; fi
+}
+for s in ${STEPS:-tests smoke bench single}; do
+  case $s in
+    tests) run tests 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${TESTK:+-k "$TESTK"} ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 300 python -u bench.py ;;
+    single) run single 300 python -u bench.py --no-pipeline --steps 20 --warmup 2 --no-cpu-baseline ;;
+    ready) run ready 300 python -u bench.py --no-pipeline --ready --steps 20 --warmup 2 --no-cpu-baseline ;;
+    prof) run prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
+    profsingle) run profsingle 300 rocprofv3 --kernel-trace --stats -d "$OUT/profsingle" -o run --output-format csv -- python3 bench.py --no-pipeline --steps 20 --warmup 2 --no-cpu-baseline ;;
+    hetero) run hetero 600 python -u bench.py --workload hetero --steps 10 --warmup 2 --phases ;;
+    interest) run interest 600 python -u bench.py --workload interest --steps 3 --warmup 1 ;;
+    social) run social 600 python -u bench.py --workload social --steps 1 --warmup 0 ;;
+    config1) run config1 300 python -u bench.py --workload config1 --steps 50 --warmup 3 ;;
+    phases) run phases 300 python -u bench.py --phases --steps 10 --warmup 2 --no-cpu-baseline ;;
+    wgtime) run wgtime 300 env SBR_LIB=replication-social-bank-runs_amd/lib_var/wgtime/libsbr.so WG_OUT=$OUT/wgtime.npz python -u tools/wgtime.py ;;
+    phasevars) for v in ${VARS:-}; do run phases_$v 300 env SBR_LIB=replication-social-bank-runs_amd/lib_var/$v/libsbr.so python -u bench.py --phases --steps 10 --warmup 2 --no-cpu-baseline; done ;;
+    pmc) PMC_OUT=$OUT/pmc bash tools/pmc.sh > "$OUT/pmc.out" 2>&1; echo "pmc rc=$?" | tee -a "$OUT/steps.log" ;;
+    pmcphase) for fl in 0x100 0x200 0; do run pmcph_$fl 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY --output-format csv -d "$OUT/pmcph_$fl" -o pass -- python3 tools/eq_diag_run.py $fl; done ;;
+    socprobe) run socprobe 600 python -u tools/social_step_probe.py ${PROBE_ITERS:-8} && run socprobe_nocoop 600 env SBR_LIB=replication-social-bank-runs_amd/lib_var/nocoop/libsbr.so python -u tools/social_step_probe.py ${PROBE_ITERS:-8} ;;
+    socphase) run socphase 600 python -u tools/social_phase_probe.py ${PROBE_ITERS:-8} && run socphase_nocoop 600 env SBR_LIB=replication-social-bank-runs_amd/lib_var/nocoop/libsbr.so python -u tools/social_phase_probe.py ${PROBE_ITERS:-8} ;;
+    soctrace) run soctrace 600 env SBR_SOCIAL_TRACE=1 python -u bench.py --workload social --steps 1 --warmup 0 --no-cpu-baseline ;;
+    soctracevar) run soctrace_$VAR 600 env SBR_SOCIAL_TRACE=1 SBR_LIB=replication-social-bank-runs_amd/lib_var/$VAR/libsbr.so python -u bench.py --workload social --steps 1 --warmup 0 --no-cpu-baseline ;;
+    socdump) run socdump 600 python -u bench.py --workload social --steps 1 --warmup 0 --no-cpu-baseline --social-dump $OUT/social_dump.npz ;;
+    hetvars) for v in ${VARS:-}; do run hetero_$v 600 env SBR_LIB=replication-social-bank-runs_amd/lib_var/$v/libsbr.so python -u bench.py --workload hetero --steps 10 --warmup 2 --phases --no-cpu-baseline; done ;;
+    config2) run config2 300 python -u bench.py --workload config2 --steps 20 --warmup 2 ;;
+    dropin) run dropin 600 python -u bench.py --workload dropin --steps 30 ;;
+    knots) run knots 600 python -u -m pytest tests/test_gpu_knots.py tests/test_gpu_baseline.py -x -v --timeout 300 --timeout-method thread ${TESTK:+-k "$TESTK"} ;;
+  esac
+done
