@@ -61,6 +61,11 @@ typedef struct {
  * use) runs its hazard and equilibria.  Same results; slower on the configs (the columns'
  * learning ends late and the equilibria lose the learning CUs), kept for A/B. */
 #define SBR_FLAG_READY_SWEEP 0x2 /* a timed-out wait marks every point SBR_ENGINE_SCHED (_dev) / SBR_EDEVICE (host) */
+/* n-device contexts (sbr_init_multi): return the host-pointer sweep's results through an RCCL
+ * gather of every rank's block to device 0 over xGMI and one scatter from there, instead of
+ * the default direct transport (each GPU copies its own columns into the caller's arrays over
+ * its own PCIe link, no collective).  Same results. */
+#define SBR_FLAG_RCCL_GATHER 0x4
 /* Diagnostics (timing breakdown only — results are NOT the reference's):
  * stop every point after the crossing scan / after the ξ bisection, or
  * report the number of 64-knot AW blocks evaluated in `iters` instead of
@@ -397,8 +402,11 @@ int sbr_device_info(sbr_ctx* ctx, int32_t* lds_bytes_per_block, int32_t* lds_kno
  * host_out[f] (n_col·n_u·per_pt[f] elements, u-fastest per column, NULL = dropped). */
 typedef int (*sbr_shard_compute_fn)(void* user, int32_t rank, int64_t n_cols, const int64_t* col_ids,
                                     void* const* fields);
+/* rccl_gather = 0: the direct transport (each rank scatters its own block); 1: the gather to rank
+ * 0 and one scatter from there (SBR_FLAG_RCCL_GATHER's data movement). */
 int sbr_shard_host_run(int32_t n_ranks, int64_t n_col, int64_t n_u, int32_t n_fields, const int64_t* esz,
-                       const int64_t* per_pt, void* const* host_out, sbr_shard_compute_fn compute, void* user);
+                       const int64_t* per_pt, void* const* host_out, sbr_shard_compute_fn compute, void* user,
+                       int32_t rccl_gather);
 
 /* Diagnostics: sbr_exp / sbr_log / sbr_pow_pos (include/sbr_detmath.h)
  * evaluated on the device, for host/device bit-equality tests. */

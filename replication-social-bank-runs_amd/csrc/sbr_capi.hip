@@ -2150,7 +2150,7 @@ int multi_sweep_baseline(sbr_ctx* c, const double* beta, const double* eta, cons
         return sbr_sweep_baseline_dev(kid, s, d, d + nc, d + 2 * nc, x0, d + 3 * nc, nc, n_u, p, kappa, lambda, &o,
                                       &ro);
     };
-    int rc = sbr_multi_impl::run_sharded(c->multi, n_beta, n_u, fs, (size_t)(3 * cmax + n_u) * 8, stage, run);
+    int rc = sbr_multi_impl::run_sharded(c->multi, n_beta, n_u, fs, (size_t)(3 * cmax + n_u) * 8, stage, run, (o.flags & SBR_FLAG_RCCL_GATHER) != 0);
     if (rc) return fail(c, rc, sbr_multi_impl::last_error(c->multi));
     if (o.early_exit_nan_run > 0 && out->status && out->xi && out->aw_max && out->tol)
         sbr_apply_early_exit(n_beta, n_u, o.early_exit_nan_run, out);
@@ -2181,7 +2181,7 @@ int multi_sweep_interest(sbr_ctx* c, const double* beta, const double* eta, cons
         return sbr_sweep_interest_dev(kid, s, d, d + nc, d + 2 * nc, x0, d + 3 * nc, nc, n_u, p, kappa, lambda, r_,
                                       delta, &o, &ro, (int64_t*)f[7]);
     };
-    int rc = sbr_multi_impl::run_sharded(c->multi, n_beta, n_u, fs, (size_t)(3 * cmax + n_u) * 8, stage, run);
+    int rc = sbr_multi_impl::run_sharded(c->multi, n_beta, n_u, fs, (size_t)(3 * cmax + n_u) * 8, stage, run, (o.flags & SBR_FLAG_RCCL_GATHER) != 0);
     return rc ? fail(c, rc, sbr_multi_impl::last_error(c->multi)) : SBR_OK;
 }
 
@@ -2213,7 +2213,7 @@ int multi_sweep_hetero(sbr_ctx* c, int32_t K, const double* betas, const double*
                                     (double*)f[5], (double*)f[6]);
     };
     int rc = sbr_multi_impl::run_sharded(c->multi, n_col, n_u, fs, (size_t)(cmax * K + K + 2 * cmax + n_u) * 8,
-                                         stage, run);
+                                         stage, run, (o.flags & SBR_FLAG_RCCL_GATHER) != 0);
     return rc ? fail(c, rc, sbr_multi_impl::last_error(c->multi)) : SBR_OK;
 }
 
@@ -2243,7 +2243,7 @@ int multi_sweep_social(sbr_ctx* c, const double* beta, const double* eta, double
                                     n_cmp, tol, max_iter, &o, &ro, (int32_t*)f[7], (int64_t*)f[8]);
     };
     int rc = sbr_multi_impl::run_sharded(c->multi, n_beta, n_u, fs, (size_t)(2 * cmax + n_u + cmax * n_cmp) * 8,
-                                         stage, run);
+                                         stage, run, (o.flags & SBR_FLAG_RCCL_GATHER) != 0);
     return rc ? fail(c, rc, sbr_multi_impl::last_error(c->multi)) : SBR_OK;
 }
 }  // namespace

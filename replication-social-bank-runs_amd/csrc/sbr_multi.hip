@@ -6,15 +6,22 @@
 //   2. runs each shard on its own GPU from its own host thread (the single-device
 //      *_dev entry points on that child context's own stream, inputs staged into that
 //      GPU's HBM);
-//   3. after every shard has finished, and after every fallible per-rank step of the
-//      gather (device selection, rank 0's gather buffer, its local copy) has succeeded,
-//      gathers the packed result blocks to rank 0 with RCCL point-to-point
-//      (ncclSend/ncclRecv over xGMI, posted as one group over all communicators from one
-//      thread) — the only communication of the path.  If the group or a stream fails
-//      after posting, every communicator is aborted (ncclCommAbort: no rank stays blocked)
-//      and rebuilt on the next call;
-//   4. rank 0 scatters the blocks into the caller's u-fastest arrays (strided copies:
-//      column i of the grid is block row i / N of rank i mod N).
+//   3. returns the results to the caller's host arrays by one of two transports:
+//      * direct (the default): each rank copies its own packed block straight into the
+//        caller's u-fastest arrays (strided D2H copies: column i of the grid is block row
+//        i / N of rank i mod N) from its own thread, so the N GPUs' PCIe links carry the
+//        result in parallel and no collective runs — the results of a host-pointer sweep
+//        are bound for host memory, which a gather to one GPU would funnel through a
+//        single link;
+//      * RCCL gather (SBR_FLAG_RCCL_GATHER): after every shard has finished, and after
+//        every fallible per-rank step of the gather (device selection, rank 0's gather
+//        buffer, its local copy) has succeeded, the packed blocks go to rank 0's HBM with
+//        RCCL point-to-point (ncclSend/ncclRecv over xGMI, posted as one group over all
+//        communicators from one thread).  If the group or a stream fails after posting,
+//        every communicator is aborted (ncclCommAbort: no rank stays blocked) and rebuilt
+//        on the next call; rank 0 then scatters the blocks into the caller's arrays.
+//      Only the loopback tests (N = 2, 3, 8, 20) and N = 1 hardware runs have exercised
+//      the N > 1 layouts so far: the RCCL transport is unverified on multi-GPU hardware.
 // Steps 1, 3 and 4 are sbr_shard.h's, shared with the host loopback of
 // sbr_shard_host_run (the CPU tests' N = 2, 3, 8 layouts).  Per-point results do not
 // depend on the partitioning, so a multi-GPU sweep is bit-identical to a single-device
@@ -286,7 +293,7 @@ const char* last_error(const sbr_multi* m) { return m ? m->err.c_str() : ""; }
 //   run(r, cols_r, kid, stream, in_dev, out_fields)  enqueues the single-device sweep, writing
 //                                              field f of the block at out_fields[f]
 int run_sharded(sbr_multi* m, int64_t n_col, int64_t n_u, const std::vector<sbr_shard::Field>& fields,
-                size_t in_bytes, const StageFn& stage, const RunFn& run)
+                size_t in_bytes, const StageFn& stage, const RunFn& run, bool rccl_gather)
 {
     m->err.clear();
     const int N = (int)m->ranks.size();
@@ -311,6 +318,13 @@ int run_sharded(sbr_multi* m, int64_t n_col, int64_t n_u, const std::vector<sbr_
                 std::vector<void*> fp;
                 for (size_t o : sbr_shard::field_offsets(plan, r, fields)) fp.push_back((char*)k.out + o);
                 if (rc == SBR_OK) rc = run(r, plan.cols[r], k.kid, k.stream, k.in, fp);
+                // direct transport: this rank's columns straight into the caller's arrays
+                if (rc == SBR_OK && !rccl_gather)
+                    rc = sbr_shard::scatter_rank(plan, r, fields, k.out,
+                                                 [&](void* d, size_t dp, const void* src, size_t sp, size_t w, size_t h) {
+                                                     return hipMemcpy2DAsync(d, dp, src, sp, w, h, hipMemcpyDeviceToHost,
+                                                                             k.stream) == hipSuccess ? 0 : SBR_EDEVICE;
+                                                 });
                 if (rc == SBR_OK && hipStreamSynchronize(k.stream) != hipSuccess) rc = SBR_EDEVICE;
                 if (rc != SBR_OK) { rcs[r] = rc; errs[r] = sbr_last_error(k.kid); }
             });
@@ -321,6 +335,7 @@ int run_sharded(sbr_multi* m, int64_t n_col, int64_t n_u, const std::vector<sbr_
             m->err = "rank " + std::to_string(r) + ": " + errs[r];
             return rcs[r];
         }
+    if (!rccl_gather) return SBR_OK;
 
     // phase 2, pre-checks: everything fallible before a send or receive is posted
     Rank& k0 = m->ranks[0];
@@ -360,7 +375,8 @@ int run_sharded(sbr_multi* m, int64_t n_col, int64_t n_u, const std::vector<sbr_
 // loopback transport, the per-rank sweep supplied by the caller (tests: the CPU oracle).
 // ---------------------------------------------------------------------------
 extern "C" int sbr_shard_host_run(int32_t n_ranks, int64_t n_col, int64_t n_u, int32_t n_fields, const int64_t* esz,
-                                  const int64_t* per_pt, void* const* host_out, sbr_shard_compute_fn compute, void* user)
+                                  const int64_t* per_pt, void* const* host_out, sbr_shard_compute_fn compute, void* user,
+                                  int32_t rccl_gather)
 {
     if (n_ranks <= 0 || n_col <= 0 || n_u <= 0 || n_fields <= 0 || !esz || !per_pt || !host_out || !compute)
         return SBR_EARG;
@@ -382,6 +398,13 @@ extern "C" int sbr_shard_host_run(int32_t n_ranks, int64_t n_col, int64_t n_u, i
         for (size_t o : sbr_shard::field_offsets(plan, r, fields)) fp.push_back(blocks[r].data() + o);
         const int rc = compute(user, r, plan.cols[r], ids.data(), fp.data());
         if (rc) return rc;
+    }
+    if (!rccl_gather) { // direct transport: every rank copies its own block into the caller's arrays
+        for (int r = 0; r < n_ranks; r++) {
+            const int rc = sbr_shard::scatter_rank(plan, r, fields, blocks[r].data(), sbr_shard::host_copy2d);
+            if (rc) return rc;
+        }
+        return SBR_OK;
     }
     std::vector<char> gathered(plan.gather_bytes() + 1, 0);
     sbr_shard::LoopbackTransport tr;

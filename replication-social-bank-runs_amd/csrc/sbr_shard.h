@@ -10,7 +10,9 @@
 //  * gather:  every rank's block lands in rank 0's gather buffer at block offset off[r]
 //             (rank 0 copies its own; ranks ≥ 1 send, rank 0 receives — posted together);
 //  * scatter: field f of rank r's block is a (cols[r] × row) matrix copied with pitch N·row
-//             into the caller's u-fastest array at row offset r·row.
+//             into the caller's u-fastest array at row offset r·row — either by each rank
+//             from its own block (direct: host destinations, every GPU's own PCIe link, no
+//             collective) or by rank 0 from the gathered blocks.
 #pragma once
 
 #include <stddef.h>
@@ -108,23 +110,32 @@ inline int gather(const Plan& p, Transport& t, const std::vector<const void*>& b
     return rc ? rc : rw;
 }
 
-// scatter the gathered blocks into the callers' arrays:
+// rank r's block into the callers' arrays (its columns r, r+N, … of every field):
 //   copy2d(dst, dpitch, src, spitch, width, height) -> int (0 = ok)
+template <class Copy2D>
+int scatter_rank(const Plan& p, int r, const std::vector<Field>& fields, const void* block, Copy2D&& copy2d)
+{
+    if (p.cols[r] == 0) return 0;
+    const char* blk = (const char*)block;
+    const std::vector<size_t> fo = field_offsets(p, r, fields);
+    for (size_t i = 0; i < fields.size(); i++) {
+        const Field& f = fields[i];
+        if (!f.host) continue;
+        const size_t row = (size_t)p.n_u * f.per_pt * f.esz;
+        const int rc = copy2d((char*)f.host + (size_t)r * row, (size_t)p.N * row, blk + fo[i], row, row,
+                              (size_t)p.cols[r]);
+        if (rc) return rc;
+    }
+    return 0;
+}
+
+// every rank's block from the gathered buffer (rank 0's memory) into the callers' arrays
 template <class Copy2D>
 int scatter(const Plan& p, const std::vector<Field>& fields, const void* gathered, Copy2D&& copy2d)
 {
     for (int r = 0; r < p.N; r++) {
-        if (p.cols[r] == 0) continue;
-        const char* blk = (const char*)gathered + (size_t)p.off[r] * p.per_col;
-        const std::vector<size_t> fo = field_offsets(p, r, fields);
-        for (size_t i = 0; i < fields.size(); i++) {
-            const Field& f = fields[i];
-            if (!f.host) continue;
-            const size_t row = (size_t)p.n_u * f.per_pt * f.esz;
-            const int rc = copy2d((char*)f.host + (size_t)r * row, (size_t)p.N * row, blk + fo[i], row, row,
-                                  (size_t)p.cols[r]);
-            if (rc) return rc;
-        }
+        const int rc = scatter_rank(p, r, fields, (const char*)gathered + (size_t)p.off[r] * p.per_col, copy2d);
+        if (rc) return rc;
     }
     return 0;
 }

@@ -24,6 +24,7 @@ _P = ctypes.c_void_p
 SBR_OK, SBR_EARG, SBR_EDEVICE, SBR_ENOMEM = 0, -1, -2, -3
 SBR_FLAG_EXHAUSTIVE = 0x1
 SBR_FLAG_READY_SWEEP = 0x2
+SBR_FLAG_RCCL_GATHER = 0x4
 SBR_FLAG_DIAG_STOP_AFTER_BUFFER = 0x100
 SBR_FLAG_DIAG_STOP_AFTER_BISECT = 0x200
 SBR_FLAG_DIAG_COUNT_AW_BLOCKS = 0x400

@@ -69,10 +69,13 @@ def test_multi_context_ccall_style(engine):
         L.sbr_free(ctx)
 
 
-def test_multi_baseline_fig5_and_early_exit(engine, multi):
+@pytest.mark.parametrize("flags", [0, _lib.SBR_FLAG_RCCL_GATHER], ids=["direct", "rccl_gather"])
+def test_multi_baseline_fig5_and_early_exit(engine, multi, flags):
+    """Both result transports of an n-device context (each rank's own D2H; the RCCL gather to
+    device 0 then one scatter) give the single-device arrays."""
     g = sbr.fig5_grid(500)
     for ee in (0, 5):
-        a = multi.sweep_baseline(g, early_exit=ee)
+        a = multi.sweep_baseline(g, early_exit=ee, flags=flags)
         b = engine.sweep_baseline(g, early_exit=ee)
         for k in (*FIELDS, "status", "iters"):
             assert_same(a[k], b[k], f"{k} (early_exit={ee})")
