@@ -255,6 +255,26 @@ int sbr_sweep_hetero_batch_dev(sbr_ctx* ctx, void* stream, int64_t n_batch, int3
                                const double* dist, const double* eta, const double* t_end, double x0,
                                const double* u, int64_t n_col, int64_t n_u, double p, double kappa, double lambda,
                                const sbr_opts* opts, sbr_result_soa* out, double* tau_in, double* tau_out);
+/*
+ * Heterogeneity equilibria on the caller's learning knots — solve_equilibrium_hetero(lr_hetero,
+ * econ) + get_AW_functions_hetero! (heterogeneity_solver.jl:241-293, 316-402) for one
+ * LearningResultsHetero: its knot grid t[n] and group CDF values G[n][K] (knot-major, the
+ * learning_cdfs' coefficients, heterogeneity_learning.jl:82-86), its βs / dist (learning.params;
+ * the pdfs follow from compute_pdf_hetero, :114-134) and tspan end t_end; n_u values of u sharing
+ * (p, κ, λ, η).  No learning ODE runs: the scripts learn once (2_heterogeneity.jl:59) and solve per
+ * u.  Knots, group CDFs and the K hazard paths stay resident while the inputs repeat (compared by
+ * value), like sbr_equilibrium_on_knots.  out->tau_in_unc / tau_out_unc are ignored; the per-group
+ * buffers go to tau_in / tau_out ([n_u][K], may be NULL).  Paths (may be NULL, capacity cap):
+ * hr = HR_k on the τ̄ grid (knots <= η, then η: hazard_rate's explicit grid, solver.jl:163-164) at
+ * hr + k·cap, *n_tau entries each (0 after the hazard's BoundsError) — SolvedModelHetero.HRs
+ * (:255); with n_u == 1, aw_total = AW_total on the knots (NaN without a run).  Synchronous.
+ */
+int sbr_hetero_equilibrium_on_knots(sbr_ctx* ctx, int32_t K, const double* t, const double* G, int64_t n_knots,
+                                    const double* betas, const double* dist, double eta, double t_end, const double* u,
+                                    int64_t n_u, double p, double kappa, double lambda, const sbr_opts* opts,
+                                    sbr_result_soa* out, double* tau_in, double* tau_out, double* hr, double* aw_total,
+                                    int64_t cap, int64_t* n_tau);
+
 /* One heterogeneity equilibrium with what scripts/2_heterogeneity.jl plots
  * (aggregate_withdrawals_hetero.pdf): learning knots t[n] and group CDFs G[n][K]
  * (solve_SInetwork_hetero), the per-group buffers, and AW_total on the knots

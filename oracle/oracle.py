@@ -347,6 +347,34 @@ def hetero_point_paths(betas, dist, eta, t_end, u, p, kappa, lam, x0=1e-4, cap=1
                 t=t[:n].copy(), G=G[:n * K].reshape(n, K).copy(), aw_total=aw[:n].copy())
 
 
+def hetero_equilibrium_knots(t, G, betas, dist, eta, t_end, u, p, kappa, lam):
+    """solve_equilibrium_hetero(lr_hetero, econ) on caller knots t [n], G [n, K] for each u
+    (sbro_hetero_equilibrium_knots): per-u arrays, per-group buffers [n_u, K], HR_k on the τ̄
+    grid [K, n_hr] and, for one u, AW_total on the knots."""
+    L = lib()
+    L.sbro_hetero_equilibrium_knots.restype = None
+    L.sbro_hetero_equilibrium_knots.argtypes = [_I32, _P, _P, _I64, _P, _P, _D, _D, _P, _I64, _D, _D, _D] + [_P] * 10
+    t = np.ascontiguousarray(t, np.float64)
+    G = np.ascontiguousarray(G, np.float64)
+    betas = np.ascontiguousarray(betas, np.float64)
+    dist = np.ascontiguousarray(dist, np.float64)
+    u = np.ascontiguousarray(np.atleast_1d(u), np.float64)
+    n, K, nu = len(t), len(dist), len(u)
+    o = {k: np.empty(nu) for k in ("xi", "aw_max", "tol")}
+    o["status"] = np.empty(nu, np.uint32)
+    o["iters"] = np.empty(nu, np.int32)
+    tin, tout = np.empty((nu, K)), np.empty((nu, K))
+    hr = np.full((K, n + 1), np.nan)
+    nhr = np.zeros(1, np.int64)
+    aw = np.full(n, np.nan) if nu == 1 else None
+    L.sbro_hetero_equilibrium_knots(K, _ptr(t), _ptr(G), n, _ptr(betas), _ptr(dist), eta, t_end, _ptr(u), nu, p,
+                                    kappa, lam, _ptr(o["xi"]), _ptr(o["aw_max"]), _ptr(o["tol"]), _ptr(o["status"]),
+                                    _ptr(o["iters"]), _ptr(tin), _ptr(tout), _ptr(hr), _ptr(nhr), _ptr(aw))
+    k = int(nhr[0])
+    o.update(tau_in_unc=tin, tau_out_unc=tout, hr=hr[:, :k].copy(), n_hr=k, aw_total=aw)
+    return o
+
+
 def set_initdt_den(d: int = 6) -> None:
     """ode_determine_initdt's exponent 1/d (6: Tsit5's order + 1, the restatement's choice);
     other values only for tools/initdt_evidence.py."""

@@ -1092,6 +1092,74 @@ static double aw_max_hetero(double xi, const double* tin, const double* tout, co
 
 /* Hetero sweep: column c has group rates betas[c*K .. c*K+K), η = eta[c],
  * tspan = (0, t_end[c]); every u.  Outputs u-fastest; tin/tout are [pt][K]. */
+/* heterogeneity_solver.jl:241-293 + get_AW_hetero on one column's knots (t[n], I[n][K]):
+ * compute_pdf_hetero, the K hazards on the explicit grid, then per u the buffers, compute_ξ_hetero
+ * and AW_max.  hr_out (may be NULL): HR_k on the τ̄ grid at hr_out + k·(n+1) (*n_hr entries, 0
+ * after a BoundsError); aw_path (may be NULL, n_u = 1): AW_total on the knots. */
+static void hetero_column(int32_t K, const double* bk, const double* dist, const double* t, const double* I,
+                          int64_t n, double eta, double t_end, const double* u, int64_t n_u, double p, double kappa,
+                          double lambda, int32_t max_iters, double tolerance, uint32_t lbits, double* xi,
+                          double* aw_max, double* tol, uint32_t* status, int32_t* iters, double* tin_out,
+                          double* tout_out, double* hr_out, int64_t* n_hr, double* aw_path)
+{
+    /* compute_pdf_hetero: pdf_k = (1 − I_k) β_k ω at the knots */
+    double* g = (double*)malloc((size_t)(n > 0 ? n : 1) * sizeof(double));
+    double* cum = (double*)malloc((size_t)(n > 0 ? n : 1) * sizeof(double));
+    hazard_t hz[MAXK];
+    int hz_oob = 0;
+    for (int k = 0; k < K; k++) {
+        for (int64_t i = 0; i < n; i++) {
+            const double* Ii = I + i * K;
+            double w = dist[0] * Ii[0];
+            for (int j = 1; j < K; j++) w = w + dist[j] * Ii[j];
+            g[i] = ((1.0 - Ii[k]) * bk[k]) * w;
+        }
+        hazard_rate(t, g, n, p, lambda, eta, 1, &hz[k]);
+        hz_oob |= hz[k].oob;
+    }
+    if (n_hr) *n_hr = hz_oob ? 0 : hz[0].n;
+    if (hr_out && !hz_oob)
+        for (int k = 0; k < K; k++) memcpy(hr_out + (size_t)k * (n + 1), hz[k].hr, (size_t)hz[k].n * sizeof(double));
+    for (int64_t j = 0; j < n_u; j++) {
+        double tin[MAXK], tout[MAXK];
+        uint32_t s = 0;
+        double x = NAN, tl = INFINITY, am = NAN;
+        int32_t it = 0;
+        if (hz_oob) {
+            s = SBR_OOB;
+            for (int k = 0; k < K; k++) tin[k] = tout[k] = NAN;
+        } else {
+            int all_eq = 1;
+            for (int k = 0; k < K; k++) {
+                optimal_buffer(u[j], hz[k].tau, hz[k].hr, hz[k].n, t_end, &tin[k], &tout[k]);
+                all_eq &= (tin[k] == tout[k]);
+            }
+            if (all_eq) {
+                s = SBR_NO_RUN_HR_BELOW_U | SBR_CONVERGED;
+                tl = 0.0;
+            } else {
+                s = compute_xi_hetero(tin, tout, dist, K, t, I, n, kappa, max_iters, tolerance, &x, &tl, &it);
+                if (s == SBR_RUN) {
+                    int oob = 0;
+                    am = aw_max_hetero(x, tin, tout, dist, K, t, I, n, aw_path ? aw_path : cum, &oob);
+                    if (oob) { s = SBR_OOB; x = NAN; tl = INFINITY; am = NAN; }
+                    else s = SBR_RUN | SBR_CONVERGED;
+                }
+            }
+        }
+        xi[j] = x; tol[j] = tl; aw_max[j] = am;
+        status[j] = s | lbits;
+        if (iters) iters[j] = it;
+        for (int k = 0; k < K; k++) {
+            if (tin_out) tin_out[j * K + k] = tin[k];
+            if (tout_out) tout_out[j * K + k] = tout[k];
+        }
+    }
+    for (int k = 0; k < K; k++) hazard_free(&hz[k]);
+    free(g);
+    free(cum);
+}
+
 int sbro_sweep_hetero(int32_t K, const double* betas, const double* dist, const double* eta, const double* t_end,
                       double x0, const double* u, int64_t n_col, int64_t n_u, double p, double kappa, double lambda,
                       int32_t max_iters, double tolerance, int32_t nthreads, double* xi, double* aw_max, double* tol,
@@ -1113,65 +1181,27 @@ int sbro_sweep_hetero(int32_t K, const double* betas, const double* dist, const 
         const ode_sys_t S = {rhs_hetero, K <= MAXJ ? jac_hetero : NULL, &hc};
         const double e = 2.220446049250313e-16;
         if (ode_solve(&S, K, 0.0, t_end[c], x0v, e, e, SBR_DEFAULT_ODE_MAXITERS, &kn, &st)) { err |= 1; continue; }
-        int64_t n = kn.n;
-        if (nknots) nknots[c] = n;
-        /* compute_pdf_hetero: pdf_k = (1 − I_k) β_k ω at the knots */
-        double* g = (double*)malloc((size_t)n * sizeof(double));
-        double* cum = (double*)malloc((size_t)n * sizeof(double));
-        hazard_t hz[MAXK];
-        int hz_oob = 0;
-        for (int k = 0; k < K; k++) {
-            for (int64_t i = 0; i < n; i++) {
-                const double* I = kn.x + i * K;
-                double w = dist[0] * I[0];
-                for (int j = 1; j < K; j++) w = w + dist[j] * I[j];
-                g[i] = ((1.0 - I[k]) * bk[k]) * w;
-            }
-            hazard_rate(kn.t, g, n, p, lambda, eta[c], 1, &hz[k]);
-            hz_oob |= hz[k].oob;
-        }
-        for (int64_t j = 0; j < n_u; j++) {
-            int64_t o = c * n_u + j;
-            double tin[MAXK], tout[MAXK];
-            uint32_t s = 0;
-            double x = NAN, tl = INFINITY, am = NAN;
-            int32_t it = 0;
-            if (hz_oob) {
-                s = SBR_OOB;
-                for (int k = 0; k < K; k++) tin[k] = tout[k] = NAN;
-            } else {
-                int all_eq = 1;
-                for (int k = 0; k < K; k++) {
-                    optimal_buffer(u[j], hz[k].tau, hz[k].hr, hz[k].n, t_end[c], &tin[k], &tout[k]);
-                    all_eq &= (tin[k] == tout[k]);
-                }
-                if (all_eq) {
-                    s = SBR_NO_RUN_HR_BELOW_U | SBR_CONVERGED;
-                    tl = 0.0;
-                } else {
-                    s = compute_xi_hetero(tin, tout, dist, K, kn.t, kn.x, n, kappa, max_iters, tolerance, &x, &tl, &it);
-                    if (s == SBR_RUN) {
-                        int oob = 0;
-                        am = aw_max_hetero(x, tin, tout, dist, K, kn.t, kn.x, n, cum, &oob);
-                        if (oob) { s = SBR_OOB; x = NAN; tl = INFINITY; am = NAN; }
-                        else s = SBR_RUN | SBR_CONVERGED;
-                    }
-                }
-            }
-            xi[o] = x; tol[o] = tl; aw_max[o] = am;
-            status[o] = s | (st.status & (SBR_ODE_MAXITERS | SBR_STIFF_SWITCH | SBR_ODE_FAILED));
-            if (iters) iters[o] = it;
-            for (int k = 0; k < K; k++) {
-                if (tin_out) tin_out[o * K + k] = tin[k];
-                if (tout_out) tout_out[o * K + k] = tout[k];
-            }
-        }
-        for (int k = 0; k < K; k++) hazard_free(&hz[k]);
-        free(g);
-        free(cum);
+        if (nknots) nknots[c] = kn.n;
+        const int64_t o = c * n_u;
+        hetero_column(K, bk, dist, kn.t, kn.x, kn.n, eta[c], t_end[c], u, n_u, p, kappa, lambda, max_iters, tolerance,
+                      st.status & (SBR_ODE_MAXITERS | SBR_STIFF_SWITCH | SBR_ODE_FAILED), xi + o, aw_max + o, tol + o,
+                      status + o, iters ? iters + o : NULL, tin_out ? tin_out + o * K : NULL,
+                      tout_out ? tout_out + o * K : NULL, NULL, NULL, NULL);
         knots_free(&kn);
     }
     return err ? -1 : 0;
+}
+
+/* solve_equilibrium_hetero(lr_hetero, econ) on caller knots (a LearningResultsHetero's grid and
+ * group CDFs, I[n][K]) for n_u values of u; hr_out [K][n+1], aw_path [n] (n_u = 1) may be NULL */
+void sbro_hetero_equilibrium_knots(int32_t K, const double* t, const double* I, int64_t n, const double* betas,
+                                   const double* dist, double eta, double t_end, const double* u, int64_t n_u,
+                                   double p, double kappa, double lambda, double* xi, double* aw_max, double* tol,
+                                   uint32_t* status, int32_t* iters, double* tin, double* tout, double* hr_out,
+                                   int64_t* n_hr, double* aw_path)
+{
+    hetero_column(K, betas, dist, t, I, n, eta, t_end, u, n_u, p, kappa, lambda, 500, 1e-12, 0, xi, aw_max, tol,
+                  status, iters, tin, tout, hr_out, n_hr, aw_path);
 }
 
 /* ======================================================================== */

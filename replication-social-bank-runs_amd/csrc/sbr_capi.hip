@@ -108,6 +108,15 @@ struct sbr_ctx {
     double kn_key[4] = {};
     std::vector<double> kn_t, kn_G, kn_hr; // host copies of the resident knots and HR
     int32_t kn_m = 0, kn_ntau = 0;         // knots <= η; τ̄ entries (0: the hazard's BoundsError)
+    // sbr_hetero_equilibrium_on_knots: the same for a LearningResultsHetero (knots, K group CDFs,
+    // the K hazard paths), keyed by K, n, t, G, βs, dist, η, p, λ
+    char* hk_dev = nullptr;
+    char* hk_pin = nullptr;
+    size_t hk_cap_k = 0, hk_cap_u = 0;
+    bool hk_valid = false;
+    int64_t hk_n = 0;
+    int32_t hk_K = 0, hk_ntau = 0;
+    std::vector<double> hk_key, hk_t, hk_G, hk_hr;
     int lds_cap = 0, lds_cap_b = 0;
     int lds_smem = 0;
     // kernel timing (HIP event pairs on the launching stream), opt-in via sbr_timing_enable
@@ -801,6 +810,8 @@ int sbr_free(sbr_ctx* c)
     if (c->stage) (void)hipFree(c->stage);
     if (c->kn_dev) (void)hipFree(c->kn_dev);
     if (c->kn_pin) (void)hipHostFree(c->kn_pin);
+    if (c->hk_dev) (void)hipFree(c->hk_dev);
+    if (c->hk_pin) (void)hipHostFree(c->hk_pin);
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->ev_grid) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(c->stream);
@@ -1205,6 +1216,8 @@ int ensure_knots(sbr_ctx* c, size_t n, size_t n_u)
     while (cu < n_u) cu *= 2;
     if (c->kn_dev) (void)hipFree(c->kn_dev);
     if (c->kn_pin) (void)hipHostFree(c->kn_pin);
+    if (c->hk_dev) (void)hipFree(c->hk_dev);
+    if (c->hk_pin) (void)hipHostFree(c->hk_pin);
     c->kn_dev = c->kn_pin = nullptr;
     c->kn_cap_k = c->kn_cap_u = 0;
     c->kn_valid = false;
@@ -1216,9 +1229,178 @@ int ensure_knots(sbr_ctx* c, size_t n, size_t n_u)
     return SBR_OK;
 }
 
+// sbr_hetero_equilibrium_on_knots' device block (and pinned mirror) for ck knots, cu u values and
+// K <= 8 groups: [counters | βs, dist, η | t, G packed by the call's n | HR, I (K·ck each) |
+// t_end, u | results, buffers, AW_total path]
+struct HeteroKnotLayout {
+    size_t sc, tg, hr, hri, u, res, bytes;
+    HeteroKnotLayout(size_t ck, size_t cu)
+    {
+        sc = 64;
+        tg = 256;
+        hr = tg + 8 * ck * 9;
+        hri = hr + 8 * ck * 8;
+        u = hri + 8 * ck * 8;
+        res = u + 8 * (cu + 8);
+        bytes = res + 8 * (5 * cu + 16 * cu + ck) + 256;
+    }
+};
+
+int ensure_hetero_knots(sbr_ctx* c, size_t n, size_t n_u)
+{
+    if (n <= c->hk_cap_k && n_u <= c->hk_cap_u) return SBR_OK;
+    size_t ck = c->hk_cap_k > 8192 ? c->hk_cap_k : 8192, cu = c->hk_cap_u > 64 ? c->hk_cap_u : 64;
+    while (ck < n) ck *= 2;
+    while (cu < n_u) cu *= 2;
+    if (c->hk_dev) (void)hipFree(c->hk_dev);
+    if (c->hk_pin) (void)hipHostFree(c->hk_pin);
+    c->hk_dev = c->hk_pin = nullptr;
+    c->hk_cap_k = c->hk_cap_u = 0;
+    c->hk_valid = false;
+    const HeteroKnotLayout Lh(ck, cu);
+    HIP_TRY(c, hipMalloc(&c->hk_dev, Lh.bytes), SBR_ENOMEM);
+    HIP_TRY(c, hipHostMalloc(&c->hk_pin, Lh.bytes), SBR_ENOMEM);
+    c->hk_cap_k = ck;
+    c->hk_cap_u = cu;
+    return SBR_OK;
+}
+
 }  // namespace
 
 extern "C" {
+
+int sbr_hetero_equilibrium_on_knots(sbr_ctx* c, int32_t K, const double* t, const double* G, int64_t n,
+                                    const double* betas, const double* dist, double eta, double t_end, const double* u,
+                                    int64_t n_u, double p, double kappa, double lambda, const sbr_opts* opts,
+                                    sbr_result_soa* out, double* tau_in, double* tau_out, double* hr, double* aw_total,
+                                    int64_t cap, int64_t* n_tau)
+{
+    SBR_ON_RANK0(c, sbr_hetero_equilibrium_on_knots(c, K, t, G, n, betas, dist, eta, t_end, u, n_u, p, kappa, lambda, opts, out, tau_in, tau_out, hr, aw_total, cap, n_tau));
+    if (!c || !t || !G || !betas || !dist || !u || !out) return SBR_EARG;
+    if (K != 1 && K != 2 && K != 3 && K != 4 && K != 8) return fail(c, SBR_EARG, "K must be 1, 2, 3, 4 or 8");
+    if (n < 1 || n > (1 << 24) || n_u < 1 || n_u > (1 << 24)) return fail(c, SBR_EARG, "knot / u count");
+    double dsum = 0.0;
+    for (int k = 0; k < K; k++) {
+        if (!(dist[k] >= 0.0)) return fail(c, SBR_EARG, "ArgumentError: distribution weights must be non-negative");
+        if (!(betas[k] > 0.0)) return fail(c, SBR_EARG, "ArgumentError: all learning rates must be positive");
+        dsum = dsum + dist[k];
+    }
+    if (!(fabs(dsum - 1.0) < 1e-10)) return fail(c, SBR_EARG, "ArgumentError: distribution must sum to 1");
+    if (!scalars_valid(0.0, p, kappa, lambda) || !(eta > 0) || !(t_end > 0))
+        return fail(c, SBR_EARG, "ArgumentError: eta/t_end/p/kappa/lambda");
+    for (int64_t j = 0; j < n_u; j++)
+        if (!(u[j] >= 0.0)) return fail(c, SBR_EARG, "ArgumentError: u must be non-negative");
+    if (!(t[0] == t[0])) return fail(c, SBR_EARG, "ArgumentError: knots must be sorted");
+    for (int64_t i = 0; i + 1 < n; i++)
+        if (!(t[i] <= t[i + 1])) return fail(c, SBR_EARG, "ArgumentError: knots must be sorted");
+    if (aw_total && n_u != 1) return fail(c, SBR_EARG, "the AW_total path needs n_u == 1");
+    if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
+    const sbr_opts o = resolve(opts);
+    int rc = ensure_hetero_knots(c, (size_t)n, (size_t)n_u);
+    if (rc) return rc;
+    const HeteroKnotLayout Lh(c->hk_cap_k, c->hk_cap_u);
+    // the explicit-grid hazard (heterogeneity_solver.jl:255, solver.jl:163-164): τ̄ = knots <= η,
+    // then η; pdf(η) is a BoundsError before the first knot or past the last one
+    int64_t m = 0;
+    while (m < n && t[m] <= eta) m++;
+    const bool hz_oob = m == 0 || (m == n && !(n >= 2 && t[n - 1] == eta));
+    const int64_t ntau = hz_oob ? 0 : m + 1;
+    if ((hr && ntau > cap) || (aw_total && n > cap)) return fail(c, SBR_EARG, "path capacity too small");
+    std::vector<double> key;
+    key.reserve(2 * (size_t)K + 5);
+    key.push_back((double)K);
+    key.insert(key.end(), betas, betas + K);
+    key.insert(key.end(), dist, dist + K);
+    key.push_back(eta);
+    key.push_back(p);
+    key.push_back(lambda);
+    const bool hit = c->hk_valid && c->hk_n == n && c->hk_K == K && c->hk_key == key &&
+                     memcmp(c->hk_t.data(), t, (size_t)n * 8) == 0 &&
+                     memcmp(c->hk_G.data(), G, (size_t)n * K * 8) == 0;
+    char* D = c->hk_dev;
+    char* H = c->hk_pin;
+    int32_t* dcnt = (int32_t*)D;
+    double* dsc = (double*)(D + Lh.sc); // βs [K], dist [K], η
+    double* dtg = (double*)(D + Lh.tg);
+    const size_t ck = c->hk_cap_k;
+    const sbr::HeteroBufs HB{dtg, dtg + n, (double*)(D + Lh.hr), (double*)(D + Lh.hri), dcnt, dcnt + 1, dcnt + 2,
+                             (uint32_t*)(dcnt + 3), dcnt + 4, dcnt + 5, (int32_t)ck};
+    double* du = (double*)(D + Lh.u); // [t_end, u...]
+    double* dres = (double*)(D + Lh.res);
+    const size_t nu = (size_t)n_u;
+    // results: xi, aw, tol [n_u] | status, iters [n_u] int32 | tau_in, tau_out [n_u][K] | AW_total [n]
+    double* dtin = dres + 4 * nu;
+    double* dtout = dtin + nu * K;
+    double* dpath = dtout + nu * K;
+    const size_t res_bytes = (4 * nu + 2 * nu * K + (aw_total ? (size_t)n : 0)) * 8;
+    if (!hit) c->hk_valid = false;
+    rc = fenced(c, nullptr, false, [&](hipStream_t s) -> int {
+        sbr::LearnArgs la{0.0, o.ode_reltol, o.ode_abstol, p, lambda, o.ode_maxiters, 1, 0, 0, nullptr, nullptr};
+        if (!hit) {
+            memset(H, 0, Lh.tg);
+            int32_t* hc = (int32_t*)H;
+            hc[0] = (int32_t)n;
+            double* hs = (double*)(H + Lh.sc);
+            memcpy(hs, betas, (size_t)K * 8);
+            memcpy(hs + K, dist, (size_t)K * 8);
+            hs[2 * K] = eta;
+            memcpy(H + Lh.tg, t, (size_t)n * 8);
+            memcpy(H + Lh.tg + (size_t)n * 8, G, (size_t)n * K * 8);
+            HIP_TRY(c, hipMemcpyAsync(D, H, Lh.tg + (size_t)n * (K + 1) * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+            HIP_TRY(c, sbr::launch_hetero(K, dsc, dsc + K, dsc + 2 * K, nullptr, nullptr, la, sbr::HeteroEqArgs{},
+                                          HB, sbr::ResultSoA{}, nullptr, nullptr, s, 2), SBR_EDEVICE);
+            for (int k = 0; k < K && ntau > 0; k++)
+                HIP_TRY(c, hipMemcpyAsync(H + Lh.hr + (size_t)k * ck * 8, D + Lh.hr + (size_t)k * ck * 8,
+                                          (size_t)ntau * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+            HIP_TRY(c, hipMemcpyAsync(H, D, 32, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        }
+        double* hu = (double*)(H + Lh.u);
+        hu[0] = t_end;
+        memcpy(hu + 1, u, nu * 8);
+        HIP_TRY(c, hipMemcpyAsync(du, hu, (nu + 1) * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+        sbr::HeteroEqArgs ea{kappa, 1e-12, (int32_t)n_u, o.hetero_max_iters, het_lds(c),
+                             (o.flags & SBR_FLAG_EXHAUSTIVE) ? 1 : 0, (o.flags >> 8) & 7, aw_total ? dpath : nullptr};
+        const sbr::ResultSoA r{dres, nullptr, nullptr, dres + nu, dres + 2 * nu, (uint32_t*)(dres + 3 * nu),
+                               (int32_t*)(dres + 3 * nu) + nu};
+        HIP_TRY(c, sbr::launch_hetero(K, dsc, dsc + K, dsc + 2 * K, du, du + 1, la, ea, HB, r, dtin, dtout, s, 1),
+                SBR_EDEVICE);
+        HIP_TRY(c, hipMemcpyAsync(H + Lh.res, D + Lh.res, res_bytes, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
+        return SBR_OK;
+    });
+    if (rc) return rc;
+    if (!hit) {
+        const int32_t* hc = (const int32_t*)H;
+        if (hc[1] != (int32_t)ntau) return fail(c, SBR_EDEVICE, "hetero hazard grid length mismatch");
+        c->hk_t.assign(t, t + n);
+        c->hk_G.assign(G, G + n * K);
+        c->hk_hr.assign((size_t)K * ntau, 0.0);
+        for (int k = 0; k < K; k++)
+            memcpy(c->hk_hr.data() + (size_t)k * ntau, H + Lh.hr + (size_t)k * ck * 8, (size_t)ntau * 8);
+        c->hk_key = key;
+        c->hk_n = n;
+        c->hk_K = K;
+        c->hk_ntau = (int32_t)ntau;
+        c->hk_valid = true;
+    }
+    const double* hres = (const double*)(H + Lh.res);
+    if (out->xi) memcpy(out->xi, hres, nu * 8);
+    if (out->aw_max) memcpy(out->aw_max, hres + nu, nu * 8);
+    if (out->tol) memcpy(out->tol, hres + 2 * nu, nu * 8);
+    if (out->status) memcpy(out->status, hres + 3 * nu, nu * 4);
+    if (out->iters) memcpy(out->iters, (const int32_t*)(hres + 3 * nu) + nu, nu * 4);
+    if (tau_in) memcpy(tau_in, hres + 4 * nu, nu * K * 8);
+    if (tau_out) memcpy(tau_out, hres + 4 * nu + nu * K, nu * K * 8);
+    if (n_tau) *n_tau = ntau;
+    if (hr)
+        for (int k = 0; k < K; k++) memcpy(hr + (size_t)k * cap, c->hk_hr.data() + (size_t)k * ntau, (size_t)ntau * 8);
+    if (aw_total) {
+        const bool run = (((const uint32_t*)(hres + 3 * nu))[0] & SBR_RUN) != 0;
+        if (run) memcpy(aw_total, hres + 4 * nu + 2 * nu * K, (size_t)n * 8);
+        else for (int64_t i = 0; i < n; i++) aw_total[i] = NAN;
+    }
+    return SBR_OK;
+}
 
 int sbr_equilibrium_on_knots(sbr_ctx* c, const double* t, const double* G, int64_t n, double beta, double eta,
                              double t_end, const double* u, int64_t n_u, double p, double kappa, double lambda,

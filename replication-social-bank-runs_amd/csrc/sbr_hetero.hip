@@ -801,6 +801,92 @@ __global__ __launch_bounds__(64) void learn_hetero_wave_kernel(const double* __r
     }
 }
 
+// The K hazards (heterogeneity_solver.jl:255: hazard_rate on the explicit grid = the learning
+// knots, η always appended) of a column whose knots and group CDFs are already in L — a
+// LearningResultsHetero the caller holds (sbr_hetero_equilibrium_on_knots).  The streamed hazard
+// of learn_hetero_wave_kernel, operation for operation, over that grid: pdf_k at a knot is
+// compute_pdf_hetero (heterogeneity_learning.jl:114-134), rhs_k of the knot's state — the FSAL
+// value the learning kernel streams.  One wave per column, lane k = group k.  Knots starting
+// after η make pdf(η) the interpolant's BoundsError (SBR_OOB) like an η past the last knot.
+template <int K>
+__global__ __launch_bounds__(64) void hazard_hetero_kernel(const double* __restrict__ betas,
+                                                           const double* __restrict__ dist,
+                                                           const double* __restrict__ eta, LearnArgs a, HeteroBufs L)
+{
+    const int c = blockIdx.x;
+    const int lane = threadIdx.x;
+    const bool act = lane < K;
+    const WaveRow<K> R(lane, betas + (size_t)c * K, dist);
+    const double ETA = eta[c];
+    const size_t cap = (size_t)L.cap;
+    const double* __restrict__ T = L.t + (size_t)c * cap;
+    const double* __restrict__ Gv = L.G + (size_t)c * cap * K;
+    double* __restrict__ H = L.hr + ((size_t)c * K + R.kk) * cap;
+    double* __restrict__ HI = L.hrI + ((size_t)c * K + R.kk) * cap;
+    const int n = L.n_knots[c];
+    uint32_t st = L.status[c];
+    const double p = a.p, lam = a.lam;
+    int m = 0;
+    double tprev = 0.0, Ik = 0.0, eprev = 0.0, gprev = 0.0;
+    bool past = false;
+    for (int i = 0; i < n && !past; i++) {
+        const double t = T[i];
+        const double g = R.rhs(Gv[(size_t)i * K + R.kk]);
+        if (t <= ETA) {
+            const double E = sbr_exp(lam * t);
+            const double e = E * g;
+            Ik = (m == 0) ? 0.0 : Ik + (0.5 * (eprev + e)) * (t - tprev);
+            if (act) { H[m] = (p * E) * g; HI[m] = Ik; }
+            eprev = e;
+            gprev = g;
+            m++;
+            tprev = t;
+        } else if (m == 0) {
+            st |= SBR_OOB; // η before the first knot
+            break;
+        } else {
+            past = true; // pdf(η) on bracket [i-1, i]
+            const double d = (ETA - tprev) / (t - tprev);
+            const double E = sbr_exp(lam * ETA);
+            const double pe = gprev * (1.0 - d) + g * d;
+            const double e = E * pe;
+            Ik = Ik + (0.5 * (eprev + e)) * (ETA - tprev);
+            if (act) { H[m] = (p * E) * pe; HI[m] = Ik; }
+            m++;
+        }
+    }
+    int n_le = m;
+    if (past) {
+        n_le = m - 1;
+    } else if (!(st & SBR_OOB)) {
+        if (n >= 2 && tprev == ETA) { // η is the last knot: pdf(η) = its value
+            const double E = sbr_exp(lam * ETA);
+            const double pe = 0.0 + gprev * 1.0;
+            if (act) { H[m] = (p * E) * pe; HI[m] = Ik; }
+            m++;
+        } else {
+            st |= SBR_OOB;
+        }
+    }
+    if (m > 0 && !(st & SBR_OOB)) {
+        __threadfence_block();
+        const double omp = 1.0 - p;
+        double* __restrict__ Hc = L.hr + (size_t)c * K * cap;
+        const double* __restrict__ HIc = L.hrI + (size_t)c * K * cap;
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const double Ieta = HIc[(size_t)k * cap + m - 1];
+            for (int i = lane; i < m; i += 64)
+                Hc[(size_t)k * cap + i] = Hc[(size_t)k * cap + i] / ((p * HIc[(size_t)k * cap + i]) + (omp * Ieta));
+        }
+    }
+    if (lane == 0) {
+        L.n_tau[c] = (st & SBR_OOB) ? 0 : m;
+        L.n_le[c] = (st & SBR_OOB) ? 0 : n_le;
+        L.status[c] = st;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // per-point solve
 // ---------------------------------------------------------------------------
@@ -1330,6 +1416,10 @@ static hipError_t launch_hetero_k(const double* betas, const double* dist, const
                                   const double* u, const LearnArgs& la, const HeteroEqArgs& ea_in, const HeteroBufs& L,
                                   const ResultSoA& out, double* tin, double* tout, hipStream_t s, int phase)
 {
+    if (phase == 2) { // hazards of knots already in L (caller knots)
+        hipLaunchKernelGGL(hazard_hetero_kernel<K>, dim3(la.n_beta), dim3(64), 0, s, betas, dist, eta, la, L);
+        return hipGetLastError();
+    }
     if (phase == 0) {
 #if SBR_HET_LEARN_WAVE
         hipLaunchKernelGGL(learn_hetero_wave_kernel<K>, dim3(la.n_beta), dim3(64), 0, s, betas, dist, eta, t_end, la, L);

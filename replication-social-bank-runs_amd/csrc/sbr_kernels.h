@@ -182,6 +182,8 @@ hipError_t launch_social_iter(const SocialArgs& a, const SocialArgs& p, const So
                               int n_inner, const int32_t* work, const int32_t* count, int32_t* work_out,
                               int32_t* count_out, hipStream_t s);
 
+// phase 0: learning (+ the streamed hazards); 1: equilibria; 2: the hazards of knots and group
+// CDFs already in L (n_knots and status set by the caller)
 hipError_t launch_hetero(int K, const double* betas, const double* dist, const double* eta, const double* t_end,
                          const double* u, const LearnArgs& la, const HeteroEqArgs& ea, const HeteroBufs& L,
                          const ResultSoA& out, double* tin, double* tout, hipStream_t s, int phase);

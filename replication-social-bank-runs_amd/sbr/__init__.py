@@ -18,6 +18,8 @@ from .engine import (  # noqa: F401
     get_AW_functions_interest,
     solve_equilibrium_baseline,
     solve_equilibrium_hetero,
+    solve_SInetwork_hetero,
+    LearningResultsHetero,
     solve_equilibrium_interest,
     solve_equilibrium_social_learning,
     solve_learning,

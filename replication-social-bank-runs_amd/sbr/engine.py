@@ -33,6 +33,9 @@ from .model import (EconomicParameters, EconomicParametersInterest, LearningPara
 _P = ctypes.c_void_p
 
 RESULT_FIELDS = ("xi", "tau_in_unc", "tau_out_unc", "aw_max", "tol")
+# learning-level status bits a sweep point carries from its column's ODE solve
+_LEARN_BITS = (_lib.STATUS["SBR_ODE_MAXITERS"] | _lib.STATUS["SBR_STIFF_SWITCH"] | _lib.STATUS["SBR_ODE_FAILED"]
+               | _lib.STATUS["SBR_KNOT_OVERFLOW"])
 
 
 def _ptr(a: np.ndarray | None):
@@ -252,6 +255,45 @@ class Engine:
             k = nt.value
             pv = pbuf.reshape(5, cap)
             out.update(tau=pv[0, :k], hr=pv[1, :k], aw_cum=pv[2, :k], aw_out=pv[3, :k], aw_in=pv[4, :k])
+        return out
+
+    def hetero_equilibrium_on_knots(self, t, G, betas, dist, eta, t_end, u, p, kappa, lam,
+                                    paths: bool = True) -> dict:
+        """solve_equilibrium_hetero(lr_hetero, econ) + get_AW_functions_hetero! on the knots a
+        LearningResultsHetero holds (t [n], G [n, K] = the learning_cdfs' values) for each u — no
+        learning ODE (sbr_hetero_equilibrium_on_knots; knots, CDFs and the K hazards stay on the
+        GPU while the inputs repeat).  Per-u arrays, buffers [n_u, K]; with ``paths`` (one u) HR_k
+        on the τ̄ grid [K, n_tau] and AW_total on the knots."""
+        t = np.ascontiguousarray(t, np.float64)
+        G = np.ascontiguousarray(G, np.float64)
+        betas = np.ascontiguousarray(betas, np.float64)
+        dist = np.ascontiguousarray(dist, np.float64)
+        u = np.ascontiguousarray(np.atleast_1d(u), np.float64)
+        n, K, nu = len(t), len(dist), len(u)
+        if G.shape != (n, K) or betas.shape != (K,):
+            raise ArgumentError("G must be [n_knots, K] and betas [K]")
+        if paths and nu != 1:
+            raise ArgumentError("paths need a single u")
+        out = {k: np.empty(nu) for k in ("xi", "aw_max", "tol")}
+        out["status"] = np.empty(nu, np.uint32)
+        out["iters"] = np.empty(nu, np.int32)
+        tin, tout = np.empty((nu, K)), np.empty((nu, K))
+        soa = _lib.ResultSoA(_ptr(out["xi"]), None, None, _ptr(out["aw_max"]), _ptr(out["tol"]), _ptr(out["status"]),
+                             _ptr(out["iters"]))
+        cap = n + 1
+        hr = np.empty((K, cap)) if paths else None
+        aw = np.empty(cap) if paths else None
+        nt = ctypes.c_int64()
+        opts = _lib.default_opts(early_exit_nan_run=0)
+        rc = self._L.sbr_hetero_equilibrium_on_knots(self._ctx, K, _ptr(t), _ptr(G), n, _ptr(betas), _ptr(dist), eta,
+                                                     t_end, _ptr(u), nu, p, kappa, lam, ctypes.byref(opts),
+                                                     ctypes.byref(soa), _ptr(tin), _ptr(tout), _ptr(hr), _ptr(aw),
+                                                     cap, ctypes.byref(nt))
+        check(rc, self._ctx, "sbr_hetero_equilibrium_on_knots")
+        out.update(tau_in_unc=tin, tau_out_unc=tout)
+        if paths:
+            k = nt.value
+            out.update(hr=hr[:, :k], aw_total=aw[:n], n_tau=k)
         return out
 
     def sweep_hetero(self, betas, dist, eta, t_end, u, p, kappa, lam, x0=1e-4, knot_capacity: int = 16384,
@@ -636,7 +678,8 @@ def solve_equilibrium_baseline(lr: LearningResults, econ: EconomicParameters,
     cdf = lr.learning_cdf
     r = eng.equilibrium_on_knots(cdf.knots, cdf.coefs, lp.beta, econ.eta, lp.tspan[1], econ.u, econ.p, econ.kappa,
                                  econ.lam)
-    st = int(r["status"][0])
+    # the learning solve's own status bits, as a sweep point carries them (maxiters, stiff switch)
+    st = int(r["status"][0]) | (lr.status & _LEARN_BITS)
     if st & _lib.SBR_OOB:
         raise IndexError("BoundsError: interpolation outside the knot range (solver.jl, Interpolations Throw())")
     bankrun = bool(st & _lib.SBR_RUN)
@@ -740,17 +783,61 @@ class SolvedModelHetero:
     G: np.ndarray = field(repr=False)
     AW_total: np.ndarray = field(repr=False)
     AW_max: float = float("nan")
+    HRs: list = field(repr=False, default_factory=list)  # HR_k on the τ̄ grid (heterogeneity_solver.jl:255)
+    learning_results: object = field(repr=False, default=None)
 
 
-def solve_equilibrium_hetero(model: ModelParametersHetero, engine: Engine | None = None) -> SolvedModelHetero:
-    """solve_SInetwork_hetero + solve_equilibrium_hetero + get_AW_functions_hetero!
-    (heterogeneity_learning.jl:49, heterogeneity_solver.jl:241, :386) for one model."""
-    eng = engine or default_engine()
-    lp, e = model.learning, model.economic
+@dataclass
+class LearningResultsHetero:
+    """heterogeneity_model.jl LearningResultsHetero: the shared knot grid and the K group CDFs
+    (learning_cdfs[k] = LinearInterpolation(grid, G[:, k])) / PDFs of solve_SInetwork_hetero."""
+
+    params: LearningParametersHetero
+    learning_cdfs: list
+    learning_pdfs: list
+    grid: np.ndarray
+    G: np.ndarray = field(repr=False)  # [n, K], the CDFs' values (knot-major, as libsbr takes them)
+    status: int = 0
+
+
+def solve_SInetwork_hetero(lp: LearningParametersHetero, engine: Engine | None = None) -> LearningResultsHetero:
+    """heterogeneity_learning.jl:49-94 on the GPU (sbr_learn_hetero: the coupled
+    AutoTsit5(Rosenbrock23()) solve at eps(), full tspan) with compute_pdf_hetero (:114-134):
+    pdf_k = (1 − G_k)·β_k·ω, ω = Σ_j dist_j G_j (left fold)."""
     if lp.tspan[0] != 0.0:
         raise _lib.ArgumentError("the engine integrates from t = 0 (every reference call site does)")
-    r = eng.hetero_point_paths(np.array(lp.betas), np.array(lp.dist), e.eta, lp.tspan[1], e.u, e.p, e.kappa, e.lam,
-                               lp.x0)
-    st = r["status"]
-    return SolvedModelHetero(r["xi"], r["tau_in_unc"], r["tau_out_unc"], bool(st & _lib.SBR_RUN),
-                             bool(st & _lib.SBR_CONVERGED), r["tol"], st, r["t"], r["G"], r["aw_total"], r["aw_max"])
+    eng = engine or default_engine()
+    betas, dist = np.array(lp.betas), np.array(lp.dist)
+    K = len(dist)
+    r = eng.learn_hetero(betas[None, :], dist, lp.tspan[1], lp.x0, cap=16384)
+    n = int(r["n_knots"][0])
+    t, G = r["t"][0, :n].copy(), np.ascontiguousarray(r["G"][0, :n, :])
+    w = dist[0] * G[:, 0]
+    for j in range(1, K):
+        w = w + dist[j] * G[:, j]
+    cdfs = [LinearInterpolation(t, G[:, k].copy()) for k in range(K)]
+    pdfs = [LinearInterpolation(t, ((1.0 - G[:, k]) * betas[k]) * w) for k in range(K)]
+    return LearningResultsHetero(lp, cdfs, pdfs, t, G, int(r["status"][0]))
+
+
+def solve_equilibrium_hetero(lr_or_model, econ: EconomicParameters | None = None,
+                             engine: Engine | None = None) -> SolvedModelHetero:
+    """heterogeneity_solver.jl:241-293 + get_AW_functions_hetero! (:386) for one point:
+    ``solve_equilibrium_hetero(lr_hetero, econ)`` solves on the LearningResultsHetero's own
+    knots and group CDFs (sbr_hetero_equilibrium_on_knots; no learning ODE); the HRs are the
+    engine's HR_k on the τ̄ grid.  ``solve_equilibrium_hetero(model)`` (ModelParametersHetero)
+    learns first."""
+    eng = engine or default_engine()
+    if isinstance(lr_or_model, ModelParametersHetero):
+        lr, econ = solve_SInetwork_hetero(lr_or_model.learning, eng), lr_or_model.economic
+    else:
+        lr = lr_or_model
+    lp = lr.params
+    r = eng.hetero_equilibrium_on_knots(lr.grid, lr.G, np.array(lp.betas), np.array(lp.dist), econ.eta, lp.tspan[1],
+                                        econ.u, econ.p, econ.kappa, econ.lam)
+    st = int(r["status"][0]) | (lr.status & _LEARN_BITS)
+    tau = np.append(lr.grid[lr.grid <= econ.eta], econ.eta)[:r["n_tau"]]
+    HRs = [LinearInterpolation(tau, r["hr"][k]) for k in range(len(lp.dist))] if r["n_tau"] else []
+    return SolvedModelHetero(float(r["xi"][0]), r["tau_in_unc"][0], r["tau_out_unc"][0], bool(st & _lib.SBR_RUN),
+                             bool(st & _lib.SBR_CONVERGED), float(r["tol"][0]), st, lr.grid, lr.G, r["aw_total"],
+                             float(r["aw_max"][0]), HRs, lr)

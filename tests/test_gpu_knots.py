@@ -164,3 +164,87 @@ def test_unchanged_fig4_loop_equals_batched_sweep(engine):
     assert same(np.array(xi), ref["xi"][0, :k])
     assert np.isnan(ref["aw_max"][0, k:]).all()
     assert int(np.isfinite(aw).sum()) == 2718
+
+
+# ---------------------------------------------------------------- heterogeneity extension
+HFIELDS = ("xi", "aw_max", "tol")
+
+
+def check_hetero(g, o, name, paths=True):
+    for f in HFIELDS:
+        assert same(g[f], o[f]), (name, f, g[f], o[f])
+    assert np.array_equal(g["status"], o["status"]), (name, g["status"], o["status"])
+    assert np.array_equal(g["iters"], o["iters"]), name
+    for f in ("tau_in_unc", "tau_out_unc"):
+        assert same(g[f], o[f]), (name, f)
+    if paths:
+        assert g["n_tau"] == o["n_hr"], name
+        assert same(g["hr"], o["hr"]), (name, "hr")
+        if o["status"][0] & sbr.STATUS["SBR_RUN"]:
+            assert same(g["aw_total"], o["aw_total"]), (name, "aw_total")
+
+
+def test_hetero_on_caller_knots_bitwise(engine, oracle):
+    """sbr_hetero_equilibrium_on_knots on the script column's learning knots (the oracle's
+    solve_SInetwork_hetero): every field, the per-group buffers, HR_k on the τ̄ grid (the
+    SolvedModelHetero.HRs, heterogeneity_solver.jl:255) and AW_total equal the oracle on the
+    same knots; the point equals sbr_hetero_point_paths (which learns); perturbed group CDFs
+    give the perturbed knots' equilibrium."""
+    g = sbr.hetero_script_grid()
+    betas, dist = g.betas[0], g.dist
+    t, G, _ = oracle.learn_hetero(betas, dist, g.t_end[0])
+    for u in (float(g.u[0]), 0.9):
+        a = engine.hetero_equilibrium_on_knots(t, G, betas, dist, g.eta[0], g.t_end[0], u, g.p, g.kappa, g.lam)
+        o = oracle.hetero_equilibrium_knots(t, G, betas, dist, g.eta[0], g.t_end[0], u, g.p, g.kappa, g.lam)
+        check_hetero(a, o, f"u={u}")
+        pp = engine.hetero_point_paths(betas, dist, g.eta[0], g.t_end[0], u, g.p, g.kappa, g.lam)
+        assert same(a["xi"][0], pp["xi"]) and same(a["aw_max"][0], pp["aw_max"])
+        if a["status"][0] & sbr.STATUS["SBR_RUN"]:
+            assert np.array_equal(a["aw_total"], pp["aw_total"])
+    u = float(g.u[0])
+    Gp = np.ascontiguousarray(G * (1 - 1e-9))
+    a = engine.hetero_equilibrium_on_knots(t, Gp, betas, dist, g.eta[0], g.t_end[0], u, g.p, g.kappa, g.lam)
+    o = oracle.hetero_equilibrium_knots(t, Gp, betas, dist, g.eta[0], g.t_end[0], u, g.p, g.kappa, g.lam)
+    check_hetero(a, o, "perturbed")
+    b = engine.hetero_equilibrium_on_knots(t, G, betas, dist, g.eta[0], g.t_end[0], u, g.p, g.kappa, g.lam)
+    assert a["xi"][0] != b["xi"][0] or a["aw_max"][0] != b["aw_max"][0]
+
+
+def test_hetero_config4_column_u_vector(engine, oracle):
+    """A config-4 column (K = 8, Rosenbrock23 knots) with 40 u values in one call, and its
+    η past the knots (the hazard's BoundsError)."""
+    c4 = sbr.hetero_config4(64, 40, 8)
+    i = 37
+    t, G, _ = oracle.learn_hetero(c4.betas[i], c4.dist, c4.t_end[i])
+    a = engine.hetero_equilibrium_on_knots(t, G, c4.betas[i], c4.dist, c4.eta[i], c4.t_end[i], c4.u, c4.p, c4.kappa,
+                                           c4.lam, paths=False)
+    o = oracle.hetero_equilibrium_knots(t, G, c4.betas[i], c4.dist, c4.eta[i], c4.t_end[i], c4.u, c4.p, c4.kappa,
+                                        c4.lam)
+    check_hetero(a, o, "config4", paths=False)
+    assert (a["status"] & sbr.STATUS["SBR_RUN"]).any()
+    a = engine.hetero_equilibrium_on_knots(t, G, c4.betas[i], c4.dist, 2 * float(t[-1]), c4.t_end[i], 0.1, c4.p,
+                                           c4.kappa, c4.lam)
+    o = oracle.hetero_equilibrium_knots(t, G, c4.betas[i], c4.dist, 2 * float(t[-1]), c4.t_end[i], 0.1, c4.p,
+                                        c4.kappa, c4.lam)
+    check_hetero(a, o, "eta_past_knots")
+    assert a["status"][0] & sbr.STATUS["SBR_OOB"] and a["n_tau"] == 0
+
+
+def test_hetero_mirror_learns_once(engine, oracle):
+    """scripts/2_heterogeneity.jl through the mirror: solve_SInetwork_hetero once, then
+    solve_equilibrium_hetero(lr, econ) per u on lr's knots; HRs are the engine's HR_k."""
+    g = sbr.hetero_script_grid()
+    m = sbr.ModelParametersHetero.make(g.betas[0], g.dist, eta_bar=30.0, u=float(g.u[0]), p=g.p, kappa=g.kappa,
+                                       lam=g.lam)
+    lr = sbr.solve_SInetwork_hetero(m.learning, engine)
+    t, G, _ = oracle.learn_hetero(g.betas[0], g.dist, m.learning.tspan[1])
+    assert np.array_equal(lr.grid, t) and np.array_equal(lr.G, G)
+    for u in (float(g.u[0]), 0.5):
+        e = sbr.ModelParametersHetero.modify(m, u=u).economic
+        r = sbr.solve_equilibrium_hetero(lr, e, engine=engine)
+        o = oracle.hetero_equilibrium_knots(t, G, g.betas[0], g.dist, e.eta, m.learning.tspan[1], u, g.p, g.kappa,
+                                            g.lam)
+        assert r.xi == o["xi"][0] or (np.isnan(r.xi) and np.isnan(o["xi"][0]))
+        assert len(r.HRs) == len(g.dist)
+        for k, hr in enumerate(r.HRs):
+            assert np.array_equal(hr.coefs, o["hr"][k])
