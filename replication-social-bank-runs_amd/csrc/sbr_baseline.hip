@@ -1242,44 +1242,12 @@ __device__ __forceinline__ void solve_interest_point(P T, P G, P H, const Summ& 
 // The equilibria of u values [j0, j1) of column b by one workgroup of BLOCK threads (smem:
 // the dynamic LDS slab of launch_equilibrium's size).  Starts and ends uniformly; the caller
 // puts a barrier between two calls on the same workgroup (the LDS slab and flags are reused).
-// get_AW (solver.jl:495-532) of a run point on the whole τ̄ grid, written by the BLOCK threads
-// of a workgroup (τ̄ entry i by thread i mod BLOCK): AW_cum, and AW_OUT / AW_IN when asked.
-// Every entry is the exhaustive path's arithmetic (eval_range: bracket k = min(searchsortedlast,
-// n − 2), the same lerp and masks), searched afresh instead of slid, so the values are the same
-// bits; the point's AW_max came from its own (scan / branch-and-bound) solve.  Called only for a
-// run point, whose every lookup was range-checked by that solve.
-template <int BLOCK, class P>
-__device__ __forceinline__ void aw_paths_coop(P T, P G, const int n, const int ntau, const int nle,
-                                              const double ETA, const double xi, const double tin,
-                                              const double tout, double* __restrict__ aw_cum,
-                                              double* __restrict__ aw_out, double* __restrict__ aw_in)
-{
-    const double icc = (tin >= xi) ? xi : tin;
-    const double occ = (tout > xi) ? xi : tout;
-    const double G0 = lerp_at(T, G, n, ssl_range(T, 0, n - 1, 0.0), 0.0);
-    for (int i = threadIdx.x; i < ntau; i += BLOCK) {
-        const double ti = i < nle ? T[i] : ETA;
-        const double av = (ti - xi) + icc;
-        const double bv = (ti - xi) + occ;
-        const double xa = av > 0 ? av : 0.0;
-        const double xb = bv > 0 ? bv : 0.0;
-        const double gi = lerp_at(T, G, n, ssl_range(T, 0, n - 1, xa), xa);
-        const double go = lerp_at(T, G, n, ssl_range(T, 0, n - 1, xb), xb);
-        const double awin = av >= 0 ? gi : 0.0;
-        const double awout = bv >= 0 ? go : 0.0;
-        aw_cum[i] = (awout - awin) + G0;
-        if (aw_out) aw_out[i] = awout;
-        if (aw_in) aw_in[i] = awin;
-    }
-}
-
-template <int BLOCK, bool INTEREST, int MODE = 0, bool PATHS = false>
+template <int BLOCK, bool INTEREST, int MODE = 0>
 __device__ __forceinline__ void eq_column(const int b, const int j0, const int j1, const LearnBufs& L,
                                           const double* __restrict__ eta, const double* __restrict__ t_end,
                                           const double* __restrict__ u, const EqArgs& a, const InterestArgs& ia,
                                           const ResultSoA& out, double* smem)
 {
-    static_assert(!(PATHS && INTEREST), "the interest mode writes its AW path from the solving lane");
     const int n = L.n_knots[b], ntau = L.n_tau[b], nle = L.n_le[b];
     const uint32_t lst = L.status[b];
     const size_t row = (size_t)b * (size_t)L.cap;
@@ -1311,15 +1279,9 @@ __device__ __forceinline__ void eq_column(const int b, const int j0, const int j
     __shared__ int s_ndec;                 // decreases of G between consecutive knots
     __shared__ unsigned long long s_maxdec; // largest decrease (bits of a nonnegative double)
     __shared__ double s_thalf;
-    // path mode: the point j0's outcome, for the workgroup's get_AW pass after the point loop
-    __shared__ double s_pxi, s_ptin, s_ptout;
-    __shared__ uint32_t s_pst;
     // every shared flag is initialised before the first barrier: lanes >= nq set
     // s_nonmono right after it, so a later store by thread 0 could clear their flag
-    if (threadIdx.x == 0) {
-        eq_next = 0; s_nonmono = 0; s_noscan = 0; s_ndec = 0; s_maxdec = 0; s_thalf = NAN;
-        if (PATHS) s_pst = 0;
-    }
+    if (threadIdx.x == 0) { eq_next = 0; s_nonmono = 0; s_noscan = 0; s_ndec = 0; s_maxdec = 0; s_thalf = NAN; }
     if (fits) {
         for (int i = threadIdx.x; i < n; i += BLOCK) { sT[i] = gT[i]; sG[i] = gG[i]; }
         if (INTEREST)
@@ -1454,12 +1416,10 @@ __device__ __forceinline__ void eq_column(const int b, const int j0, const int j
                                      r, vsteps, a.aw_path, a.diag);
         } else if (MODE != 2 && fits) {
             solve_point((const double*)sT, (const double*)sG, cH, S, n, ntau, nle, ETA, T1, trunc, uj, a.kappa,
-                        a.max_iters, lbits, r, PATHS ? nullptr : a.aw_path, a.diag);
+                        a.max_iters, lbits, r, a.aw_path, a.diag);
         } else if (MODE != 1) {
-            solve_point(gT, gG, gH, S, n, ntau, nle, ETA, T1, trunc, uj, a.kappa, a.max_iters, lbits, r,
-                        PATHS ? nullptr : a.aw_path, a.diag);
+            solve_point(gT, gG, gH, S, n, ntau, nle, ETA, T1, trunc, uj, a.kappa, a.max_iters, lbits, r, a.aw_path, a.diag);
         }
-        if (PATHS && j == j0) { s_pxi = r.xi; s_ptin = r.tin; s_ptout = r.tout; s_pst = r.status; }
         const size_t o = (size_t)b * (size_t)a.n_u + j;
         if (INTEREST && ia.steps) ia.steps[o] = vsteps;
         out.xi[o] = r.xi;
@@ -1469,17 +1429,6 @@ __device__ __forceinline__ void eq_column(const int b, const int j0, const int j
         out.tol[o] = r.tol;
         out.status[o] = r.status;
         if (out.iters) out.iters[o] = r.iters;
-    }
-    if constexpr (PATHS) {
-        __syncthreads();
-        if ((s_pst & SBR_RUN) && a.aw_path) {
-            if (fits)
-                aw_paths_coop<BLOCK>((const double*)sT, (const double*)sG, n, ntau, nle, ETA, s_pxi, s_ptin, s_ptout,
-                                     a.aw_path, a.aw_out_path, a.aw_in_path);
-            else
-                aw_paths_coop<BLOCK>(gT, gG, n, ntau, nle, ETA, s_pxi, s_ptin, s_ptout, a.aw_path, a.aw_out_path,
-                                     a.aw_in_path);
-        }
     }
 }
 
@@ -1491,7 +1440,7 @@ __device__ unsigned long long g_wgtime[2 * kWgTimeMax];
 __device__ unsigned int g_wghw[2 * kWgTimeMax];
 #endif
 
-template <int BLOCK, bool INTEREST, int MODE, bool PATHS = false>
+template <int BLOCK, bool INTEREST, int MODE>
 __global__ __launch_bounds__(BLOCK, INTEREST ? 1 : SBR_EQ_MINW) void equilibrium_kernel(LearnBufs L, const double* __restrict__ eta,
                                                             const double* __restrict__ t_end,
                                                             const double* __restrict__ u, EqArgs a, InterestArgs ia,
@@ -1507,7 +1456,7 @@ __global__ __launch_bounds__(BLOCK, INTEREST ? 1 : SBR_EQ_MINW) void equilibrium
 #ifdef SBR_EQ_WGTIME
     const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
 #endif
-    eq_column<BLOCK, INTEREST, MODE, PATHS>(b, j0, j1, L, eta, t_end, u, a, ia, out, smem);
+    eq_column<BLOCK, INTEREST, MODE>(b, j0, j1, L, eta, t_end, u, a, ia, out, smem);
 #ifdef SBR_EQ_WGTIME
     __syncthreads();
     const size_t wg = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
@@ -1593,6 +1542,311 @@ __global__ __launch_bounds__(SBR_EQ_WIDE, SBR_EQ_MINW) void eq_ready_kernel(Lear
 }
 
 // ============================================================================
+// One point by a whole workgroup (sbr_equilibrium_on_knots / sbr_solve_point_paths with
+// n_u = 1: the drop-in's per-u calls).  The throughput kernel gives each point one lane, so a
+// lone point pays every dependent LDS round trip of its searches (≈12 per lookup, ≈4 lookups
+// per bisection iteration) and its staging runs on one wave.  Here the knots are staged by
+// the whole block, wave 0 runs the point with wave-wide searches — searchsortedlast over [lo,
+// hi] by 64-ary probing: one LDS load per lane and a ballot per round, two rounds for a
+// Fig 5 column — and the block evaluates get_AW on every τ̄ knot (the exhaustive path), so
+// AW_max and the three paths come from one pass.  The same operations as solve_point /
+// solve_from_buffers' exact iteration and eval_range (each lookup lands on the bracket
+// ssl_range finds: the knots are sorted), so the same bits.
+// ============================================================================
+constexpr int CO_BLOCK = 256;
+
+// searchsortedlast in [lo, hi] (ssl_range's result for sorted t: lo + #{j in (lo, hi] : t[j] <= x})
+// by the 64 lanes of a wave; every lane returns the same index.  Call with the whole wave active.
+template <class P>
+__device__ __forceinline__ int wave_ssl(P t, int lo, int hi, double x)
+{
+    const int lane = threadIdx.x & 63;
+    if (lo >= hi) return lo; // a one-knot bracket (most bisection iterates once narrowed)
+    while (hi - lo > 64) {
+        const int step = (hi - lo + 63) >> 6; // probes lo + k·step, k = 1..64 (those <= hi)
+        const int pk = lo + (lane + 1) * step;
+        const bool pr = pk <= hi && t[pk <= hi ? pk : hi] <= x;
+        const int c = __popcll(__ballot(pr)); // the true probes are a prefix (t sorted)
+        const int nhi = lo + (c + 1) * step - 1;
+        hi = nhi < hi ? nhi : hi;
+        lo = lo + c * step;
+    }
+    const int pk = lo + 1 + lane;
+    const bool pr = pk <= hi && t[pk <= hi ? pk : hi] <= x;
+    return lo + __popcll(__ballot(pr));
+}
+
+// wave-uniform in_range (the flag as solve_from_buffers sets it)
+__device__ __forceinline__ bool co_in_range(double x, double tlo, double thi, bool trunc, uint32_t& flag)
+{
+    if (x >= tlo && x <= thi) return true;
+    flag |= (trunc && x > thi) ? SBR_ENGINE_TRUNC : SBR_OOB;
+    return false;
+}
+
+template <class P>
+__device__ __forceinline__ void point_wave(P T, P G, P H, const int n, const int ntau, const int nle,
+                                           const double ETA, const double T1, const bool trunc, const double u,
+                                           const double kappa, const int max_iters, const uint32_t lbits,
+                                           PointResult& r)
+{
+    const int lane = threadIdx.x & 63;
+    r.xi = NAN; r.aw = NAN; r.tol = INFINITY; r.iters = 0; r.status = 0;
+    // ---------------- optimal_buffer (solver.jl:211-264), 64 τ̄ entries per round ----------------
+    bool any = false, all = true;
+    int fa = -1, la = -1, cin = -1, cout = -1;
+    for (int b0 = 0; b0 < ntau; b0 += 64) {
+        const int i = b0 + lane;
+        const bool in = i < ntau;
+        const bool ab = in && H[in ? i : 0] > u;
+        const bool pv = in && i > 0 && H[i > 0 && in ? i - 1 : 0] > u;
+        const unsigned long long mab = __ballot(ab), min_ = __ballot(in);
+        any |= mab != 0ull;
+        all &= (mab & min_) == min_;
+        if (mab) {
+            if (fa < 0) fa = b0 + __ffsll((long long)mab) - 1;
+            la = b0 + 63 - __clzll((long long)mab);
+        }
+        const unsigned long long mi = __ballot(in && i > 0 && !pv && ab); // 0 → 1 at i: cin = i − 1
+        const unsigned long long mo = __ballot(in && i > 0 && pv && !ab); // 1 → 0 at i: cout = i − 1
+        if (cin < 0 && mi) cin = b0 + __ffsll((long long)mi) - 2;
+        if (mo) cout = b0 + 63 - __clzll((long long)mo) - 1;
+    }
+    auto tau = [&](int i) -> double { return i < nle ? T[i] : ETA; };
+    double tin, tout;
+    if (!any) {
+        tin = T1; tout = T1;
+    } else if (all) {
+        tin = tau(0); tout = tau(ntau - 1);
+    } else {
+        tin = T1; tout = T1;
+        if (cin >= 0) {
+            const double t0 = tau(cin), t1 = tau(cin + 1), h0 = H[cin], h1 = H[cin + 1];
+            tin = t0 + ((u - h0) * (t1 - t0)) / (h1 - h0);
+        }
+        if (cout >= 0) {
+            const double t0 = tau(cout), t1 = tau(cout + 1), h0 = H[cout], h1 = H[cout + 1];
+            tout = t0 + ((u - h0) * (t1 - t0)) / (h1 - h0);
+        }
+        if (tin == T1) tin = tau(fa);
+        if (tout == T1) tout = tau(la);
+    }
+    r.tin = tin;
+    r.tout = tout;
+    const double tlo = T[0], thi = T[n - 1];
+    if (tin == tout) {
+        r.status = SBR_NO_RUN_HR_BELOW_U | SBR_CONVERGED | lbits;
+        r.tol = 0.0;
+        return;
+    }
+    // ---------------- compute_ξ (solver.jl:308-376): the exact iteration ----------------
+    uint32_t flag = 0;
+    const double tolerance = 10.0 * sbr_jl_eps(kappa);
+    double xnew = (tin + tout) / 2.0, xmin = tin, xmax = tout;
+    const bool okmin = co_in_range(xmin, tlo, thi, trunc, flag);
+    const bool okmax = co_in_range(xmax, tlo, thi, trunc, flag);
+    if (!okmin || !okmax) { r.status = flag | lbits; return; }
+    int jlo = wave_ssl(T, 0, n - 1, xmin);
+    int jhi = wave_ssl(T, 0, n - 1, xmax);
+    const int jtin = jlo;
+    uint32_t s = SBR_NO_RUN_MAXITER;
+    double xi = NAN, tolr = INFINITY;
+    for (int iter = 1; iter <= max_iters; iter++) {
+        r.iters = iter;
+        const double dd = xmin - xmax;
+        if (collapsed(dd)) { s = SBR_NO_RUN_COLLAPSE; break; }
+        if (iter == max_iters - 1) { s = SBR_NO_RUN_MAXITER; break; }
+        const double xo = xnew;
+        const double ic = dmin(tin, xo), oc = dmin(tout, xo);
+        const int j = wave_ssl(T, jlo, jhi, xo);
+        const bool ok = co_in_range(oc, tlo, thi, trunc, flag);
+        const int joc = (oc == xo) ? j : (ok ? wave_ssl(T, 0, n - 1, oc) : 0);
+        const double Goc = ok ? lerp_at(T, G, n, joc, oc) : 0.0;
+        double Gic = 0.0;
+        int jic = 0;
+        if (co_in_range(ic, tlo, thi, trunc, flag)) {
+            jic = (ic == tin) ? jtin : (ic == xo ? j : wave_ssl(T, 0, n - 1, ic));
+            Gic = lerp_at(T, G, n, jic, ic);
+        }
+        if (j + 1 >= n) { flag |= trunc ? SBR_ENGINE_TRUNC : SBR_OOB; break; }
+        const double eps = T[j + 1] - T[j];
+        const double xoe = oc + eps, xie = ic + eps;
+        const bool oke = co_in_range(xoe, tlo, thi, trunc, flag);
+        const bool oki = co_in_range(xie, tlo, thi, trunc, flag);
+        if (flag) break;
+        const double AW = Goc - Gic;
+        const double err = AW - kappa;
+        if (fabs(err) <= tolerance) {
+            double Goce = 0.0, Gice = 0.0;
+            if (oke) Goce = lerp_at(T, G, n, wave_ssl(T, joc, n - 1, xoe), xoe);
+            if (oki) Gice = lerp_at(T, G, n, wave_ssl(T, jic, n - 1, xie), xie);
+            const double AWe = Goce - Gice;
+            if (AWe >= AW) { s = SBR_RUN; xi = xo; tolr = fabs(err); }
+            else s = SBR_FALSE_EQ;
+            break;
+        } else if (err > 0) {
+            xmax = xo; jhi = j; xnew = 0.5 * (xo + xmin);
+        } else {
+            xmin = xo; jlo = j; xnew = 0.5 * (xo + xmax);
+        }
+    }
+    if (flag) { r.status = flag | lbits; return; }
+    if (s != SBR_RUN) { r.status = s | lbits; return; }
+    // the AW stage's own range checks (solve_from_buffers: G(0), then the path's last τ̄ — the
+    // shifted arguments are nondecreasing, so the first failing knot fails there too)
+    if (!co_in_range(0.0, tlo, thi, trunc, flag)) { r.status = flag | lbits; return; }
+    const double icc = (tin >= xi) ? xi : tin;
+    const double occ = (tout > xi) ? xi : tout;
+    const double al = (tau(ntau - 1) - xi) + icc, bl = (tau(ntau - 1) - xi) + occ;
+    if (!((al > 0 ? al : 0.0) <= thi) || !((bl > 0 ? bl : 0.0) <= thi)) {
+        r.status = (trunc ? SBR_ENGINE_TRUNC : SBR_OOB) | lbits;
+        return;
+    }
+    r.xi = xi;
+    r.tol = tolr;
+    r.status = SBR_RUN | SBR_CONVERGED | lbits; // r.aw: the block's get_AW pass
+}
+
+// get_AW on τ̄ entries [i0, i1) with brackets slid along (eval_range's arithmetic); NaN-latching
+// max into mx (Julia maximum), paths written when given
+template <class P>
+__device__ __forceinline__ void co_eval(P T, P G, const int n, const int nle, const double ETA, const double xi,
+                                        const double icc, const double occ, const double G0, const int i0,
+                                        const int i1, double& mx, double* __restrict__ aw_cum,
+                                        double* __restrict__ aw_out, double* __restrict__ aw_in)
+{
+    if (i0 >= i1) return;
+    auto tau = [&](int i) -> double { return i < nle ? T[i] : ETA; };
+    auto x_of = [&](int i, double c) { const double v = (tau(i) - xi) + c; return v > 0 ? v : 0.0; };
+    int ka = ssl_range(T, 0, n - 1, x_of(i0, icc)), kb = ssl_range(T, 0, n - 1, x_of(i0, occ));
+    ka = ka < n - 2 ? ka : n - 2;
+    kb = kb < n - 2 ? kb : n - 2;
+    double ta0 = T[ka], ta1 = T[ka + 1], ga0 = G[ka], ga1 = G[ka + 1];
+    double tb0 = T[kb], tb1 = T[kb + 1], gb0 = G[kb], gb1 = G[kb + 1];
+    for (int i = i0; i < i1; i++) {
+        const double ti = tau(i);
+        const double av = (ti - xi) + icc;
+        const double bv = (ti - xi) + occ;
+        const double xa = av > 0 ? av : 0.0;
+        const double xb = bv > 0 ? bv : 0.0;
+        while (ka < n - 2 && ta1 <= xa) { ka++; ta0 = ta1; ga0 = ga1; ta1 = T[ka + 1]; ga1 = G[ka + 1]; }
+        while (kb < n - 2 && tb1 <= xb) { kb++; tb0 = tb1; gb0 = gb1; tb1 = T[kb + 1]; gb1 = G[kb + 1]; }
+        const double da = (xa - ta0) / (ta1 - ta0);
+        const double gi = ga0 * (1.0 - da) + ga1 * da;
+        double go;
+        if (xb == tb0) go = gb0 * 1.0 + gb1 * 0.0; // eval_range's δ = 0 form (the same value)
+        else { const double db = (xb - tb0) / (tb1 - tb0); go = gb0 * (1.0 - db) + gb1 * db; }
+        const double awin = av >= 0 ? gi : 0.0;
+        const double awout = bv >= 0 ? go : 0.0;
+        const double v = (awout - awin) + G0;
+        if (aw_cum) aw_cum[i] = v;
+        if (aw_out) aw_out[i] = awout;
+        if (aw_in) aw_in[i] = awin;
+        if (mx == mx && (v != v || v > mx)) mx = v;
+    }
+}
+
+__global__ __launch_bounds__(CO_BLOCK) void point_coop_kernel(LearnBufs L, const double* __restrict__ eta,
+                                                              const double* __restrict__ t_end,
+                                                              const double* __restrict__ u, EqArgs a, ResultSoA out)
+{
+    extern __shared__ double smem[];
+    __shared__ double s_r[5];
+    __shared__ uint32_t s_st;
+    __shared__ int s_it;
+    __shared__ double s_mx[CO_BLOCK / 64];
+    const int n = L.n_knots[0], ntau = L.n_tau[0], nle = L.n_le[0];
+    const uint32_t lst = L.status[0];
+    const bool fits = n <= a.lds_cap && ntau <= a.lds_cap;
+    double* sT = smem;
+    double* sG = smem + a.lds_cap;
+    double* sH = smem + 2 * a.lds_cap;
+    if (fits) {
+        for (int i = threadIdx.x; i < n; i += CO_BLOCK) { sT[i] = L.t[i]; sG[i] = L.G[i]; }
+        for (int i = threadIdx.x; i < ntau; i += CO_BLOCK) sH[i] = L.hr[i];
+    }
+    __syncthreads();
+    const double* T = fits ? (const double*)sT : (const double*)L.t;
+    const double* G = fits ? (const double*)sG : (const double*)L.G;
+    const double* H = fits ? (const double*)sH : (const double*)L.hr;
+    const double ETA = eta[0], T1 = t_end[0], uj = u[0];
+    const uint32_t lbits = lst & (SBR_ODE_MAXITERS | SBR_STIFF_SWITCH | SBR_ODE_FAILED | SBR_KNOT_OVERFLOW);
+    const bool bad_col = (lst & (SBR_ARG_INVALID | SBR_OOB)) || n < 2;
+    const bool trunc = !a.full_grid && n >= 2 && L.t[n - 1] < T1;
+    if (threadIdx.x < 64) {
+        PointResult r;
+        if (bad_col || !(uj >= 0.0)) {
+            r.xi = NAN; r.aw = NAN; r.tol = INFINITY; r.iters = 0; r.tin = NAN; r.tout = NAN;
+            r.status = ((lst & SBR_ARG_INVALID) || !(uj >= 0.0)) ? SBR_ARG_INVALID : (SBR_OOB | lbits);
+        } else {
+            point_wave(T, G, H, n, ntau, nle, ETA, T1, trunc, uj, a.kappa, a.max_iters, lbits, r);
+        }
+        if (threadIdx.x == 0) {
+            s_r[0] = r.xi; s_r[1] = r.tin; s_r[2] = r.tout; s_r[3] = r.aw; s_r[4] = r.tol;
+            s_st = r.status;
+            s_it = r.iters;
+        }
+    }
+    __syncthreads();
+    const uint32_t st = s_st;
+    double mx = -INFINITY;
+    if (st & SBR_RUN) {
+        const double xi = s_r[0], tin = s_r[1], tout = s_r[2];
+        const double icc = (tin >= xi) ? xi : tin;
+        const double occ = (tout > xi) ? xi : tout;
+        const double G0 = lerp_at(T, G, n, ssl_range(T, 0, n - 1, 0.0), 0.0);
+        // contiguous τ̄ ranges per thread (the brackets slide), a NaN-latching max per thread
+        const int per = (ntau + CO_BLOCK - 1) / CO_BLOCK;
+        const int i0 = threadIdx.x * per, i1 = i0 + per < ntau ? i0 + per : ntau;
+        double* sc = a.path_scratch;
+        if (sc && a.aw_path)
+            co_eval(T, G, n, nle, ETA, xi, icc, occ, G0, i0, i1, mx, sc, a.aw_out_path ? sc + ntau : nullptr,
+                    a.aw_in_path ? sc + 2 * ntau : nullptr);
+        else
+            co_eval(T, G, n, nle, ETA, xi, icc, occ, G0, i0, i1, mx, a.aw_path, a.aw_out_path, a.aw_in_path);
+        // block reduction in thread order (NaN latches: any NaN gives NaN, else the max)
+        for (int off = 32; off >= 1; off >>= 1) {
+            const double o = __shfl_down(mx, off, 64);
+            mx = (mx != mx || o != o) ? (double)NAN : (o > mx ? o : mx);
+        }
+        if ((threadIdx.x & 63) == 0) s_mx[threadIdx.x >> 6] = mx;
+    }
+    __syncthreads();
+    if ((st & SBR_RUN) && a.path_scratch && a.aw_path) {
+        // the rows formed per thread in scratch, copied out with consecutive lanes on consecutive
+        // entries (a mapped-host destination then takes whole-line writes)
+        const double* sc = a.path_scratch;
+        for (int i = threadIdx.x; i < ntau; i += CO_BLOCK) {
+            a.aw_path[i] = sc[i];
+            if (a.aw_out_path) a.aw_out_path[i] = sc[ntau + i];
+            if (a.aw_in_path) a.aw_in_path[i] = sc[2 * ntau + i];
+        }
+    }
+    if (threadIdx.x == 0) {
+        double aw = s_r[3];
+        if (st & SBR_RUN) {
+            aw = s_mx[0];
+            for (int w = 1; w < CO_BLOCK / 64; w++) aw = (aw != aw || s_mx[w] != s_mx[w]) ? (double)NAN : (s_mx[w] > aw ? s_mx[w] : aw);
+        }
+        out.xi[0] = s_r[0];
+        out.tau_in_unc[0] = s_r[1];
+        out.tau_out_unc[0] = s_r[2];
+        out.aw_max[0] = aw;
+        out.tol[0] = s_r[4];
+        out.status[0] = st;
+        if (out.iters) out.iters[0] = s_it;
+    }
+}
+
+hipError_t launch_point_coop(const LearnBufs& L, const double* eta, const double* t_end, const double* u,
+                             const EqArgs& a, const ResultSoA& out, hipStream_t s)
+{
+    const size_t lds = (size_t)3 * a.lds_cap * sizeof(double);
+    hipLaunchKernelGGL(point_coop_kernel, dim3(1), dim3(CO_BLOCK), lds, s, L, eta, t_end, u, a, out);
+    return hipGetLastError();
+}
+
+// ============================================================================
 // launchers
 // ============================================================================
 hipError_t launch_learn_logistic(const double* beta, const double* eta, const double* t_end, const LearnArgs& a,
@@ -1636,9 +1890,7 @@ hipError_t launch_equilibrium(const LearnBufs& L, const double* eta, const doubl
         if (only_mode != 2) hipLaunchKernelGGL(k1, grid, dim3(bs), lds, s, L, eta, t_end, u, a, none, out);
         if (only_mode != 1) hipLaunchKernelGGL(k2, grid, dim3(bs), 0, s, L, eta, t_end, u, a, none, out);
     };
-    if (a.aw_path) // path mode (n_u == 1): one wave solves the point, then writes the paths
-        go(equilibrium_kernel<64, false, 1, true>, equilibrium_kernel<64, false, 2, true>, 64);
-    else if (w > 256)
+    if (w > 256)
         go(equilibrium_kernel<SBR_EQ_WIDE, false, 1>, equilibrium_kernel<SBR_EQ_WIDE, false, 2>, SBR_EQ_WIDE);
     else if (w > 64)
         go(equilibrium_kernel<256, false, 1>, equilibrium_kernel<256, false, 2>, 256);

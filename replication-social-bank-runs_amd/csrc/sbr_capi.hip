@@ -108,6 +108,11 @@ struct sbr_ctx {
     double kn_key[4] = {};
     std::vector<double> kn_t, kn_G, kn_hr; // host copies of the resident knots and HR
     int32_t kn_m = 0, kn_ntau = 0;         // knots <= η; τ̄ entries (0: the hazard's BoundsError)
+    // single-u calls: mapped, coherent host memory the kernel reads t_end / u from and writes the
+    // results and paths to (no copy launches per call) — host view and device view
+    double* kn_zc = nullptr;
+    double* kn_zc_dev = nullptr;
+    size_t kn_zc_cap = 0; // doubles
     // sbr_hetero_equilibrium_on_knots: the same for a LearningResultsHetero (knots, K group CDFs,
     // the K hazard paths), keyed by K, n, t, G, βs, dist, η, p, λ
     char* hk_dev = nullptr;
@@ -430,6 +435,12 @@ int launch_eq(sbr_ctx* c, hipStream_t s, const sbr::LearnBufs& L, const double* 
     sbr::EqArgs ea{kappa, (int32_t)n_u, o.bisect_max_iters, c->lds_cap_b, aw_path,
                    (o.flags & SBR_FLAG_EXHAUSTIVE) ? 1 : 0, (o.flags >> 8) & 7};
     hipEvent_t t0 = tstart(c, s);
+    if (aw_path && n_beta == 1 && n_u == 1) { // single point with its path: the whole workgroup on it
+        ea.lds_cap = c->lds_cap;
+        HIP_TRY(c, sbr::launch_point_coop(L, eta, t_end, u, ea, out, s), SBR_EDEVICE);
+        tend(c, s, 1, t0);
+        return SBR_OK;
+    }
     HIP_TRY(c, sbr::launch_equilibrium(L, eta, t_end, u, ea, out, (int)n_beta, s), SBR_EDEVICE);
     tend(c, s, 1, t0);
     return SBR_OK;
@@ -810,6 +821,7 @@ int sbr_free(sbr_ctx* c)
     if (c->stage) (void)hipFree(c->stage);
     if (c->kn_dev) (void)hipFree(c->kn_dev);
     if (c->kn_pin) (void)hipHostFree(c->kn_pin);
+    if (c->kn_zc) (void)hipHostFree(c->kn_zc);
     if (c->hk_dev) (void)hipFree(c->hk_dev);
     if (c->hk_pin) (void)hipHostFree(c->hk_pin);
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
@@ -1216,6 +1228,7 @@ int ensure_knots(sbr_ctx* c, size_t n, size_t n_u)
     while (cu < n_u) cu *= 2;
     if (c->kn_dev) (void)hipFree(c->kn_dev);
     if (c->kn_pin) (void)hipHostFree(c->kn_pin);
+    if (c->kn_zc) (void)hipHostFree(c->kn_zc);
     if (c->hk_dev) (void)hipFree(c->hk_dev);
     if (c->hk_pin) (void)hipHostFree(c->hk_pin);
     c->kn_dev = c->kn_pin = nullptr;
@@ -1226,6 +1239,13 @@ int ensure_knots(sbr_ctx* c, size_t n, size_t n_u)
     HIP_TRY(c, hipHostMalloc(&c->kn_pin, K.bytes), SBR_ENOMEM);
     c->kn_cap_k = ck;
     c->kn_cap_u = cu;
+    // [t_end, u, results (8 doubles), AW_cum / AW_OUT / AW_IN (ck + 1 each)]
+    const size_t zc = 16 + 3 * (ck + 1);
+    if (c->kn_zc) (void)hipHostFree(c->kn_zc);
+    c->kn_zc = c->kn_zc_dev = nullptr;
+    HIP_TRY(c, hipHostMalloc(&c->kn_zc, zc * 8, hipHostMallocMapped | hipHostMallocCoherent), SBR_ENOMEM);
+    HIP_TRY(c, hipHostGetDevicePointer((void**)&c->kn_zc_dev, c->kn_zc, 0), SBR_EDEVICE);
+    c->kn_zc_cap = zc;
     return SBR_OK;
 }
 
@@ -1465,20 +1485,33 @@ int sbr_equilibrium_on_knots(sbr_ctx* c, const double* t, const double* G, int64
                 HIP_TRY(c, hipMemcpyAsync(H + K.hr, D + K.hr, (size_t)ntau * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
             HIP_TRY(c, hipMemcpyAsync(H, D, 32, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
         }
-        double* hu = (double*)(H + K.u);
-        hu[0] = t_end;
-        memcpy(hu + 1, u, (size_t)n_u * 8);
-        HIP_TRY(c, hipMemcpyAsync(du, hu, (size_t)(n_u + 1) * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
         const size_t nu = (size_t)n_u;
-        const sbr::ResultSoA r{dres, dres + nu, dres + 2 * nu, dres + 3 * nu, dres + 4 * nu, (uint32_t*)(dres + 5 * nu),
-                               (int32_t*)(dres + 5 * nu) + nu};
-        double* dpath = dres + 6 * nu;
-        sbr::EqArgs ea{kappa, (int32_t)n_u, o.bisect_max_iters, c->lds_cap_b, want_aw ? dpath : nullptr,
-                       (o.flags & SBR_FLAG_EXHAUSTIVE) ? 1 : 0, (o.flags >> 8) & 7,
-                       want_aw ? dpath + ntau : nullptr, want_aw ? dpath + 2 * ntau : nullptr, 1};
-        HIP_TRY(c, sbr::launch_equilibrium(L, dsc + 1, du, du + 1, ea, r, 1, s, n <= c->lds_cap_b ? 1 : 2),
-                SBR_EDEVICE);
-        HIP_TRY(c, hipMemcpyAsync(H + K.res, D + K.res, res_bytes, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        if (n_u == 1) {
+            // one point: the whole workgroup on it (latency), inputs read from and results written
+            // to mapped host memory — one launch, no copies
+            double* z = c->kn_zc;
+            double* zd = c->kn_zc_dev;
+            z[0] = t_end;
+            z[1] = u[0];
+            const sbr::ResultSoA r{zd + 2, zd + 3, zd + 4, zd + 5, zd + 6, (uint32_t*)(zd + 7), (int32_t*)(zd + 7) + 1};
+            double* zp = zd + 16;
+            sbr::EqArgs ea{kappa, 1, o.bisect_max_iters, c->lds_cap, want_aw ? zp : nullptr,
+                           (o.flags & SBR_FLAG_EXHAUSTIVE) ? 1 : 0, (o.flags >> 8) & 7,
+                           want_aw ? zp + ntau : nullptr, want_aw ? zp + 2 * ntau : nullptr, 1, dres};
+            HIP_TRY(c, sbr::launch_point_coop(L, dsc + 1, zd, zd + 1, ea, r, s), SBR_EDEVICE);
+        } else {
+            double* hu = (double*)(H + K.u);
+            hu[0] = t_end;
+            memcpy(hu + 1, u, nu * 8);
+            HIP_TRY(c, hipMemcpyAsync(du, hu, (nu + 1) * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+            const sbr::ResultSoA r{dres, dres + nu, dres + 2 * nu, dres + 3 * nu, dres + 4 * nu,
+                                   (uint32_t*)(dres + 5 * nu), (int32_t*)(dres + 5 * nu) + nu};
+            sbr::EqArgs ea{kappa, (int32_t)n_u, o.bisect_max_iters, c->lds_cap_b, nullptr,
+                           (o.flags & SBR_FLAG_EXHAUSTIVE) ? 1 : 0, (o.flags >> 8) & 7, nullptr, nullptr, 1};
+            HIP_TRY(c, sbr::launch_equilibrium(L, dsc + 1, du, du + 1, ea, r, 1, s, n <= c->lds_cap_b ? 1 : 2),
+                    SBR_EDEVICE);
+            HIP_TRY(c, hipMemcpyAsync(H + K.res, D + K.res, res_bytes, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        }
         HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
         return SBR_OK;
     });
@@ -1498,7 +1531,8 @@ int sbr_equilibrium_on_knots(sbr_ctx* c, const double* t, const double* G, int64
         c->kn_valid = true;
     }
     const size_t nu = (size_t)n_u;
-    const double* hr_ = (const double*)(H + K.res);
+    // n_u == 1: the mapped block [t_end, u, xi, τ̄_IN, τ̄_OUT, AW_max, tol, status | iters, pad, paths]
+    const double* hr_ = n_u == 1 ? c->kn_zc + 2 : (const double*)(H + K.res);
     double* hs[5] = {out->xi, out->tau_in_unc, out->tau_out_unc, out->aw_max, out->tol};
     for (int k = 0; k < 5; k++)
         if (hs[k]) memcpy(hs[k], hr_ + k * nu, nu * 8);
@@ -1510,9 +1544,9 @@ int sbr_equilibrium_on_knots(sbr_ctx* c, const double* t, const double* G, int64
         if (ntau > m) tau[m] = eta;
     }
     if (hr) memcpy(hr, c->kn_hr.data(), (size_t)ntau * 8);
-    if (want_aw) {
-        const bool run = (((const uint32_t*)(hr_ + 5 * nu))[0] & SBR_RUN) != 0;
-        const double* hp = hr_ + 6 * nu;
+    if (want_aw) { // n_u == 1
+        const bool run = (((const uint32_t*)(hr_ + 5))[0] & SBR_RUN) != 0;
+        const double* hp = c->kn_zc + 16;
         double* dst[3] = {aw_cum, aw_out, aw_in};
         for (int k = 0; k < 3; k++) {
             if (!dst[k]) continue;

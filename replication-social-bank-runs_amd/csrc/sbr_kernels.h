@@ -63,6 +63,9 @@ struct EqArgs {
     // 1: the knots are the caller's whole interpolation grid (sbr_equilibrium_on_knots), never a
     // truncated learning solve: a lookup past the last knot is the interpolant's BoundsError
     int32_t full_grid;
+    // launch_point_coop: device scratch of 3·n_tau doubles; when set, the paths are formed there and
+    // copied to aw_path / aw_out_path / aw_in_path in coalesced rows (those may be mapped host memory)
+    double* path_scratch;
 };
 
 // Interest-rate extension (sbr_baseline.hip interest mode): value function on the HR grid.
@@ -191,10 +194,15 @@ hipError_t launch_hetero(int K, const double* betas, const double* dist, const d
 hipError_t launch_learn_logistic(const double* beta, const double* eta, const double* t_end, const LearnArgs& a,
                                  const LearnBufs& L, hipStream_t s);
 // only_mode: 0 = the LDS-slab launch then the global-memory launch; 1 / 2 = only one of them
-// (a caller that knows every column fits the slab, or none does).  With a.aw_path (n_u == 1)
-// the path-mode kernels run: the point's solve, then get_AW's paths by the whole workgroup.
+// (a caller that knows every column fits the slab, or none does).  a.aw_path (n_u == 1): the
+// solving lane writes AW_cum on τ̄ (exhaustive); single points use launch_point_coop instead.
 hipError_t launch_equilibrium(const LearnBufs& L, const double* eta, const double* t_end, const double* u,
                               const EqArgs& a, const ResultSoA& out, int n_beta, hipStream_t s, int only_mode = 0);
+// one point (n_u == 1, column 0 of L) by a whole workgroup: wave-wide searches for the solve,
+// the block for get_AW's exhaustive pass (AW_max and, with a.aw_path, the three paths).  a.lds_cap
+// = knots staged per array (3 arrays: t, G, HR); larger columns run from global memory.
+hipError_t launch_point_coop(const LearnBufs& L, const double* eta, const double* t_end, const double* u,
+                             const EqArgs& a, const ResultSoA& out, hipStream_t s);
 // hazard_rate (solver.jl:153-185) of n_beta columns whose knots, n_knots, n_le (#knots <= η) and
 // status are in L (the hazard stage of launch_learn_logistic on its own)
 hipError_t launch_hazard(const double* beta, const double* eta, const LearnArgs& a, const LearnBufs& L, int n_beta,

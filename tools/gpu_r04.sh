@@ -43,6 +43,7 @@ for s in ${STEPS:-tests smoke bench single}; do
     hetvars) for v in ${VARS:-}; do run hetero_$v 600 env SBR_LIB=replication-social-bank-runs_amd/lib_var/$v/libsbr.so python -u bench.py --workload hetero --steps 10 --warmup 2 --phases --no-cpu-baseline; done ;;
     config2) run config2 300 python -u bench.py --workload config2 --steps 20 --warmup 2 ;;
     dropin) run dropin 600 python -u bench.py --workload dropin --steps 30 ;;
+    knotsprobe) run knotsprobe 300 python -u tools/knots_probe.py 2000 && run knotsprof 300 rocprofv3 --kernel-trace --stats -d "$OUT/knotsprof" -o run --output-format csv -- python3 tools/knots_probe.py 500 ;;
     knots) run knots 600 python -u -m pytest tests/test_gpu_knots.py tests/test_gpu_baseline.py -x -v --timeout 300 --timeout-method thread ${TESTK:+-k "$TESTK"} ;;
   esac
 done
