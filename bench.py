@@ -218,13 +218,22 @@ def main_small(a):
             r = eng.sweep_baseline(g, early_exit=5)
         dt = (time.perf_counter() - t0) / a.steps
         run = int(((r["status"] & sbr.STATUS["SBR_RUN"]) > 0).sum())
+        # phase breakdown of one more call (events on the call's stream + host clock)
+        eng.timing_enable(True)
+        tp = time.perf_counter()
+        eng.sweep_baseline(g, early_exit=5)
+        py_call = (time.perf_counter() - tp) * 1e3
+        phases = eng.host_phases()
+        eng.timing_read(None)
+        eng.timing_enable(False)
+        phases["python_call"] = py_call
         res = {"metric": "equilibria solved/sec on β×u grid (FP64), Fig 5 500x500, one host-API call per grid",
                "value": npts / dt, "unit": "equilibria/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
                "ms_per_step": dt * 1e3, "higher_is_better": True, "scaling": None, "vs_baseline": None,
                "dtype": "f64", "data": "the reference's Fig 5 grid (deterministic)",
                "config": {"workload": "config2: sbr_sweep_baseline on fig5 500x500, early_exit_nan_run=5, host "
                                       "arrays (PCIe included) (BASELINE config 2)", "run_cells": run},
-               "libsbr_sha16": lib_sha()}
+               "phase_ms": phases, "libsbr_sha16": lib_sha()}
         if not a.no_cpu_baseline:
             O.build()
             cores = usable_cores()
@@ -404,6 +413,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    timeline = eng.chunk_timeline(stream) if not pipe else []  # the last sweep's chunk ends
     learn_ms, eq_ms, ncalls = eng.timing_read(stream)
     eng.timing_enable(False)
     if world > 1:
@@ -468,6 +478,7 @@ def main():
     }
     if not pipe:
         res["roofline_note"] = "single-sweep mode: chunked kernels overlap; the roofline line is the pipelined default run's"
+        res["chunk_timeline_ms"] = [{"learn_end": a, "eq_end": b} for a, b in timeline]
     if a.phases:
         res["eq_phase_ms"] = phase_breakdown(eng, beta[0], eta[0], t_end[0], u, p, kappa, lam, x0,
                                              {k: v[0] for k, v in out.items()}, stream, dev)

@@ -397,6 +397,17 @@ int sbr_timing_enable(sbr_ctx* ctx, int on);
  * when the flag was given but the device could not run it: fewer than 256 CUs, or stream
  * creation failed). */
 int sbr_last_schedule(sbr_ctx* ctx, int32_t* schedule);
+/* Phases of the last host-pointer sbr_sweep_baseline made while timing is enabled, in ms:
+ * [0] H2D of the inputs, [1] the kernels (learning, hazard, equilibria), [2] D2H of the results
+ * into pinned memory (HIP events on the call's stream), [3] the host side after the sync: the copy
+ * into the caller's arrays and the early-exit post-pass, [4] the whole call (host clock; the rest
+ * is launch and synchronisation overhead). */
+int sbr_host_phases(sbr_ctx* ctx, double* ms5);
+/* Timeline of the last chunked single sweep made while timing is enabled: for each of the
+ * *n_chunks column chunks, ms[2k] = its learning end and ms[2k+1] = its equilibrium end, in ms
+ * from the sweep start (synchronises `stream` and the learning streams; *n_chunks = 0 when the
+ * last sweep was not chunked or not timed).  ms holds 2 × 3 doubles. */
+int sbr_chunk_timeline(sbr_ctx* ctx, void* stream, int32_t* n_chunks, double* ms);
 int sbr_timing_read(sbr_ctx* ctx, void* stream, double* learn_ms, double* eq_ms, int32_t* n_calls);
 
 /* Per-β learning statistics of the last sweep (knots stored, τ̄-grid length,

@@ -9,8 +9,11 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
+#include <array>
 #include <chrono>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/sbr.h"
@@ -97,6 +100,10 @@ struct sbr_ctx {
     // host-API staging
     void* stage = nullptr;
     size_t stage_bytes = 0;
+    // pinned landing buffer of the host-pointer sweeps' results: one DMA copy at full PCIe rate,
+    // then a multi-threaded host copy into the caller's (pageable) arrays
+    void* res_pin = nullptr;
+    size_t res_pin_bytes = 0;
     // sbr_equilibrium_on_knots: the caller's knot grid and its hazard path stay resident between
     // calls, keyed by value (n, t, G and β, η, p, λ); the device block and its pinned host mirror
     // share one layout (KnotLayout), so each transfer is one contiguous copy
@@ -135,6 +142,14 @@ struct sbr_ctx {
         hipEvent_t a, b;
     };
     std::vector<TRec> trec;
+    // phases of the last host-pointer baseline sweep while timing is enabled (sbr_host_phases):
+    // H2D, kernels, D2H (HIP events on the stream), the early-exit post-pass and the whole call
+    // (host clock), milliseconds
+    double ph_ms[5] = {};
+    // the last chunked single sweep while timing is enabled: per chunk, events at its learning
+    // end and its equilibrium end, and the sweep start (sbr_chunk_timeline)
+    hipEvent_t ck_start = nullptr;
+    std::vector<hipEvent_t> ck_ev;
     // readiness schedule of single sweeps: the learning kernel and the equilibrium workgroups
     // on streams with disjoint CU masks (hipExtStreamCreateWithCUMask), and the publication
     // queue [head, err, tail, pad, q[n_beta], hz_flag[n_beta]]
@@ -379,6 +394,42 @@ int ensure_stage(sbr_ctx* c, size_t bytes)
     return SBR_OK;
 }
 
+int ensure_res_pin(sbr_ctx* c, size_t bytes)
+{
+    if (bytes <= c->res_pin_bytes) return SBR_OK;
+    if (c->res_pin) (void)hipHostFree(c->res_pin);
+    c->res_pin = nullptr;
+    c->res_pin_bytes = 0;
+    HIP_TRY(c, hipHostMalloc(&c->res_pin, bytes), SBR_ENOMEM);
+    c->res_pin_bytes = bytes;
+    return SBR_OK;
+}
+
+// copy (dst_k, src_k, bytes_k) pieces with up to 8 host threads in ≈1 MiB slices: the caller's
+// result arrays are often fresh pages (first-touch faults), which one thread would take serially
+void parallel_copy(const std::vector<std::array<size_t, 3>>& pieces)
+{
+    constexpr size_t kSlice = 1 << 20;
+    std::vector<std::array<size_t, 3>> sl;
+    size_t total = 0;
+    for (const auto& p : pieces)
+        for (size_t o = 0; o < p[2]; o += kSlice) {
+            const size_t b = std::min(kSlice, p[2] - o);
+            sl.push_back({p[0] + o, p[1] + o, b});
+            total += b;
+        }
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const size_t nt = std::min<size_t>({(size_t)8, (size_t)hw, (total + (4u << 20) - 1) / (4u << 20)});
+    auto work = [&](size_t k0) {
+        for (size_t k = k0; k < sl.size(); k += nt) memcpy((void*)sl[k][0], (const void*)sl[k][1], sl[k][2]);
+    };
+    if (nt <= 1) { work(0); return; }
+    std::vector<std::thread> th;
+    for (size_t t = 1; t < nt; t++) th.emplace_back(work, t);
+    work(0);
+    for (auto& t : th) t.join();
+}
+
 // EconomicParameters / LearningParameters scalar checks (model.jl:31-35, 71-76)
 bool scalars_valid(double x0, double p, double kappa, double lambda)
 {
@@ -612,6 +663,8 @@ int run_baseline(sbr_ctx* c, hipStream_t s, const double* beta, const double* et
 #endif
     HIP_TRY(c, hipEventRecord(c->ev_in, s), SBR_EDEVICE);
     hipEvent_t t0 = tstart(c, s);
+    c->ck_start = c->timing ? t0 : nullptr;
+    c->ck_ev.assign(c->timing ? 2 * kSweepChunks : 0, nullptr);
     for (int k = 0; k < kSweepChunks; k++) {
         hipStream_t ls = c->lstream[k];
         const int64_t c0 = lo[k], nb = lo[k + 1] - lo[k];
@@ -621,11 +674,19 @@ int run_baseline(sbr_ctx* c, hipStream_t s, const double* beta, const double* et
         lk.n_beta = (int32_t)nb;
         const sbr::LearnBufs Lk = learn_rows(c->LW[0], (size_t)c0);
         HIP_TRY(c, sbr::launch_learn_logistic(beta + c0, eta + c0, t_end + c0, lk, Lk, ls), SBR_EDEVICE);
+        if (c->timing) {
+            c->ck_ev[2 * k] = next_event(c);
+            if (c->ck_ev[2 * k]) (void)hipEventRecord(c->ck_ev[2 * k], ls);
+        }
         HIP_TRY(c, hipEventRecord(c->ev_learned[k], ls), SBR_EDEVICE);
         sbr::EqArgs ea{kappa, (int32_t)n_u, o.bisect_max_iters, c->lds_cap_b, nullptr,
                        (o.flags & SBR_FLAG_EXHAUSTIVE) ? 1 : 0, (o.flags >> 8) & 7};
         HIP_TRY(c, sbr::launch_equilibrium(Lk, eta + c0, t_end + c0, u, ea, result_rows(out, (size_t)(c0 * n_u)),
                                            (int)nb, ls), SBR_EDEVICE);
+        if (c->timing) {
+            c->ck_ev[2 * k + 1] = next_event(c);
+            if (c->ck_ev[2 * k + 1]) (void)hipEventRecord(c->ck_ev[2 * k + 1], ls);
+        }
         HIP_TRY(c, hipEventRecord(c->ev_eq[k], ls), SBR_EDEVICE);
     }
     for (int k = 0; k < kSweepChunks; k++)
@@ -819,6 +880,7 @@ int sbr_free(sbr_ctx* c)
         if (e) (void)hipEventDestroy(e);
     if (c->rq) (void)hipFree(c->rq);
     if (c->stage) (void)hipFree(c->stage);
+    if (c->res_pin) (void)hipHostFree(c->res_pin);
     if (c->kn_dev) (void)hipFree(c->kn_dev);
     if (c->kn_pin) (void)hipHostFree(c->kn_pin);
     if (c->kn_zc) (void)hipHostFree(c->kn_zc);
@@ -976,24 +1038,53 @@ int sbr_sweep_baseline(sbr_ctx* c, const double* beta, const double* eta, const 
     double* dres = (double*)(base + ((in_bytes + 255) & ~(size_t)255));
     sbr::ResultSoA r{dres, dres + np, dres + 2 * np, dres + 3 * np, dres + 4 * np, (uint32_t*)(dres + 5 * np),
                      (int32_t*)((uint32_t*)(dres + 5 * np) + np)};
+    rc = ensure_res_pin(c, out_bytes);
+    if (rc) return rc;
+    const auto h0 = std::chrono::steady_clock::now();
+    hipEvent_t pe[4] = {};
     return fenced(c, nullptr, false, [&](hipStream_t s) -> int {
+        if (c->timing)
+            for (hipEvent_t& e : pe) e = next_event(c);
+        auto mark = [&](int k) { if (pe[k]) (void)hipEventRecord(pe[k], s); };
+        mark(0);
         HIP_TRY(c, hipMemcpyAsync(dbeta, beta, n_beta * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
         HIP_TRY(c, hipMemcpyAsync(deta, eta, n_beta * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
         HIP_TRY(c, hipMemcpyAsync(dtend, t_end, n_beta * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
         HIP_TRY(c, hipMemcpyAsync(du, u, n_u * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+        mark(1);
         rc = run_baseline(c, s, dbeta, deta, dtend, x0, du, n_beta, n_u, p, kappa, lambda, o, r, nullptr);
         if (rc) return rc;
-        double* hs[5] = {out->xi, out->tau_in_unc, out->tau_out_unc, out->aw_max, out->tol};
-        for (int k = 0; k < 5; k++)
-            if (hs[k]) HIP_TRY(c, hipMemcpyAsync(hs[k], dres + k * np, np * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
-        if (out->status) HIP_TRY(c, hipMemcpyAsync(out->status, r.status, np * 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
-        if (out->iters) HIP_TRY(c, hipMemcpyAsync(out->iters, r.iters, np * 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        mark(2);
+        // the result SoA is one contiguous block on the device: one DMA copy into pinned memory,
+        // then the fields into the caller's arrays on several host threads
         int32_t gave_up = 0;
         if (c->rs_used) HIP_TRY(c, hipMemcpyAsync(&gave_up, c->rq + 1, 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        const size_t blk = np * (5 * 8 + 4 + (out->iters ? 4 : 0));
+        HIP_TRY(c, hipMemcpyAsync(c->res_pin, dres, blk, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        mark(3);
         HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
         if (gave_up) return fail(c, SBR_EDEVICE, "readiness schedule: an equilibrium workgroup timed out");
+        const auto h1 = std::chrono::steady_clock::now();
+        {
+            const char* P = (const char*)c->res_pin;
+            std::vector<std::array<size_t, 3>> pieces;
+            double* hs[5] = {out->xi, out->tau_in_unc, out->tau_out_unc, out->aw_max, out->tol};
+            for (int k = 0; k < 5; k++)
+                if (hs[k]) pieces.push_back({(size_t)hs[k], (size_t)(P + (size_t)k * np * 8), np * 8});
+            if (out->status) pieces.push_back({(size_t)out->status, (size_t)(P + 5 * np * 8), np * 4});
+            if (out->iters) pieces.push_back({(size_t)out->iters, (size_t)(P + 5 * np * 8 + np * 4), np * 4});
+            parallel_copy(pieces);
+        }
         if (o.early_exit_nan_run > 0 && out->status && out->xi && out->aw_max && out->tol)
             sbr_apply_early_exit(n_beta, n_u, o.early_exit_nan_run, out);
+        if (pe[3]) {
+            float a = 0.f;
+            for (int k = 0; k < 3; k++)
+                c->ph_ms[k] = hipEventElapsedTime(&a, pe[k], pe[k + 1]) == hipSuccess ? (double)a : -1.0;
+            const auto h2 = std::chrono::steady_clock::now();
+            c->ph_ms[3] = std::chrono::duration<double, std::milli>(h2 - h1).count();
+            c->ph_ms[4] = std::chrono::duration<double, std::milli>(h2 - h0).count();
+        }
         return SBR_OK;
     });
 }
@@ -1554,6 +1645,35 @@ int sbr_equilibrium_on_knots(sbr_ctx* c, const double* t, const double* G, int64
             else for (int64_t i = 0; i < ntau; i++) dst[k][i] = NAN;
         }
     }
+    return SBR_OK;
+}
+
+int sbr_chunk_timeline(sbr_ctx* c, void* stream, int32_t* n_chunks, double* ms)
+{
+    SBR_PER_DEVICE_DIAG(c);
+    if (!c || !n_chunks) return SBR_EARG;
+    *n_chunks = 0;
+    if (!c->ck_start || c->ck_ev.empty()) return SBR_OK;
+    HIP_TRY(c, hipStreamSynchronize((hipStream_t)stream), SBR_EDEVICE);
+    for (hipStream_t ls : c->lstream)
+        if (ls) HIP_TRY(c, hipStreamSynchronize(ls), SBR_EDEVICE);
+    const int nk = (int)c->ck_ev.size() / 2;
+    for (int k = 0; k < nk; k++)
+        for (int e = 0; e < 2; e++) {
+            float a = -1.f;
+            hipEvent_t ev = c->ck_ev[2 * k + e];
+            if (ev && hipEventElapsedTime(&a, c->ck_start, ev) != hipSuccess) a = -1.f;
+            if (ms) ms[2 * k + e] = ev ? (double)a : -1.0;
+        }
+    *n_chunks = nk;
+    return SBR_OK;
+}
+
+int sbr_host_phases(sbr_ctx* c, double* ms5)
+{
+    SBR_PER_DEVICE_DIAG(c);
+    if (!c || !ms5) return SBR_EARG;
+    for (int k = 0; k < 5; k++) ms5[k] = c->ph_ms[k];
     return SBR_OK;
 }
 

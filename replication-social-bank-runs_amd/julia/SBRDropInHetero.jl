@@ -14,9 +14,10 @@ heterogeneity_solver.jl by this file.  Then :59, :67 and :76 run unchanged:
     at eps() (sbr_learn_hetero), the PDFs by compute_pdf_hetero (:114-134);
   * `solve_equilibrium_hetero(lr, econ; verbose)` → SolvedModelHetero
     (heterogeneity_solver.jl:241-293): per-group buffers, ξ of compute_ξ_hetero with its
-    validity check, bankrun / converged / tolerance — one GPU solve through
-    sbr_hetero_point_paths (bit-identical to a sweep point); HRs as the reference builds
-    them (hazard_rate per group on the learning grid, :255);
+    validity check, bankrun / converged / tolerance — one GPU solve on lr's own knot grid
+    and group CDFs through sbr_hetero_equilibrium_on_knots (no learning ODE; knots and
+    hazards stay resident across the script's per-u calls); HRs are the engine's HR_k on
+    hazard_rate's explicit grid (:255);
   * `get_AW_functions_hetero!(result)` → (AW_cum, AW_OUT_groups, AW_IN_groups, AW_groups,
     AW_max) (:386-402 / get_AW_hetero :316-375): AW_cum and AW_max are the engine's AW_total
     path, the per-group curves are rebuilt from the group CDFs.
@@ -79,16 +80,18 @@ function get_AW_hetero(result::SolvedModelHetero, AW_total = nothing)
             AW_groups = nets, AW_max = maximum(AW_total))
 end
 
-# heterogeneity_solver.jl:241-293 — one GPU solve (hazards, buffers, compute_ξ_hetero, validity, AW path)
+# heterogeneity_solver.jl:241-293 — one GPU solve on lr_hetero's own knots and group CDFs
+# (hazards, buffers, compute_ξ_hetero, validity, AW path); no learning ODE
 function solve_equilibrium_hetero(lr_hetero::LearningResultsHetero, econ::EconomicParameters; verbose = false)
     solve_start = time()
     lp = lr_hetero.params
-    r = SBREngine.solve_hetero_point_paths(sbr_context(), lp.βs, lp.dist, econ.u; η = econ.η, tspan_end = lp.tspan[2],
-                                           x0 = lp.x0, p = econ.p, κ = econ.κ, λ = econ.λ)
+    Gm = reduce(hcat, [cdf.itp.coefs for cdf in lr_hetero.learning_cdfs])   # n × K, on lr_hetero.grid
+    r = SBREngine.hetero_equilibrium_on_knots(sbr_context(), collect(Float64, lr_hetero.grid), Gm, lp.βs, lp.dist,
+                                              econ.u; η = econ.η, tspan_end = lp.tspan[2], p = econ.p, κ = econ.κ,
+                                              λ = econ.λ)
     (r.status & SBREngine.SBR_OOB) != 0 && throw(BoundsError(lr_hetero.learning_cdfs[1], econ.η))
-    length(r.t) == length(lr_hetero.grid) || error("engine knot grid differs from lr_hetero.grid")
-    HRs = Any[hazard_rate(econ.p, econ.λ, lr_hetero.learning_pdfs[k], econ.η; grid = lr_hetero.grid)
-              for k in eachindex(lp.βs)]
+    # the reference's HRs (:255): hazard_rate per group on its explicit grid, from the engine
+    HRs = Any[LinearInterpolation(r.τ_bar, r.HR[:, k]) for k in eachindex(lp.βs)]
     bankrun = (r.status & SBREngine.SBR_RUN) != 0
     converged = (r.status & SBREngine.SBR_CONVERGED) != 0
     result = SolvedModelHetero(r.ξ, r.τ_bar_IN_UNCs, r.τ_bar_OUT_UNCs, HRs, bankrun, econ, lr_hetero, converged,

@@ -48,8 +48,9 @@ end
 """
     Context(device = 0)            one MI355X
     Context(; n_gpus = 8)          n GPUs of the node: the sweeps below fan out inside libsbr
-                                   (one host thread per GPU, β columns dealt cyclically, RCCL
-                                   gather of the results to GPU 0) — same results as one GPU
+                                   (one host thread per GPU, β columns dealt cyclically, each GPU
+                                   copying its own columns into the caller's arrays) — same
+                                   results as one GPU
 """
 mutable struct Context
     ptr::Ptr{Cvoid}
@@ -351,6 +352,45 @@ function learn_hetero(ctx::Context, βs, dist, tspan_end, x0; cap = 1 << 14)
     end
     n = Int(nk[])
     return t[1:n], permutedims(reshape(G[1:n*K], K, n)), st[]
+end
+
+"""
+    hetero_equilibrium_on_knots(ctx, t, Gm, βs, dist, u; η, tspan_end, p = 0.9, κ = 0.3, λ = 0.1)
+
+`solve_equilibrium_hetero(lr_hetero, econ)` + `get_AW_functions_hetero!`
+(heterogeneity_solver.jl:241-293, 316-402) on a LearningResultsHetero's own knot grid `t` and
+group CDF values `Gm` (n × K: column k = `learning_cdfs[k]`'s coefficients): no learning ODE.
+Knots, CDFs and the K hazard paths stay on the GPU while the inputs repeat.  Returns ξ, the
+per-group buffers, AW_max, the tolerance, the status, the hazard grid τ̄ with HR_k(τ̄) as the
+columns of `HR` (the reference's `HRs`, :255) and `AW_total` on the knots (NaN without a run).
+"""
+function hetero_equilibrium_on_knots(ctx::Context, t::Vector{Float64}, Gm::AbstractMatrix, βs, dist, u; η, tspan_end,
+                                     p = 0.9, κ = 0.3, λ = 0.1)
+    n = length(t); K = length(dist)
+    size(Gm) == (n, K) || throw(ArgumentError("Gm must be length(t) × length(dist)"))
+    Gk = Matrix{Float64}(permutedims(Gm))        # knot-major [n][K] == a K × n column-major matrix
+    b = collect(Float64, βs); d = collect(Float64, dist)
+    cap = n + 1
+    res = fill(NaN, 5); st = UInt32[0]; it = Int32[0]; nt = Ref{Int64}(0)
+    tin = zeros(Float64, K); tout = zeros(Float64, K)
+    hr = Matrix{Float64}(undef, cap, K); aw = Vector{Float64}(undef, n)
+    uv = Float64[u]
+    opts = Ref(Opts(; early_exit = 0))
+    GC.@preserve t Gk b d uv res st it tin tout hr aw begin
+        soa = Ref(ResultSoA(pointer(res, 1), C_NULL, C_NULL, pointer(res, 4), pointer(res, 5), pointer(st),
+                            pointer(it)))
+        rc = ccall((:sbr_hetero_equilibrium_on_knots, libsbr), Cint,
+                   (Ptr{Cvoid}, Int32, Ptr{Float64}, Ptr{Float64}, Int64, Ptr{Float64}, Ptr{Float64}, Float64,
+                    Float64, Ptr{Float64}, Int64, Float64, Float64, Float64, Ref{Opts}, Ref{ResultSoA},
+                    Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Int64, Ref{Int64}),
+                   ctx.ptr, Int32(K), t, Gk, n, b, d, η, tspan_end, uv, 1, p, κ, λ, opts, soa, tin, tout, hr, aw,
+                   cap, nt)
+        check(ctx, rc)
+    end
+    k = nt[]
+    return (ξ = res[1], AW_max = res[4], tolerance = res[5], status = st[1], τ_bar_IN_UNCs = tin,
+            τ_bar_OUT_UNCs = tout, τ_bar = k > 0 ? vcat(t[t .<= η], η)[1:k] : Float64[], HR = hr[1:k, :],
+            AW_total = aw)
 end
 
 """

@@ -98,6 +98,8 @@ _SIGS = {
     "sbr_selftest_detmath": (ctypes.c_int, [_P, _P, _P, ctypes.c_int, _P, _P, _P]),
     "sbr_timing_enable": (ctypes.c_int, [_P, ctypes.c_int]),
     "sbr_last_schedule": (ctypes.c_int, [_P, _P]),
+    "sbr_host_phases": (ctypes.c_int, [_P, _P]),
+    "sbr_chunk_timeline": (ctypes.c_int, [_P, _P, _P, _P]),
     "sbr_timing_read": (ctypes.c_int, [_P, _P, _P, _P, _P]),
     "sbr_learn_stats": (ctypes.c_int, [_P, _I64, _P, _P, _P, _P, _P]),
     "sbr_hetero_learn_stats": (ctypes.c_int, [_P, _I64, _P, _P, _P, _P, _P]),

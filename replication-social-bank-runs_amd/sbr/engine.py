@@ -534,6 +534,20 @@ class Engine:
               "sbr_device_info")
         return dict(lds_bytes_per_block=a.value, lds_knot_capacity=b.value, cu_count=c.value)
 
+    def host_phases(self) -> dict:
+        """Phases (ms) of the last host-pointer sweep_baseline made with timing enabled."""
+        v = (ctypes.c_double * 5)()
+        check(self._L.sbr_host_phases(self._ctx, v), self._ctx, "sbr_host_phases")
+        return dict(zip(("h2d", "kernels", "d2h", "host_copy_early_exit", "call"), list(v)))
+
+    def chunk_timeline(self, stream: int | None = None) -> list:
+        """[(learning end, equilibrium end)] in ms per column chunk of the last chunked single
+        sweep made with timing enabled (sbr_chunk_timeline); [] otherwise."""
+        n = ctypes.c_int32()
+        v = (ctypes.c_double * 16)()
+        check(self._L.sbr_chunk_timeline(self._ctx, stream, ctypes.byref(n), v), self._ctx, "sbr_chunk_timeline")
+        return [(v[2 * k], v[2 * k + 1]) for k in range(n.value)]
+
     def last_schedule(self) -> int:
         """1 if the last single sweep took the per-column readiness schedule, 0 if chunked."""
         v = ctypes.c_int32()

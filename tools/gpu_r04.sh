@@ -41,6 +41,17 @@ for s in ${STEPS:-tests smoke bench single}; do
     soctracevar) run soctrace_$VAR 600 env SBR_SOCIAL_TRACE=1 SBR_LIB=replication-social-bank-runs_amd/lib_var/$VAR/libsbr.so python -u bench.py --workload social --steps 1 --warmup 0 --no-cpu-baseline ;;
     socdump) run socdump 600 python -u bench.py --workload social --steps 1 --warmup 0 --no-cpu-baseline --social-dump $OUT/social_dump.npz ;;
     hetvars) for v in ${VARS:-}; do run hetero_$v 600 env SBR_LIB=replication-social-bank-runs_amd/lib_var/$v/libsbr.so python -u bench.py --workload hetero --steps 10 --warmup 2 --phases --no-cpu-baseline; done ;;
+    pmcall) for w in ${PMCW:-base hetero interest socbulk soclone}; do
+              case $w in
+                base) BA="" ;;
+                hetero) BA="--workload hetero --steps 2 --warmup 1" ;;
+                interest) BA="--workload interest --steps 1 --warmup 1" ;;
+                socbulk) BA="--workload social --steps 1 --warmup 0 --social-max-iter 16" ;;
+                soclone) BA="--workload social --steps 1 --warmup 0 --social-cols 2 --social-max-iter 16" ;;
+              esac
+              PMC_OUT=$OUT/pmc_$w BENCH_ARGS="$BA" bash tools/pmc.sh > "$OUT/pmc_$w.out" 2>&1; rc=$?
+              echo "pmc_$w rc=$rc" | tee -a "$OUT/steps.log"; [ $rc -ne 0 ] && exit $rc
+            done ;;
     config2) run config2 300 python -u bench.py --workload config2 --steps 20 --warmup 2 ;;
     dropin) run dropin 600 python -u bench.py --workload dropin --steps 30 ;;
     knotsprobe) run knotsprobe 300 python -u tools/knots_probe.py 2000 && run knotsprof 300 rocprofv3 --kernel-trace --stats -d "$OUT/knotsprof" -o run --output-format csv -- python3 tools/knots_probe.py 500 ;;
