@@ -912,13 +912,20 @@ struct HCol {
     }
 };
 
+#ifndef SBR_HET_UBCACHE
+#define SBR_HET_UBCACHE 0 // A/B: pass 2 of AW_max re-reads pass 1's range bounds (private float array)
+#endif
+#ifndef SBR_HET_UBC_MAX
+#define SBR_HET_UBC_MAX 40 // 256-knot ranges cached (the LDS slab holds ≤ 10,176 knots: 40 ranges)
+#endif
 template <int K, class PT>
 __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const double* __restrict__ dist,
                                                    const double u, const double kappa, const int max_iters,
                                                    const double tolerance, const uint32_t lbits, double& xi_o,
                                                    double& aw_o, double& tol_o, uint32_t& st_o, int& it_o,
                                                    double* tin, double* tout, const bool mono, const int diag,
-                                                   double* __restrict__ aw_path, const double env, const bool sep)
+                                                   double* __restrict__ aw_path, const double env, const bool sep,
+                                                   double* __restrict__ tin_g, double* __restrict__ tout_g)
 {
     xi_o = NAN; aw_o = NAN; tol_o = INFINITY; it_o = 0;
     const int n = C.n;
@@ -969,6 +976,14 @@ __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const d
         tout[k] = b;
         all_eq = all_eq && (a == b);
     }
+    // the buffers are final here: store them now, so that they need no registers through the
+    // validity check and the AW phase (only min(τ_k, ξ) is live there)
+    if (tin_g)
+#pragma unroll
+        for (int k = 0; k < K; k++) tin_g[k] = tin[k];
+    if (tout_g)
+#pragma unroll
+        for (int k = 0; k < K; k++) tout_g[k] = tout[k];
     if (all_eq) {
         st_o = SBR_NO_RUN_HR_BELOW_U | SBR_CONVERGED | lbits;
         tol_o = 0.0;
@@ -1215,34 +1230,46 @@ __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const d
         };
         auto end_of = [&](int i0, int w) { return i0 + w < n ? i0 + w : n; };
         if (!flag) {
+            // pass 1 (best 256 → 64 → 8-knot range by bound, evaluated) keeps its bounds, rounded
+            // up to float, in a private array (scratch): pass 2 re-reads them instead of redoing
+            // the 2K bracket searches and gathers of each bound (ub_rng's value does not depend on
+            // the hints, so a cached bound is the bound)
+            const bool cache = SBR_HET_UBCACHE && n <= 256 * SBR_HET_UBC_MAX;
+            float c256[SBR_HET_UBCACHE ? SBR_HET_UBC_MAX : 1], c64[4], c8[8];
             int bs = 0;
             double bu = -INFINITY;
             for (int i0 = 0; i0 < n; i0 += 256) {
                 const double ub = ub_rng(i0, end_of(i0, 256) - 1);
+                if (SBR_HET_UBCACHE && cache) c256[i0 >> 8] = __double2float_ru(ub);
                 if (!(ub <= bu)) { bu = ub; bs = i0; }
             }
             int bb = bs;
             bu = -INFINITY;
             for (int i0 = bs; i0 < end_of(bs, 256); i0 += 64) {
                 const double ub = ub_rng(i0, end_of(i0, 64) - 1);
+                c64[(i0 - bs) >> 6] = __double2float_ru(ub);
                 if (!(ub <= bu)) { bu = ub; bb = i0; }
             }
             int b8 = bb;
             bu = -INFINITY;
             for (int i0 = bb; i0 < end_of(bb, 64); i0 += 8) {
                 const double ub = ub_rng(i0, end_of(i0, 8) - 1);
+                c8[(i0 - bb) >> 3] = __double2float_ru(ub);
                 if (!(ub <= bu)) { bu = ub; b8 = i0; }
             }
             eval_range(b8, end_of(b8, 8));
             for (int s0 = 0; s0 < n && mx == mx; s0 += 256) {
                 const int se = end_of(s0, 256);
-                if (ub_rng(s0, se - 1) <= mx) continue;
+                if ((SBR_HET_UBCACHE && cache) ? ((double)c256[s0 >> 8] <= mx) : (ub_rng(s0, se - 1) <= mx)) continue;
                 for (int k0 = s0; k0 < se && mx == mx; k0 += 64) {
                     const int ke = end_of(k0, 64);
-                    if (ub_rng(k0, ke - 1) <= mx) continue;
+                    if ((SBR_HET_UBCACHE && s0 == bs) ? ((double)c64[(k0 - bs) >> 6] <= mx) : (ub_rng(k0, ke - 1) <= mx))
+                        continue;
                     for (int i0 = k0; i0 < ke && mx == mx; i0 += 8) {
                         const int ie = end_of(i0, 8);
-                        if (i0 == b8 || ub_rng(i0, ie - 1) <= mx) continue;
+                        if (i0 == b8) continue;
+                        if ((SBR_HET_UBCACHE && k0 == bb) ? ((double)c8[(i0 - bb) >> 3] <= mx) : (ub_rng(i0, ie - 1) <= mx))
+                            continue;
                         eval_range(i0, ie);
                     }
                 }
@@ -1269,7 +1296,14 @@ template <int K, int BLOCK, int MODE>
 #ifndef SBR_HET_MINW
 #define SBR_HET_MINW 2 // waves per SIMD: two 4-wave workgroups per CU (LDS slab: SBR_HET_LDS in sbr_capi.hip)
 #endif
-__global__ __launch_bounds__(BLOCK, SBR_HET_MINW) void equilibrium_hetero_kernel(HeteroBufs L, const double* __restrict__ dist,
+#ifndef SBR_HET_NVGPR
+#define SBR_HET_NVGPR 0 // > 0: VGPR cap (amdgpu_num_vgpr counts half of the unified file on gfx950)
+#endif
+__global__ __launch_bounds__(BLOCK, SBR_HET_MINW)
+#if SBR_HET_NVGPR
+__attribute__((amdgpu_num_vgpr(SBR_HET_NVGPR / 2)))
+#endif
+void equilibrium_hetero_kernel(HeteroBufs L, const double* __restrict__ dist,
                                                                    const double* __restrict__ eta,
                                                                    const double* __restrict__ t_end,
                                                                    const double* __restrict__ u, HeteroEqArgs a,
@@ -1382,33 +1416,33 @@ __global__ __launch_bounds__(BLOCK, SBR_HET_MINW) void equilibrium_hetero_kernel
     double xi, aw, tol, tin[K], tout[K];
     uint32_t st;
     int it;
+    const size_t o = (size_t)c * (size_t)a.n_u + j;
+    double* const tin_g = tin_out ? tin_out + o * K : nullptr;
+    double* const tout_g = tout_out ? tout_out + o * K : nullptr;
     if ((lst & (SBR_ARG_INVALID | SBR_OOB)) || n < 2 || !(uj >= 0.0)) {
         xi = NAN; aw = NAN; tol = INFINITY; it = 0;
 #pragma unroll
-        for (int k = 0; k < K; k++) { tin[k] = NAN; tout[k] = NAN; }
+        for (int k = 0; k < K; k++) {
+            if (tin_g) tin_g[k] = NAN;
+            if (tout_g) tout_g[k] = NAN;
+        }
         st = ((lst & SBR_ARG_INVALID) || !(uj >= 0.0)) ? SBR_ARG_INVALID : (SBR_OOB | lbits);
     } else if constexpr (MODE == 1) {
         HCol<K, const double*> C{smem, L.G + (size_t)c * cap * K, L.hr + (size_t)c * K * cap, n, L.n_tau[c],
                                  L.n_le[c], cap, eta[c], t_end[c], sums && !a.exhaustive ? hsum : nullptr, nblk};
         solve_hetero_point<K>(C, dl, uj, a.kappa, a.max_iters, a.tolerance, lbits, xi, aw, tol, st, it, tin, tout,
-                              mono, a.diag, a.aw_path, env, fits && s_close == 0);
+                              mono, a.diag, a.aw_path, env, fits && s_close == 0, tin_g, tout_g);
     } else {
         HCol<K, const double*> C{gT, L.G + (size_t)c * cap * K, L.hr + (size_t)c * K * cap, n, L.n_tau[c],
                                  L.n_le[c], cap, eta[c], t_end[c], nullptr, 0};
         solve_hetero_point<K>(C, dl, uj, a.kappa, a.max_iters, a.tolerance, lbits, xi, aw, tol, st, it, tin, tout,
-                              mono, a.diag, a.aw_path, env, fits && s_close == 0);
+                              mono, a.diag, a.aw_path, env, fits && s_close == 0, tin_g, tout_g);
     }
-    const size_t o = (size_t)c * (size_t)a.n_u + j;
     out.xi[o] = xi;
     out.aw_max[o] = aw;
     out.tol[o] = tol;
     out.status[o] = st;
     if (out.iters) out.iters[o] = it;
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-        if (tin_out) tin_out[o * K + k] = tin[k];
-        if (tout_out) tout_out[o * K + k] = tout[k];
-    }
 }
 
 template <int K>

@@ -34,7 +34,12 @@ using Interpolations
 # heterogeneity_learning.jl:114-134 — g_k = (1 − G_k)·β_k·ω with ω = Σ_j dist_j G_j, on the knots
 function compute_pdf_hetero(βs, dist, learning_cdfs, t_values)
     Gm = reduce(hcat, [cdf.(t_values) for cdf in learning_cdfs])   # n × K
-    ω = Gm * dist
+    # ω as the reference's `sum(dist[j] * I_t[j] for j in 1:K)` (:124): a left fold from the
+    # first term, not a BLAS gemv, so every knot sees the same roundings
+    ω = dist[1] .* Gm[:, 1]
+    for j in 2:length(dist)
+        ω = ω .+ dist[j] .* Gm[:, j]
+    end
     return Any[LinearInterpolation(t_values, (1 .- Gm[:, k]) .* βs[k] .* ω) for k in eachindex(βs)]
 end
 

@@ -55,6 +55,17 @@ def main():
             lines.append("  -> wait_any %.1f%%  issue_stall %.1f%%  active %.1f%% of wave cycles" % (
                 100 * c["SQ_WAIT_ANY"] / w, 100 * c.get("SQ_WAIT_INST_ANY", 0) / w,
                 100 * c.get("SQ_ACTIVE_INST_ANY", 0) / w))
+        if "SQ_THREAD_CYCLES_VALU" in c and c.get("SQ_ACTIVE_INST_VALU"):
+            lines.append("  -> VALU lane utilisation %.3f (SQ_THREAD_CYCLES_VALU / (SQ_ACTIVE_INST_VALU x 64))" % (
+                c["SQ_THREAD_CYCLES_VALU"] / (64 * c["SQ_ACTIVE_INST_VALU"])))
+        if "SQ_INSTS_SALU" in c and c.get("SQ_INSTS_VALU"):
+            lines.append("  -> SALU share %.3f of VALU + SALU instructions" % (
+                c["SQ_INSTS_SALU"] / (c["SQ_INSTS_SALU"] + c["SQ_INSTS_VALU"])))
+        if c.get("TCC_HIT_sum", 0) + c.get("TCC_MISS_sum", 0) > 0:
+            lines.append("  -> L2 hit rate %.3f" % (c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"])))
+        if c.get("TCP_TOTAL_CACHE_ACCESSES_sum") and "TCP_TCC_READ_REQ_sum" in c:
+            lines.append("  -> L1 (TCP) read requests reaching L2: %.3f of accesses" % (
+                c["TCP_TCC_READ_REQ_sum"] / c["TCP_TOTAL_CACHE_ACCESSES_sum"]))
         if "FETCH_SIZE" in c:
             lines.append("  -> HBM read %.1f MB (FETCH_SIZE x2, gfx950)" % (2 * c["FETCH_SIZE"] * 1024 / 1e6))
         if "WRITE_SIZE" in c:
