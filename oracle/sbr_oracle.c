@@ -1334,6 +1334,7 @@ static void social_point(double beta, double eta, double x0, double u, double p,
                     if (k == 0) err = d;
                     else if (!(err != err || err > d)) err = d; /* generic_normInf: NaN sticks */
                 }
+                if (getenv("SBRO_DEBUG")) fprintf(stderr, "social it %d: err %.6e xi %.6f\n", iter, err, xi_new);
                 if (oob) stop_oob = 1;
                 else if (err < tol) {
                     converged = 1;

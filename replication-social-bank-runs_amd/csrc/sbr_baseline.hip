@@ -534,6 +534,9 @@ struct Summ {
     bool scan;
     double dd;
     bool bnb; // the branch-and-bound bounds are available (mono, or the prefix/suffix tables built)
+    // aw_scan's knot offset for AW_OUT(b_j) <= G[j + koff]: 1 when consecutive knots are more than
+    // 1e-15·t[n−1] apart (b_j then lies below t[j + 1]: bracket <= j), else 2 (knots 2 apart)
+    int koff;
 };
 
 template <class P>
@@ -574,10 +577,13 @@ __device__ __forceinline__ int first_ge_down(F key, int hi, double x)
 // (+ the 1e-14 rounding margin) do not already put it at or below the running maximum; runs
 // of knots the bounds dismiss are skipped with one search in G (right) or in G and τ̄ (left).
 // The maximum equals the exhaustive one bit for bit (G has no NaN here).
+#ifndef SBR_AW_K1
+#define SBR_AW_K1 1 // aw_scan bounds AW_OUT(b_j) by G[j + 1] where consecutive knots are separated
+#endif
 template <class P>
 __device__ __forceinline__ void aw_scan(P T, P G, const int n, const int ntau, const int nle, const double ETA,
                                         const double xi, const double icc, const double occ, const double G0,
-                                        const double dd, const int c, double& mx, int& nev)
+                                        const double dd, const int c, double& mx, int& nev, const int koff = 2)
 {
     const double M = 1e-14 + 4.0 * dd;
     auto tau = [&](int i) -> double { return i < nle ? T[i] : ETA; };
@@ -633,7 +639,7 @@ __device__ __forceinline__ void aw_scan(P T, P G, const int n, const int ntau, c
         const double lb = av >= 0 ? ga0 : 0.0;
         LA = LA > lb ? LA : lb;
         const double V = (((mx - G0) + LA) - M) - dd; // G[k] <= V: every knot up to k is <= V + dd
-        const int k2 = i + 2 < n - 1 ? i + 2 : n - 1;
+        const int k2 = i + koff < n - 1 ? i + koff : n - 1;
         if (G[k2] > V) {
             const double v = exact(i, av, xa);
             if (v > mx) mx = v;
@@ -644,7 +650,7 @@ __device__ __forceinline__ void aw_scan(P T, P G, const int n, const int ntau, c
         // every knot j with G[min(j + 2, n − 1)] <= V is at or below mx: skip to the first other
         const int kl = ssl_gallop(G, n, k2, V);
         if (kl >= n - 1) break;
-        const int inext = kl - 1; // G[kl + 1] > V
+        const int inext = kl + 1 - koff; // G[kl + 1] > V: the first knot whose bound is not dismissed
         const double an = av_of(inext);
         seek(ka + (inext - i), an > 0 ? an : 0.0);
         i = inext;
@@ -656,7 +662,7 @@ __device__ __forceinline__ void aw_scan(P T, P G, const int n, const int ntau, c
         seek(kc, av > 0 ? av : 0.0);
     }
     for (int i = c - 1; i >= 0;) {
-        const int k2 = i + 2 < n - 1 ? i + 2 : n - 1;
+        const int k2 = i + koff < n - 1 ? i + koff : n - 1;
         const double g2 = G[k2] > 0.0 ? G[k2] : 0.0;
         UB = UB < g2 ? UB : g2;
         const double Vp = (((UB + G0) + M) - mx) + dd; // AW_IN(a_j) >= G[bracket(a_j)] − dd
@@ -953,7 +959,8 @@ __device__ __forceinline__ void solve_from_buffers(P T, P G, P H, const Summ& S,
             const int ic = predicted ? ssl_range(T, 0, (nle > 0 ? nle : 1) - 1, tstar < T[0] ? T[0] : tstar) : 0;
 #if SBR_AW_SCAN
             if (scan) {
-                aw_scan(T, G, n, ntau, nle, ETA, xi, icc, occ, G0, S.dd, ic < ntau ? ic : ntau - 1, mx, nblk_eval);
+                aw_scan(T, G, n, ntau, nle, ETA, xi, icc, occ, G0, S.dd, ic < ntau ? ic : ntau - 1, mx, nblk_eval,
+                        S.koff);
             } else
 #endif
 #ifndef SBR_EQ_NOFALLBACK_TEST
@@ -1276,19 +1283,20 @@ __device__ __forceinline__ void eq_column(const int b, const int j0, const int j
     __shared__ int eq_next;
     __shared__ int s_nonmono;
     __shared__ int s_noscan;
+    __shared__ int s_near1;                // two consecutive knots within 1e-15·t[n−1]
     __shared__ int s_ndec;                 // decreases of G between consecutive knots
     __shared__ unsigned long long s_maxdec; // largest decrease (bits of a nonnegative double)
     __shared__ double s_thalf;
     // every shared flag is initialised before the first barrier: lanes >= nq set
     // s_nonmono right after it, so a later store by thread 0 could clear their flag
-    if (threadIdx.x == 0) { eq_next = 0; s_nonmono = 0; s_noscan = 0; s_ndec = 0; s_maxdec = 0; s_thalf = NAN; }
+    if (threadIdx.x == 0) { eq_next = 0; s_nonmono = 0; s_noscan = 0; s_near1 = 0; s_ndec = 0; s_maxdec = 0; s_thalf = NAN; }
     if (fits) {
         for (int i = threadIdx.x; i < n; i += BLOCK) { sT[i] = gT[i]; sG[i] = gG[i]; }
         if (INTEREST)
             for (int i = threadIdx.x; i < ntau; i += BLOCK) sH[i] = gH[i];
     }
     __syncthreads();
-    Summ S{nullptr, nullptr, nullptr, nullptr, false, (double)NAN, false, 0.0, false};
+    Summ S{nullptr, nullptr, nullptr, nullptr, false, (double)NAN, false, 0.0, false, 2};
     if (fits && !a.exhaustive) {
         const int nbh = (ntau + 63) >> 6, nbg = (n + 7) >> 3;
         // HR summaries: 8 lanes per 64-entry block, 8 independent loads each (HR is read from
@@ -1344,9 +1352,13 @@ __device__ __forceinline__ void eq_column(const int b, const int j0, const int j
                 }
                 // aw_scan's knot separation (Summ::scan)
                 const double sep = 1e-15 * sT[n - 1];
-                bool far = true;
-                for (int i = g << 3; i < e; i++) far &= i + 2 >= n || sT[i + 2] - sT[i] > sep;
+                bool far = true, far1 = true;
+                for (int i = g << 3; i < e; i++) {
+                    far &= i + 2 >= n || sT[i + 2] - sT[i] > sep;
+                    far1 &= i + 1 >= n || sT[i + 1] - sT[i] > sep;
+                }
                 if (!far) s_noscan = 1;
+                if (!far1) s_near1 = 1;
                 pmc[g] = mx; // block max for now
                 smc[g] = mn; // block min for now
             }
@@ -1381,7 +1393,7 @@ __device__ __forceinline__ void eq_column(const int b, const int j0, const int j
         const double dd = (double)s_ndec * sbr_bitsd(s_maxdec); // ≥ the largest drawdown
         S = Summ{hmax, hmin, pmc, smc, s_nonmono == 0, s_thalf,
                  n >= 2 && !s_noscan && dd <= 1e-12 && sG[0] >= 0.0 && sG[n - 1] <= 2.0, dd,
-                 s_nonmono == 0 || s_noscan != 0};
+                 s_nonmono == 0 || s_noscan != 0, (SBR_AW_K1 && s_near1 == 0) ? 1 : 2};
     }
     // Points are handed out to waves 64 at a time from an LDS counter, so a
     // wave that drew cheap no-run points goes back for more instead of idling

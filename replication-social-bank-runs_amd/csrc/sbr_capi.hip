@@ -1317,12 +1317,13 @@ int ensure_knots(sbr_ctx* c, size_t n, size_t n_u)
     size_t ck = c->kn_cap_k > 4096 ? c->kn_cap_k : 4096, cu = c->kn_cap_u > 64 ? c->kn_cap_u : 64;
     while (ck < n) ck *= 2;
     while (cu < n_u) cu *= 2;
+    // each buffer freed once and nulled (a second hipHostFree of the same pointer leaves a sticky
+    // error that the next HIP_TRY reports against an unrelated launch)
     if (c->kn_dev) (void)hipFree(c->kn_dev);
     if (c->kn_pin) (void)hipHostFree(c->kn_pin);
     if (c->kn_zc) (void)hipHostFree(c->kn_zc);
-    if (c->hk_dev) (void)hipFree(c->hk_dev);
-    if (c->hk_pin) (void)hipHostFree(c->hk_pin);
     c->kn_dev = c->kn_pin = nullptr;
+    c->kn_zc = c->kn_zc_dev = nullptr;
     c->kn_cap_k = c->kn_cap_u = 0;
     c->kn_valid = false;
     const KnotLayout K(ck, cu);
@@ -1332,8 +1333,6 @@ int ensure_knots(sbr_ctx* c, size_t n, size_t n_u)
     c->kn_cap_u = cu;
     // [t_end, u, results (8 doubles), AW_cum / AW_OUT / AW_IN (ck + 1 each)]
     const size_t zc = 16 + 3 * (ck + 1);
-    if (c->kn_zc) (void)hipHostFree(c->kn_zc);
-    c->kn_zc = c->kn_zc_dev = nullptr;
     HIP_TRY(c, hipHostMalloc(&c->kn_zc, zc * 8, hipHostMallocMapped | hipHostMallocCoherent), SBR_ENOMEM);
     HIP_TRY(c, hipHostGetDevicePointer((void**)&c->kn_zc_dev, c->kn_zc, 0), SBR_EDEVICE);
     c->kn_zc_cap = zc;

@@ -913,7 +913,10 @@ struct HCol {
 };
 
 #ifndef SBR_HET_UBCACHE
-#define SBR_HET_UBCACHE 0 // A/B: pass 2 of AW_max re-reads pass 1's range bounds (private float array)
+#define SBR_HET_UBCACHE 1 // pass 2 of AW_max re-reads pass 1's range bounds (config-4 step 45.3 -> 43.3 ms)
+#endif
+#ifndef SBR_HET_SHARE_DIV
+#define SBR_HET_SHARE_DIV 1 // exact AW evaluations share δ between groups with equal arguments
 #endif
 #ifndef SBR_HET_UBC_MAX
 #define SBR_HET_UBC_MAX 40 // 256-knot ranges cached (the LDS slab holds ≤ 10,176 knots: 40 ranges)
@@ -1163,6 +1166,11 @@ __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const d
         for (int i = i0; i < i1; i++) {
             const double ti = C.T[i];
             double cum = 0.0;
+            // Interpolation weights shared between groups: groups with the same shift
+            // (occ_k = ξ for most, equal icc_k where τ_IN,k ≥ ξ) have the same argument, bracket and
+            // weight δ, so δ is divided out once; and a b argument on a knot (t_i − ξ + ξ == t_i)
+            // has δ = 0 exactly — the same operands and operations as C.lerp, fewer divisions
+            double xa_p = NAN, da_p = 0.0, xb_p = NAN, db_p = 0.0;
 #pragma unroll
             for (int k = 0; k < K; k++) {
                 const double av = (ti - xi) + icc[k];
@@ -1172,8 +1180,22 @@ __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const d
                 if (!(xa <= thi) || !(xb <= thi)) flag |= SBR_OOB;
                 while (ja[k] + 1 < n && C.T[ja[k] + 1] <= xa) ja[k]++;
                 while (jb[k] + 1 < n && C.T[jb[k] + 1] <= xb) jb[k]++;
+#if SBR_HET_SHARE_DIV
+                const int qa = ja[k] > n - 2 ? n - 2 : (ja[k] < 0 ? 0 : ja[k]);
+                const int qb = jb[k] > n - 2 ? n - 2 : (jb[k] < 0 ? 0 : jb[k]);
+                double da = da_p, db = db_p;
+                if (!(xa == xa_p)) da = (xa - C.T[qa]) / (C.T[qa + 1] - C.T[qa]);
+                if (!(xb == xb_p)) {
+                    const double t0 = C.T[qb], t1 = C.T[qb + 1];
+                    db = (xb == t0 && t1 > t0) ? 0.0 : (xb - t0) / (t1 - t0);
+                }
+                xa_p = xa; da_p = da; xb_p = xb; db_p = db;
+                const double gi = C.g(qa, k) * (1.0 - da) + C.g(qa + 1, k) * da;
+                const double go = C.g(qb, k) * (1.0 - db) + C.g(qb + 1, k) * db;
+#else
                 const double gi = C.lerp(ja[k], k, xa);
                 const double go = C.lerp(jb[k], k, xb);
+#endif
                 const double awin = av >= 0 ? gi : 0.0;
                 const double awout = bv >= 0 ? go : 0.0;
                 cum = cum + dist[k] * (awout - awin);

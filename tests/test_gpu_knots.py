@@ -103,6 +103,28 @@ def test_u_vector_and_resident_cache(engine, oracle):
         check_point(a, b, str(kw))
 
 
+def test_workspace_growth_between_single_and_vector_calls(oracle):
+    """A fresh context: one-u calls (mapped-memory path), then a u vector past the workspace's
+    initial capacity (it is reallocated, mapped block included), then one-u calls again —
+    every result equal to the oracle (the reallocation leaves no stale error or buffer)."""
+    eng = sbr.Engine(0)
+    t, G, _ = oracle.learn_logistic(1.0, 30.0)
+    P = dict(beta=1.0, eta=15.0, t_end=30.0, p=0.5, kappa=0.6, lam=0.01)
+    us = sbr.julia_range("0.001", "0.2", 5000)[:2700]
+    for u in (float(us[5]), float(us[2000])):
+        g, o = solve_both(eng, oracle, t, G, P, u=u)
+        check_point(g, o, f"single {u}")
+    g = eng.equilibrium_on_knots(t, G, 1.0, 15.0, 30.0, us, 0.5, 0.6, 0.01, paths=False)
+    for j in range(0, 2700, 271):
+        o = oracle.equilibrium(t, G, 1.0, 15.0, 30.0, float(us[j]), 0.5, 0.6, 0.01)
+        for f in FIELDS:
+            assert same(g[f][j], o[f]), (j, f)
+        assert int(g["status"][j]) == o["status"] and int(g["iters"][j]) == o["iters"], j
+    for u in (float(us[7]), float(us[2699])):
+        g, o = solve_both(eng, oracle, t, G, P, u=u)
+        check_point(g, o, f"single again {u}")
+
+
 @pytest.mark.parametrize("case", ["eta_past_knots", "eta_is_last_knot", "eta_before_first"])
 def test_hazard_edges(engine, oracle, case):
     """η past the last knot (pdf(η) is the interpolant's BoundsError), η equal to the last
