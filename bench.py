@@ -644,22 +644,43 @@ def main_hetero(a):
             eng.timing_enable(False)
             ph[name] = e_ms / max(nc, 1)
         res["eq_phase_ms"] = ph
+    # the cpu_baseline leg's columns (every 16th) double as the check of the timed results: the
+    # last timed grid against the oracle, bit for bit (test infrastructure, after the timed region)
+    o_cols = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        o_cols = np.arange(0, nb, 16)
+    elif not a.no_verify:
+        o_cols = np.sort(np.random.default_rng(rank).choice(nb, min(4, nb), replace=False))
+    if o_cols is not None:
         sys.path.insert(0, str(REPO / "oracle"))
-        import oracle as O  # noqa: E402  (test infrastructure: cpu_baseline leg only)
+        import oracle as O  # noqa: E402  (test infrastructure: cpu_baseline / verification leg only)
 
         O.build()
         cores = usable_cores()
-        sub = g.subset(np.arange(0, nb, 16))
+        sub = g.subset(o_cols)
         t1 = time.perf_counter()
-        O.sweep_hetero(sub.betas, sub.dist, sub.eta, sub.t_end, sub.u, sub.p, sub.kappa, sub.lam, sub.x0,
-                       nthreads=cores)
+        o_h = O.sweep_hetero(sub.betas, sub.dist, sub.eta, sub.t_end, sub.u, sub.p, sub.kappa, sub.lam, sub.x0,
+                             nthreads=cores)
         dt = time.perf_counter() - t1
         pts = sub.betas.shape[0] * nu
-        res["cpu_baseline"] = {"value": pts / dt, "unit": "equilibria/s", "cores": cores, "kind": "port",
-                               "host": host_info(),
-                               "sample": f"{sub.betas.shape[0]} columns (every 16th) x {nu} u = {pts} equilibria "
-                                         f"in {dt:.2f} s"}
+        if not a.no_cpu_baseline and rank == 0 and world == 1:
+            res["cpu_baseline"] = {"value": pts / dt, "unit": "equilibria/s", "cores": cores, "kind": "port",
+                                   "host": host_info(),
+                                   "sample": f"{sub.betas.shape[0]} columns (every 16th) x {nu} u = {pts} equilibria "
+                                             f"in {dt:.2f} s"}
+        last = (out_b if pipe else {k: v[None] for k, v in out.items()})
+        k_last = (a.steps - 1) if pipe else 0
+        idx = torch.as_tensor(o_cols, device=dev)
+        ok = True
+        for f in ("xi", "aw_max", "tol"):
+            gv = last[f][k_last].view(nb, nu)[idx].cpu().numpy()
+            ok &= bool(np.all((gv == o_h[f]) | (np.isnan(gv) & np.isnan(o_h[f]))))
+        stv = last["status"][k_last].view(nb, nu)[idx].cpu().numpy().view(np.uint32)
+        ok &= bool(np.array_equal(stv, o_h["status"]))
+        itv = last["iters"][k_last].view(nb, nu)[idx].cpu().numpy()
+        ok &= bool(np.array_equal(itv, o_h["iters"]))
+        res["verified"] = {"bitwise_equal_oracle": ok, "grid": "last timed step", "columns": int(len(o_cols)),
+                           "points": int(pts)}
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:

@@ -297,6 +297,187 @@ struct SocialRhs {
     static constexpr bool kPinTableau = false;
 };
 
+#ifndef SBR_SOCIAL_RING
+#define SBR_SOCIAL_RING 1 // multi-point waves read AW_{n−1} through a per-lane LDS ring (SocialRhsRing)
+#endif
+constexpr int kRing = 32;                                          // knots per lane: two 16-knot lines
+constexpr size_t kRingLdsBytes = (size_t)2 * kRing * 64 * sizeof(double); // t and v, 64 lanes: 32 KiB
+
+// SocialRhs for a wave that runs many points (the bulk of a sweep: up to 32 per wave).  There
+// every lane streams its own knot lines, so each operand load of a stage lookup is a separate
+// L1 request per active lane: ≈25 load instructions per RK step × 32 lanes, and the L1 cannot
+// hold 4 waves × 32 lanes × the lines in use (PMC of the bulk: 66 % of wave cycles waiting on
+// memory, against 40 % for a lone point, profiles/r04_pmc_social_bulk_vs_lone.txt).  Here each
+// lane keeps AW_{n−1}'s knots [rb, rb + 32) (times and values) in a ring in LDS, layout
+// [slot][lane] (slot = knot mod 32): a lookup's four operands are LDS reads; the ring advances
+// by one 128-byte line (16 knots, eight 16-byte loads per array) when the accepted time's
+// bracket passes rb + 20, and the line after next is touched into L2 then.  The bracket window
+// (Win8) reloads from the ring too.  Knots outside the ring fall back to global loads.  Same
+// brackets, operands and operations as SocialRhs: bit-identical.
+struct SocialRhsRing {
+    double beta;
+    BView to;
+    BView vo;
+    int n;
+    double tfirst, tlast;
+    Win8 w;
+    double aw[5];
+    double last_aw;
+    bool oob;
+    int slow;
+    double* rt; // this lane's ring: rt[s * 64] = t[k] for the knot k ≡ s (mod 32) held
+    double* rv;
+    int rb;     // first knot held (a multiple of 16)
+    double pf_t = 0.0, pf_v = 0.0;
+    __device__ __forceinline__ bool in_ring(int j) const { return j >= rb && j + 1 < rb + kRing; }
+    __device__ __forceinline__ double RT(int j) const { return rt[(j & (kRing - 1)) * 64]; }
+    __device__ __forceinline__ double RV(int j) const { return rv[(j & (kRing - 1)) * 64]; }
+    // knots [base, base + 16) into their slots (base a multiple of 16; nothing past the grid)
+    __device__ __forceinline__ void fill_line(int base)
+    {
+        if (base >= n) return;
+        const double2* lt = (const double2*)((const char*)to.p + ((size_t)(base >> 4) << 13));
+        const double2* lv = (const double2*)((const char*)vo.p + ((size_t)(base >> 4) << 13));
+        double2 a[8], b[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) { a[q] = lt[q]; b[q] = lv[q]; }
+        const int s0 = base & (kRing - 1);
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            rt[(s0 + 2 * q) * 64] = a[q].x; rt[(s0 + 2 * q + 1) * 64] = a[q].y;
+            rv[(s0 + 2 * q) * 64] = b[q].x; rv[(s0 + 2 * q + 1) * 64] = b[q].y;
+        }
+    }
+    // Win8's refill with the ring's copies where it holds them
+    __device__ __forceinline__ void wload(int base)
+    {
+        w.wb = base;
+        const int last = n > 0 ? n - 1 : 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const int i = base + k;
+            const int ic = i < last ? i : last;
+            const double v = (ic >= rb && ic < rb + kRing) ? RT(ic) : to[ic];
+            w.tw[k] = (i < n) ? v : (double)INFINITY;
+        }
+    }
+    __device__ __forceinline__ int find_advance(double x)
+    {
+        const int j = w.find(x);
+        if (j - w.wb >= 4 || j < w.wb) wload(j);
+        return j;
+    }
+    // lerp_sel with the operands from the ring where it holds them
+    __device__ __forceinline__ double lerp_r(int j, double x, bool in) const
+    {
+        j = j > n - 2 ? n - 2 : j;
+        j = j < 0 ? 0 : j;
+        double t0, t1, v0, v1;
+        if (in_ring(j)) { t0 = RT(j); t1 = RT(j + 1); v0 = RV(j); v1 = RV(j + 1); }
+        else { t0 = to[j]; t1 = to[j + 1]; v0 = vo[j]; v1 = vo[j + 1]; }
+        const double d = (x - t0) / (t1 - t0);
+        const double r = v0 * (1.0 - d) + v1 * d;
+        return in ? r : (double)NAN;
+    }
+    __device__ __forceinline__ void init(double b, BView t_, BView v_, int n_, double* ring)
+    {
+        slow = 0;
+        beta = b; to = t_; vo = v_; n = n_;
+        tfirst = n > 0 ? to[0] : 0.0;
+        tlast = n > 0 ? to[n - 1] : 0.0;
+        oob = false;
+        last_aw = 0.0;
+        const int lane = (int)(threadIdx.x & 63);
+        rt = ring + lane;
+        rv = ring + kRing * 64 + lane;
+        rb = 0;
+        fill_line(0);
+        fill_line(16);
+        w.t = to;
+        w.n = n;
+        wload(0);
+    }
+    __device__ __forceinline__ double lookup(double x)
+    {
+        if (n < 2 || !(x >= tfirst && x <= tlast)) { oob = true; return (double)NAN; }
+        return lerp_r(w.find(x), x, true);
+    }
+    __device__ __forceinline__ double eval(double t, double x)
+    {
+        const double a = lookup(t);
+        last_aw = a;
+        return ((1.0 - x) * beta) * a;
+    }
+    __device__ __forceinline__ void prepare(double t, double dt)
+    {
+        const double xs[5] = {fma(C1, dt, t), fma(C2, dt, t), fma(C3, dt, t), fma(C4, dt, t), t + dt};
+        int js[5];
+        bool in[5];
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            in[k] = n >= 2 && xs[k] >= tfirst && xs[k] <= tlast;
+            slow += (in[k] && !(xs[k] < w.tw[7])) ? 1 : 0;
+            js[k] = w.find(in[k] ? xs[k] : tfirst);
+        }
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            aw[k] = lerp_r(js[k], xs[k], in[k]);
+            oob |= !in[k];
+        }
+        last_aw = aw[4];
+    }
+    __device__ __forceinline__ double stage(int s, double, double x) const
+    {
+        return ((1.0 - x) * beta) * aw[s < 5 ? s - 1 : 4];
+    }
+    __device__ __forceinline__ void jac(double t, double x, double& J, double& dT)
+    {
+        if (n < 2 || !(t >= tfirst && t <= tlast)) {
+            oob = true;
+            J = (double)NAN;
+            dT = (double)NAN;
+            return;
+        }
+        int j = w.find(t);
+        j = j > n - 2 ? n - 2 : (j < 0 ? 0 : j);
+        double t0, t1, v0, v1;
+        if (in_ring(j)) { t0 = RT(j); t1 = RT(j + 1); v0 = RV(j); v1 = RV(j + 1); }
+        else { t0 = to[j]; t1 = to[j + 1]; v0 = vo[j]; v1 = vo[j + 1]; }
+        const double d = (t - t0) / (t1 - t0);
+        const double a = v0 * (1.0 - d) + v1 * d;
+        const double rr = 1.0 / (t1 - t0);
+        const double ap = v0 * (-rr) + v1 * rr;
+        J = ((-1.0) * beta) * a;
+        dT = ((1.0 - x) * beta) * ap;
+    }
+    __device__ __forceinline__ void accepted(double t)
+    {
+        if (n >= 2 && t >= tfirst && t <= tlast) {
+            const int j = find_advance(t);
+            if (j - rb >= 20) {
+                if (j - rb >= 20 + 16) { // a step past the whole ring: re-seat it around j
+                    rb = ((j - 4) >> 4) << 4;
+                    fill_line(rb);
+                    fill_line(rb + 16);
+                } else {
+                    // the oldest line is behind the window (wb > j − 4 >= rb + 16): replace it by
+                    // the line after the ring
+                    fill_line(rb + kRing);
+                    rb += 16;
+                }
+                // touch the line after the ring into L2 (consumed one line later by the `slow`
+                // diagnostic, so that its wait falls where it has arrived)
+                slow += (pf_t == -1.0 || pf_v == -2.0) ? 1 : 0;
+                const int q = rb + kRing + 16 < n ? rb + kRing + 16 : n - 1;
+                pf_t = to[q];
+                pf_v = vo[q];
+            }
+        }
+    }
+    static constexpr bool kFsalExact = false;
+    static constexpr bool kPinTableau = false;
+};
+
 #ifndef SBR_SOCIAL_COOP
 #define SBR_SOCIAL_COOP 1 // a wave left with one live point runs it on all 64 lanes (SocialRhsCoop)
 #endif
@@ -498,7 +679,7 @@ __global__ __launch_bounds__(64) void social_init_kernel(SocialArgs a)
 // same values and stores them to the same places, and the few non-idempotent steps (the pool
 // promotion, the live counter) are taken by lane 0 alone.
 template <bool COOP>
-__device__ __forceinline__ bool social_iterate(const SocialArgs& a, int l, int iter)
+__device__ __forceinline__ bool social_iterate(const SocialArgs& a, int l, int iter, double* ring)
 {
     const int64_t g = a.pts ? a.pts[l] : a.pt0 + l;
     const int b = (int)(g / a.n_u);
@@ -533,8 +714,10 @@ __device__ __forceinline__ bool social_iterate(const SocialArgs& a, int l, int i
 
     stamp(0);
     // ---- (a) learning from withdrawals on (0, η) ----
-    typename std::conditional<COOP, SocialRhsCoop, SocialRhs>::type f;
-    f.init(BETA, TO, VO, n_old);
+    typename std::conditional<COOP, SocialRhsCoop,
+                              typename std::conditional<SBR_SOCIAL_RING != 0, SocialRhsRing, SocialRhs>::type>::type f;
+    if constexpr (!COOP && SBR_SOCIAL_RING != 0) f.init(BETA, TO, VO, n_old, ring);
+    else { (void)ring; f.init(BETA, TO, VO, n_old); }
     int n = 0;
     bool overflow = false;
     // knots (t, G) and AW_{n−1} at each knot: the t + dt stage lookup unless the step
@@ -890,6 +1073,7 @@ __global__ __launch_bounds__(64) void social_iter_kernel(const SocialArgs* __res
                                                          int n_inner, const int32_t* __restrict__ work,
                                                          const int32_t* __restrict__ count, int nbs)
 {
+    extern __shared__ double s_ring[]; // kRingLdsBytes: SocialRhsRing's per-lane rings
     const SocialArgs& sa = args[0];
     const SocialArgs& pa = args[1];
     const bool in_pool = (int)blockIdx.x >= nbs;
@@ -905,7 +1089,7 @@ __global__ __launch_bounds__(64) void social_iter_kernel(const SocialArgs* __res
             l = work[w];
             if (!sa.live[l]) return;
             for (int k = 0; k < n_inner; k++)
-                if (!social_iterate<true>(sa, l, iter_arg + k)) break;
+                if (!social_iterate<true>(sa, l, iter_arg + k, s_ring)) break;
             return;
         }
 #endif
@@ -925,7 +1109,7 @@ __global__ __launch_bounds__(64) void social_iter_kernel(const SocialArgs* __res
         if (!pa.live[l]) return;
         iter = pa.it_cur[l];
         for (int k = 0; k < n_inner; k++)
-            if (!social_iterate<true>(pa, l, iter + k)) break;
+            if (!social_iterate<true>(pa, l, iter + k, s_ring)) break;
         return;
 #else
         l = ((int)blockIdx.x - nbs) * 64 + threadIdx.x;
@@ -937,7 +1121,7 @@ __global__ __launch_bounds__(64) void social_iter_kernel(const SocialArgs* __res
     }
     const SocialArgs& a = args[in_pool ? 1 : 0];
     for (int k = 0; k < n_inner; k++)
-        if (!social_iterate<false>(a, l, iter + k)) break;
+        if (!social_iterate<false>(a, l, iter + k, s_ring)) break;
 }
 
 // ============================================================================
@@ -999,8 +1183,8 @@ hipError_t launch_social_iter(const SocialArgs& a, const SocialArgs& p, const So
     nbs = nbs > SBR_SOCIAL_WAVES ? nbs : SBR_SOCIAL_WAVES;
     nbs = nbs < a.n_pts ? nbs : (a.n_pts > 0 ? a.n_pts : 1);
     const int pool_waves = SBR_SOCIAL_COOP ? p.n_pts : (p.n_pts + 63) / 64;
-    hipLaunchKernelGGL(social_iter_kernel, dim3(nbs + pool_waves), dim3(64), 0, s, args_dev, iter, n_inner,
-                       work, count, nbs);
+    hipLaunchKernelGGL(social_iter_kernel, dim3(nbs + pool_waves), dim3(64), SBR_SOCIAL_RING ? kRingLdsBytes : 0, s,
+                       args_dev, iter, n_inner, work, count, nbs);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(social_compact_kernel, dim3(1), dim3(CMP_BLOCK), 0, s, work, count, a.live, work_out,

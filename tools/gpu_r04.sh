@@ -53,8 +53,10 @@ for s in ${STEPS:-tests smoke bench single}; do
                 soclone) BA="--workload social --steps 1 --warmup 0 --social-cols 2 --social-max-iter 16" ;;
               esac
               PMC_OUT=$OUT/pmc_$w BENCH_ARGS="$BA" bash tools/pmc.sh > "$OUT/pmc_$w.out" 2>&1; rc=$?
-              echo "pmc_$w rc=$rc" | tee -a "$OUT/steps.log"; [ $rc -ne 0 ] && exit $rc
+              echo "pmc_$w rc=$rc" | tee -a "$OUT/steps.log"; if [ $rc -ne 0 ]; then exit $rc; fi
             done ;;
+    socprof) run socprof 300 python -u bench.py --workload social --steps 1 --warmup 0 --social-max-iter 16 --social-prof --no-cpu-baseline --no-verify ;;
+    socprofvars) for v in ${VARS:-}; do run socprof_$v 300 env SBR_LIB=replication-social-bank-runs_amd/lib_var/$v/libsbr.so python -u bench.py --workload social --steps 1 --warmup 0 --social-max-iter 16 --social-prof --no-cpu-baseline --no-verify; done ;;
     config2) run config2 300 python -u bench.py --workload config2 --steps 20 --warmup 2 ;;
     dropin) run dropin 600 python -u bench.py --workload dropin --steps 30 ;;
     knotsprobe) run knotsprobe 300 python -u tools/knots_probe.py 2000 && run knotsprof 300 rocprofv3 --kernel-trace --stats -d "$OUT/knotsprof" -o run --output-format csv -- python3 tools/knots_probe.py 500 ;;
