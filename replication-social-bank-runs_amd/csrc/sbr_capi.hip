@@ -36,6 +36,9 @@
 #ifndef SBR_LEARN_SLOTS
 #define SBR_LEARN_SLOTS 4 // learning workspaces of the pipelined batch
 #endif
+#ifndef SBR_LEARN_GROUP
+#define SBR_LEARN_GROUP 2 // grids per learning launch of the pipelined batch
+#endif
 #ifndef SBR_LEARN_STREAMS
 #define SBR_LEARN_STREAMS 3 // learning streams (with the context stream: within GPU_MAX_HW_QUEUES = 4)
 #endif
@@ -61,6 +64,7 @@ struct sbr_ctx {
     size_t ws_beta[kLearnSlots] = {}, ws_cap[kLearnSlots] = {};
     sbr::LearnBufs LW[kLearnSlots]{};
     int last_slot = 0;
+    int64_t last_off = 0; // column offset of the last grid inside its (grouped) learning slot
     hipStream_t lstream[kLearnStreams] = {};
     hipEvent_t ev_in = nullptr, ev_learned[kLearnSlots] = {}, ev_eq[kLearnSlots] = {};
     // fork/join fences between HIP's null stream and `stream`, and the end of the last call
@@ -631,6 +635,7 @@ int run_baseline(sbr_ctx* c, hipStream_t s, const double* beta, const double* et
     int rc = ensure_learn(c, (size_t)n_beta, (size_t)o.knot_capacity);
     if (rc) return rc;
     c->last_slot = 0;
+    c->last_off = 0;
     sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, p, lambda, o.ode_maxiters, (int32_t)n_beta, 1, 0};
     // per-column readiness on request (SBR_FLAG_READY_SWEEP): see above
     c->rs_used = !aw_path && n_beta >= 64 && (o.flags & SBR_FLAG_READY_SWEEP) &&
@@ -707,6 +712,7 @@ int run_interest(sbr_ctx* c, hipStream_t s, const double* beta, const double* et
     int rc = ensure_learn(c, (size_t)n_beta, (size_t)o.knot_capacity);
     if (rc) return rc;
     c->last_slot = 0;
+    c->last_off = 0;
     sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, p, lambda, o.ode_maxiters, (int32_t)n_beta, 1, 0};
     hipEvent_t t0 = tstart(c, s);
     HIP_TRY(c, sbr::launch_learn_logistic(beta, eta, t_end, la, c->LW[0], s), SBR_EDEVICE);
@@ -939,8 +945,14 @@ int sbr_sweep_baseline_batch_dev(sbr_ctx* c, void* stream, int64_t n_batch, cons
     if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
     sbr_opts o = resolve(opts);
     const int nslot = sbr_ctx::kLearnSlots;
-    for (int k = 0; k < nslot && k < n_batch; k++) {
-        int rc = ensure_learn(c, (size_t)n_beta, (size_t)o.knot_capacity, k, SBR_FUSE_HAZARD != 0);
+    // SBR_LEARN_GROUP grids share one learning launch (their β columns are adjacent in `beta`):
+    // the learning stage is latency-bound on its slowest column, so a launch over twice the
+    // columns takes about as long as one over a single grid, and the three learning streams
+    // keep twice as many grids in flight
+    const int64_t GR = SBR_LEARN_GROUP;
+    const int64_t n_group = (n_batch + GR - 1) / GR;
+    for (int k = 0; k < nslot && k < n_group; k++) {
+        int rc = ensure_learn(c, (size_t)(n_beta * GR), (size_t)o.knot_capacity, k, SBR_FUSE_HAZARD != 0);
         if (rc) return rc;
     }
     {
@@ -960,40 +972,51 @@ int sbr_sweep_baseline_batch_dev(sbr_ctx* c, void* stream, int64_t n_batch, cons
         // inputs are ready once prior work on the caller's stream is
         HIP_TRY(c, hipEventRecord(c->ev_in, s), SBR_EDEVICE);
         for (int k = 0; k < sbr_ctx::kLearnStreams; k++) HIP_TRY(c, hipStreamWaitEvent(c->lstream[k], c->ev_in, 0), SBR_EDEVICE);
-        for (int64_t k = 0; k < n_batch; k++) {
-            const int slot = (int)(k % nslot);
+        for (int64_t m = 0; m < n_group; m++) {
+            const int slot = (int)(m % nslot);
+            const int64_t g0 = m * GR, gn = (n_batch - g0) < GR ? (n_batch - g0) : GR;
             hipStream_t es = s; // one equilibrium stream (two alternating: 15% slower, r01_ab27)
 #ifdef SBR_AB_PIPE_SERIAL // A/B only: learning on the equilibrium stream (no overlap)
             hipStream_t ls = s;
 #else
-            hipStream_t ls = c->lstream[k % sbr_ctx::kLearnStreams];
+            hipStream_t ls = c->lstream[m % sbr_ctx::kLearnStreams];
 #endif
-            const double* bk = beta + k * n_beta;
-            const double* ek = eta + k * n_beta;
-            const double* tk = t_end + k * n_beta;
-            // the slot's previous reader (equilibrium of batch k - nslot) must be done
-            if (k >= nslot) HIP_TRY(c, hipStreamWaitEvent(ls, c->ev_eq[slot], 0), SBR_EDEVICE);
+            // the slot's previous readers (equilibria of group m - nslot) must be done
+            if (m >= nslot) HIP_TRY(c, hipStreamWaitEvent(ls, c->ev_eq[slot], 0), SBR_EDEVICE);
             hipEvent_t t0 = tstart(c, ls);
-            // the first grid's learning is the pipeline fill (nothing to overlap it with): the
-            // two-kernel hazard is shorter there; later grids stream it (off the critical path)
+            // the first group's learning is the pipeline fill (nothing to overlap it with): the
+            // two-kernel hazard is shorter there; later groups stream it (off the critical path)
             sbr::LearnArgs lk = la;
-            if (k == 0) lk.fuse_hazard = 0;
-            HIP_TRY(c, sbr::launch_learn_logistic(bk, ek, tk, lk, c->LW[slot], ls), SBR_EDEVICE);
+            lk.n_beta = (int32_t)(gn * n_beta);
+            if (m == 0) lk.fuse_hazard = 0;
+            HIP_TRY(c, sbr::launch_learn_logistic(beta + g0 * n_beta, eta + g0 * n_beta, t_end + g0 * n_beta, lk,
+                                                  c->LW[slot], ls), SBR_EDEVICE);
             tend(c, ls, 0, t0);
             HIP_TRY(c, hipEventRecord(c->ev_learned[slot], ls), SBR_EDEVICE);
             HIP_TRY(c, hipStreamWaitEvent(es, c->ev_learned[slot], 0), SBR_EDEVICE);
-            sbr::ResultSoA r{out->xi ? out->xi + k * np : nullptr,
-                             out->tau_in_unc ? out->tau_in_unc + k * np : nullptr,
-                             out->tau_out_unc ? out->tau_out_unc + k * np : nullptr,
-                             out->aw_max ? out->aw_max + k * np : nullptr,
-                             out->tol ? out->tol + k * np : nullptr,
-                             out->status ? out->status + k * np : nullptr,
-                             out->iters ? out->iters + k * np : nullptr};
-            int rc = launch_eq(c, es, c->LW[slot], ek, tk, u, n_beta, n_u, kappa, o, r, nullptr);
-            if (rc) return rc;
+            for (int64_t i = 0; i < gn; i++) {
+                const int64_t k = g0 + i;
+                const sbr::LearnBufs& W = c->LW[slot];
+                const size_t co = (size_t)(i * n_beta), cc = co * (size_t)W.cap;
+                const sbr::LearnBufs Lk{W.t + cc, W.G + cc, W.hr + cc, W.hrI ? W.hrI + cc : nullptr, W.n_knots + co,
+                                        W.n_tau + co, W.n_le + co, W.status + co, W.n_accept + co, W.n_reject + co,
+                                        W.cap};
+                const double* ek = eta + k * n_beta;
+                const double* tk = t_end + k * n_beta;
+                sbr::ResultSoA r{out->xi ? out->xi + k * np : nullptr,
+                                 out->tau_in_unc ? out->tau_in_unc + k * np : nullptr,
+                                 out->tau_out_unc ? out->tau_out_unc + k * np : nullptr,
+                                 out->aw_max ? out->aw_max + k * np : nullptr,
+                                 out->tol ? out->tol + k * np : nullptr,
+                                 out->status ? out->status + k * np : nullptr,
+                                 out->iters ? out->iters + k * np : nullptr};
+                int rc = launch_eq(c, es, Lk, ek, tk, u, n_beta, n_u, kappa, o, r, nullptr);
+                if (rc) return rc;
+                HIP_TRY(c, hipEventRecord(c->ev_grid[k], es), SBR_EDEVICE);
+                c->n_grid = k + 1;
+                c->last_off = (int64_t)co;
+            }
             HIP_TRY(c, hipEventRecord(c->ev_eq[slot], es), SBR_EDEVICE);
-            HIP_TRY(c, hipEventRecord(c->ev_grid[k], es), SBR_EDEVICE);
-            c->n_grid = k + 1;
             c->last_slot = slot;
         }
         return SBR_OK;
@@ -1725,12 +1748,13 @@ int sbr_learn_stats(sbr_ctx* c, int64_t n_beta, int32_t* n_knots, int32_t* n_tau
                     int32_t* n_reject, uint32_t* status)
 {
     SBR_PER_DEVICE_DIAG(c);
-    if (!c || n_beta <= 0 || (size_t)n_beta > c->ws_beta[c->last_slot]) return SBR_EARG;
+    if (!c || n_beta <= 0 || (size_t)(n_beta + c->last_off) > c->ws_beta[c->last_slot]) return SBR_EARG;
     if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
     HIP_TRY(c, hipDeviceSynchronize(), SBR_EDEVICE);
     const sbr::LearnBufs& L = c->LW[c->last_slot];
-    struct { int32_t* h; void* d; } cp[] = {{n_knots, L.n_knots}, {n_tau, L.n_tau}, {n_accept, L.n_accept},
-                                           {n_reject, L.n_reject}, {(int32_t*)status, L.status}};
+    const int64_t o = c->last_off; // the last grid of a grouped learning slot
+    struct { int32_t* h; void* d; } cp[] = {{n_knots, L.n_knots + o}, {n_tau, L.n_tau + o}, {n_accept, L.n_accept + o},
+                                           {n_reject, L.n_reject + o}, {(int32_t*)status, L.status + o}};
     for (auto& x : cp)
         if (x.h) HIP_TRY(c, hipMemcpy(x.h, x.d, (size_t)n_beta * 4, hipMemcpyDeviceToHost), SBR_EDEVICE);
     return SBR_OK;

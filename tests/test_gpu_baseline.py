@@ -211,6 +211,12 @@ def test_pipelined_batches_equal_single_sweeps(engine):
     etas[1, :7] = 40.0  # η past tspan: the hazard stage's BoundsError (fused into learning in the batch)
     etas[2, 7:9] = 30.0  # η == t_end: the last knot is η itself
     tends = np.stack([np.full(384, 30.0), np.full(384, 30.0), np.full(384, 20.0), np.full(384, 30.0)])
+    # 11 grids: an odd count (the last learning group holds one grid) and more groups than
+    # learning workspaces (each is reused); the extra grids vary β so no two are alike
+    extra = np.arange(7)[:, None]
+    betas = np.concatenate([betas, base.beta[None, :] * (1.0 + 0.05 * (extra + 1))])
+    etas = np.concatenate([etas, np.full((7, 384), 15.0) - extra])
+    tends = np.concatenate([tends, np.full((7, 384), 30.0)])
     nbat, nb, nu = betas.shape[0], betas.shape[1], len(base.u)
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
     out = {f: torch.empty(nbat, nb * nu, dtype=torch.float64, device=dev) for f in FIELDS}
