@@ -915,6 +915,9 @@ struct HCol {
 #ifndef SBR_HET_UBCACHE
 #define SBR_HET_UBCACHE 1 // pass 2 of AW_max re-reads pass 1's range bounds (config-4 step 45.3 -> 43.3 ms)
 #endif
+#ifndef SBR_HET_K1
+#define SBR_HET_K1 1 // AW_OUT bound from the knot after next -> the next knot where consecutive knots are separated
+#endif
 #ifndef SBR_HET_SHARE_DIV
 #define SBR_HET_SHARE_DIV 1 // exact AW evaluations share δ between groups with equal arguments
 #endif
@@ -928,6 +931,7 @@ __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const d
                                                    double& aw_o, double& tol_o, uint32_t& st_o, int& it_o,
                                                    double* tin, double* tout, const bool mono, const int diag,
                                                    double* __restrict__ aw_path, const double env, const bool sep,
+                                                   const int koff,
                                                    double* __restrict__ tin_g, double* __restrict__ tout_g)
 {
     xi_o = NAN; aw_o = NAN; tol_o = INFINITY; it_o = 0;
@@ -1225,10 +1229,10 @@ __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const d
                 const double bv = (C.T[i1] - xi) + occ[k];
                 double hi = 0.0;
                 if (sep && occ[k] == xi) {
-                    // b_k(t_i1) = (t_i1 − ξ) + ξ lies within an ulp of t_i1, below t[i1 + 2] (knots
-                    // 2 apart are farther apart than that, `sep`): G_k at the knot after its
-                    // bracket is G_k at a knot <= i1 + 2, no search
-                    const double g = C.g(i1 + 2 < n - 1 ? i1 + 2 : n - 1, k);
+                    // b_k(t_i1) = (t_i1 − ξ) + ξ lies within an ulp of t_i1, below t[i1 + koff] (knots
+                    // koff apart are farther apart than that, `sep`): G_k at the knot after its
+                    // bracket is G_k at a knot <= i1 + koff, no search
+                    const double g = C.g(i1 + koff < n - 1 ? i1 + koff : n - 1, k);
                     hi = g > 0.0 ? g : 0.0;
                     hb[k] = i1; // with ib = i1 below, the next hint hb + (i − ib) is i itself
                 } else if (bv >= 0) {
@@ -1359,7 +1363,8 @@ void equilibrium_hetero_kernel(HeteroBufs L, const double* __restrict__ dist,
     if ((MODE == 1 && !fits) || (MODE == 2 && fits)) return;
     __shared__ int s_nonmono;
     __shared__ int s_close; // two knots 2 apart closer than 1e-15·t[n−1] (the AW bounds then search)
-    if (threadIdx.x == 0) { s_nonmono = a.exhaustive || a.aw_path; s_close = 0; } // path mode: every knot
+    __shared__ int s_close1; // two consecutive knots that close (the AW bounds then use knot + 2)
+    if (threadIdx.x == 0) { s_nonmono = a.exhaustive || a.aw_path; s_close = 0; s_close1 = 0; } // path mode: every knot
     if (fits)
         for (int i = threadIdx.x; i < n; i += BLOCK) smem[i] = gT[i];
     __syncthreads();
@@ -1389,10 +1394,12 @@ void equilibrium_hetero_kernel(HeteroBufs L, const double* __restrict__ dist,
             }
         if (nan) s_nonmono = 1;
         if (fits) {
-            bool close = false;
+            bool close = false, close1 = false;
             const double sepd = n > 0 ? 1e-15 * smem[n - 1] : 0.0; // n == 0: an ARG_INVALID column
             for (int i = threadIdx.x; i + 2 < n; i += BLOCK) close |= !(smem[i + 2] - smem[i] > sepd);
+            for (int i = threadIdx.x; i + 1 < n; i += BLOCK) close1 |= !(smem[i + 1] - smem[i] > sepd);
             if (close) s_close = 1;
+            if (close1) s_close1 = 1;
         }
 #pragma unroll
         for (int k = 0; k < K; k++)
@@ -1453,12 +1460,14 @@ void equilibrium_hetero_kernel(HeteroBufs L, const double* __restrict__ dist,
         HCol<K, const double*> C{smem, L.G + (size_t)c * cap * K, L.hr + (size_t)c * K * cap, n, L.n_tau[c],
                                  L.n_le[c], cap, eta[c], t_end[c], sums && !a.exhaustive ? hsum : nullptr, nblk};
         solve_hetero_point<K>(C, dl, uj, a.kappa, a.max_iters, a.tolerance, lbits, xi, aw, tol, st, it, tin, tout,
-                              mono, a.diag, a.aw_path, env, fits && s_close == 0, tin_g, tout_g);
+                              mono, a.diag, a.aw_path, env, fits && s_close == 0, (SBR_HET_K1 && s_close1 == 0) ? 1 : 2,
+                              tin_g, tout_g);
     } else {
         HCol<K, const double*> C{gT, L.G + (size_t)c * cap * K, L.hr + (size_t)c * K * cap, n, L.n_tau[c],
                                  L.n_le[c], cap, eta[c], t_end[c], nullptr, 0};
         solve_hetero_point<K>(C, dl, uj, a.kappa, a.max_iters, a.tolerance, lbits, xi, aw, tol, st, it, tin, tout,
-                              mono, a.diag, a.aw_path, env, fits && s_close == 0, tin_g, tout_g);
+                              mono, a.diag, a.aw_path, env, fits && s_close == 0, (SBR_HET_K1 && s_close1 == 0) ? 1 : 2,
+                              tin_g, tout_g);
     }
     out.xi[o] = xi;
     out.aw_max[o] = aw;

@@ -182,6 +182,138 @@ __device__ bool promote(const SocialArgs& a, int l, int64_t g, int iter, BView T
     return true;
 }
 
+
+// ---- one point on all 64 lanes (COOP): the streaming passes over the point's knots, by chunks
+// of 64 consecutive knots (lane L holds knot c0 + L).  The per-knot work is done lane-parallel;
+// only the trapezoid sum is a serial fold, taken in the reference's order (I = I + term_i, i
+// ascending, every term formed exactly as the serial loop forms it), so every value is the
+// serial loop's bit for bit.  One memory round trip per 64 knots instead of one per knot.
+__device__ __forceinline__ double rl_d(double x, int k)
+{
+    const uint64_t u = sbr_dbits(x);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, k);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), k);
+    return sbr_bitsd(((uint64_t)hi << 32) | lo);
+}
+// lane L gets lane L − 1's value, lane 0 gets `first`
+__device__ __forceinline__ double up_d(double x, double first)
+{
+    const double v = __shfl_up(x, 1, 64);
+    return (threadIdx.x & 63) == 0 ? first : v;
+}
+
+// hazard_rate on τ̄ = the knots (solver.jl:153-185) and optimal_buffer's crossing scan
+// (:211-264): the two passes of social_iterate's serial path.  X receives exp(λ t_i) and IA the
+// running integral I_i (scratch buffers of the point).
+__device__ void coop_hazard_scan(BView T, BView Gv, BView AWO, BView X, BView IA, const int n, const double BETA,
+                                 const double lam, const double p, const double U, const double ETA, bool& any,
+                                 bool& all, int& first_above, int& last_above, double& tin_c, double& tout_c)
+{
+    const int L = (int)(threadIdx.x & 63);
+    const double omp = 1.0 - p;
+    // pass A: e_i = exp(λ t_i)·pdf_i, term_i = (0.5·(e_{i−1} + e_i))·(t_i − t_{i−1}), I_i = I_{i−1} + term_i
+    double I = 0.0, ec = 0.0, tc = 0.0;
+    for (int c0 = 0; c0 < n; c0 += 64) {
+        const int i = c0 + L;
+        const bool v = i < n;
+        const int ix = v ? i : n - 1;
+        const double ti = T[ix];
+        const double ex = sbr_exp(lam * ti);
+        if (v) X[i] = ex;
+        const double e = ex * (((1.0 - Gv[ix]) * BETA) * AWO[ix]);
+        const double ep = up_d(e, ec), tp = up_d(ti, tc);
+        const double term = (0.5 * (ep + e)) * (ti - tp);
+        const int m = n - c0 < 64 ? n - c0 : 64;
+        double Ii = 0.0;
+        for (int k = 0; k < m; k++) {
+            if (c0 + k > 0) I = I + rl_d(term, k);
+            Ii = L == k ? I : Ii;
+        }
+        if (v) IA[i] = Ii;
+        ec = rl_d(e, 63);
+        tc = rl_d(ti, 63);
+    }
+    const double Ieta = I;
+    // pass B: HR_i = ((p·X_i)·pdf_i)/((p·I_i) + (1 − p)·I_η) and the crossings with u
+    bool have_in = false;
+    double hc = 0.0;
+    tc = 0.0;
+    for (int c0 = 0; c0 < n; c0 += 64) {
+        const int i = c0 + L;
+        const bool v = i < n;
+        const int ix = v ? i : n - 1;
+        const double ti = T[ix];
+        const double pdf = ((1.0 - Gv[ix]) * BETA) * AWO[ix];
+        const double hr = ((p * X[ix]) * pdf) / ((p * IA[ix]) + (omp * Ieta));
+        const double hp = up_d(hr, hc), tp = up_d(ti, tc);
+        const bool ab = v && hr > U, abp = hp > U;
+        const uint64_t mv = __ballot(v), mab = __ballot(ab);
+        const uint64_t mrise = __ballot(v && i >= 1 && !abp && ab), mfall = __ballot(v && i >= 1 && abp && !ab);
+        any |= mab != 0;
+        all &= mab == mv;
+        if (mab) {
+            if (first_above < 0) first_above = c0 + __builtin_ctzll(mab);
+            last_above = c0 + 63 - __builtin_clzll(mab);
+        }
+        const double cross = tp + ((U - hp) * (ti - tp)) / (hr - hp);
+        if (!have_in && mrise) {
+            tin_c = rl_d(cross, __builtin_ctzll(mrise));
+            have_in = true;
+        }
+        if (mfall) tout_c = rl_d(cross, 63 - __builtin_clzll(mfall));
+        hc = rl_d(hr, 63);
+        tc = rl_d(ti, 63);
+    }
+}
+
+// searchsortedlast(T, x) for T[0] <= x from a per-lane hint (either side of the answer)
+__device__ __forceinline__ int coop_ssl(BView T, int n, int hint, double x) { return ssl_near(T, n, hint, x); }
+
+// the damping AW_n(t_i) = ½ AW_{n−1}(t_i) + ½ AW*(t_i) on G_n's knots (social_learning_solver.jl
+// :174-178, :218-222) with AW* = get_AW(ξ, …) evaluated as aw_at does — lane-parallel: lane L
+// evaluates AW* at knot c0 + L (its own bracket searches, hinted by its previous chunk) and
+// damps knot c0 + L − 1, whose interpolation weights need AW* at both knots.
+__device__ void coop_damping(BView T, BView Gv, BView AWO, const int n, const double XI, const double ic,
+                             const double oc, const double G0, bool& aoob)
+{
+    const int L = (int)(threadIdx.x & 63);
+    const double tfirst = T[0], tlast = T[n - 1];
+    int ha = 0, hb = 0;
+    double awc = 0.0;
+    bool bad = false;
+    for (int c0 = 0; c0 < n; c0 += 64) {
+        const int i = c0 + L;
+        const bool v = i < n;
+        const int ix = v ? i : n - 1;
+        const double tau = T[ix];
+        const double xa = (tau - XI) + ic, xb = (tau - XI) + oc;
+        const double xa0 = xa > 0 ? xa : 0.0, xb0 = xb > 0 ? xb : 0.0;
+        const bool ina = n >= 2 && xa0 >= tfirst && xa0 <= tlast;
+        const bool inb = n >= 2 && xb0 >= tfirst && xb0 <= tlast;
+        bad |= v && !(ina && inb);
+        ha = ina ? coop_ssl(T, n, ha, xa0) : ha;
+        hb = inb ? coop_ssl(T, n, hb, xb0) : hb;
+        const double gi = lerp_sel(T, Gv, n, ina ? ha : 0, xa0, ina);
+        const double go = lerp_sel(T, Gv, n, inb ? hb : 0, xb0, inb);
+        const double awin = xa >= 0 ? gi : 0.0;
+        const double awout = xb >= 0 ? go : 0.0;
+        const double aw = (awout - awin) + G0;
+        const double awm = up_d(aw, awc);
+        if (v && i >= 1) {
+            const double vn = awm * (1.0 - 0.0) + aw * 0.0;
+            AWO[i - 1] = 0.5 * AWO[i - 1] + 0.5 * vn;
+        }
+        if (v && i == n - 1) {
+            const double vl = awm * (1.0 - 1.0) + aw * 1.0;
+            AWO[n - 1] = 0.5 * AWO[n - 1] + 0.5 * vl;
+        }
+        awc = rl_d(aw, 63);
+        ha += 64;
+        hb += 64;
+    }
+    aoob |= __ballot(bad) != 0;
+}
+
 #ifndef SBR_SOCIAL_PF
 #define SBR_SOCIAL_PF 32 // knots ahead of the step that `accepted` touches (A/B)
 #endif
@@ -297,6 +429,11 @@ struct SocialRhs {
     static constexpr bool kPinTableau = false;
 };
 
+#ifndef SBR_SOCIAL_UNROLL
+// the hazard and damping passes stream a point's knots; unrolled, a lane has the loads of
+// several knots in flight instead of one memory round trip per knot (A/B: 1)
+#define SBR_SOCIAL_UNROLL 8
+#endif
 #ifndef SBR_SOCIAL_RING
 #define SBR_SOCIAL_RING 1 // multi-point waves read AW_{n−1} through a per-lane LDS ring (SocialRhsRing)
 #endif
@@ -790,51 +927,58 @@ __device__ __forceinline__ bool social_iterate(const SocialArgs& a, int l, int i
         } else {
             BView X = TO; // AW_{n-1} knots are dead now: exp(λτ̄) scratch
             const double lam = a.lam, p = a.p, omp = 1.0 - p;
-            // pass A: ∫ trapezoid to η
-            double I = 0.0;
-            double ex = sbr_exp(lam * T[0]);
-            X[0] = ex;
-            double eprev = ex * (((1.0 - Gv[0]) * BETA) * AWO[0]);
-            for (int i = 1; i < n; i++) {
-                ex = sbr_exp(lam * T[i]);
-                X[i] = ex;
-                const double ei = ex * (((1.0 - Gv[i]) * BETA) * AWO[i]);
-                I = I + (0.5 * (eprev + ei)) * (T[i] - T[i - 1]);
-                eprev = ei;
-            }
-            const double Ieta = I;
-            // pass B: HR and optimal_buffer's crossing scan (solver.jl:211-264), streamed
             bool any = false, all = true;
             int first_above = -1, last_above = -1;
             double tin_c = ETA, tout_c = ETA;
             bool have_in = false;
-            I = 0.0;
-            double pdf = ((1.0 - Gv[0]) * BETA) * AWO[0];
-            eprev = X[0] * pdf;
-            double hr_prev = ((p * X[0]) * pdf) / ((p * I) + (omp * Ieta));
-            double tprev = T[0];
-            {
-                const bool ab = hr_prev > U;
-                any |= ab; all &= ab;
-                if (ab) { first_above = 0; last_above = 0; }
-            }
-            for (int i = 1; i < n; i++) {
-                pdf = ((1.0 - Gv[i]) * BETA) * AWO[i];
-                const double ei = X[i] * pdf;
-                const double ti = T[i];
-                I = I + (0.5 * (eprev + ei)) * (ti - tprev);
-                eprev = ei;
-                const double hr = ((p * X[i]) * pdf) / ((p * I) + (omp * Ieta));
-                const bool ab = hr > U, abp = hr_prev > U;
-                any |= ab; all &= ab;
-                if (ab) { if (first_above < 0) first_above = i; last_above = i; }
-                if (!have_in && !abp && ab) {
-                    tin_c = tprev + ((U - hr_prev) * (ti - tprev)) / (hr - hr_prev);
-                    have_in = true;
+            if constexpr (COOP) {
+                coop_hazard_scan(T, Gv, AWO, X, VO, n, BETA, lam, p, U, ETA, any, all, first_above, last_above, tin_c,
+                                 tout_c);
+            } else {
+                // pass A: ∫ trapezoid to η
+                double I = 0.0;
+                double ex = sbr_exp(lam * T[0]);
+                X[0] = ex;
+                double eprev = ex * (((1.0 - Gv[0]) * BETA) * AWO[0]);
+#pragma unroll SBR_SOCIAL_UNROLL
+                for (int i = 1; i < n; i++) {
+                    ex = sbr_exp(lam * T[i]);
+                    X[i] = ex;
+                    const double ei = ex * (((1.0 - Gv[i]) * BETA) * AWO[i]);
+                    I = I + (0.5 * (eprev + ei)) * (T[i] - T[i - 1]);
+                    eprev = ei;
                 }
-                if (abp && !ab) tout_c = tprev + ((U - hr_prev) * (ti - tprev)) / (hr - hr_prev);
-                hr_prev = hr;
-                tprev = ti;
+                const double Ieta = I;
+                // pass B: HR and optimal_buffer's crossing scan (solver.jl:211-264), streamed
+                I = 0.0;
+                double pdf = ((1.0 - Gv[0]) * BETA) * AWO[0];
+                eprev = X[0] * pdf;
+                double hr_prev = ((p * X[0]) * pdf) / ((p * I) + (omp * Ieta));
+                double tprev = T[0];
+                {
+                    const bool ab = hr_prev > U;
+                    any |= ab; all &= ab;
+                    if (ab) { first_above = 0; last_above = 0; }
+                }
+#pragma unroll SBR_SOCIAL_UNROLL
+                for (int i = 1; i < n; i++) {
+                    pdf = ((1.0 - Gv[i]) * BETA) * AWO[i];
+                    const double ei = X[i] * pdf;
+                    const double ti = T[i];
+                    I = I + (0.5 * (eprev + ei)) * (ti - tprev);
+                    eprev = ei;
+                    const double hr = ((p * X[i]) * pdf) / ((p * I) + (omp * Ieta));
+                    const bool ab = hr > U, abp = hr_prev > U;
+                    any |= ab; all &= ab;
+                    if (ab) { if (first_above < 0) first_above = i; last_above = i; }
+                    if (!have_in && !abp && ab) {
+                        tin_c = tprev + ((U - hr_prev) * (ti - tprev)) / (hr - hr_prev);
+                        have_in = true;
+                    }
+                    if (abp && !ab) tout_c = tprev + ((U - hr_prev) * (ti - tprev)) / (hr - hr_prev);
+                    hr_prev = hr;
+                    tprev = ti;
+                }
             }
             if (!any) { tin = ETA; tout = ETA; }
             else if (all) { tin = T[0]; tout = T[n - 1]; }
@@ -951,18 +1095,23 @@ __device__ __forceinline__ bool social_iterate(const SocialArgs& a, int l, int i
                 } else {
                     // damping α = 1/2 on G_n's knots (:174-178, :218-222): AW* at its own
                     // knot i is aw_i·(1−0) + aw_{i+1}·0 (i < n−1), aw_{n−2}·0 + aw_{n−1}·1
-                    Walker da, db;
-                    da.init(T, Gv, n); db.init(T, Gv, n);
-                    double aw_i = aw_at(T[0], da, db);
-                    for (int i = 0; i < n - 1; i++) {
-                        const double aw_n = aw_at(T[i + 1], da, db);
-                        const double vn = aw_i * (1.0 - 0.0) + aw_n * 0.0;
-                        AWO[i] = 0.5 * AWO[i] + 0.5 * vn;
-                        if (i == n - 2) {
-                            const double vl = aw_i * (1.0 - 1.0) + aw_n * 1.0;
-                            AWO[n - 1] = 0.5 * AWO[n - 1] + 0.5 * vl;
+                    if constexpr (COOP) {
+                        coop_damping(T, Gv, AWO, n, XI, ic, oc, G0, aoob);
+                    } else {
+                        Walker da, db;
+                        da.init(T, Gv, n); db.init(T, Gv, n);
+                        double aw_i = aw_at(T[0], da, db);
+#pragma unroll SBR_SOCIAL_UNROLL
+                        for (int i = 0; i < n - 1; i++) {
+                            const double aw_n = aw_at(T[i + 1], da, db);
+                            const double vn = aw_i * (1.0 - 0.0) + aw_n * 0.0;
+                            AWO[i] = 0.5 * AWO[i] + 0.5 * vn;
+                            if (i == n - 2) {
+                                const double vl = aw_i * (1.0 - 1.0) + aw_n * 1.0;
+                                AWO[n - 1] = 0.5 * AWO[n - 1] + 0.5 * vl;
+                            }
+                            aw_i = aw_n;
                         }
-                        aw_i = aw_n;
                     }
                     if (aoob) { finish = true; stop_oob = true; }
                     else if (iter >= a.max_iter) { finish = true; need_awmax = (st_r & SBR_RUN) != 0; }
