@@ -37,7 +37,7 @@
 #define SBR_LEARN_SLOTS 4 // learning workspaces of the pipelined batch
 #endif
 #ifndef SBR_LEARN_GROUP
-#define SBR_LEARN_GROUP 2 // grids per learning launch of the pipelined batch
+#define SBR_LEARN_GROUP 1 // grids per learning launch of the pipelined batch (A/B: 2 was slower, 1.567 -> 1.631 ms per step: r04_j)
 #endif
 #ifndef SBR_LEARN_STREAMS
 #define SBR_LEARN_STREAMS 3 // learning streams (with the context stream: within GPU_MAX_HW_QUEUES = 4)
@@ -2066,6 +2066,13 @@ constexpr int64_t kPoolSlots = 256;       // promotion pool slots (points that o
 #define SBR_SOCIAL_INNER 16
 #endif
 constexpr int kSocialInner = SBR_SOCIAL_INNER; // fixed-point iterates per launch (compaction in between)
+#ifndef SBR_SOCIAL_BULK
+#define SBR_SOCIAL_BULK 2 // launches of SBR_SOCIAL_INNER iterates before the shorter ones
+#endif
+#ifndef SBR_SOCIAL_INNER2
+#define SBR_SOCIAL_INNER2 8 // iterates per launch after the bulk launches
+#endif
+constexpr int kSocialBulk = SBR_SOCIAL_BULK, kSocialInner2 = SBR_SOCIAL_INNER2;
 
 int social_checks(sbr_ctx* c, const double* beta, const double* eta, const double* u, int64_t n_beta, int64_t n_u,
                   double x0, double p, double kappa, double lambda, const double* cmp, int32_t n_cmp, double tol,
@@ -2174,12 +2181,22 @@ int run_social_pass(sbr_ctx* c, hipStream_t s, const double* beta, const double*
         t0 = tstart(c, s);
         // kSocialInner iterates per launch; a point promoted during a launch redoes that
         // iterate in the same or the next launch: one launch past max_iter drains the pool
-        const int n_launch = (max_iter + kSocialInner - 1) / kSocialInner + (nslots > 0 ? 1 : 0);
+        // The first kSocialBulk launches run kSocialInner iterates each (the bulk: most points
+        // converge around iterate 35); later launches run kSocialInner2, so the survivors are
+        // re-spread over the waves (fewer points per wave, then one: the whole-wave mode) sooner.
+        std::vector<int> inner;
+        for (int done = 0, q = 0; done < max_iter; q++) {
+            const int m = q < kSocialBulk ? kSocialInner : kSocialInner2;
+            inner.push_back(m);
+            done += m;
+        }
+        if (nslots > 0) inner.push_back(kSocialInner2);
+        const int n_launch = (int)inner.size();
         static const bool trace = getenv("SBR_SOCIAL_TRACE") != nullptr;
         const auto tr0 = std::chrono::steady_clock::now();
-        for (int q = 0; q < n_launch; q++) {
-            const int k = q & 1, it = 1 + q * kSocialInner;
-            HIP_TRY(c, sbr::launch_social_iter(a, b, c->so_args_dev, it, kSocialInner, c->so_work[k],
+        for (int q = 0, it = 1; q < n_launch; it += inner[q], q++) {
+            const int k = q & 1;
+            HIP_TRY(c, sbr::launch_social_iter(a, b, c->so_args_dev, it, inner[q], c->so_work[k],
                                                c->so_count + k, c->so_work[k ^ 1], c->so_count + (k ^ 1), s),
                     SBR_EDEVICE);
             if ((poll > 0 || trace) && q + 1 < n_launch) {

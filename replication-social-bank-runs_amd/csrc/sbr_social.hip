@@ -432,7 +432,7 @@ struct SocialRhs {
 #ifndef SBR_SOCIAL_UNROLL
 // the hazard and damping passes stream a point's knots; unrolled, a lane has the loads of
 // several knots in flight instead of one memory round trip per knot (A/B: 1)
-#define SBR_SOCIAL_UNROLL 8
+#define SBR_SOCIAL_UNROLL 1 // A/B: 8 was 2.7 % slower on the bulk (r04_j)
 #endif
 #ifndef SBR_SOCIAL_RING
 #define SBR_SOCIAL_RING 1 // multi-point waves read AW_{n−1} through a per-lane LDS ring (SocialRhsRing)

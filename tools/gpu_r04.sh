@@ -57,6 +57,7 @@ for s in ${STEPS:-tests smoke bench single}; do
             done ;;
     socprof) run socprof 300 python -u bench.py --workload social --steps 1 --warmup 0 --social-max-iter 16 --social-prof --no-cpu-baseline --no-verify ;;
     benchvars) for v in ${VARS:-}; do run bench_$v 300 env SBR_LIB=replication-social-bank-runs_amd/lib_var/$v/libsbr.so python -u bench.py --no-cpu-baseline; done ;;
+    socialvars) for v in ${VARS:-}; do run social_$v 600 env SBR_LIB=replication-social-bank-runs_amd/lib_var/$v/libsbr.so python -u bench.py --workload social --steps 1 --warmup 0 --no-cpu-baseline --no-verify; done ;;
     socprofvars) for v in ${VARS:-}; do run socprof_$v 300 env SBR_LIB=replication-social-bank-runs_amd/lib_var/$v/libsbr.so python -u bench.py --workload social --steps 1 --warmup 0 --social-max-iter 16 --social-prof --no-cpu-baseline --no-verify; done ;;
     config2) run config2 300 python -u bench.py --workload config2 --steps 20 --warmup 2 ;;
     dropin) run dropin 600 python -u bench.py --workload dropin --steps 30 ;;
