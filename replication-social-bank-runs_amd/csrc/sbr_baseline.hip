@@ -537,6 +537,14 @@ struct Summ {
     // aw_scan's knot offset for AW_OUT(b_j) <= G[j + koff]: 1 when consecutive knots are more than
     // 1e-15·t[n−1] apart (b_j then lies below t[j + 1]: bracket <= j), else 2 (knots 2 apart)
     int koff;
+    // prefix / suffix extremes of the HR block summaries (SBR_SCAN_BS): hpm = prefix max of hmax,
+    // hpn = prefix min of hmin, hsm = suffix max of hmax, hsn = suffix min of hmin, over nbh
+    // blocks; null: the linear block scans
+    const double* hpm;
+    const double* hpn;
+    const double* hsm;
+    const double* hsn;
+    int nbh;
 };
 
 template <class P>
@@ -577,6 +585,9 @@ __device__ __forceinline__ int first_ge_down(F key, int hi, double x)
 // (+ the 1e-14 rounding margin) do not already put it at or below the running maximum; runs
 // of knots the bounds dismiss are skipped with one search in G (right) or in G and τ̄ (left).
 // The maximum equals the exhaustive one bit for bit (G has no NaN here).
+#ifndef SBR_SCAN_BS
+#define SBR_SCAN_BS 1 // crossing scans by binary search over prefix / suffix block tables
+#endif
 #ifndef SBR_AW_K1
 #define SBR_AW_K1 1 // aw_scan bounds AW_OUT(b_j) by G[j + 1] where consecutive knots are separated
 #endif
@@ -702,7 +713,9 @@ __device__ __forceinline__ void solve_point(P T, P G, P H, const Summ& S, const 
     // ---------------- optimal_buffer: crossings of HR(τ̄) with u ----------------
     bool any, all;
     int fa, la, cin, cout;
-    if (S.hmax) {
+    if (S.hpm) {
+        buffer_scan_bs(H, S, S.hpm, S.hpn, S.hsm, S.hsn, S.nbh, ntau, u, any, all, fa, la, cin, cout);
+    } else if (S.hmax) {
         buffer_scan_blocked(H, S, ntau, u, any, all, fa, la, cin, cout);
     } else {
         any = false; all = true;
@@ -1280,6 +1293,11 @@ __device__ __forceinline__ void eq_column(const int b, const int j0, const int j
     double* hmin = hmax + nsum;
     double* pmc = hmin + nsum;
     double* smc = pmc + nsum8;
+    double* hpm = smc + nsum8; // SBR_SCAN_BS tables (launch_equilibrium sizes the slab for them)
+    double* hpn = hpm + nsum;
+    double* hsm = hpn + nsum;
+    double* hsn = hsm + nsum;
+    const int nbh_s = (ntau + 63) >> 6;
     __shared__ int eq_next;
     __shared__ int s_nonmono;
     __shared__ int s_noscan;
@@ -1296,7 +1314,8 @@ __device__ __forceinline__ void eq_column(const int b, const int j0, const int j
             for (int i = threadIdx.x; i < ntau; i += BLOCK) sH[i] = gH[i];
     }
     __syncthreads();
-    Summ S{nullptr, nullptr, nullptr, nullptr, false, (double)NAN, false, 0.0, false, 2};
+    Summ S{nullptr, nullptr, nullptr, nullptr, false, (double)NAN, false, 0.0, false, 2, nullptr, nullptr, nullptr,
+           nullptr, 0};
     if (fits && !a.exhaustive) {
         const int nbh = (ntau + 63) >> 6, nbg = (n + 7) >> 3;
         // HR summaries: 8 lanes per 64-entry block, 8 independent loads each (HR is read from
@@ -1389,11 +1408,34 @@ __device__ __forceinline__ void eq_column(const int b, const int j0, const int j
                 smc[g] = (a0 != a0 || b0 != b0) ? NAN : (a0 < b0 ? a0 : b0);
             }
         }
+#if SBR_SCAN_BS
+        // the crossing scans' prefix / suffix tables over the HR blocks (hmax has no NaN, hmin has
+        // NaN as −∞): one lane each way
+        if (threadIdx.x == (BLOCK > 128 ? 128 : 2)) {
+            double a0 = -INFINITY, b0 = INFINITY;
+            for (int g = 0; g < nbh; g++) {
+                a0 = hmax[g] > a0 ? hmax[g] : a0;
+                b0 = hmin[g] < b0 ? hmin[g] : b0;
+                hpm[g] = a0;
+                hpn[g] = b0;
+            }
+        }
+        if (threadIdx.x == (BLOCK > 192 ? 192 : 3)) {
+            double a0 = -INFINITY, b0 = INFINITY;
+            for (int g = nbh - 1; g >= 0; g--) {
+                a0 = hmax[g] > a0 ? hmax[g] : a0;
+                b0 = hmin[g] < b0 ? hmin[g] : b0;
+                hsm[g] = a0;
+                hsn[g] = b0;
+            }
+        }
+#endif
         __syncthreads();
         const double dd = (double)s_ndec * sbr_bitsd(s_maxdec); // ≥ the largest drawdown
         S = Summ{hmax, hmin, pmc, smc, s_nonmono == 0, s_thalf,
                  n >= 2 && !s_noscan && dd <= 1e-12 && sG[0] >= 0.0 && sG[n - 1] <= 2.0, dd,
-                 s_nonmono == 0 || s_noscan != 0, (SBR_AW_K1 && s_near1 == 0) ? 1 : 2};
+                 s_nonmono == 0 || s_noscan != 0, (SBR_AW_K1 && s_near1 == 0) ? 1 : 2,
+                 SBR_SCAN_BS ? hpm : nullptr, hpn, hsm, hsn, nbh_s};
     }
     // Points are handed out to waves 64 at a time from an LDS counter, so a
     // wave that drew cheap no-run points goes back for more instead of idling
@@ -1889,7 +1931,7 @@ hipError_t launch_hazard(const double* beta, const double* eta, const LearnArgs&
 hipError_t launch_equilibrium(const LearnBufs& L, const double* eta, const double* t_end, const double* u,
                               const EqArgs& a, const ResultSoA& out, int n_beta, hipStream_t s, int only_mode)
 {
-    const size_t lds = ((size_t)2 * a.lds_cap + 2 * ((a.lds_cap >> 6) + 1) + 2 * ((a.lds_cap >> 3) + 1)) * sizeof(double);
+    const size_t lds = ((size_t)2 * a.lds_cap + 6 * ((a.lds_cap >> 6) + 1) + 2 * ((a.lds_cap >> 3) + 1)) * sizeof(double);
     // one block per (β column, tile of EQ_TILE u values); block size by tile width.  Wide
     // tiles use 12-wave blocks: two per CU (LDS holds two columns' t and G) = 6 waves/SIMD.
     const int tiles = (a.n_u + EQ_TILE - 1) / EQ_TILE;
@@ -1915,7 +1957,7 @@ hipError_t launch_eq_ready(const LearnBufs& L, const double* beta, const double*
                            const double* u, const LearnArgs& la, const EqArgs& a, const ReadyArgs& ra,
                            const ResultSoA& out, int n_blocks, hipStream_t s)
 {
-    size_t lds = ((size_t)2 * a.lds_cap + 2 * ((a.lds_cap >> 6) + 1) + 2 * ((a.lds_cap >> 3) + 1)) * sizeof(double);
+    size_t lds = ((size_t)2 * a.lds_cap + 6 * ((a.lds_cap >> 6) + 1) + 2 * ((a.lds_cap >> 3) + 1)) * sizeof(double);
     const size_t hz = (size_t)(3 * HZ_LDS + 3) * sizeof(double); // hazard scratch shares the slab
     if (lds < hz) lds = hz;
     (void)n_blocks; // one workgroup per item
@@ -1945,7 +1987,7 @@ hipError_t launch_ready_fail(const int32_t* gave_up, const ResultSoA& out, int64
 hipError_t launch_interest(const LearnBufs& L, const double* eta, const double* t_end, const double* u,
                            const EqArgs& a, const InterestArgs& ia, const ResultSoA& out, int n_beta, hipStream_t s)
 {
-    const size_t lds = ((size_t)3 * a.lds_cap + 2 * ((a.lds_cap >> 6) + 1) + 2 * ((a.lds_cap >> 3) + 1)) * sizeof(double);
+    const size_t lds = ((size_t)3 * a.lds_cap + 6 * ((a.lds_cap >> 6) + 1) + 2 * ((a.lds_cap >> 3) + 1)) * sizeof(double);
     // every lane integrates its own value function (~5·10⁴ Tsit5 steps): one wave per 64 u
     // of the column so that all of them run at once (the LDS slab allows one block per CU)
     const int tiles = (a.n_u + EQ_TILE - 1) / EQ_TILE;

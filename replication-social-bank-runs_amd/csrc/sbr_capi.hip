@@ -811,11 +811,11 @@ int sbr_init(int device, sbr_ctx** out)
     (void)hipDeviceGetAttribute(&smem, hipDeviceAttributeMaxSharedMemoryPerBlock, device);
     if (smem <= 0) smem = 65536;
     c->lds_smem = smem;
-    // 3 doubles per staged knot (t, G, HR) + 4 block-summary doubles per 64 knots; 1 KiB slack
-    // per 64 knots: t, G, HR (3·64) + HR max/min (2) + 8-knot G prefix-max/suffix-min (16)
-    c->lds_cap = (int)(((long)(smem - 1024) * 64) / (8 * (3 * 64 + 2 + 16)));
+    // per 64 staged knots: t, G, HR (3·64) + HR block max/min (2) + their prefix/suffix tables (4)
+    // + 8-knot G prefix-max/suffix-min (16); 1 KiB slack
+    c->lds_cap = (int)(((long)(smem - 1024) * 64) / (8 * (3 * 64 + 6 + 16)));
     // baseline equilibrium kernel: t, G (2·64) + summaries per 64 knots, two workgroups per CU
-    c->lds_cap_b = (int)(((long)(smem / 2 - 1024) * 64) / (8 * (2 * 64 + 2 + 16)));
+    c->lds_cap_b = (int)(((long)(smem / 2 - 1024) * 64) / (8 * (2 * 64 + 6 + 16)));
 #ifdef SBR_EQ_LDS_KNOTS
     c->lds_cap_b = std::min(c->lds_cap_b, (int)SBR_EQ_LDS_KNOTS);
 #endif

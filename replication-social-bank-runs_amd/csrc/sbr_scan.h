@@ -128,5 +128,77 @@ __device__ __forceinline__ void buffer_scan_blocked(P H, const SU& S, int ntau, 
     }
 }
 
+// Index queries over a monotone block table by binary search with a wave-uniform trip count
+// (the table length is the column's): no per-lane loop exits, a few LDS reads per query.
+// first b in [0, nb) with key[b] > u for a nondecreasing key (nb when none)
+template <class P>
+__device__ __forceinline__ int bs_first_gt_inc(P key, int nb, double u)
+{
+    int lo = -1; // key[lo] <= u (virtual −∞ at −1)
+    for (int step = 1 << (31 - __builtin_clz(nb | 1)); step > 0; step >>= 1) {
+        const int m = lo + step;
+        if (m < nb && !(key[m] > u)) lo = m;
+    }
+    return lo + 1;
+}
+// first b with !(key[b] > u) for a nonincreasing key (nb when none)
+template <class P>
+__device__ __forceinline__ int bs_first_le_dec(P key, int nb, double u)
+{
+    int lo = -1;
+    for (int step = 1 << (31 - __builtin_clz(nb | 1)); step > 0; step >>= 1) {
+        const int m = lo + step;
+        if (m < nb && key[m] > u) lo = m;
+    }
+    return lo + 1;
+}
+// last b with key[b] > u for a nonincreasing key (−1 when none)
+template <class P>
+__device__ __forceinline__ int bs_last_gt_dec(P key, int nb, double u)
+{
+    return bs_first_le_dec(key, nb, u) - 1;
+}
+// last b with !(key[b] > u) for a nondecreasing key (−1 when none)
+template <class P>
+__device__ __forceinline__ int bs_last_le_inc(P key, int nb, double u)
+{
+    return bs_first_gt_inc(key, nb, u) - 1;
+}
+
+// buffer_scan_blocked with the four scans from index 0 / from the end answered by the prefix /
+// suffix tables (hpm = prefix max of hmax, hpn = prefix min of hmin, hsm = suffix max of hmax,
+// hsn = suffix min of hmin: "some entry of blocks <= b above u" ⇔ hpm[b] > u, and so on), then
+// one in-block scan each; the two scans from an interior start keep the block loop.  The same
+// indices as buffer_scan_blocked.
+template <class P, class SU, class Q>
+__device__ __forceinline__ void buffer_scan_bs(P H, const SU& S, Q hpm, Q hpn, Q hsm, Q hsn, int nb, int ntau,
+                                               double u, bool& any, bool& all, int& fa, int& la, int& cin, int& cout)
+{
+    auto blk_end = [&](int b) { return (b << 6) + 64 < ntau ? (b << 6) + 64 : ntau; };
+    const int ba = bs_first_gt_inc(hpm, nb, u);
+    fa = ba < nb ? scan_fwd<true>(H, ba << 6, blk_end(ba), u) : -1;
+    any = fa >= 0;
+    const int bb = bs_first_le_dec(hpn, nb, u);
+    const int fb = bb < nb ? scan_fwd<false>(H, bb << 6, blk_end(bb), u) : -1;
+    all = fb < 0;
+    int lab = any ? bs_last_gt_dec(hsm, nb, u) : -1;
+    la = lab >= 0 ? scan_bwd<true>(H, lab << 6, blk_end(lab) - 1, u) : -1;
+    cin = -1;
+    cout = -1;
+    if (!any || all) return;
+    if (fa > 0) {
+        cin = fa - 1;
+    } else {
+        const int k = first_above(H, S, ntau, fb, u);
+        cin = k >= 0 ? k - 1 : -1;
+    }
+    if (la < ntau - 1) {
+        cout = la;
+    } else {
+        const int lbb = bs_last_le_inc(hsn, nb, u);
+        const int lb = lbb >= 0 ? scan_bwd<false>(H, lbb << 6, blk_end(lbb) - 1, u) : -1;
+        cout = last_above(H, S, lb, u);
+    }
+}
 
 }  // namespace sbr
