@@ -1630,6 +1630,18 @@ __device__ __forceinline__ int wave_ssl(P t, int lo, int hi, double x)
     return lo + __popcll(__ballot(pr));
 }
 
+#ifndef SBR_COOP_SPEC
+#define SBR_COOP_SPEC 1 // point_wave's bisection six levels per round (speculative tree over the wave)
+#endif
+// lane k's double (k wave-uniform)
+__device__ __forceinline__ double co_rl(double x, int k)
+{
+    const uint64_t u = sbr_dbits(x);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, k);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), k);
+    return sbr_bitsd(((uint64_t)hi << 32) | lo);
+}
+
 // wave-uniform in_range (the flag as solve_from_buffers sets it)
 __device__ __forceinline__ bool co_in_range(double x, double tlo, double thi, bool trunc, uint32_t& flag)
 {
@@ -1705,6 +1717,99 @@ __device__ __forceinline__ void point_wave(P T, P G, P H, const int n, const int
     const int jtin = jlo;
     uint32_t s = SBR_NO_RUN_MAXITER;
     double xi = NAN, tolr = INFINITY;
+#if SBR_COOP_SPEC
+    // Rounds of six bisection levels at once: lane ℓ < 63 evaluates node k = ℓ + 1 of the
+    // depth-6 tree below the current state (heap order; child 2k follows err > 0, 2k + 1
+    // err < 0), replaying its path's midpoint arithmetic exactly, then the wave walks the tree
+    // with the nodes' signs.  Each node runs the serial iteration's tests in its order; the walk
+    // stops at the first terminal node on the path — the iteration where the serial loop breaks,
+    // with its counters, flags and (for |err| <= tol) the slope probe, done by the whole wave.
+    int iter0 = 1;
+    for (;;) {
+        const int k = lane + 1;
+        const int d = 31 - __builtin_clz(k);
+        double nmin = xmin, nmax = xmax, xo = xnew;
+        for (int b = d - 1; b >= 0; b--) {
+            if (((k >> b) & 1) == 0) { nmax = xo; xo = 0.5 * (xo + nmin); }
+            else { nmin = xo; xo = 0.5 * (xo + nmax); }
+        }
+        const int it = iter0 + d;
+        int term = 0; // 1 collapse, 2 max_iters − 1, 3 range flag, 4 |err| <= tol, 5 past max_iters
+        uint32_t nflag = 0;
+        double err = 0.0, AW = 0.0, oc = 0.0, ic = 0.0, xoe = 0.0, xie = 0.0;
+        int j = 0, joc = 0, jic = 0;
+        bool oke = false, oki = false;
+        if (lane < 63) {
+            if (it > max_iters) term = 5;
+            else if (collapsed(nmin - nmax)) term = 1;
+            else if (it == max_iters - 1) term = 2;
+            else {
+                ic = dmin(tin, xo); oc = dmin(tout, xo);
+                j = ssl_range(T, jlo, jhi, xo);
+                const bool ok = co_in_range(oc, tlo, thi, trunc, nflag);
+                joc = (oc == xo) ? j : (ok ? ssl_range(T, 0, n - 1, oc) : 0);
+                const double Goc = ok ? lerp_at(T, G, n, joc, oc) : 0.0;
+                double Gic = 0.0;
+                if (co_in_range(ic, tlo, thi, trunc, nflag)) {
+                    jic = (ic == tin) ? jtin : (ic == xo ? j : ssl_range(T, 0, n - 1, ic));
+                    Gic = lerp_at(T, G, n, jic, ic);
+                }
+                if (j + 1 >= n) {
+                    nflag |= trunc ? SBR_ENGINE_TRUNC : SBR_OOB;
+                    term = 3;
+                } else {
+                    const double eps = T[j + 1] - T[j];
+                    xoe = oc + eps; xie = ic + eps;
+                    oke = co_in_range(xoe, tlo, thi, trunc, nflag);
+                    oki = co_in_range(xie, tlo, thi, trunc, nflag);
+                    if (nflag) term = 3;
+                    else {
+                        AW = Goc - Gic;
+                        err = AW - kappa;
+                        if (fabs(err) <= tolerance) term = 4;
+                    }
+                }
+            }
+        }
+        int node = 1, stop = 0;
+        for (int lev = 0; lev < 6 && !stop; lev++) {
+            const int src = node - 1;
+            const int t_ = __builtin_amdgcn_readlane(term, src);
+            if (t_) {
+                stop = 1;
+                r.iters = t_ == 5 ? max_iters : iter0 + lev;
+                if (t_ == 1) s = SBR_NO_RUN_COLLAPSE;
+                else if (t_ == 2) s = SBR_NO_RUN_MAXITER;
+                else if (t_ == 3) flag |= (uint32_t)__builtin_amdgcn_readlane((int)nflag, src);
+                else if (t_ == 4) {
+                    const double xo_t = co_rl(xo, src), AW_t = co_rl(AW, src), err_t = co_rl(err, src);
+                    const double xoe_t = co_rl(xoe, src), xie_t = co_rl(xie, src);
+                    const int joc_t = __builtin_amdgcn_readlane(joc, src), jic_t = __builtin_amdgcn_readlane(jic, src);
+                    const bool oke_t = __builtin_amdgcn_readlane(oke ? 1 : 0, src) != 0;
+                    const bool oki_t = __builtin_amdgcn_readlane(oki ? 1 : 0, src) != 0;
+                    double Goce = 0.0, Gice = 0.0;
+                    if (oke_t) Goce = lerp_at(T, G, n, wave_ssl(T, joc_t, n - 1, xoe_t), xoe_t);
+                    if (oki_t) Gice = lerp_at(T, G, n, wave_ssl(T, jic_t, n - 1, xie_t), xie_t);
+                    const double AWe = Goce - Gice;
+                    if (AWe >= AW_t) { s = SBR_RUN; xi = xo_t; tolr = fabs(err_t); }
+                    else s = SBR_FALSE_EQ;
+                }
+                break;
+            }
+            const double e_ = co_rl(err, src);
+            const int j_ = __builtin_amdgcn_readlane(j, src);
+            if (e_ > 0) jhi = j_; else jlo = j_;
+            if (lev == 5) { // the next round's state: the child of this depth-5 node
+                const double xs = co_rl(xo, src), mn = co_rl(nmin, src), mxv = co_rl(nmax, src);
+                if (e_ > 0) { xmin = mn; xmax = xs; xnew = 0.5 * (xs + mn); }
+                else { xmin = xs; xmax = mxv; xnew = 0.5 * (xs + mxv); }
+            }
+            node = 2 * node + (e_ > 0 ? 0 : 1);
+        }
+        if (stop) break;
+        iter0 += 6;
+    }
+#else
     for (int iter = 1; iter <= max_iters; iter++) {
         r.iters = iter;
         const double dd = xmin - xmax;
@@ -1744,6 +1849,7 @@ __device__ __forceinline__ void point_wave(P T, P G, P H, const int n, const int
             xmin = xo; jlo = j; xnew = 0.5 * (xo + xmax);
         }
     }
+#endif
     if (flag) { r.status = flag | lbits; return; }
     if (s != SBR_RUN) { r.status = s | lbits; return; }
     // the AW stage's own range checks (solve_from_buffers: G(0), then the path's last τ̄ — the
