@@ -1410,8 +1410,30 @@ __device__ __forceinline__ void eq_column(const int b, const int j0, const int j
         }
 #if SBR_SCAN_BS
         // the crossing scans' prefix / suffix tables over the HR blocks (hmax has no NaN, hmin has
-        // NaN as −∞): one lane each way
-        if (threadIdx.x == (BLOCK > 128 ? 128 : 2)) {
+        // NaN as −∞): a wave each way, 64 blocks per shuffle scan; small blocks: one lane each way
+        if (BLOCK >= 256 && (threadIdx.x >> 6) >= 2 && (threadIdx.x >> 6) <= 3) {
+            const bool fwd = (threadIdx.x >> 6) == 2;
+            const int ln = threadIdx.x & 63;
+            double ca = -INFINITY, cb = INFINITY;
+            for (int c0 = 0; c0 < nbh; c0 += 64) {
+                const int g = fwd ? c0 + ln : nbh - 1 - c0 - ln;
+                const bool in = fwd ? g < nbh : g >= 0;
+                double a = in ? hmax[g] : -INFINITY, b = in ? hmin[g] : INFINITY;
+                for (int off = 1; off < 64; off <<= 1) {
+                    const double oa = __shfl_up(a, off, 64), ob = __shfl_up(b, off, 64);
+                    if (ln >= off) { a = oa > a ? oa : a; b = ob < b ? ob : b; }
+                }
+                a = ca > a ? ca : a;
+                b = cb < b ? cb : b;
+                if (in) {
+                    if (fwd) { hpm[g] = a; hpn[g] = b; }
+                    else { hsm[g] = a; hsn[g] = b; }
+                }
+                ca = __shfl(a, 63, 64);
+                cb = __shfl(b, 63, 64);
+            }
+        }
+        if (BLOCK < 256 && threadIdx.x == 2) {
             double a0 = -INFINITY, b0 = INFINITY;
             for (int g = 0; g < nbh; g++) {
                 a0 = hmax[g] > a0 ? hmax[g] : a0;
@@ -1420,7 +1442,7 @@ __device__ __forceinline__ void eq_column(const int b, const int j0, const int j
                 hpn[g] = b0;
             }
         }
-        if (threadIdx.x == (BLOCK > 192 ? 192 : 3)) {
+        if (BLOCK < 256 && threadIdx.x == 3) {
             double a0 = -INFINITY, b0 = INFINITY;
             for (int g = nbh - 1; g >= 0; g--) {
                 a0 = hmax[g] > a0 ? hmax[g] : a0;

@@ -56,6 +56,7 @@ for s in ${STEPS:-tests smoke bench single}; do
               echo "pmc_$w rc=$rc" | tee -a "$OUT/steps.log"; if [ $rc -ne 0 ]; then exit $rc; fi
             done ;;
     socprof) run socprof 300 python -u bench.py --workload social --steps 1 --warmup 0 --social-max-iter 16 --social-prof --no-cpu-baseline --no-verify ;;
+    knotsprobevars) for v in ${VARS:-}; do run knotsprobe_$v 300 env SBR_LIB=replication-social-bank-runs_amd/lib_var/$v/libsbr.so python -u tools/knots_probe.py 2000; done ;;
     benchvars) for v in ${VARS:-}; do run bench_$v 300 env SBR_LIB=replication-social-bank-runs_amd/lib_var/$v/libsbr.so python -u bench.py --no-cpu-baseline; done ;;
     socialvars) for v in ${VARS:-}; do run social_$v 600 env SBR_LIB=replication-social-bank-runs_amd/lib_var/$v/libsbr.so python -u bench.py --workload social --steps 1 --warmup 0 --no-cpu-baseline --no-verify; done ;;
     socprofvars) for v in ${VARS:-}; do run socprof_$v 300 env SBR_LIB=replication-social-bank-runs_amd/lib_var/$v/libsbr.so python -u bench.py --workload social --steps 1 --warmup 0 --social-max-iter 16 --social-prof --no-cpu-baseline --no-verify; done ;;
