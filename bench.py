@@ -89,6 +89,23 @@ def pmc_of(kernel_prefix: str, workload: str):
     return None, None
 
 
+def pmc_social(rk_steps: float):
+    """(executed FP64 flops, HBM bytes) of social_iter_kernel over a whole share, from the PMC run
+    that tools/pmc_social.py folded into profiles/pmc_latest.json per attempted RK step (the first
+    16 iterates of the config-5 share, where the bulk runs), scaled by this run's RK steps; only
+    when the counters were taken on this kernel's machine code.  Bytes: FETCH_SIZE×2 + WRITE_SIZE."""
+    from sbr import provenance
+    try:
+        c = json.loads(PMC_SUMMARY.read_text())["workloads"]["social_64x512_bulk16"]["kernels"]["social_iter_kernel"]
+    except Exception:
+        return None, None
+    if c.get("code_sha16") is None or c["code_sha16"] != provenance.kernel_code_sha("social_iter_kernel"):
+        return None, None
+    ex = c.get("fp64_flops_executed_per_rk_step")
+    by = c.get("hbm_bytes_per_rk_step")
+    return (ex * rk_steps if ex is not None else None), (by * rk_steps if by is not None else None)
+
+
 def roofline(kernel: str, flops: float, secs: float, pmc=(None, None), limiter="latency") -> dict:
     """roofline block for `kernel`: algorithmic flops per launch / average launch time.
     The roof the metric is priced against is the FP64 vector peak (no dense
@@ -895,9 +912,14 @@ def main_social(a):
         # §8(d) flops of the forced-ODE steps only (96 per attempted step; the per-iterate
         # hazard / bisection / AW / norm work is not counted: a lower bound), over the
         # whole share's wall time of the iterate kernels
-        "roofline": roofline("social_iter_kernel", F8_RK_STEP * float(steps.sum()), iter_ms / max(a.steps, 1) / 1e3),
+        "roofline": roofline("social_iter_kernel", F8_RK_STEP * float(steps.sum()), iter_ms / max(a.steps, 1) / 1e3,
+                             pmc_social(float(steps.sum()))),
         "libsbr_sha16": lib_sha(),
     }
+    if res["roofline"]["traffic"] is not None:
+        res["roofline"]["traffic_note"] = ("HBM bytes of the whole share: the PMC run's bytes per attempted RK step "
+                                           "(first 16 iterates of the share, tools/pmc_social.py) x this run's RK steps; "
+                                           "executed flops count 64 lanes per wave instruction (an upper bound)")
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         sys.path.insert(0, str(REPO / "oracle"))
         import oracle as O  # noqa: E402  (test infrastructure: cpu_baseline leg only)
