@@ -36,6 +36,9 @@
 #ifndef SBR_LEARN_SLOTS
 #define SBR_LEARN_SLOTS 4 // learning workspaces of the pipelined batch
 #endif
+#ifndef SBR_HET_LEARN_MASK
+#define SBR_HET_LEARN_MASK 0 // A/B: hetero batch learning confined to half the CUs
+#endif
 #ifndef SBR_LEARN_GROUP
 #define SBR_LEARN_GROUP 1 // grids per learning launch of the pipelined batch (A/B: 2 was slower, 1.567 -> 1.631 ms per step: r04_j)
 #endif
@@ -66,6 +69,7 @@ struct sbr_ctx {
     int last_slot = 0;
     int64_t last_off = 0; // column offset of the last grid inside its (grouped) learning slot
     hipStream_t lstream[kLearnStreams] = {};
+    hipStream_t hl_stream[2] = {}; // hetero batch learning on a CU subset (SBR_HET_LEARN_MASK)
     hipEvent_t ev_in = nullptr, ev_learned[kLearnSlots] = {}, ev_eq[kLearnSlots] = {};
     // fork/join fences between HIP's null stream and `stream`, and the end of the last call
     // (whatever stream it ran on) that every call waits for (CallFence)
@@ -880,6 +884,8 @@ int sbr_free(sbr_ctx* c)
     }
     for (int k = 0; k < sbr_ctx::kLearnStreams; k++)
         if (c->lstream[k]) (void)hipStreamDestroy(c->lstream[k]);
+    for (hipStream_t hs : c->hl_stream)
+        if (hs) { (void)hipStreamSynchronize(hs); (void)hipStreamDestroy(hs); }
     for (hipStream_t rs : {c->rs_learn, c->rs_eq})
         if (rs) { (void)hipStreamSynchronize(rs); (void)hipStreamDestroy(rs); }
     for (hipEvent_t e : {c->ev_rin, c->ev_rq, c->ev_rl, c->ev_re})
@@ -1728,6 +1734,8 @@ int sbr_timing_read(sbr_ctx* c, void* stream, double* learn_ms, double* eq_ms, i
     int32_t n = 0;
     for (hipStream_t ls : c->lstream)
         if (ls) HIP_TRY(c, hipStreamSynchronize(ls), SBR_EDEVICE);
+    for (hipStream_t ls : c->hl_stream)
+        if (ls) HIP_TRY(c, hipStreamSynchronize(ls), SBR_EDEVICE);
     for (hipStream_t rs : {c->rs_learn, c->rs_eq})
         if (rs) HIP_TRY(c, hipStreamSynchronize(rs), SBR_EDEVICE);
     for (const auto& r : c->trec) {
@@ -1876,6 +1884,23 @@ int sbr_sweep_hetero_batch_dev(sbr_ctx* c, void* stream, int64_t n_batch, int32_
     int rc = ensure_hetero(c, (size_t)n_col, cap, (size_t)K);
     if (!rc && n_batch > 1) rc = ensure_hetero_bufs(c, c->H2, c->hs2_col, c->hs2_cap, c->hs2_K, (size_t)n_col, cap, (size_t)K);
     if (!rc) rc = ensure_pipe_streams(c);
+#if SBR_HET_LEARN_MASK
+    // the batch's learning waves (one per column, latency-bound, 101 VGPRs) packed two per SIMD
+    // on half of every XCD's CUs, so that the other half keeps two 256-VGPR equilibrium waves
+    // per SIMD instead of one beside a learning wave
+    if (!rc && !c->hl_stream[0]) {
+        int ncu = 0;
+        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device);
+        std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
+        for (int i = 0; i < ncu; i++)
+            if (((i >> 3) & 1) == 0) mask[(size_t)i >> 5] |= 1u << (i & 31);
+        for (int k = 0; k < 2 && !rc; k++)
+            if (hipExtStreamCreateWithCUMask(&c->hl_stream[k], (uint32_t)mask.size(), mask.data()) != hipSuccess) {
+                c->hl_stream[k] = nullptr;
+                rc = fail(c, SBR_EDEVICE, "hipExtStreamCreateWithCUMask");
+            }
+    }
+#endif
     if (rc) return rc;
     return fenced(c, stream, true, [&](hipStream_t s) -> int {
         sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, p, lambda, o.ode_maxiters, (int32_t)n_col, 0, 0};
@@ -1883,10 +1908,11 @@ int sbr_sweep_hetero_batch_dev(sbr_ctx* c, void* stream, int64_t n_batch, int32_
                              (o.flags & SBR_FLAG_EXHAUSTIVE) ? 1 : 0, (o.flags >> 8) & 7, nullptr};
         const size_t np = (size_t)n_col * (size_t)n_u;
         HIP_TRY(c, hipEventRecord(c->ev_in, s), SBR_EDEVICE);
-        for (int k = 0; k < 2; k++) HIP_TRY(c, hipStreamWaitEvent(c->lstream[k], c->ev_in, 0), SBR_EDEVICE);
+        for (int k = 0; k < 2; k++)
+            HIP_TRY(c, hipStreamWaitEvent(c->hl_stream[k] ? c->hl_stream[k] : c->lstream[k], c->ev_in, 0), SBR_EDEVICE);
         for (int64_t k = 0; k < n_batch; k++) {
             const int slot = (int)(k & 1);
-            hipStream_t ls = c->lstream[slot];
+            hipStream_t ls = c->hl_stream[slot] ? c->hl_stream[slot] : c->lstream[slot];
             const sbr::HeteroBufs& H = slot ? c->H2 : c->H;
             const double* bk = betas + k * n_col * K;
             const double* ek = eta + k * n_col;
