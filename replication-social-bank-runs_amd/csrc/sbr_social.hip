@@ -139,6 +139,93 @@ struct Walker {
     }
 };
 
+#ifndef SBR_SOCIAL_PAIRS
+#define SBR_SOCIAL_PAIRS 1 // streaming passes and damping walkers load knot pairs (16 B per lane per request)
+#endif
+
+// knots k, k+1 (k even) of one lane in one 16-byte load: a pair never straddles a 16-knot line
+__device__ __forceinline__ double2 ld2(BView b, int k)
+{
+    const uint32_t u = (uint32_t)k;
+    return *(const double2*)((const char*)b.p + (((u >> 4) << 13) | ((u & 15u) << 3)));
+}
+__device__ __forceinline__ void st2(BView b, int k, double x, double y)
+{
+    const uint32_t u = (uint32_t)k;
+    *(double2*)((char*)b.p + (((u >> 4) << 13) | ((u & 15u) << 3))) = make_double2(x, y);
+}
+
+// Walker with the knot values held beside the knot times: an 8-knot window on a 4-aligned base,
+// filled by four paired loads per array, so both bracket and interpolation operands come from
+// registers (one refill per ~4 knots of walk instead of 4 operand loads per lookup).  Same
+// brackets and the same lerp_at arithmetic as Walker.
+struct WalkerV {
+    BView t, v;
+    int n, wb;
+    double tw[8], vw[8];
+    double tfirst, tlast;
+    __device__ __forceinline__ void load(int base)
+    {
+        wb = base;
+        const int q = n > 0 ? ((n - 1) & ~1) : 0; // last pair that holds a knot (k+1 < cap: cap is a multiple of 16)
+#pragma unroll
+        for (int m = 0; m < 4; m++) {
+            const int k = base + 2 * m;
+            const int kc = k < q ? k : q;
+            const double2 a = ld2(t, kc), b = ld2(v, kc);
+            tw[2 * m] = (k < n) ? a.x : (double)INFINITY;
+            tw[2 * m + 1] = (k + 1 < n) ? a.y : (double)INFINITY;
+            vw[2 * m] = b.x;
+            vw[2 * m + 1] = b.y;
+        }
+    }
+    __device__ __forceinline__ void init(BView tt, BView vv, int nn)
+    {
+        t = tt;
+        v = vv;
+        n = nn;
+        load(0);
+        tfirst = nn > 0 ? tw[0] : 0.0;
+        tlast = nn > 0 ? tt[nn - 1] : 0.0;
+    }
+    __device__ __forceinline__ int find_advance(double x)
+    {
+        int c = 0;
+#pragma unroll
+        for (int k = 1; k < 7; k++) c += (tw[k] <= x) ? 1 : 0;
+        int j = wb + c;
+        if (!(x >= tw[0] && x < tw[7]))
+            j = (x >= tw[0]) ? ssl_gallop(t, n, wb + 7, x) : ssl_range(t, 0, wb, x);
+        if (j - wb >= 4 || j < wb) load(j & ~3);
+        return j;
+    }
+    __device__ __forceinline__ static double sel4(const double* w, int r)
+    {
+        const double lo = (r & 1) ? w[1] : w[0];
+        const double hi = (r & 1) ? w[3] : w[2];
+        return (r & 2) ? hi : lo;
+    }
+    __device__ __forceinline__ double at(double x, bool& oob)
+    {
+        const bool in = n >= 2 && x >= tfirst && x <= tlast;
+        oob |= !in;
+        if (!in) return (double)NAN;
+        int j = find_advance(x);
+        j = j > n - 2 ? n - 2 : j;
+        j = j < 0 ? 0 : j;
+        const int r = j - wb;
+        double t0, t1, v0, v1;
+        if (r >= 0 && r < 4) {
+            t0 = sel4(tw, r); t1 = sel4(tw + 1, r);
+            v0 = sel4(vw, r); v1 = sel4(vw + 1, r);
+        } else { // x == t_{n-1} on a window that starts at n−1
+            t0 = t[j]; t1 = t[j + 1]; v0 = v[j]; v1 = v[j + 1];
+        }
+        const double d = (x - t0) / (t1 - t0);
+        return v0 * (1.0 - d) + v1 * d;
+    }
+};
+
 // full-range lookup (non-monotone callers: the bisection)
 __device__ __forceinline__ double interp_full(BView t, BView v, int n, double x, bool& oob)
 {
@@ -934,6 +1021,58 @@ __device__ __forceinline__ bool social_iterate(const SocialArgs& a, int l, int i
             if constexpr (COOP) {
                 coop_hazard_scan(T, Gv, AWO, X, VO, n, BETA, lam, p, U, ETA, any, all, first_above, last_above, tin_c,
                                  tout_c);
+            } else if constexpr (SBR_SOCIAL_PAIRS != 0) {
+                // the two passes below on knot pairs (same fold, same order): pass A
+                double I = 0.0, eprev = 0.0, tprev = 0.0;
+                for (int i = 0; i < n; i += 2) { // i <= (n−1) & ~1: the pair holds knot i
+                    const double2 t2 = ld2(T, i), g2 = ld2(Gv, i), a2 = ld2(AWO, i);
+                    const double e0 = sbr_exp(lam * t2.x);
+                    const double ei0 = e0 * (((1.0 - g2.x) * BETA) * a2.x);
+                    if (i > 0) I = I + (0.5 * (eprev + ei0)) * (t2.x - tprev);
+                    eprev = ei0;
+                    tprev = t2.x;
+                    double e1 = 0.0;
+                    if (i + 1 < n) {
+                        e1 = sbr_exp(lam * t2.y);
+                        const double ei1 = e1 * (((1.0 - g2.y) * BETA) * a2.y);
+                        I = I + (0.5 * (eprev + ei1)) * (t2.y - tprev);
+                        eprev = ei1;
+                        tprev = t2.y;
+                    }
+                    st2(X, i, e0, e1); // X[n] (n odd) is scratch inside the capacity
+                }
+                const double Ieta = I;
+                // pass B: HR and optimal_buffer's crossing scan (solver.jl:211-264)
+                I = 0.0;
+                double hr_prev = 0.0;
+                for (int i = 0; i < n; i += 2) {
+                    const double2 t2 = ld2(T, i), g2 = ld2(Gv, i), a2 = ld2(AWO, i), x2 = ld2(X, i);
+#pragma unroll
+                    for (int h = 0; h < 2; h++) {
+                        const int k = i + h;
+                        if (k >= n) break;
+                        const double ti = h ? t2.y : t2.x;
+                        const double xi = h ? x2.y : x2.x;
+                        const double pdf = ((1.0 - (h ? g2.y : g2.x)) * BETA) * (h ? a2.y : a2.x);
+                        const double ei = xi * pdf;
+                        if (k > 0) I = I + (0.5 * (eprev + ei)) * (ti - tprev);
+                        eprev = ei;
+                        const double hr = ((p * xi) * pdf) / ((p * I) + (omp * Ieta));
+                        const bool ab = hr > U;
+                        any |= ab; all &= ab;
+                        if (ab) { if (first_above < 0) first_above = k; last_above = k; }
+                        if (k > 0) {
+                            const bool abp = hr_prev > U;
+                            if (!have_in && !abp && ab) {
+                                tin_c = tprev + ((U - hr_prev) * (ti - tprev)) / (hr - hr_prev);
+                                have_in = true;
+                            }
+                            if (abp && !ab) tout_c = tprev + ((U - hr_prev) * (ti - tprev)) / (hr - hr_prev);
+                        }
+                        hr_prev = hr;
+                        tprev = ti;
+                    }
+                }
             } else {
                 // pass A: ∫ trapezoid to η
                 double I = 0.0;
@@ -1054,7 +1193,7 @@ __device__ __forceinline__ bool social_iterate(const SocialArgs& a, int l, int i
                 const double G0 = interp_full(T, Gv, n, 0.0, aoob);
                 Walker wa, wb, wa2, wb2;
                 wa.init(T, Gv, n); wb.init(T, Gv, n); wa2.init(T, Gv, n); wb2.init(T, Gv, n);
-                auto aw_at = [&](double tau, Walker& A, Walker& B) {
+                auto aw_at = [&](double tau, auto& A, auto& B) {
                     const double xa = (tau - XI) + ic;
                     const double xb = (tau - XI) + oc;
                     const double gi = A.at(xa > 0 ? xa : 0.0, aoob);
@@ -1097,6 +1236,38 @@ __device__ __forceinline__ bool social_iterate(const SocialArgs& a, int l, int i
                     // knot i is aw_i·(1−0) + aw_{i+1}·0 (i < n−1), aw_{n−2}·0 + aw_{n−1}·1
                     if constexpr (COOP) {
                         coop_damping(T, Gv, AWO, n, XI, ic, oc, G0, aoob);
+                    } else if constexpr (SBR_SOCIAL_PAIRS != 0) {
+                        // the same loop two knots at a time: AWO and the τ grid move in 16-byte pairs
+                        WalkerV da, db;
+                        da.init(T, Gv, n); db.init(T, Gv, n);
+                        double2 tp = ld2(T, 0);
+                        double aw_i = aw_at(tp.x, da, db);
+                        for (int i = 0; i < n - 1; i += 2) {
+                            // T[i+1] from the current pair, T[i+2] from the next (clamped: unused past n−1)
+                            const int kn = i + 2 <= ((n - 1) & ~1) ? i + 2 : ((n - 1) & ~1);
+                            const double2 tq = ld2(T, kn);
+                            const double2 ao = ld2(AWO, i);
+                            double aw_1 = aw_at(tp.y, da, db);
+                            const double v0 = aw_i * (1.0 - 0.0) + aw_1 * 0.0;
+                            const double w0 = 0.5 * ao.x + 0.5 * v0;
+                            double w1;
+                            if (i == n - 2) { // the pair ends the grid: AWO[n−1] takes the last segment's right end
+                                const double vl = aw_i * (1.0 - 1.0) + aw_1 * 1.0;
+                                w1 = 0.5 * ao.y + 0.5 * vl;
+                            } else {
+                                const double aw_2 = aw_at(tq.x, da, db);
+                                const double v1 = aw_1 * (1.0 - 0.0) + aw_2 * 0.0;
+                                w1 = 0.5 * ao.y + 0.5 * v1;
+                                if (i + 1 == n - 2) {
+                                    const double vl = aw_1 * (1.0 - 1.0) + aw_2 * 1.0;
+                                    AWO[n - 1] = 0.5 * AWO[n - 1] + 0.5 * vl;
+                                }
+                                aw_1 = aw_2;
+                            }
+                            st2(AWO, i, w0, w1);
+                            aw_i = aw_1;
+                            tp = tq;
+                        }
                     } else {
                         Walker da, db;
                         da.init(T, Gv, n); db.init(T, Gv, n);
@@ -1127,7 +1298,7 @@ __device__ __forceinline__ bool social_iterate(const SocialArgs& a, int l, int i
         const double oc = (tout > XI) ? XI : tout;
         bool aoob = false;
         const double G0 = interp_full(T, Gv, n, 0.0, aoob);
-        Walker A, B;
+        typename std::conditional<SBR_SOCIAL_PAIRS != 0, WalkerV, Walker>::type A, B;
         A.init(T, Gv, n); B.init(T, Gv, n);
         double mx = -(double)INFINITY;
         for (int i = 0; i < n; i++) {
