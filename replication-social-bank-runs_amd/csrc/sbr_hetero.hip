@@ -423,6 +423,9 @@ __global__ __launch_bounds__(64) void learn_hetero_kernel(const double* __restri
 #ifndef SBR_HET_LEARN_WAVE
 #define SBR_HET_LEARN_WAVE 1 // 0: learn_hetero_kernel (one lane per column, A/B)
 #endif
+#ifndef SBR_HET_LEARN_ROWS
+#define SBR_HET_LEARN_ROWS 4 // columns per learning wave: 4 = learn_hetero_wave4_kernel (16-lane rows), 1 = one per wave
+#endif
 #ifndef SBR_HET_DIVRCP
 #define SBR_HET_DIVRCP 0 // LU back substitutions by refined pivot reciprocals (A/B)
 #endif
@@ -436,7 +439,52 @@ __device__ __forceinline__ double wave_bcast(double v, int l)
     return __hiloint2double(hi, lo);
 }
 
-template <int K>
+// Row broadcast for the 4-columns-per-wave layout (learn_hetero_wave4_kernel): every lane of
+// each 16-lane row receives lane j of its row (DPP row_newbcast:j, a VALU move: no SGPR round
+// trip).  j is a compile-time constant after unrolling; the switch folds to one case.
+template <int J>
+__device__ __forceinline__ int row_bcast_i(int v)
+{
+    return __builtin_amdgcn_mov_dpp(v, 0x150 + J, 0xf, 0xf, false); // no `old` operand to materialise
+}
+__device__ __forceinline__ int row_bcast_int(int v, int j)
+{
+    switch (j & 15) {
+    case 0: return row_bcast_i<0>(v);
+    case 1: return row_bcast_i<1>(v);
+    case 2: return row_bcast_i<2>(v);
+    case 3: return row_bcast_i<3>(v);
+    case 4: return row_bcast_i<4>(v);
+    case 5: return row_bcast_i<5>(v);
+    case 6: return row_bcast_i<6>(v);
+    case 7: return row_bcast_i<7>(v);
+    case 8: return row_bcast_i<8>(v);
+    case 9: return row_bcast_i<9>(v);
+    case 10: return row_bcast_i<10>(v);
+    case 11: return row_bcast_i<11>(v);
+    case 12: return row_bcast_i<12>(v);
+    case 13: return row_bcast_i<13>(v);
+    case 14: return row_bcast_i<14>(v);
+    default: return row_bcast_i<15>(v);
+    }
+}
+__device__ __forceinline__ double row_bcast(double v, int j)
+{
+    if (!__builtin_constant_p(j)) // a row-uniform runtime index (the LU's pivot row): LDS crossbar
+        return __shfl(v, (int)(threadIdx.x & 48u) | (j & 15), 64);
+    const int lo = row_bcast_int(__double2loint(v), j);
+    const int hi = row_bcast_int(__double2hiint(v), j);
+    return __hiloint2double(hi, lo);
+}
+// ROWS = 1: one column per wave (lane = component); ROWS = 4: one column per 16-lane row
+template <int ROWS>
+__device__ __forceinline__ double bcast(double v, int j)
+{
+    if constexpr (ROWS == 1) return wave_bcast(v, j);
+    else return row_bcast(v, j);
+}
+
+template <int K, int ROWS = 1>
 struct WaveRow {
     const int lane; // row / component index of this lane (lanes >= K: K - 1's shadow)
     const int kk;
@@ -450,26 +498,26 @@ struct WaveRow {
     __device__ __forceinline__ double omega(double I) const
     {
         const double pr = dk * I;
-        double w = wave_bcast(pr, 0);
+        double w = bcast<ROWS>(pr, 0);
 #pragma unroll
-        for (int j = 1; j < K; j++) w = w + wave_bcast(pr, j);
+        for (int j = 1; j < K; j++) w = w + bcast<ROWS>(pr, j);
         return w;
     }
     __device__ __forceinline__ double rhs(double I) const { return ((1.0 - I) * bk) * omega(I); }
     // sqrt(Σ v_k² / K), the sum from 0.0 in component order
     __device__ __forceinline__ double rms(double v) const
     {
-        if (K == 1) return wave_bcast(fabs(v), 0);
+        if (K == 1) return bcast<ROWS>(fabs(v), 0);
         const double sq = v * v;
         double s = 0.0;
 #pragma unroll
-        for (int i = 0; i < K; i++) s = s + wave_bcast(sq, i);
+        for (int i = 0; i < K; i++) s = s + bcast<ROWS>(sq, i);
         return sqrt(s / (double)K);
     }
 };
 
 // Row-distributed K×K LU (RegLU's operation sequence): lane i holds row i of A.
-template <int K>
+template <int K, int ROWS = 1>
 struct WaveLU {
     double A[K];
     int piv[K]; // wave-uniform
@@ -477,12 +525,12 @@ struct WaveLU {
     {
 #pragma unroll
         for (int k = 0; k < K; k++) {
-            double pv = wave_bcast(A[k], k);
+            double pv = bcast<ROWS>(A[k], k);
             double amax = fabs(pv);
             int kp = k;
 #pragma unroll
             for (int i = k + 1; i < K; i++) {
-                const double ai = wave_bcast(A[k], i);
+                const double ai = bcast<ROWS>(A[k], i);
                 if (fabs(ai) > amax) { kp = i; amax = fabs(ai); pv = ai; }
             }
             piv[k] = kp;
@@ -490,7 +538,7 @@ struct WaveLU {
                 if (kp != k) {
 #pragma unroll
                     for (int j = 0; j < K; j++) {
-                        const double vk = wave_bcast(A[j], k), vp = wave_bcast(A[j], kp);
+                        const double vk = bcast<ROWS>(A[j], k), vp = bcast<ROWS>(A[j], kp);
                         A[j] = lane == k ? vp : (lane == kp ? vk : A[j]);
                     }
                 }
@@ -500,7 +548,7 @@ struct WaveLU {
             }
 #pragma unroll
             for (int j = k + 1; j < K; j++) {
-                const double akj = wave_bcast(A[j], k);
+                const double akj = bcast<ROWS>(A[j], k);
                 const double v = A[j] - A[k] * akj;
                 A[j] = lane > k ? v : A[j];
             }
@@ -533,13 +581,13 @@ struct WaveLU {
         for (int k = 0; k < K; k++) {
             const int kp = piv[k];
             if (kp != k) {
-                const double x = wave_bcast(b, k), y = wave_bcast(b, kp);
+                const double x = bcast<ROWS>(b, k), y = bcast<ROWS>(b, kp);
                 b = lane == k ? y : (lane == kp ? x : b);
             }
         }
 #pragma unroll
         for (int j = 0; j < K; j++) {
-            const double a = -wave_bcast(b, j);
+            const double a = -bcast<ROWS>(b, j);
             const double v = fma(a, A[j], b);
             b = lane > j ? v : b;
         }
@@ -552,9 +600,9 @@ struct WaveLU {
             double q;
             if (fast) q = div_rcp(b, A[j], rdiag);
             else q = b / A[j];
-            const double bj = wave_bcast(q, j);
+            const double bj = bcast<ROWS>(q, j);
 #else
-            const double bj = wave_bcast(b / A[j], j); // lane j: b_j / A[j][j]
+            const double bj = bcast<ROWS>(b / A[j], j); // lane j: b_j / A[j][j]
 #endif
             b = lane == j ? bj : b;
             const double v = fma(-bj, A[j], b);
@@ -792,6 +840,264 @@ __global__ __launch_bounds__(64) void learn_hetero_wave_kernel(const double* __r
         }
     }
     if (lane == 0) {
+        L.n_knots[c] = n;
+        L.n_tau[c] = m;
+        L.n_le[c] = n_le;
+        L.status[c] = st;
+        L.n_accept[c] = naccept;
+        L.n_reject[c] = nreject;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// learn_hetero_wave4_kernel<K>: four columns per wave, one 16-lane row per column
+// ---------------------------------------------------------------------------
+// learn_hetero_wave_kernel's solve with the wave's idle lanes put to work: row r (lanes
+// 16r..16r+15) runs column 4·blockIdx + r, lane 16r + k holds component k.  The couplings read
+// the row's lanes by DPP row broadcasts (a VALU move) instead of readlanes into SGPRs, and the
+// step control (t, dt, controller, AutoSwitch, knot counters) is row-uniform in VGPRs: all
+// four columns advance in the same instructions, so a wave does four columns' steps at the
+// issue cost of one (the chain is latency-bound: config 4 issued ≈10 cycles per instruction
+// with one column per wave).  Rows disagree only on the stiff/non-stiff branch (both run,
+// masked) and on when they finish.  Every operation of a column is the one-column kernel's, in
+// the same order: bit-identical knots, CDFs and hazards.  Lanes 16r + k, k >= K, shadow
+// component K−1 and never store.
+template <int K>
+__global__ __launch_bounds__(64) void learn_hetero_wave4_kernel(const double* __restrict__ betas,
+                                                                const double* __restrict__ dist,
+                                                                const double* __restrict__ eta,
+                                                                const double* __restrict__ t_end, LearnArgs a,
+                                                                HeteroBufs L)
+{
+    static_assert(K <= 16, "one column per 16-lane row");
+    const int lane = threadIdx.x;
+    const int row = lane >> 4, comp = lane & 15;
+    const int c_raw = blockIdx.x * 4 + row;
+    const bool colok = c_raw < a.n_beta;
+    const int c = colok ? c_raw : a.n_beta - 1; // tail rows shadow the last column and never store
+    const bool act = colok && comp < K;
+    const WaveRow<K, 4> R(comp, betas + (size_t)c * K, dist);
+    const double ETA = eta[c], T1 = t_end[c], T0 = 0.0;
+    const size_t cap = (size_t)L.cap;
+    double* __restrict__ T = L.t + (size_t)c * cap;
+    double* __restrict__ Gv = L.G + (size_t)c * cap * K;
+    double* __restrict__ H = L.hr + ((size_t)c * K + R.kk) * cap;
+    double* __restrict__ HI = L.hrI + ((size_t)c * K + R.kk) * cap;
+    uint32_t st = 0;
+    bool argok = ETA > 0.0 && T1 > T0;
+#pragma unroll
+    for (int k = 0; k < K; k++) argok = argok && (bcast<4>(R.bk, k) > 0.0);
+    if (!argok && colok && comp == 0) {
+        L.status[c] = SBR_ARG_INVALID;
+        L.n_knots[c] = 0; L.n_tau[c] = 0; L.n_le[c] = 0; L.n_accept[c] = 0; L.n_reject[c] = 0;
+    }
+    bool live = argok && colok;
+    const double x0 = a.x0, rtol = a.rtol, atol = a.atol, p = a.p, lam = a.lam;
+    const double dtmax = T1 - T0;
+    const double dtmin = sbr_jl_eps(dmax(fabs(T0), fabs(T1)));
+    double x, k1, k2, k3, k4, k5, k6, k7, tmp, tmp6, u;
+
+    // ---- ode_determine_initdt (row-uniform; dead rows compute it on their shadow column) ----
+    x = x0;
+    const double sk = fma(fabs(x0), rtol, atol);
+    const double d0 = R.rms(x0 / sk);
+    k1 = R.rhs(x);
+    const double d1 = R.rms(k1 / sk);
+    double dt0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : (d0 / d1) / 100.0;
+    dt0 = dmin(dt0, dtmax);
+    double dt;
+    if (dt0 < 10.0 * DBL_EPS) {
+        dt = dmax(1e-6, dtmin);
+    } else {
+        u = fma(dt0, k1, x0);
+        k7 = R.rhs(u);
+        bool same = true;
+#pragma unroll
+        for (int k = 0; k < K; k++) same = same && (row_bcast_int((int)(k1 == k7), k) != 0);
+        if (same) {
+            dt = dmax(dtmin, 100.0 * dt0);
+        } else {
+            const double d2 = R.rms((k7 - k1) / sk) / dt0;
+            const double md = dmax(d1, d2);
+            const double dt1 = (md <= 1e-15) ? dmax(1e-6, dt0 * 1e-3) : sbr_pow_pos(0.01 / md, 1.0 / SBR_INITDT_DEN);
+            dt = dmax(dtmin, dmin(dmin(100.0 * dt0, dt1), dtmax));
+        }
+    }
+
+    // ---- knot sink (learn_hetero_wave_kernel's, per row) ----
+    int n = 0, m = 0;
+    double tprev = 0.0, Ik = 0.0, eprev = 0.0, gprev = 0.0;
+    bool past = false, done = false;
+    auto push = [&](double t, double xs, double g) {
+        if (n >= L.cap) { st |= SBR_KNOT_OVERFLOW; done = true; return; }
+        if (colok && comp == 0) T[n] = t;
+        if (act) Gv[(size_t)n * K + comp] = xs;
+        if (!past) {
+            if (t <= ETA) {
+                const double E = sbr_exp(lam * t);
+                const double e = E * g;
+                Ik = (m == 0) ? 0.0 : Ik + (0.5 * (eprev + e)) * (t - tprev);
+                if (act) { H[m] = (p * E) * g; HI[m] = Ik; }
+                eprev = e;
+                gprev = g;
+                m++;
+                tprev = t;
+            } else {
+                past = true;
+                const double d = (ETA - tprev) / (t - tprev);
+                const double E = sbr_exp(lam * ETA);
+                const double pe = gprev * (1.0 - d) + g * d;
+                const double e = E * pe;
+                Ik = Ik + (0.5 * (eprev + e)) * (ETA - tprev);
+                if (act) { H[m] = (p * E) * pe; HI[m] = Ik; }
+                m++;
+            }
+        }
+        n++;
+    };
+
+    const double snap = 100.0 * sbr_jl_eps(T1);
+    double t = T0;
+    double eig = 1.0;
+    PIControl pc;
+    AutoSwitch as;
+    int naccept = 0, nreject = 0;
+    if (live) push(t, x, k1);
+    int64_t iter = 0;
+    for (;;) {
+        const bool run = live && t < T1 && !done;
+        if (!__any(run)) break;
+        if (!run) continue; // finished rows idle (masked) until every row of the wave is done
+        if (++iter > a.maxiters) { st |= SBR_ODE_MAXITERS; live = false; continue; }
+        (void)as.choose(eig, dt);
+        dt = dmin(dtmax, dt);
+        dt = dmax(dt, dtmin);
+        dt = dmin(dt, T1 - t);
+        if (dt <= dtmin && t + dt < T1) { st |= SBR_ODE_FAILED; live = false; continue; }
+        double EEst;
+        if (as.stiff) {
+            const double dtg = dt * ROS23_D;
+            const double invdtg = 1.0 / dtg, neginvdtg = -(1.0 / dtg);
+            const double dto2 = dt / 2.0, dto6 = dt / 6.0;
+            WaveLU<K, 4> W;
+            {
+                const double w = R.omega(x);
+                const double bkx = (1.0 - x) * R.bk;
+                const double dg = (-R.bk) * w + R.dk * bkx;
+                double s = 0.0;
+#pragma unroll
+                for (int j = 0; j < K; j++) {
+                    W.A[j] = (j == comp) ? dg : dist[j] * bkx;
+                    s = s + fabs(W.A[j]);
+                }
+                double nrm = 0.0;
+#pragma unroll
+                for (int i = 0; i < K; i++) {
+                    const double si = bcast<4>(s, i);
+                    nrm = (nrm != nrm || si != si) ? (double)NAN : (si > nrm ? si : nrm);
+                }
+                eig = nrm;
+#pragma unroll
+                for (int j = 0; j < K; j++) W.A[j] = (j == comp) ? fma(-1.0, invdtg, W.A[j]) : W.A[j];
+            }
+            W.factor(comp);
+            double r = k1 + dtg * 0.0;
+            W.solve(r, comp);
+            const double s1 = r * neginvdtg;
+            tmp = fma(dto2, s1, x);
+            const double f1 = R.rhs(tmp);
+            r = f1 - s1;
+            W.solve(r, comp);
+            const double s2 = fma(r, neginvdtg, s1);
+            u = fma(dt, s2, x);
+            k7 = R.rhs(u);
+            r = fma(dt, 0.0, fma(-2.0, s1 - k1, fma(-ROS23_C32, s2 - f1, k7)));
+            W.solve(r, comp);
+            const double s3 = r * neginvdtg;
+            const double ut = dto6 * (fma(-2.0, s2, s1) + s3);
+            EEst = R.rms(ut / fma(dmax(fabs(x), fabs(u)), rtol, atol));
+        } else {
+            const double a21 = dt * A21;
+            tmp = fma(a21, k1, x);
+            k2 = R.rhs(tmp);
+            tmp = fma(dt, fma(A31, k1, A32 * k2), x);
+            k3 = R.rhs(tmp);
+            tmp = fma(dt, fma(A41, k1, fma(A42, k2, A43 * k3)), x);
+            k4 = R.rhs(tmp);
+            tmp = fma(dt, fma(A51, k1, fma(A52, k2, fma(A53, k3, A54 * k4))), x);
+            k5 = R.rhs(tmp);
+            tmp6 = fma(dt, fma(A61, k1, fma(A62, k2, fma(A63, k3, fma(A64, k4, A65 * k5)))), x);
+            k6 = R.rhs(tmp6);
+            u = fma(dt, fma(A71, k1, fma(A72, k2, fma(A73, k3, fma(A74, k4, fma(A75, k5, A76 * k6))))), x);
+            k7 = R.rhs(u);
+            const double rr = fabs((k7 - k6) / (u - tmp6));
+            double e = 0.0;
+            bool e_nan = false;
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+                const double v = bcast<4>(rr, k);
+                if (v != v) e_nan = true;
+                else if (v > e) e = v;
+            }
+            eig = e_nan ? (double)NAN : e;
+            const double ut = dt * fma(BT1, k1, fma(BT2, k2, fma(BT3, k3, fma(BT4, k4,
+                                       fma(BT5, k5, fma(BT6, k6, BT7 * k7))))));
+            EEst = R.rms(ut / fma(dmax(fabs(x), fabs(u)), rtol, atol));
+        }
+        if (EEst != EEst) { st |= SBR_ODE_FAILED; live = false; continue; }
+        bool acc;
+        const double dtn = pc.next_dt(EEst, dt, dtmax, dtmin, acc);
+        if (acc) {
+            naccept++;
+            double tn = t + dt;
+            if (fabs(tn - T1) < snap) tn = T1;
+            t = tn;
+            x = u;
+            k1 = k7;
+            dt = dtn;
+            push(t, x, k1);
+        } else {
+            nreject++;
+            dt = dtn;
+        }
+        if (!(dt > 0.0) || !isfinite(dt)) { st |= SBR_ODE_FAILED; live = false; }
+    }
+    const bool ran = argok && colok;
+    if (as.nswitch > 0) st |= SBR_STIFF_SWITCH;
+    int n_le = m;
+    if (ran) {
+        if (past) {
+            n_le = m - 1;
+        } else if (!(st & SBR_KNOT_OVERFLOW)) {
+            if (n >= 2 && tprev == ETA) {
+                const double E = sbr_exp(lam * ETA);
+                const double pe = 0.0 + gprev * 1.0;
+                if (act) { H[m] = (p * E) * pe; HI[m] = Ik; }
+                m++;
+            } else {
+                st |= SBR_OOB;
+            }
+        }
+    }
+    // normalisation hr = p·e^{λτ̄}g / (p·I(τ̄) + (1 − p)·I(η)), all 64 lanes over each column's rows
+    __threadfence_block();
+    const double omp = 1.0 - p;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int cr = blockIdx.x * 4 + r;
+        const int mr = __builtin_amdgcn_readlane(m, 16 * r);
+        const int okr = __builtin_amdgcn_readlane((ran && !(st & SBR_OOB)) ? 1 : 0, 16 * r);
+        if (cr >= a.n_beta || mr <= 0 || !okr) continue;
+        double* __restrict__ Hc = L.hr + (size_t)cr * K * cap;
+        const double* __restrict__ HIc = L.hrI + (size_t)cr * K * cap;
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const double Ieta = HIc[(size_t)k * cap + mr - 1];
+            for (int i = lane; i < mr; i += 64)
+                Hc[(size_t)k * cap + i] = Hc[(size_t)k * cap + i] / ((p * HIc[(size_t)k * cap + i]) + (omp * Ieta));
+        }
+    }
+    if (ran && comp == 0) {
         L.n_knots[c] = n;
         L.n_tau[c] = m;
         L.n_le[c] = n_le;
@@ -1486,7 +1792,10 @@ static hipError_t launch_hetero_k(const double* betas, const double* dist, const
         return hipGetLastError();
     }
     if (phase == 0) {
-#if SBR_HET_LEARN_WAVE
+#if SBR_HET_LEARN_WAVE && SBR_HET_LEARN_ROWS == 4
+        hipLaunchKernelGGL(learn_hetero_wave4_kernel<K>, dim3((la.n_beta + 3) / 4), dim3(64), 0, s, betas, dist, eta,
+                           t_end, la, L);
+#elif SBR_HET_LEARN_WAVE
         hipLaunchKernelGGL(learn_hetero_wave_kernel<K>, dim3(la.n_beta), dim3(64), 0, s, betas, dist, eta, t_end, la, L);
 #else
         hipLaunchKernelGGL(learn_hetero_kernel<K>, dim3((la.n_beta + 63) / 64), dim3(64), 0, s, betas, dist, eta,

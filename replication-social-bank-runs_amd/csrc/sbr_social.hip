@@ -39,13 +39,33 @@ namespace {
 // line by line (an 8 KiB row per 16-knot block).  A lane still streams its own
 // lines sequentially, but a wave's 64 concurrent accesses fall within a few
 // MiB instead of 64 separate multi-MiB rows (page/TLB locality).
+// Typed address spaces (A/B knob): the workspace is global memory and the rings are LDS.  With
+// generic pointers the compiler issues FLAT loads, and it merges a ring read and its global
+// fallback (`in_ring ? RT(j) : to[j]`) into one FLAT load of a selected pointer; a FLAT load
+// counts on both the vector-memory and the LDS counters, so every ring read waited for the
+// lane's outstanding global loads and stores.
+#ifndef SBR_SOCIAL_AS
+#define SBR_SOCIAL_AS 1
+#endif
+typedef double sbr_dv2 __attribute__((ext_vector_type(2))); // 16-byte knot pair
+#if SBR_SOCIAL_AS
+typedef __attribute__((address_space(1))) double gdouble;
+typedef __attribute__((address_space(1))) char gchar;
+typedef __attribute__((address_space(1))) sbr_dv2 gdouble2;
+typedef __attribute__((address_space(3))) double ldouble;
+#else
+typedef double gdouble;
+typedef char gchar;
+typedef sbr_dv2 gdouble2;
+typedef double ldouble;
+#endif
 struct BView {
-    double* p; // ws + (group·5 + slot)·cap·64 + lane·16
+    gdouble* p; // ws + (group·5 + slot)·cap·64 + lane·16
     // 32-bit byte offset (a group's buffer is < 4 GiB): one shift-and-or pair, no sign extension
-    __device__ __forceinline__ double& operator[](int k) const
+    __device__ __forceinline__ gdouble& operator[](int k) const
     {
         const uint32_t u = (uint32_t)k;
-        return *(double*)((char*)p + (((u >> 4) << 13) | ((u & 15u) << 3)));
+        return *(gdouble*)((gchar*)p + (((u >> 4) << 13) | ((u & 15u) << 3)));
     }
 };
 
@@ -147,12 +167,13 @@ struct Walker {
 __device__ __forceinline__ double2 ld2(BView b, int k)
 {
     const uint32_t u = (uint32_t)k;
-    return *(const double2*)((const char*)b.p + (((u >> 4) << 13) | ((u & 15u) << 3)));
+    const sbr_dv2 v = *(const gdouble2*)((const gchar*)b.p + (((u >> 4) << 13) | ((u & 15u) << 3)));
+    return make_double2(v.x, v.y);
 }
 __device__ __forceinline__ void st2(BView b, int k, double x, double y)
 {
     const uint32_t u = (uint32_t)k;
-    *(double2*)((char*)b.p + (((u >> 4) << 13) | ((u & 15u) << 3))) = make_double2(x, y);
+    *(gdouble2*)((gchar*)b.p + (((u >> 4) << 13) | ((u & 15u) << 3))) = sbr_dv2{x, y};
 }
 
 // Walker with the knot values held beside the knot times: an 8-knot window on a 4-aligned base,
@@ -235,7 +256,7 @@ __device__ __forceinline__ double interp_full(BView t, BView v, int n, double x,
 
 __device__ __forceinline__ BView buf_at(double* ws, int cap, int l, int slot)
 {
-    return BView{ws + ((size_t)(l >> 6) * 5 + (size_t)slot) * (size_t)cap * 64 + (size_t)(l & 63) * 16};
+    return BView{(gdouble*)(ws + ((size_t)(l >> 6) * 5 + (size_t)slot) * (size_t)cap * 64 + (size_t)(l & 63) * 16)};
 }
 __device__ __forceinline__ BView buf(const SocialArgs& a, int l, int slot) { return buf_at(a.ws, a.cap, l, slot); }
 
@@ -549,8 +570,8 @@ struct SocialRhsRing {
     double last_aw;
     bool oob;
     int slow;
-    double* rt; // this lane's ring: rt[s * 64] = t[k] for the knot k ≡ s (mod 32) held
-    double* rv;
+    ldouble* rt; // this lane's ring: rt[s * 64] = t[k] for the knot k ≡ s (mod 32) held
+    ldouble* rv;
     int rb;     // first knot held (a multiple of 16)
     double pf_t = 0.0, pf_v = 0.0;
     __device__ __forceinline__ bool in_ring(int j) const { return j >= rb && j + 1 < rb + kRing; }
@@ -560,9 +581,9 @@ struct SocialRhsRing {
     __device__ __forceinline__ void fill_line(int base)
     {
         if (base >= n) return;
-        const double2* lt = (const double2*)((const char*)to.p + ((size_t)(base >> 4) << 13));
-        const double2* lv = (const double2*)((const char*)vo.p + ((size_t)(base >> 4) << 13));
-        double2 a[8], b[8];
+        const gdouble2* lt = (const gdouble2*)((const gchar*)to.p + ((size_t)(base >> 4) << 13));
+        const gdouble2* lv = (const gdouble2*)((const gchar*)vo.p + ((size_t)(base >> 4) << 13));
+        sbr_dv2 a[8], b[8];
 #pragma unroll
         for (int q = 0; q < 8; q++) { a[q] = lt[q]; b[q] = lv[q]; }
         const int s0 = base & (kRing - 1);
@@ -612,8 +633,8 @@ struct SocialRhsRing {
         oob = false;
         last_aw = 0.0;
         const int lane = (int)(threadIdx.x & 63);
-        rt = ring + lane;
-        rv = ring + kRing * 64 + lane;
+        rt = (ldouble*)ring + lane;
+        rv = (ldouble*)ring + kRing * 64 + lane;
         rb = 0;
         fill_line(0);
         fill_line(16);
@@ -909,7 +930,7 @@ __device__ __forceinline__ bool social_iterate(const SocialArgs& a, int l, int i
     const int b = (int)(g / a.n_u);
     const int ju = (int)(g % a.n_u);
     const double BETA = a.beta[b], ETA = a.eta[b], U = a.u[ju];
-    const double* __restrict__ CMP = a.cmp + (size_t)b * a.n_cmp;
+    const gdouble* __restrict__ CMP = (const gdouble*)(a.cmp + (size_t)b * a.n_cmp);
     const uint32_t P = a.slots[l];
     const int s_to = P & 7, s_vo = (P >> 3) & 7, s_t = (P >> 6) & 7, s_G = (P >> 9) & 7, s_aw = (P >> 12) & 7;
     BView TO = buf(a, l, s_to);
@@ -917,7 +938,7 @@ __device__ __forceinline__ bool social_iterate(const SocialArgs& a, int l, int i
     BView T = buf(a, l, s_t);
     BView Gv = buf(a, l, s_G);
     BView AWO = buf(a, l, s_aw);
-    double* CMPO = a.cmpo + (size_t)l * a.n_cmp;
+    gdouble* CMPO = (gdouble*)(a.cmpo + (size_t)l * a.n_cmp);
     const int n_old = a.n_old[l];
     uint32_t bits = a.bits[l];
     const double xi_old = a.xi_new[l];
