@@ -424,7 +424,7 @@ __global__ __launch_bounds__(64) void learn_hetero_kernel(const double* __restri
 #define SBR_HET_LEARN_WAVE 1 // 0: learn_hetero_kernel (one lane per column, A/B)
 #endif
 #ifndef SBR_HET_LEARN_ROWS
-#define SBR_HET_LEARN_ROWS 4 // columns per learning wave: 4 = learn_hetero_wave4_kernel (16-lane rows), 1 = one per wave
+#define SBR_HET_LEARN_ROWS 1 // columns per learning wave: 1 = one per wave; 4 = learn_hetero_wave4_kernel (16-lane rows, bitwise but slower: 42.4 -> 45.2 ms, profiles/experiments/r04_s_*)
 #endif
 #ifndef SBR_HET_DIVRCP
 #define SBR_HET_DIVRCP 0 // LU back substitutions by refined pivot reciprocals (A/B)

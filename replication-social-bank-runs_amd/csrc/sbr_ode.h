@@ -261,6 +261,11 @@ struct Tsit5Tab<false> : Tsit5Lits {};
 // rejected independently, so the step bookkeeping is branch-free (state updates by
 // select, knots written unconditionally at the fill index): a divergent accept / reject
 // branch would run both sides and serialise exec-mask updates on the lane's chain.
+template <class S, class = void>
+struct accept_first : std::false_type {};
+template <class S>
+struct accept_first<S, std::void_t<decltype(S::kAcceptFirst)>> : std::bool_constant<S::kAcceptFirst> {};
+
 template <class Sys, class Sink>
 __device__ __forceinline__ void ode_scalar(Sys& f, Sink& sink, double T1, double x0, double rtol, double atol,
                                            int64_t maxiters, OdeOut& o)
@@ -353,8 +358,12 @@ __device__ __forceinline__ void ode_scalar(Sys& f, Sink& sink, double T1, double
         const double dtn = pc.next_dt(EEst, dt, dtmax, dtmin, acc, ok);
         const double tdt = t + dt;
         const double tn = fabs(tdt - T1) < snap ? T1 : tdt; // fixed_t_for_floatingpoint_error!
+        // a Sys whose accepted() issues loads (SocialRhsRing's ring refill) takes it before the
+        // knot's stores, so that the refill's wait does not drain them (the lookups are exact
+        // whatever the window's position: the same knot values either way)
+        if constexpr (accept_first<Sys>::value) { if (acc) f.accepted(tn); }
         const bool go = sink.step(acc, t, tn, dt, x, u, K, tn == tdt);
-        if (acc) f.accepted(tn);
+        if constexpr (!accept_first<Sys>::value) { if (acc) f.accepted(tn); }
         t = acc ? tn : t;
         x = acc ? u : x;
         k1 = acc ? fnew : k1;

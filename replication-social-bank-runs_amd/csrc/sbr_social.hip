@@ -163,6 +163,21 @@ struct Walker {
 #define SBR_SOCIAL_PAIRS 1 // streaming passes and damping walkers load knot pairs (16 B per lane per request)
 #endif
 
+#ifndef SBR_SOCIAL_FBWAIT
+#define SBR_SOCIAL_FBWAIT 1 // ring misses wait for their own global loads inside the miss branch (A/B)
+#endif
+// A ring miss loads its operands from global memory inside a divergent branch.  Unless the
+// branch waits for them itself, the wait lands where the ring path writes the same registers,
+// and it is a vmcnt wait that also drains every older store and refill load of the wave — on
+// every lookup, whether or not any lane missed.  vmcnt(0) here (expcnt/lgkmcnt left alone)
+// is paid only when a lane misses.
+__device__ __forceinline__ void ring_miss_wait()
+{
+#if SBR_SOCIAL_FBWAIT
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+#endif
+}
+
 // knots k, k+1 (k even) of one lane in one 16-byte load: a pair never straddles a 16-knot line
 __device__ __forceinline__ double2 ld2(BView b, int k)
 {
@@ -241,6 +256,7 @@ struct WalkerV {
             v0 = sel4(vw, r); v1 = sel4(vw + 1, r);
         } else { // x == t_{n-1} on a window that starts at n−1
             t0 = t[j]; t1 = t[j + 1]; v0 = v[j]; v1 = v[j + 1];
+            ring_miss_wait();
         }
         const double d = (x - t0) / (t1 - t0);
         return v0 * (1.0 - d) + v1 * d;
@@ -546,7 +562,14 @@ struct SocialRhs {
 #define SBR_SOCIAL_RING 1 // multi-point waves read AW_{n−1} through a per-lane LDS ring (SocialRhsRing)
 #endif
 constexpr int kRing = 32;                                          // knots per lane: two 16-knot lines
-constexpr size_t kRingLdsBytes = (size_t)2 * kRing * 64 * sizeof(double); // t and v, 64 lanes: 32 KiB
+#ifndef SBR_SOCIAL_RING_LANES
+#define SBR_SOCIAL_RING_LANES 32 // lanes a multi-point wave may use (the launch makes L <= this)
+#endif
+#ifndef SBR_SOCIAL_MINW
+#define SBR_SOCIAL_MINW 2 // waves per SIMD the iterate kernel is compiled for (register budget)
+#endif
+constexpr int kRingLanes = SBR_SOCIAL_RING_LANES;
+constexpr size_t kRingLdsBytes = (size_t)2 * kRing * kRingLanes * sizeof(double); // t and v: 16 KiB at 32 lanes
 
 // SocialRhs for a wave that runs many points (the bulk of a sweep: up to 32 per wave).  There
 // every lane streams its own knot lines, so each operand load of a stage lookup is a separate
@@ -570,13 +593,17 @@ struct SocialRhsRing {
     double last_aw;
     bool oob;
     int slow;
-    ldouble* rt; // this lane's ring: rt[s * 64] = t[k] for the knot k ≡ s (mod 32) held
+    ldouble* rt; // this lane's ring: rt[s * kRingLanes] = t[k] for the knot k ≡ s (mod 32) held
     ldouble* rv;
     int rb;     // first knot held (a multiple of 16)
     double pf_t = 0.0, pf_v = 0.0;
+#ifndef SBR_SOCIAL_ACCEPT_FIRST
+#define SBR_SOCIAL_ACCEPT_FIRST 1
+#endif
+    static constexpr bool kAcceptFirst = SBR_SOCIAL_ACCEPT_FIRST != 0; // refill before the knot's stores (ode_scalar)
     __device__ __forceinline__ bool in_ring(int j) const { return j >= rb && j + 1 < rb + kRing; }
-    __device__ __forceinline__ double RT(int j) const { return rt[(j & (kRing - 1)) * 64]; }
-    __device__ __forceinline__ double RV(int j) const { return rv[(j & (kRing - 1)) * 64]; }
+    __device__ __forceinline__ double RT(int j) const { return rt[(j & (kRing - 1)) * kRingLanes]; }
+    __device__ __forceinline__ double RV(int j) const { return rv[(j & (kRing - 1)) * kRingLanes]; }
     // knots [base, base + 16) into their slots (base a multiple of 16; nothing past the grid)
     __device__ __forceinline__ void fill_line(int base)
     {
@@ -589,8 +616,8 @@ struct SocialRhsRing {
         const int s0 = base & (kRing - 1);
 #pragma unroll
         for (int q = 0; q < 8; q++) {
-            rt[(s0 + 2 * q) * 64] = a[q].x; rt[(s0 + 2 * q + 1) * 64] = a[q].y;
-            rv[(s0 + 2 * q) * 64] = b[q].x; rv[(s0 + 2 * q + 1) * 64] = b[q].y;
+            rt[(s0 + 2 * q) * kRingLanes] = a[q].x; rt[(s0 + 2 * q + 1) * kRingLanes] = a[q].y;
+            rv[(s0 + 2 * q) * kRingLanes] = b[q].x; rv[(s0 + 2 * q + 1) * kRingLanes] = b[q].y;
         }
     }
     // Win8's refill with the ring's copies where it holds them
@@ -602,7 +629,9 @@ struct SocialRhsRing {
         for (int k = 0; k < 8; k++) {
             const int i = base + k;
             const int ic = i < last ? i : last;
-            const double v = (ic >= rb && ic < rb + kRing) ? RT(ic) : to[ic];
+            double v;
+            if (ic >= rb && ic < rb + kRing) v = RT(ic);
+            else { v = to[ic]; ring_miss_wait(); }
             w.tw[k] = (i < n) ? v : (double)INFINITY;
         }
     }
@@ -619,7 +648,7 @@ struct SocialRhsRing {
         j = j < 0 ? 0 : j;
         double t0, t1, v0, v1;
         if (in_ring(j)) { t0 = RT(j); t1 = RT(j + 1); v0 = RV(j); v1 = RV(j + 1); }
-        else { t0 = to[j]; t1 = to[j + 1]; v0 = vo[j]; v1 = vo[j + 1]; }
+        else { t0 = to[j]; t1 = to[j + 1]; v0 = vo[j]; v1 = vo[j + 1]; ring_miss_wait(); }
         const double d = (x - t0) / (t1 - t0);
         const double r = v0 * (1.0 - d) + v1 * d;
         return in ? r : (double)NAN;
@@ -634,7 +663,7 @@ struct SocialRhsRing {
         last_aw = 0.0;
         const int lane = (int)(threadIdx.x & 63);
         rt = (ldouble*)ring + lane;
-        rv = (ldouble*)ring + kRing * 64 + lane;
+        rv = (ldouble*)ring + kRing * kRingLanes + lane;
         rb = 0;
         fill_line(0);
         fill_line(16);
@@ -687,7 +716,7 @@ struct SocialRhsRing {
         j = j > n - 2 ? n - 2 : (j < 0 ? 0 : j);
         double t0, t1, v0, v1;
         if (in_ring(j)) { t0 = RT(j); t1 = RT(j + 1); v0 = RV(j); v1 = RV(j + 1); }
-        else { t0 = to[j]; t1 = to[j + 1]; v0 = vo[j]; v1 = vo[j + 1]; }
+        else { t0 = to[j]; t1 = to[j + 1]; v0 = vo[j]; v1 = vo[j + 1]; ring_miss_wait(); }
         const double d = (t - t0) / (t1 - t0);
         const double a = v0 * (1.0 - d) + v1 * d;
         const double rr = 1.0 / (t1 - t0);
@@ -1401,16 +1430,19 @@ __device__ __forceinline__ bool social_iterate(const SocialArgs& a, int l, int i
 // picked up here or by the next launch; either way it redoes that iterate).
 // args[0]: the main worklist's arguments, args[1]: the pool's (n_pts = 0: none),
 // in device memory so that the wave-uniform choice between them stays scalar loads.
+static_assert(!SBR_SOCIAL_RING || kRingLanes == 64 || SBR_SOCIAL_COOP,
+              "a ring narrower than the wave needs the one-point-per-wave pool path");
 #ifndef SBR_SOCIAL_WAVES
-#define SBR_SOCIAL_WAVES 1024 // A/B: 0 = dense waves (64 worklist entries each, the round-1 layout)
+#define SBR_SOCIAL_WAVES 2048 // two waves per SIMD (A/B: 1024 = one; 0 = dense waves of 64 entries, the round-1 layout)
 #endif
+static_assert(SBR_SOCIAL_WAVES != 0 || !SBR_SOCIAL_RING || kRingLanes == 64, "dense waves use all 64 lanes of the ring");
 // Main blocks (one wave each) spread the live worklist over all `nbs` of them: L = ⌈live/nbs⌉
 // consecutive entries per wave (L ≤ 64), lanes ≥ L idle.  A fixed-point lane's RK step is a
 // serial chain whose memory side grows with the wave's active lanes (each lane streams its own
 // knot lines: a wave load touches one line per active lane), so as points retire the
 // survivors run in ever sparser waves, down to one per wave — and with nbs = one wave per
 // SIMD the bulk uses every SIMD instead of half of them.
-__global__ __launch_bounds__(64) void social_iter_kernel(const SocialArgs* __restrict__ args, int iter_arg,
+__global__ __launch_bounds__(64, SBR_SOCIAL_MINW) void social_iter_kernel(const SocialArgs* __restrict__ args, int iter_arg,
                                                          int n_inner, const int32_t* __restrict__ work,
                                                          const int32_t* __restrict__ count, int nbs)
 {
@@ -1520,7 +1552,7 @@ hipError_t launch_social_iter(const SocialArgs& a, const SocialArgs& p, const So
 {
     // main blocks: one wave per SIMD of the MI355X (4 × 256), at least one wave per 64 points
     // and no more than one per point
-    int nbs = (a.n_pts + 63) / 64;
+    int nbs = (a.n_pts + kRingLanes - 1) / kRingLanes; // L = ⌈live / nbs⌉ <= kRingLanes (the ring's lanes)
     nbs = nbs > SBR_SOCIAL_WAVES ? nbs : SBR_SOCIAL_WAVES;
     nbs = nbs < a.n_pts ? nbs : (a.n_pts > 0 ? a.n_pts : 1);
     const int pool_waves = SBR_SOCIAL_COOP ? p.n_pts : (p.n_pts + 63) / 64;

@@ -26,7 +26,7 @@ for s in ${STEPS:-tests smoke bench single}; do
     ready) run ready 300 python -u bench.py --no-pipeline --ready --steps 20 --warmup 2 --no-cpu-baseline ;;
     prof) run prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
     profsingle) run profsingle 300 rocprofv3 --kernel-trace --stats -d "$OUT/profsingle" -o run --output-format csv -- python3 bench.py --no-pipeline --steps 20 --warmup 2 --no-cpu-baseline ;;
-    hetero) run hetero 600 python -u bench.py --workload hetero --steps 10 --warmup 2 --phases ;;
+    hetero) run hetero 600 python -u bench.py --workload hetero --steps 20 --warmup 2 --phases ;;
     interest) run interest 600 python -u bench.py --workload interest --steps 3 --warmup 1 ;;
     social) run social 600 python -u bench.py --workload social --steps 1 --warmup 0 ;;
     config1) run config1 300 python -u bench.py --workload config1 --steps 50 --warmup 3 ;;
