@@ -563,13 +563,14 @@ struct SocialRhs {
 #endif
 constexpr int kRing = 32;                                          // knots per lane: two 16-knot lines
 #ifndef SBR_SOCIAL_RING_LANES
-#define SBR_SOCIAL_RING_LANES 32 // lanes a multi-point wave may use (the launch makes L <= this)
+#define SBR_SOCIAL_RING_LANES 64 // lanes a multi-point wave may use (the launch makes L <= this)
 #endif
 #ifndef SBR_SOCIAL_MINW
-#define SBR_SOCIAL_MINW 2 // waves per SIMD the iterate kernel is compiled for (register budget)
+#define SBR_SOCIAL_MINW 1 // waves per SIMD the iterate kernel is compiled for (A/B: 2 with 2048 waves of
+                          // 16 points and 32-lane rings spilled 84 B/lane and was slower, 10.98 -> 11.64 s: r04_u)
 #endif
 constexpr int kRingLanes = SBR_SOCIAL_RING_LANES;
-constexpr size_t kRingLdsBytes = (size_t)2 * kRing * kRingLanes * sizeof(double); // t and v: 16 KiB at 32 lanes
+constexpr size_t kRingLdsBytes = (size_t)2 * kRing * kRingLanes * sizeof(double); // t and v: 32 KiB at 64 lanes
 
 // SocialRhs for a wave that runs many points (the bulk of a sweep: up to 32 per wave).  There
 // every lane streams its own knot lines, so each operand load of a stage lookup is a separate
@@ -1433,7 +1434,7 @@ __device__ __forceinline__ bool social_iterate(const SocialArgs& a, int l, int i
 static_assert(!SBR_SOCIAL_RING || kRingLanes == 64 || SBR_SOCIAL_COOP,
               "a ring narrower than the wave needs the one-point-per-wave pool path");
 #ifndef SBR_SOCIAL_WAVES
-#define SBR_SOCIAL_WAVES 2048 // two waves per SIMD (A/B: 1024 = one; 0 = dense waves of 64 entries, the round-1 layout)
+#define SBR_SOCIAL_WAVES 1024 // one wave per SIMD (A/B: 2048 with SBR_SOCIAL_MINW 2; 0 = dense waves, the round-1 layout)
 #endif
 static_assert(SBR_SOCIAL_WAVES != 0 || !SBR_SOCIAL_RING || kRingLanes == 64, "dense waves use all 64 lanes of the ring");
 // Main blocks (one wave each) spread the live worklist over all `nbs` of them: L = ⌈live/nbs⌉

@@ -121,14 +121,28 @@ class Engine:
     # ------------------------------------------------------------------ sweeps
     def sweep_baseline(self, grid: BaselineGrid, early_exit: int = 0, max_iters: int = 100,
                        knot_capacity: int = 65536, with_iters: bool = True, exhaustive: bool = False,
-                       flags: int = 0) -> dict:
+                       flags: int = 0, out: dict | None = None) -> dict:
         """Every (β, u) of ``grid`` through learning → HR → buffers → bisection
         → AW_max.  Returns [n_beta, n_u] arrays (row i = β_i).  ``early_exit=5``
-        applies the reference's 5-consecutive-no-run rule as a post-pass."""
+        applies the reference's 5-consecutive-no-run rule as a post-pass.  ``out``: the
+        caller's result arrays (as the reference's scripts fill matrices they allocated
+        once), reused across calls; float64 RESULT_FIELDS, uint32 ``status``, optional int32
+        ``iters``, each C-contiguous with n_beta·n_u elements."""
         nb, nu = grid.shape
-        out = {k: np.empty(nb * nu) for k in RESULT_FIELDS}
-        out["status"] = np.empty(nb * nu, np.uint32)
-        out["iters"] = np.empty(nb * nu, np.int32) if with_iters else None
+        if out is None:
+            out = {k: np.empty(nb * nu) for k in RESULT_FIELDS}
+            out["status"] = np.empty(nb * nu, np.uint32)
+            out["iters"] = np.empty(nb * nu, np.int32) if with_iters else None
+        else:
+            want = {**{k: np.float64 for k in RESULT_FIELDS}, "status": np.uint32, "iters": np.int32}
+            for k, dt in want.items():
+                v = out.get(k)
+                if v is None and k == "iters":
+                    continue
+                if (not isinstance(v, np.ndarray) or v.dtype != dt or v.size != nb * nu
+                        or not v.flags["C_CONTIGUOUS"]):
+                    raise ArgumentError(f"out[{k!r}] must be a C-contiguous {np.dtype(dt).name} array of {nb * nu}")
+            out = {k: out[k].reshape(-1) if out.get(k) is not None else None for k in want}
         soa = _lib.ResultSoA(*[_ptr(out[k]) for k in (*RESULT_FIELDS, "status", "iters")])
         opts = _lib.default_opts(early_exit_nan_run=early_exit, bisect_max_iters=max_iters,
                                  knot_capacity=knot_capacity,

@@ -72,6 +72,29 @@ def test_fig5_500_sweep_bitwise(engine, oracle, golden):
     assert run.sum() == golden("fig5_prefix.json")["n500"]["total"]
 
 
+def test_sweep_into_caller_arrays(engine, oracle):
+    """sweep_baseline(out=...) fills the caller's arrays in place (the config-2 bench path),
+    call after call, with the oracle's bits; wrong dtypes or sizes are refused before the call."""
+    grid = sbr.fig5_grid(96)
+    n = grid.n_points
+    host = {f: np.full(n, -1.0) for f in FIELDS}
+    host["status"] = np.zeros(n, np.uint32)
+    host["iters"] = np.zeros(n, np.int32)
+    o = _oracle_sweep(oracle, grid)
+    for _ in range(2):
+        r = engine.sweep_baseline(grid, out=host)
+        assert np.shares_memory(r["xi"], host["xi"])
+        for f in FIELDS:
+            assert_bitwise(host[f].reshape(o[f].shape), o[f], f)
+        assert np.array_equal(host["status"].reshape(o["status"].shape), o["status"])
+        host["xi"][:] = 0.0
+    bad = dict(host, status=np.zeros(n, np.int64))
+    with pytest.raises(sbr.ArgumentError):
+        engine.sweep_baseline(grid, out=bad)
+    with pytest.raises(sbr.ArgumentError):
+        engine.sweep_baseline(grid, out=dict(host, xi=np.zeros(n - 1)))
+
+
 def test_fig4_sweep_bitwise_and_boundary(engine, oracle, golden):
     grid = sbr.fig4_grid(5000)
     g = engine.sweep_baseline(grid, early_exit=5)
