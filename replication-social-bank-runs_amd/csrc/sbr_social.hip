@@ -821,6 +821,7 @@ struct SocialRhsCoop {
             t0 = lane_d(wt, k); t1 = lane_d(wt, k + 1); v0 = lane_d(wv, k); v1 = lane_d(wv, k + 1);
         } else {
             t0 = to[j]; t1 = to[j + 1]; v0 = vo[j]; v1 = vo[j + 1];
+            ring_miss_wait(); // not at the join: there it would drain the knot stores every lookup
         }
         const double d = (x - t0) / (t1 - t0);
         return v0 * (1.0 - d) + v1 * d;
@@ -879,6 +880,7 @@ struct SocialRhsCoop {
     }
     static constexpr bool kFsalExact = false;
     static constexpr bool kPinTableau = false;
+    static constexpr bool kAcceptFirst = SBR_SOCIAL_ACCEPT_FIRST != 0; // the refill's loads ahead of the knot stores
 };
 
 }  // namespace

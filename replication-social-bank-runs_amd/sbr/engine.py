@@ -76,6 +76,23 @@ def _out_ptrs(out: dict, fields, n: int, required=()):
     return ptrs
 
 
+def host_result_views(out: dict, n: int) -> dict:
+    """Flat views of a caller's host result arrays for sbr_sweep_baseline: float64 RESULT_FIELDS,
+    uint32 ``status`` and optional int32 ``iters``, each C-contiguous with ``n`` elements.
+    Anything else raises ArgumentError before the C call (no write past a caller's array)."""
+    want = {**{k: np.float64 for k in RESULT_FIELDS}, "status": np.uint32, "iters": np.int32}
+    views = {}
+    for k, dt in want.items():
+        v = out.get(k)
+        if v is None and k == "iters":
+            views[k] = None
+            continue
+        if not isinstance(v, np.ndarray) or v.dtype != dt or v.size != n or not v.flags["C_CONTIGUOUS"]:
+            raise ArgumentError(f"out[{k!r}] must be a C-contiguous {np.dtype(dt).name} array of {n}")
+        views[k] = v.reshape(-1)
+    return views
+
+
 class Engine:
     """One libsbr context: one HIP device (``device``), or — with ``n_gpus`` /
     ``devices`` — an n-device context whose host-pointer sweeps fan out over the GPUs
@@ -134,15 +151,7 @@ class Engine:
             out["status"] = np.empty(nb * nu, np.uint32)
             out["iters"] = np.empty(nb * nu, np.int32) if with_iters else None
         else:
-            want = {**{k: np.float64 for k in RESULT_FIELDS}, "status": np.uint32, "iters": np.int32}
-            for k, dt in want.items():
-                v = out.get(k)
-                if v is None and k == "iters":
-                    continue
-                if (not isinstance(v, np.ndarray) or v.dtype != dt or v.size != nb * nu
-                        or not v.flags["C_CONTIGUOUS"]):
-                    raise ArgumentError(f"out[{k!r}] must be a C-contiguous {np.dtype(dt).name} array of {nb * nu}")
-            out = {k: out[k].reshape(-1) if out.get(k) is not None else None for k in want}
+            out = host_result_views(out, nb * nu)
         soa = _lib.ResultSoA(*[_ptr(out[k]) for k in (*RESULT_FIELDS, "status", "iters")])
         opts = _lib.default_opts(early_exit_nan_run=early_exit, bisect_max_iters=max_iters,
                                  knot_capacity=knot_capacity,

@@ -71,3 +71,22 @@ def test_interest_parameters_mirror_reference_checks():
     assert m2.economic.eta == 15.0 and m2.learning.tspan == (0.0, 30.0)  # carried, as in the reference
     with pytest.raises(TypeError):
         sbr.ModelParametersInterest.modify(m, gamma=1.0)
+
+
+def test_host_result_views_checks_caller_arrays():
+    """sweep_baseline(out=...) hands the caller's arrays to the C ABI only when every field has
+    the dtype, size and layout the call writes (engine.host_result_views)."""
+    from sbr.engine import RESULT_FIELDS, host_result_views
+    n = 12
+    out = {k: np.zeros((3, 4)) for k in RESULT_FIELDS}
+    out["status"] = np.zeros(n, np.uint32)
+    v = host_result_views(out, n)
+    assert v["iters"] is None and v["xi"].shape == (n,) and np.shares_memory(v["xi"], out["xi"])
+    out["iters"] = np.zeros(n, np.int32)
+    assert host_result_views(out, n)["iters"].base is out["iters"] or np.shares_memory(
+        host_result_views(out, n)["iters"], out["iters"])
+    for bad in (dict(out, status=np.zeros(n, np.int32)), dict(out, xi=np.zeros(n + 1)),
+                dict(out, tol=np.zeros((4, 6))[:, ::2]), dict(out, aw_max=None),
+                dict(out, iters=np.zeros(n, np.int64))):
+        with pytest.raises(ArgumentError):
+            host_result_views(bad, n)
