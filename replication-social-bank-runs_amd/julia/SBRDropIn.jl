@@ -137,39 +137,41 @@ function solve_equilibrium_baseline(learning_results::LearningResults, econ::Eco
                        time() - solve_start, r.tolerance, aw_engine)
 end
 
-# solver.jl:153-185 (host; plotting.jl:62-132 evaluates it on the learning PDF)
+# hazard_rate (solver.jl:153-185) for the host-side plots (plotting.jl:62-132 calls it on the
+# learning PDF).  The τ̄ grid: the PDF's knots up to η with η appended unless it is the last
+# one, or an explicit grid's points up to η with η always appended.  Then the running
+# trapezoid of w(τ) = e^{aτ}·pdf(τ) from the first point, and the hazard at each point: its
+# numerator (p·e^{aτ})·pdf(τ) over p·∫₀^τ w + (1 − p)·∫₀^η w.  Every product and sum is formed
+# in the order the engine's hazard kernels use (the same values to the bit).
 function hazard_rate(p, a, learning_pdf, η; grid = nothing)
-    if isnothing(grid)
-        τ_bar = learning_pdf.itp.knots[1][learning_pdf.itp.knots[1] .<= η]
-        if length(τ_bar) == 0 || τ_bar[end] != η
-            push!(τ_bar, η)
-        end
-    else
-        τ_bar = grid[grid .<= η]
-        push!(τ_bar, η)
+    pts = isnothing(grid) ? learning_pdf.itp.knots[1] : grid
+    τs = Float64[τ for τ in pts if τ <= η]
+    (!isnothing(grid) || isempty(τs) || τs[end] != η) && push!(τs, η)
+    m = length(τs)
+    w = [exp(a * τ) * learning_pdf(τ) for τ in τs]
+    acc = zeros(m)
+    for i in 2:m
+        acc[i] = acc[i-1] + 0.5 * (w[i-1] + w[i]) * (τs[i] - τs[i-1])
     end
-    eg(t) = exp(a * t) * learning_pdf(t)
-    int_0_τ_bar = zeros(length(τ_bar))
-    for i in 2:length(τ_bar)
-        int_0_τ_bar[i] = int_0_τ_bar[i-1] + 0.5 * (eg(τ_bar[i-1]) + eg(τ_bar[i])) * (τ_bar[i] - τ_bar[i-1])
-    end
-    int_0_η = int_0_τ_bar[end]
-    return LinearInterpolation(τ_bar,
-        (p .* exp.(a .* τ_bar) .* learning_pdf.(τ_bar)) ./ (p .* int_0_τ_bar .+ (1 - p) .* int_0_η))
+    hr = [(p * exp(a * τs[i]) * learning_pdf(τs[i])) / (p * acc[i] + (1 - p) * acc[m]) for i in 1:m]
+    return LinearInterpolation(τs, hr)
 end
 
-# solver.jl:495-532 (host; AW_OUT / AW_IN for plot_equilibrium)
+# get_AW (solver.jl:495-532) for plot_equilibrium: on HR's knots, the CDF mass that has
+# entered (IN) and left (OUT) the withdrawal window by t, each the learning CDF at
+# max(t − ξ + τ_con, 0) and zero where t − ξ + τ_con < 0 (τ_con = min(τ_UNC, ξ), with the
+# reference's ≥ / > tie rules), and AW_cum = (OUT − IN) + G(0).  All IN values are evaluated
+# before all OUT values, as in the reference (the same BoundsError, if any, comes first).
 function get_AW(ξ, τ_bar_IN_UNC, τ_bar_OUT_UNC, HR, learning_cdf)
-    t_grid = HR.itp.knots[1]
-    τ_bar_IN_CON = τ_bar_IN_UNC >= ξ ? ξ : τ_bar_IN_UNC
-    τ_bar_OUT_CON = τ_bar_OUT_UNC > ξ ? ξ : τ_bar_OUT_UNC
-    grid_IN_trunc = ifelse.(t_grid .- ξ .+ τ_bar_IN_CON .> 0, t_grid .- ξ .+ τ_bar_IN_CON, 0)
-    AW_IN = ifelse.(t_grid .- ξ .+ τ_bar_IN_CON .>= 0, learning_cdf(grid_IN_trunc), 0)
-    grid_OUT_trunc = ifelse.(t_grid .- ξ .+ τ_bar_OUT_CON .> 0, t_grid .- ξ .+ τ_bar_OUT_CON, 0)
-    AW_OUT = ifelse.(t_grid .- ξ .+ τ_bar_OUT_CON .>= 0, learning_cdf(grid_OUT_trunc), 0)
-    AW_cum = AW_OUT .- AW_IN
-    AW_cum .+= learning_cdf(0)
-    return LinearInterpolation(t_grid, AW_cum), LinearInterpolation(t_grid, AW_OUT), LinearInterpolation(t_grid, AW_IN)
+    ts = HR.itp.knots[1]
+    c_in = τ_bar_IN_UNC >= ξ ? ξ : τ_bar_IN_UNC
+    c_out = τ_bar_OUT_UNC > ξ ? ξ : τ_bar_OUT_UNC
+    window(t, c) = (s = (t - ξ) + c; g = learning_cdf(s > 0 ? s : 0); s >= 0 ? g : zero(g))
+    aw_in = [window(t, c_in) for t in ts]
+    aw_out = [window(t, c_out) for t in ts]
+    g0 = learning_cdf(0)
+    aw_cum = [(aw_out[i] - aw_in[i]) + g0 for i in eachindex(ts)]
+    return LinearInterpolation(ts, aw_cum), LinearInterpolation(ts, aw_out), LinearInterpolation(ts, aw_in)
 end
 
 # solver.jl:553-576 — the engine's get_AW paths on the HR grid and its AW_max (the same maximum
