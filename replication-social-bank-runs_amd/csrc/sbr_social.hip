@@ -561,16 +561,19 @@ struct SocialRhs {
 #ifndef SBR_SOCIAL_RING
 #define SBR_SOCIAL_RING 1 // multi-point waves read AW_{n−1} through a per-lane LDS ring (SocialRhsRing)
 #endif
-constexpr int kRing = 32;                                          // knots per lane: two 16-knot lines
+#ifndef SBR_SOCIAL_RING4
+#define SBR_SOCIAL_RING4 1 // four 16-knot lines per lane (32 lanes) and refills batched every 8 steps
+#endif
+constexpr int kRing = SBR_SOCIAL_RING4 ? 64 : 32; // knots per lane: four (two) 16-knot lines
 #ifndef SBR_SOCIAL_RING_LANES
-#define SBR_SOCIAL_RING_LANES 64 // lanes a multi-point wave may use (the launch makes L <= this)
+#define SBR_SOCIAL_RING_LANES (SBR_SOCIAL_RING4 ? 32 : 64) // lanes a multi-point wave may use (the launch makes L <= this)
 #endif
 #ifndef SBR_SOCIAL_MINW
 #define SBR_SOCIAL_MINW 1 // waves per SIMD the iterate kernel is compiled for (A/B: 2 with 2048 waves of
                           // 16 points and 32-lane rings spilled 84 B/lane and was slower, 10.98 -> 11.64 s: r04_u)
 #endif
 constexpr int kRingLanes = SBR_SOCIAL_RING_LANES;
-constexpr size_t kRingLdsBytes = (size_t)2 * kRing * kRingLanes * sizeof(double); // t and v: 32 KiB at 64 lanes
+constexpr size_t kRingLdsBytes = (size_t)2 * kRing * kRingLanes * sizeof(double); // t and v: 32 KiB either way
 
 // SocialRhs for a wave that runs many points (the bulk of a sweep: up to 32 per wave).  There
 // every lane streams its own knot lines, so each operand load of a stage lookup is a separate
@@ -597,6 +600,7 @@ struct SocialRhsRing {
     ldouble* rt; // this lane's ring: rt[s * kRingLanes] = t[k] for the knot k ≡ s (mod 32) held
     ldouble* rv;
     int rb;     // first knot held (a multiple of 16)
+    int tick = 0; // attempted Tsit5 steps (prepare calls): equal across the live lanes of a wave
     double pf_t = 0.0, pf_v = 0.0;
 #ifndef SBR_SOCIAL_ACCEPT_FIRST
 #define SBR_SOCIAL_ACCEPT_FIRST 1
@@ -666,8 +670,8 @@ struct SocialRhsRing {
         rt = (ldouble*)ring + lane;
         rv = (ldouble*)ring + kRing * kRingLanes + lane;
         rb = 0;
-        fill_line(0);
-        fill_line(16);
+#pragma unroll
+        for (int b = 0; b < kRing; b += 16) fill_line(b);
         w.t = to;
         w.n = n;
         wload(0);
@@ -685,6 +689,7 @@ struct SocialRhsRing {
     }
     __device__ __forceinline__ void prepare(double t, double dt)
     {
+        tick++;
         const double xs[5] = {fma(C1, dt, t), fma(C2, dt, t), fma(C3, dt, t), fma(C4, dt, t), t + dt};
         int js[5];
         bool in[5];
@@ -729,6 +734,27 @@ struct SocialRhsRing {
     {
         if (n >= 2 && t >= tfirst && t <= tlast) {
             const int j = find_advance(t);
+#if SBR_SOCIAL_RING4
+            // Four lines: a lane whose bracket has passed rb + 20 replaces its oldest lines
+            // (wb > j − 4 >= the new rb), but only on every 8th attempted step — the same step
+            // for every lane of the wave, so one wave-wide wait on the refill loads serves all
+            // the lanes due — unless fewer than 24 knots are left ahead of the bracket.
+            if (j + 2 >= rb + kRing) { // past the ring: re-seat it around j
+                rb = ((j - 4) >> 4) << 4;
+#pragma unroll
+                for (int b = 0; b < kRing; b += 16) fill_line(rb + b);
+            } else if (j - rb >= 20 && ((tick & 7) == 0 || j - rb >= kRing - 24)) {
+                for (int k = 0; k < 3 && j - rb >= 20; k++) {
+                    fill_line(rb + kRing);
+                    rb += 16;
+                }
+                slow += (pf_t == -1.0 || pf_v == -2.0) ? 1 : 0;
+                const int q = rb + kRing + 16 < n ? rb + kRing + 16 : n - 1;
+                pf_t = to[q];
+                pf_v = vo[q];
+            }
+            if (SBR_SOCIAL_RING4) return;
+#endif
             if (j - rb >= 20) {
                 if (j - rb >= 20 + 16) { // a step past the whole ring: re-seat it around j
                     rb = ((j - 4) >> 4) << 4;
