@@ -64,6 +64,7 @@ for s in ${STEPS:-tests smoke bench single}; do
     dropin) run dropin 600 python -u bench.py --workload dropin --steps 30 ;;
     knotsprobe) run knotsprobe 300 python -u tools/knots_probe.py 2000 && run knotsprof 300 rocprofv3 --kernel-trace --stats -d "$OUT/knotsprof" -o run --output-format csv -- python3 tools/knots_probe.py 500 ;;
     dpp) run dpp 60 ./tools/micro/dpp_newbcast ;;
+    drv) run drv 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 ;;
     hetero2) run hetero2 600 python -u bench.py --workload hetero --steps 10 --warmup 2 --phases --no-cpu-baseline ;;
     socprof2) run socprof2 300 python -u bench.py --workload social --steps 1 --warmup 0 --social-max-iter 16 --social-prof --no-cpu-baseline --no-verify ;;
     knots) run knots 600 python -u -m pytest tests/test_gpu_knots.py tests/test_gpu_baseline.py -x -v --timeout 300 --timeout-method thread ${KTESTK:+-k "$KTESTK"} ;;
