@@ -39,6 +39,79 @@ import numpy as np
 REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO / "replication-social-bank-runs_amd"))
 
+
+# ---- N-rank launcher: `python bench.py --gpus N` without a launcher's WORLD_SIZE starts N rank
+# processes itself (one per GPU, as torchrun would), before this process imports torch or libsbr:
+# the parent never initialises HIP; it waits for its children and exits with their status ----
+def launch_plan(argv: list[str], env: dict, port: int) -> list[tuple[list[str], dict]]:
+    """(command, environment) of every rank process for `python bench.py argv`, or [] when this
+    process is itself a rank (a launcher set WORLD_SIZE) or --gpus is 1."""
+    pre = argparse.ArgumentParser(add_help=False)
+    pre.add_argument("--gpus", type=int, default=1)
+    n = pre.parse_known_args(argv)[0].gpus
+    if "WORLD_SIZE" in env or n <= 1:
+        return []
+    plan = []
+    for r in range(n):
+        e = dict(env)
+        e.update(WORLD_SIZE=str(n), RANK=str(r), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(n),
+                 GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        plan.append(([sys.executable, "-u", str(Path(__file__).resolve())] + list(argv), e))
+    return plan
+
+
+def world_of(gpus: int, env=None) -> tuple[int, int, int]:
+    """(world, rank, local rank) of this process; a launcher's WORLD_SIZE must equal --gpus."""
+    env = os.environ if env is None else env
+    world = int(env.get("WORLD_SIZE", "1"))
+    if world != gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {gpus}: refusing a mismatched world")
+    return world, int(env.get("RANK", "0")), int(env.get("LOCAL_RANK", "0"))
+
+
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _launch(argv: list[str]) -> int | None:
+    import signal
+    import subprocess
+    plan = launch_plan(argv, dict(os.environ), _free_port())
+    if not plan:
+        return None
+    procs = [subprocess.Popen(cmd, env=e) for cmd, e in plan]
+    rc = 0
+    try:
+        pending = list(procs)
+        while pending:
+            for p in list(pending):
+                r = p.poll()
+                if r is None:
+                    continue
+                pending.remove(p)
+                if r != 0 and rc == 0:
+                    rc = r if r > 0 else 128 - r
+                    for q in pending:  # one rank failed: the others would wait in a collective
+                        q.send_signal(signal.SIGTERM)
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc
+
+
+if __name__ == "__main__":
+    _rc = _launch(sys.argv[1:])
+    if _rc is not None:
+        sys.exit(_rc)
+
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
@@ -155,6 +228,13 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--n", type=int, default=2048, help="β columns per GPU and u rows")
     ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling: the --n x --n grid (config 3) dealt over the N ranks (default: weak, "
+                         "--n columns per rank)")
+    ap.add_argument("--shard-of", type=int, default=0,
+                    help="one-GPU rehearsal of a strong run: solve the β-column shard that rank --shard-rank of "
+                         "a --shard-of-rank run owns")
+    ap.add_argument("--shard-rank", type=int, default=0)
     ap.add_argument("--no-pipeline", action="store_true",
                     help="one sbr_sweep_baseline_dev call per step (no learning/equilibrium overlap across steps)")
     ap.add_argument("--ready", action="store_true",
@@ -166,7 +246,7 @@ def parse():
     ap.add_argument("--phases", action="store_true",
                     help="also time the equilibrium kernel stopped after each stage (diagnostic flags)")
     ap.add_argument("--workload", choices=("baseline", "social", "hetero", "interest", "config1", "config2",
-                                           "dropin"),
+                                           "dropin", "launchcheck", "multihost"),
                     default="baseline",
                     help="baseline: BASELINE config 3 (the metric); social: config 5 per-GPU share; "
                          "hetero: config 4 (K = 8, 1024x1024 per GPU); interest: the interest-rate "
@@ -191,6 +271,8 @@ def main_small(a):
     ξ, the AW_cum path) — latency per call.
     config2: the Fig 5 500×500 grid (scripts/1_baseline.jl:210-267) — one sbr_sweep_baseline
     call with early_exit_nan_run = 5 — equilibria per second over the whole grid."""
+    if world_of(a.gpus)[0] != 1:
+        raise SystemExit(f"bench.py: --workload {a.workload} is a one-GPU latency line (--gpus 1)")
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     torch.cuda.init()
@@ -199,6 +281,8 @@ def main_small(a):
     import oracle as O  # noqa: E402  (test infrastructure: cpu_baseline leg only)
     if a.workload == "dropin":
         return main_dropin(a, eng, O)
+    if a.workload == "multihost":
+        return main_multihost(a)
     if a.workload == "config1":
         args = dict(beta=1.0, eta=15.0, t_end=30.0, u=0.1, p=0.5, kappa=0.6, lam=0.01)
         for _ in range(max(a.warmup, 1)):
@@ -267,6 +351,39 @@ def main_small(a):
             res["cpu_baseline"] = {"value": npts / c, "unit": "equilibria/s", "cores": cores, "kind": "port",
                                    "host": host_info(), "sample": f"the whole 500x500 grid ({npts} points, every "
                                    f"point solved, 5-NaN rule as a post-pass like the GPU) in {c:.2f} s"}
+    print(json.dumps(res), flush=True)
+
+
+def main_multihost(a):
+    """Config 3 (2048 x 2048) through the host-pointer C ABI on an n-device context
+    (sbr_init_multi over every visible GPU, one process, one host thread per GPU): what a Julia
+    ccall of sbr_sweep_baseline pays, PCIe included.  Reports the fan-out's phases: the slowest
+    rank's sweep, its D2H into the pinned landing buffer, the host copy into the caller's arrays."""
+    n_dev = torch.cuda.device_count()
+    eng = sbr.Engine(n_gpus=n_dev)
+    g = sbr.fig5_grid(a.n)
+    npts = g.n_points
+    host_out = {k: np.empty(npts) for k in sbr.engine.RESULT_FIELDS}
+    host_out["status"] = np.empty(npts, np.uint32)
+    host_out["iters"] = np.empty(npts, np.int32)
+    for _ in range(max(a.warmup, 1)):
+        eng.sweep_baseline(g, out=host_out)
+    phases = []
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        eng.sweep_baseline(g, out=host_out)
+        phases.append(eng.host_phases())
+    dt = (time.perf_counter() - t0) / a.steps
+    mean = {k: float(np.mean([p[k] for p in phases])) for k in phases[0]}
+    d2h_gbs = npts * 48 / n_dev / (mean["slowest_rank_d2h_pinned"] * 1e-3) / 1e9
+    res = {"metric": "equilibria solved/sec on β×u grid (FP64), host-pointer n-device call (PCIe included)",
+           "value": npts / dt, "unit": "equilibria/s", "n_gpus": n_dev, "steps": a.steps, "warmup": a.warmup,
+           "ms_per_step": dt * 1e3, "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+           "dtype": "f64", "data": "the reference's Fig 5 grid at 2048 x 2048 (deterministic)",
+           "config": {"workload": f"sbr_sweep_baseline on an sbr_init_multi({n_dev}) context, fig5 {a.n}x{a.n}, "
+                                  "host arrays out, direct transport (pinned landing buffer per rank)",
+                      "result_bytes_per_rank": npts * 48 // n_dev},
+           "phase_ms_mean": mean, "d2h_GBps_per_rank": d2h_gbs, "libsbr_sha16": lib_sha()}
     print(json.dumps(res), flush=True)
 
 
@@ -355,9 +472,30 @@ def main_dropin(a, eng, O):
     print(json.dumps(res), flush=True)
 
 
+def main_launchcheck(a):
+    """The launcher's plumbing without a GPU (tests/test_bench_launcher.py): every rank joins a
+    gloo group on the MASTER_* rendezvous, the ranks' ids are summed, and rank 0 prints one line."""
+    world, rank, _ = world_of(a.gpus)
+    if world > 1:
+        dist.init_process_group("gloo")
+        world = dist.get_world_size()
+        t = torch.tensor([rank], dtype=torch.int64)
+        dist.all_reduce(t)
+        rank_sum = int(t.item())
+    else:
+        rank_sum = 0
+    if rank == 0:
+        print(json.dumps({"workload": "launchcheck", "n_gpus": world, "rank_sum": rank_sum,
+                          "parallelism": f"beta-column shards x{world}"}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     a = parse()
-    if a.workload in ("config1", "config2", "dropin"):
+    if a.workload == "launchcheck":
+        return main_launchcheck(a)
+    if a.workload in ("config1", "config2", "dropin", "multihost"):
         return main_small(a)
     if a.workload == "social":
         return main_social(a)
@@ -365,17 +503,27 @@ def main():
         return main_hetero(a)
     if a.workload == "interest":
         return main_interest(a)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world, rank, local = world_of(a.gpus)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+        world = dist.get_world_size()
 
     n = a.n
-    amt = sbr.julia_range("0.0001", "1", n * world)
-    cols = np.arange(rank, n * world, world)
+    # weak (default): rank r owns columns r, r+N, … of a (n·N)-column grid; strong (--strong):
+    # the n-column grid itself is dealt over the N ranks; --shard-of V: one process runs the
+    # shard that rank --shard-rank of a V-rank strong run would own (a one-GPU rehearsal)
+    rehearsal = a.shard_of > 1
+    strong = a.strong or rehearsal
+    if rehearsal and world != 1:
+        raise SystemExit("bench.py: --shard-of rehearses one shard in one process (--gpus 1)")
+    n_shards, shard = (a.shard_of, a.shard_rank) if rehearsal else (world, rank)
+    if strong and n % n_shards:
+        raise SystemExit(f"bench.py: --strong needs --n ({n}) divisible by the shard count ({n_shards})")
+    n_axis = n if strong else n * world
+    amt = sbr.julia_range("0.0001", "1", n_axis)
+    cols = np.arange(shard, n_axis, n_shards)
     beta_h = 1.0 / amt[cols]
     u_h = sbr.julia_range("0.001", "1", n)
     nb, nu = len(beta_h), len(u_h)
@@ -454,10 +602,20 @@ def main():
     f_eq = (F8_BUFFER * nb * nu + F8_BISECT_ITER * int(iters.sum())
             + F8_AW_KNOT * int((run * n_tau[:, None]).sum()))
     f_learn = F8_RK_STEP * int((ls["n_accept"] + ls["n_reject"]).sum()) + F8_HZ_KNOT * int(n_tau.sum())
+    # pipelined: narrow grids (strong-scaled shards) share learning and equilibrium launches
+    # (libsbr groups them up to 2048 columns); the roofline is per launch, the kernel times per grid
+    gpl = (a.steps / max(ncalls, 1)) if pipe else 1.0
     eq_s = eq_ms / max(ncalls, 1) / 1e3
 
-    total_pts = nb * nu * world
+    total_pts = nb * nu * world  # every rank's shard (strong: the whole n x n grid)
     value = total_pts * a.steps / elapsed
+    if rehearsal:
+        workload = (f"fig5_beta_u_sweep_{n}x{n} strong-scaled: shard {shard} of {n_shards} ({nb} beta columns x "
+                    f"{nu} u) on one GPU, the per-GPU work of a {n_shards}-GPU run (BASELINE config 3)")
+    elif strong:
+        workload = f"fig5_beta_u_sweep_{n}x{n}_total strong-scaled over {world} GPU(s) (BASELINE config 3)"
+    else:
+        workload = f"fig5_beta_u_sweep_{n}x{n}_per_gpu (BASELINE config 3)"
     res = {
         "metric": "equilibria solved/sec on β×u grid (FP64)",
         "value": value,
@@ -467,24 +625,26 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": elapsed / a.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (deterministic Fig 5 parameter grid; no RNG in the reference)",
         "config": {
-            "workload": f"fig5_beta_u_sweep_{n}x{n}_per_gpu (BASELINE config 3)",
+            "workload": workload,
             "n_beta_per_gpu": nb, "n_u": nu, "eta": 15.0, "t_end": 30.0, "p": p, "kappa": kappa,
             "lambda": lam, "x0": x0, "early_exit": False,
             "collect": ("full SoA (48 B/pt) of every step on rank k mod N, all-to-all per N steps"
                         if gather else None),
             "parallelism": f"beta-column shards x{world}",
+            "beta_axis_columns": n_axis,
             "pipelined": pipe,
             "single_sweep_schedule": None if pipe else ("per-column readiness" if a.ready else "chunked"),
         },
         # pipelined: per-launch kernel times (HIP events around each launch on its stream);
         # single sweep: libsbr cuts the grid into column chunks whose kernels overlap, so the
         # events give the learning stage's wall time and the equilibrium tail after it
-        "kernel_ms_per_step": ({"learn_logistic": learn_ms / max(ncalls, 1), "equilibrium": eq_ms / max(ncalls, 1)}
+        "kernel_ms_per_step": ({"learn_logistic": learn_ms / a.steps, "equilibrium": eq_ms / a.steps,
+                                "equilibrium_launches": ncalls, "grids_per_launch": gpl}
                                if pipe else
                                {"learning_stage_wall": learn_ms / max(ncalls, 1),
                                 "equilibrium_tail_after_learning": eq_ms / max(ncalls, 1)}
@@ -495,7 +655,8 @@ def main():
         "work_per_step": {"run_points": int(run.sum()), "bisect_iters": int(iters.sum()),
                           "aw_knots_run": int((run * n_tau[:, None]).sum()),
                           "rk_steps": int((ls["n_accept"] + ls["n_reject"]).sum())},
-        "roofline": (roofline("equilibrium_kernel", f_eq, eq_s, pmc_of("equilibrium_kernel<768, false, 1>", f"fig5_{n}x{n}"))
+        "roofline": (roofline("equilibrium_kernel", f_eq * gpl, eq_s, pmc_of("equilibrium_kernel<768, false, 1>",
+                                                                   "-" if strong else f"fig5_{n}x{n}"))
                      if pipe else None),
         "libsbr_sha16": lib_sha(),
     }
@@ -529,6 +690,19 @@ def oracle_sweep(beta_cols, u_h, p, kappa, lam, x0, nthreads=0):
     return O.sweep_baseline(beta_cols, 15.0, 30.0, u_h, p, kappa, lam, x0=x0, nthreads=nthreads or usable_cores())
 
 
+def same_results(g: dict, o: dict, int_fields=("iters",)) -> bool:
+    """Every float result field equal bit for bit (NaN where NaN), the status bits and the
+    integer counters `int_fields` identical; g: GPU arrays, o: the oracle's, same shape."""
+    ok = True
+    for f in sbr.engine.RESULT_FIELDS:
+        a, b = np.asarray(g[f]), np.asarray(o[f])
+        ok &= a.shape == b.shape and bool(np.all((a == b) | (np.isnan(a) & np.isnan(b))))
+    ok &= bool(np.array_equal(np.asarray(g["status"]).view(np.uint32), np.asarray(o["status"]).view(np.uint32)))
+    for f in int_fields:
+        ok &= bool(np.array_equal(np.asarray(g[f]).astype(np.int64), np.asarray(o[f]).astype(np.int64)))
+    return bool(ok)
+
+
 def verify_grid(out, k, nb, nu, cols, o) -> dict:
     """Grid k of the timed run (the last timed step) against the oracle on columns `cols`:
     every result field, status bit and bisection count, bit for bit."""
@@ -551,13 +725,12 @@ def main_hetero(a):
     Weak scaling: rank r owns columns r, r+N, …  One step = learning (K-group Tsit5 +
     K hazards) for every column and buffers + ξ bisection + validity check + AW_max for
     every (column, u)."""
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world, rank, local = world_of(a.gpus)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+        world = dist.get_world_size()
     n = a.hetero_n
     full = sbr.hetero_config4(n * world, n, K=8)
     g = full.subset(np.arange(rank, n * world, world))
@@ -717,13 +890,12 @@ def main_interest(a):
     r = 0.06, δ = 0.1.  Weak scaling over β columns.  One step = learning + hazard per
     column and, per (β, u), the value-function Tsit5 solve on the HR grid, the buffers
     on h − rV, the ξ bisection and AW_max."""
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world, rank, local = world_of(a.gpus)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+        world = dist.get_world_size()
     n = a.interest_n
     beta_all = 1.0 / sbr.julia_range("0.0001", "1", n * world)
     beta_h = np.ascontiguousarray(beta_all[rank::world])
@@ -807,13 +979,18 @@ def main_interest(a):
         cores = usable_cores()
         sub = beta_h[::10]
         t1 = time.perf_counter()
-        O.sweep_interest(sub, 15.0, 30.0, u_h, p, kappa, lam, r_, delta, nthreads=cores)
+        o_i = O.sweep_interest(sub, 15.0, 30.0, u_h, p, kappa, lam, r_, delta, nthreads=cores)
         dt = time.perf_counter() - t1
         pts = len(sub) * nu
         res["cpu_baseline"] = {"value": pts / dt, "unit": "equilibria/s", "cores": cores, "kind": "port",
                                "host": host_info(),
                                "sample": f"{len(sub)} columns (every 10th) x {nu} u = {pts} equilibria "
                                          f"in {dt:.2f} s"}
+        # the sample's points of the last timed sweep against the oracle, bit for bit
+        gv = {k: v.view(nb, nu)[::10].cpu().numpy() for k, v in out.items()}
+        res["verified"] = dict(bitwise_equal_oracle=same_results(gv, o_i, ("iters", "rk_steps")),
+                               grid="last timed step", columns=len(sub), points=pts,
+                               fields="xi, tau_in_unc, tau_out_unc, aw_max, tol, status, iters, rk_steps")
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:
@@ -826,13 +1003,12 @@ def main_social(a):
     × u = range(0.001, 1, 512) with m_social's other parameters (η = 30/0.9 carried).  Weak
     scaling: rank r owns β columns r, r+N, … of a (cols·N)-column grid; cols = 64 makes N = 8
     exactly the 512×512 config.  One step = the whole fixed point for every point."""
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world, rank, local = world_of(a.gpus)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+        world = dist.get_world_size()
     ncol = a.social_cols * world
     # the config-5 β axis (512 columns); fewer ranks take an evenly strided share of it
     n_axis = max(512, ncol)
@@ -949,6 +1125,12 @@ def main_social(a):
         pts = len(bsel) * len(usel)
         cpu_steps = float((cs["n_accept"] + cs["n_reject"]).sum())
         grid_steps = float(steps.mean())
+        # the sample's fixed points of the timed sweep against the oracle, bit for bit
+        gv = {k: v.view(nb, nu)[::4, ::128].cpu().numpy() for k, v in out.items()}
+        res["verified"] = dict(bitwise_equal_oracle=same_results(gv, cs, ("iters", "fp_iters")),
+                               grid="the timed sweep", points=pts,
+                               fields="xi, tau_in_unc, tau_out_unc, aw_max, tol, status, iters, fp_iters",
+                               rk_steps_equal=bool(np.array_equal(gv["rk_steps"], cs["n_accept"] + cs["n_reject"])))
         res["cpu_baseline"] = {"value": (cpu_steps / dt) / grid_steps, "unit": "equilibria/s", "cores": cores,
                                "kind": "port", "host": host_info(),
                                "raw_sample_rate": pts / dt,

@@ -98,13 +98,18 @@ const char* sbr_last_error(const sbr_ctx* ctx);
 
 /*
  * n-device context (SURVEY.md §8(b) `sbr_init(n_gpus, …)`, §8(e)): n_gpus HIP devices
- * (`devices` lists their ids, NULL = 0 .. n_gpus-1), one single-device context per
- * device, an RCCL communicator over them (librccl.so.1, loaded at run time).  The
- * host-pointer sweeps — sbr_sweep_baseline, sbr_sweep_hetero, sbr_sweep_social,
- * sbr_sweep_interest — on such a context deal the parameter columns cyclically
- * (column i to device i mod n_gpus), solve every shard on its GPU from one host thread
- * per GPU, gather the result arrays to device 0 over RCCL (xGMI) and return them in
- * the single-device layout: bit-identical to a one-GPU sweep (per-point results do not
+ * (`devices` lists their ids, NULL = 0 .. n_gpus-1), one single-device context per device.
+ * The host-pointer sweeps — sbr_sweep_baseline, sbr_sweep_hetero, sbr_sweep_social,
+ * sbr_sweep_interest — on such a context deal the parameter columns cyclically (column i
+ * to device i mod n_gpus) and solve every shard on its GPU from one host thread per GPU.
+ * Results travel by the direct transport (default): each GPU copies its own packed result
+ * block in one DMA over its own PCIe link into a pinned landing buffer, and once every rank
+ * has succeeded host threads copy the columns into the caller's arrays — no collective runs,
+ * nothing funnels through device 0, and a failed call writes none of the caller's arrays.
+ * With SBR_FLAG_RCCL_GATHER the blocks are gathered to device 0 over RCCL (xGMI) and
+ * scattered from there instead; librccl.so.1 is loaded and the communicators created only
+ * then (that transport is unverified on multi-GPU hardware).  Either way the results are in
+ * the single-device layout, bit-identical to a one-GPU sweep (per-point results do not
  * depend on the partitioning).  Single-point, learning-only and diagnostic calls run on
  * device 0; the device-pointer (*_dev) entry points need a single-device context:
  * sbr_multi_child(ctx, rank).  A call is synchronous; contexts are independent, so
@@ -401,7 +406,10 @@ int sbr_last_schedule(sbr_ctx* ctx, int32_t* schedule);
  * [0] H2D of the inputs, [1] the kernels (learning, hazard, equilibria), [2] D2H of the results
  * into pinned memory (HIP events on the call's stream), [3] the host side after the sync: the copy
  * into the caller's arrays and the early-exit post-pass, [4] the whole call (host clock; the rest
- * is launch and synchronisation overhead). */
+ * is launch and synchronisation overhead).  On an n-device context (any host-pointer sweep,
+ * host clock, timing need not be enabled): [0] the slowest rank's staging + sweep, [1] the
+ * slowest rank's D2H into its landing buffer, [2] the host copy into the caller's arrays (or the
+ * RCCL gather + scatter), [3] 0, [4] the whole fan-out. */
 int sbr_host_phases(sbr_ctx* ctx, double* ms5);
 /* Timeline of the last chunked single sweep made while timing is enabled: for each of the
  * *n_chunks column chunks, ms[2k] = its learning end and ms[2k+1] = its equilibrium end, in ms

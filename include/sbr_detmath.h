@@ -67,10 +67,62 @@ SBR_HD double sbr_jl_eps(double x)
 #define SBR_LN2_LO 1.90821492927058770002e-10
 #define SBR_INV_LN2 1.44269504088896338700e+00
 
+/* (r·c) / (2 − c) of sbr_exp, correctly rounded.  On gfx950 for the fast path's operands
+ * (a = 0 or 2^-900 < |a| < 1, b in [1.6, 2.4]) the compiler's IEEE division sequence without
+ * its v_div_scale / v_div_fmas scaling and v_div_fixup special-case steps, which are identities
+ * there (v_rcp_f64, two Newton steps on the reciprocal, q = a·r, one fma remainder correction):
+ * the same quotient bit for bit; the host divides. */
+SBR_HD double sbr_ddiv_mid(double a, double b)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    double y = __builtin_amdgcn_rcp(b);
+    y = __builtin_fma(y, __builtin_fma(-b, y, 1.0), y);
+    y = __builtin_fma(y, __builtin_fma(-b, y, 1.0), y);
+    const double q = a * y;
+    return __builtin_fma(__builtin_fma(-b, q, a), y, q);
+#else
+    return a / b;
+#endif
+}
+
+/* sbr_exp for x = 0 or 2^-400 <= |x| <= 708 (k in [-1021, 1021]: the normal-result branch,
+ * no special input): the same operations as sbr_exp's, so the same bits, without the
+ * special-input and sub/overnormal selects. */
+SBR_HD double sbr_exp_mid(double x)
+{
+    const double P1 = 1.66666666666666019037e-01;
+    const double P2 = -2.77777777770155933842e-03;
+    const double P3 = 6.61375632143793436117e-05;
+    const double P4 = -1.65339022054652515390e-06;
+    const double P5 = 4.13813679705723846039e-08;
+    const double t = x * SBR_INV_LN2;
+    const int k = (int)(t < 0.0 ? t - 0.5 : t + 0.5);
+    const double kd = (double)k;
+    const double hi = x - kd * SBR_LN2_HI;
+    const double lo = kd * SBR_LN2_LO;
+    const double r = hi - lo;
+    const double r2 = r * r;
+    const double c = r - r2 * (P1 + r2 * (P2 + r2 * (P3 + r2 * (P4 + r2 * P5))));
+    const double y = 1.0 - ((lo - sbr_ddiv_mid(r * c, 2.0 - c)) - hi);
+    return y * sbr_bitsd((uint64_t)(k + 1023) << 52);
+}
+
 /* exp: Cody–Waite reduction x = k ln2 + r, |r| <= ln2/2, then the fdlibm
  * rational form.  Special inputs are computed on a safe argument and
- * replaced by select at the end. */
+ * replaced by select at the end.  On the device the common range takes
+ * sbr_exp_mid (same bits) behind one branch, which a wave whose lanes all
+ * hold such arguments never leaves. */
+SBR_HD double sbr_exp_full(double x);
 SBR_HD double sbr_exp(double x)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    const double ax = __builtin_fabs(x);
+    if ((ax <= 708.0 && ax >= 0x1p-400) || x == 0.0) return sbr_exp_mid(x);
+#endif
+    return sbr_exp_full(x);
+}
+
+SBR_HD double sbr_exp_full(double x)
 {
     const double P1 = 1.66666666666666019037e-01;
     const double P2 = -2.77777777770155933842e-03;

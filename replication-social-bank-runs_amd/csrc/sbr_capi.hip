@@ -18,6 +18,7 @@
 
 #include "../../include/sbr.h"
 #include "../../include/sbr_detmath.h"
+#include "sbr_hostcopy.h"
 #include "sbr_kernels.h"
 #include "sbr_multi.h"
 
@@ -41,6 +42,9 @@
 #endif
 #ifndef SBR_LEARN_GROUP
 #define SBR_LEARN_GROUP 1 // grids per learning launch of the pipelined batch (A/B: 2 was slower, 1.567 -> 1.631 ms per step: r04_j)
+#endif
+#ifndef SBR_LEARN_FILL_COLS
+#define SBR_LEARN_FILL_COLS 2048 // narrower grids share a learning launch up to this many columns
 #endif
 #ifndef SBR_LEARN_STREAMS
 #define SBR_LEARN_STREAMS 3 // learning streams (with the context stream: within GPU_MAX_HW_QUEUES = 4)
@@ -411,31 +415,6 @@ int ensure_res_pin(sbr_ctx* c, size_t bytes)
     HIP_TRY(c, hipHostMalloc(&c->res_pin, bytes), SBR_ENOMEM);
     c->res_pin_bytes = bytes;
     return SBR_OK;
-}
-
-// copy (dst_k, src_k, bytes_k) pieces with up to 8 host threads in ≈1 MiB slices: the caller's
-// result arrays are often fresh pages (first-touch faults), which one thread would take serially
-void parallel_copy(const std::vector<std::array<size_t, 3>>& pieces)
-{
-    constexpr size_t kSlice = 1 << 20;
-    std::vector<std::array<size_t, 3>> sl;
-    size_t total = 0;
-    for (const auto& p : pieces)
-        for (size_t o = 0; o < p[2]; o += kSlice) {
-            const size_t b = std::min(kSlice, p[2] - o);
-            sl.push_back({p[0] + o, p[1] + o, b});
-            total += b;
-        }
-    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    const size_t nt = std::min<size_t>({(size_t)8, (size_t)hw, (total + (4u << 20) - 1) / (4u << 20)});
-    auto work = [&](size_t k0) {
-        for (size_t k = k0; k < sl.size(); k += nt) memcpy((void*)sl[k][0], (const void*)sl[k][1], sl[k][2]);
-    };
-    if (nt <= 1) { work(0); return; }
-    std::vector<std::thread> th;
-    for (size_t t = 1; t < nt; t++) th.emplace_back(work, t);
-    work(0);
-    for (auto& t : th) t.join();
 }
 
 // EconomicParameters / LearningParameters scalar checks (model.jl:31-35, 71-76)
@@ -955,7 +934,13 @@ int sbr_sweep_baseline_batch_dev(sbr_ctx* c, void* stream, int64_t n_batch, cons
     // the learning stage is latency-bound on its slowest column, so a launch over twice the
     // columns takes about as long as one over a single grid, and the three learning streams
     // keep twice as many grids in flight
-    const int64_t GR = SBR_LEARN_GROUP;
+    // A launch is as long as its slowest column whatever its width, so grids narrower than
+    // SBR_LEARN_FILL_COLS columns (a strong-scaled shard: 2048/N columns) are grouped up to that
+    // width — 32 waves per launch, the full grid's count: a 256-column shard learns 8 grids per
+    // launch instead of 4 waves per launch in series on each stream.
+    int64_t GR = (SBR_LEARN_FILL_COLS + n_beta - 1) / n_beta;
+    if (GR < SBR_LEARN_GROUP) GR = SBR_LEARN_GROUP;
+    if (GR > n_batch) GR = n_batch;
     const int64_t n_group = (n_batch + GR - 1) / GR;
     for (int k = 0; k < nslot && k < n_group; k++) {
         int rc = ensure_learn(c, (size_t)(n_beta * GR), (size_t)o.knot_capacity, k, SBR_FUSE_HAZARD != 0);
@@ -1000,27 +985,27 @@ int sbr_sweep_baseline_batch_dev(sbr_ctx* c, void* stream, int64_t n_batch, cons
             tend(c, ls, 0, t0);
             HIP_TRY(c, hipEventRecord(c->ev_learned[slot], ls), SBR_EDEVICE);
             HIP_TRY(c, hipStreamWaitEvent(es, c->ev_learned[slot], 0), SBR_EDEVICE);
-            for (int64_t i = 0; i < gn; i++) {
-                const int64_t k = g0 + i;
+            // the group's gn grids in ONE equilibrium launch over their gn·n_beta columns: the slot
+            // holds them adjacently, and eta / t_end / every out field are [n_batch × n_beta(× n_u)]
+            // contiguous, so column i·n_beta + j of the launch is grid g0+i's column j at exactly
+            // its own offsets.  A narrow grid (a strong-scaled shard: 256 columns × 3 u-tiles =
+            // 768 workgroups) would otherwise be one launch of its slowest workgroups (≈0.5 ms,
+            // DESIGN §4) with the CUs idle behind them; grouped, the launch is as wide as a full grid.
+            {
                 const sbr::LearnBufs& W = c->LW[slot];
-                const size_t co = (size_t)(i * n_beta), cc = co * (size_t)W.cap;
-                const sbr::LearnBufs Lk{W.t + cc, W.G + cc, W.hr + cc, W.hrI ? W.hrI + cc : nullptr, W.n_knots + co,
-                                        W.n_tau + co, W.n_le + co, W.status + co, W.n_accept + co, W.n_reject + co,
-                                        W.cap};
-                const double* ek = eta + k * n_beta;
-                const double* tk = t_end + k * n_beta;
-                sbr::ResultSoA r{out->xi ? out->xi + k * np : nullptr,
-                                 out->tau_in_unc ? out->tau_in_unc + k * np : nullptr,
-                                 out->tau_out_unc ? out->tau_out_unc + k * np : nullptr,
-                                 out->aw_max ? out->aw_max + k * np : nullptr,
-                                 out->tol ? out->tol + k * np : nullptr,
-                                 out->status ? out->status + k * np : nullptr,
-                                 out->iters ? out->iters + k * np : nullptr};
-                int rc = launch_eq(c, es, Lk, ek, tk, u, n_beta, n_u, kappa, o, r, nullptr);
+                sbr::ResultSoA r{out->xi ? out->xi + g0 * np : nullptr,
+                                 out->tau_in_unc ? out->tau_in_unc + g0 * np : nullptr,
+                                 out->tau_out_unc ? out->tau_out_unc + g0 * np : nullptr,
+                                 out->aw_max ? out->aw_max + g0 * np : nullptr,
+                                 out->tol ? out->tol + g0 * np : nullptr,
+                                 out->status ? out->status + g0 * np : nullptr,
+                                 out->iters ? out->iters + g0 * np : nullptr};
+                int rc = launch_eq(c, es, W, eta + g0 * n_beta, t_end + g0 * n_beta, u, gn * n_beta, n_u, kappa, o, r,
+                                   nullptr);
                 if (rc) return rc;
-                HIP_TRY(c, hipEventRecord(c->ev_grid[k], es), SBR_EDEVICE);
-                c->n_grid = k + 1;
-                c->last_off = (int64_t)co;
+                for (int64_t i = 0; i < gn; i++) HIP_TRY(c, hipEventRecord(c->ev_grid[g0 + i], es), SBR_EDEVICE);
+                c->n_grid = g0 + gn;
+                c->last_off = (gn - 1) * n_beta;
             }
             HIP_TRY(c, hipEventRecord(c->ev_eq[slot], es), SBR_EDEVICE);
             c->last_slot = slot;
@@ -1102,7 +1087,7 @@ int sbr_sweep_baseline(sbr_ctx* c, const double* beta, const double* eta, const 
                 if (hs[k]) pieces.push_back({(size_t)hs[k], (size_t)(P + (size_t)k * np * 8), np * 8});
             if (out->status) pieces.push_back({(size_t)out->status, (size_t)(P + 5 * np * 8), np * 4});
             if (out->iters) pieces.push_back({(size_t)out->iters, (size_t)(P + 5 * np * 8 + np * 4), np * 4});
-            parallel_copy(pieces);
+            sbr_host::parallel_copy(pieces);
         }
         if (o.early_exit_nan_run > 0 && out->status && out->xi && out->aw_max && out->tol)
             sbr_apply_early_exit(n_beta, n_u, o.early_exit_nan_run, out);
@@ -1699,9 +1684,9 @@ int sbr_chunk_timeline(sbr_ctx* c, void* stream, int32_t* n_chunks, double* ms)
 
 int sbr_host_phases(sbr_ctx* c, double* ms5)
 {
-    SBR_PER_DEVICE_DIAG(c);
     if (!c || !ms5) return SBR_EARG;
-    for (int k = 0; k < 5; k++) ms5[k] = c->ph_ms[k];
+    const double* ph = c->multi ? sbr_multi_impl::phases(c->multi) : c->ph_ms;
+    for (int k = 0; k < 5; k++) ms5[k] = ph[k];
     return SBR_OK;
 }
 
@@ -2216,11 +2201,11 @@ int run_social_pass(sbr_ctx* c, hipStream_t s, const double* beta, const double*
             inner.push_back(m);
             done += m;
         }
-        if (nslots > 0) inner.push_back(kSocialInner2);
         const int n_launch = (int)inner.size();
         static const bool trace = getenv("SBR_SOCIAL_TRACE") != nullptr;
         const auto tr0 = std::chrono::steady_clock::now();
-        for (int q = 0, it = 1; q < n_launch; it += inner[q], q++) {
+        int q = 0, it = 1;
+        for (; q < n_launch; it += inner[q], q++) {
             const int k = q & 1;
             HIP_TRY(c, sbr::launch_social_iter(a, b, c->so_args_dev, it, inner[q], c->so_work[k],
                                                c->so_count + k, c->so_work[k ^ 1], c->so_count + (k ^ 1), s),
@@ -2233,8 +2218,24 @@ int run_social_pass(sbr_ctx* c, hipStream_t s, const double* beta, const double*
                     fprintf(stderr, "sbr_social_trace launch=%d t=%.3f live=%d pool_used=%d pool_live=%d\n", q,
                                  std::chrono::duration<double>(std::chrono::steady_clock::now() - tr0).count(),
                                  c->so_count_host[k ^ 1], c->so_count_host[2], c->so_count_host[3]);
-                if (poll > 0 && c->so_count_host[k ^ 1] == 0 && c->so_count_host[3] == 0) break;
+                if (poll > 0 && c->so_count_host[k ^ 1] == 0 && c->so_count_host[3] == 0) { q++; break; }
             }
+        }
+        // Pool drain.  A point promoted during a launch restarts at its promotion iterate in the
+        // next launch, so it can trail the main worklist by up to one launch's iterates (16) and
+        // still be live once the main list has reached max_iter: drain launches of kSocialInner
+        // iterates run until the pool has no live point (bounded: each advances every pool point
+        // by kSocialInner iterates towards max_iter).
+        for (int d = 0; nslots > 0 && d <= max_iter / kSocialInner + 1; d++, it += kSocialInner, q++) {
+            HIP_TRY(c, hipMemcpyAsync(c->so_count_host, c->so_count, 4 * 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+            HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
+            if (c->so_count_host[3] == 0) break;
+            const int k = q & 1;
+            HIP_TRY(c, sbr::launch_social_iter(a, b, c->so_args_dev, it, kSocialInner, c->so_work[k],
+                                               c->so_count + k, c->so_work[k ^ 1], c->so_count + (k ^ 1), s),
+                    SBR_EDEVICE);
+            if (trace)
+                fprintf(stderr, "sbr_social_trace drain=%d pool_live_before=%d\n", d, c->so_count_host[3]);
         }
         tend(c, s, 1, t0);
         // promotions of this chunk (diagnostics), and the sync that frees the argument staging

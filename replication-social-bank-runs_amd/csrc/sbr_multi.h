@@ -31,6 +31,8 @@ void destroy(sbr_multi* m);
 int size(const sbr_multi* m);
 sbr_ctx* child(sbr_multi* m, int rank);
 const char* last_error(const sbr_multi* m);
+// phases of the last sweep, ms (sbr_host_phases on an n-device context)
+const double* phases(const sbr_multi* m);
 // rccl_gather: results to rank 0 over RCCL, then scattered from there (SBR_FLAG_RCCL_GATHER);
 // otherwise every rank copies its own columns into the caller's arrays
 int run_sharded(sbr_multi* m, int64_t n_col, int64_t n_u, const std::vector<FieldSpec>& fields, size_t in_bytes,

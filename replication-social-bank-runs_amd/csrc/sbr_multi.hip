@@ -7,12 +7,13 @@
 //      *_dev entry points on that child context's own stream, inputs staged into that
 //      GPU's HBM);
 //   3. returns the results to the caller's host arrays by one of two transports:
-//      * direct (the default): each rank copies its own packed block straight into the
-//        caller's u-fastest arrays (strided D2H copies: column i of the grid is block row
-//        i / N of rank i mod N) from its own thread, so the N GPUs' PCIe links carry the
-//        result in parallel and no collective runs — the results of a host-pointer sweep
-//        are bound for host memory, which a gather to one GPU would funnel through a
-//        single link;
+//      * direct (the default): each rank copies its own packed block in one DMA into its
+//        own pinned landing buffer (from its own thread, so the N GPUs' PCIe links carry
+//        the result in parallel and no collective runs — the results of a host-pointer
+//        sweep are bound for host memory, which a gather to one GPU would funnel through a
+//        single link); once every rank has succeeded, host threads copy the blocks into the
+//        caller's u-fastest arrays (column i of the grid is block row i / N of rank
+//        i mod N).  A failed call leaves the caller's arrays untouched;
 //      * RCCL gather (SBR_FLAG_RCCL_GATHER): after every shard has finished, and after
 //        every fallible per-rank step of the gather (device selection, rank 0's gather
 //        buffer, its local copy) has succeeded, the packed blocks go to rank 0's HBM with
@@ -25,8 +26,9 @@
 // Steps 1, 3 and 4 are sbr_shard.h's, shared with the host loopback of
 // sbr_shard_host_run (the CPU tests' N = 2, 3, 8 layouts).  Per-point results do not
 // depend on the partitioning, so a multi-GPU sweep is bit-identical to a single-device
-// one.  librccl.so.1 is loaded at run time (reusing an already-loaded copy, e.g.
-// torch's), so libsbr has no link-time dependency on it.
+// one.  librccl.so.1 is loaded, and the communicators created, only when a sweep asks
+// for the RCCL gather (reusing an already-loaded copy, e.g. torch's), so libsbr has no
+// link-time dependency on it and the default transport never touches it.
 #include <dlfcn.h>
 #include <math.h>
 #include <string.h>
@@ -40,6 +42,7 @@
 #include <rccl/rccl.h>
 
 #include "../../include/sbr.h"
+#include "sbr_hostcopy.h"
 #include "sbr_multi.h"
 #include "sbr_shard.h"
 
@@ -98,7 +101,25 @@ struct Rank {
     size_t out_bytes = 0;
     void* gather = nullptr; // rank 0: every rank's block
     size_t gather_bytes = 0;
+    void* pin = nullptr;    // pinned landing buffer of the direct transport
+    size_t pin_bytes = 0;
 };
+
+int grow_pinned(void** p, size_t* have, size_t need)
+{
+    if (need <= *have) return 0;
+    if (*p) (void)hipHostFree(*p);
+    *p = nullptr;
+    *have = 0;
+    if (hipHostMalloc(p, need) != hipSuccess) return -1;
+    *have = need;
+    return 0;
+}
+
+double ms_since(std::chrono::steady_clock::time_point t0)
+{
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
 
 int grow(void** p, size_t* have, size_t need)
 {
@@ -116,7 +137,11 @@ int grow(void** p, size_t* have, size_t need)
 struct sbr_multi {
     std::vector<Rank> ranks;
     std::string err;
-    bool comms_ok = false; // false after an abort: rebuilt by the next gather
+    bool comms_ok = false; // false after an abort (or before the first gather): (re)built by the next gather
+    // phases of the last sweep, ms: [0] slowest rank's staging + sweep, [1] slowest rank's D2H
+    // into its landing buffer, [2] the host copy into the caller's arrays (direct transport) or
+    // the RCCL gather + scatter, [3] unused, [4] the whole call
+    double ph[5] = {};
 };
 
 namespace {
@@ -241,16 +266,11 @@ int create(int n_gpus, const int* devices, sbr_multi** out, std::vector<sbr_ctx*
         for (int q = 0; q < r; q++)
             if (dl[q] == dl[r]) { err = "duplicate device id"; return SBR_EARG; }
     }
-    const Rccl& R = rccl();
-    if (!R.ok) { err = R.err; return SBR_EDEVICE; }
+    // no RCCL here: the communicators are created by the first sweep that asks for the gather
     sbr_multi* m = new sbr_multi();
     m->ranks.resize(n_gpus);
     for (int r = 0; r < n_gpus; r++) m->ranks[r].device = dl[r];
-    int rc = init_comms(m, err);
-    if (rc != SBR_OK) {
-        delete m;
-        return rc;
-    }
+    int rc = SBR_OK;
     for (int r = 0; r < n_gpus; r++) {
         Rank& k = m->ranks[r];
         rc = sbr_init(dl[r], &k.kid);
@@ -269,13 +289,13 @@ int create(int n_gpus, const int* devices, sbr_multi** out, std::vector<sbr_ctx*
 void destroy(sbr_multi* m)
 {
     if (!m) return;
-    const Rccl& R = rccl();
     for (Rank& k : m->ranks) {
         (void)hipSetDevice(k.device);
         if (k.stream) (void)hipStreamSynchronize(k.stream);
-        if (k.comm && R.ok) (void)R.CommDestroy(k.comm);
+        if (k.comm) (void)rccl().CommDestroy(k.comm); // a communicator implies a loaded librccl
         for (void* p : {k.in, k.out, k.gather})
             if (p) (void)hipFree(p);
+        if (k.pin) (void)hipHostFree(k.pin);
         if (k.kid) (void)sbr_free(k.kid); // owns k.stream
     }
     delete m;
@@ -287,6 +307,8 @@ sbr_ctx* child(sbr_multi* m, int r) { return (m && r >= 0 && r < (int)m->ranks.s
 
 const char* last_error(const sbr_multi* m) { return m ? m->err.c_str() : ""; }
 
+const double* phases(const sbr_multi* m) { return m ? m->ph : nullptr; }
+
 // One sweep over the ranks (plan, deal, pack, gather, scatter: sbr_shard.h).  For rank r
 // with cols_r columns:
 //   stage(r, cols_r, in_dev, stream) -> int   stages its inputs into in_dev (device)
@@ -296,20 +318,26 @@ int run_sharded(sbr_multi* m, int64_t n_col, int64_t n_u, const std::vector<sbr_
                 size_t in_bytes, const StageFn& stage, const RunFn& run, bool rccl_gather)
 {
     m->err.clear();
+    const auto t_call = std::chrono::steady_clock::now();
+    for (double& x : m->ph) x = 0.0;
     const int N = (int)m->ranks.size();
     const sbr_shard::Plan plan = sbr_shard::make_plan(N, n_col, n_u, fields);
     std::vector<int> rcs(N, SBR_OK);
     std::vector<std::string> errs(N);
+    std::vector<double> t_run(N, 0.0), t_d2h(N, 0.0);
 
-    // phase 1: every shard on its GPU, to completion (no collective is entered unless all succeed)
+    // phase 1: every shard on its GPU, to completion (no collective is entered and no caller array
+    // is written unless all succeed); direct transport: each rank's block lands in its pinned buffer
     {
         std::vector<std::thread> th;
         for (int r = 0; r < N; r++)
             th.emplace_back([&, r] {
                 Rank& k = m->ranks[r];
                 if (plan.cols[r] == 0) return;
+                const auto t0 = std::chrono::steady_clock::now();
                 if (hipSetDevice(k.device) != hipSuccess) { rcs[r] = SBR_EDEVICE; errs[r] = "hipSetDevice"; return; }
-                if (grow(&k.in, &k.in_bytes, in_bytes + 256) || grow(&k.out, &k.out_bytes, plan.block_bytes(r) + 256)) {
+                if (grow(&k.in, &k.in_bytes, in_bytes + 256) || grow(&k.out, &k.out_bytes, plan.block_bytes(r) + 256) ||
+                    (!rccl_gather && grow_pinned(&k.pin, &k.pin_bytes, plan.block_bytes(r) + 256))) {
                     rcs[r] = SBR_ENOMEM;
                     errs[r] = "rank buffers";
                     return;
@@ -318,24 +346,50 @@ int run_sharded(sbr_multi* m, int64_t n_col, int64_t n_u, const std::vector<sbr_
                 std::vector<void*> fp;
                 for (size_t o : sbr_shard::field_offsets(plan, r, fields)) fp.push_back((char*)k.out + o);
                 if (rc == SBR_OK) rc = run(r, plan.cols[r], k.kid, k.stream, k.in, fp);
-                // direct transport: this rank's columns straight into the caller's arrays
-                if (rc == SBR_OK && !rccl_gather)
-                    rc = sbr_shard::scatter_rank(plan, r, fields, k.out,
-                                                 [&](void* d, size_t dp, const void* src, size_t sp, size_t w, size_t h) {
-                                                     return hipMemcpy2DAsync(d, dp, src, sp, w, h, hipMemcpyDeviceToHost,
-                                                                             k.stream) == hipSuccess ? 0 : SBR_EDEVICE;
-                                                 });
                 if (rc == SBR_OK && hipStreamSynchronize(k.stream) != hipSuccess) rc = SBR_EDEVICE;
+                t_run[r] = ms_since(t0);
+                // direct transport: the rank's packed block in one DMA over its own PCIe link
+                if (rc == SBR_OK && !rccl_gather) {
+                    const auto t1 = std::chrono::steady_clock::now();
+                    if (hipMemcpyAsync(k.pin, k.out, plan.block_bytes(r), hipMemcpyDeviceToHost, k.stream) != hipSuccess ||
+                        hipStreamSynchronize(k.stream) != hipSuccess)
+                        rc = SBR_EDEVICE;
+                    t_d2h[r] = ms_since(t1);
+                }
                 if (rc != SBR_OK) { rcs[r] = rc; errs[r] = sbr_last_error(k.kid); }
             });
         for (auto& t : th) t.join();
+    }
+    for (int r = 0; r < N; r++) {
+        m->ph[0] = t_run[r] > m->ph[0] ? t_run[r] : m->ph[0];
+        m->ph[1] = t_d2h[r] > m->ph[1] ? t_d2h[r] : m->ph[1];
     }
     for (int r = 0; r < N; r++)
         if (rcs[r] != SBR_OK) {
             m->err = "rank " + std::to_string(r) + ": " + errs[r];
             return rcs[r];
         }
-    if (!rccl_gather) return SBR_OK;
+    if (!rccl_gather) {
+        // every rank succeeded: its columns from the landing buffers into the caller's arrays
+        const auto t2 = std::chrono::steady_clock::now();
+        std::vector<std::array<size_t, 3>> pieces;
+        for (int r = 0; r < N; r++) {
+            if (plan.cols[r] == 0) continue;
+            const std::vector<size_t> fo = sbr_shard::field_offsets(plan, r, fields);
+            for (size_t i = 0; i < fields.size(); i++) {
+                const sbr_shard::Field& f = fields[i];
+                if (!f.host) continue;
+                const size_t row = (size_t)n_u * f.per_pt * f.esz;
+                for (int64_t c = 0; c < plan.cols[r]; c++)
+                    pieces.push_back({(size_t)((char*)f.host + (size_t)sbr_shard::global_col(r, c, N) * row),
+                                      (size_t)((const char*)m->ranks[r].pin + fo[i] + (size_t)c * row), row});
+            }
+        }
+        sbr_host::parallel_copy(pieces, 16);
+        m->ph[2] = ms_since(t2);
+        m->ph[4] = ms_since(t_call);
+        return SBR_OK;
+    }
 
     // phase 2, pre-checks: everything fallible before a send or receive is posted
     Rank& k0 = m->ranks[0];
@@ -343,6 +397,8 @@ int run_sharded(sbr_multi* m, int64_t n_col, int64_t n_u, const std::vector<sbr_
         if (hipSetDevice(m->ranks[r].device) != hipSuccess) { m->err = "hipSetDevice"; return SBR_EDEVICE; }
     if (hipSetDevice(k0.device) != hipSuccess) { m->err = "hipSetDevice"; return SBR_EDEVICE; }
     if (grow(&k0.gather, &k0.gather_bytes, plan.gather_bytes() + 256)) { m->err = "gather buffer"; return SBR_ENOMEM; }
+    const auto t2 = std::chrono::steady_clock::now();
+    if (!rccl().ok) { m->err = rccl().err; return SBR_EDEVICE; }
     if (N > 1 && !m->comms_ok) {
         int rc = init_comms(m, m->err);
         if (rc) return rc;
@@ -365,6 +421,8 @@ int run_sharded(sbr_multi* m, int64_t n_col, int64_t n_u, const std::vector<sbr_
                                       });
     if (rc) { m->err = "result copy"; return rc; }
     if (hipStreamSynchronize(k0.stream) != hipSuccess) { m->err = "result sync"; return SBR_EDEVICE; }
+    m->ph[2] = ms_since(t2);
+    m->ph[4] = ms_since(t_call);
     return SBR_OK;
 }
 

@@ -96,12 +96,14 @@ def host_result_views(out: dict, n: int) -> dict:
 class Engine:
     """One libsbr context: one HIP device (``device``), or — with ``n_gpus`` /
     ``devices`` — an n-device context whose host-pointer sweeps fan out over the GPUs
-    inside libsbr (one host thread per GPU, RCCL gather; sbr_init_multi)."""
+    inside libsbr (one host thread per GPU, each GPU's results over its own PCIe link;
+    sbr_init_multi)."""
 
     def __init__(self, device: int | None = None, n_gpus: int | None = None, devices=None):
         L = _lib.load()
         ctx = _P()
-        if n_gpus is not None or devices is not None:
+        self._multi = n_gpus is not None or devices is not None
+        if self._multi:
             devs = None if devices is None else (ctypes.c_int * len(devices))(*devices)
             n = len(devices) if devices is not None else int(n_gpus)
             rc = L.sbr_init_multi(n, devs, ctypes.byref(ctx))
@@ -558,9 +560,13 @@ class Engine:
         return dict(lds_bytes_per_block=a.value, lds_knot_capacity=b.value, cu_count=c.value)
 
     def host_phases(self) -> dict:
-        """Phases (ms) of the last host-pointer sweep_baseline made with timing enabled."""
+        """Phases (ms) of the last host-pointer sweep_baseline made with timing enabled; on an
+        n-device context, of the last host-pointer sweep's fan-out (always recorded)."""
         v = (ctypes.c_double * 5)()
         check(self._L.sbr_host_phases(self._ctx, v), self._ctx, "sbr_host_phases")
+        if self.n_gpus > 1 or self._multi:
+            return dict(zip(("slowest_rank_sweep", "slowest_rank_d2h_pinned", "host_copy_or_gather", "unused",
+                             "call"), list(v)))
         return dict(zip(("h2d", "kernels", "d2h", "host_copy_early_exit", "call"), list(v)))
 
     def chunk_timeline(self, stream: int | None = None) -> list:

@@ -22,8 +22,16 @@ def assert_bitwise(a, b, name):
 
 def test_detmath_host_device_bitwise(engine, oracle):
     rng = np.random.default_rng(0)
+    # sbr_exp's device fast path (x = 0 or 2^-400 <= |x| <= 708) and the full branch-free
+    # form around its edges, the hazard's λτ̄ range, and every k's reduction boundary
+    edges = np.array([708.0, -708.0, np.nextafter(708.0, 1e3), np.nextafter(-708.0, -1e3), 2.0 ** -400,
+                      -(2.0 ** -400), np.nextafter(2.0 ** -400, 0.0), 5e-324, -5e-324, 709.78, -745.1, np.inf,
+                      -np.inf, np.nan, -0.0])
+    ks = np.arange(-1030, 1030) * np.log(2.0)
     x = np.concatenate([rng.uniform(-745, 709, 20000), np.exp(rng.uniform(-700, 700, 20000)),
-                        rng.uniform(1e-300, 1e-290, 100), [0.0, 1.0, 2.0, 0.5]])
+                        rng.uniform(1e-300, 1e-290, 100), [0.0, 1.0, 2.0, 0.5], edges, ks,
+                        np.nextafter(ks, np.inf), np.nextafter(ks, -np.inf), ks + np.log(2.0) / 2,
+                        rng.uniform(0.0, 8.0, 20000)])
     y = rng.uniform(-1.0, 1.0, len(x))
     xe = x.copy()
     e_d, _, _ = engine.selftest_detmath(xe, y)
@@ -222,24 +230,27 @@ def test_device_info(engine):
     assert info["lds_knot_capacity"] >= 3400  # every config-3 column staged in LDS
 
 
-def test_pipelined_batches_equal_single_sweeps(engine):
+@pytest.mark.parametrize("ncol", [384, 1200])
+def test_pipelined_batches_equal_single_sweeps(engine, ncol):
     """sbr_sweep_baseline_batch_dev (learning of batch k+1 overlapping the
     equilibrium of batch k on two streams, alternating workspaces) returns for
-    every batch exactly what a single sweep of that grid returns."""
+    every batch exactly what a single sweep of that grid returns.  Grids narrower than
+    2048 columns share learning and equilibrium launches: 384 columns, 6 grids per launch
+    (11 grids: groups of 6 and 5); 1200 columns, 2 per launch (6 groups, more than the 4
+    learning workspaces, so each is reused; the last group holds one grid)."""
     torch = pytest.importorskip("torch")
     dev = torch.device("cuda", 0)
-    base = sbr.fig5_grid(384)
+    base = sbr.fig5_grid(ncol, n_u=384)
     betas = np.stack([base.beta, base.beta[::-1], base.beta * 0.5, base.beta])
-    etas = np.stack([np.full(384, 15.0), np.full(384, 10.0), np.full(384, 15.0), np.full(384, 7.5)])
+    etas = np.stack([np.full(ncol, 15.0), np.full(ncol, 10.0), np.full(ncol, 15.0), np.full(ncol, 7.5)])
     etas[1, :7] = 40.0  # η past tspan: the hazard stage's BoundsError (fused into learning in the batch)
     etas[2, 7:9] = 30.0  # η == t_end: the last knot is η itself
-    tends = np.stack([np.full(384, 30.0), np.full(384, 30.0), np.full(384, 20.0), np.full(384, 30.0)])
-    # 11 grids: an odd count (the last learning group holds one grid) and more groups than
-    # learning workspaces (each is reused); the extra grids vary β so no two are alike
+    tends = np.stack([np.full(ncol, 30.0), np.full(ncol, 30.0), np.full(ncol, 20.0), np.full(ncol, 30.0)])
+    # 11 grids; the extra grids vary β so no two are alike
     extra = np.arange(7)[:, None]
     betas = np.concatenate([betas, base.beta[None, :] * (1.0 + 0.05 * (extra + 1))])
-    etas = np.concatenate([etas, np.full((7, 384), 15.0) - extra])
-    tends = np.concatenate([tends, np.full((7, 384), 30.0)])
+    etas = np.concatenate([etas, np.full((7, ncol), 15.0) - extra])
+    tends = np.concatenate([tends, np.full((7, ncol), 30.0)])
     nbat, nb, nu = betas.shape[0], betas.shape[1], len(base.u)
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
     out = {f: torch.empty(nbat, nb * nu, dtype=torch.float64, device=dev) for f in FIELDS}

@@ -1,8 +1,9 @@
 """Multi-GPU fan-out inside libsbr (sbr_init_multi, include/sbr.h; SURVEY.md §8(b)
 threading contract, §8(e) partitioning): an n-device context deals the parameter
-columns cyclically over its GPUs, one host thread per GPU, and gathers the result
-arrays to device 0 over RCCL.  On the one-GPU test box n = 1 (the RCCL communicator,
-the rank threads, the gather and the strided scatter all run); the multi-rank column
+columns cyclically over its GPUs, one host thread per GPU, and returns each rank's result
+block over its own link (pinned landing buffer, then host threads into the caller's arrays;
+SBR_FLAG_RCCL_GATHER: an RCCL gather to device 0 instead).  On the one-GPU test box n = 1
+(the rank threads, both transports and the strided scatter all run); the multi-rank column
 interleaving of the Python layer is covered by the world-2/3 gloo tests of
 tests/test_distributed.py.  Every result must equal the single-device context's bit
 for bit, and the engine-backed sbr.distributed sweeps (compute=None) must run."""
@@ -79,6 +80,16 @@ def test_multi_baseline_fig5_and_early_exit(engine, multi, flags):
         b = engine.sweep_baseline(g, early_exit=ee)
         for k in (*FIELDS, "status", "iters"):
             assert_same(a[k], b[k], f"{k} (early_exit={ee})")
+
+
+def test_multi_phases_recorded(multi):
+    """sbr_host_phases on an n-device context: the fan-out's phases of the last sweep."""
+    g = sbr.fig5_grid(500).subset(np.arange(0, 500, 5))
+    multi.sweep_baseline(g)
+    ph = multi.host_phases()
+    assert set(ph) == {"slowest_rank_sweep", "slowest_rank_d2h_pinned", "host_copy_or_gather", "unused", "call"}
+    assert ph["slowest_rank_sweep"] > 0 and ph["slowest_rank_d2h_pinned"] > 0 and ph["host_copy_or_gather"] > 0
+    assert ph["call"] >= ph["slowest_rank_sweep"]
 
 
 def test_multi_hetero_interest_social_bitwise(engine, multi):

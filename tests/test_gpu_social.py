@@ -122,6 +122,25 @@ def test_social_knot_overflow_promotion_and_rerun(engine, oracle):
         assert not (g["status"] & sbr.STATUS["SBR_KNOT_OVERFLOW"]).any()
 
 
+def test_social_promoted_points_reach_max_iter(engine, oracle):
+    """Points that never converge (tol = 1e-300) and outgrow an 8192-knot capacity: they are
+    promoted into the pool during the first launches and trail the main worklist by up to one
+    launch's iterates, so the pool must be drained past the main list's last launch until
+    every promoted point has run all max_iter = 30 iterates (one 8-iterate drain
+    left such points live, their results unwritten).  GPU == oracle on every field."""
+    beta = 1.0 / sbr.julia_range("0.01", "2", 512)
+    u = sbr.julia_range("0.001", "1", 512)
+    bsel, usel = beta[[128, 511]], u[[140, 25]]
+    cmp = sbr.julia_range(0.0, ETA, 1000)
+    o = oracle.sweep_social(bsel, ETA, usel, P, KAPPA, LAM, cmp, tol=1e-300, max_iter=30)
+    g = engine.sweep_social(bsel, ETA, usel, P, KAPPA, LAM, cmp=cmp, tol=1e-300, max_iter=30, knot_capacity=8192)
+    stats = engine.social_overflow_stats()
+    assert stats["promoted"] > 0 and stats["rerun"] == 0, stats
+    _compare(g, o)
+    assert (g["fp_iters"] == 30).all()
+    assert (g["status"] & sbr.STATUS["SBR_SOCIAL_NOT_CONVERGED"]).all()
+
+
 def test_social_point_paths_bitwise(engine, oracle):
     """sbr_social_point_paths: the returned SolvedModel's learning knots (t, G) — from which
     scripts/4_social_learning.jl's AW curves are rebuilt — equal the oracle's, on the script
