@@ -588,6 +588,14 @@ __device__ __forceinline__ int first_ge_down(F key, int hi, double x)
 #ifndef SBR_SCAN_BS
 #define SBR_SCAN_BS 1 // crossing scans by binary search over prefix / suffix block tables
 #endif
+#ifndef SBR_AW_OWN
+// aw_scan: knot offset 0 for the AW_OUT bound inside [ξ/2, 2ξ] (b_i = t[i] exactly there).  A/B
+// (profiles/experiments/r05_d_*): exact evaluations per run point 38.7 → 20.4, but the kernel
+// 1.320 → 1.361 ms alone (1.389 → 1.450 ms in the pipeline): an exact evaluation costs about what
+// a bounded trip costs (the bracket walk's LDS round trips dominate both), and the window test
+// adds to every trip.  Off.
+#define SBR_AW_OWN 0
+#endif
 #ifndef SBR_AW_K1
 #define SBR_AW_K1 1 // aw_scan bounds AW_OUT(b_j) by G[j + 1] where consecutive knots are separated
 #endif
@@ -642,15 +650,27 @@ __device__ __forceinline__ void aw_scan(P T, P G, const int n, const int ntau, c
     }
     const int kc = ka;
     const double ub_left = awout;
+    // Own-knot bounds (SBR_AW_OWN, off by default): for τ̄_i = t[i] in [ξ/2, 2ξ] with occ = ξ,
+    // b_i = (t[i] − ξ) + ξ is t[i] exactly (Sterbenz), so AW_OUT(b_j) <= G[j] for every j <= i
+    // there: the run bounds may take knot offset 0 instead of koff inside that window
+    // (tools/aw_scan_sim.py, config 3: 39 → 21 exact evaluations and 72 → 63 loop trips per run
+    // point; the maximum is unchanged) — measured slower, see SBR_AW_OWN.
+    const bool own_ok = SBR_AW_OWN && occ == xi;
+    const double own_lo = 0.5 * xi, own_hi = 2.0 * xi;
+    auto koff_at = [&](int i, double ti) -> int {
+        return (own_ok && i < nle && ti >= own_lo && ti <= own_hi) ? 0 : koff;
+    };
     // right of c
     double LA = awin; // lower bound of AW_IN(a_j) for every j >= i
     for (int i = c + 1; i < ntau;) {
-        const double av = av_of(i), xa = av > 0 ? av : 0.0;
+        const double ti = tau(i);
+        const double av = (ti - xi) + icc, xa = av > 0 ? av : 0.0;
         fwd(xa);
         const double lb = av >= 0 ? ga0 : 0.0;
         LA = LA > lb ? LA : lb;
         const double V = (((mx - G0) + LA) - M) - dd; // G[k] <= V: every knot up to k is <= V + dd
-        const int k2 = i + koff < n - 1 ? i + koff : n - 1;
+        const int ko = koff_at(i, ti);
+        const int k2 = i + ko < n - 1 ? i + ko : n - 1;
         if (G[k2] > V) {
             const double v = exact(i, av, xa);
             if (v > mx) mx = v;
@@ -661,7 +681,10 @@ __device__ __forceinline__ void aw_scan(P T, P G, const int n, const int ntau, c
         // every knot j with G[min(j + 2, n − 1)] <= V is at or below mx: skip to the first other
         const int kl = ssl_gallop(G, n, k2, V);
         if (kl >= n - 1) break;
-        const int inext = kl + 1 - koff; // G[kl + 1] > V: the first knot whose bound is not dismissed
+        // G[kl + 1] > V: the first knot whose bound is not dismissed (offset 0 while the skip stays
+        // inside the own-bound window, else the run offset koff)
+        int inext = kl + 1 - koff;
+        if (ko == 0) inext = T[kl] <= own_hi ? kl + 1 : (inext > i + 1 ? inext : i + 1);
         const double an = av_of(inext);
         seek(ka + (inext - i), an > 0 ? an : 0.0);
         i = inext;
@@ -673,12 +696,14 @@ __device__ __forceinline__ void aw_scan(P T, P G, const int n, const int ntau, c
         seek(kc, av > 0 ? av : 0.0);
     }
     for (int i = c - 1; i >= 0;) {
-        const int k2 = i + koff < n - 1 ? i + koff : n - 1;
+        const double ti = tau(i);
+        const int ko = koff_at(i, ti);
+        const int k2 = i + ko < n - 1 ? i + ko : n - 1;
         const double g2 = G[k2] > 0.0 ? G[k2] : 0.0;
         UB = UB < g2 ? UB : g2;
         const double Vp = (((UB + G0) + M) - mx) + dd; // AW_IN(a_j) >= G[bracket(a_j)] − dd
         if (!(Vp - dd > 0.0)) break; // AW_IN(a_j) >= 0 for every j: all pruned
-        const double av = av_of(i), xa = av > 0 ? av : 0.0;
+        const double av = (ti - xi) + icc, xa = av > 0 ? av : 0.0;
         bwd(xa);
         const double lb = av >= 0 ? ga0 : 0.0;
         if (!(lb >= Vp)) {
@@ -2100,9 +2125,12 @@ __global__ __launch_bounds__(256) void ready_fail_kernel(const int32_t* __restri
     if (__hip_atomic_load(gave_up, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n_pts; i += (int64_t)gridDim.x * 256) {
         out.xi[i] = NAN;
+        out.tau_in_unc[i] = NAN;
+        out.tau_out_unc[i] = NAN;
         out.aw_max[i] = NAN;
         out.tol[i] = INFINITY;
         out.status[i] = SBR_ENGINE_SCHED;
+        if (out.iters) out.iters[i] = 0;
     }
 }
 

@@ -779,6 +779,9 @@ struct SocialRhsRing {
     static constexpr bool kPinTableau = false;
 };
 
+#ifndef SBR_SOCIAL_PAR_STAGES
+#define SBR_SOCIAL_PAR_STAGES 1 // SocialRhsCoop: the five stage lookups of a step on lanes 0..4 at once
+#endif
 #ifndef SBR_SOCIAL_COOP
 #define SBR_SOCIAL_COOP 1 // a wave left with one live point runs it on all 64 lanes (SocialRhsCoop)
 #endif
@@ -863,9 +866,57 @@ struct SocialRhsCoop {
         last_aw = a;
         return ((1.0 - x) * beta) * a;
     }
+    // lane k's copy of x from lane `src` (ds_bpermute, 64-bit as two dwords)
+    __device__ __forceinline__ static double perm_d(double x, int src)
+    {
+        const uint64_t u = sbr_dbits(x);
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)(uint32_t)u);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)(uint32_t)(u >> 32));
+        return sbr_bitsd(((uint64_t)hi << 32) | lo);
+    }
     __device__ __forceinline__ void prepare(double t, double dt)
     {
         const double xs[5] = {fma(C1, dt, t), fma(C2, dt, t), fma(C3, dt, t), fma(C4, dt, t), t + dt};
+#if SBR_SOCIAL_PAR_STAGES
+        // The five stage lookups side by side (SBR_SOCIAL_PAR_STAGES): the stage times depend on
+        // t and dt only, so their brackets are five ballots over the window, and lane k runs stage
+        // k's lerp — the same operands and operations as lerp_j, hence the same bits — on the
+        // window knots it fetches with ds_bpermute; the five values come back by readlane.  One
+        // division and one lerp of wave time instead of five, off the serial RK chain.  Any
+        // stage time off the grid or past the window's last interval takes the serial form.
+        {
+            bool fast = n >= 2;
+#pragma unroll
+            for (int k = 0; k < 5; k++) fast &= xs[k] >= tfirst && xs[k] <= tlast;
+            if (fast) {
+                const int lane = (int)(threadIdx.x & 63);
+                int src = 0;
+                double xl = xs[4];
+#pragma unroll
+                for (int k = 0; k < 5; k++) {
+                    const int c = __popcll(__ballot(wt <= xs[k]));
+                    // bracket j = wb + c − 1 (searchsortedlast), clamped to n − 2 as lerp_j does;
+                    // window lane q = j − wb must hold both operand knots (q < 63)
+                    int q = c - 1;
+                    q = q > n - 2 - wb ? n - 2 - wb : q;
+                    fast &= c >= 1 && c < 64 && q >= 0 && q < 63;
+                    src = lane == k ? q : src;
+                    xl = lane == k ? xs[k] : xl;
+                }
+                if (fast) {
+                    const double t0 = perm_d(wt, src), t1 = perm_d(wt, src + 1);
+                    const double v0 = perm_d(wv, src), v1 = perm_d(wv, src + 1);
+                    const double d = (xl - t0) / (t1 - t0);
+                    const double a = v0 * (1.0 - d) + v1 * d;
+#pragma unroll
+                    for (int k = 0; k < 5; k++) aw[k] = lane_d(a, k);
+                    last_aw = aw[4];
+                    return;
+                }
+                slow++;
+            }
+        }
+#endif
 #pragma unroll
         for (int k = 0; k < 5; k++) {
             const bool in = n >= 2 && xs[k] >= tfirst && xs[k] <= tlast;
@@ -1483,7 +1534,11 @@ __global__ __launch_bounds__(64, SBR_SOCIAL_MINW) void social_iter_kernel(const 
     if (!in_pool) {
         const int cnt = *count;
         int L = SBR_SOCIAL_WAVES ? (cnt + nbs - 1) / nbs : 64;
-        L = L < 1 ? 1 : (L > 64 ? 64 : L);
+        // the ring holds kRingLanes lanes: the host's nbs = ⌈n_pts / kRingLanes⌉ >= ⌈cnt / kRingLanes⌉
+        // keeps L within it; the clamp stops a future change of that arithmetic from letting lanes
+        // share ring slots (which in_ring() would trust)
+        constexpr int kLmax = SBR_SOCIAL_RING ? kRingLanes : 64;
+        L = L < 1 ? 1 : (L > kLmax ? kLmax : L);
 #if SBR_SOCIAL_COOP
         if (L == 1) { // one point per wave: the whole wave runs it
             const int w = blockIdx.x;

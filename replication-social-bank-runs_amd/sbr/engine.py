@@ -236,7 +236,7 @@ class Engine:
                     status=int(st[0]), tau=tau[:k].copy(), hr=hr[:k].copy(), aw_cum=aw[:k].copy())
 
     def equilibrium_on_knots(self, t, G, beta, eta, t_end, u, p, kappa, lam, max_iters: int = 100,
-                             paths: bool = True) -> dict:
+                             paths: bool = True, exhaustive: bool = False) -> dict:
         """solve_equilibrium_baseline(lr, econ) + get_AW_functions!(r) (solver.jl:413-462, 553-576)
         on the learning knots the caller holds (t, G = lr.learning_cdf's knots and values) for each
         u — no learning ODE (sbr_equilibrium_on_knots).  The knots and the hazard path stay on the
@@ -258,9 +258,10 @@ class Engine:
         base = res.ctypes.data
         soa = _lib.ResultSoA(base, base + 8 * nu, base + 16 * nu, base + 24 * nu, base + 32 * nu, base + 40 * nu,
                              base + 44 * nu)
-        opts = self._knot_opts.get(max_iters)
+        opts = self._knot_opts.get((max_iters, exhaustive))
         if opts is None:
-            opts = self._knot_opts[max_iters] = _lib.default_opts(bisect_max_iters=max_iters)
+            opts = self._knot_opts[(max_iters, exhaustive)] = _lib.default_opts(
+                bisect_max_iters=max_iters, flags=_lib.SBR_FLAG_EXHAUSTIVE if exhaustive else 0)
         cap = n + 1
         nt = ctypes.c_int64()
         if paths:
@@ -283,7 +284,7 @@ class Engine:
         return out
 
     def hetero_equilibrium_on_knots(self, t, G, betas, dist, eta, t_end, u, p, kappa, lam,
-                                    paths: bool = True) -> dict:
+                                    paths: bool = True, exhaustive: bool = False) -> dict:
         """solve_equilibrium_hetero(lr_hetero, econ) + get_AW_functions_hetero! on the knots a
         LearningResultsHetero holds (t [n], G [n, K] = the learning_cdfs' values) for each u — no
         learning ODE (sbr_hetero_equilibrium_on_knots; knots, CDFs and the K hazards stay on the
@@ -309,7 +310,7 @@ class Engine:
         hr = np.empty((K, cap)) if paths else None
         aw = np.empty(cap) if paths else None
         nt = ctypes.c_int64()
-        opts = _lib.default_opts(early_exit_nan_run=0)
+        opts = _lib.default_opts(early_exit_nan_run=0, flags=_lib.SBR_FLAG_EXHAUSTIVE if exhaustive else 0)
         rc = self._L.sbr_hetero_equilibrium_on_knots(self._ctx, K, _ptr(t), _ptr(G), n, _ptr(betas), _ptr(dist), eta,
                                                      t_end, _ptr(u), nu, p, kappa, lam, ctypes.byref(opts),
                                                      ctypes.byref(soa), _ptr(tin), _ptr(tout), _ptr(hr), _ptr(aw),

@@ -270,3 +270,60 @@ def test_hetero_mirror_learns_once(engine, oracle):
         assert len(r.HRs) == len(g.dist)
         for k, hr in enumerate(r.HRs):
             assert np.array_equal(hr.coefs, o["hr"][k])
+
+
+# ------------------------------------------------ AW_max bounds at the knot-separation edges
+def _crowd(t, G, picks, sep, K=None):
+    """t / G with one extra knot after each index in `picks`, `sep`·t[n−1] past it (G between its
+    neighbours' values, so G stays nondecreasing): consecutive knots just above (sep = 2e-15) or
+    below (sep = 0.5e-15) the 1e-15·t[n−1] separation the AW bounds test (Summ::koff)."""
+    tn, Gn = [t[0]], [G[0]]
+    for i in range(len(t) - 1):
+        if i in picks:
+            tn.append(t[i] + sep * t[-1])
+            Gn.append(G[i] + (G[i + 1] - G[i]) * 1e-3)
+        tn.append(t[i + 1])
+        Gn.append(G[i + 1])
+    return np.asarray(tn), np.asarray(Gn) if K is None else np.stack(Gn)
+
+
+@pytest.mark.parametrize("sep", [2e-15, 0.5e-15])
+def test_aw_bounds_at_knot_separation_edge(engine, oracle, sep):
+    """AW_OUT(b_j) is bounded by G[j + 1] only when consecutive knots are more than
+    1e-15·t[n−1] apart (else G[j + 2]), and by G[j] where b_j = t[j] exactly (SBR_AW_OWN).  Knots
+    crowded to 2e-15 / 0.5e-15·t[n−1] around the AW peak, the buffers and ξ of a u sweep: the
+    pruned AW_max (aw_scan / branch and bound) equals the exhaustive evaluation bit for bit,
+    and both equal the oracle."""
+    t, G, _ = oracle.learn_logistic(1.0, 30.0)
+    picks = set(range(200, len(t) - 200, 37))
+    tc, Gc = _crowd(t, G, picks, sep)
+    assert np.all(np.diff(tc) > 0) and np.all(np.diff(Gc) >= 0)
+    u = sbr.julia_range("0.001", "0.2", 400)
+    a = engine.equilibrium_on_knots(tc, Gc, 1.0, 15.0, 30.0, u, 0.5, 0.6, 0.01, paths=False)
+    b = engine.equilibrium_on_knots(tc, Gc, 1.0, 15.0, 30.0, u, 0.5, 0.6, 0.01, paths=False, exhaustive=True)
+    for f in FIELDS:
+        assert same(a[f], b[f]), f
+    assert np.array_equal(a["status"], b["status"]) and np.array_equal(a["iters"], b["iters"])
+    run = (a["status"] & sbr.STATUS["SBR_RUN"]) > 0
+    assert run.sum() > 100
+    for j in range(0, 400, 23):
+        o = oracle.equilibrium(tc, Gc, 1.0, 15.0, 30.0, float(u[j]), 0.5, 0.6, 0.01)
+        for f in FIELDS:
+            assert same(a[f][j], o[f]), (j, f)
+
+
+@pytest.mark.parametrize("sep", [2e-15, 0.5e-15])
+def test_hetero_aw_bounds_at_knot_separation_edge(engine, oracle, sep):
+    """The same for the heterogeneity branch and bound (SBR_HET_K1): a config-4 column's knots
+    crowded to 2e-15 / 0.5e-15·t[n−1], 60 u: pruned == exhaustive bit for bit."""
+    c4 = sbr.hetero_config4(64, 60, 8)
+    i = 37
+    t, G, _ = oracle.learn_hetero(c4.betas[i], c4.dist, c4.t_end[i])
+    picks = set(range(100, len(t) - 100, 29))
+    tc, Gc = _crowd(t, list(G), picks, sep, K=8)
+    assert np.all(np.diff(tc) > 0)
+    args = (tc, np.ascontiguousarray(Gc), c4.betas[i], c4.dist, c4.eta[i], c4.t_end[i], c4.u, c4.p, c4.kappa, c4.lam)
+    a = engine.hetero_equilibrium_on_knots(*args, paths=False)
+    b = engine.hetero_equilibrium_on_knots(*args, paths=False, exhaustive=True)
+    check_hetero(a, b, "pruned vs exhaustive", paths=False)
+    assert (a["status"] & sbr.STATUS["SBR_RUN"]).any()
