@@ -50,6 +50,9 @@ typedef struct {
     int32_t hetero_max_iters;   /* heterogeneity_solver.jl:49 max_iters = 500 */
     int32_t flags;              /* SBR_FLAG_* */
     int32_t pad;                /* social sweep: knot capacity per buffer (0 = default 98304) */
+    double xi_guess;            /* solver.jl:413,441 ξ_guess: compute_ξ's first iterate; NaN = the default
+                                   midpoint (τ̄_IN + τ̄_OUT)/2.  sbr_equilibrium_on_knots only: the other
+                                   entry points return SBR_EARG when it is set */
 } sbr_opts;
 
 /* Evaluate every τ̄ knot of the crossing scan and of the AW path (no block
@@ -88,7 +91,7 @@ typedef struct {
     int32_t* iters;      /* bisection iterations (may be NULL)  */
 } sbr_result_soa;
 
-/* Fills *o with the reference defaults (eps() tolerances, 1e6, 100, 5, 65536, 500). */
+/* Fills *o with the reference defaults (eps() tolerances, 1e6, 100, 5, 65536, 500, ξ_guess = NaN). */
 void sbr_default_opts(sbr_opts* o);
 
 /* Creates a context on HIP device `device` (the caller's rank-local GPU). */
@@ -213,6 +216,20 @@ int sbr_equilibrium_on_knots(sbr_ctx* ctx, const double* t, const double* G, int
                              double eta, double t_end, const double* u, int64_t n_u, double p, double kappa,
                              double lambda, const sbr_opts* opts, sbr_result_soa* out, double* tau, double* hr,
                              double* aw_cum, double* aw_out, double* aw_in, int64_t cap, int64_t* n_tau);
+
+/*
+ * The same on an explicit learning pdf: pdf[i] = the pdf's value at knot t[i] (n_knots values;
+ * its LinearInterpolation feeds hazard_rate(p, λ, pdf, η), solver.jl:153-185) instead of
+ * βG(1−G).  The social drop-in's final SolvedModel (social_learning_solver.jl:139-143, 262) is
+ * this call on the last iterate's knots with pdf = (1 − G)·β·AW_{n−1}
+ * (compute_pdf_social_learning, social_learning_dynamics.jl:98-114): its HR and AW paths are
+ * the social point's, bit for bit.  Residency is keyed by t, G, pdf, η, p, λ.
+ */
+int sbr_equilibrium_on_knots_pdf(sbr_ctx* ctx, const double* t, const double* G, const double* pdf,
+                                 int64_t n_knots, double eta, double t_end, const double* u, int64_t n_u, double p,
+                                 double kappa, double lambda, const sbr_opts* opts, sbr_result_soa* out, double* tau,
+                                 double* hr, double* aw_cum, double* aw_out, double* aw_in, int64_t cap,
+                                 int64_t* n_tau);
 
 /*
  * Heterogeneity extension sweep — for each column c (group rates

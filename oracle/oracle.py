@@ -43,6 +43,8 @@ def lib() -> ctypes.CDLL:
         L.sbro_equilibrium.argtypes = [_P, _P, _I64, _D, _D, _D, _D, _D, _D, _D, _I32, _P, _P, _P, _P, _P, _P, _P]
         L.sbro_equilibrium_paths.restype = None
         L.sbro_equilibrium_paths.argtypes = [_P, _P, _I64, _D, _D, _D, _D, _D, _D, _D, _I32] + [_P] * 9
+        L.sbro_equilibrium_paths_pdf.restype = None
+        L.sbro_equilibrium_paths_pdf.argtypes = [_P, _P, _P, _I64, _D, _D, _D, _D, _D, _D, _I32] + [_P] * 9
         L.sbro_sweep_baseline.restype = ctypes.c_int
         L.sbro_sweep_baseline.argtypes = [_P, _P, _P, _D, _P, _I64, _I64, _D, _D, _D, _I32, _I32] + [_P] * 8
         L.sbro_apply_early_exit.restype = None
@@ -73,6 +75,14 @@ def learn_logistic(beta, t_end, x0=1e-4, t0=0.0, rtol=EPS, atol=EPS, maxiters=1_
     return t[:n].copy(), G[:n].copy(), dict(naccept=int(stats[0]), nreject=int(stats[1]), status=int(stats[2]),
                                             t_switch=float(stats[4:5].view(np.float64)[0]),
                                             nswitch=int(stats[5]), nstiff=int(stats[6]))
+
+
+def set_xi_guess(g: float = float("nan")) -> None:
+    """compute_ξ's first iterate ξ_guess for the following calls (NaN: the default midpoint)."""
+    L = lib()
+    L.sbro_set_xi_guess.restype = None
+    L.sbro_set_xi_guess.argtypes = [ctypes.c_double]
+    L.sbro_set_xi_guess(g)
 
 
 def equilibrium(t, G, beta, eta, t_end, u, p, kappa, lam, max_iters=100, paths=False):
@@ -109,6 +119,28 @@ def equilibrium_paths(t, G, beta, eta, t_end, u, p, kappa, lam, max_iters=100):
     nhr = np.zeros(1, np.int64)
     lib().sbro_equilibrium_paths(_ptr(t), _ptr(G), n, beta, eta, t_end, u, p, kappa, lam, max_iters, _ptr(res),
                                  _ptr(st), _ptr(it), *[_ptr(b) for b in bufs], _ptr(nhr))
+    k = int(nhr[0])
+    out = dict(xi=res[0], tau_in_unc=res[1], tau_out_unc=res[2], aw_max=res[3], tol=res[4], status=int(st[0]),
+               iters=int(it[0]), n_hr=k)
+    for name, b in zip(("hr_tau", "hr", "aw_cum", "aw_out", "aw_in"), bufs):
+        out[name] = b[:k]
+    return out
+
+
+def equilibrium_paths_pdf(t, G, pdf, eta, t_end, u, p, kappa, lam, max_iters=100):
+    """equilibrium_paths on an explicit learning pdf given by its knot values (hazard_rate(p, λ,
+    LinearInterpolation(t, pdf), η); the social extension's (1 − G)·β·AW_{n−1})."""
+    t = np.ascontiguousarray(t, np.float64)
+    G = np.ascontiguousarray(G, np.float64)
+    pdf = np.ascontiguousarray(pdf, np.float64)
+    n = len(t)
+    res = np.zeros(5)
+    st = np.zeros(1, np.uint32)
+    it = np.zeros(1, np.int32)
+    bufs = [np.full(n + 1, np.nan) for _ in range(5)]
+    nhr = np.zeros(1, np.int64)
+    lib().sbro_equilibrium_paths_pdf(_ptr(t), _ptr(G), _ptr(pdf), n, eta, t_end, u, p, kappa, lam, max_iters,
+                                     _ptr(res), _ptr(st), _ptr(it), *[_ptr(b) for b in bufs], _ptr(nhr))
     k = int(nhr[0])
     out = dict(xi=res[0], tau_in_unc=res[1], tau_out_unc=res[2], aw_max=res[3], tol=res[4], status=int(st[0]),
                iters=int(it[0]), n_hr=k)

@@ -687,11 +687,16 @@ static void optimal_buffer(double u, const double* tau, const double* hr, int64_
 /* compute_ξ bisection (solver.jl:308-376)                                  */
 /* returns status bits; *xi / *tol set; *iters = loop iterations executed   */
 /* ------------------------------------------------------------------------ */
+/* compute_ξ's ξ_guess (solver.jl:309-312; solve_equilibrium_baseline passes it through, :413,441):
+ * NaN = the default midpoint.  Set by tests around single calls (sbro_set_xi_guess). */
+static double g_xi_guess = NAN;
+void sbro_set_xi_guess(double g) { g_xi_guess = g; }
+
 static uint32_t compute_xi(double tin, double tout, const double* t, const double* G, int64_t n, double kappa,
                            int32_t max_iters, double* xi_out, double* tol_out, int32_t* iters)
 {
     const double tolerance = 10.0 * sbr_jl_eps(kappa);
-    double xnew = (tin + tout) / 2.0, xmin = tin, xmax = tout;
+    double xnew = g_xi_guess == g_xi_guess ? g_xi_guess : (tin + tout) / 2.0, xmin = tin, xmax = tout;
     int oob = 0;
     *xi_out = NAN;
     *tol_out = INFINITY;
@@ -800,6 +805,26 @@ static void equilibrium_point(const double* t, const double* G, int64_t n, const
 
 /* public single-point API on caller-provided knots (used by tests): solve_equilibrium_baseline on a
  * LearningResults' knots (solver.jl:413-462) + get_AW's three paths (solver.jl:495-532) */
+/* the same on an explicit learning pdf's knot values g (hazard_rate(p, λ, pdf, η) for any pdf on
+ * the knots, e.g. the social extension's (1 − G)·β·AW_{n−1}, social_learning_dynamics.jl:98-114) */
+void sbro_equilibrium_paths_pdf(const double* t, const double* G, const double* g, int64_t n, double eta,
+                                double t_end, double u, double p, double kappa, double lambda, int32_t max_iters,
+                                double* res, uint32_t* status, int32_t* iters, double* hr_tau, double* hr_v,
+                                double* aw, double* aw_out, double* aw_in, int64_t* n_hr)
+{
+    hazard_t h;
+    hazard_rate(t, g, n, p, lambda, eta, 0, &h);
+    point_t r;
+    equilibrium_point3(t, G, n, &h, t_end, u, kappa, max_iters, &r, aw, aw_out, aw_in);
+    res[0] = r.xi; res[1] = r.tin; res[2] = r.tout; res[3] = r.aw_max; res[4] = r.tol;
+    *status = r.status;
+    *iters = r.iters;
+    if (n_hr) *n_hr = h.oob ? 0 : h.n;
+    if (hr_tau && !h.oob) memcpy(hr_tau, h.tau, (size_t)h.n * sizeof(double));
+    if (hr_v && !h.oob) memcpy(hr_v, h.hr, (size_t)h.n * sizeof(double));
+    hazard_free(&h);
+}
+
 void sbro_equilibrium_paths(const double* t, const double* G, int64_t n, double beta, double eta, double t_end,
                             double u, double p, double kappa, double lambda, int32_t max_iters, double* res,
                             uint32_t* status, int32_t* iters, double* hr_tau, double* hr_v, double* aw,

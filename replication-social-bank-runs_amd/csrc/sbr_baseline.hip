@@ -332,11 +332,19 @@ __device__ __forceinline__ void hazard_column(const int b, const double BETA, co
         }
         return;
     }
+    // the pdf at knot i: compute_pdf_symbolic_baseline's βG(1 − G) (learning.jl:161-173), or the
+    // caller's values (a.pdf: the interpolant of another pdf on the same knots)
+    const double* __restrict__ PD = a.pdf;
+    auto pdf_k = [&](int i) -> double {
+        if (PD) return PD[i];
+        const double x = Gv[i];
+        return (BETA * x) * (1.0 - x);
+    };
     auto pdf_at = [&](int i) -> double {
-        if (i < m) { const double x = Gv[i]; return (BETA * x) * (1.0 - x); }
+        if (i < m) return pdf_k(i);
         // η on bracket [m-1, m]
-        const double g0 = (BETA * Gv[m - 1]) * (1.0 - Gv[m - 1]);
-        const double g1 = (BETA * Gv[m]) * (1.0 - Gv[m]);
+        const double g0 = pdf_k(m - 1);
+        const double g1 = pdf_k(m);
         const double d = (ETA - T[m - 1]) / (T[m] - T[m - 1]);
         return g0 * (1.0 - d) + g1 * d;
     };
@@ -359,14 +367,14 @@ __device__ __forceinline__ void hazard_column(const int b, const double BETA, co
                 const int i = tid + HZ_BLOCK * j;
                 const int ic = i < m ? i : m - 1;
                 tv[j] = T[ic];
-                gk[j] = Gv[ic];
+                gk[j] = PD ? PD[ic] : Gv[ic];
             }
 #pragma unroll
             for (int j = 0; j < HZ_REG; j++) {
                 const int i = tid + HZ_BLOCK * j;
                 const double x = gk[j];
                 const double ti = i < m ? tv[j] : ETA;
-                const double g = i < m ? (BETA * x) * (1.0 - x) : pdf_eta;
+                const double g = i < m ? (PD ? x : (BETA * x) * (1.0 - x)) : pdf_eta;
                 const double E = sbr_exp(lam * ti);
                 tv[j] = ti;
                 egv[j] = E * g;        // e_i = exp(λτ̄_i)·pdf_i
@@ -722,6 +730,53 @@ __device__ __forceinline__ void aw_scan(P T, P G, const int n, const int ntau, c
         const double an = av_of(inext);
         seek(ks, an > 0 ? an : 0.0);
         i = inext;
+    }
+}
+
+// compute_ξ (solver.jl:308-376) from an arbitrary first iterate ξ_guess (the single-point kernel's
+// knots-in calls only: the sweep kernel carries none of this): the reference's iteration as
+// written, every lookup bracketed by a search over the whole grid (the oracle's compute_xi).  A
+// lookup outside [t[0], t[n−1]] — G at a constrained time, searchsortedlast(grid, ξ_old) below the
+// first knot or at the last, the ε probes — is the interpolant's BoundsError.
+template <class P>
+__device__ __forceinline__ void bisect_plain(P T, P G, const int n, const double tlo, const double thi,
+                                             const bool trunc, const double tin, const double tout,
+                                             const double guess, const double kappa, const double tolerance,
+                                             const int max_iters, PointResult& r, uint32_t& flag, uint32_t& s,
+                                             double& xi, double& tolr)
+{
+    double xnew = guess, xmin = tin, xmax = tout;
+    for (int iter = 1; iter <= max_iters; iter++) {
+        r.iters = iter;
+        if (collapsed(xmin - xmax)) { s = SBR_NO_RUN_COLLAPSE; return; }
+        if (iter == max_iters - 1) { s = SBR_NO_RUN_MAXITER; return; }
+        const double xo = xnew;
+        const double ic = dmin(tin, xo), oc = dmin(tout, xo);
+        double Goc = 0.0, Gic = 0.0;
+        if (in_range(oc, tlo, thi, trunc, flag)) Goc = lerp_at(T, G, n, ssl_range(T, 0, n - 1, oc), oc);
+        if (in_range(ic, tlo, thi, trunc, flag)) Gic = lerp_at(T, G, n, ssl_range(T, 0, n - 1, ic), ic);
+        if (!(xo >= tlo)) { flag |= SBR_OOB; return; } // searchsortedlast = 0: grid[0]
+        const int j = ssl_range(T, 0, n - 1, xo);
+        if (j + 1 >= n) { flag |= trunc ? SBR_ENGINE_TRUNC : SBR_OOB; return; }
+        const double eps = T[j + 1] - T[j];
+        const double xoe = oc + eps, xie = ic + eps;
+        const bool oke = in_range(xoe, tlo, thi, trunc, flag);
+        const bool oki = in_range(xie, tlo, thi, trunc, flag);
+        if (flag) return;
+        const double AW = Goc - Gic;
+        const double err = AW - kappa;
+        if (fabs(err) <= tolerance) {
+            double Goce = 0.0, Gice = 0.0;
+            if (oke) Goce = lerp_at(T, G, n, ssl_range(T, 0, n - 1, xoe), xoe);
+            if (oki) Gice = lerp_at(T, G, n, ssl_range(T, 0, n - 1, xie), xie);
+            if (Goce - Gice >= AW) { s = SBR_RUN; xi = xo; tolr = fabs(err); }
+            else s = SBR_FALSE_EQ;
+            return;
+        } else if (err > 0) {
+            xmax = xo; xnew = 0.5 * (xo + xmin);
+        } else {
+            xmin = xo; xnew = 0.5 * (xo + xmax);
+        }
     }
 }
 
@@ -1701,7 +1756,7 @@ template <class P>
 __device__ __forceinline__ void point_wave(P T, P G, P H, const int n, const int ntau, const int nle,
                                            const double ETA, const double T1, const bool trunc, const double u,
                                            const double kappa, const int max_iters, const uint32_t lbits,
-                                           PointResult& r)
+                                           PointResult& r, const double guess)
 {
     const int lane = threadIdx.x & 63;
     r.xi = NAN; r.aw = NAN; r.tol = INFINITY; r.iters = 0; r.status = 0;
@@ -1755,6 +1810,11 @@ __device__ __forceinline__ void point_wave(P T, P G, P H, const int n, const int
     // ---------------- compute_ξ (solver.jl:308-376): the exact iteration ----------------
     uint32_t flag = 0;
     const double tolerance = 10.0 * sbr_jl_eps(kappa);
+    uint32_t s = SBR_NO_RUN_MAXITER;
+    double xi = NAN, tolr = INFINITY;
+    if (guess == guess) { // ξ_guess: the plain iteration (solve_from_buffers), wave-uniform
+        bisect_plain(T, G, n, tlo, thi, trunc, tin, tout, guess, kappa, tolerance, max_iters, r, flag, s, xi, tolr);
+    } else {
     double xnew = (tin + tout) / 2.0, xmin = tin, xmax = tout;
     const bool okmin = co_in_range(xmin, tlo, thi, trunc, flag);
     const bool okmax = co_in_range(xmax, tlo, thi, trunc, flag);
@@ -1762,8 +1822,6 @@ __device__ __forceinline__ void point_wave(P T, P G, P H, const int n, const int
     int jlo = wave_ssl(T, 0, n - 1, xmin);
     int jhi = wave_ssl(T, 0, n - 1, xmax);
     const int jtin = jlo;
-    uint32_t s = SBR_NO_RUN_MAXITER;
-    double xi = NAN, tolr = INFINITY;
 #if SBR_COOP_SPEC
     // Rounds of six bisection levels at once: lane ℓ < 63 evaluates node k = ℓ + 1 of the
     // depth-6 tree below the current state (heap order; child 2k follows err > 0, 2k + 1
@@ -1897,6 +1955,7 @@ __device__ __forceinline__ void point_wave(P T, P G, P H, const int n, const int
         }
     }
 #endif
+    } // default first iterate
     if (flag) { r.status = flag | lbits; return; }
     if (s != SBR_RUN) { r.status = s | lbits; return; }
     // the AW stage's own range checks (solve_from_buffers: G(0), then the path's last τ̄ — the
@@ -1986,7 +2045,7 @@ __global__ __launch_bounds__(CO_BLOCK) void point_coop_kernel(LearnBufs L, const
             r.xi = NAN; r.aw = NAN; r.tol = INFINITY; r.iters = 0; r.tin = NAN; r.tout = NAN;
             r.status = ((lst & SBR_ARG_INVALID) || !(uj >= 0.0)) ? SBR_ARG_INVALID : (SBR_OOB | lbits);
         } else {
-            point_wave(T, G, H, n, ntau, nle, ETA, T1, trunc, uj, a.kappa, a.max_iters, lbits, r);
+            point_wave(T, G, H, n, ntau, nle, ETA, T1, trunc, uj, a.kappa, a.max_iters, lbits, r, a.xi_guess);
         }
         if (threadIdx.x == 0) {
             s_r[0] = r.xi; s_r[1] = r.tin; s_r[2] = r.tout; s_r[3] = r.aw; s_r[4] = r.tol;

@@ -126,6 +126,7 @@ struct sbr_ctx {
     int64_t kn_n = 0;
     double kn_key[4] = {};
     std::vector<double> kn_t, kn_G, kn_hr; // host copies of the resident knots and HR
+    std::vector<double> kn_pdf;            // sbr_equilibrium_on_knots_pdf's pdf values (empty: βG(1 − G))
     int32_t kn_m = 0, kn_ntau = 0;         // knots <= η; τ̄ entries (0: the hazard's BoundsError)
     // single-u calls: mapped, coherent host memory the kernel reads t_end / u from and writes the
     // results and paths to (no copy launches per call) — host view and device view
@@ -416,6 +417,11 @@ int ensure_res_pin(sbr_ctx* c, size_t bytes)
     c->res_pin_bytes = bytes;
     return SBR_OK;
 }
+
+// ξ_guess (solver.jl:413,441) is honoured by sbr_equilibrium_on_knots, which solves on the caller's
+// whole knot grid; the sweeps' truncated learning (DESIGN.md §Truncated learning) and the
+// extensions' own bisections start at the reference's defaults, so they refuse a guess
+bool guess_set(const sbr_opts* o) { return o && o->xi_guess == o->xi_guess; }
 
 // EconomicParameters / LearningParameters scalar checks (model.jl:31-35, 71-76)
 bool scalars_valid(double x0, double p, double kappa, double lambda)
@@ -773,6 +779,7 @@ void sbr_default_opts(sbr_opts* o)
     o->hetero_max_iters = 500;
     o->flags = 0;
     o->pad = 0;
+    o->xi_guess = __builtin_nan(""); // compute_ξ's default first iterate, the midpoint (solver.jl:309)
 }
 
 int sbr_init(int device, sbr_ctx** out)
@@ -895,6 +902,7 @@ int sbr_sweep_baseline_dev(sbr_ctx* c, void* stream, const double* beta, const d
                            double x0, const double* u, int64_t n_beta, int64_t n_u, double p, double kappa,
                            double lambda, const sbr_opts* opts, sbr_result_soa* out)
 {
+    if (guess_set(opts)) return fail(c, SBR_EARG, "xi_guess: only sbr_equilibrium_on_knots takes a first iterate");
     SBR_SINGLE_DEVICE(c);
     if (!c || !out || !out->xi || !out->tau_in_unc || !out->tau_out_unc || !out->aw_max || !out->tol || !out->status)
         return SBR_EARG;
@@ -921,6 +929,7 @@ int sbr_sweep_baseline_batch_dev(sbr_ctx* c, void* stream, int64_t n_batch, cons
                                  const double* t_end, double x0, const double* u, int64_t n_beta, int64_t n_u,
                                  double p, double kappa, double lambda, const sbr_opts* opts, sbr_result_soa* out)
 {
+    if (guess_set(opts)) return fail(c, SBR_EARG, "xi_guess: only sbr_equilibrium_on_knots takes a first iterate");
     SBR_SINGLE_DEVICE(c);
     if (!c || !out || !beta || !eta || !t_end || !u) return SBR_EARG;
     if (!out->xi || !out->tau_in_unc || !out->tau_out_unc || !out->aw_max || !out->tol || !out->status) return SBR_EARG;
@@ -1028,6 +1037,7 @@ int sbr_sweep_baseline(sbr_ctx* c, const double* beta, const double* eta, const 
                        const double* u, int64_t n_beta, int64_t n_u, double p, double kappa, double lambda,
                        const sbr_opts* opts, sbr_result_soa* out)
 {
+    if (guess_set(opts)) return fail(c, SBR_EARG, "xi_guess: only sbr_equilibrium_on_knots takes a first iterate");
     if (!c || !out || !beta || !eta || !t_end || !u) return SBR_EARG;
     if (n_beta <= 0 || n_u <= 0) return fail(c, SBR_EARG, "grid size");
     if (!scalars_valid(x0, p, kappa, lambda)) return fail(c, SBR_EARG, "ArgumentError: x0/p/kappa/lambda");
@@ -1108,6 +1118,7 @@ int sbr_sweep_interest_dev(sbr_ctx* c, void* stream, const double* beta, const d
                            double lambda, double r, double delta, const sbr_opts* opts, sbr_result_soa* out,
                            int64_t* rk_steps)
 {
+    if (guess_set(opts)) return fail(c, SBR_EARG, "xi_guess: only sbr_equilibrium_on_knots takes a first iterate");
     SBR_SINGLE_DEVICE(c);
     if (!c || !out || !out->xi || !out->tau_in_unc || !out->tau_out_unc || !out->aw_max || !out->tol || !out->status)
         return SBR_EARG;
@@ -1126,6 +1137,7 @@ int sbr_sweep_interest(sbr_ctx* c, const double* beta, const double* eta, const 
                        const double* u, int64_t n_beta, int64_t n_u, double p, double kappa, double lambda, double r,
                        double delta, const sbr_opts* opts, sbr_result_soa* out, int64_t* rk_steps)
 {
+    if (guess_set(opts)) return fail(c, SBR_EARG, "xi_guess: only sbr_equilibrium_on_knots takes a first iterate");
     if (!c || !out || !beta || !eta || !t_end || !u) return SBR_EARG;
     if (n_beta <= 0 || n_u <= 0) return fail(c, SBR_EARG, "grid size");
     if (!scalars_valid(x0, p, kappa, lambda)) return fail(c, SBR_EARG, "ArgumentError: x0/p/kappa/lambda");
@@ -1177,6 +1189,7 @@ int sbr_interest_point_paths(sbr_ctx* c, double beta, double eta, double t_end, 
                              uint32_t* status, double* tau, double* hr, double* V, double* aw_cum, int64_t cap,
                              int64_t* n_tau, int64_t* n_v)
 {
+    if (guess_set(opts)) return fail(c, SBR_EARG, "xi_guess: only sbr_equilibrium_on_knots takes a first iterate");
     SBR_ON_RANK0(c, sbr_interest_point_paths(c, beta, eta, t_end, x0, u, p, kappa, lambda, r, delta, opts, res, status, tau, hr, V, aw_cum, cap, n_tau, n_v));
     if (!c || !res || !status) return SBR_EARG;
     if (!scalars_valid(x0, p, kappa, lambda) || !(beta > 0) || !(eta > 0) || !(t_end > 0) || !(u >= 0))
@@ -1230,6 +1243,7 @@ int sbr_learn_baseline(sbr_ctx* c, const double* beta, const double* eta, const 
                        int64_t n_beta, int32_t stop_after_eta, const sbr_opts* opts, double* t_out, double* G_out,
                        int64_t cap, int32_t* n_knots, uint32_t* status)
 {
+    if (guess_set(opts)) return fail(c, SBR_EARG, "xi_guess: only sbr_equilibrium_on_knots takes a first iterate");
     SBR_ON_RANK0(c, sbr_learn_baseline(c, beta, eta, t_end, x0, n_beta, stop_after_eta, opts, t_out, G_out, cap, n_knots, status));
     if (!c || !beta || !eta || !t_end || n_beta <= 0 || cap <= 0) return SBR_EARG;
     if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
@@ -1264,6 +1278,7 @@ int sbr_solve_point_paths(sbr_ctx* c, double beta, double eta, double t_end, dou
                           double kappa, double lambda, const sbr_opts* opts, double* res, uint32_t* status,
                           double* tau, double* hr, double* aw_cum, int64_t cap, int64_t* n_tau)
 {
+    if (guess_set(opts)) return fail(c, SBR_EARG, "xi_guess: only sbr_equilibrium_on_knots takes a first iterate");
     SBR_ON_RANK0(c, sbr_solve_point_paths(c, beta, eta, t_end, x0, u, p, kappa, lambda, opts, res, status, tau, hr, aw_cum, cap, n_tau));
     if (!c || !res || !status) return SBR_EARG;
     if (!scalars_valid(x0, p, kappa, lambda) || !(beta > 0) || !(eta > 0) || !(t_end > 0) || !(u >= 0))
@@ -1311,14 +1326,15 @@ int sbr_solve_point_paths(sbr_ctx* c, double beta, double eta, double t_end, dou
 namespace {
 
 // byte offsets of sbr_equilibrium_on_knots' device block (and of its pinned mirror) for ck knots
-// and cu u values: [counters | β, η | t, G (packed by the call's n) | HR | t_end, u | results, paths]
+// and cu u values: [counters | β, η | t, G, pdf (packed by the call's n) | HR | t_end, u | results,
+// paths]
 struct KnotLayout {
     size_t sc, tg, hr, u, res, bytes;
     KnotLayout(size_t ck, size_t cu)
     {
         sc = 64;
         tg = 128;
-        hr = tg + 16 * ck;
+        hr = tg + 24 * ck;
         u = hr + 8 * (ck + 8);
         res = u + 8 * (cu + 8);
         bytes = res + 8 * (6 * cu + 3 * (ck + 1)) + 256;
@@ -1399,6 +1415,7 @@ int sbr_hetero_equilibrium_on_knots(sbr_ctx* c, int32_t K, const double* t, cons
                                     sbr_result_soa* out, double* tau_in, double* tau_out, double* hr, double* aw_total,
                                     int64_t cap, int64_t* n_tau)
 {
+    if (guess_set(opts)) return fail(c, SBR_EARG, "xi_guess: only sbr_equilibrium_on_knots takes a first iterate");
     SBR_ON_RANK0(c, sbr_hetero_equilibrium_on_knots(c, K, t, G, n, betas, dist, eta, t_end, u, n_u, p, kappa, lambda, opts, out, tau_in, tau_out, hr, aw_total, cap, n_tau));
     if (!c || !t || !G || !betas || !dist || !u || !out) return SBR_EARG;
     if (K != 1 && K != 2 && K != 3 && K != 4 && K != 8) return fail(c, SBR_EARG, "K must be 1, 2, 3, 4 or 8");
@@ -1526,12 +1543,17 @@ int sbr_hetero_equilibrium_on_knots(sbr_ctx* c, int32_t K, const double* t, cons
     return SBR_OK;
 }
 
-int sbr_equilibrium_on_knots(sbr_ctx* c, const double* t, const double* G, int64_t n, double beta, double eta,
-                             double t_end, const double* u, int64_t n_u, double p, double kappa, double lambda,
-                             const sbr_opts* opts, sbr_result_soa* out, double* tau, double* hr, double* aw_cum,
-                             double* aw_out, double* aw_in, int64_t cap, int64_t* n_tau)
+}  // extern "C"
+
+namespace {
+
+// sbr_equilibrium_on_knots (pdf == nullptr: the learning pdf βG(1 − G) of the knots' G) and
+// sbr_equilibrium_on_knots_pdf (the caller's pdf values on the same knots)
+int on_knots(sbr_ctx* c, const double* t, const double* G, const double* pdf, int64_t n, double beta, double eta,
+             double t_end, const double* u, int64_t n_u, double p, double kappa, double lambda, const sbr_opts* opts,
+             sbr_result_soa* out, double* tau, double* hr, double* aw_cum, double* aw_out, double* aw_in, int64_t cap,
+             int64_t* n_tau)
 {
-    SBR_ON_RANK0(c, sbr_equilibrium_on_knots(c, t, G, n, beta, eta, t_end, u, n_u, p, kappa, lambda, opts, out, tau, hr, aw_cum, aw_out, aw_in, cap, n_tau));
     if (!c || !t || !G || !u || !out) return SBR_EARG;
     if (n < 1 || n > (1 << 26) || n_u < 1 || n_u > (1 << 24)) return fail(c, SBR_EARG, "knot / u count");
     if (!scalars_valid(0.0, p, kappa, lambda) || !(beta > 0) || !(eta > 0) || !(t_end > 0))
@@ -1559,7 +1581,9 @@ int sbr_equilibrium_on_knots(sbr_ctx* c, const double* t, const double* G, int64
     if ((tau || hr || want_aw) && ntau > cap) return fail(c, SBR_EARG, "path capacity too small");
     const double key[4] = {beta, eta, p, lambda};
     const bool hit = c->kn_valid && c->kn_n == n && memcmp(c->kn_key, key, sizeof key) == 0 &&
-                     memcmp(c->kn_t.data(), t, (size_t)n * 8) == 0 && memcmp(c->kn_G.data(), G, (size_t)n * 8) == 0;
+                     memcmp(c->kn_t.data(), t, (size_t)n * 8) == 0 && memcmp(c->kn_G.data(), G, (size_t)n * 8) == 0 &&
+                     (pdf ? c->kn_pdf.size() == (size_t)n && memcmp(c->kn_pdf.data(), pdf, (size_t)n * 8) == 0
+                          : c->kn_pdf.empty());
     char* D = c->kn_dev;
     char* H = c->kn_pin;
     int32_t* dcnt = (int32_t*)D; // n_knots, n_tau, n_le, status, n_accept, n_reject
@@ -1582,8 +1606,10 @@ int sbr_equilibrium_on_knots(sbr_ctx* c, const double* t, const double* G, int64
             hs[1] = eta;
             memcpy(H + K.tg, t, (size_t)n * 8);
             memcpy(H + K.tg + (size_t)n * 8, G, (size_t)n * 8);
-            HIP_TRY(c, hipMemcpyAsync(D, H, K.tg + (size_t)n * 16, hipMemcpyHostToDevice, s), SBR_EDEVICE);
+            if (pdf) memcpy(H + K.tg + (size_t)n * 16, pdf, (size_t)n * 8);
+            HIP_TRY(c, hipMemcpyAsync(D, H, K.tg + (size_t)n * (pdf ? 24 : 16), hipMemcpyHostToDevice, s), SBR_EDEVICE);
             sbr::LearnArgs la{0.0, o.ode_reltol, o.ode_abstol, p, lambda, o.ode_maxiters, 1, 0, 0, nullptr, nullptr};
+            la.pdf = pdf ? dtg + 2 * n : nullptr;
             HIP_TRY(c, sbr::launch_hazard(dsc, dsc + 1, la, L, 1, s), SBR_EDEVICE);
             if (ntau > 0)
                 HIP_TRY(c, hipMemcpyAsync(H + K.hr, D + K.hr, (size_t)ntau * 8, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
@@ -1602,6 +1628,7 @@ int sbr_equilibrium_on_knots(sbr_ctx* c, const double* t, const double* G, int64
             sbr::EqArgs ea{kappa, 1, o.bisect_max_iters, c->lds_cap, want_aw ? zp : nullptr,
                            (o.flags & SBR_FLAG_EXHAUSTIVE) ? 1 : 0, (o.flags >> 8) & 7,
                            want_aw ? zp + ntau : nullptr, want_aw ? zp + 2 * ntau : nullptr, 1, dres};
+            ea.xi_guess = o.xi_guess;
             HIP_TRY(c, sbr::launch_point_coop(L, dsc + 1, zd, zd + 1, ea, r, s), SBR_EDEVICE);
         } else {
             double* hu = (double*)(H + K.u);
@@ -1610,10 +1637,23 @@ int sbr_equilibrium_on_knots(sbr_ctx* c, const double* t, const double* G, int64
             HIP_TRY(c, hipMemcpyAsync(du, hu, (nu + 1) * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
             const sbr::ResultSoA r{dres, dres + nu, dres + 2 * nu, dres + 3 * nu, dres + 4 * nu,
                                    (uint32_t*)(dres + 5 * nu), (int32_t*)(dres + 5 * nu) + nu};
-            sbr::EqArgs ea{kappa, (int32_t)n_u, o.bisect_max_iters, c->lds_cap_b, nullptr,
-                           (o.flags & SBR_FLAG_EXHAUSTIVE) ? 1 : 0, (o.flags >> 8) & 7, nullptr, nullptr, 1};
-            HIP_TRY(c, sbr::launch_equilibrium(L, dsc + 1, du, du + 1, ea, r, 1, s, n <= c->lds_cap_b ? 1 : 2),
-                    SBR_EDEVICE);
+            if (o.xi_guess == o.xi_guess) {
+                // ξ_guess: the single-point kernel once per u (its plain first-iterate bisection; the
+                // sweep kernel carries no guess path, it would cost the sweeps registers)
+                sbr::EqArgs ea{kappa, 1, o.bisect_max_iters, c->lds_cap, nullptr,
+                               (o.flags & SBR_FLAG_EXHAUSTIVE) ? 1 : 0, (o.flags >> 8) & 7, nullptr, nullptr, 1};
+                ea.xi_guess = o.xi_guess;
+                for (size_t j = 0; j < nu; j++) {
+                    const sbr::ResultSoA rj{r.xi + j, r.tau_in_unc + j, r.tau_out_unc + j, r.aw_max + j, r.tol + j,
+                                            r.status + j, r.iters + j};
+                    HIP_TRY(c, sbr::launch_point_coop(L, dsc + 1, du, du + 1 + j, ea, rj, s), SBR_EDEVICE);
+                }
+            } else {
+                sbr::EqArgs ea{kappa, (int32_t)n_u, o.bisect_max_iters, c->lds_cap_b, nullptr,
+                               (o.flags & SBR_FLAG_EXHAUSTIVE) ? 1 : 0, (o.flags >> 8) & 7, nullptr, nullptr, 1};
+                HIP_TRY(c, sbr::launch_equilibrium(L, dsc + 1, du, du + 1, ea, r, 1, s, n <= c->lds_cap_b ? 1 : 2),
+                        SBR_EDEVICE);
+            }
             HIP_TRY(c, hipMemcpyAsync(H + K.res, D + K.res, res_bytes, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
         }
         HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
@@ -1626,6 +1666,8 @@ int sbr_equilibrium_on_knots(sbr_ctx* c, const double* t, const double* G, int64
         if (hc[1] != (int32_t)ntau) return fail(c, SBR_EDEVICE, "hazard grid length mismatch");
         c->kn_t.assign(t, t + n);
         c->kn_G.assign(G, G + n);
+        if (pdf) c->kn_pdf.assign(pdf, pdf + n);
+        else c->kn_pdf.clear();
         const double* hh = (const double*)(H + K.hr);
         c->kn_hr.assign(hh, hh + ntau);
         memcpy(c->kn_key, key, sizeof key);
@@ -1659,6 +1701,32 @@ int sbr_equilibrium_on_knots(sbr_ctx* c, const double* t, const double* G, int64
         }
     }
     return SBR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sbr_equilibrium_on_knots(sbr_ctx* c, const double* t, const double* G, int64_t n, double beta, double eta,
+                             double t_end, const double* u, int64_t n_u, double p, double kappa, double lambda,
+                             const sbr_opts* opts, sbr_result_soa* out, double* tau, double* hr, double* aw_cum,
+                             double* aw_out, double* aw_in, int64_t cap, int64_t* n_tau)
+{
+    SBR_ON_RANK0(c, sbr_equilibrium_on_knots(c, t, G, n, beta, eta, t_end, u, n_u, p, kappa, lambda, opts, out, tau, hr, aw_cum, aw_out, aw_in, cap, n_tau));
+    return on_knots(c, t, G, nullptr, n, beta, eta, t_end, u, n_u, p, kappa, lambda, opts, out, tau, hr, aw_cum,
+                    aw_out, aw_in, cap, n_tau);
+}
+
+int sbr_equilibrium_on_knots_pdf(sbr_ctx* c, const double* t, const double* G, const double* pdf, int64_t n,
+                                 double eta, double t_end, const double* u, int64_t n_u, double p, double kappa,
+                                 double lambda, const sbr_opts* opts, sbr_result_soa* out, double* tau, double* hr,
+                                 double* aw_cum, double* aw_out, double* aw_in, int64_t cap, int64_t* n_tau)
+{
+    SBR_ON_RANK0(c, sbr_equilibrium_on_knots_pdf(c, t, G, pdf, n, eta, t_end, u, n_u, p, kappa, lambda, opts, out, tau, hr, aw_cum, aw_out, aw_in, cap, n_tau));
+    if (!pdf) return c ? fail(c, SBR_EARG, "pdf values missing") : SBR_EARG;
+    // β only forms the default pdf; 1.0 passes the argument check and keys nothing else
+    return on_knots(c, t, G, pdf, n, 1.0, eta, t_end, u, n_u, p, kappa, lambda, opts, out, tau, hr, aw_cum,
+                    aw_out, aw_in, cap, n_tau);
 }
 
 int sbr_chunk_timeline(sbr_ctx* c, void* stream, int32_t* n_chunks, double* ms)
@@ -1772,6 +1840,7 @@ int sbr_learn_hetero(sbr_ctx* c, int32_t K, const double* betas, const double* d
                      int64_t n_col, const sbr_opts* opts, double* t_out, double* G_out, int64_t cap, int32_t* n_knots,
                      uint32_t* status)
 {
+    if (guess_set(opts)) return fail(c, SBR_EARG, "xi_guess: only sbr_equilibrium_on_knots takes a first iterate");
     SBR_ON_RANK0(c, sbr_learn_hetero(c, K, betas, dist, t_end, x0, n_col, opts, t_out, G_out, cap, n_knots, status));
     if (!c || !betas || !dist || !t_end || n_col <= 0 || n_col > (1 << 30) || cap <= 0) return SBR_EARG;
     if (K != 1 && K != 2 && K != 3 && K != 4 && K != 8) return fail(c, SBR_EARG, "K must be 1, 2, 3, 4 or 8");
@@ -1827,6 +1896,7 @@ int sbr_sweep_hetero_dev(sbr_ctx* c, void* stream, int32_t K, const double* beta
                          int64_t n_u, double p, double kappa, double lambda, const sbr_opts* opts,
                          sbr_result_soa* out, double* tau_in, double* tau_out)
 {
+    if (guess_set(opts)) return fail(c, SBR_EARG, "xi_guess: only sbr_equilibrium_on_knots takes a first iterate");
     SBR_SINGLE_DEVICE(c);
     if (!c || !out || !out->xi || !out->aw_max || !out->tol || !out->status) return SBR_EARG;
     if (K != 1 && K != 2 && K != 3 && K != 4 && K != 8) return fail(c, SBR_EARG, "K must be 1, 2, 3, 4 or 8");
@@ -1856,6 +1926,7 @@ int sbr_sweep_hetero_batch_dev(sbr_ctx* c, void* stream, int64_t n_batch, int32_
                                int64_t n_col, int64_t n_u, double p, double kappa, double lambda, const sbr_opts* opts,
                                sbr_result_soa* out, double* tau_in, double* tau_out)
 {
+    if (guess_set(opts)) return fail(c, SBR_EARG, "xi_guess: only sbr_equilibrium_on_knots takes a first iterate");
     SBR_SINGLE_DEVICE(c);
     if (!c || !out || !out->xi || !out->aw_max || !out->tol || !out->status || !betas || !dist || !eta || !t_end || !u)
         return SBR_EARG;
@@ -1927,6 +1998,7 @@ int sbr_hetero_point_paths(sbr_ctx* c, int32_t K, const double* betas, const dou
                            double* res, uint32_t* status, double* tau_in, double* tau_out, double* t, double* G,
                            double* aw_total, int64_t cap, int64_t* n_knots)
 {
+    if (guess_set(opts)) return fail(c, SBR_EARG, "xi_guess: only sbr_equilibrium_on_knots takes a first iterate");
     SBR_ON_RANK0(c, sbr_hetero_point_paths(c, K, betas, dist, eta, t_end, x0, u, p, kappa, lambda, opts, res, status, tau_in, tau_out, t, G, aw_total, cap, n_knots));
     if (!c || !res || !status || !betas || !dist) return SBR_EARG;
     if (K != 1 && K != 2 && K != 3 && K != 4 && K != 8) return fail(c, SBR_EARG, "K must be 1, 2, 3, 4 or 8");
@@ -1985,6 +2057,7 @@ int sbr_sweep_hetero(sbr_ctx* c, int32_t K, const double* betas, const double* d
                      double kappa, double lambda, const sbr_opts* opts, sbr_result_soa* out, double* tau_in,
                      double* tau_out)
 {
+    if (guess_set(opts)) return fail(c, SBR_EARG, "xi_guess: only sbr_equilibrium_on_knots takes a first iterate");
     if (!c || !out || !betas || !dist || !eta || !t_end || !u || K <= 0) return SBR_EARG;
     if (n_col <= 0 || n_u <= 0) return fail(c, SBR_EARG, "grid size");
     // LearningParametersHetero checks (heterogeneity_model.jl:33-41)
@@ -2313,6 +2386,7 @@ int sbr_sweep_social_dev(sbr_ctx* c, void* stream, const double* beta, const dou
                          int32_t n_cmp, double tol, int32_t max_iter, const sbr_opts* opts, sbr_result_soa* out,
                          int32_t* fp_iters, int64_t* rk_steps)
 {
+    if (guess_set(opts)) return fail(c, SBR_EARG, "xi_guess: only sbr_equilibrium_on_knots takes a first iterate");
     SBR_SINGLE_DEVICE(c);
     int rc = social_checks(c, beta, eta, u, n_beta, n_u, x0, p, kappa, lambda, cmp_grid, n_cmp, tol, max_iter, out);
     if (rc) return rc;
@@ -2329,6 +2403,7 @@ int sbr_social_point_paths(sbr_ctx* c, double beta, double eta, double x0, doubl
                            const sbr_opts* opts, double* res, uint32_t* status, int32_t* fp_iters, double* t,
                            double* G, double* aw_old, int64_t cap, int64_t* n_knots)
 {
+    if (guess_set(opts)) return fail(c, SBR_EARG, "xi_guess: only sbr_equilibrium_on_knots takes a first iterate");
     SBR_ON_RANK0(c, sbr_social_point_paths(c, beta, eta, x0, u, p, kappa, lambda, cmp_grid, n_cmp, tol, max_iter, opts, res, status, fp_iters, t, G, aw_old, cap, n_knots));
     if (!c || !res || !status || !t || !G || cap <= 0 || cap > (int64_t(1) << 30)) return SBR_EARG;
     double* d = nullptr;
@@ -2371,6 +2446,7 @@ int sbr_sweep_social(sbr_ctx* c, const double* beta, const double* eta, double x
                      double tol, int32_t max_iter, const sbr_opts* opts, sbr_result_soa* out, int32_t* fp_iters,
                      int64_t* rk_steps)
 {
+    if (guess_set(opts)) return fail(c, SBR_EARG, "xi_guess: only sbr_equilibrium_on_knots takes a first iterate");
     int rc = social_checks(c, beta, eta, u, n_beta, n_u, x0, p, kappa, lambda, cmp_grid, n_cmp, tol, max_iter, out);
     if (rc) return rc;
     for (int64_t i = 0; i < n_beta; i++)

@@ -31,6 +31,9 @@ struct LearnArgs {
     // takes slot k = atomicAdd(ready_tail, 1) and release-stores b + 1 into ready_q[k]
     int32_t* ready_tail;
     int32_t* ready_q;
+    // hazard_kernel: the learning pdf's values on the knots (sbr_equilibrium_on_knots_pdf, e.g. the
+    // social extension's (1 − G)·β·AW_{n−1}); null: compute_pdf_symbolic_baseline's βG(1 − G)
+    const double* pdf = nullptr;
 };
 
 // The equilibrium side of a readiness sweep (eq_ready_kernel): one workgroup per item, each
@@ -66,6 +69,9 @@ struct EqArgs {
     // launch_point_coop: device scratch of 3·n_tau doubles; when set, the paths are formed there and
     // copied to aw_path / aw_out_path / aw_in_path in coalesced rows (those may be mapped host memory)
     double* path_scratch;
+    // compute_ξ's first iterate ξ_guess (solve_equilibrium_baseline(…; ξ_guess), solver.jl:413,441;
+    // compute_ξ :309-312); NaN: the reference's default midpoint (τ̄_IN + τ̄_OUT)/2
+    double xi_guess = __builtin_nan("");
 };
 
 // Interest-rate extension (sbr_baseline.hip interest mode): value function on the HR grid.

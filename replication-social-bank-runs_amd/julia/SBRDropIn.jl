@@ -34,7 +34,7 @@ The Fig 4 / Fig 5 loops can keep calling these per point, or call
 `SBREngine.Context(; n_gpus = 8)`).
 
 Differences a caller can see: `LearningResults.ode_solution` is `nothing` (the engine returns
-the knots, not an ODESolution); `ξ_guess` must be `nothing` (the reference's default midpoint);
+the knots, not an ODESolution); `ξ_guess` is compute_ξ's first iterate as in the reference;
 `tol` of `solve_learning` must be `nothing` / `eps()` (the engine integrates at eps()).
 
 NOT EXECUTED IN THIS REPOSITORY: the build image has no Julia.  The same entry points are
@@ -123,11 +123,11 @@ end
 function solve_equilibrium_baseline(learning_results::LearningResults, econ::EconomicParameters;
                                     ξ_guess = nothing, verbose = false)
     solve_start = time()
-    ξ_guess === nothing || throw(ArgumentError("the engine starts the bisection at the reference's default midpoint"))
     lp = learning_results.params
     cdf = learning_results.learning_cdf
     r = SBREngine.equilibrium_on_knots(sbr_context(), cdf.itp.knots[1], cdf.itp.coefs, lp.β, econ.u; η = econ.η,
-                                       tspan_end = lp.tspan[2], p = econ.p, κ = econ.κ, λ = econ.λ)
+                                       tspan_end = lp.tspan[2], p = econ.p, κ = econ.κ, λ = econ.λ,
+                                       ξ_guess = ξ_guess)
     (r.status & SBREngine.SBR_OOB) != 0 && throw(BoundsError(cdf, econ.η))
     HR = LinearInterpolation(r.τ_bar, r.HR)
     bankrun = (r.status & SBREngine.SBR_RUN) != 0
@@ -180,7 +180,7 @@ function get_AW_functions!(result::SolvedModel)
     result.aw[] !== nothing && return result.aw[]
     result.bankrun || return result.aw[]
     a = result.aw_engine
-    if a === nothing # built without the engine's paths (SBRDropInSocial's last inner SolvedModel)
+    if a === nothing # built without the engine's paths (a SolvedModel constructed by the caller)
         AW_cum, AW_OUT, AW_IN = get_AW(result.ξ, result.τ_bar_IN_UNC, result.τ_bar_OUT_UNC, result.HR,
                                        result.learning_results.learning_cdf)
         result.aw[] = (AW_cum = AW_cum, AW_OUT = AW_OUT, AW_IN = AW_IN, AW_max = maximum(AW_cum.itp.coefs))

@@ -14,9 +14,10 @@ baseline comparison :68-69, :88-89, the plots :104-118) run unchanged:
     range(0, η, 1000)) runs on the GPU through sbr_social_point_paths (bit-identical to a
     sweep point).  Its learning_results hold the last iterate's learning_cdf on its knots and
     learning_pdf = (1 − G)·β·AW_{n-1} (compute_pdf_social_learning, dynamics.jl:98-114, from
-    the AW_{n-1} the engine returns), HR = hazard_rate(p, λ, pdf, η) like solver.jl:424;
-  * `get_AW_functions!(result)` (SBRDropIn.jl) then rebuilds AW_cum / AW_OUT / AW_IN from
-    that SolvedModel exactly as the reference's does (solver.jl:553-576).
+    the AW_{n-1} the engine returns); HR (solver.jl:424) and get_AW's paths come from the engine
+    too (sbr_equilibrium_on_knots_pdf on those knots and pdf values, bit-identical to the
+    social point's own inner equilibrium), so `get_AW_functions!(result)` (SBRDropIn.jl) returns
+    the engine's AW_cum / AW_OUT / AW_IN (solver.jl:553-576) with no host recomputation.
 A β×u grid of fixed points is one call: `SBREngine.solve_equilibrium_social_learning_grid`.
 
 NOT EXECUTED IN THIS REPOSITORY (no Julia in the image): the same entry point runs through
@@ -54,13 +55,19 @@ function solve_equilibrium_social_learning(model::ModelParameters; tol = 1e-4, m
     # the reference raises where an interpolant is read past (0, η) (status SBR_OOB)
     (r.status & SBREngine.SBR_OOB) != 0 && throw(BoundsError(LinearInterpolation(r.t, r.G), η))
     cdf = LinearInterpolation(r.t, r.G)
-    pdf = LinearInterpolation(r.t, ((1 .- r.G) .* β) .* r.AW_old)
+    g = ((1 .- r.G) .* β) .* r.AW_old
+    pdf = LinearInterpolation(r.t, g)
     lr = LearningResults(LearningParameters(β, (0.0, η), x0), cdf, pdf, r.t, 0.0, nothing)
-    HR = hazard_rate(econ.p, econ.λ, pdf, η)
+    # the last inner equilibrium's HR and get_AW paths from the engine (sbr_equilibrium_on_knots_pdf
+    # on the last iterate's knots and pdf: the social point's ξ, HR and AW, bit for bit)
+    e = SBREngine.equilibrium_on_knots(sbr_context(), r.t, r.G, β, econ.u; η = η, tspan_end = η, p = econ.p,
+                                       κ = econ.κ, λ = econ.λ, pdf = g)
+    HR = LinearInterpolation(e.τ_bar, e.HR)
     bankrun = (r.status & SBREngine.SBR_RUN) != 0
     converged = (r.status & SBREngine.SBR_CONVERGED) != 0
+    aw_engine = bankrun ? (AW_cum = e.AW_cum, AW_OUT = e.AW_OUT, AW_IN = e.AW_IN, AW_max = e.AW_max) : nothing
     result = SolvedModel(r.ξ, r.τ_bar_IN_UNC, r.τ_bar_OUT_UNC, HR, bankrun, econ, lr, converged,
-                         time() - solve_start, r.tolerance)
+                         time() - solve_start, r.tolerance, aw_engine)
     if verbose
         fp_ok = (r.status & SBREngine.SBR_SOCIAL_NOT_CONVERGED) == 0
         println("  Social learning: $(r.fp_iters) fixed-point iterations, converged = $fp_ok")

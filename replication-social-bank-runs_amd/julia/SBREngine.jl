@@ -31,9 +31,12 @@ struct Opts            # sbr_opts
     hetero_max_iters::Int32
     flags::Int32
     pad::Int32
+    xi_guess::Float64
 end
-# pad = social knot capacity per buffer (0: library default 98304)
-Opts(; early_exit = 5) = Opts(eps(), eps(), 1_000_000, 100, early_exit, 65536, 500, 0, 0)
+# pad = social knot capacity per buffer (0: library default 98304); xi_guess = compute_ξ's first
+# iterate (NaN: the reference's midpoint; equilibrium_on_knots only)
+Opts(; early_exit = 5, xi_guess = NaN) = Opts(eps(), eps(), 1_000_000, 100, early_exit, 65536, 500, 0, 0,
+                                              Float64(xi_guess))
 
 struct ResultSoA       # sbr_result_soa
     xi::Ptr{Float64}
@@ -156,28 +159,41 @@ end
 
 `solve_equilibrium_baseline(lr, econ)` + `get_AW_functions!` (src/baseline/solver.jl:413-462,
 495-576) on a LearningResults' own knot grid (`t`, `G` = `lr.learning_cdf`'s knots and values,
-`β` = `lr.params.β`, `tspan_end` = `lr.params.tspan[2]`): no learning ODE.  The knots and the
+`β` = `lr.params.β`, `tspan_end` = `lr.params.tspan[2]`): no learning ODE; `ξ_guess` is
+compute_ξ's first iterate (solver.jl:413,441; `nothing` = the midpoint).  The knots and the
 hazard path stay on the GPU while `t`, `G`, β, η, p and λ repeat, so the scripts' per-u loops
 (1_baseline.jl:169, 248) upload only `u`.  Returns ξ, the buffers, AW_max, the tolerance, the
 status and the hazard grid τ̄ with HR(τ̄), AW_cum, AW_OUT and AW_IN on it (NaN without a run).
+`pdf`: the learning pdf's values on the knots (sbr_equilibrium_on_knots_pdf; β unused) — the
+social extension's (1 − G)·β·AW_{n−1}; `nothing` = βG(1 − G).
 """
 function equilibrium_on_knots(ctx::Context, t::Vector{Float64}, G::Vector{Float64}, β, u; η, tspan_end,
-                              p = 0.5, κ = 0.6, λ = 0.01)
+                              p = 0.5, κ = 0.6, λ = 0.01, ξ_guess = nothing, pdf = nothing)
     n = length(t)
     length(G) == n || throw(ArgumentError("t and G must have the same length"))
+    pdf === nothing || length(pdf) == n || throw(ArgumentError("t and pdf must have the same length"))
     cap = n + 1
     res = fill(NaN, 5); st = UInt32[0]; it = Int32[0]; nt = Ref{Int64}(0)
     τ = Vector{Float64}(undef, cap); hr = similar(τ); cum = similar(τ); awo = similar(τ); awi = similar(τ)
     uv = Float64[u]
-    opts = Ref(Opts(; early_exit = 0))
+    opts = Ref(Opts(; early_exit = 0, xi_guess = ξ_guess === nothing ? NaN : ξ_guess))
     GC.@preserve t G uv res st it τ hr cum awo awi begin
         soa = Ref(ResultSoA(pointer(res, 1), pointer(res, 2), pointer(res, 3), pointer(res, 4), pointer(res, 5),
                             pointer(st), pointer(it)))
-        rc = ccall((:sbr_equilibrium_on_knots, libsbr), Cint,
-                   (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Int64, Float64, Float64, Float64, Ptr{Float64}, Int64,
-                    Float64, Float64, Float64, Ref{Opts}, Ref{ResultSoA}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
-                    Ptr{Float64}, Ptr{Float64}, Int64, Ref{Int64}),
-                   ctx.ptr, t, G, n, β, η, tspan_end, uv, 1, p, κ, λ, opts, soa, τ, hr, cum, awo, awi, cap, nt)
+        rc = if pdf === nothing
+            ccall((:sbr_equilibrium_on_knots, libsbr), Cint,
+                  (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Int64, Float64, Float64, Float64, Ptr{Float64}, Int64,
+                   Float64, Float64, Float64, Ref{Opts}, Ref{ResultSoA}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
+                   Ptr{Float64}, Ptr{Float64}, Int64, Ref{Int64}),
+                  ctx.ptr, t, G, n, β, η, tspan_end, uv, 1, p, κ, λ, opts, soa, τ, hr, cum, awo, awi, cap, nt)
+        else
+            pv = Vector{Float64}(pdf)
+            GC.@preserve pv ccall((:sbr_equilibrium_on_knots_pdf, libsbr), Cint,
+                  (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Int64, Float64, Float64, Ptr{Float64},
+                   Int64, Float64, Float64, Float64, Ref{Opts}, Ref{ResultSoA}, Ptr{Float64}, Ptr{Float64},
+                   Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Int64, Ref{Int64}),
+                  ctx.ptr, t, G, pv, n, η, tspan_end, uv, 1, p, κ, λ, opts, soa, τ, hr, cum, awo, awi, cap, nt)
+        end
         check(ctx, rc)
     end
     k = nt[]

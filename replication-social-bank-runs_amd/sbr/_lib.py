@@ -50,6 +50,7 @@ class Opts(ctypes.Structure):
         ("hetero_max_iters", _I32),
         ("flags", _I32),
         ("pad", _I32),  # social sweep knot capacity per buffer (0 = 98304)
+        ("xi_guess", _D),  # compute_ξ's first iterate (NaN: the midpoint); knots-in calls only
     ]
 
 
@@ -92,6 +93,8 @@ _SIGS = {
     "sbr_solve_point_paths": (ctypes.c_int, [_P, _D, _D, _D, _D, _D, _D, _D, _D, _P, _P, _P, _P, _P, _P, _I64, _P]),
     "sbr_equilibrium_on_knots": (ctypes.c_int, [_P, _P, _P, _I64, _D, _D, _D, _P, _I64, _D, _D, _D, _P, _P, _P, _P,
                                                 _P, _P, _P, _I64, _P]),
+    "sbr_equilibrium_on_knots_pdf": (ctypes.c_int, [_P, _P, _P, _P, _I64, _D, _D, _P, _I64, _D, _D, _D, _P, _P, _P,
+                                                    _P, _P, _P, _P, _I64, _P]),
     "sbr_hetero_equilibrium_on_knots": (ctypes.c_int, [_P, _I32, _P, _P, _I64, _P, _P, _D, _D, _P, _I64, _D, _D, _D,
                                                        _P, _P, _P, _P, _P, _P, _I64, _P]),
     "sbr_apply_early_exit": (None, [_I64, _I64, _I32, _P]),

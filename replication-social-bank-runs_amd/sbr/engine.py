@@ -236,13 +236,17 @@ class Engine:
                     status=int(st[0]), tau=tau[:k].copy(), hr=hr[:k].copy(), aw_cum=aw[:k].copy())
 
     def equilibrium_on_knots(self, t, G, beta, eta, t_end, u, p, kappa, lam, max_iters: int = 100,
-                             paths: bool = True, exhaustive: bool = False) -> dict:
+                             paths: bool = True, exhaustive: bool = False, xi_guess: float | None = None,
+                             pdf=None) -> dict:
         """solve_equilibrium_baseline(lr, econ) + get_AW_functions!(r) (solver.jl:413-462, 553-576)
         on the learning knots the caller holds (t, G = lr.learning_cdf's knots and values) for each
         u — no learning ODE (sbr_equilibrium_on_knots).  The knots and the hazard path stay on the
         GPU while (t, G, β, η, p, λ) repeat, so a per-u loop over one LearningResults uploads only
         u.  Returns the SoA fields ([n_u] arrays); with ``paths`` (one u) also the hazard grid
-        ``tau``, ``hr`` and ``aw_cum`` / ``aw_out`` / ``aw_in`` on it (NaN without a run)."""
+        ``tau``, ``hr`` and ``aw_cum`` / ``aw_out`` / ``aw_in`` on it (NaN without a run).
+        ``xi_guess``: compute_ξ's first iterate (solver.jl:413,441; None = the midpoint).
+        ``pdf``: the learning pdf's values on the knots (sbr_equilibrium_on_knots_pdf; ``beta`` is
+        then unused) — the social extension's (1 − G)·β·AW_{n−1}; None = βG(1 − G)."""
         t = t if (isinstance(t, np.ndarray) and t.dtype == np.float64 and t.flags.c_contiguous) else \
             np.ascontiguousarray(t, np.float64)
         G = G if (isinstance(G, np.ndarray) and G.dtype == np.float64 and G.flags.c_contiguous) else \
@@ -258,10 +262,14 @@ class Engine:
         base = res.ctypes.data
         soa = _lib.ResultSoA(base, base + 8 * nu, base + 16 * nu, base + 24 * nu, base + 32 * nu, base + 40 * nu,
                              base + 44 * nu)
-        opts = self._knot_opts.get((max_iters, exhaustive))
+        key = (max_iters, exhaustive, xi_guess)
+        opts = self._knot_opts.get(key)
         if opts is None:
-            opts = self._knot_opts[(max_iters, exhaustive)] = _lib.default_opts(
-                bisect_max_iters=max_iters, flags=_lib.SBR_FLAG_EXHAUSTIVE if exhaustive else 0)
+            if len(self._knot_opts) > 64:  # per-call guesses: keep the cache bounded
+                self._knot_opts = {}
+            opts = self._knot_opts[key] = _lib.default_opts(
+                bisect_max_iters=max_iters, flags=_lib.SBR_FLAG_EXHAUSTIVE if exhaustive else 0,
+                xi_guess=float("nan") if xi_guess is None else float(xi_guess))
         cap = n + 1
         nt = ctypes.c_int64()
         if paths:
@@ -270,10 +278,20 @@ class Engine:
             pp = (pb, pb + 8 * cap, pb + 16 * cap, pb + 24 * cap, pb + 32 * cap)
         else:
             pp = (None,) * 5
-        rc = self._L.sbr_equilibrium_on_knots(self._ctx, t.ctypes.data, G.ctypes.data, n, beta, eta, t_end,
-                                              u.ctypes.data, nu, p, kappa, lam, ctypes.byref(opts),
-                                              ctypes.byref(soa), *pp, cap, ctypes.byref(nt))
-        check(rc, self._ctx, "sbr_equilibrium_on_knots")
+        if pdf is None:
+            rc = self._L.sbr_equilibrium_on_knots(self._ctx, t.ctypes.data, G.ctypes.data, n, beta, eta, t_end,
+                                                  u.ctypes.data, nu, p, kappa, lam, ctypes.byref(opts),
+                                                  ctypes.byref(soa), *pp, cap, ctypes.byref(nt))
+            check(rc, self._ctx, "sbr_equilibrium_on_knots")
+        else:
+            pdf = np.ascontiguousarray(pdf, np.float64)
+            if len(pdf) != n:
+                raise ArgumentError("t and pdf must have the same length")
+            rc = self._L.sbr_equilibrium_on_knots_pdf(self._ctx, t.ctypes.data, G.ctypes.data, pdf.ctypes.data, n,
+                                                      eta, t_end, u.ctypes.data, nu, p, kappa, lam,
+                                                      ctypes.byref(opts), ctypes.byref(soa), *pp, cap,
+                                                      ctypes.byref(nt))
+            check(rc, self._ctx, "sbr_equilibrium_on_knots_pdf")
         out = dict(xi=res[:nu], tau_in_unc=res[nu:2 * nu], tau_out_unc=res[2 * nu:3 * nu],
                    aw_max=res[3 * nu:4 * nu], tol=res[4 * nu:5 * nu], status=st_it[:nu].view(np.uint32),
                    iters=st_it[nu:2 * nu])
@@ -713,7 +731,7 @@ def solve_learning(lp: LearningParameters, engine: Engine | None = None) -> Lear
 
 
 def solve_equilibrium_baseline(lr: LearningResults, econ: EconomicParameters,
-                               engine: Engine | None = None) -> SolvedModel:
+                               engine: Engine | None = None, xi_guess: float | None = None) -> SolvedModel:
     """solver.jl:413-462 for one point on the GPU, on ``lr``'s own knots (no learning ODE: the
     scripts learn once per β and call this per u, 1_baseline.jl:169, 248), with the HR path and
     get_AW's three paths."""
@@ -721,7 +739,7 @@ def solve_equilibrium_baseline(lr: LearningResults, econ: EconomicParameters,
     lp = lr.params
     cdf = lr.learning_cdf
     r = eng.equilibrium_on_knots(cdf.knots, cdf.coefs, lp.beta, econ.eta, lp.tspan[1], econ.u, econ.p, econ.kappa,
-                                 econ.lam)
+                                 econ.lam, xi_guess=xi_guess)
     # the learning solve's own status bits, as a sweep point carries them (maxiters, stiff switch)
     st = int(r["status"][0]) | (lr.status & _LEARN_BITS)
     if st & _lib.SBR_OOB:

@@ -327,3 +327,44 @@ def test_hetero_aw_bounds_at_knot_separation_edge(engine, oracle, sep):
     b = engine.hetero_equilibrium_on_knots(*args, paths=False, exhaustive=True)
     check_hetero(a, b, "pruned vs exhaustive", paths=False)
     assert (a["status"] & sbr.STATUS["SBR_RUN"]).any()
+
+
+def test_knots_pdf_matches_oracle(engine, oracle):
+    """sbr_equilibrium_on_knots_pdf: an explicit pdf on the knots (here βG(1 − G)·(1 + G) and
+    the pdf βG(1 − G) itself) — single point with paths, a u vector, η at the knots' edges —
+    bitwise equal to the oracle's hazard_rate + equilibrium on the same pdf; alternating with
+    the symbolic-pdf call on the same knots swaps the resident hazard (cache keyed by pdf)."""
+    t, G, _ = oracle.learn_logistic(1.0, 30.0)
+    P = dict(eta=15.0, t_end=30.0, p=0.5, kappa=0.6, lam=0.01)
+    sym = (1.0 * G) * (1.0 - G)
+    shaped = sym * (1.0 + G)
+    for rep in range(2):
+        for name, pdf in (("shaped", shaped), ("symbolic", sym)):
+            for u in (0.02, 0.3, 5.0):
+                g = engine.equilibrium_on_knots(t, G, 7.0, P["eta"], P["t_end"], u, P["p"], P["kappa"], P["lam"],
+                                                pdf=pdf)
+                o = oracle.equilibrium_paths_pdf(t, G, pdf, P["eta"], P["t_end"], u, P["p"], P["kappa"], P["lam"])
+                check_point(g, o, f"{name} {u} {rep}")
+            s = engine.equilibrium_on_knots(t, G, 1.0, P["eta"], P["t_end"], 0.3, P["p"], P["kappa"], P["lam"])
+            o = oracle.equilibrium_paths(t, G, 1.0, P["eta"], P["t_end"], 0.3, P["p"], P["kappa"], P["lam"])
+            check_point(s, o, f"plain after {name}")
+    # the explicit βG(1 − G) is the symbolic path
+    a = engine.equilibrium_on_knots(t, G, 1.0, 15.0, 30.0, 0.3, 0.5, 0.6, 0.01)
+    b = engine.equilibrium_on_knots(t, G, 1.0, 15.0, 30.0, 0.3, 0.5, 0.6, 0.01, pdf=sym)
+    for k in FIELDS + ("tau", "hr", "aw_cum", "aw_out", "aw_in"):
+        assert same(a[k], b[k]), k
+    u = sbr.julia_range("0.0", "1.2", 301)
+    g = engine.equilibrium_on_knots(t, G, 1.0, 15.0, 30.0, u, 0.5, 0.6, 0.01, paths=False, pdf=shaped)
+    for j in range(0, 301, 20):
+        o = oracle.equilibrium_paths_pdf(t, G, shaped, 15.0, 30.0, float(u[j]), 0.5, 0.6, 0.01)
+        for f in FIELDS:
+            assert same(g[f][j], o[f]), (j, f)
+        assert int(g["status"][j]) == o["status"] and int(g["iters"][j]) == o["iters"], j
+    for eta in (float(t[-1]), 45.0):
+        g = engine.equilibrium_on_knots(t, G, 1.0, eta, 30.0, 0.1, 0.5, 0.6, 0.01, pdf=shaped)
+        o = oracle.equilibrium_paths_pdf(t, G, shaped, eta, 30.0, 0.1, 0.5, 0.6, 0.01)
+        for f in FIELDS:
+            assert same(g[f][0], o[f]), (eta, f)
+        assert int(g["status"][0]) == o["status"] and len(g["tau"]) == o["n_hr"], eta
+    with pytest.raises(sbr.ArgumentError):
+        engine.equilibrium_on_knots(t, G, 1.0, 15.0, 30.0, 0.1, 0.5, 0.6, 0.01, pdf=shaped[:-1])

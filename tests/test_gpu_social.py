@@ -170,3 +170,24 @@ def test_social_config5_sample_full_workload(engine, golden):
     assert_bitwise(g["iters"], gold["iters"], "bisection iterations")
     assert_bitwise(g["fp_iters"], gold["fp_iters"], "fixed-point iterations")
     assert (g["status"] & sbr.STATUS["SBR_RUN"]).any() and (g["status"] & sbr.STATUS["SBR_OOB"]).any()
+
+
+def test_social_point_engine_hr_and_aw_paths(engine, oracle):
+    """The social drop-in's HR and get_AW paths come from the engine (SBRDropInSocial.jl):
+    sbr_equilibrium_on_knots_pdf on the returned knots with pdf = ((1 − G)·β)·AW_{n−1}
+    (compute_pdf_social_learning, social_learning_dynamics.jl:98-114) reproduces the social
+    point's last inner equilibrium bit for bit, and its τ̄ / HR / AW_cum / AW_OUT / AW_IN equal
+    the oracle's hazard_rate + get_AW on the same pdf — on a run and on a no-run point."""
+    for b, uu in ((0.9, 0.5), (0.9, 50.0)):
+        g = engine.social_point_paths(b, ETA, uu, P, KAPPA, LAM)
+        pdf = ((1.0 - g["G"]) * b) * g["aw_old"]
+        e = engine.equilibrium_on_knots(g["t"], g["G"], b, ETA, ETA, uu, P, KAPPA, LAM, pdf=pdf)
+        for k in FIELDS:
+            assert np.array_equal(e[k][0], g[k], equal_nan=True), (b, uu, k, e[k][0], g[k])
+        run = sbr.STATUS["SBR_RUN"]
+        assert (int(e["status"][0]) & run) == (g["status"] & run)
+        o = oracle.equilibrium_paths_pdf(g["t"], g["G"], pdf, ETA, ETA, uu, P, KAPPA, LAM)
+        assert o["status"] == int(e["status"][0])
+        for k in ("hr_tau", "hr", "aw_cum", "aw_out", "aw_in"):
+            x = e["tau" if k == "hr_tau" else k]
+            assert x.shape == o[k].shape and np.array_equal(x, o[k], equal_nan=True), (b, uu, k)
