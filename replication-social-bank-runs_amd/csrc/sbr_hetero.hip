@@ -1219,7 +1219,20 @@ struct HCol {
 };
 
 #ifndef SBR_HET_UBCACHE
-#define SBR_HET_UBCACHE 1 // pass 2 of AW_max re-reads pass 1's range bounds (config-4 step 45.3 -> 43.3 ms)
+// pass 2 of AW_max reuses pass 1's range bounds: 1 = every 256-knot range's bound in a private
+// array (scratch; config-4 step 45.3 -> 43.3 ms over none), 2 = the two best bounds of each
+// level in registers plus the largest bound of the rest (no scratch; 44.9 ms: too many
+// recomputed), 3 = every bound as a 16-bit code (ceil(65536·ub), exact) in the LDS left between
+// the knot slab and the HR block sums (no scratch)
+#define SBR_HET_UBCACHE 3
+#endif
+#ifndef SBR_HET_UBC_BITS
+#define SBR_HET_UBC_BITS 16 // code width of UBCACHE 3 (8: 29.8 ms alone, the 1/256 window recomputes)
+#endif
+#if SBR_HET_UBC_BITS == 16
+typedef unsigned short ubc_t;
+#else
+typedef unsigned char ubc_t;
 #endif
 #ifndef SBR_HET_K1
 #define SBR_HET_K1 1 // AW_OUT bound from the knot after next -> the next knot where consecutive knots are separated
@@ -1238,7 +1251,9 @@ __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const d
                                                    double* tin, double* tout, const bool mono, const int diag,
                                                    double* __restrict__ aw_path, const double env, const bool sep,
                                                    const int koff,
-                                                   double* __restrict__ tin_g, double* __restrict__ tout_g)
+                                                   double* __restrict__ tin_g, double* __restrict__ tout_g,
+                                                   ubc_t* __restrict__ ubc = nullptr, const int ubc_stride = 0,
+                                                   const int ubc_rows = 0)
 {
     xi_o = NAN; aw_o = NAN; tol_o = INFINITY; it_o = 0;
     const int n = C.n;
@@ -1322,6 +1337,9 @@ __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const d
     int jlo = 0, jhi = n - 1;
     uint32_t s = SBR_NO_RUN_MAXITER;
     double xi = NAN, tolr = INFINITY;
+    bool term = false;
+    double xt = 0.0, et = 0.0, awt = 0.0, errt = 0.0;
+    int jt = 0;
     for (int iter = 1; iter <= max_iters; iter++) {
         it_o = iter;
         const double dd = xmin - xmax;
@@ -1332,7 +1350,7 @@ __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const d
         const int j = ssl_range(C.T, jlo, jhi, xo); // t[jlo] <= ξmin <= xo <= ξmax < t[jhi+1]
         const int i2 = j + 1 < n - 1 ? j + 1 : n - 1;
         const double eps = C.T[i2] - C.T[j];
-        double AW = 0.0, AWe = 0.0;
+        double AW = 0.0;
 #pragma unroll
         for (int k = 0; k < K; k++) {
             const double ic = dmin(tin[k], xo), oc = dmin(tout[k], xo);
@@ -1354,20 +1372,14 @@ __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const d
         if (flag) break;
         const double err = AW - kappa;
         if (fabs(err) <= tolerance) {
-#pragma unroll
-            for (int k = 0; k < K; k++) {
-                const double ic = dmin(tin[k], xo), oc = dmin(tout[k], xo);
-                const int joc = oc == xo ? j : jout[k], jic = ic == xo ? j : jin[k];
-                const double xoe = oc + eps, xie = ic + eps;
-                const double Goce = C.lerp(ssl_gallop(C.T, n, joc, xoe), k, xoe);
-                const double Gice = C.lerp(ssl_gallop(C.T, n, jic, xie), k, xie);
-                AWe = AWe + dist[k] * (Goce - Gice);
-            }
-        }
-        const bool inc = AWe >= AW;
-        if (fabs(err) <= tolerance) {
-            if (inc) { s = SBR_RUN; xi = xo; tolr = fabs(err); }
-            else s = SBR_FALSE_EQ;
+            // the terminal iterate: its slope probe runs after the loop, where the bracket state and
+            // the constant lookups are dead (inside the loop it spilled them to scratch)
+            term = true;
+            xt = xo;
+            jt = j;
+            et = eps;
+            awt = AW;
+            errt = err;
             break;
         } else if (err > 0) {
             xmax = xo;
@@ -1380,6 +1392,20 @@ __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const d
         }
     }
     if (flag) { st_o = flag | lbits; return; }
+    if (term) {
+        double AWe = 0.0;
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const double ic = dmin(tin[k], xt), oc = dmin(tout[k], xt);
+            const int joc = oc == xt ? jt : jout[k], jic = ic == xt ? jt : jin[k];
+            const double xoe = oc + et, xie = ic + et;
+            const double Goce = C.lerp(ssl_gallop(C.T, n, joc, xoe), k, xoe);
+            const double Gice = C.lerp(ssl_gallop(C.T, n, jic, xie), k, xie);
+            AWe = AWe + dist[k] * (Goce - Gice);
+        }
+        if (AWe >= awt) { s = SBR_RUN; xi = xt; tolr = fabs(errt); }
+        else s = SBR_FALSE_EQ;
+    }
     if (s != SBR_RUN) { st_o = s | lbits; return; }
     if (diag & 2) return; // ... after the bisection
 
@@ -1561,6 +1587,144 @@ __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const d
             return (sum + 1e-14) + env;
         };
         auto end_of = [&](int i0, int w) { return i0 + w < n ? i0 + w : n; };
+#if SBR_HET_UBCACHE == 3
+        if (!flag) {
+            // pass 1 keeps every range bound as a code in LDS (this lane's column of ubc rows:
+            // the 256-knot ranges, then the best one's four 64-knot and its eight 8-knot ranges),
+            // c = ceil(S·ub) clamped to [0, S − 2] — c/S >= ub exactly (S = 2^bits: ×S is exact) —
+            // or S − 1 (ub > (S − 2)/S: unknown).  Pass 2: c/S <= mx prunes, (c − 1)/S >= mx
+            // descends (ub > mx), in between — and for rows past ubc_rows, the LDS left — the bound
+            // is recomputed (ub_rng's value does not depend on the hints).
+            constexpr double S = (double)(1 << SBR_HET_UBC_BITS), rS = 1.0 / S;
+            constexpr int unk = (1 << SBR_HET_UBC_BITS) - 1;
+            const int nr = (n + 255) >> 8;
+            auto put = [&](int row, double ub) {
+                if (row >= ubc_rows) return;
+                const double q = ceil(ub * S);
+                ubc[row * ubc_stride] = (ubc_t)(q != q || q > S - 2.0 ? unk : (q < 0.0 ? 0 : (int)q));
+            };
+            auto pruned = [&](int row, int i0, int i1) -> bool {
+                if (row < ubc_rows) {
+                    const int cv = ubc[row * ubc_stride];
+                    if (cv != unk) {
+                        if ((double)cv * rS <= mx) return true;
+                        if ((double)(cv - 1) * rS >= mx) return false;
+                    }
+                }
+                return ub_rng(i0, i1) <= mx;
+            };
+            int bs = 0;
+            double bu = -INFINITY;
+            for (int i0 = 0; i0 < n; i0 += 256) {
+                const double ub = ub_rng(i0, end_of(i0, 256) - 1);
+                put(i0 >> 8, ub);
+                if (!(ub <= bu)) { bu = ub; bs = i0; }
+            }
+            int bb = bs;
+            bu = -INFINITY;
+            for (int i0 = bs; i0 < end_of(bs, 256); i0 += 64) {
+                const double ub = ub_rng(i0, end_of(i0, 64) - 1);
+                put(nr + ((i0 - bs) >> 6), ub);
+                if (!(ub <= bu)) { bu = ub; bb = i0; }
+            }
+            int b8 = bb;
+            bu = -INFINITY;
+            for (int i0 = bb; i0 < end_of(bb, 64); i0 += 8) {
+                const double ub = ub_rng(i0, end_of(i0, 8) - 1);
+                put(nr + 4 + ((i0 - bb) >> 3), ub);
+                if (!(ub <= bu)) { bu = ub; b8 = i0; }
+            }
+            eval_range(b8, end_of(b8, 8));
+            for (int s0 = 0; s0 < n && mx == mx; s0 += 256) {
+                const int se = end_of(s0, 256);
+                if (pruned(s0 >> 8, s0, se - 1)) continue;
+                for (int k0 = s0; k0 < se && mx == mx; k0 += 64) {
+                    const int ke = end_of(k0, 64);
+                    if (s0 == bs ? pruned(nr + ((k0 - bs) >> 6), k0, ke - 1) : (ub_rng(k0, ke - 1) <= mx)) continue;
+                    for (int i0 = k0; i0 < ke && mx == mx; i0 += 8) {
+                        const int ie = end_of(i0, 8);
+                        if (i0 == b8) continue;
+                        if (k0 == bb ? pruned(nr + 4 + ((i0 - bb) >> 3), i0, ie - 1) : (ub_rng(i0, ie - 1) <= mx))
+                            continue;
+                        eval_range(i0, ie);
+                    }
+                }
+            }
+        }
+#elif SBR_HET_UBCACHE == 2
+        if (!flag) {
+            // pass 1 keeps, per level (256-knot ranges; the best one's 64-knot ranges; the best
+            // one's 8-knot ranges), the two largest bounds with their ranges and the
+            // largest bound among the others (`rest`), each rounded up to float: in pass 2 a
+            // range is pruned by its kept bound, or — when `rest` <= the running maximum — with
+            // every other range of its level, without recomputing a bound; otherwise its bound is
+            // recomputed (ub_rng's value does not depend on the hints).  All in registers.
+            struct Top { // the two largest bounds of a level (v0 >= v1) and the largest other one
+                float v0, v1, rest;
+                int a0, a1;
+            };
+            auto top_init = [](Top& t) { t.v0 = t.v1 = t.rest = -INFINITY; t.a0 = t.a1 = -1; };
+            auto top_add = [](Top& t, double ub, int i0) {
+                float f = __double2float_ru(ub);
+                if (ub != ub) f = INFINITY; // (no NaN reaches here: NaN CDFs take the exhaustive path)
+                if (f > t.v0) { t.rest = t.v1 > t.rest ? t.v1 : t.rest; t.v1 = t.v0; t.a1 = t.a0; t.v0 = f; t.a0 = i0; }
+                else if (f > t.v1) { t.rest = t.v1 > t.rest ? t.v1 : t.rest; t.v1 = f; t.a1 = i0; }
+                else t.rest = f > t.rest ? f : t.rest;
+            };
+            // 1 / 0: the kept bound of range i0 (or `rest` if i0 is not kept) is / is not <= mx;
+            // -1: recompute
+            auto top_pruned = [](const Top& t, int i0, double mx) -> int {
+                const float f = t.a0 == i0 ? t.v0 : (t.a1 == i0 ? t.v1 : t.rest);
+                return (double)f <= mx ? 1 : ((t.a0 == i0 || t.a1 == i0) ? 0 : -1);
+            };
+            Top t256, t64, t8;
+            top_init(t256);
+            top_init(t64);
+            top_init(t8);
+            int bs = 0;
+            double bu = -INFINITY;
+            for (int i0 = 0; i0 < n; i0 += 256) {
+                const double ub = ub_rng(i0, end_of(i0, 256) - 1);
+                top_add(t256, ub, i0);
+                if (!(ub <= bu)) { bu = ub; bs = i0; }
+            }
+            int bb = bs;
+            bu = -INFINITY;
+            for (int i0 = bs; i0 < end_of(bs, 256); i0 += 64) {
+                const double ub = ub_rng(i0, end_of(i0, 64) - 1);
+                top_add(t64, ub, i0);
+                if (!(ub <= bu)) { bu = ub; bb = i0; }
+            }
+            int b8 = bb;
+            bu = -INFINITY;
+            for (int i0 = bb; i0 < end_of(bb, 64); i0 += 8) {
+                const double ub = ub_rng(i0, end_of(i0, 8) - 1);
+                top_add(t8, ub, i0);
+                if (!(ub <= bu)) { bu = ub; b8 = i0; }
+            }
+            eval_range(b8, end_of(b8, 8));
+            for (int s0 = 0; s0 < n && mx == mx; s0 += 256) {
+                const int se = end_of(s0, 256);
+                int pr = top_pruned(t256, s0, mx);
+                if (pr < 0) pr = ub_rng(s0, se - 1) <= mx;
+                if (pr) continue;
+                for (int k0 = s0; k0 < se && mx == mx; k0 += 64) {
+                    const int ke = end_of(k0, 64);
+                    int pk = s0 == bs ? top_pruned(t64, k0, mx) : -1;
+                    if (pk < 0) pk = ub_rng(k0, ke - 1) <= mx;
+                    if (pk) continue;
+                    for (int i0 = k0; i0 < ke && mx == mx; i0 += 8) {
+                        const int ie = end_of(i0, 8);
+                        if (i0 == b8) continue;
+                        int pi = k0 == bb ? top_pruned(t8, i0, mx) : -1;
+                        if (pi < 0) pi = ub_rng(i0, ie - 1) <= mx;
+                        if (pi) continue;
+                        eval_range(i0, ie);
+                    }
+                }
+            }
+        }
+#else
         if (!flag) {
             // pass 1 (best 256 → 64 → 8-knot range by bound, evaluated) keeps its bounds, rounded
             // up to float, in a private array (scratch): pass 2 re-reads them instead of redoing
@@ -1607,6 +1771,7 @@ __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const d
                 }
             }
         }
+#endif
     }
     if (flag) { st_o = flag | lbits; return; }
     xi_o = xi;
@@ -1765,9 +1930,13 @@ void equilibrium_hetero_kernel(HeteroBufs L, const double* __restrict__ dist,
     } else if constexpr (MODE == 1) {
         HCol<K, const double*> C{smem, L.G + (size_t)c * cap * K, L.hr + (size_t)c * K * cap, n, L.n_tau[c],
                                  L.n_le[c], cap, eta[c], t_end[c], sums && !a.exhaustive ? hsum : nullptr, nblk};
+        // AW_max's byte bound cache: rows of BLOCK bytes (one per lane) between the knot times
+        // and the HR block sums
+        const int ubc_rows = ((sums ? a.lds_cap - 2 * K * nblk : a.lds_cap) - n) * 8 / (BLOCK * (int)sizeof(ubc_t));
+        ubc_t* const ubc = (ubc_t*)(smem + n) + threadIdx.x;
         solve_hetero_point<K>(C, dl, uj, a.kappa, a.max_iters, a.tolerance, lbits, xi, aw, tol, st, it, tin, tout,
                               mono, a.diag, a.aw_path, env, fits && s_close == 0, (SBR_HET_K1 && s_close1 == 0) ? 1 : 2,
-                              tin_g, tout_g);
+                              tin_g, tout_g, ubc, BLOCK, ubc_rows);
     } else {
         HCol<K, const double*> C{gT, L.G + (size_t)c * cap * K, L.hr + (size_t)c * K * cap, n, L.n_tau[c],
                                  L.n_le[c], cap, eta[c], t_end[c], nullptr, 0};
