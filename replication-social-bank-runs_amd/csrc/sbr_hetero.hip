@@ -1239,6 +1239,8 @@ typedef unsigned char ubc_t;
 #endif
 #ifndef SBR_HET_SHARE_DIV
 #define SBR_HET_SHARE_DIV 1 // exact AW evaluations share δ between groups with equal arguments
+// (A/B r05: also skipping the second CDF load of an on-knot argument, g0·1 + g1·0 = g0, made the
+// data-dependent loads serial — config-4 equilibrium alone 29.1 -> 33.6 ms; not kept)
 #endif
 #ifndef SBR_HET_UBC_MAX
 #define SBR_HET_UBC_MAX 40 // 256-knot ranges cached (the LDS slab holds ≤ 10,176 knots: 40 ranges)
@@ -1844,7 +1846,7 @@ void equilibrium_hetero_kernel(HeteroBufs L, const double* __restrict__ dist,
     // decreases in the saturated tail (G_k = 1 − 2^-53 after 1.0: most config-4 columns), so
     // the bounds take G_k[j] ± Δ_k for the prefix max / suffix min, with
     // Δ_k = (#decreases)·(largest decrease) ≥ the largest drawdown max_{j<j'} G_k[j] − G_k[j'].
-    // NaN anywhere -> exhaustive evaluation.
+    // NaN or ±Inf anywhere -> exhaustive evaluation.
     __shared__ int s_dcnt[K];
     __shared__ unsigned long long s_dmax[K];
     if (threadIdx.x < K) { s_dcnt[threadIdx.x] = 0; s_dmax[threadIdx.x] = 0ull; }
@@ -1860,7 +1862,7 @@ void equilibrium_hetero_kernel(HeteroBufs L, const double* __restrict__ dist,
 #pragma unroll
             for (int k = 0; k < K; k++) {
                 const double g1 = Gc[(size_t)i * K + k], g0 = Gc[(size_t)(i - 1) * K + k];
-                if (g0 != g0 || g1 != g1) nan = true;
+                if (!(fabs(g0) < INFINITY) || !(fabs(g1) < INFINITY)) nan = true; // NaN or ±Inf
                 else if (g1 < g0) { cnt[k]++; dm[k] = dmax(dm[k], g0 - g1); }
             }
         if (nan) s_nonmono = 1;
