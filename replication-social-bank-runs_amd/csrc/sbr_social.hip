@@ -1516,6 +1516,11 @@ static_assert(!SBR_SOCIAL_RING || kRingLanes == 64 || SBR_SOCIAL_COOP,
 #define SBR_SOCIAL_WAVES 1024 // one wave per SIMD (A/B: 2048 with SBR_SOCIAL_MINW 2; 0 = dense waves, the round-1 layout)
 #endif
 static_assert(SBR_SOCIAL_WAVES != 0 || !SBR_SOCIAL_RING || kRingLanes == 64, "dense waves use all 64 lanes of the ring");
+#ifndef SBR_SOCIAL_COOP_MAX
+// live points up to which every point gets a whole wave (SocialRhsCoop), in rounds of the
+// SBR_SOCIAL_WAVES resident ones, instead of ⌈live/SBR_SOCIAL_WAVES⌉ points per wave
+#define SBR_SOCIAL_COOP_MAX 4096
+#endif
 // Main blocks (one wave each) spread the live worklist over all `nbs` of them: L = ⌈live/nbs⌉
 // consecutive entries per wave (L ≤ 64), lanes ≥ L idle.  A fixed-point lane's RK step is a
 // serial chain whose memory side grows with the wave's active lanes (each lane streams its own
@@ -1524,16 +1529,17 @@ static_assert(SBR_SOCIAL_WAVES != 0 || !SBR_SOCIAL_RING || kRingLanes == 64, "de
 // SIMD the bulk uses every SIMD instead of half of them.
 __global__ __launch_bounds__(64, SBR_SOCIAL_MINW) void social_iter_kernel(const SocialArgs* __restrict__ args, int iter_arg,
                                                          int n_inner, const int32_t* __restrict__ work,
-                                                         const int32_t* __restrict__ count, int nbs)
+                                                         const int32_t* __restrict__ count, int nbs, int nmain)
 {
     extern __shared__ double s_ring[]; // kRingLdsBytes: SocialRhsRing's per-lane rings
     const SocialArgs& sa = args[0];
     const SocialArgs& pa = args[1];
-    const bool in_pool = (int)blockIdx.x >= nbs;
+    const bool in_pool = (int)blockIdx.x >= nmain;
     int l, iter;
     if (!in_pool) {
         const int cnt = *count;
-        int L = SBR_SOCIAL_WAVES ? (cnt + nbs - 1) / nbs : 64;
+        // at most nmain live points: one per wave (coop), beyond that the first nbs waves
+        int L = SBR_SOCIAL_WAVES ? (cnt <= nmain ? 1 : (cnt + nbs - 1) / nbs) : 64;
         // the ring holds kRingLanes lanes: the host's nbs = ⌈n_pts / kRingLanes⌉ >= ⌈cnt / kRingLanes⌉
         // keeps L within it; the clamp stops a future change of that arithmetic from letting lanes
         // share ring slots (which in_ring() would trust)
@@ -1550,7 +1556,7 @@ __global__ __launch_bounds__(64, SBR_SOCIAL_MINW) void social_iter_kernel(const 
             return;
         }
 #endif
-        if ((int)threadIdx.x >= L) return;
+        if ((int)threadIdx.x >= L || (int)blockIdx.x >= nbs) return;
         const int w = blockIdx.x * L + threadIdx.x;
         if (w >= cnt) return;
         l = work[w];
@@ -1560,7 +1566,7 @@ __global__ __launch_bounds__(64, SBR_SOCIAL_MINW) void social_iter_kernel(const 
 #if SBR_SOCIAL_COOP
         // one pool slot per wave, run by the whole wave (the pool holds the longest fixed
         // points — the ones whose iterates outgrew the main capacity)
-        l = (int)blockIdx.x - nbs;
+        l = (int)blockIdx.x - nmain;
         if (l >= pa.n_pts) return;
         if (__hip_atomic_load(pa.ready + l, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
         if (!pa.live[l]) return;
@@ -1569,7 +1575,7 @@ __global__ __launch_bounds__(64, SBR_SOCIAL_MINW) void social_iter_kernel(const 
             if (!social_iterate<true>(pa, l, iter + k, s_ring)) break;
         return;
 #else
-        l = ((int)blockIdx.x - nbs) * 64 + threadIdx.x;
+        l = ((int)blockIdx.x - nmain) * 64 + threadIdx.x;
         if (l >= pa.n_pts) return;
         if (__hip_atomic_load(pa.ready + l, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
         if (!pa.live[l]) return;
@@ -1640,8 +1646,11 @@ hipError_t launch_social_iter(const SocialArgs& a, const SocialArgs& p, const So
     nbs = nbs > SBR_SOCIAL_WAVES ? nbs : SBR_SOCIAL_WAVES;
     nbs = nbs < a.n_pts ? nbs : (a.n_pts > 0 ? a.n_pts : 1);
     const int pool_waves = SBR_SOCIAL_COOP ? p.n_pts : (p.n_pts + 63) / 64;
-    hipLaunchKernelGGL(social_iter_kernel, dim3(nbs + pool_waves), dim3(64), SBR_SOCIAL_RING ? kRingLdsBytes : 0, s,
-                       args_dev, iter, n_inner, work, count, nbs);
+    // main blocks: nbs multi-point waves, or up to SBR_SOCIAL_COOP_MAX one-point waves
+    const int coop_max = (SBR_SOCIAL_COOP) && (SBR_SOCIAL_WAVES != 0) ? (SBR_SOCIAL_COOP_MAX < a.n_pts ? SBR_SOCIAL_COOP_MAX : a.n_pts) : 0;
+    const int nmain = nbs > coop_max ? nbs : coop_max;
+    hipLaunchKernelGGL(social_iter_kernel, dim3(nmain + pool_waves), dim3(64), SBR_SOCIAL_RING ? kRingLdsBytes : 0, s,
+                       args_dev, iter, n_inner, work, count, nbs, nmain);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(social_compact_kernel, dim3(1), dim3(CMP_BLOCK), 0, s, work, count, a.live, work_out,
