@@ -191,3 +191,16 @@ def test_social_point_engine_hr_and_aw_paths(engine, oracle):
         for k in ("hr_tau", "hr", "aw_cum", "aw_out", "aw_in"):
             x = e["tau" if k == "hr_tau" else k]
             assert x.shape == o[k].shape and np.array_equal(x, o[k], equal_nan=True), (b, uu, k)
+
+
+def test_social_config5_strided_points_full_workload(engine, oracle):
+    """BASELINE config 5 at its stated workload (tol 1e-4, max_iter 500) on 128 points of the
+    512² axes — every 64th β × every 32nd u, a stratified sample four times the golden
+    fixture's — bit for bit against the oracle's fixed points computed here (every field,
+    status bit, bisection and fixed-point iteration count)."""
+    beta = (1.0 / sbr.julia_range("0.01", "2", 512))[::64]
+    u = sbr.julia_range("0.001", "1", 512)[::32]
+    g, o = _both(engine, oracle, beta, u, tol=1e-4, max_iter=500)
+    _compare(g, o)
+    st = g["status"]
+    assert (st & sbr.STATUS["SBR_RUN"]).any() and ((st & sbr.STATUS["SBR_RUN"]) == 0).any()
