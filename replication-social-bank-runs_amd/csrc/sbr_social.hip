@@ -793,6 +793,9 @@ struct SocialRhsRing {
 // L2/HBM round trip per step.  The window moves forward by 32 knots when the step's time passes
 // its middle (one coalesced load per array); lookups outside it fall back to the global search.
 // Same brackets, same operands, same operations as SocialRhs: bit-identical.
+#ifndef SBR_SOCIAL_COOP_PIN
+#define SBR_SOCIAL_COOP_PIN 1 // one-point waves hold the Tsit5 tableau in VGPRs (Tsit5Regs; ODE 3,077 -> 2,876 cycles per RK step, r05_r)
+#endif
 struct SocialRhsCoop {
     double beta;
     BView to;
@@ -956,7 +959,7 @@ struct SocialRhsCoop {
         }
     }
     static constexpr bool kFsalExact = false;
-    static constexpr bool kPinTableau = false;
+    static constexpr bool kPinTableau = SBR_SOCIAL_COOP_PIN != 0;
     static constexpr bool kAcceptFirst = SBR_SOCIAL_ACCEPT_FIRST != 0; // the refill's loads ahead of the knot stores
 };
 
