@@ -1220,10 +1220,10 @@ struct HCol {
 
 #ifndef SBR_HET_UBCACHE
 // pass 2 of AW_max reuses pass 1's range bounds: 1 = every 256-knot range's bound in a private
-// array (scratch; config-4 step 45.3 -> 43.3 ms over none), 2 = the two best bounds of each
-// level in registers plus the largest bound of the rest (no scratch; 44.9 ms: too many
-// recomputed), 3 = every bound as a 16-bit code (ceil(65536·ub), exact) in the LDS left between
-// the knot slab and the HR block sums (no scratch)
+// array (scratch; config-4 step 45.3 -> 43.3 ms over none), 3 = every bound as a 16-bit code
+// (ceil(65536·ub), exact) in the LDS left between the knot slab and the HR block sums (no
+// scratch).  A/B r05: the two best bounds of each level in registers plus the largest of the
+// rest, recomputing the others, was 44.9 ms (removed)
 #define SBR_HET_UBCACHE 3
 #endif
 #ifndef SBR_HET_UBC_BITS
@@ -1648,79 +1648,6 @@ __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const d
                         if (i0 == b8) continue;
                         if (k0 == bb ? pruned(nr + 4 + ((i0 - bb) >> 3), i0, ie - 1) : (ub_rng(i0, ie - 1) <= mx))
                             continue;
-                        eval_range(i0, ie);
-                    }
-                }
-            }
-        }
-#elif SBR_HET_UBCACHE == 2
-        if (!flag) {
-            // pass 1 keeps, per level (256-knot ranges; the best one's 64-knot ranges; the best
-            // one's 8-knot ranges), the two largest bounds with their ranges and the
-            // largest bound among the others (`rest`), each rounded up to float: in pass 2 a
-            // range is pruned by its kept bound, or — when `rest` <= the running maximum — with
-            // every other range of its level, without recomputing a bound; otherwise its bound is
-            // recomputed (ub_rng's value does not depend on the hints).  All in registers.
-            struct Top { // the two largest bounds of a level (v0 >= v1) and the largest other one
-                float v0, v1, rest;
-                int a0, a1;
-            };
-            auto top_init = [](Top& t) { t.v0 = t.v1 = t.rest = -INFINITY; t.a0 = t.a1 = -1; };
-            auto top_add = [](Top& t, double ub, int i0) {
-                float f = __double2float_ru(ub);
-                if (ub != ub) f = INFINITY; // (no NaN reaches here: NaN CDFs take the exhaustive path)
-                if (f > t.v0) { t.rest = t.v1 > t.rest ? t.v1 : t.rest; t.v1 = t.v0; t.a1 = t.a0; t.v0 = f; t.a0 = i0; }
-                else if (f > t.v1) { t.rest = t.v1 > t.rest ? t.v1 : t.rest; t.v1 = f; t.a1 = i0; }
-                else t.rest = f > t.rest ? f : t.rest;
-            };
-            // 1 / 0: the kept bound of range i0 (or `rest` if i0 is not kept) is / is not <= mx;
-            // -1: recompute
-            auto top_pruned = [](const Top& t, int i0, double mx) -> int {
-                const float f = t.a0 == i0 ? t.v0 : (t.a1 == i0 ? t.v1 : t.rest);
-                return (double)f <= mx ? 1 : ((t.a0 == i0 || t.a1 == i0) ? 0 : -1);
-            };
-            Top t256, t64, t8;
-            top_init(t256);
-            top_init(t64);
-            top_init(t8);
-            int bs = 0;
-            double bu = -INFINITY;
-            for (int i0 = 0; i0 < n; i0 += 256) {
-                const double ub = ub_rng(i0, end_of(i0, 256) - 1);
-                top_add(t256, ub, i0);
-                if (!(ub <= bu)) { bu = ub; bs = i0; }
-            }
-            int bb = bs;
-            bu = -INFINITY;
-            for (int i0 = bs; i0 < end_of(bs, 256); i0 += 64) {
-                const double ub = ub_rng(i0, end_of(i0, 64) - 1);
-                top_add(t64, ub, i0);
-                if (!(ub <= bu)) { bu = ub; bb = i0; }
-            }
-            int b8 = bb;
-            bu = -INFINITY;
-            for (int i0 = bb; i0 < end_of(bb, 64); i0 += 8) {
-                const double ub = ub_rng(i0, end_of(i0, 8) - 1);
-                top_add(t8, ub, i0);
-                if (!(ub <= bu)) { bu = ub; b8 = i0; }
-            }
-            eval_range(b8, end_of(b8, 8));
-            for (int s0 = 0; s0 < n && mx == mx; s0 += 256) {
-                const int se = end_of(s0, 256);
-                int pr = top_pruned(t256, s0, mx);
-                if (pr < 0) pr = ub_rng(s0, se - 1) <= mx;
-                if (pr) continue;
-                for (int k0 = s0; k0 < se && mx == mx; k0 += 64) {
-                    const int ke = end_of(k0, 64);
-                    int pk = s0 == bs ? top_pruned(t64, k0, mx) : -1;
-                    if (pk < 0) pk = ub_rng(k0, ke - 1) <= mx;
-                    if (pk) continue;
-                    for (int i0 = k0; i0 < ke && mx == mx; i0 += 8) {
-                        const int ie = end_of(i0, 8);
-                        if (i0 == b8) continue;
-                        int pi = k0 == bb ? top_pruned(t8, i0, mx) : -1;
-                        if (pi < 0) pi = ub_rng(i0, ie - 1) <= mx;
-                        if (pi) continue;
                         eval_range(i0, ie);
                     }
                 }
