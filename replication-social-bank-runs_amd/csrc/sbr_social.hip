@@ -586,6 +586,9 @@ constexpr size_t kRingLdsBytes = (size_t)2 * kRing * kRingLanes * sizeof(double)
 // bracket passes rb + 20, and the line after next is touched into L2 then.  The bracket window
 // (Win8) reloads from the ring too.  Knots outside the ring fall back to global loads.  Same
 // brackets, operands and operations as SocialRhs: bit-identical.
+#ifndef SBR_SOCIAL_RING_PIN
+#define SBR_SOCIAL_RING_PIN 1 // multi-point waves hold the Tsit5 tableau in VGPRs (Tsit5Regs; AGPR overflow, no scratch; share 45.3 -> 44.7 s, r05_v)
+#endif
 struct SocialRhsRing {
     double beta;
     BView to;
@@ -776,7 +779,7 @@ struct SocialRhsRing {
         }
     }
     static constexpr bool kFsalExact = false;
-    static constexpr bool kPinTableau = false;
+    static constexpr bool kPinTableau = SBR_SOCIAL_RING_PIN != 0;
 };
 
 #ifndef SBR_SOCIAL_PAR_STAGES
