@@ -426,6 +426,9 @@ __global__ __launch_bounds__(64) void learn_hetero_kernel(const double* __restri
 #ifndef SBR_HET_LEARN_ROWS
 #define SBR_HET_LEARN_ROWS 1 // columns per learning wave: 1 = one per wave; 4 = learn_hetero_wave4_kernel (16-lane rows, bitwise but slower: 42.4 -> 45.2 ms, profiles/experiments/r04_s_*)
 #endif
+#ifndef SBR_HET_LEARN_PIN
+#define SBR_HET_LEARN_PIN 0 // learn_hetero_wave_kernel holds the Tsit5 tableau in VGPRs (A/B r05_x: 103 -> 157 VGPRs, step 42.7 -> 46.6 ms)
+#endif
 #ifndef SBR_HET_DIVRCP
 #define SBR_HET_DIVRCP 0 // LU back substitutions by refined pivot reciprocals (A/B)
 #endif
@@ -709,6 +712,7 @@ __global__ __launch_bounds__(64) void learn_hetero_wave_kernel(const double* __r
     double eig = 1.0; // integrator.eigen_est at init
     PIControl pc;
     AutoSwitch as;
+    const Tsit5Tab<SBR_HET_LEARN_PIN != 0> cf; // the tableau in VGPRs, or literals
     int naccept = 0, nreject = 0;
     push(t, x, k1);
     int64_t iter = 0;
@@ -768,15 +772,15 @@ __global__ __launch_bounds__(64) void learn_hetero_wave_kernel(const double* __r
             const double a21 = dt * A21;
             tmp = fma(a21, k1, x);
             k2 = R.rhs(tmp);
-            tmp = fma(dt, fma(A31, k1, A32 * k2), x);
+            tmp = fma(dt, fma(cf.a31, k1, cf.a32 * k2), x);
             k3 = R.rhs(tmp);
-            tmp = fma(dt, fma(A41, k1, fma(A42, k2, A43 * k3)), x);
+            tmp = fma(dt, fma(cf.a41, k1, fma(cf.a42, k2, cf.a43 * k3)), x);
             k4 = R.rhs(tmp);
-            tmp = fma(dt, fma(A51, k1, fma(A52, k2, fma(A53, k3, A54 * k4))), x);
+            tmp = fma(dt, fma(cf.a51, k1, fma(cf.a52, k2, fma(cf.a53, k3, cf.a54 * k4))), x);
             k5 = R.rhs(tmp);
-            tmp6 = fma(dt, fma(A61, k1, fma(A62, k2, fma(A63, k3, fma(A64, k4, A65 * k5)))), x);
+            tmp6 = fma(dt, fma(cf.a61, k1, fma(cf.a62, k2, fma(cf.a63, k3, fma(cf.a64, k4, cf.a65 * k5)))), x);
             k6 = R.rhs(tmp6);
-            u = fma(dt, fma(A71, k1, fma(A72, k2, fma(A73, k3, fma(A74, k4, fma(A75, k5, A76 * k6))))), x);
+            u = fma(dt, fma(cf.a71, k1, fma(cf.a72, k2, fma(cf.a73, k3, fma(cf.a74, k4, fma(cf.a75, k5, cf.a76 * k6))))), x);
             k7 = R.rhs(u);
             const double rr = fabs((k7 - k6) / (u - tmp6));
             double e = 0.0;
@@ -788,8 +792,8 @@ __global__ __launch_bounds__(64) void learn_hetero_wave_kernel(const double* __r
                 else if (v > e) e = v;
             }
             eig = e_nan ? (double)NAN : e;
-            const double ut = dt * fma(BT1, k1, fma(BT2, k2, fma(BT3, k3, fma(BT4, k4,
-                                       fma(BT5, k5, fma(BT6, k6, BT7 * k7))))));
+            const double ut = dt * fma(cf.bt1, k1, fma(cf.bt2, k2, fma(cf.bt3, k3, fma(cf.bt4, k4,
+                                       fma(cf.bt5, k5, fma(cf.bt6, k6, cf.bt7 * k7))))));
             EEst = R.rms(ut / fma(dmax(fabs(x), fabs(u)), rtol, atol));
         }
         if (EEst != EEst) { st |= SBR_ODE_FAILED; break; } // NaN trial state (ReturnCode.Unstable)
