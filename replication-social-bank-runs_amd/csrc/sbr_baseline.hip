@@ -1152,6 +1152,9 @@ __device__ __forceinline__ double tsit5_dense(double th, double dt, double y0, d
 
 // hjb_equation! (value_function_solver.jl:86-95): dV = (h + δ)(1 − V) + max(u + rV − h, 0)
 // with h = HR(τ̄) (gridded linear, Throw()); brackets galloped from the step's own.
+#ifndef SBR_VALUE_PIN
+#define SBR_VALUE_PIN 0 // the value-function ODE's Tsit5 tableau: 0 literals, 2 the a_ij in VGPRs (A/B r05_y: 636 -> 633 ms, kept off; 1 spills)
+#endif
 template <class P>
 struct ValueRhs {
     TauView<P> tau;
@@ -1201,7 +1204,7 @@ struct ValueRhs {
         if (ntau >= 2 && t >= tlo && t <= thi) jb = ssl_gallop(tau, ntau, jb, t);
     }
     static constexpr bool kFsalExact = false;
-    static constexpr bool kPinTableau = false;
+    static constexpr int kPinTableau = SBR_VALUE_PIN;
 };
 
 // The value function saved on the HR grid (saveat) streamed into optimal_buffer

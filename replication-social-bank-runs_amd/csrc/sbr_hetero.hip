@@ -712,7 +712,7 @@ __global__ __launch_bounds__(64) void learn_hetero_wave_kernel(const double* __r
     double eig = 1.0; // integrator.eigen_est at init
     PIControl pc;
     AutoSwitch as;
-    const Tsit5Tab<SBR_HET_LEARN_PIN != 0> cf; // the tableau in VGPRs, or literals
+    const Tsit5Tab<SBR_HET_LEARN_PIN> cf; // the tableau in VGPRs, or literals
     int naccept = 0, nreject = 0;
     push(t, x, k1);
     int64_t iter = 0;

@@ -239,10 +239,49 @@ struct Tsit5Lits {
     static constexpr double bt6 = BT6;
     static constexpr double bt7 = BT7;
 };
-template <bool PIN>
+// The stage coefficients a_ij in VGPRs and the error weights as literals (a right-hand side
+// with room for 40 more VGPRs but not 54)
+struct Tsit5RegsA {
+    double a31, a32, a41, a42, a43, a51, a52, a53, a54, a61, a62, a63, a64, a65, a71, a72, a73, a74, a75, a76;
+    static constexpr double bt1 = BT1;
+    static constexpr double bt2 = BT2;
+    static constexpr double bt3 = BT3;
+    static constexpr double bt4 = BT4;
+    static constexpr double bt5 = BT5;
+    static constexpr double bt6 = BT6;
+    static constexpr double bt7 = BT7;
+    __device__ __forceinline__ Tsit5RegsA()
+        : a31(A31), a32(A32), a41(A41), a42(A42), a43(A43), a51(A51), a52(A52), a53(A53), a54(A54), a61(A61), a62(A62), a63(A63), a64(A64), a65(A65), a71(A71), a72(A72), a73(A73), a74(A74), a75(A75), a76(A76)
+    {
+        asm volatile("" : "+v"(a31));
+        asm volatile("" : "+v"(a32));
+        asm volatile("" : "+v"(a41));
+        asm volatile("" : "+v"(a42));
+        asm volatile("" : "+v"(a43));
+        asm volatile("" : "+v"(a51));
+        asm volatile("" : "+v"(a52));
+        asm volatile("" : "+v"(a53));
+        asm volatile("" : "+v"(a54));
+        asm volatile("" : "+v"(a61));
+        asm volatile("" : "+v"(a62));
+        asm volatile("" : "+v"(a63));
+        asm volatile("" : "+v"(a64));
+        asm volatile("" : "+v"(a65));
+        asm volatile("" : "+v"(a71));
+        asm volatile("" : "+v"(a72));
+        asm volatile("" : "+v"(a73));
+        asm volatile("" : "+v"(a74));
+        asm volatile("" : "+v"(a75));
+        asm volatile("" : "+v"(a76));
+    }
+};
+// PIN: 0 = literals, 1 = the whole tableau in VGPRs, 2 = the stage coefficients only
+template <int PIN>
 struct Tsit5Tab : Tsit5Regs {};
 template <>
-struct Tsit5Tab<false> : Tsit5Lits {};
+struct Tsit5Tab<0> : Tsit5Lits {};
+template <>
+struct Tsit5Tab<2> : Tsit5RegsA {};
 
 // Scalar AutoTsit5(Rosenbrock23()) on (0, T1) from x0.  Sys provides
 //   double eval(double t, double x)                       f at any (t, x)
@@ -251,7 +290,8 @@ struct Tsit5Tab<false> : Tsit5Lits {};
 //   void   jac(double t, double x, double& J, double& dT) ForwardDiff ∂f/∂x, ∂f/∂t
 //   void   accepted(double t)                             after an accepted step
 //   static constexpr bool kFsalExact                      f(t, x) == the carried k1 bit for bit
-//   static constexpr bool kPinTableau                     hold the Tsit5 tableau in VGPRs (Tsit5Regs)
+//   static constexpr bool/int kPinTableau                 the Tsit5 tableau in VGPRs: 0 / false literals,
+//                                                          1 / true all (Tsit5Regs), 2 the a_ij (Tsit5RegsA)
 // Sink provides
 //   bool start(double t0, double x0)                      the first knot; false = stop
 //   bool step(bool acc, double tprev, double tn, double dt, double y0, double y1, const StepK& k, bool exact)
@@ -280,7 +320,7 @@ __device__ __forceinline__ void ode_scalar(Sys& f, Sink& sink, double T1, double
     double eig = 1.0; // integrator.eigen_est = 1/oneunit(t) at init
     PIControl pc;
     AutoSwitch as;
-    const Tsit5Tab<Sys::kPinTableau> cf;
+    const Tsit5Tab<(int)Sys::kPinTableau> cf;
     if (!sink.start(t, x)) { sink_finish(sink, o); return; }
     if (!(t < T1)) { sink_finish(sink, o); return; }
     if (maxiters < 1) { o.status |= SBR_ODE_MAXITERS; sink_finish(sink, o); return; }

@@ -75,6 +75,7 @@ for s in ${STEPS:-tests smoke bench single}; do
     profconfig1) run profconfig1 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$OUT/profconfig1" -o run --output-format csv -- python3 bench.py --workload config1 --steps 50 --warmup 3 ;;
     soclone) run soclone 300 python -u bench.py --workload social --steps 1 --warmup 0 --social-cols 2 --social-max-iter 16 --social-prof --no-cpu-baseline --no-verify ;;
     soclonevars) for v in ${VARS:-}; do run soclone_$v 300 env SBR_LIB=replication-social-bank-runs_amd/lib_var/$v/libsbr.so python -u bench.py --workload social --steps 1 --warmup 0 --social-cols 2 --social-max-iter 16 --social-prof --no-cpu-baseline --no-verify; done ;;
+    interestvars) for v in ${VARS:-}; do run interest_$v 600 env SBR_LIB=replication-social-bank-runs_amd/lib_var/$v/libsbr.so python -u bench.py --workload interest --steps 3 --warmup 1 --no-cpu-baseline; done ;;
     knots) run knots 600 python -u -m pytest tests/test_gpu_knots.py tests/test_gpu_baseline.py -x -v --timeout 300 --timeout-method thread ${KTESTK:+-k "$KTESTK"} ;;
   esac
 done
