@@ -116,7 +116,10 @@ const char* sbr_last_error(const sbr_ctx* ctx);
  * depend on the partitioning).  Single-point, learning-only and diagnostic calls run on
  * device 0; the device-pointer (*_dev) entry points need a single-device context:
  * sbr_multi_child(ctx, rank).  A call is synchronous; contexts are independent, so
- * distinct contexts may be used from distinct threads.
+ * distinct contexts may be used from distinct threads.  Diagnostic: with the environment
+ * variable SBR_MULTI_SHARED_DEVICES=1, ranks may share a device (duplicate ids, or rank r
+ * on device r mod count) — the n-rank fan-out rehearsed on fewer GPUs; the RCCL gather is
+ * refused (SBR_EARG) on such a context.
  */
 int sbr_init_multi(int n_gpus, const int* devices, sbr_ctx** ctx);
 /* number of devices of a context (1 for sbr_init's) */

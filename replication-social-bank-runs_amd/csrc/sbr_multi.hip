@@ -138,6 +138,7 @@ struct sbr_multi {
     std::vector<Rank> ranks;
     std::string err;
     bool comms_ok = false; // false after an abort (or before the first gather): (re)built by the next gather
+    bool shared = false;   // rank rehearsal: ranks may share a device (SBR_MULTI_SHARED_DEVICES=1)
     // phases of the last sweep, ms: [0] slowest rank's staging + sweep, [1] slowest rank's D2H
     // into its landing buffer, [2] the host copy into the caller's arrays (direct transport) or
     // the RCCL gather + scatter, [3] unused, [4] the whole call
@@ -255,19 +256,28 @@ int create(int n_gpus, const int* devices, sbr_multi** out, std::vector<sbr_ctx*
 {
     *out = nullptr;
     int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || n_gpus <= 0 || n_gpus > ndev) {
+    // Rank rehearsal (diagnostic): with SBR_MULTI_SHARED_DEVICES=1 in the environment, ranks may
+    // share a device (explicit duplicate ids; without a device list, rank r on device r mod
+    // ndev), so the n-rank fan-out — host threads, per-rank streams and pinned landing buffers,
+    // strided D2H, the all-or-nothing scatter — runs on a one-GPU box.  The RCCL gather needs
+    // distinct devices and is refused on such a context.
+    const char* sh = getenv("SBR_MULTI_SHARED_DEVICES");
+    const bool shared = sh && sh[0] == '1' && sh[1] == 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || n_gpus <= 0 || (!shared && n_gpus > ndev) ||
+        n_gpus > 64) {
         err = "n_gpus exceeds the visible HIP devices";
         return SBR_EDEVICE;
     }
     std::vector<int> dl(n_gpus);
     for (int r = 0; r < n_gpus; r++) {
-        dl[r] = devices ? devices[r] : r;
+        dl[r] = devices ? devices[r] : r % ndev;
         if (dl[r] < 0 || dl[r] >= ndev) { err = "device id out of range"; return SBR_EDEVICE; }
-        for (int q = 0; q < r; q++)
+        for (int q = 0; q < r && !shared; q++)
             if (dl[q] == dl[r]) { err = "duplicate device id"; return SBR_EARG; }
     }
     // no RCCL here: the communicators are created by the first sweep that asks for the gather
     sbr_multi* m = new sbr_multi();
+    m->shared = shared;
     m->ranks.resize(n_gpus);
     for (int r = 0; r < n_gpus; r++) m->ranks[r].device = dl[r];
     int rc = SBR_OK;
@@ -399,6 +409,7 @@ int run_sharded(sbr_multi* m, int64_t n_col, int64_t n_u, const std::vector<sbr_
     if (grow(&k0.gather, &k0.gather_bytes, plan.gather_bytes() + 256)) { m->err = "gather buffer"; return SBR_ENOMEM; }
     const auto t2 = std::chrono::steady_clock::now();
     if (!rccl().ok) { m->err = rccl().err; return SBR_EDEVICE; }
+    if (m->shared && N > 1) { m->err = "the RCCL gather needs distinct devices (shared-device rehearsal)"; return SBR_EARG; }
     if (N > 1 && !m->comms_ok) {
         int rc = init_comms(m, m->err);
         if (rc) return rc;

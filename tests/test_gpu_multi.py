@@ -145,3 +145,46 @@ def test_fastpow_host_device_bitwise(engine, oracle):
                         [1e-4, 1.0, 0.5, 1.5, 1e-45, 1e-40, 3e38, np.inf]])
     for y in (0.14, 0.08):
         assert_same(engine.selftest_fastpow(x, np.full(len(x), y)), oracle.fastpow(x, y), f"fastpow y={y}")
+
+
+@pytest.mark.parametrize("n", [2, 3, 8])
+def test_multi_rank_rehearsal_on_shared_device(engine, monkeypatch, n):
+    """The n-rank fan-out on the one-GPU box (SBR_MULTI_SHARED_DEVICES=1: n ranks on device 0):
+    n host threads, n child contexts and streams, per-rank pinned landing buffers, the cyclic
+    deal with strided D2H and the all-or-nothing host scatter — the code an n-GPU node runs
+    with the direct transport — bitwise equal to the single-device context for the baseline
+    (with and without the 5-NaN early exit), hetero, interest and social sweeps.  The RCCL
+    gather needs distinct devices and is refused here, leaving the caller's arrays untouched."""
+    monkeypatch.setenv("SBR_MULTI_SHARED_DEVICES", "1")
+    m = sbr.Engine(n_gpus=n)
+    try:
+        assert m.n_gpus == n
+        g = sbr.fig5_grid(500).subset(np.arange(0, 500, 3))
+        for ee in (0, 5):
+            a = m.sweep_baseline(g, early_exit=ee)
+            b = engine.sweep_baseline(g, early_exit=ee)
+            for k in (*FIELDS, "status", "iters"):
+                assert_same(a[k], b[k], f"n={n} {k} (early_exit={ee})")
+        ph = m.host_phases()
+        assert ph["slowest_rank_sweep"] > 0 and ph["host_copy_or_gather"] > 0
+        with pytest.raises(Exception):
+            m.sweep_baseline(g, flags=_lib.SBR_FLAG_RCCL_GATHER)
+        h = sbr.hetero_config4(1024, 64).subset(np.arange(0, 1024, 97))
+        a = m.sweep_hetero(h.betas, h.dist, h.eta, h.t_end, h.u, h.p, h.kappa, h.lam, h.x0)
+        b = engine.sweep_hetero(h.betas, h.dist, h.eta, h.t_end, h.u, h.p, h.kappa, h.lam, h.x0)
+        for k in ("xi", "aw_max", "tol", "status", "iters", "tau_in_unc", "tau_out_unc"):
+            assert_same(a[k], b[k], f"n={n} hetero {k}")
+        beta = 1.0 / sbr.julia_range("0.0001", "1", 30)
+        u = sbr.julia_range("0.001", "1", 20)
+        a = m.sweep_interest(beta, 15.0, 30.0, u, 0.5, 0.6, 0.01, 0.06, 0.1)
+        b = engine.sweep_interest(beta, 15.0, 30.0, u, 0.5, 0.6, 0.01, 0.06, 0.1)
+        for k in (*FIELDS, "status", "iters", "rk_steps"):
+            assert_same(a[k], b[k], f"n={n} interest {k}")
+        bs = 1.0 / sbr.julia_range("0.01", "2", 512)[[0, 100, 200, 511]]
+        us = sbr.julia_range("0.001", "1", 512)[[10, 300]]
+        a = m.sweep_social(bs, 30.0 / 0.9, us, 0.99, 0.25, 0.25, max_iter=3)
+        b = engine.sweep_social(bs, 30.0 / 0.9, us, 0.99, 0.25, 0.25, max_iter=3)
+        for k in (*FIELDS, "status", "iters", "fp_iters", "rk_steps"):
+            assert_same(a[k], b[k], f"n={n} social {k}")
+    finally:
+        m.close()
