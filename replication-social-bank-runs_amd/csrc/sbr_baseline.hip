@@ -40,6 +40,15 @@ __device__ __forceinline__ void publish_column(const LearnArgs& a, int b)
 #ifndef SBR_LEARN_LANES
 #define SBR_LEARN_LANES 64 // columns per wave of learn_logistic_kernel
 #endif
+#ifndef SBR_LEARN_NT
+#define SBR_LEARN_NT 0 // the learning kernel's knot / hazard-term stores with the nontemporal hint (A/B r05_ee: neutral)
+#endif
+// one lane's knot-row store of the learning kernel
+#if SBR_LEARN_NT
+#define st_knot(p, v) __builtin_nontemporal_store((v), (p))
+#else
+#define st_knot(p, v) (*(p) = (v))
+#endif
 __global__ __launch_bounds__(SBR_LEARN_BLOCK) void learn_logistic_kernel(const double* __restrict__ beta,
                                                             const double* __restrict__ eta,
                                                             const double* __restrict__ t_end, LearnArgs a,
@@ -91,7 +100,7 @@ __global__ __launch_bounds__(SBR_LEARN_BLOCK) void learn_logistic_kernel(const d
         {
             const bool room = n < cap;
             const int w = room ? n : cap - 1;
-            if (room) { T[w] = t; Gv[w] = x; } // a rejected candidate is overwritten later
+            if (room) { st_knot(T + w, t); st_knot(Gv + w, x); } // a rejected candidate is overwritten later
             // bitwise (not short-circuit) logic: selects, no branches
             const bool pushed = acc & room;
             const bool over = acc & !room;
@@ -109,7 +118,7 @@ __global__ __launch_bounds__(SBR_LEARN_BLOCK) void learn_logistic_kernel(const d
                 const double E = sbr_exp(lam * t);
                 const double e = E * g;
                 const double In = hm == 0 ? 0.0 : hI + (0.5 * (he + e)) * (t - ht);
-                if (le) { H[n] = (p * E) * g; HI[n] = In; }
+                if (le) { st_knot(H + n, (p * E) * g); st_knot(HI + n, In); }
                 hI = le ? In : hI;
                 he = le ? e : he;
                 ht = le ? t : ht;

@@ -76,6 +76,9 @@ for s in ${STEPS:-tests smoke bench single}; do
     soclone) run soclone 300 python -u bench.py --workload social --steps 1 --warmup 0 --social-cols 2 --social-max-iter 16 --social-prof --no-cpu-baseline --no-verify ;;
     soclonevars) for v in ${VARS:-}; do run soclone_$v 300 env SBR_LIB=replication-social-bank-runs_amd/lib_var/$v/libsbr.so python -u bench.py --workload social --steps 1 --warmup 0 --social-cols 2 --social-max-iter 16 --social-prof --no-cpu-baseline --no-verify; done ;;
     interestvars) for v in ${VARS:-}; do run interest_$v 600 env SBR_LIB=replication-social-bank-runs_amd/lib_var/$v/libsbr.so python -u bench.py --workload interest --steps 3 --warmup 1 --no-cpu-baseline; done ;;
+    drvvars) for v in ${VARS:-}; do run drv_$v 300 env SBR_LIB=replication-social-bank-runs_amd/lib_var/$v/libsbr.so python -u bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline; done ;;
+    singlevars) for v in ${VARS:-}; do run single_$v 300 env SBR_LIB=replication-social-bank-runs_amd/lib_var/$v/libsbr.so python -u bench.py --no-pipeline --steps 20 --warmup 2 --no-cpu-baseline; done ;;
+    config1vars) for v in ${VARS:-}; do run config1_$v 300 env SBR_LIB=replication-social-bank-runs_amd/lib_var/$v/libsbr.so python -u bench.py --workload config1 --steps 50 --warmup 3 --no-cpu-baseline; done ;;
     knots) run knots 600 python -u -m pytest tests/test_gpu_knots.py tests/test_gpu_baseline.py -x -v --timeout 300 --timeout-method thread ${KTESTK:+-k "$KTESTK"} ;;
   esac
 done

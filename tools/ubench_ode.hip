@@ -38,6 +38,25 @@ struct StoreSink {
     }
 };
 
+// the same stores with the nontemporal hint (streamed past the caches' allocation)
+struct NtStoreSink {
+    double* T;
+    double* G;
+    int n = 0, cap;
+    __device__ bool push(bool acc, double t, double x)
+    {
+        const bool room = n < cap;
+        if (room) { __builtin_nontemporal_store(t, T + n); __builtin_nontemporal_store(x, G + n); }
+        n += (acc & room) ? 1 : 0;
+        return true;
+    }
+    __device__ bool start(double t, double x) { return push(true, t, x); }
+    __device__ bool step(bool acc, double, double tn, double, double, double y1, const StepK&, bool)
+    {
+        return push(acc, tn, y1);
+    }
+};
+
 #define OPAQUE(x) asm volatile("" : "+v"(x))
 constexpr int REPS = 2048;
 
@@ -48,6 +67,30 @@ template <int PART>
 __global__ void part(const double* beta, double* out, long long* cyc, long long* rt, long long* steps)
 {
     const double B = PART >= 6 ? beta[blockIdx.x * 64 + threadIdx.x] : beta[threadIdx.x & 63];
+    if (PART == 8) { // the full loop without stores on the bench grid's columns (compare with 6 / 9)
+        LogisticSys f{B};
+        NullSink sink;
+        OdeOut o;
+        const long long a0 = __builtin_amdgcn_s_memtime();
+        ode_scalar(f, sink, 30.0, 1e-4, DBL_EPS, DBL_EPS, 1000000, o);
+        const long long a1 = __builtin_amdgcn_s_memtime();
+        out[blockIdx.x * blockDim.x + threadIdx.x] = (double)sink.n;
+        if (threadIdx.x == 0 && blockIdx.x == 0) { cyc[0] = a1 - a0; rt[0] = 1; steps[0] = o.naccept + o.nreject; }
+        return;
+    }
+    if (PART == 9) { // nontemporal knot stores, row per column
+        const int col = blockIdx.x * 64 + threadIdx.x;
+        constexpr int cap = 4096;
+        NtStoreSink sink{g_T + (size_t)col * cap, g_G + (size_t)col * cap, 0, cap};
+        LogisticSys f{B};
+        OdeOut o;
+        const long long a0 = __builtin_amdgcn_s_memtime();
+        ode_scalar(f, sink, 30.0, 1e-4, DBL_EPS, DBL_EPS, 1000000, o);
+        const long long a1 = __builtin_amdgcn_s_memtime();
+        out[blockIdx.x * blockDim.x + threadIdx.x] = (double)sink.n;
+        if (threadIdx.x == 0 && blockIdx.x == 0) { cyc[0] = a1 - a0; rt[0] = 1; steps[0] = o.naccept + o.nreject; }
+        return;
+    }
     double acc = 0.0;
     long long nsteps = 0;
     __syncthreads();
@@ -167,6 +210,20 @@ int main()
     run(part<0>, 0); run(part<1>, 1); run(part<2>, 2); run(part<3>, 3); run(part<4>, 4); run(part<5>, 5);
     run(part<0>, 0, 32); run(part<0>, 0, 2048);
     run(part<6>, 6, 1); run(part<6>, 6, 32); run(part<7>, 7, 1); run(part<7>, 7, 32);
+    // every 4th wave of the grid alone: the loop without stores (8), with stores (6), with
+    // nontemporal stores (9), on the same 64 columns
+    for (int w = 0; w < 32; w += 4) {
+        double us[3];
+        int k = 0;
+        for (auto kern : {part<8>, part<6>, part<9>}) {
+            hipLaunchKernelGGL(kern, dim3(1), dim3(64), 0, 0, dg + w * 64, dout, dc, dr, ds);
+            long long c = 0;
+            (void)hipDeviceSynchronize();
+            (void)hipMemcpy(&c, dc, 8, hipMemcpyDeviceToHost);
+            us[k++] = c / 2400.0;
+        }
+        printf("  wave %2d: no stores %.1f us, stores %.1f us, nontemporal stores %.1f us\n", w, us[0], us[1], us[2]);
+    }
     // every wave of the grid: cycles of the slowest one
     for (int w = 0; w < 32; w += 4) {
         hipLaunchKernelGGL(part<6>, dim3(1), dim3(64), 0, 0, dg + w * 64, dout, dc, dr, ds);
