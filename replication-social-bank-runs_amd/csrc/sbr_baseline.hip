@@ -237,6 +237,9 @@ constexpr int EQ_TILE = SBR_EQ_TILE;  // u values per equilibrium block (one blo
 #ifndef SBR_EQ_REVERSE
 #define SBR_EQ_REVERSE 0 // A/B: dispatch the β columns last to first
 #endif
+#ifndef SBR_EQ_GROUP_INTERLEAVE
+#define SBR_EQ_GROUP_INTERLEAVE 1 // grouped equilibrium launches dispatch a column's copies together
+#endif
 #ifndef SBR_EQ_PRIO
 #define SBR_EQ_PRIO 0
 #endif
@@ -1618,7 +1621,13 @@ __global__ __launch_bounds__(BLOCK, INTEREST ? 1 : SBR_EQ_MINW) void equilibrium
 #if SBR_EQ_PRIO
     __builtin_amdgcn_s_setprio(SBR_EQ_PRIO); // A/B: issue priority over co-resident learning waves
 #endif
-    const int b = SBR_EQ_REVERSE ? (int)(gridDim.y - 1 - blockIdx.y) : (int)blockIdx.y;
+    int b = SBR_EQ_REVERSE ? (int)(gridDim.y - 1 - blockIdx.y) : (int)blockIdx.y;
+#if SBR_EQ_GROUP_INTERLEAVE
+    if (a.group > 1) { // grouped launch: the copies of a column back to back
+        const int per = (int)gridDim.y / a.group;
+        b = (b % a.group) * per + b / a.group;
+    }
+#endif
     const int j0 = blockIdx.x * EQ_TILE;
     const int j1 = j0 + EQ_TILE < a.n_u ? j0 + EQ_TILE : a.n_u;
 #ifdef SBR_EQ_WGTIME

@@ -474,10 +474,11 @@ void tend(sbr_ctx* c, hipStream_t s, int kind, hipEvent_t a)
 
 int launch_eq(sbr_ctx* c, hipStream_t s, const sbr::LearnBufs& L, const double* eta, const double* t_end,
               const double* u, int64_t n_beta, int64_t n_u, double kappa, const sbr_opts& o,
-              const sbr::ResultSoA& out, double* aw_path)
+              const sbr::ResultSoA& out, double* aw_path, int group = 1)
 {
     sbr::EqArgs ea{kappa, (int32_t)n_u, o.bisect_max_iters, c->lds_cap_b, aw_path,
                    (o.flags & SBR_FLAG_EXHAUSTIVE) ? 1 : 0, (o.flags >> 8) & 7};
+    ea.group = group;
     hipEvent_t t0 = tstart(c, s);
     if (aw_path && n_beta == 1 && n_u == 1) { // single point with its path: the whole workgroup on it
         ea.lds_cap = c->lds_cap;
@@ -1010,7 +1011,7 @@ int sbr_sweep_baseline_batch_dev(sbr_ctx* c, void* stream, int64_t n_batch, cons
                                  out->status ? out->status + g0 * np : nullptr,
                                  out->iters ? out->iters + g0 * np : nullptr};
                 int rc = launch_eq(c, es, W, eta + g0 * n_beta, t_end + g0 * n_beta, u, gn * n_beta, n_u, kappa, o, r,
-                                   nullptr);
+                                   nullptr, (int)gn);
                 if (rc) return rc;
                 for (int64_t i = 0; i < gn; i++) HIP_TRY(c, hipEventRecord(c->ev_grid[g0 + i], es), SBR_EDEVICE);
                 c->n_grid = g0 + gn;

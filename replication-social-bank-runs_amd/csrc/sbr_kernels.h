@@ -72,6 +72,11 @@ struct EqArgs {
     // compute_ξ's first iterate ξ_guess (solve_equilibrium_baseline(…; ξ_guess), solver.jl:413,441;
     // compute_ξ :309-312); NaN: the reference's default midpoint (τ̄_IN + τ̄_OUT)/2
     double xi_guess = __builtin_nan("");
+    // equilibrium_kernel launched over `group` grids of gridDim.y / group columns each (the
+    // pipelined batch's grouped launch): workgroups take the grids' copies of a column together
+    // (dispatch index y -> column (y mod group)·per + y / group), so a heavy column's copies start
+    // early instead of one per grid spread to the end of the launch
+    int32_t group = 1;
 };
 
 // Interest-rate extension (sbr_baseline.hip interest mode): value function on the HR grid.
