@@ -614,15 +614,22 @@ struct WaveLU {
     }
 };
 
+#ifndef SBR_HET_LEARN_WG
+// waves (columns) per learning workgroup.  Config-4 step, same-call A/Bs (r05_kk, r05_ll): one
+// wave per workgroup 43.4 ms (45.7–46.0 with this kernel's wave indexing), 4 waves (one per SIMD
+// of a CU) 42.2–42.3, 8 waves (two per SIMD: the learning becomes the critical path) 47.6
+#define SBR_HET_LEARN_WG 4
+#endif
 template <int K>
-__global__ __launch_bounds__(64) void learn_hetero_wave_kernel(const double* __restrict__ betas,
+__global__ __launch_bounds__(64 * SBR_HET_LEARN_WG) void learn_hetero_wave_kernel(const double* __restrict__ betas,
                                                                const double* __restrict__ dist,
                                                                const double* __restrict__ eta,
                                                                const double* __restrict__ t_end, LearnArgs a,
                                                                HeteroBufs L)
 {
-    const int c = blockIdx.x;
-    const int lane = threadIdx.x;
+    const int c = blockIdx.x * SBR_HET_LEARN_WG + (int)(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (c >= a.n_beta) return; // a whole wave (the column index is wave-uniform)
     const bool act = lane < K;
     const WaveRow<K> R(lane, betas + (size_t)c * K, dist);
     const double ETA = eta[c], T1 = t_end[c], T0 = 0.0;
@@ -1898,7 +1905,8 @@ static hipError_t launch_hetero_k(const double* betas, const double* dist, const
         hipLaunchKernelGGL(learn_hetero_wave4_kernel<K>, dim3((la.n_beta + 3) / 4), dim3(64), 0, s, betas, dist, eta,
                            t_end, la, L);
 #elif SBR_HET_LEARN_WAVE
-        hipLaunchKernelGGL(learn_hetero_wave_kernel<K>, dim3(la.n_beta), dim3(64), 0, s, betas, dist, eta, t_end, la, L);
+        hipLaunchKernelGGL(learn_hetero_wave_kernel<K>, dim3((la.n_beta + SBR_HET_LEARN_WG - 1) / SBR_HET_LEARN_WG),
+                           dim3(64 * SBR_HET_LEARN_WG), 0, s, betas, dist, eta, t_end, la, L);
 #else
         hipLaunchKernelGGL(learn_hetero_kernel<K>, dim3((la.n_beta + 63) / 64), dim3(64), 0, s, betas, dist, eta,
                            t_end, la, L);
