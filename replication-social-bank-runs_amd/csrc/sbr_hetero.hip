@@ -617,7 +617,7 @@ struct WaveLU {
 #ifndef SBR_HET_LEARN_WG
 // waves (columns) per learning workgroup.  Config-4 step, same-call A/Bs (r05_kk, r05_ll): one
 // wave per workgroup 43.4 ms (45.7–46.0 with this kernel's wave indexing), 4 waves (one per SIMD
-// of a CU) 42.2–42.3, 8 waves (two per SIMD: the learning becomes the critical path) 47.6
+// of a CU) 42.2–42.3, 2 waves 51.6 (r05_nn), 8 waves (two per SIMD: the learning becomes the critical path) 47.6
 #define SBR_HET_LEARN_WG 4
 #endif
 template <int K>
