@@ -27,7 +27,10 @@ namespace sbr {
 // Learning kernel
 // ============================================================================
 #ifndef SBR_LEARN_BLOCK
-#define SBR_LEARN_BLOCK 64
+// lanes per learning workgroup: two waves (two columns' 64-lane rows) per workgroup.  Same-call
+// A/Bs (r05_oo, r05_pp): the co-running equilibrium kernel 1.39 -> 1.36 ms, config-3 step
+// 1.487-1.507 -> 1.455 ms at 50 steps; 256 lanes slower (1.524 ms)
+#define SBR_LEARN_BLOCK 128
 #endif
 
 // readiness sweeps: column b is complete (knots, counters, status written by this lane) —

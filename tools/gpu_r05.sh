@@ -79,6 +79,7 @@ for s in ${STEPS:-tests smoke bench single}; do
     drvvars) for v in ${VARS:-}; do run drv_$v 300 env SBR_LIB=replication-social-bank-runs_amd/lib_var/$v/libsbr.so python -u bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline; done ;;
     singlevars) for v in ${VARS:-}; do run single_$v 300 env SBR_LIB=replication-social-bank-runs_amd/lib_var/$v/libsbr.so python -u bench.py --no-pipeline --steps 20 --warmup 2 --no-cpu-baseline; done ;;
     config1vars) for v in ${VARS:-}; do run config1_$v 300 env SBR_LIB=replication-social-bank-runs_amd/lib_var/$v/libsbr.so python -u bench.py --workload config1 --steps 50 --warmup 3 --no-cpu-baseline; done ;;
+    abrep) for i in 1 2; do run rep${i}_base 300 python -u bench.py --no-cpu-baseline --no-verify && for v in ${VARS:-}; do run rep${i}_$v 300 env SBR_LIB=replication-social-bank-runs_amd/lib_var/$v/libsbr.so python -u bench.py --no-cpu-baseline --no-verify; done && run rep${i}_drvbase 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-verify && for v in ${VARS:-}; do run rep${i}_drv$v 300 env SBR_LIB=replication-social-bank-runs_amd/lib_var/$v/libsbr.so python -u bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-verify; done; done ;;
     knots) run knots 600 python -u -m pytest tests/test_gpu_knots.py tests/test_gpu_baseline.py -x -v --timeout 300 --timeout-method thread ${KTESTK:+-k "$KTESTK"} ;;
   esac
 done
