@@ -27,10 +27,16 @@ namespace sbr {
 // Learning kernel
 // ============================================================================
 #ifndef SBR_LEARN_BLOCK
-// lanes per learning workgroup: two waves (two columns' 64-lane rows) per workgroup.  Same-call
-// A/Bs (r05_oo, r05_pp): the co-running equilibrium kernel 1.39 -> 1.36 ms, config-3 step
-// 1.487-1.507 -> 1.455 ms at 50 steps; 256 lanes slower (1.524 ms)
+// lanes per learning workgroup of the pipelined batch's streamed-hazard launches (learning that
+// runs beside the equilibrium kernel): two waves per workgroup.  Same-call A/Bs (r05_oo, r05_pp):
+// the co-running equilibrium kernel 1.39 -> 1.36 ms, config-3 step 1.487-1.507 -> 1.455 ms at 50
+// steps; 256 lanes slower (1.524 ms).  Latency-critical launches (single sweeps, the batch's
+// first group, config 1) keep one wave per workgroup: with two, config 1 took 2.24 instead of
+// 2.15 ms and a single sweep 4.20 instead of 4.01 ms (r05_qq)
 #define SBR_LEARN_BLOCK 128
+#endif
+#ifndef SBR_LEARN_BLOCK_LAT
+#define SBR_LEARN_BLOCK_LAT 64
 #endif
 
 // readiness sweeps: column b is complete (knots, counters, status written by this lane) —
@@ -52,7 +58,8 @@ __device__ __forceinline__ void publish_column(const LearnArgs& a, int b)
 #else
 #define st_knot(p, v) (*(p) = (v))
 #endif
-__global__ __launch_bounds__(SBR_LEARN_BLOCK) void learn_logistic_kernel(const double* __restrict__ beta,
+template <int LB>
+__global__ __launch_bounds__(LB) void learn_logistic_kernel(const double* __restrict__ beta,
                                                             const double* __restrict__ eta,
                                                             const double* __restrict__ t_end, LearnArgs a,
                                                             LearnBufs L)
@@ -65,7 +72,7 @@ __global__ __launch_bounds__(SBR_LEARN_BLOCK) void learn_logistic_kernel(const d
     // SBR_LEARN_LANES columns per wave (lanes beyond idle): a knot store or load of the wave
     // touches one row per active lane
     const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
-    const int b = (blockIdx.x * (SBR_LEARN_BLOCK / 64) + wv) * SBR_LEARN_LANES + ln;
+    const int b = (blockIdx.x * (LB / 64) + wv) * SBR_LEARN_LANES + ln;
     const bool live = ln < SBR_LEARN_LANES && b < a.n_beta;
     const double BETA = live ? beta[b] : 1.0, ETA = live ? eta[b] : 1.0, T1 = live ? t_end[b] : 1.0, T0 = 0.0;
     const size_t row = (size_t)(live ? b : 0) * (size_t)L.cap;
@@ -2142,9 +2149,15 @@ hipError_t launch_point_coop(const LearnBufs& L, const double* eta, const double
 hipError_t launch_learn_logistic(const double* beta, const double* eta, const double* t_end, const LearnArgs& a,
                                  const LearnBufs& L, hipStream_t s)
 {
-    constexpr int per_block = (SBR_LEARN_BLOCK / 64) * SBR_LEARN_LANES;
-    dim3 grid((a.n_beta + per_block - 1) / per_block);
-    hipLaunchKernelGGL(learn_logistic_kernel, grid, dim3(SBR_LEARN_BLOCK), 0, s, beta, eta, t_end, a, L);
+    if (a.fuse_hazard && !a.ready_q) {
+        constexpr int per_block = (SBR_LEARN_BLOCK / 64) * SBR_LEARN_LANES;
+        hipLaunchKernelGGL(learn_logistic_kernel<SBR_LEARN_BLOCK>, dim3((a.n_beta + per_block - 1) / per_block),
+                           dim3(SBR_LEARN_BLOCK), 0, s, beta, eta, t_end, a, L);
+    } else {
+        constexpr int per_block = (SBR_LEARN_BLOCK_LAT / 64) * SBR_LEARN_LANES;
+        hipLaunchKernelGGL(learn_logistic_kernel<SBR_LEARN_BLOCK_LAT>, dim3((a.n_beta + per_block - 1) / per_block),
+                           dim3(SBR_LEARN_BLOCK_LAT), 0, s, beta, eta, t_end, a, L);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (a.ready_q) return hipSuccess; // readiness sweep: eq_ready_kernel runs each column's hazard
