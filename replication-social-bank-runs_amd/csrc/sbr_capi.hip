@@ -41,7 +41,13 @@
 #define SBR_HET_LEARN_MASK 0 // A/B: hetero batch learning confined to half the CUs
 #endif
 #ifndef SBR_LEARN_GROUP
-#define SBR_LEARN_GROUP 1 // grids per learning launch of the pipelined batch (A/B: 2 was slower, 1.567 -> 1.631 ms per step: r04_j)
+// grids per learning (and equilibrium) launch of the pipelined batch.  Round 4 measured 2 slower
+// (1.567 -> 1.631 ms per step, r04_j); with the column-interleaved grouped equilibrium launch and
+// two-wave learning workgroups it is faster: the equilibrium launch over 4,096 columns sheds half
+// the per-grid tails (1.35 -> 1.28 ms per grid), step 1.445-1.462 -> 1.411-1.437 ms at 50 steps and
+// 1.529-1.576 -> 1.483-1.524 ms at the driver's 20 (same-call A/Bs r05_uu, r05_vv, r05_ww; 3 and 4
+// grids were no better, 6 learning workspaces slower)
+#define SBR_LEARN_GROUP 2
 #endif
 #ifndef SBR_LEARN_FILL_COLS
 #define SBR_LEARN_FILL_COLS 2048 // narrower grids share a learning launch up to this many columns
