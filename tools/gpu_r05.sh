@@ -46,7 +46,7 @@ for s in ${STEPS:-tests smoke bench single}; do
     hetvars) for v in ${VARS:-}; do run hetero_$v 600 env SBR_LIB=replication-social-bank-runs_amd/lib_var/$v/libsbr.so python -u bench.py --workload hetero --steps 10 --warmup 2 --phases --no-cpu-baseline; done ;;
     pmcall) for w in ${PMCW:-base hetero interest socbulk soclone}; do
               case $w in
-                base) BA="" ;;
+                base) BA="--steps 4 --warmup 2" ;;  # whole 2-grid launches only (SBR_LEARN_GROUP)
                 hetero) BA="--workload hetero --steps 2 --warmup 1" ;;
                 interest) BA="--workload interest --steps 1 --warmup 1" ;;
                 socbulk) BA="--workload social --steps 1 --warmup 0 --social-max-iter 16" ;;
