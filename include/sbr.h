@@ -41,8 +41,8 @@ extern "C" {
 typedef struct sbr_ctx sbr_ctx;
 
 typedef struct {
-    double ode_reltol;          /* learning.jl:43 reltol = eps() */
-    double ode_abstol;          /* learning.jl:43 abstol = eps() */
+    double ode_reltol;          /* learning.jl:43 reltol = eps() (0 = eps(): every zero field is the default) */
+    double ode_abstol;          /* learning.jl:43 abstol = eps() (0 = eps()) */
     int64_t ode_maxiters;       /* OrdinaryDiffEq default maxiters = 1e6 (SBR_DEFAULT_ODE_MAXITERS) */
     int32_t bisect_max_iters;   /* solver.jl:309 max_iters = 100 */
     int32_t early_exit_nan_run; /* 1_baseline.jl:147,221: 5; 0 disables */
@@ -50,9 +50,10 @@ typedef struct {
     int32_t hetero_max_iters;   /* heterogeneity_solver.jl:49 max_iters = 500 */
     int32_t flags;              /* SBR_FLAG_* */
     int32_t pad;                /* social sweep: knot capacity per buffer (0 = default 98304) */
-    double xi_guess;            /* solver.jl:413,441 ξ_guess: compute_ξ's first iterate; NaN = the default
-                                   midpoint (τ̄_IN + τ̄_OUT)/2.  sbr_equilibrium_on_knots only: the other
-                                   entry points return SBR_EARG when it is set */
+    double xi_guess;            /* solver.jl:413,441 ξ_guess: compute_ξ's first iterate, read only with
+                                   SBR_FLAG_XI_GUESS (a zero-filled opts is the default midpoint
+                                   (τ̄_IN + τ̄_OUT)/2).  sbr_equilibrium_on_knots[_pdf] only: the other
+                                   entry points return SBR_EARG when the flag is set */
 } sbr_opts;
 
 /* Evaluate every τ̄ knot of the crossing scan and of the AW path (no block
@@ -69,6 +70,9 @@ typedef struct {
  * the default direct transport (each GPU copies its own columns into the caller's arrays over
  * its own PCIe link, no collective).  Same results. */
 #define SBR_FLAG_RCCL_GATHER 0x4
+/* opts->xi_guess holds compute_ξ's first iterate (solve_equilibrium_baseline(...; ξ_guess),
+ * solver.jl:413,441); without this flag xi_guess is ignored and the midpoint is used. */
+#define SBR_FLAG_XI_GUESS 0x8
 /* Diagnostics (timing breakdown only — results are NOT the reference's):
  * stop every point after the crossing scan / after the ξ bisection, or
  * report the number of 64-knot AW blocks evaluated in `iters` instead of
@@ -91,7 +95,7 @@ typedef struct {
     int32_t* iters;      /* bisection iterations (may be NULL)  */
 } sbr_result_soa;
 
-/* Fills *o with the reference defaults (eps() tolerances, 1e6, 100, 5, 65536, 500, ξ_guess = NaN). */
+/* Fills *o with the reference defaults (eps() tolerances, 1e6, 100, 5, 65536, 500, no ξ_guess). */
 void sbr_default_opts(sbr_opts* o);
 
 /* Creates a context on HIP device `device` (the caller's rank-local GPU). */
@@ -150,20 +154,33 @@ int sbr_sweep_baseline_dev(sbr_ctx* ctx, void* stream, const double* beta, const
                            double kappa, double lambda, const sbr_opts* opts, sbr_result_soa* out);
 
 /*
- * n_batch grids that share n_beta, n_u, u and the scalars, swept back to back
- * and pipelined: the learning stage (latency-bound, one lane per β) of batch
- * k+1 runs on a second, highest-priority stream while the equilibrium stage of
- * batch k fills the CUs.  beta/eta/t_end are [n_batch × n_beta] (row k =
- * batch k); every out field is [n_batch × n_beta × n_u] (iters may be NULL).
- * Device pointers; inputs are read after the work already enqueued on
- * `stream`, results are complete for work enqueued on `stream` afterwards.
- * Each batch gives exactly what sbr_sweep_baseline_dev gives for it.  Use a
- * context from one stream at a time.
+ * n_batch grids that share n_beta, n_u, u and the scalars (the Fig 5 loop of
+ * scripts/1_baseline.jl:224-267 for n_batch parameter grids), swept back to back.
+ * The learning stage is latency-bound (one serial ODE per β lane), so the grids
+ * are learned together — as many as fit one learning launch of at most one wave
+ * per SIMD and the workspace budget (sbr_set_batch_workspace) — and their
+ * equilibria then run back to back; a longer batch learns its next group into a
+ * second workspace beside those equilibria.  beta/eta/t_end are
+ * [n_batch × n_beta] (row k = batch k); every out field is
+ * [n_batch × n_beta × n_u] (iters may be NULL).  Device pointers; inputs are read
+ * after the work already enqueued on `stream`, results are complete for work
+ * enqueued on `stream` afterwards.  Each batch gives exactly what
+ * sbr_sweep_baseline_dev gives for it.  Use a context from one stream at a time.
  */
 int sbr_sweep_baseline_batch_dev(sbr_ctx* ctx, void* stream, int64_t n_batch, const double* beta,
                                  const double* eta, const double* t_end, double x0, const double* u,
                                  int64_t n_beta, int64_t n_u, double p, double kappa, double lambda,
                                  const sbr_opts* opts, sbr_result_soa* out);
+/* Size (allocate) now the workspaces a later sbr_sweep_baseline_batch_dev of n_batch grids of
+ * n_beta columns with these opts (knot_capacity) will use, so that the call itself allocates
+ * nothing — the HBM allocator's work stays out of a timed loop.  Waits for the context's
+ * earlier work.  The batch call re-sizes by itself when needed; this is never required. */
+int sbr_batch_reserve(sbr_ctx* ctx, int64_t n_batch, int64_t n_beta, const sbr_opts* opts);
+/* Budget in bytes for the learning workspaces of baseline batches (0 = 40 % of the free plus
+ * already held HBM at call time): it caps the grids learned per launch (each grid takes
+ * n_beta × (4 × knot_capacity × 8 + 24) bytes, two workspaces when the batch needs more than
+ * one group).  An allocation that fails anyway halves the group and retries, down to one grid. */
+int sbr_set_batch_workspace(sbr_ctx* ctx, int64_t bytes);
 
 /*
  * Make `stream` wait (device side, no host sync) until grid k of the last

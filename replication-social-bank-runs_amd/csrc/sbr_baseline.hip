@@ -26,18 +26,14 @@ namespace sbr {
 // ============================================================================
 // Learning kernel
 // ============================================================================
-#ifndef SBR_LEARN_BLOCK
 // lanes per learning workgroup of the pipelined batch's streamed-hazard launches (learning that
 // runs beside the equilibrium kernel): two waves per workgroup.  Same-call A/Bs (r05_oo, r05_pp):
 // the co-running equilibrium kernel 1.39 -> 1.36 ms, config-3 step 1.487-1.507 -> 1.455 ms at 50
 // steps; 256 lanes slower (1.524 ms).  Latency-critical launches (single sweeps, the batch's
 // first group, config 1) keep one wave per workgroup: with two, config 1 took 2.24 instead of
 // 2.15 ms and a single sweep 4.20 instead of 4.01 ms (r05_qq)
-#define SBR_LEARN_BLOCK 128
-#endif
-#ifndef SBR_LEARN_BLOCK_LAT
-#define SBR_LEARN_BLOCK_LAT 64
-#endif
+constexpr int kLearnBlock = 128;
+constexpr int kLearnBlockLat = 64;
 
 // readiness sweeps: column b is complete (knots, counters, status written by this lane) —
 // release it to the equilibrium workgroups (agent scope: they run on other CUs / XCDs)
@@ -46,18 +42,8 @@ __device__ __forceinline__ void publish_column(const LearnArgs& a, int b)
     const int k = atomicAdd(a.ready_tail, 1);
     __hip_atomic_store(a.ready_q + k, b + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
-#ifndef SBR_LEARN_LANES
-#define SBR_LEARN_LANES 64 // columns per wave of learn_logistic_kernel
-#endif
-#ifndef SBR_LEARN_NT
-#define SBR_LEARN_NT 0 // the learning kernel's knot / hazard-term stores with the nontemporal hint (A/B r05_ee: neutral)
-#endif
-// one lane's knot-row store of the learning kernel
-#if SBR_LEARN_NT
-#define st_knot(p, v) __builtin_nontemporal_store((v), (p))
-#else
+// one lane's knot-row store of the learning kernel (the nontemporal hint was neutral, r05_ee)
 #define st_knot(p, v) (*(p) = (v))
-#endif
 template <int LB>
 __global__ __launch_bounds__(LB) void learn_logistic_kernel(const double* __restrict__ beta,
                                                             const double* __restrict__ eta,
@@ -66,14 +52,10 @@ __global__ __launch_bounds__(LB) void learn_logistic_kernel(const double* __rest
 {
     // latency-bound (one serial ODE per lane): take issue priority over co-resident
     // equilibrium waves of a previous batch
-#ifndef SBR_LEARN_NOPRIO
     __builtin_amdgcn_s_setprio(3);
-#endif
-    // SBR_LEARN_LANES columns per wave (lanes beyond idle): a knot store or load of the wave
-    // touches one row per active lane
-    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
-    const int b = (blockIdx.x * (LB / 64) + wv) * SBR_LEARN_LANES + ln;
-    const bool live = ln < SBR_LEARN_LANES && b < a.n_beta;
+    // one column per lane (a knot store or load of the wave touches one row per active lane)
+    const int b = blockIdx.x * LB + threadIdx.x;
+    const bool live = b < a.n_beta;
     const double BETA = live ? beta[b] : 1.0, ETA = live ? eta[b] : 1.0, T1 = live ? t_end[b] : 1.0, T0 = 0.0;
     const size_t row = (size_t)(live ? b : 0) * (size_t)L.cap;
     double* __restrict__ T = L.t + row;
@@ -186,7 +168,7 @@ __global__ __launch_bounds__(LB) void learn_logistic_kernel(const double* __rest
             Lp->n_reject[b] = (int)o.nreject;
             if (ap->ready_q) publish_column(*ap, b);
         }
-    } sink{T, Gv, fuse ? L.hr + row : nullptr, fuse ? L.hrI + row : nullptr, 0, L.cap, -1, 0.0, -INFINITY, ETA,
+    } sink{T, Gv, fuse ? L.hr + row : nullptr, fuse ? L.hrI + row : nullptr, 0, L.lim, -1, 0.0, -INFINITY, ETA,
            0, 0, a.stop_after_eta != 0 ? 1 : 0, st, fuse ? 1 : 0, 0, BETA, a.lam, a.p, 0.0, 0.0, 0.0, 0.0,
            &L, &a, b};
     LogisticSys f{BETA};
@@ -231,38 +213,13 @@ __global__ __launch_bounds__(HN_BLOCK) void hazard_norm_kernel(LearnArgs a, Lear
 // e = exp(λτ̄)·g, the cumulative trapezoid (sequential, in the reference's
 // order) and HR = (p·exp(λτ̄))·g / (p·I + (1−p)·I_η).
 // ============================================================================
-#ifndef SBR_EQ_WIDE
-#define SBR_EQ_WIDE 768
-#endif
-#ifndef SBR_EQ_MINW
-#define SBR_EQ_MINW 6 // waves per SIMD the baseline equilibrium kernel must fit (two 12-wave blocks per CU)
-#endif
+constexpr int kEqWide = 768; // lanes per equilibrium workgroup on wide u tiles
+constexpr int kEqMinW = 6;    // waves per SIMD the baseline equilibrium kernel must fit (two 12-wave blocks per CU)
 constexpr int HZ_BLOCK = 256;
 constexpr int HZ_LDS = 1024; // τ̄ knots per LDS chunk of the hazard kernel
 constexpr int HZ_REG = 16;   // τ̄ knots per thread held in registers (ntau <= 4096: one pass over HBM)
-#ifndef SBR_EQ_TILE
-#define SBR_EQ_TILE 4096
-#endif
-constexpr int EQ_TILE = SBR_EQ_TILE;  // u values per equilibrium block (one block per β column up to this)
-#ifndef SBR_EQ_REVERSE
-#define SBR_EQ_REVERSE 0 // A/B: dispatch the β columns last to first
-#endif
-#ifndef SBR_EQ_GROUP_INTERLEAVE
-#define SBR_EQ_GROUP_INTERLEAVE 1 // grouped equilibrium launches dispatch a column's copies together
-#endif
-#ifndef SBR_EQ_PRIO
-#define SBR_EQ_PRIO 0
-#endif
-#ifndef SBR_AW_WIN
-#define SBR_AW_WIN 6
-#endif
-#ifndef SBR_AW_SCAN
-#define SBR_AW_SCAN 1 // AW_max by the outward scan from the predicted peak (aw_scan) where its bounds hold
-#endif
-constexpr int kAwWin = SBR_AW_WIN; // 8-blocks each side of the predicted AW peak evaluated first
-#ifndef SBR_BISECT_FAST
-#define SBR_BISECT_FAST 1 // single-interval bisection steps decided by the line's estimate (solve_from_buffers)
-#endif
+constexpr int EQ_TILE = 4096; // u values per equilibrium block (one block per β column up to this)
+constexpr int kAwWin = 6;     // 8-blocks each side of the predicted AW peak evaluated first
 
 // I_k = I_{k-1} + term_k over s_I[0, cn) in place, left to right (the reference's rounding
 // order), by the 64 lanes of one wave: lane l holds terms [16l, 16l + 16) in registers and
@@ -356,7 +313,7 @@ __device__ __forceinline__ void hazard_column(const int b, const double BETA, co
     }
     // the pdf at knot i: compute_pdf_symbolic_baseline's βG(1 − G) (learning.jl:161-173), or the
     // caller's values (a.pdf: the interpolant of another pdf on the same knots)
-    const double* __restrict__ PD = a.pdf;
+    const double* __restrict__ PD = a.pdf ? a.pdf + row : nullptr; // the caller's pdf rows, laid out like G
     auto pdf_k = [&](int i) -> double {
         if (PD) return PD[i];
         const double x = Gv[i];
@@ -521,9 +478,7 @@ __global__ __launch_bounds__(HZ_BLOCK) void hazard_kernel(const double* __restri
     __shared__ double s_t[HZ_LDS + 1];  // τ̄ likewise
     __shared__ double s_I[HZ_LDS];
     __shared__ double s_Ieta;
-#ifndef SBR_HZ_NOPRIO
     __builtin_amdgcn_s_setprio(3);
-#endif
     const int b = blockIdx.x;
     hazard_column<HZ_BLOCK>(b, beta[b], eta[b], a, L, s_eg, s_t, s_I, &s_Ieta);
 }
@@ -567,7 +522,7 @@ struct Summ {
     // aw_scan's knot offset for AW_OUT(b_j) <= G[j + koff]: 1 when consecutive knots are more than
     // 1e-15·t[n−1] apart (b_j then lies below t[j + 1]: bracket <= j), else 2 (knots 2 apart)
     int koff;
-    // prefix / suffix extremes of the HR block summaries (SBR_SCAN_BS): hpm = prefix max of hmax,
+    // prefix / suffix extremes of the HR block summaries: hpm = prefix max of hmax,
     // hpn = prefix min of hmin, hsm = suffix max of hmax, hsn = suffix min of hmin, over nbh
     // blocks; null: the linear block scans
     const double* hpm;
@@ -615,20 +570,9 @@ __device__ __forceinline__ int first_ge_down(F key, int hi, double x)
 // (+ the 1e-14 rounding margin) do not already put it at or below the running maximum; runs
 // of knots the bounds dismiss are skipped with one search in G (right) or in G and τ̄ (left).
 // The maximum equals the exhaustive one bit for bit (G has no NaN here).
-#ifndef SBR_SCAN_BS
-#define SBR_SCAN_BS 1 // crossing scans by binary search over prefix / suffix block tables
-#endif
-#ifndef SBR_AW_OWN
-// aw_scan: knot offset 0 for the AW_OUT bound inside [ξ/2, 2ξ] (b_i = t[i] exactly there).  A/B
-// (profiles/experiments/r05_d_*): exact evaluations per run point 38.7 → 20.4, but the kernel
-// 1.320 → 1.361 ms alone (1.389 → 1.450 ms in the pipeline): an exact evaluation costs about what
-// a bounded trip costs (the bracket walk's LDS round trips dominate both), and the window test
-// adds to every trip.  Off.
-#define SBR_AW_OWN 0
-#endif
-#ifndef SBR_AW_K1
-#define SBR_AW_K1 1 // aw_scan bounds AW_OUT(b_j) by G[j + 1] where consecutive knots are separated
-#endif
+// (A knot offset 0 for the AW_OUT bound inside [ξ/2, 2ξ], where b_i = t[i] exactly, halved the exact
+// evaluations and was slower: an exact evaluation costs about what a bounded trip costs,
+// profiles/experiments/r05_d_*)
 template <class P>
 __device__ __forceinline__ void aw_scan(P T, P G, const int n, const int ntau, const int nle, const double ETA,
                                         const double xi, const double icc, const double occ, const double G0,
@@ -680,16 +624,6 @@ __device__ __forceinline__ void aw_scan(P T, P G, const int n, const int ntau, c
     }
     const int kc = ka;
     const double ub_left = awout;
-    // Own-knot bounds (SBR_AW_OWN, off by default): for τ̄_i = t[i] in [ξ/2, 2ξ] with occ = ξ,
-    // b_i = (t[i] − ξ) + ξ is t[i] exactly (Sterbenz), so AW_OUT(b_j) <= G[j] for every j <= i
-    // there: the run bounds may take knot offset 0 instead of koff inside that window
-    // (tools/aw_scan_sim.py, config 3: 39 → 21 exact evaluations and 72 → 63 loop trips per run
-    // point; the maximum is unchanged) — measured slower, see SBR_AW_OWN.
-    const bool own_ok = SBR_AW_OWN && occ == xi;
-    const double own_lo = 0.5 * xi, own_hi = 2.0 * xi;
-    auto koff_at = [&](int i, double ti) -> int {
-        return (own_ok && i < nle && ti >= own_lo && ti <= own_hi) ? 0 : koff;
-    };
     // right of c
     double LA = awin; // lower bound of AW_IN(a_j) for every j >= i
     for (int i = c + 1; i < ntau;) {
@@ -699,8 +633,7 @@ __device__ __forceinline__ void aw_scan(P T, P G, const int n, const int ntau, c
         const double lb = av >= 0 ? ga0 : 0.0;
         LA = LA > lb ? LA : lb;
         const double V = (((mx - G0) + LA) - M) - dd; // G[k] <= V: every knot up to k is <= V + dd
-        const int ko = koff_at(i, ti);
-        const int k2 = i + ko < n - 1 ? i + ko : n - 1;
+        const int k2 = i + koff < n - 1 ? i + koff : n - 1;
         if (G[k2] > V) {
             const double v = exact(i, av, xa);
             if (v > mx) mx = v;
@@ -711,10 +644,8 @@ __device__ __forceinline__ void aw_scan(P T, P G, const int n, const int ntau, c
         // every knot j with G[min(j + 2, n − 1)] <= V is at or below mx: skip to the first other
         const int kl = ssl_gallop(G, n, k2, V);
         if (kl >= n - 1) break;
-        // G[kl + 1] > V: the first knot whose bound is not dismissed (offset 0 while the skip stays
-        // inside the own-bound window, else the run offset koff)
-        int inext = kl + 1 - koff;
-        if (ko == 0) inext = T[kl] <= own_hi ? kl + 1 : (inext > i + 1 ? inext : i + 1);
+        // G[kl + 1] > V: the first knot whose bound is not dismissed
+        const int inext = kl + 1 - koff;
         const double an = av_of(inext);
         seek(ka + (inext - i), an > 0 ? an : 0.0);
         i = inext;
@@ -727,8 +658,7 @@ __device__ __forceinline__ void aw_scan(P T, P G, const int n, const int ntau, c
     }
     for (int i = c - 1; i >= 0;) {
         const double ti = tau(i);
-        const int ko = koff_at(i, ti);
-        const int k2 = i + ko < n - 1 ? i + ko : n - 1;
+        const int k2 = i + koff < n - 1 ? i + koff : n - 1;
         const double g2 = G[k2] > 0.0 ? G[k2] : 0.0;
         UB = UB < g2 ? UB : g2;
         const double Vp = (((UB + G0) + M) - mx) + dd; // AW_IN(a_j) >= G[bracket(a_j)] − dd
@@ -894,7 +824,6 @@ __device__ __forceinline__ void solve_from_buffers(P T, P G, P H, const Summ& S,
     double c_ic_x = NAN, c_ic_v = 0.0;
     uint32_t s = SBR_NO_RUN_MAXITER;
     double xi = NAN, tolr = INFINITY;
-#if SBR_BISECT_FAST
     // Single-interval bisection.  Once the bracket is one knot interval [t0, t1) (jlo == jhi),
     // G(ξ) there is the line g0·(1 − δ) + g1·δ, and the error AW − κ of a midpoint is
     // e0 + s·(x − t0) up to a few ulps of the operands.  Every midpoint whose estimate is
@@ -909,20 +838,17 @@ __device__ __forceinline__ void solve_from_buffers(P T, P G, P H, const Summ& S,
     // the exact body.
     double f_s = NAN, f_c = 0.0;
     const double f_lim = tolerance + 1e-13;
-#endif
     for (int iter = 1; iter <= max_iters; iter++) {
         r.iters = iter;
         const double dd = xmin - xmax;
         if (collapsed(dd)) { s = SBR_NO_RUN_COLLAPSE; break; }
         if (iter == max_iters - 1) { s = SBR_NO_RUN_MAXITER; break; }
         const double xo = xnew;
-#if SBR_BISECT_FAST
         {
             const double ea = fma(f_s, xo, f_c);
             if (ea < -f_lim) { xmin = xo; xnew = 0.5 * (xo + xmax); continue; }
             if (ea > f_lim) { xmax = xo; xnew = 0.5 * (xo + xmin); continue; }
         }
-#endif
         const double ic = dmin(tin, xo), oc = dmin(tout, xo);
         const int j = ssl_range(T, jlo, jhi, xo); // t[jlo] <= ξmin <= xo <= ξmax < t[jhi+1]
         // G(oc)
@@ -961,7 +887,6 @@ __device__ __forceinline__ void solve_from_buffers(P T, P G, P H, const Summ& S,
         } else {
             xmin = xo; jlo = j; xnew = 0.5 * (xo + xmax);
         }
-#if SBR_BISECT_FAST
         if (f_s != f_s && jlo == jhi && ic == tin && tin <= xmin && xmax <= tout && xmax + eps <= thi) {
             // j + 1 < n and ξ + ε, tin + ε in range were tested by this iteration
             const double t0 = T[j], g0 = G[j], g1 = G[j + 1];
@@ -974,7 +899,6 @@ __device__ __forceinline__ void solve_from_buffers(P T, P G, P H, const Summ& S,
                 }
             }
         }
-#endif
     }
     if (flag) { r.status = flag | lbits; return; }
     if (s != SBR_RUN) { r.status = s | lbits; return; }
@@ -1036,11 +960,9 @@ __device__ __forceinline__ void solve_from_buffers(P T, P G, P H, const Summ& S,
     // τ* = t_half + (s_in + s_out)/2
     const double tstar = S.t_half + 0.5 * ((xi - icc) + (xi - occ));
     const bool predicted = tstar == tstar && tstar >= tau(0) && tstar <= tau(ntau - 1);
-    const bool scan = SBR_AW_SCAN && S.scan && predicted;
+    const bool scan = S.scan && predicted;
     if (!S.pmc || aw_path || !(scan || S.bnb)) {
-#ifndef SBR_EQ_NOFALLBACK_TEST // timing A/B only (wrong results off the scan path)
         eval_range(0, ntau); // exhaustive (single-point path mode, or summaries unavailable)
-#endif
     } else {
         // Branch and bound over a 256/64/8 hierarchy of τ̄ ranges — the same maximum,
         // far fewer evaluations.  Every argument sequence is nondecreasing in i, so the
@@ -1072,17 +994,11 @@ __device__ __forceinline__ void solve_from_buffers(P T, P G, P H, const Summ& S,
             // (a heuristic — exactness comes from pass 2's bounds).  Otherwise descend the
             // bound hierarchy to the most promising 8-block.
             const int ic = predicted ? ssl_range(T, 0, (nle > 0 ? nle : 1) - 1, tstar < T[0] ? T[0] : tstar) : 0;
-#if SBR_AW_SCAN
             if (scan) {
                 aw_scan(T, G, n, ntau, nle, ETA, xi, icc, occ, G0, S.dd, ic < ntau ? ic : ntau - 1, mx, nblk_eval,
                         S.koff);
             } else
-#endif
-#ifndef SBR_EQ_NOFALLBACK_TEST
             {
-#else
-            if (0) {
-#endif
             int b8 = -1, w0 = 0, w1 = 0;
             if (predicted) {
                 const int c8 = (ic < ntau ? ic : ntau - 1) & ~7;
@@ -1174,9 +1090,6 @@ __device__ __forceinline__ double tsit5_dense(double th, double dt, double y0, d
 
 // hjb_equation! (value_function_solver.jl:86-95): dV = (h + δ)(1 − V) + max(u + rV − h, 0)
 // with h = HR(τ̄) (gridded linear, Throw()); brackets galloped from the step's own.
-#ifndef SBR_VALUE_PIN
-#define SBR_VALUE_PIN 0 // the value-function ODE's Tsit5 tableau: 0 literals, 2 the a_ij in VGPRs (A/B r05_y: 636 -> 633 ms, kept off; 1 spills)
-#endif
 template <class P>
 struct ValueRhs {
     TauView<P> tau;
@@ -1226,7 +1139,7 @@ struct ValueRhs {
         if (ntau >= 2 && t >= tlo && t <= thi) jb = ssl_gallop(tau, ntau, jb, t);
     }
     static constexpr bool kFsalExact = false;
-    static constexpr int kPinTableau = SBR_VALUE_PIN;
+    static constexpr int kPinTableau = 0;
 };
 
 // The value function saved on the HR grid (saveat) streamed into optimal_buffer
@@ -1398,7 +1311,7 @@ __device__ __forceinline__ void eq_column(const int b, const int j0, const int j
     double* hmin = hmax + nsum;
     double* pmc = hmin + nsum;
     double* smc = pmc + nsum8;
-    double* hpm = smc + nsum8; // SBR_SCAN_BS tables (launch_equilibrium sizes the slab for them)
+    double* hpm = smc + nsum8; // crossing-scan tables (launch_equilibrium sizes the slab for them)
     double* hpn = hpm + nsum;
     double* hsm = hpn + nsum;
     double* hsn = hsm + nsum;
@@ -1513,7 +1426,6 @@ __device__ __forceinline__ void eq_column(const int b, const int j0, const int j
                 smc[g] = (a0 != a0 || b0 != b0) ? NAN : (a0 < b0 ? a0 : b0);
             }
         }
-#if SBR_SCAN_BS
         // the crossing scans' prefix / suffix tables over the HR blocks (hmax has no NaN, hmin has
         // NaN as −∞): a wave each way, 64 blocks per shuffle scan; small blocks: one lane each way
         if (BLOCK >= 256 && (threadIdx.x >> 6) >= 2 && (threadIdx.x >> 6) <= 3) {
@@ -1556,13 +1468,12 @@ __device__ __forceinline__ void eq_column(const int b, const int j0, const int j
                 hsn[g] = b0;
             }
         }
-#endif
         __syncthreads();
         const double dd = (double)s_ndec * sbr_bitsd(s_maxdec); // ≥ the largest drawdown
         S = Summ{hmax, hmin, pmc, smc, s_nonmono == 0, s_thalf,
                  n >= 2 && !s_noscan && dd <= 1e-12 && sG[0] >= 0.0 && sG[n - 1] <= 2.0, dd,
-                 s_nonmono == 0 || s_noscan != 0, (SBR_AW_K1 && s_near1 == 0) ? 1 : 2,
-                 SBR_SCAN_BS ? hpm : nullptr, hpn, hsm, hsn, nbh_s};
+                 s_nonmono == 0 || s_noscan != 0, s_near1 == 0 ? 1 : 2,
+                 hpm, hpn, hsm, hsn, nbh_s};
     }
     // Points are handed out to waves 64 at a time from an LDS counter, so a
     // wave that drew cheap no-run points goes back for more instead of idling
@@ -1622,22 +1533,17 @@ __device__ unsigned int g_wghw[2 * kWgTimeMax];
 #endif
 
 template <int BLOCK, bool INTEREST, int MODE>
-__global__ __launch_bounds__(BLOCK, INTEREST ? 1 : SBR_EQ_MINW) void equilibrium_kernel(LearnBufs L, const double* __restrict__ eta,
+__global__ __launch_bounds__(BLOCK, INTEREST ? 1 : kEqMinW) void equilibrium_kernel(LearnBufs L, const double* __restrict__ eta,
                                                             const double* __restrict__ t_end,
                                                             const double* __restrict__ u, EqArgs a, InterestArgs ia,
                                                             ResultSoA out)
 {
     extern __shared__ double smem[];
-#if SBR_EQ_PRIO
-    __builtin_amdgcn_s_setprio(SBR_EQ_PRIO); // A/B: issue priority over co-resident learning waves
-#endif
-    int b = SBR_EQ_REVERSE ? (int)(gridDim.y - 1 - blockIdx.y) : (int)blockIdx.y;
-#if SBR_EQ_GROUP_INTERLEAVE
+    int b = (int)blockIdx.y;
     if (a.group > 1) { // grouped launch: the copies of a column back to back
         const int per = (int)gridDim.y / a.group;
         b = (b % a.group) * per + b / a.group;
     }
-#endif
     const int j0 = blockIdx.x * EQ_TILE;
     const int j1 = j0 + EQ_TILE < a.n_u ? j0 + EQ_TILE : a.n_u;
 #ifdef SBR_EQ_WGTIME
@@ -1669,11 +1575,7 @@ __device__ __forceinline__ int ready_wait(const int32_t* p, const int32_t* err, 
 {
     int v = 0;
     for (int k = 0; k < limit; k++) {
-#ifdef SBR_READY_RELAXED // A/B only (timing of the cache maintenance): no acquire
-        v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#else
         v = __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-#endif
         if (v) break;
         if ((k & 63) == 63 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
         __builtin_amdgcn_s_sleep(8);
@@ -1685,7 +1587,7 @@ __device__ __forceinline__ int ready_wait(const int32_t* p, const int32_t* err, 
 // starts (tickets follow the publication order, so resident workgroups wait for the columns
 // that come next), rather than persistent workgroups looping over items — a loop around the
 // equilibrium body lets the compiler hoist its invariants and spill the 80-VGPR budget.
-__global__ __launch_bounds__(SBR_EQ_WIDE, SBR_EQ_MINW) void eq_ready_kernel(LearnBufs L, const double* __restrict__ beta,
+__global__ __launch_bounds__(kEqWide, kEqMinW) void eq_ready_kernel(LearnBufs L, const double* __restrict__ beta,
                                                                             const double* __restrict__ eta,
                                                                             const double* __restrict__ t_end,
                                                                             const double* __restrict__ u, LearnArgs la,
@@ -1717,7 +1619,7 @@ __global__ __launch_bounds__(SBR_EQ_WIDE, SBR_EQ_MINW) void eq_ready_kernel(Lear
     if (tile == 0) {
         // (the LDS-chunked path: the register-resident one needs 5 × 16 doubles per thread,
         // which the equilibrium's 80-VGPR budget would spill)
-        hazard_column<SBR_EQ_WIDE, false>(col, beta[col], eta[col], la, L, smem, smem + (HZ_LDS + 1),
+        hazard_column<kEqWide, false>(col, beta[col], eta[col], la, L, smem, smem + (HZ_LDS + 1),
                                           smem + 2 * (HZ_LDS + 1), smem + 3 * HZ_LDS + 2);
         __syncthreads();
         if (threadIdx.x == 0 && ra.tiles > 1)
@@ -1725,7 +1627,7 @@ __global__ __launch_bounds__(SBR_EQ_WIDE, SBR_EQ_MINW) void eq_ready_kernel(Lear
     }
     const int j0 = tile * ra.tile_u;
     const int j1 = j0 + ra.tile_u < a.n_u ? j0 + ra.tile_u : a.n_u;
-    eq_column<SBR_EQ_WIDE, false>(col, j0, j1, L, eta, t_end, u, a, none, out, smem);
+    eq_column<kEqWide, false>(col, j0, j1, L, eta, t_end, u, a, none, out, smem);
 }
 
 // ============================================================================
@@ -1763,9 +1665,6 @@ __device__ __forceinline__ int wave_ssl(P t, int lo, int hi, double x)
     return lo + __popcll(__ballot(pr));
 }
 
-#ifndef SBR_COOP_SPEC
-#define SBR_COOP_SPEC 1 // point_wave's bisection six levels per round (speculative tree over the wave)
-#endif
 // lane k's double (k wave-uniform)
 __device__ __forceinline__ double co_rl(double x, int k)
 {
@@ -1853,7 +1752,6 @@ __device__ __forceinline__ void point_wave(P T, P G, P H, const int n, const int
     int jlo = wave_ssl(T, 0, n - 1, xmin);
     int jhi = wave_ssl(T, 0, n - 1, xmax);
     const int jtin = jlo;
-#if SBR_COOP_SPEC
     // Rounds of six bisection levels at once: lane ℓ < 63 evaluates node k = ℓ + 1 of the
     // depth-6 tree below the current state (heap order; child 2k follows err > 0, 2k + 1
     // err < 0), replaying its path's midpoint arithmetic exactly, then the wave walks the tree
@@ -1945,47 +1843,6 @@ __device__ __forceinline__ void point_wave(P T, P G, P H, const int n, const int
         if (stop) break;
         iter0 += 6;
     }
-#else
-    for (int iter = 1; iter <= max_iters; iter++) {
-        r.iters = iter;
-        const double dd = xmin - xmax;
-        if (collapsed(dd)) { s = SBR_NO_RUN_COLLAPSE; break; }
-        if (iter == max_iters - 1) { s = SBR_NO_RUN_MAXITER; break; }
-        const double xo = xnew;
-        const double ic = dmin(tin, xo), oc = dmin(tout, xo);
-        const int j = wave_ssl(T, jlo, jhi, xo);
-        const bool ok = co_in_range(oc, tlo, thi, trunc, flag);
-        const int joc = (oc == xo) ? j : (ok ? wave_ssl(T, 0, n - 1, oc) : 0);
-        const double Goc = ok ? lerp_at(T, G, n, joc, oc) : 0.0;
-        double Gic = 0.0;
-        int jic = 0;
-        if (co_in_range(ic, tlo, thi, trunc, flag)) {
-            jic = (ic == tin) ? jtin : (ic == xo ? j : wave_ssl(T, 0, n - 1, ic));
-            Gic = lerp_at(T, G, n, jic, ic);
-        }
-        if (j + 1 >= n) { flag |= trunc ? SBR_ENGINE_TRUNC : SBR_OOB; break; }
-        const double eps = T[j + 1] - T[j];
-        const double xoe = oc + eps, xie = ic + eps;
-        const bool oke = co_in_range(xoe, tlo, thi, trunc, flag);
-        const bool oki = co_in_range(xie, tlo, thi, trunc, flag);
-        if (flag) break;
-        const double AW = Goc - Gic;
-        const double err = AW - kappa;
-        if (fabs(err) <= tolerance) {
-            double Goce = 0.0, Gice = 0.0;
-            if (oke) Goce = lerp_at(T, G, n, wave_ssl(T, joc, n - 1, xoe), xoe);
-            if (oki) Gice = lerp_at(T, G, n, wave_ssl(T, jic, n - 1, xie), xie);
-            const double AWe = Goce - Gice;
-            if (AWe >= AW) { s = SBR_RUN; xi = xo; tolr = fabs(err); }
-            else s = SBR_FALSE_EQ;
-            break;
-        } else if (err > 0) {
-            xmax = xo; jhi = j; xnew = 0.5 * (xo + xmin);
-        } else {
-            xmin = xo; jlo = j; xnew = 0.5 * (xo + xmax);
-        }
-    }
-#endif
     } // default first iterate
     if (flag) { r.status = flag | lbits; return; }
     if (s != SBR_RUN) { r.status = s | lbits; return; }
@@ -2066,7 +1923,9 @@ __global__ __launch_bounds__(CO_BLOCK) void point_coop_kernel(LearnBufs L, const
     const double* T = fits ? (const double*)sT : (const double*)L.t;
     const double* G = fits ? (const double*)sG : (const double*)L.G;
     const double* H = fits ? (const double*)sH : (const double*)L.hr;
-    const double ETA = eta[0], T1 = t_end[0], uj = u[0];
+    // one workgroup per u value (a ξ_guess call over n_u values; paths only with one workgroup)
+    const int jb = blockIdx.x;
+    const double ETA = eta[0], T1 = t_end[0], uj = u[jb];
     const uint32_t lbits = lst & (SBR_ODE_MAXITERS | SBR_STIFF_SWITCH | SBR_ODE_FAILED | SBR_KNOT_OVERFLOW);
     const bool bad_col = (lst & (SBR_ARG_INVALID | SBR_OOB)) || n < 2;
     const bool trunc = !a.full_grid && n >= 2 && L.t[n - 1] < T1;
@@ -2125,46 +1984,64 @@ __global__ __launch_bounds__(CO_BLOCK) void point_coop_kernel(LearnBufs L, const
             aw = s_mx[0];
             for (int w = 1; w < CO_BLOCK / 64; w++) aw = (aw != aw || s_mx[w] != s_mx[w]) ? (double)NAN : (s_mx[w] > aw ? s_mx[w] : aw);
         }
-        out.xi[0] = s_r[0];
-        out.tau_in_unc[0] = s_r[1];
-        out.tau_out_unc[0] = s_r[2];
-        out.aw_max[0] = aw;
-        out.tol[0] = s_r[4];
-        out.status[0] = st;
-        if (out.iters) out.iters[0] = s_it;
+        out.xi[jb] = s_r[0];
+        out.tau_in_unc[jb] = s_r[1];
+        out.tau_out_unc[jb] = s_r[2];
+        out.aw_max[jb] = aw;
+        out.tol[jb] = s_r[4];
+        out.status[jb] = st;
+        if (out.iters) out.iters[jb] = s_it;
     }
 }
 
 hipError_t launch_point_coop(const LearnBufs& L, const double* eta, const double* t_end, const double* u,
-                             const EqArgs& a, const ResultSoA& out, hipStream_t s)
+                             const EqArgs& a, const ResultSoA& out, hipStream_t s, int n_points)
 {
+    if (n_points > 1 && (a.aw_path || a.aw_out_path || a.aw_in_path || a.path_scratch)) return hipErrorInvalidValue;
     const size_t lds = (size_t)3 * a.lds_cap * sizeof(double);
-    hipLaunchKernelGGL(point_coop_kernel, dim3(1), dim3(CO_BLOCK), lds, s, L, eta, t_end, u, a, out);
+    hipLaunchKernelGGL(point_coop_kernel, dim3(n_points), dim3(CO_BLOCK), lds, s, L, eta, t_end, u, a, out);
     return hipGetLastError();
 }
 
 // ============================================================================
 // launchers
 // ============================================================================
+#ifndef SBR_LEARN_WIDE_BLOCK
+#define SBR_LEARN_WIDE_BLOCK 64 // lanes per workgroup of a batch's wide learning launch
+#endif
+#ifndef SBR_LEARN_WIDE_LDS
+#define SBR_LEARN_WIDE_LDS 0 // LDS bytes reserved per such workgroup (caps the workgroups per CU)
+#endif
+hipError_t launch_learn_kernel(const double* beta, const double* eta, const double* t_end, const LearnArgs& a,
+                               const LearnBufs& L, hipStream_t s, int mode)
+{
+    if (mode == 2) {
+        constexpr int B = SBR_LEARN_WIDE_BLOCK;
+        hipLaunchKernelGGL(learn_logistic_kernel<B>, dim3((a.n_beta + B - 1) / B), dim3(B), SBR_LEARN_WIDE_LDS, s, beta,
+                           eta, t_end, a, L);
+    } else if (mode == 0) {
+        hipLaunchKernelGGL(learn_logistic_kernel<kLearnBlock>, dim3((a.n_beta + kLearnBlock - 1) / kLearnBlock),
+                           dim3(kLearnBlock), 0, s, beta, eta, t_end, a, L);
+    } else {
+        hipLaunchKernelGGL(learn_logistic_kernel<kLearnBlockLat>, dim3((a.n_beta + kLearnBlockLat - 1) / kLearnBlockLat),
+                           dim3(kLearnBlockLat), 0, s, beta, eta, t_end, a, L);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_hazard_norm(const LearnArgs& a, const LearnBufs& L, int n_cols, hipStream_t s)
+{
+    hipLaunchKernelGGL(hazard_norm_kernel, dim3(n_cols), dim3(HN_BLOCK), 0, s, a, L);
+    return hipGetLastError();
+}
+
 hipError_t launch_learn_logistic(const double* beta, const double* eta, const double* t_end, const LearnArgs& a,
                                  const LearnBufs& L, hipStream_t s)
 {
-    if (a.fuse_hazard && !a.ready_q) {
-        constexpr int per_block = (SBR_LEARN_BLOCK / 64) * SBR_LEARN_LANES;
-        hipLaunchKernelGGL(learn_logistic_kernel<SBR_LEARN_BLOCK>, dim3((a.n_beta + per_block - 1) / per_block),
-                           dim3(SBR_LEARN_BLOCK), 0, s, beta, eta, t_end, a, L);
-    } else {
-        constexpr int per_block = (SBR_LEARN_BLOCK_LAT / 64) * SBR_LEARN_LANES;
-        hipLaunchKernelGGL(learn_logistic_kernel<SBR_LEARN_BLOCK_LAT>, dim3((a.n_beta + per_block - 1) / per_block),
-                           dim3(SBR_LEARN_BLOCK_LAT), 0, s, beta, eta, t_end, a, L);
-    }
-    hipError_t e = hipGetLastError();
+    hipError_t e = launch_learn_kernel(beta, eta, t_end, a, L, s, (a.fuse_hazard && !a.ready_q) ? 0 : 1);
     if (e != hipSuccess) return e;
     if (a.ready_q) return hipSuccess; // readiness sweep: eq_ready_kernel runs each column's hazard
-    if (a.fuse_hazard) {
-        hipLaunchKernelGGL(hazard_norm_kernel, dim3(a.n_beta), dim3(HN_BLOCK), 0, s, a, L);
-        return hipGetLastError();
-    }
+    if (a.fuse_hazard) return launch_hazard_norm(a, L, a.n_beta, s);
     hipLaunchKernelGGL(hazard_kernel, dim3(a.n_beta), dim3(HZ_BLOCK), 0, s, beta,
                        eta, a, L);
     return hipGetLastError();
@@ -2194,7 +2071,7 @@ hipError_t launch_equilibrium(const LearnBufs& L, const double* eta, const doubl
         if (only_mode != 1) hipLaunchKernelGGL(k2, grid, dim3(bs), 0, s, L, eta, t_end, u, a, none, out);
     };
     if (w > 256)
-        go(equilibrium_kernel<SBR_EQ_WIDE, false, 1>, equilibrium_kernel<SBR_EQ_WIDE, false, 2>, SBR_EQ_WIDE);
+        go(equilibrium_kernel<kEqWide, false, 1>, equilibrium_kernel<kEqWide, false, 2>, kEqWide);
     else if (w > 64)
         go(equilibrium_kernel<256, false, 1>, equilibrium_kernel<256, false, 2>, 256);
     else
@@ -2210,7 +2087,7 @@ hipError_t launch_eq_ready(const LearnBufs& L, const double* beta, const double*
     const size_t hz = (size_t)(3 * HZ_LDS + 3) * sizeof(double); // hazard scratch shares the slab
     if (lds < hz) lds = hz;
     (void)n_blocks; // one workgroup per item
-    hipLaunchKernelGGL(eq_ready_kernel, dim3(ra.n_items), dim3(SBR_EQ_WIDE), lds, s, L, beta, eta, t_end, u, la, a, ra,
+    hipLaunchKernelGGL(eq_ready_kernel, dim3(ra.n_items), dim3(kEqWide), lds, s, L, beta, eta, t_end, u, la, a, ra,
                        out);
     return hipGetLastError();
 }

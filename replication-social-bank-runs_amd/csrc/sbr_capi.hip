@@ -24,37 +24,10 @@
 
 // Event flags. Timing events only time (no system-scope cache writeback/invalidate when they
 // complete); dependency events between this device's queues release to device scope.
-#ifndef SBR_TIMING_EVENT_FLAGS
-#define SBR_TIMING_EVENT_FLAGS hipEventDisableSystemFence
-#endif
-#ifndef SBR_SYNC_EVENT_FLAGS
-#define SBR_SYNC_EVENT_FLAGS (hipEventDisableTiming | hipEventReleaseToDevice)
-#endif
+constexpr unsigned kTimingEventFlags = hipEventDisableSystemFence;
+constexpr unsigned kSyncEventFlags = hipEventDisableTiming | hipEventReleaseToDevice;
 
-#ifndef SBR_LEARN_PRIO_HI
-#define SBR_LEARN_PRIO_HI 1 // learning streams at the greatest stream priority
-#endif
-#ifndef SBR_LEARN_SLOTS
-#define SBR_LEARN_SLOTS 4 // learning workspaces of the pipelined batch
-#endif
-#ifndef SBR_HET_LEARN_MASK
-#define SBR_HET_LEARN_MASK 0 // A/B: hetero batch learning confined to half the CUs
-#endif
-#ifndef SBR_LEARN_GROUP
-// grids per learning (and equilibrium) launch of the pipelined batch.  Round 4 measured 2 slower
-// (1.567 -> 1.631 ms per step, r04_j); with the column-interleaved grouped equilibrium launch and
-// two-wave learning workgroups it is faster: the equilibrium launch over 4,096 columns sheds half
-// the per-grid tails (1.35 -> 1.28 ms per grid), step 1.445-1.462 -> 1.411-1.437 ms at 50 steps and
-// 1.529-1.576 -> 1.483-1.524 ms at the driver's 20 (same-call A/Bs r05_uu, r05_vv, r05_ww; 3 and 4
-// grids were no better, 6 learning workspaces slower)
-#define SBR_LEARN_GROUP 2
-#endif
-#ifndef SBR_LEARN_FILL_COLS
-#define SBR_LEARN_FILL_COLS 2048 // narrower grids share a learning launch up to this many columns
-#endif
-#ifndef SBR_LEARN_STREAMS
-#define SBR_LEARN_STREAMS 3 // learning streams (with the context stream: within GPU_MAX_HW_QUEUES = 4)
-#endif
+
 
 struct sbr_ctx {
     int device = 0;
@@ -69,17 +42,16 @@ struct sbr_ctx {
     // concurrently with the equilibrium of the current one
     // (workspace slots and streams are separate counts: grid k learns into slot k mod
     // kLearnSlots on stream k mod kLearnStreams)
-    static constexpr int kLearnSlots = SBR_LEARN_SLOTS;
-    static constexpr int kLearnStreams = SBR_LEARN_STREAMS;
+    static constexpr int kLearnSlots = 3; // slot 0: single sweeps; slots 0, 1: batch groups
+    static constexpr int kLearnStreams = 3; // learning streams (with the context stream: within GPU_MAX_HW_QUEUES = 4)
     // the hetero batch pipeline alternates two of these slots' streams/events; single sweeps
     // run their column chunks on the streams with slot events 0..kLearnStreams-1
-    static_assert(kLearnStreams >= 2 && kLearnSlots >= kLearnStreams, "SBR_LEARN_SLOTS >= SBR_LEARN_STREAMS >= 2");
+    static_assert(kLearnStreams >= 2 && kLearnSlots >= kLearnStreams, "kLearnSlots >= kLearnStreams >= 2");
     size_t ws_beta[kLearnSlots] = {}, ws_cap[kLearnSlots] = {};
     sbr::LearnBufs LW[kLearnSlots]{};
     int last_slot = 0;
     int64_t last_off = 0; // column offset of the last grid inside its (grouped) learning slot
     hipStream_t lstream[kLearnStreams] = {};
-    hipStream_t hl_stream[2] = {}; // hetero batch learning on a CU subset (SBR_HET_LEARN_MASK)
     hipEvent_t ev_in = nullptr, ev_learned[kLearnSlots] = {}, ev_eq[kLearnSlots] = {};
     // fork/join fences between HIP's null stream and `stream`, and the end of the last call
     // (whatever stream it ran on) that every call waits for (CallFence)
@@ -154,7 +126,9 @@ struct sbr_ctx {
     bool timing = false;
     std::vector<hipEvent_t> ev_pool;
     std::vector<hipEvent_t> ev_grid; // per grid of the last baseline batch: results complete
+    std::vector<hipEvent_t> ev_hn;   // per equilibrium launch of a baseline batch: its hazards normalised
     int64_t n_grid = 0;
+    int64_t bt_budget = 0; // baseline batch learning workspaces, bytes (0: 40 % of free + held HBM)
     size_t ev_used = 0;
     struct TRec {
         int kind; // 0 learning (+ hazard), 1 equilibrium
@@ -264,12 +238,19 @@ void free_learn(sbr_ctx* c, int slot)
     c->ws_beta[slot] = c->ws_cap[slot] = 0;
 }
 
+// Row stride of a learning workspace for a knot capacity: the capacity rounded up to a 128-B line
+// plus one line.  A wave's 64 lanes each stream their own column's row; with a power-of-two
+// stride (65536 knots = 512 KiB) all 64 rows map to the same L2 set and channel, the partial
+// lines are evicted before they fill, and every 8-B knot store costs a memory write.
+size_t learn_ld(size_t cap) { return ((cap + 15) & ~(size_t)15) + 16; }
+
 int ensure_learn(sbr_ctx* c, size_t n_beta, size_t cap, int slot = 0, bool hri = false)
 {
     if (n_beta <= c->ws_beta[slot] && cap == c->ws_cap[slot] && (!hri || c->LW[slot].hrI)) return SBR_OK;
     free_learn(c, slot);
     sbr::LearnBufs& L = c->LW[slot];
-    const size_t slab = n_beta * cap * sizeof(double);
+    const size_t ld = learn_ld(cap);
+    const size_t slab = n_beta * ld * sizeof(double);
     HIP_TRY(c, hipMalloc(&L.t, slab), SBR_ENOMEM);
     HIP_TRY(c, hipMalloc(&L.G, slab), SBR_ENOMEM);
     HIP_TRY(c, hipMalloc(&L.hr, slab), SBR_ENOMEM);
@@ -281,7 +262,8 @@ int ensure_learn(sbr_ctx* c, size_t n_beta, size_t cap, int slot = 0, bool hri =
     HIP_TRY(c, hipMalloc(&L.status, n_beta * 4), SBR_ENOMEM);
     HIP_TRY(c, hipMalloc(&L.n_accept, n_beta * 4), SBR_ENOMEM);
     HIP_TRY(c, hipMalloc(&L.n_reject, n_beta * 4), SBR_ENOMEM);
-    L.cap = (int32_t)cap;
+    L.cap = (int32_t)ld;
+    L.lim = (int32_t)cap;
     c->ws_beta[slot] = n_beta;
     c->ws_cap[slot] = cap;
     return SBR_OK;
@@ -427,7 +409,7 @@ int ensure_res_pin(sbr_ctx* c, size_t bytes)
 // ξ_guess (solver.jl:413,441) is honoured by sbr_equilibrium_on_knots, which solves on the caller's
 // whole knot grid; the sweeps' truncated learning (DESIGN.md §Truncated learning) and the
 // extensions' own bisections start at the reference's defaults, so they refuse a guess
-bool guess_set(const sbr_opts* o) { return o && o->xi_guess == o->xi_guess; }
+bool guess_set(const sbr_opts* o) { return o && (o->flags & SBR_FLAG_XI_GUESS); }
 
 // EconomicParameters / LearningParameters scalar checks (model.jl:31-35, 71-76)
 bool scalars_valid(double x0, double p, double kappa, double lambda)
@@ -441,6 +423,9 @@ sbr_opts resolve(const sbr_opts* o)
     sbr_default_opts(&r);
     if (o) {
         r = *o;
+        // a zero field is the default (a zero-filled sbr_opts is the reference's defaults)
+        if (!(r.ode_reltol > 0.0)) r.ode_reltol = 2.220446049250313e-16;
+        if (!(r.ode_abstol > 0.0)) r.ode_abstol = 2.220446049250313e-16;
         if (r.knot_capacity <= 0) r.knot_capacity = kDefaultCap;
         if (r.ode_maxiters <= 0) r.ode_maxiters = SBR_DEFAULT_ODE_MAXITERS;
         // the device ODE loops count a solve's steps in int32 (sbr_ode.h OdeOut)
@@ -455,7 +440,7 @@ hipEvent_t next_event(sbr_ctx* c)
 {
     if (c->ev_used == c->ev_pool.size()) {
         hipEvent_t e;
-        if (hipEventCreateWithFlags(&e, SBR_TIMING_EVENT_FLAGS) != hipSuccess) return nullptr;
+        if (hipEventCreateWithFlags(&e, kTimingEventFlags) != hipSuccess) return nullptr;
         c->ev_pool.push_back(e);
     }
     return c->ev_pool[c->ev_used++];
@@ -504,13 +489,82 @@ int ensure_pipe_streams(sbr_ctx* c)
     int lo = 0, hi = 0;
     (void)hipDeviceGetStreamPriorityRange(&lo, &hi); // hi = greatest priority
     for (int k = 0; k < sbr_ctx::kLearnStreams; k++)
-        HIP_TRY(c, hipStreamCreateWithPriority(&c->lstream[k], hipStreamNonBlocking, SBR_LEARN_PRIO_HI ? hi : lo), SBR_EDEVICE);
+        HIP_TRY(c, hipStreamCreateWithPriority(&c->lstream[k], hipStreamNonBlocking, hi), SBR_EDEVICE);
     for (int k = 0; k < sbr_ctx::kLearnSlots; k++) {
-        HIP_TRY(c, hipEventCreateWithFlags(&c->ev_learned[k], SBR_SYNC_EVENT_FLAGS), SBR_EDEVICE);
-        HIP_TRY(c, hipEventCreateWithFlags(&c->ev_eq[k], SBR_SYNC_EVENT_FLAGS), SBR_EDEVICE);
+        HIP_TRY(c, hipEventCreateWithFlags(&c->ev_learned[k], kSyncEventFlags), SBR_EDEVICE);
+        HIP_TRY(c, hipEventCreateWithFlags(&c->ev_eq[k], kSyncEventFlags), SBR_EDEVICE);
     }
-    HIP_TRY(c, hipEventCreateWithFlags(&c->ev_in, SBR_SYNC_EVENT_FLAGS), SBR_EDEVICE);
+    HIP_TRY(c, hipEventCreateWithFlags(&c->ev_in, kSyncEventFlags), SBR_EDEVICE);
     return SBR_OK;
+}
+
+// Pipelined batch plan (sbr_sweep_baseline_batch_dev).  The learning kernel is latency-bound
+// (one serial ODE per lane, ≈32 waves per 2048-column grid) and a launch lasts as long as its
+// slowest column whatever its width; run beside the equilibrium kernel a learning wave holds
+// an equilibrium workgroup slot of its CU (169 VGPRs next to 6 × 80) and issues ahead of it.
+// So the batch learns as many grids as it can in ONE launch — up to SBR_BATCH_LEARN_WAVES waves,
+// at most one per SIMD — while the chip has nothing else to do, and then runs the equilibria
+// back to back with nothing beside them; a batch longer than that learns its next group into
+// the second workspace beside the first group's equilibria.
+#ifndef SBR_BATCH_LEARN_WAVES
+#define SBR_BATCH_LEARN_WAVES 768 // learning waves per batch learning launch (of 1,024 SIMDs)
+#endif
+#ifndef SBR_BATCH_EQ_COLS
+#define SBR_BATCH_EQ_COLS 4096 // columns per equilibrium launch of a batch (two full grids: one tail per two)
+#endif
+struct BatchPlan {
+    int64_t L = 1;  // grids per learning launch (and workspace slot)
+    int64_t E = 1;  // grids per equilibrium launch
+    int nslot = 1;  // workspace slots in rotation (1 when one group holds the batch, else 2)
+};
+
+// bytes of one learning column of a batch workspace: t, G, the HR numerators and the running
+// integrals (cap doubles each) and six counters
+size_t batch_col_bytes(size_t cap) { return learn_ld(cap) * 4 * sizeof(double) + 6 * sizeof(int32_t); }
+
+// Size the plan and its workspaces.  L is capped by the wave budget and by the memory budget
+// (c->bt_budget, default 40 % of the free plus the already held HBM); if an allocation fails
+// anyway the slots are released and L is halved, down to one grid (then SBR_ENOMEM).
+int batch_alloc(sbr_ctx* c, int64_t n_batch, int64_t n_beta, size_t cap, BatchPlan& P)
+{
+    const int64_t wpg = (n_beta + 63) / 64; // learning waves per grid
+    int64_t L = SBR_BATCH_LEARN_WAVES / wpg;
+    if (L < 1) L = 1;
+    if (L > n_batch) L = n_batch;
+    size_t freeb = 0, total = 0;
+    (void)hipMemGetInfo(&freeb, &total);
+    size_t held = 0;
+    for (int k = 0; k < 2; k++) held += c->ws_beta[k] * batch_col_bytes(c->ws_cap[k]);
+    const double budget = c->bt_budget > 0 ? (double)c->bt_budget : 0.4 * (double)(freeb + held);
+    const double per_grid = (double)n_beta * (double)batch_col_bytes(cap);
+    for (;;) {
+        int nslot = n_batch > L ? 2 : 1;
+        while (L > 1 && (double)(L * nslot) * per_grid > budget) {
+            L = L > 2 ? (L + 1) / 2 : 1;
+            nslot = n_batch > L ? 2 : 1;
+        }
+        // balanced groups: ⌈n_batch / L⌉ groups of (nearly) equal size
+        const int64_t ng = (n_batch + L - 1) / L;
+        L = (n_batch + ng - 1) / ng;
+        nslot = ng > 1 ? 2 : 1;
+        // launch columns are int32 in the kernels' arguments
+        if (L * n_beta > INT32_MAX) return fail(c, SBR_EARG, "batch: n_beta too large for one learning launch");
+        int rc = SBR_OK;
+        for (int k = 0; k < nslot && rc == SBR_OK; k++) rc = ensure_learn(c, (size_t)(L * n_beta), cap, k, true);
+        if (rc == SBR_OK) {
+            P.L = L;
+            P.nslot = nslot;
+            int64_t E = (SBR_BATCH_EQ_COLS + n_beta - 1) / n_beta;
+            P.E = E < 1 ? 1 : (E > L ? L : E);
+            return SBR_OK;
+        }
+        for (int k = 0; k < sbr_ctx::kLearnSlots; k++) free_learn(c, k);
+        if (L == 1) return rc;
+        // the failed hipMalloc left hipErrorOutOfMemory as the thread's last error: clear it, or
+        // the next launch check (hipGetLastError) would report it against a good launch
+        (void)hipGetLastError();
+        L = (L + 1) / 2;
+    }
 }
 
 // the learning buffers / results of columns [c0, ...) of a sweep (row views)
@@ -518,7 +572,7 @@ sbr::LearnBufs learn_rows(const sbr::LearnBufs& L, size_t c0)
 {
     const size_t k = c0 * (size_t)L.cap;
     return {L.t + k,        L.G + k,        L.hr + k,     L.hrI + k,         L.n_knots + c0, L.n_tau + c0,
-            L.n_le + c0,    L.status + c0,  L.n_accept + c0, L.n_reject + c0, L.cap};
+            L.n_le + c0,    L.status + c0,  L.n_accept + c0, L.n_reject + c0, L.cap, L.lim};
 }
 sbr::ResultSoA result_rows(const sbr::ResultSoA& r, size_t off)
 {
@@ -536,21 +590,10 @@ sbr::ResultSoA result_rows(const sbr::ResultSoA& r, size_t off)
 constexpr int kSweepChunks = sbr_ctx::kLearnStreams;
 // pipelined batch: hazard_rate streamed by the learning kernel (no separate hazard launch
 // competing with the equilibrium kernel for CU slots); single sweeps keep the hazard kernel
-#ifndef SBR_FUSE_HAZARD
-#define SBR_FUSE_HAZARD 1
-#endif
-#ifndef SBR_SWEEP_FRONT
-#define SBR_SWEEP_FRONT 32 // 0: halving chunks only (A/B: 4.44 -> 4.25 ms per config-3 sweep)
-#endif
-#ifndef SBR_READY_LEARN_CUS
-#define SBR_READY_LEARN_CUS 64 // CUs reserved for the learning waves (8 / 16 / 32 / 64: 13.3 / 9.2 / 3.5 / 3.0 ms of learning)
-#endif
-#ifndef SBR_READY_TILE_U
-#define SBR_READY_TILE_U 4096 // u values per equilibrium workgroup (768: three tiles of a config-3 column, 6.7 vs 5.5 ms)
-#endif
-#ifndef SBR_READY_SPIN
-#define SBR_READY_SPIN (1 << 24) // polls (≈ 0.5 µs each) before a waiting workgroup gives up: a bug guard
-#endif
+constexpr int kSweepFront = 32;       // the front chunk of a single sweep: 1/32 of the waves (halving only: 4.44 vs 4.25 ms)
+constexpr int kReadyLearnCus = 64;    // CUs reserved for the learning waves (8 / 16 / 32 / 64: 13.3 / 9.2 / 3.5 / 3.0 ms of learning)
+constexpr int kReadyTileU = 4096;     // u values per equilibrium workgroup (768: three tiles of a config-3 column, 6.7 vs 5.5 ms)
+constexpr int kReadySpin = 1 << 24;   // polls (≈ 0.5 µs each) before a waiting workgroup gives up: a bug guard
 
 // the streams with disjoint CU masks and the queue of a readiness sweep
 int ensure_ready(sbr_ctx* c, size_t n_beta)
@@ -559,15 +602,15 @@ int ensure_ready(sbr_ctx* c, size_t n_beta)
         c->rs_state = -1;
         int ncu = 0;
         (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device);
-        if (ncu >= 4 * SBR_READY_LEARN_CUS) {
+        if (ncu >= 4 * kReadyLearnCus) {
             std::vector<uint32_t> ml((size_t)(ncu + 31) / 32, 0u), me(ml.size(), 0u);
-            for (int i = 0; i < ncu; i++) (i < SBR_READY_LEARN_CUS ? ml : me)[(size_t)i / 32] |= 1u << (i % 32);
+            for (int i = 0; i < ncu; i++) (i < kReadyLearnCus ? ml : me)[(size_t)i / 32] |= 1u << (i % 32);
             if (hipExtStreamCreateWithCUMask(&c->rs_learn, (uint32_t)ml.size(), ml.data()) == hipSuccess &&
                 hipExtStreamCreateWithCUMask(&c->rs_eq, (uint32_t)me.size(), me.data()) == hipSuccess &&
-                hipEventCreateWithFlags(&c->ev_rin, SBR_SYNC_EVENT_FLAGS) == hipSuccess &&
-                hipEventCreateWithFlags(&c->ev_rq, SBR_SYNC_EVENT_FLAGS) == hipSuccess &&
-                hipEventCreateWithFlags(&c->ev_rl, SBR_SYNC_EVENT_FLAGS) == hipSuccess &&
-                hipEventCreateWithFlags(&c->ev_re, SBR_SYNC_EVENT_FLAGS) == hipSuccess)
+                hipEventCreateWithFlags(&c->ev_rin, kSyncEventFlags) == hipSuccess &&
+                hipEventCreateWithFlags(&c->ev_rq, kSyncEventFlags) == hipSuccess &&
+                hipEventCreateWithFlags(&c->ev_rl, kSyncEventFlags) == hipSuccess &&
+                hipEventCreateWithFlags(&c->ev_re, kSyncEventFlags) == hipSuccess)
                 c->rs_state = 1;
         }
     }
@@ -595,7 +638,7 @@ int run_baseline_ready(sbr_ctx* c, hipStream_t s, const double* beta, const doub
                        const double* u, int64_t n_beta, int64_t n_u, double kappa, const sbr_opts& o,
                        sbr::LearnArgs la, const sbr::ResultSoA& out)
 {
-    const int tiles = (int)((n_u + SBR_READY_TILE_U - 1) / SBR_READY_TILE_U);
+    const int tiles = (int)((n_u + kReadyTileU - 1) / kReadyTileU);
     int32_t* q = c->rq;
     HIP_TRY(c, hipEventRecord(c->ev_rin, s), SBR_EDEVICE);
     HIP_TRY(c, hipStreamWaitEvent(c->rs_learn, c->ev_rin, 0), SBR_EDEVICE);
@@ -610,7 +653,7 @@ int run_baseline_ready(sbr_ctx* c, hipStream_t s, const double* beta, const doub
     tend(c, c->rs_learn, 0, t0);
     sbr::EqArgs ea{kappa, (int32_t)n_u, o.bisect_max_iters, c->lds_cap_b, nullptr,
                    (o.flags & SBR_FLAG_EXHAUSTIVE) ? 1 : 0, (o.flags >> 8) & 7};
-    sbr::ReadyArgs ra{q, q + 4, q + 4 + n_beta, (int32_t)(n_beta * tiles), tiles, SBR_READY_TILE_U, SBR_READY_SPIN};
+    sbr::ReadyArgs ra{q, q + 4, q + 4 + n_beta, (int32_t)(n_beta * tiles), tiles, kReadyTileU, kReadySpin};
     hipEvent_t t1 = tstart(c, c->rs_eq);
     HIP_TRY(c, sbr::launch_eq_ready(c->LW[0], beta, eta, t_end, u, la, ea, ra, out, 0, c->rs_eq), SBR_EDEVICE);
     tend(c, c->rs_eq, 1, t1);
@@ -657,11 +700,9 @@ int run_baseline(sbr_ctx* c, hipStream_t s, const double* beta, const double* et
         const int64_t wk = waves >> (kSweepChunks - k); // waves before chunk k
         lo[k] = std::min<int64_t>(n_beta, std::max<int64_t>(wk * 64, (int64_t)k * 64));
     }
-#if SBR_SWEEP_FRONT
-    // A/B: the front chunk is 1/SBR_SWEEP_FRONT of the waves (the Fig 5 grid's outliers sit in
+    // the front chunk is 1/kSweepFront of the waves (the Fig 5 grid's outliers sit in
     // its first wave: 1.25x the steps of the next slowest)
-    lo[1] = std::min<int64_t>(lo[2] - 64, std::max<int64_t>(64, (waves / SBR_SWEEP_FRONT) * 64));
-#endif
+    lo[1] = std::min<int64_t>(lo[2] - 64, std::max<int64_t>(64, (waves / kSweepFront) * 64));
     HIP_TRY(c, hipEventRecord(c->ev_in, s), SBR_EDEVICE);
     hipEvent_t t0 = tstart(c, s);
     c->ck_start = c->timing ? t0 : nullptr;
@@ -798,9 +839,9 @@ int sbr_init(int device, sbr_ctx** out)
     sbr_ctx* c = new sbr_ctx();
     c->device = device;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_fork, SBR_SYNC_EVENT_FLAGS) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_join, SBR_SYNC_EVENT_FLAGS) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_last, SBR_SYNC_EVENT_FLAGS) != hipSuccess) {
+        hipEventCreateWithFlags(&c->ev_fork, kSyncEventFlags) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_join, kSyncEventFlags) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_last, kSyncEventFlags) != hipSuccess) {
         delete c;
         return SBR_EDEVICE;
     }
@@ -813,9 +854,6 @@ int sbr_init(int device, sbr_ctx** out)
     c->lds_cap = (int)(((long)(smem - 1024) * 64) / (8 * (3 * 64 + 6 + 16)));
     // baseline equilibrium kernel: t, G (2·64) + summaries per 64 knots, two workgroups per CU
     c->lds_cap_b = (int)(((long)(smem / 2 - 1024) * 64) / (8 * (2 * 64 + 6 + 16)));
-#ifdef SBR_EQ_LDS_KNOTS
-    c->lds_cap_b = std::min(c->lds_cap_b, (int)SBR_EQ_LDS_KNOTS);
-#endif
     *out = c;
     return SBR_OK;
 }
@@ -877,8 +915,6 @@ int sbr_free(sbr_ctx* c)
     }
     for (int k = 0; k < sbr_ctx::kLearnStreams; k++)
         if (c->lstream[k]) (void)hipStreamDestroy(c->lstream[k]);
-    for (hipStream_t hs : c->hl_stream)
-        if (hs) { (void)hipStreamSynchronize(hs); (void)hipStreamDestroy(hs); }
     for (hipStream_t rs : {c->rs_learn, c->rs_eq})
         if (rs) { (void)hipStreamSynchronize(rs); (void)hipStreamDestroy(rs); }
     for (hipEvent_t e : {c->ev_rin, c->ev_rq, c->ev_rl, c->ev_re})
@@ -893,6 +929,7 @@ int sbr_free(sbr_ctx* c)
     if (c->hk_pin) (void)hipHostFree(c->hk_pin);
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->ev_grid) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->ev_hn) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(c->stream);
     delete c;
     return SBR_OK;
@@ -926,10 +963,8 @@ int sbr_sweep_baseline_dev(sbr_ctx* c, void* stream, const double* beta, const d
 // hetero equilibrium LDS slab (doubles): knot times + per-group HR summaries of one column,
 // capped so that SBR_HET_MINW = 2 workgroups share a CU's 160 KB (2 x (79.5 KB + the kernel's
 // static LDS)); config 4 with Rosenbrock23 after the switch: n <= 7.9k knots
-#ifndef SBR_HET_LDS
-#define SBR_HET_LDS 10176
-#endif
-static int het_lds(const sbr_ctx* c) { return c->lds_cap * 3 < SBR_HET_LDS ? c->lds_cap * 3 : SBR_HET_LDS; }
+constexpr int kHetLds = 10176;
+static int het_lds(const sbr_ctx* c) { return c->lds_cap * 3 < kHetLds ? c->lds_cap * 3 : kHetLds; }
 
 
 int sbr_sweep_baseline_batch_dev(sbr_ctx* c, void* stream, int64_t n_batch, const double* beta, const double* eta,
@@ -945,89 +980,100 @@ int sbr_sweep_baseline_batch_dev(sbr_ctx* c, void* stream, int64_t n_batch, cons
     if (!scalars_valid(x0, p, kappa, lambda)) return fail(c, SBR_EARG, "ArgumentError: x0/p/kappa/lambda");
     if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
     sbr_opts o = resolve(opts);
-    const int nslot = sbr_ctx::kLearnSlots;
-    // SBR_LEARN_GROUP grids share one learning launch (their β columns are adjacent in `beta`):
-    // the learning stage is latency-bound on its slowest column, so a launch over twice the
-    // columns takes about as long as one over a single grid, and the three learning streams
-    // keep twice as many grids in flight
-    // A launch is as long as its slowest column whatever its width, so grids narrower than
-    // SBR_LEARN_FILL_COLS columns (a strong-scaled shard: 2048/N columns) are grouped up to that
-    // width — 32 waves per launch, the full grid's count: a 256-column shard learns 8 grids per
-    // launch instead of 4 waves per launch in series on each stream.
-    int64_t GR = (SBR_LEARN_FILL_COLS + n_beta - 1) / n_beta;
-    if (GR < SBR_LEARN_GROUP) GR = SBR_LEARN_GROUP;
-    if (GR > n_batch) GR = n_batch;
-    const int64_t n_group = (n_batch + GR - 1) / GR;
-    for (int k = 0; k < nslot && k < n_group; k++) {
-        int rc = ensure_learn(c, (size_t)(n_beta * GR), (size_t)o.knot_capacity, k, SBR_FUSE_HAZARD != 0);
-        if (rc) return rc;
-    }
-    {
-        int rc = ensure_pipe_streams(c);
-        if (rc) return rc;
-    }
+    BatchPlan P;
+    int rc = batch_alloc(c, n_batch, n_beta, (size_t)o.knot_capacity, P);
+    if (rc) return rc;
+    rc = ensure_pipe_streams(c);
+    if (rc) return rc;
+    const int64_t n_group = (n_batch + P.L - 1) / P.L;
+    const int64_t n_eq_per_group = (P.L + P.E - 1) / P.E;
     while ((int64_t)c->ev_grid.size() < n_batch) {
         hipEvent_t e = nullptr;
         HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming), SBR_EDEVICE);
         c->ev_grid.push_back(e);
     }
+    while ((int64_t)c->ev_hn.size() < n_group * n_eq_per_group) {
+        hipEvent_t e = nullptr;
+        HIP_TRY(c, hipEventCreateWithFlags(&e, kSyncEventFlags), SBR_EDEVICE);
+        c->ev_hn.push_back(e);
+    }
     c->n_grid = 0;
     return fenced(c, stream, true, [&](hipStream_t s) -> int {
         const size_t np = (size_t)n_beta * (size_t)n_u;
-        sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, p, lambda, o.ode_maxiters, (int32_t)n_beta, 1,
-                          SBR_FUSE_HAZARD};
-        // inputs are ready once prior work on the caller's stream is
+        // learning on lstream[0] (greatest priority), the hazard normalisations on lstream[1],
+        // the equilibrium launches on the caller's stream
+        hipStream_t ls = c->lstream[0], hs = c->lstream[1], es = s;
         HIP_TRY(c, hipEventRecord(c->ev_in, s), SBR_EDEVICE);
-        for (int k = 0; k < sbr_ctx::kLearnStreams; k++) HIP_TRY(c, hipStreamWaitEvent(c->lstream[k], c->ev_in, 0), SBR_EDEVICE);
+        HIP_TRY(c, hipStreamWaitEvent(ls, c->ev_in, 0), SBR_EDEVICE);
+        int64_t k_hn = 0;
         for (int64_t m = 0; m < n_group; m++) {
-            const int slot = (int)(m % nslot);
-            const int64_t g0 = m * GR, gn = (n_batch - g0) < GR ? (n_batch - g0) : GR;
-            hipStream_t es = s; // one equilibrium stream (two alternating: 15% slower, r01_ab27)
-#ifdef SBR_AB_PIPE_SERIAL // A/B only: learning on the equilibrium stream (no overlap)
-            hipStream_t ls = s;
-#else
-            hipStream_t ls = c->lstream[m % sbr_ctx::kLearnStreams];
-#endif
-            // the slot's previous readers (equilibria of group m - nslot) must be done
-            if (m >= nslot) HIP_TRY(c, hipStreamWaitEvent(ls, c->ev_eq[slot], 0), SBR_EDEVICE);
+            const int slot = (int)(m % P.nslot);
+            const int64_t g0 = m * P.L, gn = (n_batch - g0) < P.L ? (n_batch - g0) : P.L;
+            const sbr::LearnBufs& W = c->LW[slot];
+            // the slot's previous readers (the equilibria of group m - nslot) must be done
+            if (m >= P.nslot) HIP_TRY(c, hipStreamWaitEvent(ls, c->ev_eq[slot], 0), SBR_EDEVICE);
+            // every grid of the group in ONE learning launch (the hazard numerators and running
+            // integrals streamed with the knots): the launch lasts as long as its slowest column
+            // whatever its width, so up to SBR_BATCH_LEARN_WAVES waves learn together.  The
+            // first group has the chip to itself (one wave per workgroup: lone-wave latency);
+            // later groups run beside the equilibrium launches (two waves per workgroup)
+            sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, p, lambda, o.ode_maxiters, (int32_t)(gn * n_beta), 1, 1};
             hipEvent_t t0 = tstart(c, ls);
-            // the first group's learning is the pipeline fill (nothing to overlap it with): the
-            // two-kernel hazard is shorter there; later groups stream it (off the critical path)
-            sbr::LearnArgs lk = la;
-            lk.n_beta = (int32_t)(gn * n_beta);
-            if (m == 0) lk.fuse_hazard = 0;
-            HIP_TRY(c, sbr::launch_learn_logistic(beta + g0 * n_beta, eta + g0 * n_beta, t_end + g0 * n_beta, lk,
-                                                  c->LW[slot], ls), SBR_EDEVICE);
+            HIP_TRY(c, sbr::launch_learn_kernel(beta + g0 * n_beta, eta + g0 * n_beta, t_end + g0 * n_beta, la, W, ls,
+                                                m == 0 ? 2 : 0), SBR_EDEVICE);
             tend(c, ls, 0, t0);
             HIP_TRY(c, hipEventRecord(c->ev_learned[slot], ls), SBR_EDEVICE);
-            HIP_TRY(c, hipStreamWaitEvent(es, c->ev_learned[slot], 0), SBR_EDEVICE);
-            // the group's gn grids in ONE equilibrium launch over their gn·n_beta columns: the slot
-            // holds them adjacently, and eta / t_end / every out field are [n_batch × n_beta(× n_u)]
-            // contiguous, so column i·n_beta + j of the launch is grid g0+i's column j at exactly
-            // its own offsets.  A narrow grid (a strong-scaled shard: 256 columns × 3 u-tiles =
-            // 768 workgroups) would otherwise be one launch of its slowest workgroups (≈0.5 ms,
-            // DESIGN §4) with the CUs idle behind them; grouped, the launch is as wide as a full grid.
-            {
-                const sbr::LearnBufs& W = c->LW[slot];
-                sbr::ResultSoA r{out->xi ? out->xi + g0 * np : nullptr,
-                                 out->tau_in_unc ? out->tau_in_unc + g0 * np : nullptr,
-                                 out->tau_out_unc ? out->tau_out_unc + g0 * np : nullptr,
-                                 out->aw_max ? out->aw_max + g0 * np : nullptr,
-                                 out->tol ? out->tol + g0 * np : nullptr,
-                                 out->status ? out->status + g0 * np : nullptr,
-                                 out->iters ? out->iters + g0 * np : nullptr};
-                int rc = launch_eq(c, es, W, eta + g0 * n_beta, t_end + g0 * n_beta, u, gn * n_beta, n_u, kappa, o, r,
-                                   nullptr, (int)gn);
+            HIP_TRY(c, hipStreamWaitEvent(hs, c->ev_learned[slot], 0), SBR_EDEVICE);
+            // the group's equilibria in launches of E grids (balanced), each after the hazard
+            // normalisation of its own columns: the normalisations (HBM streams) run ahead on hs,
+            // overlapped with the previous equilibrium launch; only the first one is exposed
+            const int64_t ne = (gn + P.E - 1) / P.E, Eg = (gn + ne - 1) / ne;
+            for (int64_t e0 = 0; e0 < gn; e0 += Eg) {
+                const int64_t en = (gn - e0) < Eg ? (gn - e0) : Eg;
+                const sbr::LearnBufs We = learn_rows(W, (size_t)(e0 * n_beta));
+                HIP_TRY(c, sbr::launch_hazard_norm(la, We, (int)(en * n_beta), hs), SBR_EDEVICE);
+                hipEvent_t eh = c->ev_hn[(size_t)k_hn++];
+                HIP_TRY(c, hipEventRecord(eh, hs), SBR_EDEVICE);
+                HIP_TRY(c, hipStreamWaitEvent(es, eh, 0), SBR_EDEVICE);
+                // column i·n_beta + j of the launch is grid g0+e0+i's column j: eta / t_end and
+                // every out field are [n_batch × n_beta (× n_u)] contiguous
+                const int64_t gg = g0 + e0;
+                sbr::ResultSoA r{out->xi + gg * np, out->tau_in_unc + gg * np, out->tau_out_unc + gg * np,
+                                 out->aw_max + gg * np, out->tol + gg * np, out->status + gg * np,
+                                 out->iters ? out->iters + gg * np : nullptr};
+                rc = launch_eq(c, es, We, eta + gg * n_beta, t_end + gg * n_beta, u, en * n_beta, n_u, kappa, o, r,
+                               nullptr, (int)en);
                 if (rc) return rc;
-                for (int64_t i = 0; i < gn; i++) HIP_TRY(c, hipEventRecord(c->ev_grid[g0 + i], es), SBR_EDEVICE);
-                c->n_grid = g0 + gn;
-                c->last_off = (gn - 1) * n_beta;
+                for (int64_t i = 0; i < en; i++) HIP_TRY(c, hipEventRecord(c->ev_grid[gg + i], es), SBR_EDEVICE);
+                c->n_grid = gg + en;
             }
             HIP_TRY(c, hipEventRecord(c->ev_eq[slot], es), SBR_EDEVICE);
             c->last_slot = slot;
+            c->last_off = (gn - 1) * n_beta;
         }
         return SBR_OK;
     });
+}
+
+int sbr_batch_reserve(sbr_ctx* c, int64_t n_batch, int64_t n_beta, const sbr_opts* opts)
+{
+    SBR_SINGLE_DEVICE(c);
+    if (!c) return SBR_EARG;
+    if (n_batch <= 0 || n_beta <= 0 || n_beta > (1 << 30)) return fail(c, SBR_EARG, "grid size");
+    if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
+    const sbr_opts o = resolve(opts);
+    // the workspaces are replaced only once nothing enqueued earlier can still read them
+    if (c->have_last) HIP_TRY(c, hipEventSynchronize(c->ev_last), SBR_EDEVICE);
+    BatchPlan P;
+    return batch_alloc(c, n_batch, n_beta, (size_t)o.knot_capacity, P);
+}
+
+int sbr_set_batch_workspace(sbr_ctx* c, int64_t bytes)
+{
+    SBR_SINGLE_DEVICE(c);
+    if (!c || bytes < 0) return SBR_EARG;
+    c->bt_budget = bytes;
+    return SBR_OK;
 }
 
 int sbr_batch_wait(sbr_ctx* c, void* stream, int64_t k)
@@ -1269,11 +1315,11 @@ int sbr_learn_baseline(sbr_ctx* c, const double* beta, const double* eta, const 
         HIP_TRY(c, hipMemcpyAsync(dtend, t_end, n_beta * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
         sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, 0.5, 1.0, o.ode_maxiters, (int32_t)n_beta, stop_after_eta, 0};
         HIP_TRY(c, sbr::launch_learn_logistic(dbeta, deta, dtend, la, c->LW[0], s), SBR_EDEVICE);
-        const size_t w = (size_t)o.knot_capacity;
+        const size_t w = (size_t)o.knot_capacity, ld = (size_t)c->LW[0].cap;
         if (t_out)
-            HIP_TRY(c, hipMemcpy2DAsync(t_out, cap * 8, c->LW[0].t, w * 8, w * 8, n_beta, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+            HIP_TRY(c, hipMemcpy2DAsync(t_out, cap * 8, c->LW[0].t, ld * 8, w * 8, n_beta, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
         if (G_out)
-            HIP_TRY(c, hipMemcpy2DAsync(G_out, cap * 8, c->LW[0].G, w * 8, w * 8, n_beta, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+            HIP_TRY(c, hipMemcpy2DAsync(G_out, cap * 8, c->LW[0].G, ld * 8, w * 8, n_beta, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
         if (n_knots) HIP_TRY(c, hipMemcpyAsync(n_knots, c->LW[0].n_knots, n_beta * 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
         if (status) HIP_TRY(c, hipMemcpyAsync(status, c->LW[0].status, n_beta * 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
         HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
@@ -1597,7 +1643,7 @@ int on_knots(sbr_ctx* c, const double* t, const double* G, const double* pdf, in
     double* dsc = (double*)(D + K.sc);
     double* dtg = (double*)(D + K.tg);
     const sbr::LearnBufs L{dtg, dtg + n, (double*)(D + K.hr), nullptr, dcnt, dcnt + 1, dcnt + 2,
-                           (uint32_t*)(dcnt + 3), dcnt + 4, dcnt + 5, (int32_t)c->kn_cap_k};
+                           (uint32_t*)(dcnt + 3), dcnt + 4, dcnt + 5, (int32_t)c->kn_cap_k, (int32_t)c->kn_cap_k};
     double* du = (double*)(D + K.u); // [t_end, u_0 .. u_{n_u-1}]
     double* dres = (double*)(D + K.res);
     const size_t res_bytes = (size_t)n_u * 48 + (want_aw ? (size_t)ntau * 24 : 0);
@@ -1635,7 +1681,7 @@ int on_knots(sbr_ctx* c, const double* t, const double* G, const double* pdf, in
             sbr::EqArgs ea{kappa, 1, o.bisect_max_iters, c->lds_cap, want_aw ? zp : nullptr,
                            (o.flags & SBR_FLAG_EXHAUSTIVE) ? 1 : 0, (o.flags >> 8) & 7,
                            want_aw ? zp + ntau : nullptr, want_aw ? zp + 2 * ntau : nullptr, 1, dres};
-            ea.xi_guess = o.xi_guess;
+            if (o.flags & SBR_FLAG_XI_GUESS) ea.xi_guess = o.xi_guess;
             HIP_TRY(c, sbr::launch_point_coop(L, dsc + 1, zd, zd + 1, ea, r, s), SBR_EDEVICE);
         } else {
             double* hu = (double*)(H + K.u);
@@ -1644,17 +1690,14 @@ int on_knots(sbr_ctx* c, const double* t, const double* G, const double* pdf, in
             HIP_TRY(c, hipMemcpyAsync(du, hu, (nu + 1) * 8, hipMemcpyHostToDevice, s), SBR_EDEVICE);
             const sbr::ResultSoA r{dres, dres + nu, dres + 2 * nu, dres + 3 * nu, dres + 4 * nu,
                                    (uint32_t*)(dres + 5 * nu), (int32_t*)(dres + 5 * nu) + nu};
-            if (o.xi_guess == o.xi_guess) {
-                // ξ_guess: the single-point kernel once per u (its plain first-iterate bisection; the
-                // sweep kernel carries no guess path, it would cost the sweeps registers)
+            if ((o.flags & SBR_FLAG_XI_GUESS) && o.xi_guess == o.xi_guess) {
+                // ξ_guess: the single-point kernel, one workgroup per u, in one launch (its plain
+                // first-iterate bisection; the sweep kernel carries no guess path, it would cost the
+                // sweeps registers)
                 sbr::EqArgs ea{kappa, 1, o.bisect_max_iters, c->lds_cap, nullptr,
                                (o.flags & SBR_FLAG_EXHAUSTIVE) ? 1 : 0, (o.flags >> 8) & 7, nullptr, nullptr, 1};
                 ea.xi_guess = o.xi_guess;
-                for (size_t j = 0; j < nu; j++) {
-                    const sbr::ResultSoA rj{r.xi + j, r.tau_in_unc + j, r.tau_out_unc + j, r.aw_max + j, r.tol + j,
-                                            r.status + j, r.iters + j};
-                    HIP_TRY(c, sbr::launch_point_coop(L, dsc + 1, du, du + 1 + j, ea, rj, s), SBR_EDEVICE);
-                }
+                HIP_TRY(c, sbr::launch_point_coop(L, dsc + 1, du, du + 1, ea, r, s, (int)nu), SBR_EDEVICE);
             } else {
                 sbr::EqArgs ea{kappa, (int32_t)n_u, o.bisect_max_iters, c->lds_cap_b, nullptr,
                                (o.flags & SBR_FLAG_EXHAUSTIVE) ? 1 : 0, (o.flags >> 8) & 7, nullptr, nullptr, 1};
@@ -1793,8 +1836,6 @@ int sbr_timing_read(sbr_ctx* c, void* stream, double* learn_ms, double* eq_ms, i
     double a = 0.0, b = 0.0;
     int32_t n = 0;
     for (hipStream_t ls : c->lstream)
-        if (ls) HIP_TRY(c, hipStreamSynchronize(ls), SBR_EDEVICE);
-    for (hipStream_t ls : c->hl_stream)
         if (ls) HIP_TRY(c, hipStreamSynchronize(ls), SBR_EDEVICE);
     for (hipStream_t rs : {c->rs_learn, c->rs_eq})
         if (rs) HIP_TRY(c, hipStreamSynchronize(rs), SBR_EDEVICE);
@@ -1947,23 +1988,6 @@ int sbr_sweep_hetero_batch_dev(sbr_ctx* c, void* stream, int64_t n_batch, int32_
     int rc = ensure_hetero(c, (size_t)n_col, cap, (size_t)K);
     if (!rc && n_batch > 1) rc = ensure_hetero_bufs(c, c->H2, c->hs2_col, c->hs2_cap, c->hs2_K, (size_t)n_col, cap, (size_t)K);
     if (!rc) rc = ensure_pipe_streams(c);
-#if SBR_HET_LEARN_MASK
-    // the batch's learning waves (one per column, latency-bound, 101 VGPRs) packed two per SIMD
-    // on half of every XCD's CUs, so that the other half keeps two 256-VGPR equilibrium waves
-    // per SIMD instead of one beside a learning wave
-    if (!rc && !c->hl_stream[0]) {
-        int ncu = 0;
-        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device);
-        std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
-        for (int i = 0; i < ncu; i++)
-            if (((i >> 3) & 1) == 0) mask[(size_t)i >> 5] |= 1u << (i & 31);
-        for (int k = 0; k < 2 && !rc; k++)
-            if (hipExtStreamCreateWithCUMask(&c->hl_stream[k], (uint32_t)mask.size(), mask.data()) != hipSuccess) {
-                c->hl_stream[k] = nullptr;
-                rc = fail(c, SBR_EDEVICE, "hipExtStreamCreateWithCUMask");
-            }
-    }
-#endif
     if (rc) return rc;
     return fenced(c, stream, true, [&](hipStream_t s) -> int {
         sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, p, lambda, o.ode_maxiters, (int32_t)n_col, 0, 0};
@@ -1971,11 +1995,10 @@ int sbr_sweep_hetero_batch_dev(sbr_ctx* c, void* stream, int64_t n_batch, int32_
                              (o.flags & SBR_FLAG_EXHAUSTIVE) ? 1 : 0, (o.flags >> 8) & 7, nullptr};
         const size_t np = (size_t)n_col * (size_t)n_u;
         HIP_TRY(c, hipEventRecord(c->ev_in, s), SBR_EDEVICE);
-        for (int k = 0; k < 2; k++)
-            HIP_TRY(c, hipStreamWaitEvent(c->hl_stream[k] ? c->hl_stream[k] : c->lstream[k], c->ev_in, 0), SBR_EDEVICE);
+        for (int k = 0; k < 2; k++) HIP_TRY(c, hipStreamWaitEvent(c->lstream[k], c->ev_in, 0), SBR_EDEVICE);
         for (int64_t k = 0; k < n_batch; k++) {
             const int slot = (int)(k & 1);
-            hipStream_t ls = c->hl_stream[slot] ? c->hl_stream[slot] : c->lstream[slot];
+            hipStream_t ls = c->lstream[slot];
             const sbr::HeteroBufs& H = slot ? c->H2 : c->H;
             const double* bk = betas + k * n_col * K;
             const double* ek = eta + k * n_col;
@@ -2153,17 +2176,9 @@ namespace {
 constexpr int kSocialDefaultCap = 98304;  // ≈1.4× the typical longest iterate on config 5 (≈70k knots)
 constexpr int kSocialMaxCap = 1 << 22;    // overflow retries grow 4× per pass up to this
 constexpr int64_t kPoolSlots = 256;       // promotion pool slots (points that outgrow the capacity)
-#ifndef SBR_SOCIAL_INNER
-#define SBR_SOCIAL_INNER 16
-#endif
-constexpr int kSocialInner = SBR_SOCIAL_INNER; // fixed-point iterates per launch (compaction in between)
-#ifndef SBR_SOCIAL_BULK
-#define SBR_SOCIAL_BULK 2 // launches of SBR_SOCIAL_INNER iterates before the shorter ones
-#endif
-#ifndef SBR_SOCIAL_INNER2
-#define SBR_SOCIAL_INNER2 8 // iterates per launch after the bulk launches
-#endif
-constexpr int kSocialBulk = SBR_SOCIAL_BULK, kSocialInner2 = SBR_SOCIAL_INNER2;
+constexpr int kSocialInner = 16; // fixed-point iterates per launch (compaction in between)
+constexpr int kSocialBulk = 2;   // launches of kSocialInner iterates before the shorter ones
+constexpr int kSocialInner2 = 8; // iterates per launch after the bulk launches
 
 int social_checks(sbr_ctx* c, const double* beta, const double* eta, const double* u, int64_t n_beta, int64_t n_u,
                   double x0, double p, double kappa, double lambda, const double* cmp, int32_t n_cmp, double tol,
@@ -2318,9 +2333,14 @@ int run_social_pass(sbr_ctx* c, hipStream_t s, const double* beta, const double*
                 fprintf(stderr, "sbr_social_trace drain=%d pool_live_before=%d\n", d, c->so_count_host[3]);
         }
         tend(c, s, 1, t0);
-        // promotions of this chunk (diagnostics), and the sync that frees the argument staging
-        HIP_TRY(c, hipMemcpyAsync(c->so_count_host + 2, c->so_count + 2, 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
+        // promotions of this chunk (diagnostics), the pool's live count, and the sync that frees
+        // the argument staging
+        HIP_TRY(c, hipMemcpyAsync(c->so_count_host + 2, c->so_count + 2, 2 * 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
         HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
+        // the drain is bounded by max_iter; a pool point still live past it would leave its results
+        // unwritten — never returned as if solved
+        if (nslots > 0 && c->so_count_host[3] != 0)
+            return fail(c, SBR_EDEVICE, "social sweep: promoted points still live after the pool drain");
         if (nslots > 0) {
             const int64_t used = c->so_count_host[2];
             c->so_promoted += used < nslots ? used : nslots;

@@ -1,7 +1,8 @@
 // sbr_hetero.hip — gfx950 kernels for the heterogeneity extension (K coupled
 // learning groups), src/extensions/heterogeneity/.
 //
-//   learn_hetero_kernel<K>        one lane per parameter column: FP64 Tsit5 on
+//   learn_hetero_wave_kernel<K>   one wave per parameter column (lane k = group k):
+//                                 FP64 AutoTsit5(Rosenbrock23()) on
 //                                 dG_k/dt = (1−G_k) β_k Σ_j dist_j G_j with the
 //                                 RMS error norm over K components
 //                                 (heterogeneity_learning.jl:49-94), pdfs
@@ -78,339 +79,12 @@ __device__ __forceinline__ double opnorm_inf(const double* J)
     return nrm;
 }
 
-// K×K LU in registers (oracle lu_factor / lu_solve): generic_lufact! with RowMaximum
-// pivoting, then getrs (row interchanges, unit-lower and upper column sweeps in fma,
-// division by the pivots).  Row interchanges are selects so every index is static.
-template <int K>
-struct RegLU {
-    double A[K * K];
-    int piv[K];
-    __device__ __forceinline__ void factor()
-    {
-#pragma unroll
-        for (int k = 0; k < K; k++) {
-            int kp = k;
-            double amax = fabs(A[k * K + k]), pv = A[k * K + k];
-#pragma unroll
-            for (int i = k + 1; i < K; i++) {
-                const double ai = fabs(A[i * K + k]);
-                if (ai > amax) { kp = i; amax = ai; pv = A[i * K + k]; }
-            }
-            piv[k] = kp;
-            if (pv != 0.0) {
-#pragma unroll
-                for (int i = k + 1; i < K; i++) {
-                    const bool sw = kp == i;
-#pragma unroll
-                    for (int j = 0; j < K; j++) {
-                        const double a = A[k * K + j], c = A[i * K + j];
-                        A[k * K + j] = sw ? c : a;
-                        A[i * K + j] = sw ? a : c;
-                    }
-                }
-                const double inv = 1.0 / A[k * K + k];
-#pragma unroll
-                for (int i = k + 1; i < K; i++) A[i * K + k] = A[i * K + k] * inv;
-            }
-#pragma unroll
-            for (int j = k + 1; j < K; j++)
-#pragma unroll
-                for (int i = k + 1; i < K; i++) A[i * K + j] = A[i * K + j] - A[i * K + k] * A[k * K + j];
-        }
-    }
-    __device__ __forceinline__ void solve(double* b) const
-    {
-#pragma unroll
-        for (int k = 0; k < K; k++)
-#pragma unroll
-            for (int i = k + 1; i < K; i++) {
-                const bool sw = piv[k] == i;
-                const double x = b[k], y = b[i];
-                b[k] = sw ? y : x;
-                b[i] = sw ? x : y;
-            }
-#pragma unroll
-        for (int j = 0; j < K; j++) {
-            const double a = -b[j];
-#pragma unroll
-            for (int i = j + 1; i < K; i++) b[i] = fma(a, A[i * K + j], b[i]);
-        }
-#pragma unroll
-        for (int j = K - 1; j >= 0; j--) {
-            b[j] = b[j] / A[j * K + j];
-            const double a = -b[j];
-#pragma unroll
-            for (int i = 0; i < j; i++) b[i] = fma(a, A[i * K + j], b[i]);
-        }
-    }
-};
-
-template <int K>
-__global__ __launch_bounds__(64) void learn_hetero_kernel(const double* __restrict__ betas,
-                                                          const double* __restrict__ dist,
-                                                          const double* __restrict__ eta,
-                                                          const double* __restrict__ t_end, LearnArgs a, HeteroBufs L)
-{
-    const int c = blockIdx.x * 64 + threadIdx.x;
-    if (c >= a.n_beta) return;
-    double b[K];
-#pragma unroll
-    for (int k = 0; k < K; k++) b[k] = betas[(size_t)c * K + k];
-    const double ETA = eta[c], T1 = t_end[c], T0 = 0.0;
-    const size_t cap = (size_t)L.cap;
-    double* __restrict__ T = L.t + (size_t)c * cap;
-    double* __restrict__ Gv = L.G + (size_t)c * cap * K;
-    double* __restrict__ H = L.hr + (size_t)c * K * cap;
-    double* __restrict__ HI = L.hrI + (size_t)c * K * cap;
-    uint32_t st = 0;
-    bool argok = ETA > 0.0 && T1 > T0;
-#pragma unroll
-    for (int k = 0; k < K; k++) argok = argok && (b[k] > 0.0);
-    if (!argok) {
-        L.status[c] = SBR_ARG_INVALID;
-        L.n_knots[c] = 0; L.n_tau[c] = 0; L.n_le[c] = 0; L.n_accept[c] = 0; L.n_reject[c] = 0;
-        return;
-    }
-    const double x0 = a.x0, rtol = a.rtol, atol = a.atol, p = a.p, lam = a.lam;
-    const double dtmax = T1 - T0;
-    const double dtmin = sbr_jl_eps(dmax(fabs(T0), fabs(T1)));
-    double x[K], k1[K], k2[K], k3[K], k4[K], k5[K], k6[K], k7[K], tmp[K], tmp6[K], u[K], buf[K];
-
-    // ---- ode_determine_initdt ----
-    double sk[K];
-#pragma unroll
-    for (int k = 0; k < K; k++) { x[k] = x0; sk[k] = fma(fabs(x0), rtol, atol); buf[k] = x0 / sk[k]; }
-    const double d0 = rms<K>(buf);
-    rhs<K>(dist, b, x, k1);
-#pragma unroll
-    for (int k = 0; k < K; k++) buf[k] = k1[k] / sk[k];
-    const double d1 = rms<K>(buf);
-    double dt0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : (d0 / d1) / 100.0;
-    dt0 = dmin(dt0, dtmax);
-    double dt;
-    if (dt0 < 10.0 * DBL_EPS) {
-        dt = dmax(1e-6, dtmin);
-    } else {
-#pragma unroll
-        for (int k = 0; k < K; k++) u[k] = fma(dt0, k1[k], x0);
-        rhs<K>(dist, b, u, k7);
-        bool same = true;
-#pragma unroll
-        for (int k = 0; k < K; k++) same = same && (k1[k] == k7[k]);
-        if (same) {
-            dt = dmax(dtmin, 100.0 * dt0);
-        } else {
-#pragma unroll
-            for (int k = 0; k < K; k++) buf[k] = (k7[k] - k1[k]) / sk[k];
-            const double d2 = rms<K>(buf) / dt0;
-            const double md = dmax(d1, d2);
-            const double dt1 = (md <= 1e-15) ? dmax(1e-6, dt0 * 1e-3) : sbr_pow_pos(0.01 / md, 1.0 / SBR_INITDT_DEN);
-            dt = dmax(dtmin, dmin(dmin(100.0 * dt0, dt1), dtmax));
-        }
-    }
-
-    // ---- knot sink: (t, G[K]) + streamed hazard terms per group ----
-    int n = 0, m = 0;
-    double tprev = 0.0, Ik[K], eprev[K], gprev[K];
-    bool past = false, done = false;
-#pragma unroll
-    for (int k = 0; k < K; k++) { Ik[k] = 0.0; eprev[k] = 0.0; gprev[k] = 0.0; }
-    auto push = [&](double t, const double* xs) {
-        if (n >= L.cap) { st |= SBR_KNOT_OVERFLOW; done = true; return; }
-        T[n] = t;
-#pragma unroll
-        for (int k = 0; k < K; k++) Gv[(size_t)n * K + k] = xs[k];
-        if (!past) {
-            const double w = omega<K>(dist, xs);
-            double g[K];
-#pragma unroll
-            for (int k = 0; k < K; k++) g[k] = ((1.0 - xs[k]) * b[k]) * w;
-            if (t <= ETA) {
-                const double E = sbr_exp(lam * t);
-#pragma unroll
-                for (int k = 0; k < K; k++) {
-                    const double e = E * g[k];
-                    Ik[k] = (m == 0) ? 0.0 : Ik[k] + (0.5 * (eprev[k] + e)) * (t - tprev);
-                    H[(size_t)k * cap + m] = (p * E) * g[k];
-                    HI[(size_t)k * cap + m] = Ik[k];
-                    eprev[k] = e;
-                    gprev[k] = g[k];
-                }
-                m++;
-                tprev = t;
-            } else {
-                past = true; // η always appended (explicit grid): pdf(η) on bracket [n-1, n]
-                const double d = (ETA - tprev) / (t - tprev);
-                const double E = sbr_exp(lam * ETA);
-#pragma unroll
-                for (int k = 0; k < K; k++) {
-                    const double pe = gprev[k] * (1.0 - d) + g[k] * d;
-                    const double e = E * pe;
-                    Ik[k] = Ik[k] + (0.5 * (eprev[k] + e)) * (ETA - tprev);
-                    H[(size_t)k * cap + m] = (p * E) * pe;
-                    HI[(size_t)k * cap + m] = Ik[k];
-                }
-                m++;
-            }
-        }
-        n++;
-    };
-
-    const double snap = 100.0 * sbr_jl_eps(T1);
-    double t = T0;
-    double eig = 1.0; // integrator.eigen_est at init
-    PIControl pc;
-    AutoSwitch as;
-    int naccept = 0, nreject = 0;
-    push(t, x);
-    int64_t iter = 0;
-    while (t < T1 && !done) {
-        if (++iter > a.maxiters) { st |= SBR_ODE_MAXITERS; break; }
-        if (as.choose(eig, dt)) rhs<K>(dist, b, x, k1); // initialize!: fsalfirst = f(uprev, t)
-        dt = dmin(dtmax, dt);
-        dt = dmax(dt, dtmin);
-        dt = dmin(dt, T1 - t);
-        if (dt <= dtmin && t + dt < T1) { st |= SBR_ODE_FAILED; break; } // DtLessThanMin
-        double EEst;
-        if (as.stiff) {
-            // ---- Rosenbrock23 (perform_step!, Rosenbrock23Cache, @muladd); k7 <- fsallast ----
-            const double dtg = dt * ROS23_D;
-            const double invdtg = 1.0 / dtg, neginvdtg = -(1.0 / dtg);
-            const double dto2 = dt / 2.0, dto6 = dt / 6.0;
-            RegLU<K> W;
-            jac<K>(dist, b, x, W.A);
-            eig = opnorm_inf<K>(W.A);
-#pragma unroll
-            for (int k = 0; k < K; k++) W.A[k * K + k] = fma(-1.0, invdtg, W.A[k * K + k]);
-            W.factor();
-            double* s1 = k2; // Tsit5's stage arrays are free in a stiff step
-            double* s2 = k3;
-            double* f1 = k4;
-            double* r = k5;
-#pragma unroll
-            for (int k = 0; k < K; k++) r[k] = k1[k] + dtg * 0.0; // fsalfirst + dt·d·∂f/∂t
-            W.solve(r);
-#pragma unroll
-            for (int k = 0; k < K; k++) { s1[k] = r[k] * neginvdtg; tmp[k] = fma(dto2, s1[k], x[k]); }
-            rhs<K>(dist, b, tmp, f1);
-#pragma unroll
-            for (int k = 0; k < K; k++) r[k] = f1[k] - s1[k];
-            W.solve(r);
-#pragma unroll
-            for (int k = 0; k < K; k++) { s2[k] = fma(r[k], neginvdtg, s1[k]); u[k] = fma(dt, s2[k], x[k]); }
-            rhs<K>(dist, b, u, k7);
-#pragma unroll
-            for (int k = 0; k < K; k++)
-                r[k] = fma(dt, 0.0, fma(-2.0, s1[k] - k1[k], fma(-ROS23_C32, s2[k] - f1[k], k7[k])));
-            W.solve(r);
-#pragma unroll
-            for (int k = 0; k < K; k++) {
-                const double s3 = r[k] * neginvdtg;
-                const double ut = dto6 * (fma(-2.0, s2[k], s1[k]) + s3);
-                buf[k] = ut / fma(dmax(fabs(x[k]), fabs(u[k])), rtol, atol);
-            }
-            EEst = rms<K>(buf);
-        } else {
-            const double a21 = dt * A21;
-#pragma unroll
-            for (int k = 0; k < K; k++) tmp[k] = fma(a21, k1[k], x[k]);
-            rhs<K>(dist, b, tmp, k2);
-#pragma unroll
-            for (int k = 0; k < K; k++) tmp[k] = fma(dt, fma(A31, k1[k], A32 * k2[k]), x[k]);
-            rhs<K>(dist, b, tmp, k3);
-#pragma unroll
-            for (int k = 0; k < K; k++) tmp[k] = fma(dt, fma(A41, k1[k], fma(A42, k2[k], A43 * k3[k])), x[k]);
-            rhs<K>(dist, b, tmp, k4);
-#pragma unroll
-            for (int k = 0; k < K; k++)
-                tmp[k] = fma(dt, fma(A51, k1[k], fma(A52, k2[k], fma(A53, k3[k], A54 * k4[k]))), x[k]);
-            rhs<K>(dist, b, tmp, k5);
-#pragma unroll
-            for (int k = 0; k < K; k++)
-                tmp6[k] = fma(dt, fma(A61, k1[k], fma(A62, k2[k], fma(A63, k3[k], fma(A64, k4[k], A65 * k5[k])))), x[k]);
-            rhs<K>(dist, b, tmp6, k6);
-#pragma unroll
-            for (int k = 0; k < K; k++)
-                u[k] = fma(dt, fma(A71, k1[k], fma(A72, k2[k], fma(A73, k3[k], fma(A74, k4[k], fma(A75, k5[k], A76 * k6[k]))))),
-                           x[k]);
-            rhs<K>(dist, b, u, k7);
-            double e = 0.0;
-            bool e_nan = false;
-#pragma unroll
-            for (int k = 0; k < K; k++) {
-                const double rr = fabs((k7[k] - k6[k]) / (u[k] - tmp6[k]));
-                if (rr != rr) e_nan = true;
-                else if (rr > e) e = rr;
-            }
-            eig = e_nan ? (double)NAN : e;
-#pragma unroll
-            for (int k = 0; k < K; k++) {
-                const double ut = dt * fma(BT1, k1[k], fma(BT2, k2[k], fma(BT3, k3[k], fma(BT4, k4[k],
-                                           fma(BT5, k5[k], fma(BT6, k6[k], BT7 * k7[k]))))));
-                buf[k] = ut / fma(dmax(fabs(x[k]), fabs(u[k])), rtol, atol);
-            }
-            EEst = rms<K>(buf);
-        }
-        if (EEst != EEst) { st |= SBR_ODE_FAILED; break; } // NaN trial state (ReturnCode.Unstable)
-        bool acc;
-        const double dtn = pc.next_dt(EEst, dt, dtmax, dtmin, acc);
-        if (acc) {
-            naccept++;
-            double tn = t + dt;
-            if (fabs(tn - T1) < snap) tn = T1;
-            t = tn;
-#pragma unroll
-            for (int k = 0; k < K; k++) { x[k] = u[k]; k1[k] = k7[k]; }
-            dt = dtn;
-            push(t, x);
-        } else {
-            nreject++;
-            dt = dtn;
-        }
-        if (!(dt > 0.0) || !isfinite(dt)) { st |= SBR_ODE_FAILED; break; }
-    }
-    if (as.nswitch > 0) st |= SBR_STIFF_SWITCH;
-    int n_le = m;
-    if (past) {
-        n_le = m - 1;
-    } else if (!(st & SBR_KNOT_OVERFLOW)) {
-        // no knot beyond η: pdf(η) exists only if the last knot is η itself
-        if (n >= 2 && tprev == ETA) {
-            const double E = sbr_exp(lam * ETA);
-#pragma unroll
-            for (int k = 0; k < K; k++) {
-                // bracket clamps to [n-2, n-1] with δ = 1: gprev*(1-1) ... = g_{n-1}
-                const double pe = 0.0 + gprev[k] * 1.0;
-                H[(size_t)k * cap + m] = (p * E) * pe;
-                HI[(size_t)k * cap + m] = Ik[k];
-            }
-            m++;
-        } else {
-            st |= SBR_OOB;
-        }
-    }
-    if (m > 0 && !(st & SBR_OOB)) {
-        const double omp = 1.0 - p;
-#pragma unroll
-        for (int k = 0; k < K; k++) {
-            const double Ieta = HI[(size_t)k * cap + m - 1];
-            for (int i = 0; i < m; i++)
-                H[(size_t)k * cap + i] = H[(size_t)k * cap + i] / ((p * HI[(size_t)k * cap + i]) + (omp * Ieta));
-        }
-    }
-    L.n_knots[c] = n;
-    L.n_tau[c] = m;
-    L.n_le[c] = n_le;
-    L.status[c] = st;
-    L.n_accept[c] = naccept;
-    L.n_reject[c] = nreject;
-}
-
 // ---------------------------------------------------------------------------
 // learn_hetero_wave_kernel<K>: one wave per column, lane k = group k
 // ---------------------------------------------------------------------------
-// The same AutoTsit5(Rosenbrock23()) solve as learn_hetero_kernel, bit for bit, laid out
-// for the lone wave's serial chain instead of 64 columns per wave:
+// The oracle's AutoTsit5(Rosenbrock23()) solve (sbro_learn_hetero), bit for bit, laid out for the
+// lone wave's serial chain (one lane per column, 64 columns per wave, ran both the Tsit5 and the
+// Rosenbrock23 branch whenever the columns disagreed: 85 -> 28–32 ms per config-4 grid):
 //  * lane k holds component k of every stage vector and row k of W; the couplings (ω, the
 //    RMS error norm, the eigen estimates, the LU's pivot column and pivot row, the
 //    substitutions) read the other lanes' values with v_readlane into SGPRs and fold them
@@ -420,74 +94,17 @@ __global__ __launch_bounds__(64) void learn_hetero_kernel(const double* __restri
 //    wave both branches ran whenever the columns disagreed);
 //  * a row interchange is a uniform branch taken only when the pivot leaves the diagonal.
 // Lanes >= K shadow component K-1's arithmetic and never store or get read.
-#ifndef SBR_HET_LEARN_WAVE
-#define SBR_HET_LEARN_WAVE 1 // 0: learn_hetero_kernel (one lane per column, A/B)
-#endif
-#ifndef SBR_HET_LEARN_ROWS
-#define SBR_HET_LEARN_ROWS 1 // columns per learning wave: 1 = one per wave; 4 = learn_hetero_wave4_kernel (16-lane rows, bitwise but slower: 42.4 -> 45.2 ms, profiles/experiments/r04_s_*)
-#endif
-#ifndef SBR_HET_LEARN_PIN
-#define SBR_HET_LEARN_PIN 0 // learn_hetero_wave_kernel holds the Tsit5 tableau in VGPRs (A/B r05_x: 103 -> 157 VGPRs, step 42.7 -> 46.6 ms)
-#endif
-#ifndef SBR_HET_DIVRCP
-#define SBR_HET_DIVRCP 0 // LU back substitutions by refined pivot reciprocals (A/B)
-#endif
+// (Four columns per wave, one 16-lane row each with DPP row broadcasts, was bit-identical and
+// slower: a wave runs until its slowest column and executes both branches while its rows
+// disagree, 42.4 -> 45.2 ms per config-4 step, profiles/experiments/r04_s_*.)
 __device__ __forceinline__ double wave_bcast(double v, int l)
 {
-#if SBR_HET_BCAST_SHFL // A/B: through the LDS crossbar into VGPRs instead of SGPRs
-    return __shfl(v, l, 64);
-#endif
     const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
     const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
     return __hiloint2double(hi, lo);
 }
 
-// Row broadcast for the 4-columns-per-wave layout (learn_hetero_wave4_kernel): every lane of
-// each 16-lane row receives lane j of its row (DPP row_newbcast:j, a VALU move: no SGPR round
-// trip).  j is a compile-time constant after unrolling; the switch folds to one case.
-template <int J>
-__device__ __forceinline__ int row_bcast_i(int v)
-{
-    return __builtin_amdgcn_mov_dpp(v, 0x150 + J, 0xf, 0xf, false); // no `old` operand to materialise
-}
-__device__ __forceinline__ int row_bcast_int(int v, int j)
-{
-    switch (j & 15) {
-    case 0: return row_bcast_i<0>(v);
-    case 1: return row_bcast_i<1>(v);
-    case 2: return row_bcast_i<2>(v);
-    case 3: return row_bcast_i<3>(v);
-    case 4: return row_bcast_i<4>(v);
-    case 5: return row_bcast_i<5>(v);
-    case 6: return row_bcast_i<6>(v);
-    case 7: return row_bcast_i<7>(v);
-    case 8: return row_bcast_i<8>(v);
-    case 9: return row_bcast_i<9>(v);
-    case 10: return row_bcast_i<10>(v);
-    case 11: return row_bcast_i<11>(v);
-    case 12: return row_bcast_i<12>(v);
-    case 13: return row_bcast_i<13>(v);
-    case 14: return row_bcast_i<14>(v);
-    default: return row_bcast_i<15>(v);
-    }
-}
-__device__ __forceinline__ double row_bcast(double v, int j)
-{
-    if (!__builtin_constant_p(j)) // a row-uniform runtime index (the LU's pivot row): LDS crossbar
-        return __shfl(v, (int)(threadIdx.x & 48u) | (j & 15), 64);
-    const int lo = row_bcast_int(__double2loint(v), j);
-    const int hi = row_bcast_int(__double2hiint(v), j);
-    return __hiloint2double(hi, lo);
-}
-// ROWS = 1: one column per wave (lane = component); ROWS = 4: one column per 16-lane row
-template <int ROWS>
-__device__ __forceinline__ double bcast(double v, int j)
-{
-    if constexpr (ROWS == 1) return wave_bcast(v, j);
-    else return row_bcast(v, j);
-}
-
-template <int K, int ROWS = 1>
+template <int K>
 struct WaveRow {
     const int lane; // row / component index of this lane (lanes >= K: K - 1's shadow)
     const int kk;
@@ -501,26 +118,27 @@ struct WaveRow {
     __device__ __forceinline__ double omega(double I) const
     {
         const double pr = dk * I;
-        double w = bcast<ROWS>(pr, 0);
+        double w = wave_bcast(pr, 0);
 #pragma unroll
-        for (int j = 1; j < K; j++) w = w + bcast<ROWS>(pr, j);
+        for (int j = 1; j < K; j++) w = w + wave_bcast(pr, j);
         return w;
     }
     __device__ __forceinline__ double rhs(double I) const { return ((1.0 - I) * bk) * omega(I); }
     // sqrt(Σ v_k² / K), the sum from 0.0 in component order
     __device__ __forceinline__ double rms(double v) const
     {
-        if (K == 1) return bcast<ROWS>(fabs(v), 0);
+        if (K == 1) return wave_bcast(fabs(v), 0);
         const double sq = v * v;
         double s = 0.0;
 #pragma unroll
-        for (int i = 0; i < K; i++) s = s + bcast<ROWS>(sq, i);
+        for (int i = 0; i < K; i++) s = s + wave_bcast(sq, i);
         return sqrt(s / (double)K);
     }
 };
 
-// Row-distributed K×K LU (RegLU's operation sequence): lane i holds row i of A.
-template <int K, int ROWS = 1>
+// Row-distributed K×K LU (generic_lufact! / getrs, the oracle's lu_factor / lu_solve operation
+// sequence): lane i holds row i of A.
+template <int K>
 struct WaveLU {
     double A[K];
     int piv[K]; // wave-uniform
@@ -528,12 +146,12 @@ struct WaveLU {
     {
 #pragma unroll
         for (int k = 0; k < K; k++) {
-            double pv = bcast<ROWS>(A[k], k);
+            double pv = wave_bcast(A[k], k);
             double amax = fabs(pv);
             int kp = k;
 #pragma unroll
             for (int i = k + 1; i < K; i++) {
-                const double ai = bcast<ROWS>(A[k], i);
+                const double ai = wave_bcast(A[k], i);
                 if (fabs(ai) > amax) { kp = i; amax = fabs(ai); pv = ai; }
             }
             piv[k] = kp;
@@ -541,7 +159,7 @@ struct WaveLU {
                 if (kp != k) {
 #pragma unroll
                     for (int j = 0; j < K; j++) {
-                        const double vk = bcast<ROWS>(A[j], k), vp = bcast<ROWS>(A[j], kp);
+                        const double vk = wave_bcast(A[j], k), vp = wave_bcast(A[j], kp);
                         A[j] = lane == k ? vp : (lane == kp ? vk : A[j]);
                     }
                 }
@@ -551,32 +169,12 @@ struct WaveLU {
             }
 #pragma unroll
             for (int j = k + 1; j < K; j++) {
-                const double akj = bcast<ROWS>(A[j], k);
+                const double akj = wave_bcast(A[j], k);
                 const double v = A[j] - A[k] * akj;
                 A[j] = lane > k ? v : A[j];
             }
         }
-#if SBR_HET_DIVRCP
-        // this lane's pivot U_ll and its refined reciprocal, for the back substitutions
-        double dg = A[0];
-#pragma unroll
-        for (int j = 1; j < K; j++) dg = j == lane ? A[j] : dg;
-        rdiag = rcp_refined(dg);
-        okd = in_div_range(dg) ? 1 : 0;
-#endif
     }
-#if SBR_HET_DIVRCP
-    double rdiag;
-    int okd;
-    // |x| in [2^-400, 2^400]: with both operands there the division sequence needs no scaling
-    // and its intermediates neither overflow nor underflow, so div_rcp (the compiler's IEEE
-    // sequence without its identity scale / fixup steps) is the correctly rounded quotient
-    static __device__ __forceinline__ bool in_div_range(double x)
-    {
-        const double ax = fabs(x);
-        return ax >= 0x1p-400 && ax <= 0x1p400;
-    }
-#endif
     // b: this lane's component of the right-hand side, overwritten with the solution's
     __device__ __forceinline__ void solve(double& b, int lane) const
     {
@@ -584,29 +182,19 @@ struct WaveLU {
         for (int k = 0; k < K; k++) {
             const int kp = piv[k];
             if (kp != k) {
-                const double x = bcast<ROWS>(b, k), y = bcast<ROWS>(b, kp);
+                const double x = wave_bcast(b, k), y = wave_bcast(b, kp);
                 b = lane == k ? y : (lane == kp ? x : b);
             }
         }
 #pragma unroll
         for (int j = 0; j < K; j++) {
-            const double a = -bcast<ROWS>(b, j);
+            const double a = -wave_bcast(b, j);
             const double v = fma(a, A[j], b);
             b = lane > j ? v : b;
         }
 #pragma unroll
         for (int j = K - 1; j >= 0; j--) {
-#if SBR_HET_DIVRCP
-            // lane j: b_j / U_jj, by the refined reciprocal when both operands are in range
-            // (wave-uniform choice on lane j's operands), else the IEEE division
-            const int fast = __builtin_amdgcn_readlane((okd & (b == 0.0 || in_div_range(b))) ? 1 : 0, j);
-            double q;
-            if (fast) q = div_rcp(b, A[j], rdiag);
-            else q = b / A[j];
-            const double bj = bcast<ROWS>(q, j);
-#else
-            const double bj = bcast<ROWS>(b / A[j], j); // lane j: b_j / A[j][j]
-#endif
+            const double bj = wave_bcast(b / A[j], j); // lane j: b_j / A[j][j]
             b = lane == j ? bj : b;
             const double v = fma(-bj, A[j], b);
             b = lane < j ? v : b;
@@ -614,20 +202,18 @@ struct WaveLU {
     }
 };
 
-#ifndef SBR_HET_LEARN_WG
 // waves (columns) per learning workgroup.  Config-4 step, same-call A/Bs (r05_kk, r05_ll): one
 // wave per workgroup 43.4 ms (45.7–46.0 with this kernel's wave indexing), 4 waves (one per SIMD
 // of a CU) 42.2–42.3, 2 waves 51.6 (r05_nn), 8 waves (two per SIMD: the learning becomes the critical path) 47.6
-#define SBR_HET_LEARN_WG 4
-#endif
+constexpr int kHetLearnWG = 4;
 template <int K>
-__global__ __launch_bounds__(64 * SBR_HET_LEARN_WG) void learn_hetero_wave_kernel(const double* __restrict__ betas,
+__global__ __launch_bounds__(64 * kHetLearnWG) void learn_hetero_wave_kernel(const double* __restrict__ betas,
                                                                const double* __restrict__ dist,
                                                                const double* __restrict__ eta,
                                                                const double* __restrict__ t_end, LearnArgs a,
                                                                HeteroBufs L)
 {
-    const int c = blockIdx.x * SBR_HET_LEARN_WG + (int)(threadIdx.x >> 6);
+    const int c = blockIdx.x * kHetLearnWG + (int)(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (c >= a.n_beta) return; // a whole wave (the column index is wave-uniform)
     const bool act = lane < K;
@@ -719,7 +305,7 @@ __global__ __launch_bounds__(64 * SBR_HET_LEARN_WG) void learn_hetero_wave_kerne
     double eig = 1.0; // integrator.eigen_est at init
     PIControl pc;
     AutoSwitch as;
-    const Tsit5Tab<SBR_HET_LEARN_PIN> cf; // the tableau in VGPRs, or literals
+    const Tsit5Tab<0> cf; // literals (the tableau in VGPRs: 103 -> 157 VGPRs, step 42.7 -> 46.6 ms, r05_x)
     int naccept = 0, nreject = 0;
     push(t, x, k1);
     int64_t iter = 0;
@@ -860,264 +446,6 @@ __global__ __launch_bounds__(64 * SBR_HET_LEARN_WG) void learn_hetero_wave_kerne
     }
 }
 
-// ---------------------------------------------------------------------------
-// learn_hetero_wave4_kernel<K>: four columns per wave, one 16-lane row per column
-// ---------------------------------------------------------------------------
-// learn_hetero_wave_kernel's solve with the wave's idle lanes put to work: row r (lanes
-// 16r..16r+15) runs column 4·blockIdx + r, lane 16r + k holds component k.  The couplings read
-// the row's lanes by DPP row broadcasts (a VALU move) instead of readlanes into SGPRs, and the
-// step control (t, dt, controller, AutoSwitch, knot counters) is row-uniform in VGPRs: all
-// four columns advance in the same instructions, so a wave does four columns' steps at the
-// issue cost of one (the chain is latency-bound: config 4 issued ≈10 cycles per instruction
-// with one column per wave).  Rows disagree only on the stiff/non-stiff branch (both run,
-// masked) and on when they finish.  Every operation of a column is the one-column kernel's, in
-// the same order: bit-identical knots, CDFs and hazards.  Lanes 16r + k, k >= K, shadow
-// component K−1 and never store.
-template <int K>
-__global__ __launch_bounds__(64) void learn_hetero_wave4_kernel(const double* __restrict__ betas,
-                                                                const double* __restrict__ dist,
-                                                                const double* __restrict__ eta,
-                                                                const double* __restrict__ t_end, LearnArgs a,
-                                                                HeteroBufs L)
-{
-    static_assert(K <= 16, "one column per 16-lane row");
-    const int lane = threadIdx.x;
-    const int row = lane >> 4, comp = lane & 15;
-    const int c_raw = blockIdx.x * 4 + row;
-    const bool colok = c_raw < a.n_beta;
-    const int c = colok ? c_raw : a.n_beta - 1; // tail rows shadow the last column and never store
-    const bool act = colok && comp < K;
-    const WaveRow<K, 4> R(comp, betas + (size_t)c * K, dist);
-    const double ETA = eta[c], T1 = t_end[c], T0 = 0.0;
-    const size_t cap = (size_t)L.cap;
-    double* __restrict__ T = L.t + (size_t)c * cap;
-    double* __restrict__ Gv = L.G + (size_t)c * cap * K;
-    double* __restrict__ H = L.hr + ((size_t)c * K + R.kk) * cap;
-    double* __restrict__ HI = L.hrI + ((size_t)c * K + R.kk) * cap;
-    uint32_t st = 0;
-    bool argok = ETA > 0.0 && T1 > T0;
-#pragma unroll
-    for (int k = 0; k < K; k++) argok = argok && (bcast<4>(R.bk, k) > 0.0);
-    if (!argok && colok && comp == 0) {
-        L.status[c] = SBR_ARG_INVALID;
-        L.n_knots[c] = 0; L.n_tau[c] = 0; L.n_le[c] = 0; L.n_accept[c] = 0; L.n_reject[c] = 0;
-    }
-    bool live = argok && colok;
-    const double x0 = a.x0, rtol = a.rtol, atol = a.atol, p = a.p, lam = a.lam;
-    const double dtmax = T1 - T0;
-    const double dtmin = sbr_jl_eps(dmax(fabs(T0), fabs(T1)));
-    double x, k1, k2, k3, k4, k5, k6, k7, tmp, tmp6, u;
-
-    // ---- ode_determine_initdt (row-uniform; dead rows compute it on their shadow column) ----
-    x = x0;
-    const double sk = fma(fabs(x0), rtol, atol);
-    const double d0 = R.rms(x0 / sk);
-    k1 = R.rhs(x);
-    const double d1 = R.rms(k1 / sk);
-    double dt0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : (d0 / d1) / 100.0;
-    dt0 = dmin(dt0, dtmax);
-    double dt;
-    if (dt0 < 10.0 * DBL_EPS) {
-        dt = dmax(1e-6, dtmin);
-    } else {
-        u = fma(dt0, k1, x0);
-        k7 = R.rhs(u);
-        bool same = true;
-#pragma unroll
-        for (int k = 0; k < K; k++) same = same && (row_bcast_int((int)(k1 == k7), k) != 0);
-        if (same) {
-            dt = dmax(dtmin, 100.0 * dt0);
-        } else {
-            const double d2 = R.rms((k7 - k1) / sk) / dt0;
-            const double md = dmax(d1, d2);
-            const double dt1 = (md <= 1e-15) ? dmax(1e-6, dt0 * 1e-3) : sbr_pow_pos(0.01 / md, 1.0 / SBR_INITDT_DEN);
-            dt = dmax(dtmin, dmin(dmin(100.0 * dt0, dt1), dtmax));
-        }
-    }
-
-    // ---- knot sink (learn_hetero_wave_kernel's, per row) ----
-    int n = 0, m = 0;
-    double tprev = 0.0, Ik = 0.0, eprev = 0.0, gprev = 0.0;
-    bool past = false, done = false;
-    auto push = [&](double t, double xs, double g) {
-        if (n >= L.cap) { st |= SBR_KNOT_OVERFLOW; done = true; return; }
-        if (colok && comp == 0) T[n] = t;
-        if (act) Gv[(size_t)n * K + comp] = xs;
-        if (!past) {
-            if (t <= ETA) {
-                const double E = sbr_exp(lam * t);
-                const double e = E * g;
-                Ik = (m == 0) ? 0.0 : Ik + (0.5 * (eprev + e)) * (t - tprev);
-                if (act) { H[m] = (p * E) * g; HI[m] = Ik; }
-                eprev = e;
-                gprev = g;
-                m++;
-                tprev = t;
-            } else {
-                past = true;
-                const double d = (ETA - tprev) / (t - tprev);
-                const double E = sbr_exp(lam * ETA);
-                const double pe = gprev * (1.0 - d) + g * d;
-                const double e = E * pe;
-                Ik = Ik + (0.5 * (eprev + e)) * (ETA - tprev);
-                if (act) { H[m] = (p * E) * pe; HI[m] = Ik; }
-                m++;
-            }
-        }
-        n++;
-    };
-
-    const double snap = 100.0 * sbr_jl_eps(T1);
-    double t = T0;
-    double eig = 1.0;
-    PIControl pc;
-    AutoSwitch as;
-    int naccept = 0, nreject = 0;
-    if (live) push(t, x, k1);
-    int64_t iter = 0;
-    for (;;) {
-        const bool run = live && t < T1 && !done;
-        if (!__any(run)) break;
-        if (!run) continue; // finished rows idle (masked) until every row of the wave is done
-        if (++iter > a.maxiters) { st |= SBR_ODE_MAXITERS; live = false; continue; }
-        (void)as.choose(eig, dt);
-        dt = dmin(dtmax, dt);
-        dt = dmax(dt, dtmin);
-        dt = dmin(dt, T1 - t);
-        if (dt <= dtmin && t + dt < T1) { st |= SBR_ODE_FAILED; live = false; continue; }
-        double EEst;
-        if (as.stiff) {
-            const double dtg = dt * ROS23_D;
-            const double invdtg = 1.0 / dtg, neginvdtg = -(1.0 / dtg);
-            const double dto2 = dt / 2.0, dto6 = dt / 6.0;
-            WaveLU<K, 4> W;
-            {
-                const double w = R.omega(x);
-                const double bkx = (1.0 - x) * R.bk;
-                const double dg = (-R.bk) * w + R.dk * bkx;
-                double s = 0.0;
-#pragma unroll
-                for (int j = 0; j < K; j++) {
-                    W.A[j] = (j == comp) ? dg : dist[j] * bkx;
-                    s = s + fabs(W.A[j]);
-                }
-                double nrm = 0.0;
-#pragma unroll
-                for (int i = 0; i < K; i++) {
-                    const double si = bcast<4>(s, i);
-                    nrm = (nrm != nrm || si != si) ? (double)NAN : (si > nrm ? si : nrm);
-                }
-                eig = nrm;
-#pragma unroll
-                for (int j = 0; j < K; j++) W.A[j] = (j == comp) ? fma(-1.0, invdtg, W.A[j]) : W.A[j];
-            }
-            W.factor(comp);
-            double r = k1 + dtg * 0.0;
-            W.solve(r, comp);
-            const double s1 = r * neginvdtg;
-            tmp = fma(dto2, s1, x);
-            const double f1 = R.rhs(tmp);
-            r = f1 - s1;
-            W.solve(r, comp);
-            const double s2 = fma(r, neginvdtg, s1);
-            u = fma(dt, s2, x);
-            k7 = R.rhs(u);
-            r = fma(dt, 0.0, fma(-2.0, s1 - k1, fma(-ROS23_C32, s2 - f1, k7)));
-            W.solve(r, comp);
-            const double s3 = r * neginvdtg;
-            const double ut = dto6 * (fma(-2.0, s2, s1) + s3);
-            EEst = R.rms(ut / fma(dmax(fabs(x), fabs(u)), rtol, atol));
-        } else {
-            const double a21 = dt * A21;
-            tmp = fma(a21, k1, x);
-            k2 = R.rhs(tmp);
-            tmp = fma(dt, fma(A31, k1, A32 * k2), x);
-            k3 = R.rhs(tmp);
-            tmp = fma(dt, fma(A41, k1, fma(A42, k2, A43 * k3)), x);
-            k4 = R.rhs(tmp);
-            tmp = fma(dt, fma(A51, k1, fma(A52, k2, fma(A53, k3, A54 * k4))), x);
-            k5 = R.rhs(tmp);
-            tmp6 = fma(dt, fma(A61, k1, fma(A62, k2, fma(A63, k3, fma(A64, k4, A65 * k5)))), x);
-            k6 = R.rhs(tmp6);
-            u = fma(dt, fma(A71, k1, fma(A72, k2, fma(A73, k3, fma(A74, k4, fma(A75, k5, A76 * k6))))), x);
-            k7 = R.rhs(u);
-            const double rr = fabs((k7 - k6) / (u - tmp6));
-            double e = 0.0;
-            bool e_nan = false;
-#pragma unroll
-            for (int k = 0; k < K; k++) {
-                const double v = bcast<4>(rr, k);
-                if (v != v) e_nan = true;
-                else if (v > e) e = v;
-            }
-            eig = e_nan ? (double)NAN : e;
-            const double ut = dt * fma(BT1, k1, fma(BT2, k2, fma(BT3, k3, fma(BT4, k4,
-                                       fma(BT5, k5, fma(BT6, k6, BT7 * k7))))));
-            EEst = R.rms(ut / fma(dmax(fabs(x), fabs(u)), rtol, atol));
-        }
-        if (EEst != EEst) { st |= SBR_ODE_FAILED; live = false; continue; }
-        bool acc;
-        const double dtn = pc.next_dt(EEst, dt, dtmax, dtmin, acc);
-        if (acc) {
-            naccept++;
-            double tn = t + dt;
-            if (fabs(tn - T1) < snap) tn = T1;
-            t = tn;
-            x = u;
-            k1 = k7;
-            dt = dtn;
-            push(t, x, k1);
-        } else {
-            nreject++;
-            dt = dtn;
-        }
-        if (!(dt > 0.0) || !isfinite(dt)) { st |= SBR_ODE_FAILED; live = false; }
-    }
-    const bool ran = argok && colok;
-    if (as.nswitch > 0) st |= SBR_STIFF_SWITCH;
-    int n_le = m;
-    if (ran) {
-        if (past) {
-            n_le = m - 1;
-        } else if (!(st & SBR_KNOT_OVERFLOW)) {
-            if (n >= 2 && tprev == ETA) {
-                const double E = sbr_exp(lam * ETA);
-                const double pe = 0.0 + gprev * 1.0;
-                if (act) { H[m] = (p * E) * pe; HI[m] = Ik; }
-                m++;
-            } else {
-                st |= SBR_OOB;
-            }
-        }
-    }
-    // normalisation hr = p·e^{λτ̄}g / (p·I(τ̄) + (1 − p)·I(η)), all 64 lanes over each column's rows
-    __threadfence_block();
-    const double omp = 1.0 - p;
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-        const int cr = blockIdx.x * 4 + r;
-        const int mr = __builtin_amdgcn_readlane(m, 16 * r);
-        const int okr = __builtin_amdgcn_readlane((ran && !(st & SBR_OOB)) ? 1 : 0, 16 * r);
-        if (cr >= a.n_beta || mr <= 0 || !okr) continue;
-        double* __restrict__ Hc = L.hr + (size_t)cr * K * cap;
-        const double* __restrict__ HIc = L.hrI + (size_t)cr * K * cap;
-#pragma unroll
-        for (int k = 0; k < K; k++) {
-            const double Ieta = HIc[(size_t)k * cap + mr - 1];
-            for (int i = lane; i < mr; i += 64)
-                Hc[(size_t)k * cap + i] = Hc[(size_t)k * cap + i] / ((p * HIc[(size_t)k * cap + i]) + (omp * Ieta));
-        }
-    }
-    if (ran && comp == 0) {
-        L.n_knots[c] = n;
-        L.n_tau[c] = m;
-        L.n_le[c] = n_le;
-        L.status[c] = st;
-        L.n_accept[c] = naccept;
-        L.n_reject[c] = nreject;
-    }
-}
-
 // The K hazards (heterogeneity_solver.jl:255: hazard_rate on the explicit grid = the learning
 // knots, η always appended) of a column whose knots and group CDFs are already in L — a
 // LearningResultsHetero the caller holds (sbr_hetero_equilibrium_on_knots).  The streamed hazard
@@ -1229,33 +557,8 @@ struct HCol {
     }
 };
 
-#ifndef SBR_HET_UBCACHE
-// pass 2 of AW_max reuses pass 1's range bounds: 1 = every 256-knot range's bound in a private
-// array (scratch; config-4 step 45.3 -> 43.3 ms over none), 3 = every bound as a 16-bit code
-// (ceil(65536·ub), exact) in the LDS left between the knot slab and the HR block sums (no
-// scratch).  A/B r05: the two best bounds of each level in registers plus the largest of the
-// rest, recomputing the others, was 44.9 ms (removed)
-#define SBR_HET_UBCACHE 3
-#endif
-#ifndef SBR_HET_UBC_BITS
-#define SBR_HET_UBC_BITS 16 // code width of UBCACHE 3 (8: 29.8 ms alone, the 1/256 window recomputes)
-#endif
-#if SBR_HET_UBC_BITS == 16
+constexpr int kHetUbcBits = 16; // bound-code width (8: 29.8 ms alone, the 1/256 window recomputes)
 typedef unsigned short ubc_t;
-#else
-typedef unsigned char ubc_t;
-#endif
-#ifndef SBR_HET_K1
-#define SBR_HET_K1 1 // AW_OUT bound from the knot after next -> the next knot where consecutive knots are separated
-#endif
-#ifndef SBR_HET_SHARE_DIV
-#define SBR_HET_SHARE_DIV 1 // exact AW evaluations share δ between groups with equal arguments
-// (A/B r05: also skipping the second CDF load of an on-knot argument, g0·1 + g1·0 = g0, made the
-// data-dependent loads serial — config-4 equilibrium alone 29.1 -> 33.6 ms; not kept)
-#endif
-#ifndef SBR_HET_UBC_MAX
-#define SBR_HET_UBC_MAX 40 // 256-knot ranges cached (the LDS slab holds ≤ 10,176 knots: 40 ranges)
-#endif
 template <int K, class PT>
 __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const double* __restrict__ dist,
                                                    const double u, const double kappa, const int max_iters,
@@ -1529,7 +832,6 @@ __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const d
                 if (!(xa <= thi) || !(xb <= thi)) flag |= SBR_OOB;
                 while (ja[k] + 1 < n && C.T[ja[k] + 1] <= xa) ja[k]++;
                 while (jb[k] + 1 < n && C.T[jb[k] + 1] <= xb) jb[k]++;
-#if SBR_HET_SHARE_DIV
                 const int qa = ja[k] > n - 2 ? n - 2 : (ja[k] < 0 ? 0 : ja[k]);
                 const int qb = jb[k] > n - 2 ? n - 2 : (jb[k] < 0 ? 0 : jb[k]);
                 double da = da_p, db = db_p;
@@ -1541,10 +843,6 @@ __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const d
                 xa_p = xa; da_p = da; xb_p = xb; db_p = db;
                 const double gi = C.g(qa, k) * (1.0 - da) + C.g(qa + 1, k) * da;
                 const double go = C.g(qb, k) * (1.0 - db) + C.g(qb + 1, k) * db;
-#else
-                const double gi = C.lerp(ja[k], k, xa);
-                const double go = C.lerp(jb[k], k, xb);
-#endif
                 const double awin = av >= 0 ? gi : 0.0;
                 const double awout = bv >= 0 ? go : 0.0;
                 cum = cum + dist[k] * (awout - awin);
@@ -1600,7 +898,6 @@ __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const d
             return (sum + 1e-14) + env;
         };
         auto end_of = [&](int i0, int w) { return i0 + w < n ? i0 + w : n; };
-#if SBR_HET_UBCACHE == 3
         if (!flag) {
             // pass 1 keeps every range bound as a code in LDS (this lane's column of ubc rows:
             // the 256-knot ranges, then the best one's four 64-knot and its eight 8-knot ranges),
@@ -1608,8 +905,8 @@ __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const d
             // or S − 1 (ub > (S − 2)/S: unknown).  Pass 2: c/S <= mx prunes, (c − 1)/S >= mx
             // descends (ub > mx), in between — and for rows past ubc_rows, the LDS left — the bound
             // is recomputed (ub_rng's value does not depend on the hints).
-            constexpr double S = (double)(1 << SBR_HET_UBC_BITS), rS = 1.0 / S;
-            constexpr int unk = (1 << SBR_HET_UBC_BITS) - 1;
+            constexpr double S = (double)(1 << kHetUbcBits), rS = 1.0 / S;
+            constexpr int unk = (1 << kHetUbcBits) - 1;
             const int nr = (n + 255) >> 8;
             auto put = [&](int row, double ub) {
                 if (row >= ubc_rows) return;
@@ -1664,54 +961,6 @@ __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const d
                 }
             }
         }
-#else
-        if (!flag) {
-            // pass 1 (best 256 → 64 → 8-knot range by bound, evaluated) keeps its bounds, rounded
-            // up to float, in a private array (scratch): pass 2 re-reads them instead of redoing
-            // the 2K bracket searches and gathers of each bound (ub_rng's value does not depend on
-            // the hints, so a cached bound is the bound)
-            const bool cache = SBR_HET_UBCACHE && n <= 256 * SBR_HET_UBC_MAX;
-            float c256[SBR_HET_UBCACHE ? SBR_HET_UBC_MAX : 1], c64[4], c8[8];
-            int bs = 0;
-            double bu = -INFINITY;
-            for (int i0 = 0; i0 < n; i0 += 256) {
-                const double ub = ub_rng(i0, end_of(i0, 256) - 1);
-                if (SBR_HET_UBCACHE && cache) c256[i0 >> 8] = __double2float_ru(ub);
-                if (!(ub <= bu)) { bu = ub; bs = i0; }
-            }
-            int bb = bs;
-            bu = -INFINITY;
-            for (int i0 = bs; i0 < end_of(bs, 256); i0 += 64) {
-                const double ub = ub_rng(i0, end_of(i0, 64) - 1);
-                c64[(i0 - bs) >> 6] = __double2float_ru(ub);
-                if (!(ub <= bu)) { bu = ub; bb = i0; }
-            }
-            int b8 = bb;
-            bu = -INFINITY;
-            for (int i0 = bb; i0 < end_of(bb, 64); i0 += 8) {
-                const double ub = ub_rng(i0, end_of(i0, 8) - 1);
-                c8[(i0 - bb) >> 3] = __double2float_ru(ub);
-                if (!(ub <= bu)) { bu = ub; b8 = i0; }
-            }
-            eval_range(b8, end_of(b8, 8));
-            for (int s0 = 0; s0 < n && mx == mx; s0 += 256) {
-                const int se = end_of(s0, 256);
-                if ((SBR_HET_UBCACHE && cache) ? ((double)c256[s0 >> 8] <= mx) : (ub_rng(s0, se - 1) <= mx)) continue;
-                for (int k0 = s0; k0 < se && mx == mx; k0 += 64) {
-                    const int ke = end_of(k0, 64);
-                    if ((SBR_HET_UBCACHE && s0 == bs) ? ((double)c64[(k0 - bs) >> 6] <= mx) : (ub_rng(k0, ke - 1) <= mx))
-                        continue;
-                    for (int i0 = k0; i0 < ke && mx == mx; i0 += 8) {
-                        const int ie = end_of(i0, 8);
-                        if (i0 == b8) continue;
-                        if ((SBR_HET_UBCACHE && k0 == bb) ? ((double)c8[(i0 - bb) >> 3] <= mx) : (ub_rng(i0, ie - 1) <= mx))
-                            continue;
-                        eval_range(i0, ie);
-                    }
-                }
-            }
-        }
-#endif
     }
     if (flag) { st_o = flag | lbits; return; }
     xi_o = xi;
@@ -1720,26 +969,10 @@ __device__ __forceinline__ void solve_hetero_point(const HCol<K, PT>& C, const d
     st_o = SBR_RUN | SBR_CONVERGED | lbits;
 }
 
-#ifndef SBR_HET_XCD
-#define SBR_HET_XCD 1
-#endif
-#ifndef SBR_HET_BLOCK
-#define SBR_HET_BLOCK 256 // u points per hetero equilibrium workgroup (A/B: 512)
-#endif
-#ifndef SBR_HET_EQ_PRIO
-#define SBR_HET_EQ_PRIO 2 // equilibrium waves ahead of the co-resident learning waves (config-4 step 49.7 -> 47.9 ms)
-#endif
+constexpr int kHetBlock = 256; // u points per hetero equilibrium workgroup (512 was slower)
+constexpr int kHetMinW = 2; // waves per SIMD: two 4-wave workgroups per CU (LDS slab: kHetLds in sbr_capi.hip)
 template <int K, int BLOCK, int MODE>
-#ifndef SBR_HET_MINW
-#define SBR_HET_MINW 2 // waves per SIMD: two 4-wave workgroups per CU (LDS slab: SBR_HET_LDS in sbr_capi.hip)
-#endif
-#ifndef SBR_HET_NVGPR
-#define SBR_HET_NVGPR 0 // > 0: VGPR cap (amdgpu_num_vgpr counts half of the unified file on gfx950)
-#endif
-__global__ __launch_bounds__(BLOCK, SBR_HET_MINW)
-#if SBR_HET_NVGPR
-__attribute__((amdgpu_num_vgpr(SBR_HET_NVGPR / 2)))
-#endif
+__global__ __launch_bounds__(BLOCK, kHetMinW)
 void equilibrium_hetero_kernel(HeteroBufs L, const double* __restrict__ dist,
                                                                    const double* __restrict__ eta,
                                                                    const double* __restrict__ t_end,
@@ -1748,10 +981,7 @@ void equilibrium_hetero_kernel(HeteroBufs L, const double* __restrict__ dist,
                                                                    double* __restrict__ tout_out)
 {
     extern __shared__ double smem[];
-#if SBR_HET_EQ_PRIO
-    __builtin_amdgcn_s_setprio(SBR_HET_EQ_PRIO); // A/B: issue priority over co-resident learning waves
-#endif
-#if SBR_HET_XCD
+    __builtin_amdgcn_s_setprio(2); // issue priority over co-resident learning waves (step 49.7 -> 47.9 ms)
     // XCD-aware tile order (1-D grid): workgroup w runs on XCD w mod 8, so the u-tiles of one
     // column are given to consecutive workgroups of the same XCD — they share that XCD's L2
     // copy of the column's G and HR rows instead of fetching four copies into four L2s.
@@ -1760,10 +990,6 @@ void equilibrium_hetero_kernel(HeteroBufs L, const double* __restrict__ dist,
     const int c = (seq / ntile) * 8 + xcd;
     const int tile = seq - (seq / ntile) * ntile;
     if (c >= a.n_col) return;
-#else
-    const int c = blockIdx.y;
-    const int tile = blockIdx.x;
-#endif
     const int n = L.n_knots[c];
     const uint32_t lst = L.status[c];
     const size_t cap = (size_t)L.cap;
@@ -1875,13 +1101,13 @@ void equilibrium_hetero_kernel(HeteroBufs L, const double* __restrict__ dist,
         const int ubc_rows = ((sums ? a.lds_cap - 2 * K * nblk : a.lds_cap) - n) * 8 / (BLOCK * (int)sizeof(ubc_t));
         ubc_t* const ubc = (ubc_t*)(smem + n) + threadIdx.x;
         solve_hetero_point<K>(C, dl, uj, a.kappa, a.max_iters, a.tolerance, lbits, xi, aw, tol, st, it, tin, tout,
-                              mono, a.diag, a.aw_path, env, fits && s_close == 0, (SBR_HET_K1 && s_close1 == 0) ? 1 : 2,
+                              mono, a.diag, a.aw_path, env, fits && s_close == 0, s_close1 == 0 ? 1 : 2,
                               tin_g, tout_g, ubc, BLOCK, ubc_rows);
     } else {
         HCol<K, const double*> C{gT, L.G + (size_t)c * cap * K, L.hr + (size_t)c * K * cap, n, L.n_tau[c],
                                  L.n_le[c], cap, eta[c], t_end[c], nullptr, 0};
         solve_hetero_point<K>(C, dl, uj, a.kappa, a.max_iters, a.tolerance, lbits, xi, aw, tol, st, it, tin, tout,
-                              mono, a.diag, a.aw_path, env, fits && s_close == 0, (SBR_HET_K1 && s_close1 == 0) ? 1 : 2,
+                              mono, a.diag, a.aw_path, env, fits && s_close == 0, s_close1 == 0 ? 1 : 2,
                               tin_g, tout_g);
     }
     out.xi[o] = xi;
@@ -1901,16 +1127,8 @@ static hipError_t launch_hetero_k(const double* betas, const double* dist, const
         return hipGetLastError();
     }
     if (phase == 0) {
-#if SBR_HET_LEARN_WAVE && SBR_HET_LEARN_ROWS == 4
-        hipLaunchKernelGGL(learn_hetero_wave4_kernel<K>, dim3((la.n_beta + 3) / 4), dim3(64), 0, s, betas, dist, eta,
-                           t_end, la, L);
-#elif SBR_HET_LEARN_WAVE
-        hipLaunchKernelGGL(learn_hetero_wave_kernel<K>, dim3((la.n_beta + SBR_HET_LEARN_WG - 1) / SBR_HET_LEARN_WG),
-                           dim3(64 * SBR_HET_LEARN_WG), 0, s, betas, dist, eta, t_end, la, L);
-#else
-        hipLaunchKernelGGL(learn_hetero_kernel<K>, dim3((la.n_beta + 63) / 64), dim3(64), 0, s, betas, dist, eta,
-                           t_end, la, L);
-#endif
+        hipLaunchKernelGGL(learn_hetero_wave_kernel<K>, dim3((la.n_beta + kHetLearnWG - 1) / kHetLearnWG),
+                           dim3(64 * kHetLearnWG), 0, s, betas, dist, eta, t_end, la, L);
         return hipGetLastError();
     }
     const size_t lds = (size_t)ea_in.lds_cap * sizeof(double);
@@ -1921,19 +1139,12 @@ static hipError_t launch_hetero_k(const double* betas, const double* dist, const
         hipLaunchKernelGGL(k1, grid, dim3(bs), lds, s, L, dist, eta, t_end, u, ea, out, tin, tout);
         hipLaunchKernelGGL(k2, grid, dim3(bs), 0, s, L, dist, eta, t_end, u, ea, out, tin, tout);
     };
-#if SBR_HET_XCD
     const unsigned ncol8 = (unsigned)((la.n_beta + 7) / 8) * 8;
-    if (ea.n_u >= SBR_HET_BLOCK)
-        go(equilibrium_hetero_kernel<K, SBR_HET_BLOCK, 1>, equilibrium_hetero_kernel<K, SBR_HET_BLOCK, 2>,
-           dim3(((ea.n_u + SBR_HET_BLOCK - 1) / SBR_HET_BLOCK) * ncol8), SBR_HET_BLOCK);
+    if (ea.n_u >= kHetBlock)
+        go(equilibrium_hetero_kernel<K, kHetBlock, 1>, equilibrium_hetero_kernel<K, kHetBlock, 2>,
+           dim3(((ea.n_u + kHetBlock - 1) / kHetBlock) * ncol8), kHetBlock);
     else
         go(equilibrium_hetero_kernel<K, 64, 1>, equilibrium_hetero_kernel<K, 64, 2>, dim3(((ea.n_u + 63) / 64) * ncol8), 64);
-#else
-    if (ea.n_u >= 256)
-        go(equilibrium_hetero_kernel<K, 256, 1>, equilibrium_hetero_kernel<K, 256, 2>, dim3((ea.n_u + 255) / 256, la.n_beta), 256);
-    else
-        go(equilibrium_hetero_kernel<K, 64, 1>, equilibrium_hetero_kernel<K, 64, 2>, dim3((ea.n_u + 63) / 64, la.n_beta), 64);
-#endif
     return hipGetLastError();
 }
 

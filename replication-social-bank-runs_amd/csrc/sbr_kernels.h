@@ -18,7 +18,8 @@ struct LearnBufs {
     uint32_t* status;   // learning-level SBR_* bits
     int32_t* n_accept;  // accepted RK steps (flop accounting)
     int32_t* n_reject;  // rejected RK steps
-    int32_t cap;
+    int32_t cap;        // row stride (doubles) of t / G / hr / hrI: column b's row starts at b·cap
+    int32_t lim;        // knots a column may store (<= cap; the learning kernel's SBR_KNOT_OVERFLOW bound)
 };
 
 struct LearnArgs {
@@ -204,16 +205,23 @@ hipError_t launch_hetero(int K, const double* betas, const double* dist, const d
 
 hipError_t launch_learn_logistic(const double* beta, const double* eta, const double* t_end, const LearnArgs& a,
                                  const LearnBufs& L, hipStream_t s);
+// the learning kernel alone (a.fuse_hazard: HR numerators and running integrals streamed, to be
+// normalised by launch_hazard_norm); mode 0: two waves per workgroup (beside a running equilibrium
+// launch), 1: one wave per workgroup (latency), 2: a batch's wide learning launch (the chip otherwise idle)
+hipError_t launch_learn_kernel(const double* beta, const double* eta, const double* t_end, const LearnArgs& a,
+                               const LearnBufs& L, hipStream_t s, int mode);
+// HR = numerator / (p·I + (1 − p)·I_η) over the first n_cols columns of L (after a fused learning)
+hipError_t launch_hazard_norm(const LearnArgs& a, const LearnBufs& L, int n_cols, hipStream_t s);
 // only_mode: 0 = the LDS-slab launch then the global-memory launch; 1 / 2 = only one of them
 // (a caller that knows every column fits the slab, or none does).  a.aw_path (n_u == 1): the
 // solving lane writes AW_cum on τ̄ (exhaustive); single points use launch_point_coop instead.
 hipError_t launch_equilibrium(const LearnBufs& L, const double* eta, const double* t_end, const double* u,
                               const EqArgs& a, const ResultSoA& out, int n_beta, hipStream_t s, int only_mode = 0);
-// one point (n_u == 1, column 0 of L) by a whole workgroup: wave-wide searches for the solve,
+// one point per workgroup (u[j], results at [j], j < n_points; column 0 of L): wave-wide searches for the solve,
 // the block for get_AW's exhaustive pass (AW_max and, with a.aw_path, the three paths).  a.lds_cap
 // = knots staged per array (3 arrays: t, G, HR); larger columns run from global memory.
 hipError_t launch_point_coop(const LearnBufs& L, const double* eta, const double* t_end, const double* u,
-                             const EqArgs& a, const ResultSoA& out, hipStream_t s);
+                             const EqArgs& a, const ResultSoA& out, hipStream_t s, int n_points = 1);
 // hazard_rate (solver.jl:153-185) of n_beta columns whose knots, n_knots, n_le (#knots <= η) and
 // status are in L (the hazard stage of launch_learn_logistic on its own)
 hipError_t launch_hazard(const double* beta, const double* eta, const LearnArgs& a, const LearnBufs& L, int n_beta,

@@ -11,10 +11,7 @@ namespace sbr {
 
 // Inside a block the entries are read 8 at a time (independent loads issued together, then
 // tested in order), so finding the index costs ≤ 8 dependent round trips to L2 instead of ≤ 64.
-#ifndef SBR_SCAN_CHUNK
-#define SBR_SCAN_CHUNK 8
-#endif
-constexpr int kScanChunk = SBR_SCAN_CHUNK;
+constexpr int kScanChunk = 8;
 
 // first i in [i, e) with (H[i] > u) == ABOVE, or -1
 template <bool ABOVE, class P>

@@ -44,21 +44,11 @@ namespace {
 // fallback (`in_ring ? RT(j) : to[j]`) into one FLAT load of a selected pointer; a FLAT load
 // counts on both the vector-memory and the LDS counters, so every ring read waited for the
 // lane's outstanding global loads and stores.
-#ifndef SBR_SOCIAL_AS
-#define SBR_SOCIAL_AS 1
-#endif
 typedef double sbr_dv2 __attribute__((ext_vector_type(2))); // 16-byte knot pair
-#if SBR_SOCIAL_AS
 typedef __attribute__((address_space(1))) double gdouble;
 typedef __attribute__((address_space(1))) char gchar;
 typedef __attribute__((address_space(1))) sbr_dv2 gdouble2;
 typedef __attribute__((address_space(3))) double ldouble;
-#else
-typedef double gdouble;
-typedef char gchar;
-typedef sbr_dv2 gdouble2;
-typedef double ldouble;
-#endif
 struct BView {
     gdouble* p; // ws + (group·5 + slot)·cap·64 + lane·16
     // 32-bit byte offset (a group's buffer is < 4 GiB): one shift-and-or pair, no sign extension
@@ -159,13 +149,7 @@ struct Walker {
     }
 };
 
-#ifndef SBR_SOCIAL_PAIRS
-#define SBR_SOCIAL_PAIRS 1 // streaming passes and damping walkers load knot pairs (16 B per lane per request)
-#endif
 
-#ifndef SBR_SOCIAL_FBWAIT
-#define SBR_SOCIAL_FBWAIT 1 // ring misses wait for their own global loads inside the miss branch (A/B)
-#endif
 // A ring miss loads its operands from global memory inside a divergent branch.  Unless the
 // branch waits for them itself, the wait lands where the ring path writes the same registers,
 // and it is a vmcnt wait that also drains every older store and refill load of the wave — on
@@ -173,9 +157,7 @@ struct Walker {
 // is paid only when a lane misses.
 __device__ __forceinline__ void ring_miss_wait()
 {
-#if SBR_SOCIAL_FBWAIT
     __builtin_amdgcn_s_waitcnt(0x0F70);
-#endif
 }
 
 // knots k, k+1 (k even) of one lane in one 16-byte load: a pair never straddles a 16-knot line
@@ -438,145 +420,16 @@ __device__ void coop_damping(BView T, BView Gv, BView AWO, const int n, const do
     aoob |= __ballot(bad) != 0;
 }
 
-#ifndef SBR_SOCIAL_PF
-#define SBR_SOCIAL_PF 32 // knots ahead of the step that `accepted` touches (A/B)
-#endif
-// dG/dt = (1 − G) β AW_old(t) (social_learning_dynamics.jl:61-67).  All stage
-// times of a step (t + c_i·dt, t + dt) are known when the step starts, so the
-// five AW_old lookups are done up front (prepare): brackets from the register
-// window anchored at the step's t, then 20 independent operand loads and five
-// independent divisions — off the serial chain of the RK stages.
-struct SocialRhs {
-    double beta;
-    BView to;
-    BView vo;
-    int n;
-    double tfirst, tlast;
-    Win8 w;
-    double aw[5];
-    double last_aw;
-    bool oob;
-    int slow;   // diagnostics: stage lookups past the register window
-    __device__ __forceinline__ void init(double b, BView t_, BView v_, int n_)
-    {
-        slow = 0;
-        beta = b; to = t_; vo = v_; n = n_;
-        tfirst = n > 0 ? to[0] : 0.0;
-        tlast = n > 0 ? to[n - 1] : 0.0;
-        w.init(to, n);
-        oob = false;
-        last_aw = 0.0;
-    }
-    __device__ __forceinline__ double lookup(double x)
-    {
-        if (n < 2 || !(x >= tfirst && x <= tlast)) { oob = true; return (double)NAN; }
-        return lerp_at(to, vo, n, w.find(x), x);
-    }
-    // generic evaluation (initial-dt probes)
-    __device__ __forceinline__ double eval(double t, double x)
-    {
-        const double a = lookup(t);
-        last_aw = a;
-        return ((1.0 - x) * beta) * a;
-    }
-    __device__ __forceinline__ void prepare(double t, double dt)
-    {
-        const double xs[5] = {fma(C1, dt, t), fma(C2, dt, t), fma(C3, dt, t), fma(C4, dt, t), t + dt};
-        int js[5];
-        bool in[5];
-#pragma unroll
-        for (int k = 0; k < 5; k++) {
-            in[k] = n >= 2 && xs[k] >= tfirst && xs[k] <= tlast;
-            slow += (in[k] && !(xs[k] < w.tw[7])) ? 1 : 0;
-            js[k] = w.find(in[k] ? xs[k] : tfirst);
-        }
-        // 20 independent operand loads, then five independent divisions
-#ifdef SBR_EXPERIMENT_NOLOOKUP
-#pragma unroll
-        for (int k = 0; k < 5; k++) aw[k] = in[k] ? 0.5 + 1e-3 * xs[k] : (double)NAN;
-#else
-#pragma unroll
-        for (int k = 0; k < 5; k++) {
-            aw[k] = lerp_sel(to, vo, n, js[k], xs[k], in[k]);
-            oob |= !in[k];
-        }
-#endif
-        last_aw = aw[4];
-    }
-    // stage s = 1..6 (k2..k7): times C1..C4, then t + dt twice
-    __device__ __forceinline__ double stage(int s, double, double x) const
-    {
-        return ((1.0 - x) * beta) * aw[s < 5 ? s - 1 : 4];
-    }
-    // ForwardDiff (oracle jac_social): J = ((−1)·β)·AW_old(t), ∂f/∂t = ((1 − G)·β)·AW_old'(t)
-    // with the interpolant's dual-number slope v_j·(−1/Δ) + v_{j+1}·(1/Δ) on t's bracket
-    __device__ __forceinline__ void jac(double t, double x, double& J, double& dT)
-    {
-        if (n < 2 || !(t >= tfirst && t <= tlast)) {
-            oob = true;
-            J = (double)NAN;
-            dT = (double)NAN;
-            return;
-        }
-        int j = w.find(t);
-        j = j > n - 2 ? n - 2 : (j < 0 ? 0 : j);
-        const double t0 = to[j], t1 = to[j + 1], v0 = vo[j], v1 = vo[j + 1];
-        const double d = (t - t0) / (t1 - t0);
-        const double a = v0 * (1.0 - d) + v1 * d;
-        const double rr = 1.0 / (t1 - t0);
-        const double ap = v0 * (-rr) + v1 * rr;
-        J = ((-1.0) * beta) * a;
-        dT = ((1.0 - x) * beta) * ap;
-    }
-    // After an accepted step, touch AW_{n−1}'s knot 32 ahead (two 16-knot lines of the lane's
-    // wave-blocked buffer): those lines were written a whole iterate ago and live in HBM, so
-    // every stage lookup would otherwise wait on an HBM round trip; the touch brings them into
-    // L2 while the intervening steps run.  The loaded values are consumed one step later (an
-    // impossible-value compare into the `slow` diagnostic), so the wait for them falls where
-    // they have long arrived.
-    double pf_t = 0.0, pf_v = 0.0;
-    __device__ __forceinline__ void accepted(double t)
-    {
-        if (n >= 2 && t >= tfirst && t <= tlast) {
-            const int j = w.find_advance(t);
-#ifndef SBR_SOCIAL_NO_PREFETCH
-            slow += (pf_t == -1.0 || pf_v == -2.0) ? 1 : 0;
-            const int q = j + SBR_SOCIAL_PF < n ? j + SBR_SOCIAL_PF : n - 1;
-            pf_t = to[q];
-            pf_v = vo[q];
-#else
-            (void)j;
-#endif
-        }
-    }
-    static constexpr bool kFsalExact = false;
-    static constexpr bool kPinTableau = false;
-};
 
-#ifndef SBR_SOCIAL_UNROLL
-// the hazard and damping passes stream a point's knots; unrolled, a lane has the loads of
-// several knots in flight instead of one memory round trip per knot (A/B: 1)
-#define SBR_SOCIAL_UNROLL 1 // A/B: 8 was 2.7 % slower on the bulk (r04_j)
-#endif
-#ifndef SBR_SOCIAL_RING
-#define SBR_SOCIAL_RING 1 // multi-point waves read AW_{n−1} through a per-lane LDS ring (SocialRhsRing)
-#endif
-#ifndef SBR_SOCIAL_RING4
-#define SBR_SOCIAL_RING4 1 // four 16-knot lines per lane (32 lanes) and refills batched every 8 steps
-#endif
-constexpr int kRing = SBR_SOCIAL_RING4 ? 64 : 32; // knots per lane: four (two) 16-knot lines
-#ifndef SBR_SOCIAL_RING_LANES
-#define SBR_SOCIAL_RING_LANES (SBR_SOCIAL_RING4 ? 32 : 64) // lanes a multi-point wave may use (the launch makes L <= this)
-#endif
-#ifndef SBR_SOCIAL_MINW
-#define SBR_SOCIAL_MINW 1 // waves per SIMD the iterate kernel is compiled for (A/B: 2 with 2048 waves of
-                          // 16 points and 32-lane rings spilled 84 B/lane and was slower, 10.98 -> 11.64 s: r04_u)
-#endif
-constexpr int kRingLanes = SBR_SOCIAL_RING_LANES;
+constexpr int kRing = 64; // knots per lane: four 16-knot lines (two lines per lane for 64 lanes was slower: r04_z)
+
+constexpr int kRingLanes = 32; // lanes a multi-point wave may use (the launch makes L <= this)
 constexpr size_t kRingLdsBytes = (size_t)2 * kRing * kRingLanes * sizeof(double); // t and v: 32 KiB either way
 
-// SocialRhs for a wave that runs many points (the bulk of a sweep: up to 32 per wave).  There
-// every lane streams its own knot lines, so each operand load of a stage lookup is a separate
+// dG/dt = (1 − G) β AW_old(t) (social_learning_dynamics.jl:61-67) for a wave that runs many
+// points (the bulk of a sweep: up to 32 per wave).  All stage times of a step (t + c_i·dt,
+// t + dt) are known when the step starts, so the five AW_old lookups are done up front
+// (prepare), off the serial chain of the RK stages.  Every lane streams its own knot lines, so each operand load of a stage lookup is a separate
 // L1 request per active lane: ≈25 load instructions per RK step × 32 lanes, and the L1 cannot
 // hold 4 waves × 32 lanes × the lines in use (PMC of the bulk: 66 % of wave cycles waiting on
 // memory, against 40 % for a lone point, profiles/r04_pmc_social_bulk_vs_lone.txt).  Here each
@@ -585,10 +438,7 @@ constexpr size_t kRingLdsBytes = (size_t)2 * kRing * kRingLanes * sizeof(double)
 // by one 128-byte line (16 knots, eight 16-byte loads per array) when the accepted time's
 // bracket passes rb + 20, and the line after next is touched into L2 then.  The bracket window
 // (Win8) reloads from the ring too.  Knots outside the ring fall back to global loads.  Same
-// brackets, operands and operations as SocialRhs: bit-identical.
-#ifndef SBR_SOCIAL_RING_PIN
-#define SBR_SOCIAL_RING_PIN 1 // multi-point waves hold the Tsit5 tableau in VGPRs (Tsit5Regs; AGPR overflow, no scratch; share 45.3 -> 44.7 s, r05_v)
-#endif
+// brackets, operands and operations as the oracle's forced right-hand side: bit-identical.
 struct SocialRhsRing {
     double beta;
     BView to;
@@ -605,10 +455,7 @@ struct SocialRhsRing {
     int rb;     // first knot held (a multiple of 16)
     int tick = 0; // attempted Tsit5 steps (prepare calls): equal across the live lanes of a wave
     double pf_t = 0.0, pf_v = 0.0;
-#ifndef SBR_SOCIAL_ACCEPT_FIRST
-#define SBR_SOCIAL_ACCEPT_FIRST 1
-#endif
-    static constexpr bool kAcceptFirst = SBR_SOCIAL_ACCEPT_FIRST != 0; // refill before the knot's stores (ode_scalar)
+    static constexpr bool kAcceptFirst = true; // refill before the knot's stores (ode_scalar)
     __device__ __forceinline__ bool in_ring(int j) const { return j >= rb && j + 1 < rb + kRing; }
     __device__ __forceinline__ double RT(int j) const { return rt[(j & (kRing - 1)) * kRingLanes]; }
     __device__ __forceinline__ double RV(int j) const { return rv[(j & (kRing - 1)) * kRingLanes]; }
@@ -737,7 +584,6 @@ struct SocialRhsRing {
     {
         if (n >= 2 && t >= tfirst && t <= tlast) {
             const int j = find_advance(t);
-#if SBR_SOCIAL_RING4
             // Four lines: a lane whose bracket has passed rb + 20 replaces its oldest lines
             // (wb > j − 4 >= the new rb), but only on every 8th attempted step — the same step
             // for every lane of the wave, so one wave-wide wait on the refill loads serves all
@@ -756,38 +602,12 @@ struct SocialRhsRing {
                 pf_t = to[q];
                 pf_v = vo[q];
             }
-            if (SBR_SOCIAL_RING4) return;
-#endif
-            if (j - rb >= 20) {
-                if (j - rb >= 20 + 16) { // a step past the whole ring: re-seat it around j
-                    rb = ((j - 4) >> 4) << 4;
-                    fill_line(rb);
-                    fill_line(rb + 16);
-                } else {
-                    // the oldest line is behind the window (wb > j − 4 >= rb + 16): replace it by
-                    // the line after the ring
-                    fill_line(rb + kRing);
-                    rb += 16;
-                }
-                // touch the line after the ring into L2 (consumed one line later by the `slow`
-                // diagnostic, so that its wait falls where it has arrived)
-                slow += (pf_t == -1.0 || pf_v == -2.0) ? 1 : 0;
-                const int q = rb + kRing + 16 < n ? rb + kRing + 16 : n - 1;
-                pf_t = to[q];
-                pf_v = vo[q];
-            }
         }
     }
     static constexpr bool kFsalExact = false;
-    static constexpr bool kPinTableau = SBR_SOCIAL_RING_PIN != 0;
+    static constexpr bool kPinTableau = true;
 };
 
-#ifndef SBR_SOCIAL_PAR_STAGES
-#define SBR_SOCIAL_PAR_STAGES 1 // SocialRhsCoop: the five stage lookups of a step on lanes 0..4 at once
-#endif
-#ifndef SBR_SOCIAL_COOP
-#define SBR_SOCIAL_COOP 1 // a wave left with one live point runs it on all 64 lanes (SocialRhsCoop)
-#endif
 // The same right-hand side for a wave whose 64 lanes all run ONE point (the tail of a sweep,
 // when the spread worklist leaves one live point per wave): every lane executes the identical
 // chain, and AW_{n−1}'s knots are held across the wave — lane L holds knot wb + L (time and
@@ -795,10 +615,7 @@ struct SocialRhsRing {
 // a prefix: the bracket is wb + popcount − 1) and four v_readlanes, instead of waiting on an
 // L2/HBM round trip per step.  The window moves forward by 32 knots when the step's time passes
 // its middle (one coalesced load per array); lookups outside it fall back to the global search.
-// Same brackets, same operands, same operations as SocialRhs: bit-identical.
-#ifndef SBR_SOCIAL_COOP_PIN
-#define SBR_SOCIAL_COOP_PIN 1 // one-point waves hold the Tsit5 tableau in VGPRs (Tsit5Regs; ODE 3,077 -> 2,876 cycles per RK step, r05_r)
-#endif
+// Same brackets, same operands, same operations as SocialRhsRing: bit-identical.
 struct SocialRhsCoop {
     double beta;
     BView to;
@@ -883,8 +700,7 @@ struct SocialRhsCoop {
     __device__ __forceinline__ void prepare(double t, double dt)
     {
         const double xs[5] = {fma(C1, dt, t), fma(C2, dt, t), fma(C3, dt, t), fma(C4, dt, t), t + dt};
-#if SBR_SOCIAL_PAR_STAGES
-        // The five stage lookups side by side (SBR_SOCIAL_PAR_STAGES): the stage times depend on
+        // The five stage lookups side by side (1): the stage times depend on
         // t and dt only, so their brackets are five ballots over the window, and lane k runs stage
         // k's lerp — the same operands and operations as lerp_j, hence the same bits — on the
         // window knots it fetches with ds_bpermute; the five values come back by readlane.  One
@@ -922,7 +738,6 @@ struct SocialRhsCoop {
                 slow++;
             }
         }
-#endif
 #pragma unroll
         for (int k = 0; k < 5; k++) {
             const bool in = n >= 2 && xs[k] >= tfirst && xs[k] <= tlast;
@@ -962,8 +777,8 @@ struct SocialRhsCoop {
         }
     }
     static constexpr bool kFsalExact = false;
-    static constexpr bool kPinTableau = SBR_SOCIAL_COOP_PIN != 0;
-    static constexpr bool kAcceptFirst = SBR_SOCIAL_ACCEPT_FIRST != 0; // the refill's loads ahead of the knot stores
+    static constexpr bool kPinTableau = true;
+    static constexpr bool kAcceptFirst = true; // the refill's loads ahead of the knot stores
 };
 
 }  // namespace
@@ -1075,8 +890,8 @@ __device__ __forceinline__ bool social_iterate(const SocialArgs& a, int l, int i
     stamp(0);
     // ---- (a) learning from withdrawals on (0, η) ----
     typename std::conditional<COOP, SocialRhsCoop,
-                              typename std::conditional<SBR_SOCIAL_RING != 0, SocialRhsRing, SocialRhs>::type>::type f;
-    if constexpr (!COOP && SBR_SOCIAL_RING != 0) f.init(BETA, TO, VO, n_old, ring);
+                              SocialRhsRing>::type f;
+    if constexpr (!COOP) f.init(BETA, TO, VO, n_old, ring);
     else { (void)ring; f.init(BETA, TO, VO, n_old); }
     int n = 0;
     bool overflow = false;
@@ -1157,7 +972,7 @@ __device__ __forceinline__ bool social_iterate(const SocialArgs& a, int l, int i
             if constexpr (COOP) {
                 coop_hazard_scan(T, Gv, AWO, X, VO, n, BETA, lam, p, U, ETA, any, all, first_above, last_above, tin_c,
                                  tout_c);
-            } else if constexpr (SBR_SOCIAL_PAIRS != 0) {
+            } else {
                 // the two passes below on knot pairs (same fold, same order): pass A
                 double I = 0.0, eprev = 0.0, tprev = 0.0;
                 for (int i = 0; i < n; i += 2) { // i <= (n−1) & ~1: the pair holds knot i
@@ -1208,51 +1023,6 @@ __device__ __forceinline__ bool social_iterate(const SocialArgs& a, int l, int i
                         hr_prev = hr;
                         tprev = ti;
                     }
-                }
-            } else {
-                // pass A: ∫ trapezoid to η
-                double I = 0.0;
-                double ex = sbr_exp(lam * T[0]);
-                X[0] = ex;
-                double eprev = ex * (((1.0 - Gv[0]) * BETA) * AWO[0]);
-#pragma unroll SBR_SOCIAL_UNROLL
-                for (int i = 1; i < n; i++) {
-                    ex = sbr_exp(lam * T[i]);
-                    X[i] = ex;
-                    const double ei = ex * (((1.0 - Gv[i]) * BETA) * AWO[i]);
-                    I = I + (0.5 * (eprev + ei)) * (T[i] - T[i - 1]);
-                    eprev = ei;
-                }
-                const double Ieta = I;
-                // pass B: HR and optimal_buffer's crossing scan (solver.jl:211-264), streamed
-                I = 0.0;
-                double pdf = ((1.0 - Gv[0]) * BETA) * AWO[0];
-                eprev = X[0] * pdf;
-                double hr_prev = ((p * X[0]) * pdf) / ((p * I) + (omp * Ieta));
-                double tprev = T[0];
-                {
-                    const bool ab = hr_prev > U;
-                    any |= ab; all &= ab;
-                    if (ab) { first_above = 0; last_above = 0; }
-                }
-#pragma unroll SBR_SOCIAL_UNROLL
-                for (int i = 1; i < n; i++) {
-                    pdf = ((1.0 - Gv[i]) * BETA) * AWO[i];
-                    const double ei = X[i] * pdf;
-                    const double ti = T[i];
-                    I = I + (0.5 * (eprev + ei)) * (ti - tprev);
-                    eprev = ei;
-                    const double hr = ((p * X[i]) * pdf) / ((p * I) + (omp * Ieta));
-                    const bool ab = hr > U, abp = hr_prev > U;
-                    any |= ab; all &= ab;
-                    if (ab) { if (first_above < 0) first_above = i; last_above = i; }
-                    if (!have_in && !abp && ab) {
-                        tin_c = tprev + ((U - hr_prev) * (ti - tprev)) / (hr - hr_prev);
-                        have_in = true;
-                    }
-                    if (abp && !ab) tout_c = tprev + ((U - hr_prev) * (ti - tprev)) / (hr - hr_prev);
-                    hr_prev = hr;
-                    tprev = ti;
                 }
             }
             if (!any) { tin = ETA; tout = ETA; }
@@ -1372,7 +1142,7 @@ __device__ __forceinline__ bool social_iterate(const SocialArgs& a, int l, int i
                     // knot i is aw_i·(1−0) + aw_{i+1}·0 (i < n−1), aw_{n−2}·0 + aw_{n−1}·1
                     if constexpr (COOP) {
                         coop_damping(T, Gv, AWO, n, XI, ic, oc, G0, aoob);
-                    } else if constexpr (SBR_SOCIAL_PAIRS != 0) {
+                    } else {
                         // the same loop two knots at a time: AWO and the τ grid move in 16-byte pairs
                         WalkerV da, db;
                         da.init(T, Gv, n); db.init(T, Gv, n);
@@ -1404,21 +1174,6 @@ __device__ __forceinline__ bool social_iterate(const SocialArgs& a, int l, int i
                             aw_i = aw_1;
                             tp = tq;
                         }
-                    } else {
-                        Walker da, db;
-                        da.init(T, Gv, n); db.init(T, Gv, n);
-                        double aw_i = aw_at(T[0], da, db);
-#pragma unroll SBR_SOCIAL_UNROLL
-                        for (int i = 0; i < n - 1; i++) {
-                            const double aw_n = aw_at(T[i + 1], da, db);
-                            const double vn = aw_i * (1.0 - 0.0) + aw_n * 0.0;
-                            AWO[i] = 0.5 * AWO[i] + 0.5 * vn;
-                            if (i == n - 2) {
-                                const double vl = aw_i * (1.0 - 1.0) + aw_n * 1.0;
-                                AWO[n - 1] = 0.5 * AWO[n - 1] + 0.5 * vl;
-                            }
-                            aw_i = aw_n;
-                        }
                     }
                     if (aoob) { finish = true; stop_oob = true; }
                     else if (iter >= a.max_iter) { finish = true; need_awmax = (st_r & SBR_RUN) != 0; }
@@ -1434,7 +1189,7 @@ __device__ __forceinline__ bool social_iterate(const SocialArgs& a, int l, int i
         const double oc = (tout > XI) ? XI : tout;
         bool aoob = false;
         const double G0 = interp_full(T, Gv, n, 0.0, aoob);
-        typename std::conditional<SBR_SOCIAL_PAIRS != 0, WalkerV, Walker>::type A, B;
+        WalkerV A, B;
         A.init(T, Gv, n); B.init(T, Gv, n);
         double mx = -(double)INFINITY;
         for (int i = 0; i < n; i++) {
@@ -1516,24 +1271,17 @@ __device__ __forceinline__ bool social_iterate(const SocialArgs& a, int l, int i
 // picked up here or by the next launch; either way it redoes that iterate).
 // args[0]: the main worklist's arguments, args[1]: the pool's (n_pts = 0: none),
 // in device memory so that the wave-uniform choice between them stays scalar loads.
-static_assert(!SBR_SOCIAL_RING || kRingLanes == 64 || SBR_SOCIAL_COOP,
-              "a ring narrower than the wave needs the one-point-per-wave pool path");
-#ifndef SBR_SOCIAL_WAVES
-#define SBR_SOCIAL_WAVES 1024 // one wave per SIMD (A/B: 2048 with SBR_SOCIAL_MINW 2; 0 = dense waves, the round-1 layout)
-#endif
-static_assert(SBR_SOCIAL_WAVES != 0 || !SBR_SOCIAL_RING || kRingLanes == 64, "dense waves use all 64 lanes of the ring");
-#ifndef SBR_SOCIAL_COOP_MAX
+constexpr int kSocialWaves = 1024; // one wave per SIMD (2048 waves, two per SIMD, were slower: r04_u)
 // live points up to which every point gets a whole wave (SocialRhsCoop), in rounds of the
-// SBR_SOCIAL_WAVES resident ones, instead of ⌈live/SBR_SOCIAL_WAVES⌉ points per wave
-#define SBR_SOCIAL_COOP_MAX 4096
-#endif
+// kSocialWaves resident ones, instead of ⌈live/kSocialWaves⌉ points per wave
+constexpr int kSocialCoopMax = 4096;
 // Main blocks (one wave each) spread the live worklist over all `nbs` of them: L = ⌈live/nbs⌉
 // consecutive entries per wave (L ≤ 64), lanes ≥ L idle.  A fixed-point lane's RK step is a
 // serial chain whose memory side grows with the wave's active lanes (each lane streams its own
 // knot lines: a wave load touches one line per active lane), so as points retire the
 // survivors run in ever sparser waves, down to one per wave — and with nbs = one wave per
 // SIMD the bulk uses every SIMD instead of half of them.
-__global__ __launch_bounds__(64, SBR_SOCIAL_MINW) void social_iter_kernel(const SocialArgs* __restrict__ args, int iter_arg,
+__global__ __launch_bounds__(64, 1) void social_iter_kernel(const SocialArgs* __restrict__ args, int iter_arg,
                                                          int n_inner, const int32_t* __restrict__ work,
                                                          const int32_t* __restrict__ count, int nbs, int nmain)
 {
@@ -1545,13 +1293,12 @@ __global__ __launch_bounds__(64, SBR_SOCIAL_MINW) void social_iter_kernel(const 
     if (!in_pool) {
         const int cnt = *count;
         // at most nmain live points: one per wave (coop), beyond that the first nbs waves
-        int L = SBR_SOCIAL_WAVES ? (cnt <= nmain ? 1 : (cnt + nbs - 1) / nbs) : 64;
+        int L = cnt <= nmain ? 1 : (cnt + nbs - 1) / nbs;
         // the ring holds kRingLanes lanes: the host's nbs = ⌈n_pts / kRingLanes⌉ >= ⌈cnt / kRingLanes⌉
         // keeps L within it; the clamp stops a future change of that arithmetic from letting lanes
         // share ring slots (which in_ring() would trust)
-        constexpr int kLmax = SBR_SOCIAL_RING ? kRingLanes : 64;
+        constexpr int kLmax = kRingLanes;
         L = L < 1 ? 1 : (L > kLmax ? kLmax : L);
-#if SBR_SOCIAL_COOP
         if (L == 1) { // one point per wave: the whole wave runs it
             const int w = blockIdx.x;
             if (w >= cnt) return;
@@ -1561,7 +1308,6 @@ __global__ __launch_bounds__(64, SBR_SOCIAL_MINW) void social_iter_kernel(const 
                 if (!social_iterate<true>(sa, l, iter_arg + k, s_ring)) break;
             return;
         }
-#endif
         if ((int)threadIdx.x >= L || (int)blockIdx.x >= nbs) return;
         const int w = blockIdx.x * L + threadIdx.x;
         if (w >= cnt) return;
@@ -1569,7 +1315,6 @@ __global__ __launch_bounds__(64, SBR_SOCIAL_MINW) void social_iter_kernel(const 
         if (!sa.live[l]) return; // retired by the init kernel (knot overflow)
         iter = iter_arg;
     } else {
-#if SBR_SOCIAL_COOP
         // one pool slot per wave, run by the whole wave (the pool holds the longest fixed
         // points — the ones whose iterates outgrew the main capacity)
         l = (int)blockIdx.x - nmain;
@@ -1580,13 +1325,6 @@ __global__ __launch_bounds__(64, SBR_SOCIAL_MINW) void social_iter_kernel(const 
         for (int k = 0; k < n_inner; k++)
             if (!social_iterate<true>(pa, l, iter + k, s_ring)) break;
         return;
-#else
-        l = ((int)blockIdx.x - nmain) * 64 + threadIdx.x;
-        if (l >= pa.n_pts) return;
-        if (__hip_atomic_load(pa.ready + l, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
-        if (!pa.live[l]) return;
-        iter = pa.it_cur[l];
-#endif
     }
     const SocialArgs& a = args[in_pool ? 1 : 0];
     for (int k = 0; k < n_inner; k++)
@@ -1649,13 +1387,13 @@ hipError_t launch_social_iter(const SocialArgs& a, const SocialArgs& p, const So
     // main blocks: one wave per SIMD of the MI355X (4 × 256), at least one wave per 64 points
     // and no more than one per point
     int nbs = (a.n_pts + kRingLanes - 1) / kRingLanes; // L = ⌈live / nbs⌉ <= kRingLanes (the ring's lanes)
-    nbs = nbs > SBR_SOCIAL_WAVES ? nbs : SBR_SOCIAL_WAVES;
+    nbs = nbs > kSocialWaves ? nbs : kSocialWaves;
     nbs = nbs < a.n_pts ? nbs : (a.n_pts > 0 ? a.n_pts : 1);
-    const int pool_waves = SBR_SOCIAL_COOP ? p.n_pts : (p.n_pts + 63) / 64;
-    // main blocks: nbs multi-point waves, or up to SBR_SOCIAL_COOP_MAX one-point waves
-    const int coop_max = (SBR_SOCIAL_COOP) && (SBR_SOCIAL_WAVES != 0) ? (SBR_SOCIAL_COOP_MAX < a.n_pts ? SBR_SOCIAL_COOP_MAX : a.n_pts) : 0;
+    const int pool_waves = p.n_pts;
+    // main blocks: nbs multi-point waves, or up to kSocialCoopMax one-point waves
+    const int coop_max = kSocialCoopMax < a.n_pts ? kSocialCoopMax : a.n_pts;
     const int nmain = nbs > coop_max ? nbs : coop_max;
-    hipLaunchKernelGGL(social_iter_kernel, dim3(nmain + pool_waves), dim3(64), SBR_SOCIAL_RING ? kRingLdsBytes : 0, s,
+    hipLaunchKernelGGL(social_iter_kernel, dim3(nmain + pool_waves), dim3(64), kRingLdsBytes, s,
                        args_dev, iter, n_inner, work, count, nbs, nmain);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;

@@ -72,9 +72,10 @@ end
 # learning.jl:109-124
 function solve_learning(learning_params::LearningParameters; tol = nothing)
     solve_start = time()
-    (tol === nothing || tol == eps()) || throw(ArgumentError("the engine integrates at reltol = abstol = eps()"))
     learning_params.tspan[1] == 0 || throw(ArgumentError("the engine integrates from t = 0"))
-    t, G, _ = SBREngine.learn(sbr_context(), learning_params.β, learning_params.tspan[2], learning_params.x0)
+    # solve_SIhomogeneous(…; tol): reltol = abstol = tol, eps() when nothing (learning.jl:41-51)
+    t, G, _ = SBREngine.learn(sbr_context(), learning_params.β, learning_params.tspan[2], learning_params.x0;
+                              tol = tol === nothing ? eps() : tol)
     cdf = LinearInterpolation(t, G)
     pdf = compute_pdf_symbolic_baseline(learning_params.β, cdf, t)
     return LearningResults(learning_params, cdf, pdf, t, time() - solve_start, nothing)

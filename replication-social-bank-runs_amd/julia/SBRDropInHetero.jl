@@ -46,9 +46,9 @@ end
 # heterogeneity_learning.jl:49-94
 function solve_SInetwork_hetero(params::LearningParametersHetero; tol = eps())
     solve_start = time()
-    tol == eps() || throw(ArgumentError("the engine integrates at reltol = abstol = eps()"))
     params.tspan[1] == 0 || throw(ArgumentError("the engine integrates from t = 0"))
-    t, Gm, _ = SBREngine.learn_hetero(sbr_context(), params.βs, params.dist, params.tspan[2], params.x0)
+    # reltol = abstol = tol (heterogeneity_learning.jl:74)
+    t, Gm, _ = SBREngine.learn_hetero(sbr_context(), params.βs, params.dist, params.tspan[2], params.x0; tol)
     cdfs = Any[LinearInterpolation(t, Gm[:, k]) for k in eachindex(params.βs)]
     pdfs = compute_pdf_hetero(params.βs, params.dist, cdfs, t)
     return LearningResultsHetero(params, cdfs, pdfs, t, time() - solve_start, nothing)

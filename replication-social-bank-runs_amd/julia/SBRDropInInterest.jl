@@ -32,7 +32,8 @@ using Interpolations
 function solve_equilibrium_interest(lr::LearningResults, econ::EconomicParametersInterest,
                                     model::ModelParametersInterest; ξ_guess = nothing, verbose = false)
     solve_start = time()
-    ξ_guess === nothing || throw(ArgumentError("the engine starts the bisection at the reference's default midpoint"))
+    # ξ_guess is accepted and, as in the reference, not used: interest_rate_solver.jl:113 calls
+    # compute_ξ(τ̄_IN, τ̄_OUT, learning_cdf, κ; verbose) without it — the bisection starts at the midpoint
     lp = lr.params
     r = SBREngine.solve_interest_point_paths(sbr_context(), lp.β, econ.u; r = econ.r, δ = econ.δ, η = econ.η,
                                              tspan_end = lp.tspan[2], x0 = lp.x0, p = econ.p, κ = econ.κ, λ = econ.λ)

@@ -34,9 +34,12 @@ struct Opts            # sbr_opts
     xi_guess::Float64
 end
 # pad = social knot capacity per buffer (0: library default 98304); xi_guess = compute_ξ's first
-# iterate (NaN: the reference's midpoint; equilibrium_on_knots only)
-Opts(; early_exit = 5, xi_guess = NaN) = Opts(eps(), eps(), 1_000_000, 100, early_exit, 65536, 500, 0, 0,
-                                              Float64(xi_guess))
+# iterate (NaN: the reference's midpoint; equilibrium_on_knots only), flagged by SBR_FLAG_XI_GUESS
+const SBR_FLAG_XI_GUESS = Int32(0x8)
+# tol = the learning ODE's reltol = abstol (solve_learning(lp; tol), learning.jl:43,109; eps() by default)
+Opts(; early_exit = 5, xi_guess = NaN, tol = eps()) =
+    Opts(Float64(tol), Float64(tol), 1_000_000, 100, early_exit, 65536, 500,
+         isnan(xi_guess) ? Int32(0) : SBR_FLAG_XI_GUESS, 0, Float64(xi_guess))
 
 struct ResultSoA       # sbr_result_soa
     xi::Ptr{Float64}
@@ -114,10 +117,10 @@ end
 `solve_SIhomogeneous` (learning.jl:41-54) on the GPU: the knot grid `t` and CDF values `G`
 of the adaptive AutoTsit5(Rosenbrock23()) solution on (0, tspan_end), and the status bits.
 """
-function learn(ctx::Context, β, tspan_end, x0; cap = 1 << 16)
+function learn(ctx::Context, β, tspan_end, x0; cap = 1 << 16, tol = eps())
     t = Vector{Float64}(undef, cap); G = similar(t); nk = Ref{Int32}(0); st = Ref{UInt32}(0)
     b = Float64[β]; e = Float64[tspan_end]; te = Float64[tspan_end]
-    opts = Ref(Opts(; early_exit = 0))
+    opts = Ref(Opts(; early_exit = 0, tol))
     GC.@preserve t G b e te begin
         rc = ccall((:sbr_learn_baseline, libsbr), Cint,
                    (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Float64, Int64, Int32, Ref{Opts},
@@ -354,11 +357,11 @@ end
 `t` and the group CDFs `G` (n × K) of the coupled AutoTsit5(Rosenbrock23()) solve at eps()
 on (0, tspan_end), and the status bits.
 """
-function learn_hetero(ctx::Context, βs, dist, tspan_end, x0; cap = 1 << 14)
+function learn_hetero(ctx::Context, βs, dist, tspan_end, x0; cap = 1 << 14, tol = eps())
     b = collect(Float64, βs); d = collect(Float64, dist); K = length(d)
     t = Vector{Float64}(undef, cap); G = Vector{Float64}(undef, cap * K)
     nk = Ref{Int32}(0); st = Ref{UInt32}(0); te = Float64[tspan_end]
-    opts = Ref(Opts(; early_exit = 0))
+    opts = Ref(Opts(; early_exit = 0, tol))
     GC.@preserve b d t G te begin
         rc = ccall((:sbr_learn_hetero, libsbr), Cint,
                    (Ptr{Cvoid}, Int32, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Float64, Int64, Ref{Opts},

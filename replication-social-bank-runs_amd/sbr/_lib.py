@@ -25,6 +25,7 @@ SBR_OK, SBR_EARG, SBR_EDEVICE, SBR_ENOMEM = 0, -1, -2, -3
 SBR_FLAG_EXHAUSTIVE = 0x1
 SBR_FLAG_READY_SWEEP = 0x2
 SBR_FLAG_RCCL_GATHER = 0x4
+SBR_FLAG_XI_GUESS = 0x8
 SBR_FLAG_DIAG_STOP_AFTER_BUFFER = 0x100
 SBR_FLAG_DIAG_STOP_AFTER_BISECT = 0x200
 SBR_FLAG_DIAG_COUNT_AW_BLOCKS = 0x400
@@ -89,6 +90,8 @@ _SIGS = {
     "sbr_sweep_baseline_batch_dev": (ctypes.c_int, [_P, _P, _I64, _P, _P, _P, _D, _P, _I64, _I64, _D, _D, _D, _P,
                                                     _P]),
     "sbr_batch_wait": (ctypes.c_int, [_P, _P, _I64]),
+    "sbr_batch_reserve": (ctypes.c_int, [_P, _I64, _I64, _P]),
+    "sbr_set_batch_workspace": (ctypes.c_int, [_P, _I64]),
     "sbr_learn_baseline": (ctypes.c_int, [_P, _P, _P, _P, _D, _I64, _I32, _P, _P, _P, _I64, _P, _P]),
     "sbr_solve_point_paths": (ctypes.c_int, [_P, _D, _D, _D, _D, _D, _D, _D, _D, _P, _P, _P, _P, _P, _P, _I64, _P]),
     "sbr_equilibrium_on_knots": (ctypes.c_int, [_P, _P, _P, _I64, _D, _D, _D, _P, _I64, _D, _D, _D, _P, _P, _P, _P,
@@ -151,7 +154,11 @@ def load() -> ctypes.CDLL:
             "there is no CPU fallback")
     L = ctypes.CDLL(str(LIB_PATH))
     for name, (res, args) in _SIGS.items():
-        fn = getattr(L, name)
+        # an older libsbr.so loaded for an A/B (SBR_LIB) may lack a newer entry point: calling it
+        # then raises AttributeError; tests/test_capi.py asserts the built library exports them all
+        fn = getattr(L, name, None)
+        if fn is None:
+            continue
         fn.restype = res
         fn.argtypes = args
     _lib = L

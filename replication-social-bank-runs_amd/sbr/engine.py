@@ -200,12 +200,24 @@ class Engine:
                                                   ctypes.byref(opts), ctypes.byref(soa))
         check(rc, self._ctx, "sbr_sweep_baseline_batch_dev")
 
+    def batch_reserve(self, n_batch: int, n_beta: int, knot_capacity: int = 65536):
+        """Allocate now the workspaces a later ``sweep_baseline_batch_dev`` of ``n_batch`` grids of
+        ``n_beta`` columns uses (sbr_batch_reserve): the batch call then allocates nothing."""
+        opts = _lib.default_opts(knot_capacity=knot_capacity)
+        check(self._L.sbr_batch_reserve(self._ctx, int(n_batch), int(n_beta), ctypes.byref(opts)), self._ctx,
+              "sbr_batch_reserve")
+
+    def set_batch_workspace(self, nbytes: int):
+        """Budget in bytes for the baseline batch's learning workspaces (0 = the default, 40 % of
+        free HBM); it caps the grids learned per launch (sbr_set_batch_workspace)."""
+        check(self._L.sbr_set_batch_workspace(self._ctx, int(nbytes)), self._ctx, "sbr_set_batch_workspace")
+
     def batch_wait(self, stream: int | None, k: int):
         """Make ``stream`` wait until grid ``k`` of the last batch call has its results
         (sbr_batch_wait): ship grid k while the rest of the batch is still being swept."""
         check(self._L.sbr_batch_wait(self._ctx, stream, int(k)), self._ctx, "sbr_batch_wait")
 
-    def learn_baseline(self, beta, eta, t_end, x0=1e-4, stop_after_eta=False, cap=65536):
+    def learn_baseline(self, beta, eta, t_end, x0=1e-4, stop_after_eta=False, cap=65536, tol=None):
         beta = np.ascontiguousarray(beta, np.float64)
         nb = len(beta)
         eta = np.ascontiguousarray(np.broadcast_to(eta, beta.shape), np.float64)
@@ -215,6 +227,8 @@ class Engine:
         nk = np.zeros(nb, np.int32)
         st = np.zeros(nb, np.uint32)
         opts = _lib.default_opts(knot_capacity=cap)
+        if tol is not None:  # solve_SIhomogeneous(…; tol): reltol = abstol = tol (learning.jl:41-51)
+            opts.ode_reltol = opts.ode_abstol = float(tol)
         rc = self._L.sbr_learn_baseline(self._ctx, _ptr(beta), _ptr(eta), _ptr(t_end), x0, nb, int(stop_after_eta),
                                         ctypes.byref(opts), _ptr(T), _ptr(G), cap, _ptr(nk), _ptr(st))
         check(rc, self._ctx, "sbr_learn_baseline")
@@ -268,7 +282,9 @@ class Engine:
             if len(self._knot_opts) > 64:  # per-call guesses: keep the cache bounded
                 self._knot_opts = {}
             opts = self._knot_opts[key] = _lib.default_opts(
-                bisect_max_iters=max_iters, flags=_lib.SBR_FLAG_EXHAUSTIVE if exhaustive else 0,
+                bisect_max_iters=max_iters,
+                flags=(_lib.SBR_FLAG_EXHAUSTIVE if exhaustive else 0)
+                | (_lib.SBR_FLAG_XI_GUESS if xi_guess is not None else 0),
                 xi_guess=float("nan") if xi_guess is None else float(xi_guess))
         cap = n + 1
         nt = ctypes.c_int64()
@@ -720,12 +736,13 @@ class SolvedModel:
         return max(self.xi - self.tau_bar_OUT_UNC, 0.0) if self.xi == self.xi else float("nan")
 
 
-def solve_learning(lp: LearningParameters, engine: Engine | None = None) -> LearningResults:
-    """learning.jl:109-124 on the GPU (full tspan, like the reference)."""
+def solve_learning(lp: LearningParameters, engine: Engine | None = None, tol: float | None = None) -> LearningResults:
+    """learning.jl:109-124 on the GPU (full tspan, like the reference); ``tol`` = the ODE's
+    reltol = abstol (None: eps(), learning.jl:43)."""
     if lp.tspan[0] != 0.0:
         raise _lib.ArgumentError("the engine integrates from t = 0 (every reference call site does)")
     eng = engine or default_engine()
-    (t, G, st), = eng.learn_baseline([lp.beta], [lp.tspan[1]], [lp.tspan[1]], lp.x0, stop_after_eta=False)
+    (t, G, st), = eng.learn_baseline([lp.beta], [lp.tspan[1]], [lp.tspan[1]], lp.x0, stop_after_eta=False, tol=tol)
     g = (lp.beta * G) * (1.0 - G)
     return LearningResults(lp, LinearInterpolation(t, G), LinearInterpolation(t, g), t, st)
 

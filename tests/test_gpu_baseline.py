@@ -62,6 +62,19 @@ def test_learning_knots_bitwise(engine, oracle, stop):
         assert_bitwise(G, Go[: len(t)], f"G β={b}")
 
 
+@pytest.mark.parametrize("tol", [1e-10, 1e-6])
+def test_learning_tol_bitwise(engine, oracle, tol):
+    """solve_learning(lp; tol) (learning.jl:109, reltol = abstol = tol in solve_SIhomogeneous
+    :41-51): the drop-ins pass the keyword through (julia/SBRDropIn.jl), and the device knots at a
+    looser tolerance equal the oracle's, knot for knot."""
+    for b in (0.5, 1.0, 3.0, 61.654026637430945):
+        lr = sbr.solve_learning(sbr.LearningParameters(b, (0.0, 30.0), 1e-4), engine, tol=tol)
+        to, Go, _ = oracle.learn_logistic(float(b), 30.0, rtol=tol, atol=tol)
+        assert len(lr.grid) == len(to)
+        assert_bitwise(lr.grid, to, f"t β={b}")
+        assert_bitwise(lr.learning_cdf.coefs, Go, f"G β={b}")
+
+
 def _oracle_sweep(oracle, grid):
     return oracle.sweep_baseline(grid.beta, grid.eta, grid.t_end, grid.u, grid.p, grid.kappa, grid.lam, grid.x0)
 
@@ -230,15 +243,19 @@ def test_device_info(engine):
     assert info["lds_knot_capacity"] >= 3400  # every config-3 column staged in LDS
 
 
-@pytest.mark.parametrize("ncol", [384, 1200])
-def test_pipelined_batches_equal_single_sweeps(engine, ncol):
-    """sbr_sweep_baseline_batch_dev (learning of batch k+1 overlapping the
-    equilibrium of batch k on two streams, alternating workspaces) returns for
-    every batch exactly what a single sweep of that grid returns.  Grids narrower than
-    2048 columns share learning and equilibrium launches: 384 columns, 6 grids per launch
-    (11 grids: groups of 6 and 5); 1200 columns, 2 per launch (6 groups, more than the 4
-    learning workspaces, so each is reused; the last group holds one grid)."""
+@pytest.mark.parametrize("ncol,group", [(384, None), (1200, None), (384, 3), (1200, 2)])
+def test_pipelined_batches_equal_single_sweeps(engine, ncol, group):
+    """sbr_sweep_baseline_batch_dev returns for every batch exactly what a single sweep of that
+    grid returns.  By default the 11 grids are learned in one launch (≤ one wave per SIMD) and
+    solved by equilibrium launches of ⌈4096 / n_β⌉ grids (384 columns: 11 grids in one launch;
+    1200: three launches of 4, 4, 3).  With a workspace budget of `group` grids per learning
+    launch (sbr_set_batch_workspace) the batch runs in groups — 384: four groups of 3, 3, 3, 2;
+    1200: six of 2, ..., 1 — learned into two alternating workspaces, each group beside the
+    previous group's equilibria, so each workspace is reused behind its readers."""
     torch = pytest.importorskip("torch")
+    if group is not None:
+        # two workspaces of `group` grids: n_β × (4 × cap × 8 + 24) bytes per grid
+        engine.set_batch_workspace(2 * group * ncol * (4 * 65536 * 8 + 24) + 4096)
     dev = torch.device("cuda", 0)
     base = sbr.fig5_grid(ncol, n_u=384)
     betas = np.stack([base.beta, base.beta[::-1], base.beta * 0.5, base.beta])
@@ -286,6 +303,43 @@ def test_pipelined_batches_equal_single_sweeps(engine, ncol):
         st = out["status"][k].cpu().numpy().view(np.uint32).reshape(nb, nu)
         assert np.array_equal(st, ref["status"])
         assert np.array_equal(out["iters"][k].cpu().numpy().reshape(nb, nu), ref["iters"])
+    engine.set_batch_workspace(0)
+
+
+def test_batch_workspace_allocation_falls_back(engine):
+    """A batch whose planned workspace does not fit the device (budget lifted, a 20M-knot
+    capacity: 41 GB per 64-column grid, 8 grids planned into one 328 GB workspace) halves its
+    learning group until the allocation succeeds — here two workspaces of two
+    grids — and still returns every grid exactly as single sweeps do.  sbr_batch_reserve takes
+    the same path.  Own context: the 164 GB are released at the end."""
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda", 0)
+    cap = 20_000_000
+    base = sbr.fig5_grid(64, n_u=64)
+    nbat = 8
+    betas = np.stack([base.beta * (1.0 + 0.03 * k) for k in range(nbat)])
+    eta = np.full((nbat, 64), 15.0)
+    tend = np.full((nbat, 64), 30.0)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    out = {f: torch.empty(nbat, 64 * 64, dtype=torch.float64, device=dev) for f in FIELDS}
+    out["status"] = torch.empty(nbat, 64 * 64, dtype=torch.int32, device=dev)
+    out["iters"] = torch.empty(nbat, 64 * 64, dtype=torch.int32, device=dev)
+    eng = sbr.Engine(0)
+    try:
+        eng.set_batch_workspace(1 << 50)
+        eng.batch_reserve(nbat, 64, knot_capacity=cap)
+        eng.sweep_baseline_batch_dev(t(betas), t(eta), t(tend), t(base.u), base.p, base.kappa, base.lam, base.x0,
+                                     out, knot_capacity=cap)
+        torch.cuda.synchronize(dev)
+    finally:
+        eng.close()
+    for k in (0, 3, nbat - 1):
+        g = sbr.BaselineGrid(betas[k], base.u, eta[k], tend[k], x0=base.x0, p=base.p, kappa=base.kappa,
+                             lam=base.lam)
+        ref = engine.sweep_baseline(g)
+        for f in FIELDS:
+            assert_bitwise(out[f][k].cpu().numpy().reshape(64, 64), ref[f], f"batch {k} {f}")
+        assert np.array_equal(out["status"][k].cpu().numpy().view(np.uint32).reshape(64, 64), ref["status"])
 
 
 @pytest.mark.parametrize("n_u", [50, 9000])

@@ -77,9 +77,19 @@ def test_sweeps_refuse_a_guess(engine):
     out = {k: np.empty(nb * nu) for k in FIELDS}
     out["status"] = np.empty(nb * nu, np.uint32)
     soa = _lib.ResultSoA(*[out[k].ctypes.data_as(ctypes.c_void_p) for k in (*FIELDS, "status")], None)
-    opts = _lib.default_opts(xi_guess=5.0)
+    opts = _lib.default_opts(xi_guess=5.0, flags=_lib.SBR_FLAG_XI_GUESS)
     P_ = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
     rc = L.sbr_sweep_baseline(engine._ctx, P_(g.beta), P_(g.eta), P_(g.t_end), g.x0, P_(g.u), nb, nu, g.p, g.kappa,
                               g.lam, ctypes.byref(opts), ctypes.byref(soa))
     assert rc == _lib.SBR_EARG and b"xi_guess" in L.sbr_last_error(engine._ctx)
     assert np.isnan(_lib.default_opts().xi_guess)
+    # xi_guess is read only with SBR_FLAG_XI_GUESS: a zero-filled sbr_opts — what a
+    # caller built against the round-4 header, or a memset, passes — sweeps with the defaults
+    zero = _lib.Opts()
+    rc = L.sbr_sweep_baseline(engine._ctx, P_(g.beta), P_(g.eta), P_(g.t_end), g.x0, P_(g.u), nb, nu, g.p, g.kappa,
+                              g.lam, ctypes.byref(zero), ctypes.byref(soa))
+    assert rc == _lib.SBR_OK
+    ref = engine.sweep_baseline(g)
+    for k in FIELDS:
+        a, b = out[k].reshape(nb, nu), ref[k]
+        assert np.array_equal(a.view(np.int64), b.view(np.int64)), k
