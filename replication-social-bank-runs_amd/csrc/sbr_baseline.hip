@@ -44,12 +44,24 @@ __device__ __forceinline__ void publish_column(const LearnArgs& a, int b)
 }
 // one lane's knot-row store of the learning kernel (the nontemporal hint was neutral, r05_ee)
 #define st_knot(p, v) (*(p) = (v))
-template <int LB>
+// STAGE (a batch's wide learning launch, the chip otherwise idle; fused hazard): the knot rows
+// (t, G) and the hazard rows (numerator, running integral) go through a per-lane ring of
+// kStageSlots slots in LDS, [array][slot][lane], and leave as whole 128-B lines — eight 16-B
+// stores per array — on every 8th attempted step (the same step for every live lane), the rest
+// when the lane's solve ends.  With hundreds of learning waves the direct 8-B knot stores (one
+// line per lane per store instruction) made the launch twice the chain alone
+// (tools/ubench_wide.hip: 640 waves 3.74 ms without stores, 6.48 direct, 4.43 staged).  Between
+// two flushes a lane accepts at most 8 knots and holds fewer than 16 unflushed after one, so 24
+// slots never overwrite an unflushed entry; 48 KiB per wave lets three waves share a CU.
+constexpr int kStageSlots = 24;
+constexpr size_t kStageLdsPerWave = (size_t)4 * kStageSlots * 64 * sizeof(double); // 48 KiB
+template <int LB, bool STAGE = false>
 __global__ __launch_bounds__(LB) void learn_logistic_kernel(const double* __restrict__ beta,
                                                             const double* __restrict__ eta,
                                                             const double* __restrict__ t_end, LearnArgs a,
                                                             LearnBufs L)
 {
+    extern __shared__ double stage_lds[];
     // latency-bound (one serial ODE per lane): take issue priority over co-resident
     // equilibrium waves of a previous batch
     __builtin_amdgcn_s_setprio(3);
@@ -81,6 +93,9 @@ __global__ __launch_bounds__(LB) void learn_logistic_kernel(const double* __rest
         double* __restrict__ Gv;
         double* __restrict__ H;
         double* __restrict__ HI;
+        double* SL;       // STAGE: this lane's ring, slot k of array a at SL[(a·kStageSlots + k)·64]
+        int fl, tick;     // STAGE: entries flushed (a multiple of 16), attempted steps
+        int ws, fs;       // STAGE: the ring slots of entry n and of entry fl
         int n, cap, m; // m: knots ≤ η (the hazard stage's τ̄ prefix), set at the first knot past η
         double tlast, bound, eta;
         int past, done, stop_after_eta; // 0 / 1 (ints: loop-carried bools cost mask conversions)
@@ -92,7 +107,11 @@ __global__ __launch_bounds__(LB) void learn_logistic_kernel(const double* __rest
         {
             const bool room = n < cap;
             const int w = room ? n : cap - 1;
-            if (room) { st_knot(T + w, t); st_knot(Gv + w, x); } // a rejected candidate is overwritten later
+            if (STAGE) {
+                if (room) { SL[ws * 64] = t; SL[(kStageSlots + ws) * 64] = x; }
+            } else if (room) {
+                st_knot(T + w, t); st_knot(Gv + w, x); // a rejected candidate is overwritten later
+            }
             // bitwise (not short-circuit) logic: selects, no branches
             const bool pushed = acc & room;
             const bool over = acc & !room;
@@ -110,7 +129,11 @@ __global__ __launch_bounds__(LB) void learn_logistic_kernel(const double* __rest
                 const double E = sbr_exp(lam * t);
                 const double e = E * g;
                 const double In = hm == 0 ? 0.0 : hI + (0.5 * (he + e)) * (t - ht);
-                if (le) { st_knot(H + n, (p * E) * g); st_knot(HI + n, In); }
+                if (STAGE) {
+                    if (le) { SL[(2 * kStageSlots + ws) * 64] = (p * E) * g; SL[(3 * kStageSlots + ws) * 64] = In; }
+                } else if (le) {
+                    st_knot(H + n, (p * E) * g); st_knot(HI + n, In);
+                }
                 hI = le ? In : hI;
                 he = le ? e : he;
                 ht = le ? t : ht;
@@ -123,8 +146,13 @@ __global__ __launch_bounds__(LB) void learn_logistic_kernel(const double* __rest
                     const double E2 = sbr_exp(lam * eta);
                     const double e2 = E2 * pe;
                     hI = hI + (0.5 * (he + e2)) * (eta - ht);
-                    H[hm] = (p * E2) * pe;
-                    HI[hm] = hI;
+                    if (STAGE) { // hm == n here: every earlier knot is ≤ η
+                        SL[(2 * kStageSlots + ws) * 64] = (p * E2) * pe;
+                        SL[(3 * kStageSlots + ws) * 64] = hI;
+                    } else {
+                        H[hm] = (p * E2) * pe;
+                        HI[hm] = hI;
+                    }
                     hm++;
                 }
             }
@@ -132,8 +160,32 @@ __global__ __launch_bounds__(LB) void learn_logistic_kernel(const double* __rest
             past |= cross ? 1 : 0;
             tlast = pushed ? t : tlast;
             n += pushed ? 1 : 0;
+            if (STAGE) {
+                ws = pushed ? (ws == kStageSlots - 1 ? 0 : ws + 1) : ws;
+                if ((++tick & 7) == 0 && n - fl >= 16) flush_line();
+            }
             done |= (over | (pushed & (stop_after_eta != 0) & (past != 0) & (t >= bound))) ? 1 : 0;
             return done == 0;
+        }
+        // STAGE: entries [fl, fl + 16) from the ring to the rows, as 16-B pairs (hazard entries
+        // past the τ̄ grid carry stale slots: never read)
+        __device__ __forceinline__ void flush_line()
+        {
+            typedef double d2 __attribute__((ext_vector_type(2)));
+            double* const R[4] = {T, Gv, H, HI};
+#pragma unroll
+            for (int k = 0; k < 16; k += 2) {
+                const int s0 = fs + k < kStageSlots ? fs + k : fs + k - kStageSlots; // pairs never straddle the wrap
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    d2 v;
+                    v.x = SL[(q * kStageSlots + s0) * 64];
+                    v.y = SL[(q * kStageSlots + s0 + 1) * 64];
+                    *(d2*)(R[q] + fl + k) = v;
+                }
+            }
+            fl += 16;
+            fs = fs + 16 < kStageSlots ? fs + 16 : fs + 16 - kStageSlots;
         }
         __device__ __forceinline__ bool start(double t, double x) { return push(true, t, x); }
         __device__ __forceinline__ bool step(bool acc, double, double tn, double, double, double y1, const StepK&, bool)
@@ -148,6 +200,15 @@ __global__ __launch_bounds__(LB) void learn_logistic_kernel(const double* __rest
         int b;
         __device__ __forceinline__ void finish(const OdeOut& o)
         {
+            if (STAGE) // the entries not flushed yet: knots [fl, n), τ̄ entries [fl, hm)
+                for (int i = fl, sl = fs; i < n; i++, sl = sl == kStageSlots - 1 ? 0 : sl + 1) {
+                    T[i] = SL[sl * 64];
+                    Gv[i] = SL[(kStageSlots + sl) * 64];
+                    if (i < hm) {
+                        H[i] = SL[(2 * kStageSlots + sl) * 64];
+                        HI[i] = SL[(3 * kStageSlots + sl) * 64];
+                    }
+                }
             st |= o.status;
             int n_le = m < 0 ? n : m; // every knot ≤ η when none passed it
             int n_tau = 0;
@@ -168,7 +229,9 @@ __global__ __launch_bounds__(LB) void learn_logistic_kernel(const double* __rest
             Lp->n_reject[b] = (int)o.nreject;
             if (ap->ready_q) publish_column(*ap, b);
         }
-    } sink{T, Gv, fuse ? L.hr + row : nullptr, fuse ? L.hrI + row : nullptr, 0, L.lim, -1, 0.0, -INFINITY, ETA,
+    } sink{T, Gv, fuse ? L.hr + row : nullptr, fuse ? L.hrI + row : nullptr,
+           stage_lds + (size_t)(threadIdx.x >> 6) * (4 * kStageSlots * 64) + (threadIdx.x & 63), 0, 0, 0, 0,
+           0, L.lim, -1, 0.0, -INFINITY, ETA,
            0, 0, a.stop_after_eta != 0 ? 1 : 0, st, fuse ? 1 : 0, 0, BETA, a.lam, a.p, 0.0, 0.0, 0.0, 0.0,
            &L, &a, b};
     LogisticSys f{BETA};
@@ -2006,19 +2069,13 @@ hipError_t launch_point_coop(const LearnBufs& L, const double* eta, const double
 // ============================================================================
 // launchers
 // ============================================================================
-#ifndef SBR_LEARN_WIDE_BLOCK
-#define SBR_LEARN_WIDE_BLOCK 64 // lanes per workgroup of a batch's wide learning launch
-#endif
-#ifndef SBR_LEARN_WIDE_LDS
-#define SBR_LEARN_WIDE_LDS 0 // LDS bytes reserved per such workgroup (caps the workgroups per CU)
-#endif
 hipError_t launch_learn_kernel(const double* beta, const double* eta, const double* t_end, const LearnArgs& a,
                                const LearnBufs& L, hipStream_t s, int mode)
 {
-    if (mode == 2) {
-        constexpr int B = SBR_LEARN_WIDE_BLOCK;
-        hipLaunchKernelGGL(learn_logistic_kernel<B>, dim3((a.n_beta + B - 1) / B), dim3(B), SBR_LEARN_WIDE_LDS, s, beta,
-                           eta, t_end, a, L);
+    if (mode == 2) { // LDS-staged rows with the fused hazard (launch_hazard_norm after)
+        if (!a.fuse_hazard) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((learn_logistic_kernel<64, true>), dim3((a.n_beta + 63) / 64), dim3(64), kStageLdsPerWave, s,
+                           beta, eta, t_end, a, L);
     } else if (mode == 0) {
         hipLaunchKernelGGL(learn_logistic_kernel<kLearnBlock>, dim3((a.n_beta + kLearnBlock - 1) / kLearnBlock),
                            dim3(kLearnBlock), 0, s, beta, eta, t_end, a, L);

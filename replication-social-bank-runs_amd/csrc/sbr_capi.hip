@@ -1013,14 +1013,19 @@ int sbr_sweep_baseline_batch_dev(sbr_ctx* c, void* stream, int64_t n_batch, cons
             // the slot's previous readers (the equilibria of group m - nslot) must be done
             if (m >= P.nslot) HIP_TRY(c, hipStreamWaitEvent(ls, c->ev_eq[slot], 0), SBR_EDEVICE);
             // every grid of the group in ONE learning launch (the hazard numerators and running
-            // integrals streamed with the knots): the launch lasts as long as its slowest column
-            // whatever its width, so up to SBR_BATCH_LEARN_WAVES waves learn together.  The
-            // first group has the chip to itself (one wave per workgroup: lone-wave latency);
-            // later groups run beside the equilibrium launches (two waves per workgroup)
+            // integrals streamed with the knots, normalised by launch_hazard_norm): the launch
+            // lasts as long as its slowest column whatever its width, so up to
+            // SBR_BATCH_LEARN_WAVES waves learn together.  The first group has the chip to itself:
+            // its rows leave through LDS as whole lines (mode 2).  Later groups run beside the
+            // equilibrium launches and store directly (no LDS taken from the equilibrium slabs).
+            const bool wide = m == 0;
             sbr::LearnArgs la{x0, o.ode_reltol, o.ode_abstol, p, lambda, o.ode_maxiters, (int32_t)(gn * n_beta), 1, 1};
             hipEvent_t t0 = tstart(c, ls);
+            // (a narrow first group — under 256 waves, e.g. a strong-scaled shard — stores directly:
+            // the staging's flush instructions cost more than the stores' contention there)
+            const int lmode = !wide ? 0 : ((gn * n_beta + 63) / 64 >= 256 ? 2 : 1);
             HIP_TRY(c, sbr::launch_learn_kernel(beta + g0 * n_beta, eta + g0 * n_beta, t_end + g0 * n_beta, la, W, ls,
-                                                m == 0 ? 2 : 0), SBR_EDEVICE);
+                                                lmode), SBR_EDEVICE);
             tend(c, ls, 0, t0);
             HIP_TRY(c, hipEventRecord(c->ev_learned[slot], ls), SBR_EDEVICE);
             HIP_TRY(c, hipStreamWaitEvent(hs, c->ev_learned[slot], 0), SBR_EDEVICE);
@@ -1031,13 +1036,13 @@ int sbr_sweep_baseline_batch_dev(sbr_ctx* c, void* stream, int64_t n_batch, cons
             for (int64_t e0 = 0; e0 < gn; e0 += Eg) {
                 const int64_t en = (gn - e0) < Eg ? (gn - e0) : Eg;
                 const sbr::LearnBufs We = learn_rows(W, (size_t)(e0 * n_beta));
+                const int64_t gg = g0 + e0;
                 HIP_TRY(c, sbr::launch_hazard_norm(la, We, (int)(en * n_beta), hs), SBR_EDEVICE);
                 hipEvent_t eh = c->ev_hn[(size_t)k_hn++];
                 HIP_TRY(c, hipEventRecord(eh, hs), SBR_EDEVICE);
                 HIP_TRY(c, hipStreamWaitEvent(es, eh, 0), SBR_EDEVICE);
                 // column i·n_beta + j of the launch is grid g0+e0+i's column j: eta / t_end and
                 // every out field are [n_batch × n_beta (× n_u)] contiguous
-                const int64_t gg = g0 + e0;
                 sbr::ResultSoA r{out->xi + gg * np, out->tau_in_unc + gg * np, out->tau_out_unc + gg * np,
                                  out->aw_max + gg * np, out->tol + gg * np, out->status + gg * np,
                                  out->iters ? out->iters + gg * np : nullptr};

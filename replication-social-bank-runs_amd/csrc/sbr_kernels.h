@@ -207,7 +207,8 @@ hipError_t launch_learn_logistic(const double* beta, const double* eta, const do
                                  const LearnBufs& L, hipStream_t s);
 // the learning kernel alone (a.fuse_hazard: HR numerators and running integrals streamed, to be
 // normalised by launch_hazard_norm); mode 0: two waves per workgroup (beside a running equilibrium
-// launch), 1: one wave per workgroup (latency), 2: a batch's wide learning launch (the chip otherwise idle)
+// launch), 1: one wave per workgroup (latency), 2: a batch's wide learning launch (the chip otherwise idle:
+// LDS-staged rows; a.fuse_hazard must be 1, launch_hazard_norm follows)
 hipError_t launch_learn_kernel(const double* beta, const double* eta, const double* t_end, const LearnArgs& a,
                                const LearnBufs& L, hipStream_t s, int mode);
 // HR = numerator / (p·I + (1 − p)·I_η) over the first n_cols columns of L (after a fused learning)
