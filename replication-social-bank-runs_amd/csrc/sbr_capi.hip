@@ -289,17 +289,19 @@ int ensure_hetero_bufs(sbr_ctx* c, sbr::HeteroBufs& H, size_t& hcol, size_t& hca
 {
     if (n_col <= hcol && cap == hcap && K == hK) return SBR_OK;
     free_hetero_bufs(H, hcol, hcap, hK);
-    HIP_TRY(c, hipMalloc(&H.t, n_col * cap * 8), SBR_ENOMEM);
-    HIP_TRY(c, hipMalloc(&H.G, n_col * cap * K * 8), SBR_ENOMEM);
-    HIP_TRY(c, hipMalloc(&H.hr, n_col * cap * K * 8), SBR_ENOMEM);
-    HIP_TRY(c, hipMalloc(&H.hrI, n_col * cap * K * 8), SBR_ENOMEM);
+    const size_t ld = learn_ld(cap); // padded rows, as for the baseline workspaces
+    HIP_TRY(c, hipMalloc(&H.t, n_col * ld * 8), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&H.G, n_col * ld * K * 8), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&H.hr, n_col * ld * K * 8), SBR_ENOMEM);
+    HIP_TRY(c, hipMalloc(&H.hrI, n_col * ld * K * 8), SBR_ENOMEM);
     HIP_TRY(c, hipMalloc(&H.n_knots, n_col * 4), SBR_ENOMEM);
     HIP_TRY(c, hipMalloc(&H.n_tau, n_col * 4), SBR_ENOMEM);
     HIP_TRY(c, hipMalloc(&H.n_le, n_col * 4), SBR_ENOMEM);
     HIP_TRY(c, hipMalloc(&H.status, n_col * 4), SBR_ENOMEM);
     HIP_TRY(c, hipMalloc(&H.n_accept, n_col * 4), SBR_ENOMEM);
     HIP_TRY(c, hipMalloc(&H.n_reject, n_col * 4), SBR_ENOMEM);
-    H.cap = (int32_t)cap;
+    H.cap = (int32_t)ld;
+    H.lim = (int32_t)cap;
     hcol = n_col;
     hcap = cap;
     hK = K;
@@ -1523,7 +1525,7 @@ int sbr_hetero_equilibrium_on_knots(sbr_ctx* c, int32_t K, const double* t, cons
     double* dtg = (double*)(D + Lh.tg);
     const size_t ck = c->hk_cap_k;
     const sbr::HeteroBufs HB{dtg, dtg + n, (double*)(D + Lh.hr), (double*)(D + Lh.hri), dcnt, dcnt + 1, dcnt + 2,
-                             (uint32_t*)(dcnt + 3), dcnt + 4, dcnt + 5, (int32_t)ck};
+                             (uint32_t*)(dcnt + 3), dcnt + 4, dcnt + 5, (int32_t)ck, (int32_t)ck};
     double* du = (double*)(D + Lh.u); // [t_end, u...]
     double* dres = (double*)(D + Lh.res);
     const size_t nu = (size_t)n_u;
@@ -1930,12 +1932,12 @@ int sbr_learn_hetero(sbr_ctx* c, int32_t K, const double* betas, const double* d
         sbr::ResultSoA r{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
         HIP_TRY(c, sbr::launch_hetero(K, dbeta, ddist, dtend, dtend, nullptr, la, ea, c->H, r, nullptr, nullptr, s, 0),
                 SBR_EDEVICE);
-        const size_t w = (size_t)o.knot_capacity;
+        const size_t w = (size_t)o.knot_capacity, ld = (size_t)c->H.cap;
         if (t_out)
-            HIP_TRY(c, hipMemcpy2DAsync(t_out, (size_t)cap * 8, c->H.t, w * 8, w * 8, (size_t)n_col, hipMemcpyDeviceToHost, s),
+            HIP_TRY(c, hipMemcpy2DAsync(t_out, (size_t)cap * 8, c->H.t, ld * 8, w * 8, (size_t)n_col, hipMemcpyDeviceToHost, s),
                     SBR_EDEVICE);
         if (G_out)
-            HIP_TRY(c, hipMemcpy2DAsync(G_out, (size_t)cap * K * 8, c->H.G, w * K * 8, w * K * 8, (size_t)n_col,
+            HIP_TRY(c, hipMemcpy2DAsync(G_out, (size_t)cap * K * 8, c->H.G, ld * K * 8, w * K * 8, (size_t)n_col,
                                         hipMemcpyDeviceToHost, s), SBR_EDEVICE);
         if (n_knots) HIP_TRY(c, hipMemcpyAsync(n_knots, c->H.n_knots, (size_t)n_col * 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
         if (status) HIP_TRY(c, hipMemcpyAsync(status, c->H.status, (size_t)n_col * 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);

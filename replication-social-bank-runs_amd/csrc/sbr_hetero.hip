@@ -273,7 +273,7 @@ __global__ __launch_bounds__(64 * kHetLearnWG) void learn_hetero_wave_kernel(con
     double tprev = 0.0, Ik = 0.0, eprev = 0.0, gprev = 0.0;
     bool past = false, done = false;
     auto push = [&](double t, double xs, double g) {
-        if (n >= L.cap) { st |= SBR_KNOT_OVERFLOW; done = true; return; }
+        if (n >= L.lim) { st |= SBR_KNOT_OVERFLOW; done = true; return; }
         if (lane == 0) T[n] = t;
         if (act) Gv[(size_t)n * K + lane] = xs;
         if (!past) {

@@ -108,7 +108,8 @@ struct HeteroBufs {
     uint32_t* status;
     int32_t* n_accept;
     int32_t* n_reject;
-    int32_t cap;
+    int32_t cap; // row stride (knots) of t, G and the K hazard rows
+    int32_t lim; // knots a column may store (<= cap; SBR_KNOT_OVERFLOW beyond)
 };
 
 struct HeteroEqArgs {
