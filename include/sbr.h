@@ -309,24 +309,27 @@ int sbr_sweep_hetero_batch_dev(sbr_ctx* ctx, void* stream, int64_t n_batch, int3
  * buffers go to tau_in / tau_out ([n_u][K], may be NULL).  Paths (may be NULL, capacity cap):
  * hr = HR_k on the τ̄ grid (knots <= η, then η: hazard_rate's explicit grid, solver.jl:163-164) at
  * hr + k·cap, *n_tau entries each (0 after the hazard's BoundsError) — SolvedModelHetero.HRs
- * (:255); with n_u == 1, aw_total = AW_total on the knots (NaN without a run).  Synchronous.
+ * (:255); with n_u == 1, aw_total = AW_total on the knots and aw_groups = get_AW_hetero's per-group
+ * curves on the knots (:335-362): AW_OUT_k at aw_groups + k·cap, AW_IN_k at aw_groups + (K + k)·cap
+ * (each may be NULL; NaN rows without a run, where get_AW_hetero returns nothing).  Synchronous.
  */
 int sbr_hetero_equilibrium_on_knots(sbr_ctx* ctx, int32_t K, const double* t, const double* G, int64_t n_knots,
                                     const double* betas, const double* dist, double eta, double t_end, const double* u,
                                     int64_t n_u, double p, double kappa, double lambda, const sbr_opts* opts,
                                     sbr_result_soa* out, double* tau_in, double* tau_out, double* hr, double* aw_total,
-                                    int64_t cap, int64_t* n_tau);
+                                    double* aw_groups, int64_t cap, int64_t* n_tau);
 
 /* One heterogeneity equilibrium with what scripts/2_heterogeneity.jl plots
  * (aggregate_withdrawals_hetero.pdf): learning knots t[n] and group CDFs G[n][K]
  * (solve_SInetwork_hetero), the per-group buffers, and AW_total on the knots
- * (get_AW_functions_hetero!, heterogeneity_solver.jl:386; NaN without a run), from
- * which each group's AW curve follows.  res = {ξ, AW_max, tol}; t / aw_total hold
- * `cap` doubles, G cap·K. */
+ * (get_AW_functions_hetero!, heterogeneity_solver.jl:386; NaN without a run) and each
+ * group's curves AW_OUT_k / AW_IN_k on the knots (get_AW_hetero, :335-362; aw_groups rows
+ * k and K + k, stride cap).  res = {ξ, AW_max, tol}; t / aw_total hold `cap` doubles,
+ * G cap·K, aw_groups 2K·cap (any of them may be NULL). */
 int sbr_hetero_point_paths(sbr_ctx* ctx, int32_t K, const double* betas, const double* dist, double eta, double t_end,
                            double x0, double u, double p, double kappa, double lambda, const sbr_opts* opts,
                            double* res, uint32_t* status, double* tau_in, double* tau_out, double* t, double* G,
-                           double* aw_total, int64_t cap, int64_t* n_knots);
+                           double* aw_total, double* aw_groups, int64_t cap, int64_t* n_knots);
 
 /*
  * Social-learning extension sweep — for each β column b and each u:

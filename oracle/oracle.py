@@ -360,10 +360,11 @@ def interest_point(beta, eta, t_end, u, p, kappa, lam, r, delta, x0=1e-4, cap=1 
 
 def hetero_point_paths(betas, dist, eta, t_end, u, p, kappa, lam, x0=1e-4, cap=1 << 16):
     """One heterogeneity equilibrium with the learning knots t, G [n, K], the per-group
-    buffers and AW_total on the knots (get_AW_functions_hetero!, heterogeneity_solver.jl:386)."""
+    buffers, AW_total on the knots (get_AW_functions_hetero!, heterogeneity_solver.jl:386) and
+    get_AW_hetero's per-group curves aw_out / aw_in [K, n] (:335-362)."""
     L = lib()
     L.sbro_hetero_point_paths.restype = _I64
-    L.sbro_hetero_point_paths.argtypes = [_I32, _P, _P, _D, _D, _D, _D, _D, _D, _D, _P, _P, _P, _P, _P, _P, _P, _I64]
+    L.sbro_hetero_point_paths.argtypes = [_I32, _P, _P, _D, _D, _D, _D, _D, _D, _D, _P, _P, _P, _P, _P, _P, _P, _P, _I64]
     betas = np.ascontiguousarray(betas, np.float64)
     dist = np.ascontiguousarray(dist, np.float64)
     K = len(dist)
@@ -371,12 +372,14 @@ def hetero_point_paths(betas, dist, eta, t_end, u, p, kappa, lam, x0=1e-4, cap=1
     st = np.zeros(1, np.uint32)
     tin, tout = np.empty(K), np.empty(K)
     t, G, aw = np.empty(cap), np.empty(cap * K), np.empty(cap)
+    awg = np.empty((2 * K, cap))
     n = L.sbro_hetero_point_paths(K, _ptr(betas), _ptr(dist), eta, t_end, x0, u, p, kappa, lam, _ptr(res), _ptr(st),
-                                  _ptr(tin), _ptr(tout), _ptr(t), _ptr(G), _ptr(aw), cap)
+                                  _ptr(tin), _ptr(tout), _ptr(t), _ptr(G), _ptr(aw), _ptr(awg), cap)
     if n < 0:
         raise RuntimeError("oracle hetero point failed")
     return dict(xi=res[0], aw_max=res[1], tol=res[2], status=int(st[0]), tau_in_unc=tin, tau_out_unc=tout,
-                t=t[:n].copy(), G=G[:n * K].reshape(n, K).copy(), aw_total=aw[:n].copy())
+                t=t[:n].copy(), G=G[:n * K].reshape(n, K).copy(), aw_total=aw[:n].copy(),
+                aw_out=awg[:K, :n].copy(), aw_in=awg[K:, :n].copy())
 
 
 def hetero_equilibrium_knots(t, G, betas, dist, eta, t_end, u, p, kappa, lam):

@@ -1093,8 +1093,11 @@ static uint32_t compute_xi_hetero(const double* tin, const double* tout, const d
 }
 
 /* get_AW_hetero's AW_max over the whole learning grid (heterogeneity_solver.jl:316-375) */
-static double aw_max_hetero(double xi, const double* tin, const double* tout, const double* dist, int K,
-                            const double* t, const double* G, int64_t n, double* cum, int* oob)
+/* get_AW_hetero (heterogeneity_solver.jl:316-375) on the knots: AW_cum into cum[n], returns its
+ * maximum; grp (may be NULL): the per-group AW_OUT_k at grp + k·ld, AW_IN_k at grp + (K + k)·ld */
+static double aw_max_hetero_groups(double xi, const double* tin, const double* tout, const double* dist, int K,
+                                   const double* t, const double* G, int64_t n, double* cum, int* oob, double* grp,
+                                   int64_t ld)
 {
     for (int64_t i = 0; i < n; i++) cum[i] = 0.0;
     for (int k = 0; k < K; k++) {
@@ -1107,12 +1110,22 @@ static double aw_max_hetero(double xi, const double* tin, const double* tout, co
             double awin = a >= 0 ? gi : 0.0;
             double awout = b >= 0 ? go : 0.0;
             cum[i] = cum[i] + dist[k] * (awout - awin);
+            if (grp) {
+                grp[(int64_t)k * ld + i] = awout;
+                grp[(int64_t)(K + k) * ld + i] = awin;
+            }
         }
     }
     double mx = -INFINITY;
     for (int64_t i = 0; i < n; i++)
         if (mx == mx && (cum[i] != cum[i] || cum[i] > mx)) mx = cum[i];
     return mx;
+}
+
+static double aw_max_hetero(double xi, const double* tin, const double* tout, const double* dist, int K,
+                            const double* t, const double* G, int64_t n, double* cum, int* oob)
+{
+    return aw_max_hetero_groups(xi, tin, tout, dist, K, t, G, n, cum, oob, NULL, 0);
 }
 
 /* Hetero sweep: column c has group rates betas[c*K .. c*K+K), η = eta[c],
@@ -1438,11 +1451,12 @@ int64_t sbro_social_point(double beta, double eta, double x0, double u, double p
 }
 
 /* one hetero point with its paths (aggregate_withdrawals_hetero.pdf): res = {ξ, AW_max, tol};
- * learning knots t[n], G[n][K], per-group buffers, AW_total on the knots (NaN without a run) */
+ * learning knots t[n], G[n][K], per-group buffers, AW_total on the knots and (aw_groups, may be
+ * NULL) AW_OUT_k / AW_IN_k at rows k / K + k of stride cap — NaN without a run */
 int64_t sbro_hetero_point_paths(int32_t K, const double* betas, const double* dist, double eta, double t_end,
                                 double x0, double u, double p, double kappa, double lambda, double* res,
                                 uint32_t* status, double* tin, double* tout, double* t_out, double* G_out,
-                                double* aw_out, int64_t cap)
+                                double* aw_out, double* aw_groups, int64_t cap)
 {
     int32_t it = 0;
     int64_t nk = 0;
@@ -1453,9 +1467,11 @@ int64_t sbro_hetero_point_paths(int32_t K, const double* betas, const double* di
     if (n < 0) return n;
     if (*status & SBR_RUN) {
         int oob = 0;
-        (void)aw_max_hetero(res[0], tin, tout, dist, K, t_out, G_out, n, aw_out, &oob);
+        (void)aw_max_hetero_groups(res[0], tin, tout, dist, K, t_out, G_out, n, aw_out, &oob, aw_groups, cap);
     } else {
         for (int64_t i = 0; i < n; i++) aw_out[i] = NAN;
+        for (int64_t r = 0; aw_groups && r < 2 * K; r++)
+            for (int64_t i = 0; i < n; i++) aw_groups[r * cap + i] = NAN;
     }
     return n;
 }

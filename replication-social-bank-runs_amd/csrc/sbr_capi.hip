@@ -1442,9 +1442,22 @@ struct HeteroKnotLayout {
         hri = hr + 8 * ck * 8;
         u = hri + 8 * ck * 8;
         res = u + 8 * (cu + 8);
-        bytes = res + 8 * (5 * cu + 16 * cu + ck) + 256;
+        bytes = res + 8 * (5 * cu + 16 * cu + 17 * ck) + 256; // path mode: AW_total + 2K group rows
     }
 };
+
+// path mode's rows (AW_total, then AW_OUT_k and AW_IN_k, each n long) into the caller's
+// aw_total [n] and aw_groups [2K][cap]; NaN rows without a run (get_AW_hetero returns nothing)
+void copy_hetero_paths(const double* src, bool run, int K, int64_t n, int64_t cap, double* aw_total,
+                       double* aw_groups)
+{
+    for (int r = 0; r <= 2 * K; r++) {
+        double* dst = r == 0 ? aw_total : (aw_groups ? aw_groups + (size_t)(r - 1) * cap : nullptr);
+        if (!dst) continue;
+        if (run) memcpy(dst, src + (size_t)r * n, (size_t)n * 8);
+        else for (int64_t i = 0; i < n; i++) dst[i] = NAN;
+    }
+}
 
 int ensure_hetero_knots(sbr_ctx* c, size_t n, size_t n_u)
 {
@@ -1473,10 +1486,10 @@ int sbr_hetero_equilibrium_on_knots(sbr_ctx* c, int32_t K, const double* t, cons
                                     const double* betas, const double* dist, double eta, double t_end, const double* u,
                                     int64_t n_u, double p, double kappa, double lambda, const sbr_opts* opts,
                                     sbr_result_soa* out, double* tau_in, double* tau_out, double* hr, double* aw_total,
-                                    int64_t cap, int64_t* n_tau)
+                                    double* aw_groups, int64_t cap, int64_t* n_tau)
 {
     if (guess_set(opts)) return fail(c, SBR_EARG, "xi_guess: only sbr_equilibrium_on_knots takes a first iterate");
-    SBR_ON_RANK0(c, sbr_hetero_equilibrium_on_knots(c, K, t, G, n, betas, dist, eta, t_end, u, n_u, p, kappa, lambda, opts, out, tau_in, tau_out, hr, aw_total, cap, n_tau));
+    SBR_ON_RANK0(c, sbr_hetero_equilibrium_on_knots(c, K, t, G, n, betas, dist, eta, t_end, u, n_u, p, kappa, lambda, opts, out, tau_in, tau_out, hr, aw_total, aw_groups, cap, n_tau));
     if (!c || !t || !G || !betas || !dist || !u || !out) return SBR_EARG;
     if (K != 1 && K != 2 && K != 3 && K != 4 && K != 8) return fail(c, SBR_EARG, "K must be 1, 2, 3, 4 or 8");
     if (n < 1 || n > (1 << 24) || n_u < 1 || n_u > (1 << 24)) return fail(c, SBR_EARG, "knot / u count");
@@ -1494,7 +1507,8 @@ int sbr_hetero_equilibrium_on_knots(sbr_ctx* c, int32_t K, const double* t, cons
     if (!(t[0] == t[0])) return fail(c, SBR_EARG, "ArgumentError: knots must be sorted");
     for (int64_t i = 0; i + 1 < n; i++)
         if (!(t[i] <= t[i + 1])) return fail(c, SBR_EARG, "ArgumentError: knots must be sorted");
-    if (aw_total && n_u != 1) return fail(c, SBR_EARG, "the AW_total path needs n_u == 1");
+    const bool paths = aw_total || aw_groups;
+    if (paths && n_u != 1) return fail(c, SBR_EARG, "the AW paths need n_u == 1");
     if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
     const sbr_opts o = resolve(opts);
     int rc = ensure_hetero_knots(c, (size_t)n, (size_t)n_u);
@@ -1506,7 +1520,7 @@ int sbr_hetero_equilibrium_on_knots(sbr_ctx* c, int32_t K, const double* t, cons
     while (m < n && t[m] <= eta) m++;
     const bool hz_oob = m == 0 || (m == n && !(n >= 2 && t[n - 1] == eta));
     const int64_t ntau = hz_oob ? 0 : m + 1;
-    if ((hr && ntau > cap) || (aw_total && n > cap)) return fail(c, SBR_EARG, "path capacity too small");
+    if ((hr && ntau > cap) || (paths && n > cap)) return fail(c, SBR_EARG, "path capacity too small");
     std::vector<double> key;
     key.reserve(2 * (size_t)K + 5);
     key.push_back((double)K);
@@ -1529,11 +1543,12 @@ int sbr_hetero_equilibrium_on_knots(sbr_ctx* c, int32_t K, const double* t, cons
     double* du = (double*)(D + Lh.u); // [t_end, u...]
     double* dres = (double*)(D + Lh.res);
     const size_t nu = (size_t)n_u;
-    // results: xi, aw, tol [n_u] | status, iters [n_u] int32 | tau_in, tau_out [n_u][K] | AW_total [n]
+    // results: xi, aw, tol [n_u] | status, iters [n_u] int32 | tau_in, tau_out [n_u][K] |
+    // path mode: AW_total [n], AW_OUT_k [K][n], AW_IN_k [K][n]
     double* dtin = dres + 4 * nu;
     double* dtout = dtin + nu * K;
     double* dpath = dtout + nu * K;
-    const size_t res_bytes = (4 * nu + 2 * nu * K + (aw_total ? (size_t)n : 0)) * 8;
+    const size_t res_bytes = (4 * nu + 2 * nu * K + (paths ? (size_t)n * (1 + 2 * K) : 0)) * 8;
     if (!hit) c->hk_valid = false;
     rc = fenced(c, nullptr, false, [&](hipStream_t s) -> int {
         sbr::LearnArgs la{0.0, o.ode_reltol, o.ode_abstol, p, lambda, o.ode_maxiters, 1, 0, 0, nullptr, nullptr};
@@ -1565,6 +1580,10 @@ int sbr_hetero_equilibrium_on_knots(sbr_ctx* c, int32_t K, const double* t, cons
                                (int32_t*)(dres + 3 * nu) + nu};
         HIP_TRY(c, sbr::launch_hetero(K, dsc, dsc + K, dsc + 2 * K, du, du + 1, la, ea, HB, r, dtin, dtout, s, 1),
                 SBR_EDEVICE);
+        if (aw_groups)
+            HIP_TRY(c, sbr::launch_hetero_aw_groups(K, dtg, dtg + n, dcnt, (int)n, dres, dtin, dtout,
+                                                    (const uint32_t*)(dres + 3 * nu), dpath + n, (size_t)n, s),
+                    SBR_EDEVICE);
         HIP_TRY(c, hipMemcpyAsync(H + Lh.res, D + Lh.res, res_bytes, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
         HIP_TRY(c, hipStreamSynchronize(s), SBR_EDEVICE);
         return SBR_OK;
@@ -1595,10 +1614,9 @@ int sbr_hetero_equilibrium_on_knots(sbr_ctx* c, int32_t K, const double* t, cons
     if (n_tau) *n_tau = ntau;
     if (hr)
         for (int k = 0; k < K; k++) memcpy(hr + (size_t)k * cap, c->hk_hr.data() + (size_t)k * ntau, (size_t)ntau * 8);
-    if (aw_total) {
+    if (paths) {
         const bool run = (((const uint32_t*)(hres + 3 * nu))[0] & SBR_RUN) != 0;
-        if (run) memcpy(aw_total, hres + 4 * nu + 2 * nu * K, (size_t)n * 8);
-        else for (int64_t i = 0; i < n; i++) aw_total[i] = NAN;
+        copy_hetero_paths(hres + 4 * nu + 2 * nu * K, run, K, n, cap, aw_total, aw_groups);
     }
     return SBR_OK;
 }
@@ -2033,10 +2051,10 @@ int sbr_sweep_hetero_batch_dev(sbr_ctx* c, void* stream, int64_t n_batch, int32_
 int sbr_hetero_point_paths(sbr_ctx* c, int32_t K, const double* betas, const double* dist, double eta, double t_end,
                            double x0, double u, double p, double kappa, double lambda, const sbr_opts* opts,
                            double* res, uint32_t* status, double* tau_in, double* tau_out, double* t, double* G,
-                           double* aw_total, int64_t cap, int64_t* n_knots)
+                           double* aw_total, double* aw_groups, int64_t cap, int64_t* n_knots)
 {
     if (guess_set(opts)) return fail(c, SBR_EARG, "xi_guess: only sbr_equilibrium_on_knots takes a first iterate");
-    SBR_ON_RANK0(c, sbr_hetero_point_paths(c, K, betas, dist, eta, t_end, x0, u, p, kappa, lambda, opts, res, status, tau_in, tau_out, t, G, aw_total, cap, n_knots));
+    SBR_ON_RANK0(c, sbr_hetero_point_paths(c, K, betas, dist, eta, t_end, x0, u, p, kappa, lambda, opts, res, status, tau_in, tau_out, t, G, aw_total, aw_groups, cap, n_knots));
     if (!c || !res || !status || !betas || !dist) return SBR_EARG;
     if (K != 1 && K != 2 && K != 3 && K != 4 && K != 8) return fail(c, SBR_EARG, "K must be 1, 2, 3, 4 or 8");
     double dsum = 0.0;
@@ -2051,7 +2069,7 @@ int sbr_hetero_point_paths(sbr_ctx* c, int32_t K, const double* betas, const dou
     if (hipSetDevice(c->device) != hipSuccess) return fail(c, SBR_EDEVICE, "hipSetDevice");
     sbr_opts o = resolve(opts);
     const size_t kc = (size_t)o.knot_capacity;
-    int rc = ensure_stage(c, (2 * (size_t)K + 3 + 4 + 2 * (size_t)K + kc) * 8 + 512);
+    int rc = ensure_stage(c, (2 * (size_t)K + 3 + 4 + 2 * (size_t)K + (1 + 2 * (size_t)K) * kc) * 8 + 512);
     if (rc) return rc;
     double* d = (double*)c->stage;
     double *dbeta = d, *ddist = d + K, *deta = d + 2 * K, *dtend = deta + 1, *du = dtend + 1;
@@ -2070,6 +2088,10 @@ int sbr_hetero_point_paths(sbr_ctx* c, int32_t K, const double* betas, const dou
         rc = sbr_sweep_hetero_dev(c, s, K, dbeta, ddist, deta, dtend, x0, du, 1, 1, p, kappa, lambda, &o, &r, dtin, dtout);
         c->het_aw_path = nullptr;
         if (rc) return rc;
+        double* dgrp = dpath + kc; // AW_OUT_k / AW_IN_k rows of stride kc
+        if (aw_groups)
+            HIP_TRY(c, sbr::launch_hetero_aw_groups(K, c->H.t, c->H.G, c->H.n_knots, (int)kc, dres, dtin, dtout, dst,
+                                                    dgrp, kc, s), SBR_EDEVICE);
         int32_t n = 0;
         HIP_TRY(c, hipMemcpyAsync(res, dres, 24, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
         HIP_TRY(c, hipMemcpyAsync(status, dst, 4, hipMemcpyDeviceToHost, s), SBR_EDEVICE);
@@ -2081,9 +2103,13 @@ int sbr_hetero_point_paths(sbr_ctx* c, int32_t K, const double* betas, const dou
         if (n > cap) return fail(c, SBR_EARG, "path capacity too small");
         if (t) HIP_TRY(c, hipMemcpy(t, c->H.t, (size_t)n * 8, hipMemcpyDeviceToHost), SBR_EDEVICE);
         if (G) HIP_TRY(c, hipMemcpy(G, c->H.G, (size_t)n * K * 8, hipMemcpyDeviceToHost), SBR_EDEVICE);
-        if (aw_total) {
-            if (*status & SBR_RUN) HIP_TRY(c, hipMemcpy(aw_total, dpath, (size_t)n * 8, hipMemcpyDeviceToHost), SBR_EDEVICE);
-            else for (int i = 0; i < n; i++) aw_total[i] = NAN;
+        if (aw_total || aw_groups) {
+            const bool run = (*status & SBR_RUN) != 0;
+            std::vector<double> h(run ? (size_t)n * (1 + 2 * K) : 0);
+            for (int r = 0; run && r <= 2 * K; r++)
+                HIP_TRY(c, hipMemcpy(h.data() + (size_t)r * n, r == 0 ? dpath : dgrp + (size_t)(r - 1) * kc,
+                                     (size_t)n * 8, hipMemcpyDeviceToHost), SBR_EDEVICE);
+            copy_hetero_paths(h.data(), run, K, n, cap, aw_total, aw_groups);
         }
         return SBR_OK;
     });

@@ -1162,4 +1162,61 @@ hipError_t launch_hetero(int K, const double* betas, const double* dist, const d
     }
 }
 
+// ---------------------------------------------------------------------------
+// hetero_aw_groups_kernel<K>: get_AW_hetero's per-group curves (heterogeneity_solver.jl:335-362)
+// of one solved point on its learning knots, one lane per knot i:
+//   AW_OUT_k(t_i) = t_i − ξ + min(τ̄_OUT,k, ξ) >= 0 ? G_k(max(that, 0)) : 0, AW_IN_k alike,
+// G_k the gridded-linear interpolant on the knots (bracket = searchsortedlast, clamped to
+// [0, n−2]) — the operations of equilibrium_hetero_kernel's AW pass, so the same bits.  Runs
+// after the equilibrium on the same stream (ξ, τ̄ and status read on the device); writes nothing
+// without a run (the host fills NaN rows).  Rows: AW_OUT_k at out + k·ld, AW_IN_k at out + (K+k)·ld.
+// ---------------------------------------------------------------------------
+template <int K>
+__global__ __launch_bounds__(256) void hetero_aw_groups_kernel(const double* __restrict__ T,
+                                                               const double* __restrict__ G,
+                                                               const int32_t* __restrict__ n_p,
+                                                               const double* __restrict__ xi_p,
+                                                               const double* __restrict__ tin,
+                                                               const double* __restrict__ tout,
+                                                               const uint32_t* __restrict__ status,
+                                                               double* __restrict__ out, size_t ld)
+{
+    const int n = *n_p;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n || n < 2 || !(status[0] & SBR_RUN)) return;
+    const double xi = *xi_p, ti = T[i];
+    auto at = [&](int k, double x) {
+        int q = ssl_range(T, 0, n - 1, x);
+        q = q > n - 2 ? n - 2 : (q < 0 ? 0 : q);
+        const double d = (x - T[q]) / (T[q + 1] - T[q]);
+        return G[(size_t)q * K + k] * (1.0 - d) + G[(size_t)(q + 1) * K + k] * d;
+    };
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const double av = (ti - xi) + dmin(tin[k], xi);
+        const double bv = (ti - xi) + dmin(tout[k], xi);
+        const double gi = at(k, av > 0 ? av : 0.0);
+        const double go = at(k, bv > 0 ? bv : 0.0);
+        out[(size_t)k * ld + i] = bv >= 0 ? go : 0.0;
+        out[(size_t)(K + k) * ld + i] = av >= 0 ? gi : 0.0;
+    }
+}
+
+hipError_t launch_hetero_aw_groups(int K, const double* T, const double* G, const int32_t* n_dev, int n_max,
+                                   const double* xi, const double* tin, const double* tout, const uint32_t* status,
+                                   double* out, size_t ld, hipStream_t s)
+{
+    if (n_max < 1) return hipSuccess;
+    const dim3 grid((unsigned)((n_max + 255) / 256)), block(256);
+    switch (K) {
+    case 1: hipLaunchKernelGGL(hetero_aw_groups_kernel<1>, grid, block, 0, s, T, G, n_dev, xi, tin, tout, status, out, ld); break;
+    case 2: hipLaunchKernelGGL(hetero_aw_groups_kernel<2>, grid, block, 0, s, T, G, n_dev, xi, tin, tout, status, out, ld); break;
+    case 3: hipLaunchKernelGGL(hetero_aw_groups_kernel<3>, grid, block, 0, s, T, G, n_dev, xi, tin, tout, status, out, ld); break;
+    case 4: hipLaunchKernelGGL(hetero_aw_groups_kernel<4>, grid, block, 0, s, T, G, n_dev, xi, tin, tout, status, out, ld); break;
+    case 8: hipLaunchKernelGGL(hetero_aw_groups_kernel<8>, grid, block, 0, s, T, G, n_dev, xi, tin, tout, status, out, ld); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 }  // namespace sbr

@@ -200,6 +200,11 @@ hipError_t launch_social_iter(const SocialArgs& a, const SocialArgs& p, const So
 
 // phase 0: learning (+ the streamed hazards); 1: equilibria; 2: the hazards of knots and group
 // CDFs already in L (n_knots and status set by the caller)
+// get_AW_hetero's per-group AW_OUT_k / AW_IN_k on one solved point's knots (T [n], G [n][K],
+// n = *n_dev <= n_max; ξ, τ̄_IN [K], τ̄_OUT [K], status on the device): rows of stride ld
+hipError_t launch_hetero_aw_groups(int K, const double* T, const double* G, const int32_t* n_dev, int n_max,
+                                   const double* xi, const double* tin, const double* tout, const uint32_t* status,
+                                   double* out, size_t ld, hipStream_t s);
 hipError_t launch_hetero(int K, const double* betas, const double* dist, const double* eta, const double* t_end,
                          const double* u, const LearnArgs& la, const HeteroEqArgs& ea, const HeteroBufs& L,
                          const ResultSoA& out, double* tin, double* tout, hipStream_t s, int phase);

@@ -19,8 +19,9 @@ heterogeneity_solver.jl by this file.  Then :59, :67 and :76 run unchanged:
     hazards stay resident across the script's per-u calls); HRs are the engine's HR_k on
     hazard_rate's explicit grid (:255);
   * `get_AW_functions_hetero!(result)` → (AW_cum, AW_OUT_groups, AW_IN_groups, AW_groups,
-    AW_max) (:386-402 / get_AW_hetero :316-375): AW_cum and AW_max are the engine's AW_total
-    path, the per-group curves are rebuilt from the group CDFs.
+    AW_max) (:386-402 / get_AW_hetero :316-375): every curve comes from the engine — AW_cum and
+    AW_max from its AW_total path, AW_OUT_k / AW_IN_k from its per-group rows (AW_k = their
+    difference, as :358 forms it), all on lr.grid.
 
 A β×u (or βs-column × u) grid is one call: `SBREngine.solve_equilibrium_hetero_grid`.
 
@@ -54,35 +55,31 @@ function solve_SInetwork_hetero(params::LearningParametersHetero; tol = eps())
     return LearningResultsHetero(params, cdfs, pdfs, t, time() - solve_start, nothing)
 end
 
-# the per-group withdrawal curves of get_AW_hetero (heterogeneity_solver.jl:335-362) on the grid
-function _hetero_group_curves(ξ, τ_bar_IN_UNCs, τ_bar_OUT_UNCs, learning_cdfs, t_grid)
-    shifted(cdf, τ) = (s = t_grid .- ξ .+ min(τ, ξ); ifelse.(s .>= 0, cdf.(max.(s, 0)), 0.0))
-    outs, ins, nets = Any[], Any[], Any[]
-    for k in eachindex(learning_cdfs)
-        o = shifted(learning_cdfs[k], τ_bar_OUT_UNCs[k])
-        i = shifted(learning_cdfs[k], τ_bar_IN_UNCs[k])
-        push!(outs, LinearInterpolation(t_grid, o)); push!(ins, LinearInterpolation(t_grid, i))
-        push!(nets, LinearInterpolation(t_grid, o .- i))
-    end
-    return outs, ins, nets
+# heterogeneity_solver.jl:316-375 from the engine's paths on lr.grid: `r` is what
+# SBREngine.hetero_equilibrium_on_knots returned for this result (AW_total, AW_OUT, AW_IN)
+function _get_AW_hetero(result::SolvedModelHetero, r)
+    result.bankrun || return nothing
+    t_grid = result.learning_results.grid
+    K = size(r.AW_OUT, 2)
+    outs = Any[LinearInterpolation(t_grid, r.AW_OUT[:, k]) for k in 1:K]
+    ins = Any[LinearInterpolation(t_grid, r.AW_IN[:, k]) for k in 1:K]
+    nets = Any[LinearInterpolation(t_grid, r.AW_OUT[:, k] .- r.AW_IN[:, k]) for k in 1:K]
+    return (AW_cum = LinearInterpolation(t_grid, r.AW_total), AW_OUT_groups = outs, AW_IN_groups = ins,
+            AW_groups = nets, AW_max = maximum(r.AW_total))
 end
 
-# heterogeneity_solver.jl:316-375 (host restatement; the engine's AW_total is used when present)
-function get_AW_hetero(result::SolvedModelHetero, AW_total = nothing)
+# heterogeneity_solver.jl:316-375 for a SolvedModelHetero built elsewhere: one engine call on its
+# learning results' knots (the equilibrium is re-solved on the GPU, its paths returned)
+function get_AW_hetero(result::SolvedModelHetero)
     result.bankrun || return nothing
     lr = result.learning_results
-    t_grid = lr.grid
-    dist = result.model_params.learning.dist
-    outs, ins, nets = _hetero_group_curves(result.ξ, result.τ_bar_IN_UNCs, result.τ_bar_OUT_UNCs,
-                                           lr.learning_cdfs, t_grid)
-    if AW_total === nothing
-        AW_total = zeros(length(t_grid))
-        for k in eachindex(dist)
-            AW_total .+= dist[k] .* nets[k].itp.coefs
-        end
-    end
-    return (AW_cum = LinearInterpolation(t_grid, AW_total), AW_OUT_groups = outs, AW_IN_groups = ins,
-            AW_groups = nets, AW_max = maximum(AW_total))
+    lp = lr.params
+    econ = result.model_params.economic
+    Gm = reduce(hcat, [cdf.itp.coefs for cdf in lr.learning_cdfs])
+    r = SBREngine.hetero_equilibrium_on_knots(sbr_context(), collect(Float64, lr.grid), Gm, lp.βs, lp.dist,
+                                              econ.u; η = econ.η, tspan_end = lp.tspan[2], p = econ.p, κ = econ.κ,
+                                              λ = econ.λ)
+    return _get_AW_hetero(result, r)
 end
 
 # heterogeneity_solver.jl:241-293 — one GPU solve on lr_hetero's own knots and group CDFs
@@ -101,7 +98,7 @@ function solve_equilibrium_hetero(lr_hetero::LearningResultsHetero, econ::Econom
     converged = (r.status & SBREngine.SBR_CONVERGED) != 0
     result = SolvedModelHetero(r.ξ, r.τ_bar_IN_UNCs, r.τ_bar_OUT_UNCs, HRs, bankrun, econ, lr_hetero, converged,
                                time() - solve_start, r.tolerance)
-    bankrun && (result.aw[] = get_AW_hetero(result, r.AW_total))
+    bankrun && (result.aw[] = _get_AW_hetero(result, r))
     verbose && println(bankrun ? "Converged: ξ = $(result.ξ), tolerance = $(result.tolerance)" :
                                  "No valid run equilibrium exists (status 0x$(string(r.status, base = 16)))")
     return result

@@ -381,7 +381,8 @@ end
 group CDF values `Gm` (n × K: column k = `learning_cdfs[k]`'s coefficients): no learning ODE.
 Knots, CDFs and the K hazard paths stay on the GPU while the inputs repeat.  Returns ξ, the
 per-group buffers, AW_max, the tolerance, the status, the hazard grid τ̄ with HR_k(τ̄) as the
-columns of `HR` (the reference's `HRs`, :255) and `AW_total` on the knots (NaN without a run).
+columns of `HR` (the reference's `HRs`, :255), `AW_total` on the knots and get_AW_hetero's
+per-group curves `AW_OUT` / `AW_IN` (n × K, column k = group k, :335-362) — NaN without a run.
 """
 function hetero_equilibrium_on_knots(ctx::Context, t::Vector{Float64}, Gm::AbstractMatrix, βs, dist, u; η, tspan_end,
                                      p = 0.9, κ = 0.3, λ = 0.1)
@@ -393,30 +394,32 @@ function hetero_equilibrium_on_knots(ctx::Context, t::Vector{Float64}, Gm::Abstr
     res = fill(NaN, 5); st = UInt32[0]; it = Int32[0]; nt = Ref{Int64}(0)
     tin = zeros(Float64, K); tout = zeros(Float64, K)
     hr = Matrix{Float64}(undef, cap, K); aw = Vector{Float64}(undef, n)
+    awg = Matrix{Float64}(undef, cap, 2K)          # columns: AW_OUT_1..K, AW_IN_1..K (stride cap)
     uv = Float64[u]
     opts = Ref(Opts(; early_exit = 0))
-    GC.@preserve t Gk b d uv res st it tin tout hr aw begin
+    GC.@preserve t Gk b d uv res st it tin tout hr aw awg begin
         soa = Ref(ResultSoA(pointer(res, 1), C_NULL, C_NULL, pointer(res, 4), pointer(res, 5), pointer(st),
                             pointer(it)))
         rc = ccall((:sbr_hetero_equilibrium_on_knots, libsbr), Cint,
                    (Ptr{Cvoid}, Int32, Ptr{Float64}, Ptr{Float64}, Int64, Ptr{Float64}, Ptr{Float64}, Float64,
                     Float64, Ptr{Float64}, Int64, Float64, Float64, Float64, Ref{Opts}, Ref{ResultSoA},
-                    Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Int64, Ref{Int64}),
+                    Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Int64, Ref{Int64}),
                    ctx.ptr, Int32(K), t, Gk, n, b, d, η, tspan_end, uv, 1, p, κ, λ, opts, soa, tin, tout, hr, aw,
-                   cap, nt)
+                   awg, cap, nt)
         check(ctx, rc)
     end
     k = nt[]
     return (ξ = res[1], AW_max = res[4], tolerance = res[5], status = st[1], τ_bar_IN_UNCs = tin,
             τ_bar_OUT_UNCs = tout, τ_bar = k > 0 ? vcat(t[t .<= η], η)[1:k] : Float64[], HR = hr[1:k, :],
-            AW_total = aw)
+            AW_total = aw, AW_OUT = awg[1:n, 1:K], AW_IN = awg[1:n, K+1:2K])
 end
 
 """
     solve_hetero_point_paths(ctx, βs, dist, u; η, tspan_end, x0 = 1e-4, p = 0.9, κ = 0.3, λ = 0.1)
 
 One heterogeneity equilibrium with the learning knots `t`, the group CDFs `G` (n × K), the
-per-group buffers and `AW_total` on the knots (`get_AW_functions_hetero!`).
+per-group buffers, `AW_total` on the knots (`get_AW_functions_hetero!`) and the per-group
+curves `AW_OUT` / `AW_IN` (n × K, get_AW_hetero :335-362).
 """
 function solve_hetero_point_paths(ctx::Context, βs, dist, u; η, tspan_end, x0 = 1e-4, p = 0.9, κ = 0.3, λ = 0.1,
                                   cap = 1 << 16)
@@ -424,18 +427,20 @@ function solve_hetero_point_paths(ctx::Context, βs, dist, u; η, tspan_end, x0 
     res = zeros(Float64, 3); st = Ref{UInt32}(0); nk = Ref{Int64}(0)
     tin = zeros(Float64, K); tout = zeros(Float64, K)
     t = Vector{Float64}(undef, cap); G = Vector{Float64}(undef, cap * K); aw = similar(t)
+    awg = Matrix{Float64}(undef, cap, 2K)
     opts = Ref(Opts(; early_exit = 0))
-    GC.@preserve b d res tin tout t G aw begin
+    GC.@preserve b d res tin tout t G aw awg begin
         rc = ccall((:sbr_hetero_point_paths, libsbr), Cint,
                    (Ptr{Cvoid}, Int32, Ptr{Float64}, Ptr{Float64}, Float64, Float64, Float64, Float64, Float64,
                     Float64, Float64, Ref{Opts}, Ptr{Float64}, Ref{UInt32}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
-                    Ptr{Float64}, Ptr{Float64}, Int64, Ref{Int64}),
-                   ctx.ptr, K, b, d, η, tspan_end, x0, u, p, κ, λ, opts, res, st, tin, tout, t, G, aw, cap, nk)
+                    Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Int64, Ref{Int64}),
+                   ctx.ptr, K, b, d, η, tspan_end, x0, u, p, κ, λ, opts, res, st, tin, tout, t, G, aw, awg, cap, nk)
         check(ctx, rc)
     end
     n = nk[]
     return (ξ = res[1], AW_max = res[2], tolerance = res[3], status = st[], τ_bar_IN_UNCs = tin,
-            τ_bar_OUT_UNCs = tout, t = t[1:n], G = permutedims(reshape(G[1:n*K], K, n)), AW_total = aw[1:n])
+            τ_bar_OUT_UNCs = tout, t = t[1:n], G = permutedims(reshape(G[1:n*K], K, n)), AW_total = aw[1:n],
+            AW_OUT = awg[1:n, 1:K], AW_IN = awg[1:n, K+1:2K])
 end
 
 end # module

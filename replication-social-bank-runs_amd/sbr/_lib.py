@@ -99,7 +99,7 @@ _SIGS = {
     "sbr_equilibrium_on_knots_pdf": (ctypes.c_int, [_P, _P, _P, _P, _I64, _D, _D, _P, _I64, _D, _D, _D, _P, _P, _P,
                                                     _P, _P, _P, _P, _I64, _P]),
     "sbr_hetero_equilibrium_on_knots": (ctypes.c_int, [_P, _I32, _P, _P, _I64, _P, _P, _D, _D, _P, _I64, _D, _D, _D,
-                                                       _P, _P, _P, _P, _P, _P, _I64, _P]),
+                                                       _P, _P, _P, _P, _P, _P, _P, _I64, _P]),
     "sbr_apply_early_exit": (None, [_I64, _I64, _I32, _P]),
     "sbr_selftest_detmath": (ctypes.c_int, [_P, _P, _P, ctypes.c_int, _P, _P, _P]),
     "sbr_timing_enable": (ctypes.c_int, [_P, ctypes.c_int]),
@@ -127,7 +127,7 @@ _SIGS = {
                                               ctypes.c_int32, _P, _P, _P, _P, _P, _P, _P, _I64, _P]),
     "sbr_learn_hetero": (ctypes.c_int, [_P, _I32, _P, _P, _P, _D, _I64, _P, _P, _P, _I64, _P, _P]),
     "sbr_hetero_point_paths": (ctypes.c_int, [_P, ctypes.c_int32, _P, _P, _D, _D, _D, _D, _D, _D, _D, _P, _P, _P,
-                                              _P, _P, _P, _P, _P, _I64, _P]),
+                                              _P, _P, _P, _P, _P, _P, _I64, _P]),
     "sbr_interest_point_paths": (ctypes.c_int, [_P, _D, _D, _D, _D, _D, _D, _D, _D, _D, _D, _P, _P, _P, _P, _P, _P,
                                                 _P, _I64, _P, _P]),
     "sbr_sweep_interest": (ctypes.c_int, [_P, _P, _P, _P, _D, _P, _I64, _I64, _D, _D, _D, _D, _D, _P, _P, _P]),

@@ -323,7 +323,8 @@ class Engine:
         LearningResultsHetero holds (t [n], G [n, K] = the learning_cdfs' values) for each u — no
         learning ODE (sbr_hetero_equilibrium_on_knots; knots, CDFs and the K hazards stay on the
         GPU while the inputs repeat).  Per-u arrays, buffers [n_u, K]; with ``paths`` (one u) HR_k
-        on the τ̄ grid [K, n_tau] and AW_total on the knots."""
+        on the τ̄ grid [K, n_tau], AW_total on the knots and get_AW_hetero's per-group curves
+        aw_out / aw_in [K, n] (heterogeneity_solver.jl:335-362; NaN without a run)."""
         t = np.ascontiguousarray(t, np.float64)
         G = np.ascontiguousarray(G, np.float64)
         betas = np.ascontiguousarray(betas, np.float64)
@@ -343,17 +344,18 @@ class Engine:
         cap = n + 1
         hr = np.empty((K, cap)) if paths else None
         aw = np.empty(cap) if paths else None
+        awg = np.empty((2 * K, cap)) if paths else None
         nt = ctypes.c_int64()
         opts = _lib.default_opts(early_exit_nan_run=0, flags=_lib.SBR_FLAG_EXHAUSTIVE if exhaustive else 0)
         rc = self._L.sbr_hetero_equilibrium_on_knots(self._ctx, K, _ptr(t), _ptr(G), n, _ptr(betas), _ptr(dist), eta,
                                                      t_end, _ptr(u), nu, p, kappa, lam, ctypes.byref(opts),
                                                      ctypes.byref(soa), _ptr(tin), _ptr(tout), _ptr(hr), _ptr(aw),
-                                                     cap, ctypes.byref(nt))
+                                                     _ptr(awg), cap, ctypes.byref(nt))
         check(rc, self._ctx, "sbr_hetero_equilibrium_on_knots")
         out.update(tau_in_unc=tin, tau_out_unc=tout)
         if paths:
             k = nt.value
-            out.update(hr=hr[:, :k], aw_total=aw[:n], n_tau=k)
+            out.update(hr=hr[:, :k], aw_total=aw[:n], aw_out=awg[:K, :n], aw_in=awg[K:, :n], n_tau=k)
         return out
 
     def sweep_hetero(self, betas, dist, eta, t_end, u, p, kappa, lam, x0=1e-4, knot_capacity: int = 16384,
@@ -529,7 +531,8 @@ class Engine:
 
     def hetero_point_paths(self, betas, dist, eta, t_end, u, p, kappa, lam, x0=1e-4, cap=65536) -> dict:
         """One heterogeneity equilibrium with learning knots t, group CDFs G [n, K], the
-        per-group buffers and AW_total(t) — what scripts/2_heterogeneity.jl plots."""
+        per-group buffers, AW_total(t) and the per-group AW_OUT_k / AW_IN_k curves on the knots
+        (aw_out / aw_in [K, n]) — what scripts/2_heterogeneity.jl plots."""
         betas = np.ascontiguousarray(betas, np.float64)
         dist = np.ascontiguousarray(dist, np.float64)
         K = len(dist)
@@ -537,15 +540,17 @@ class Engine:
         st = np.zeros(1, np.uint32)
         tin, tout = np.empty(K), np.empty(K)
         t, G, aw = np.empty(cap), np.empty(cap * K), np.empty(cap)
+        awg = np.empty((2 * K, cap))
         nk = ctypes.c_int64()
         opts = _lib.default_opts(early_exit_nan_run=0, knot_capacity=16384)
         rc = self._L.sbr_hetero_point_paths(self._ctx, K, _ptr(betas), _ptr(dist), eta, t_end, x0, u, p, kappa, lam,
                                             ctypes.byref(opts), _ptr(res), _ptr(st), _ptr(tin), _ptr(tout), _ptr(t),
-                                            _ptr(G), _ptr(aw), cap, ctypes.byref(nk))
+                                            _ptr(G), _ptr(aw), _ptr(awg), cap, ctypes.byref(nk))
         check(rc, self._ctx, "sbr_hetero_point_paths")
         n = nk.value
         return dict(xi=res[0], aw_max=res[1], tol=res[2], status=int(st[0]), tau_in_unc=tin, tau_out_unc=tout,
-                    t=t[:n].copy(), G=G[:n * K].reshape(n, K).copy(), aw_total=aw[:n].copy())
+                    t=t[:n].copy(), G=G[:n * K].reshape(n, K).copy(), aw_total=aw[:n].copy(),
+                    aw_out=awg[:K, :n].copy(), aw_in=awg[K:, :n].copy())
 
     def interest_point_paths(self, beta, eta, t_end, u, p, kappa, lam, r, delta, x0=1e-4, cap=65536) -> dict:
         """One interest-rate equilibrium with τ̄, HR(τ̄), V(τ̄) (saved on the HR grid) and
@@ -864,6 +869,22 @@ class SolvedModelHetero:
     AW_max: float = float("nan")
     HRs: list = field(repr=False, default_factory=list)  # HR_k on the τ̄ grid (heterogeneity_solver.jl:255)
     learning_results: object = field(repr=False, default=None)
+    # get_AW_hetero's per-group curves on the knots, from the engine (heterogeneity_solver.jl:335-362)
+    AW_OUT_groups: np.ndarray = field(repr=False, default=None)  # [K, n]
+    AW_IN_groups: np.ndarray = field(repr=False, default=None)   # [K, n]
+
+    def get_AW_functions_hetero(self):
+        """get_AW_functions_hetero! (heterogeneity_solver.jl:386-402): (AW_cum, AW_OUT_groups,
+        AW_IN_groups, AW_groups, AW_max) as interpolants on the knots, None without a run.
+        AW_groups = AW_OUT_k − AW_IN_k as get_AW_hetero forms them (:358)."""
+        if not self.bankrun:
+            return None
+        t = self.t
+        outs = [LinearInterpolation(t, self.AW_OUT_groups[k]) for k in range(len(self.AW_OUT_groups))]
+        ins = [LinearInterpolation(t, self.AW_IN_groups[k]) for k in range(len(self.AW_IN_groups))]
+        nets = [LinearInterpolation(t, self.AW_OUT_groups[k] - self.AW_IN_groups[k]) for k in range(len(outs))]
+        return dict(AW_cum=LinearInterpolation(t, self.AW_total), AW_OUT_groups=outs, AW_IN_groups=ins,
+                    AW_groups=nets, AW_max=self.AW_max)
 
 
 @dataclass
@@ -919,4 +940,4 @@ def solve_equilibrium_hetero(lr_or_model, econ: EconomicParameters | None = None
     HRs = [LinearInterpolation(tau, r["hr"][k]) for k in range(len(lp.dist))] if r["n_tau"] else []
     return SolvedModelHetero(float(r["xi"][0]), r["tau_in_unc"][0], r["tau_out_unc"][0], bool(st & _lib.SBR_RUN),
                              bool(st & _lib.SBR_CONVERGED), float(r["tol"][0]), st, lr.grid, lr.G, r["aw_total"],
-                             float(r["aw_max"][0]), HRs, lr)
+                             float(r["aw_max"][0]), HRs, lr, r["aw_out"], r["aw_in"])

@@ -157,11 +157,14 @@ def test_social_point_paths_bitwise(engine, oracle):
             assert x.shape == y.shape and np.array_equal(x, y, equal_nan=True), (b, uu, k)
 
 
-def test_social_config5_sample_full_workload(engine, golden):
+@pytest.mark.parametrize("fixture", ["config5_sample.npz", "config5_sample_1024.npz"])
+def test_social_config5_sample_full_workload(engine, golden, fixture):
     """BASELINE config 5 at its stated workload (tol 1e-4, max_iter 500) on an 8 β × 4 u
-    sample of the 512² axes, incl. the corner β = 100, u = 0.001: bit for bit against the
-    oracle's fixed points (tests/golden/config5_sample.npz, tools/make_config5_sample.py)."""
-    gold = golden("config5_sample.npz")
+    sample of the 512² axes, incl. the corner β = 100, u = 0.001, and on the stratified
+    1,024-point sample (every 16th β × every 16th u, corner included): bit for bit against
+    the oracle's fixed points (tests/golden/config5_sample*.npz, tools/make_config5_sample.py
+    [--stride 16]) on every field, status bit, bisection and fixed-point iteration count."""
+    gold = golden(fixture)
     cmp = np.stack([sbr.julia_range(0.0, ETA, 1000)] * len(gold["beta"]))
     g = engine.sweep_social(gold["beta"], ETA, gold["u"], P, KAPPA, LAM, cmp=cmp, tol=1e-4, max_iter=500)
     for k in FIELDS:

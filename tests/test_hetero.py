@@ -94,13 +94,14 @@ def test_hetero_aw_branch_and_bound_equals_exhaustive(engine, oracle):
 @pytest.mark.gpu
 def test_hetero_point_paths_bitwise(engine, oracle):
     """sbr_hetero_point_paths (the script point with its plotted paths: learning knots, the
-    group CDFs, per-group buffers, AW_total on the knots) == the oracle bit for bit."""
+    group CDFs, per-group buffers, AW_total and get_AW_hetero's per-group AW_OUT_k / AW_IN_k
+    on the knots) == the oracle bit for bit."""
     g = sbr.hetero_script_grid()
     for u in (g.u[0], 0.9):
         a = engine.hetero_point_paths(g.betas[0], g.dist, g.eta[0], g.t_end[0], u, g.p, g.kappa, g.lam)
         b = oracle.hetero_point_paths(g.betas[0], g.dist, g.eta[0], g.t_end[0], u, g.p, g.kappa, g.lam)
         assert a["status"] == b["status"], u
-        for k in ("xi", "aw_max", "tol", "tau_in_unc", "tau_out_unc", "t", "G", "aw_total"):
+        for k in ("xi", "aw_max", "tol", "tau_in_unc", "tau_out_unc", "t", "G", "aw_total", "aw_out", "aw_in"):
             x, y = np.atleast_1d(a[k]), np.atleast_1d(b[k])
             assert x.shape == y.shape and np.array_equal(x, y, equal_nan=True), (u, k)
         if a["status"] & sbr.STATUS["SBR_RUN"]:
@@ -131,12 +132,21 @@ def test_hetero_point_paths_oracle_figure(oracle, golden):
     assert r["status"] & sbr.STATUS["SBR_RUN"]
     assert np.nanmax(r["aw_total"]) == r["aw_max"]
     assert r["G"].shape == (len(r["t"]), len(g.dist))
+    # the per-group curves fold into AW_total in get_AW_hetero's order (:356-358: AW_cum .+=
+    # dist[k] .* (AW_OUT_k .- AW_IN_k), k = 1..K), bit for bit
+    cum = np.zeros(len(r["t"]))
+    for k in range(len(g.dist)):
+        cum = cum + g.dist[k] * (r["aw_out"][k] - r["aw_in"][k])
+    assert np.array_equal(cum, r["aw_total"])
+    # AW_OUT_k / AW_IN_k are group CDF values (0 where the shifted time is negative)
+    assert (r["aw_out"] >= 0).all() and (r["aw_in"] >= 0).all() and (r["aw_in"] <= r["aw_out"] + 1e-12).all()
 
 
 @pytest.mark.gpu
 def test_hetero_reference_call_surface(engine, oracle):
     """scripts/2_heterogeneity.jl through the host mirror: ModelParametersHetero →
-    solve_equilibrium_hetero (learning + equilibrium + AW paths), equal to the oracle."""
+    solve_equilibrium_hetero (learning + equilibrium + AW paths) and get_AW_functions_hetero!
+    (every curve from the engine), equal to the oracle."""
     g = sbr.hetero_script_grid()
     m = sbr.ModelParametersHetero.make(g.betas[0], g.dist, eta_bar=30.0, u=float(g.u[0]), p=g.p, kappa=g.kappa,
                                        lam=g.lam)
@@ -145,6 +155,12 @@ def test_hetero_reference_call_surface(engine, oracle):
                                   g.kappa, g.lam)
     assert r.status == o["status"] and r.xi == o["xi"] and r.AW_max == o["aw_max"]
     assert np.array_equal(r.AW_total, o["aw_total"])
+    aw = r.get_AW_functions_hetero()
+    assert aw["AW_max"] == o["aw_max"] and np.array_equal(aw["AW_cum"].coefs, o["aw_total"])
+    for k in range(len(g.dist)):
+        assert np.array_equal(aw["AW_OUT_groups"][k].coefs, o["aw_out"][k]), k
+        assert np.array_equal(aw["AW_IN_groups"][k].coefs, o["aw_in"][k]), k
+        assert np.array_equal(aw["AW_groups"][k].coefs, o["aw_out"][k] - o["aw_in"][k]), k
 
 
 @pytest.mark.gpu
@@ -206,8 +222,8 @@ def test_hetero_batch_ordered_on_torch_default_stream(engine):
 def test_hetero_config4_full_properties_and_strided_columns(engine, oracle):
     """BASELINE config 4 at its stated size (K = 8, 1024 × 1024 = 1,048,576 equilibria) on
     the GPU: every learning column switches to Rosenbrock23 (AutoSwitch, handled); size-
-    independent properties over the whole grid; 64 strided columns (every 16th, all 1024 u:
-    65,536 equilibria) bit for bit against the oracle's sweep_hetero."""
+    independent properties over the whole grid; 128 strided columns (every 8th, all 1024 u:
+    131,072 equilibria, 12.5 % of the grid) bit for bit against the oracle's sweep_hetero."""
     g = sbr.hetero_config4(1024, 1024, 8)
     r = engine.sweep_hetero(g.betas, g.dist, g.eta, g.t_end, g.u, g.p, g.kappa, g.lam, g.x0, with_groups=False)
     st = r["status"]
@@ -233,12 +249,12 @@ def test_hetero_config4_full_properties_and_strided_columns(engine, oracle):
     # AW(ξ*) = κ within the bisection tolerance, so the path maximum is at least κ
     assert (r["aw_max"][run] >= g.kappa - 1e-12).all()
     assert 0.5 < run.mean() < 1.0
-    # 64 strided columns (every 16th), every u, bit for bit
-    sub = g.subset(np.arange(0, 1024, 16))
+    # 128 strided columns (every 8th), every u, bit for bit
+    sub = g.subset(np.arange(0, 1024, 8))
     o = oracle.sweep_hetero(sub.betas, sub.dist, sub.eta, sub.t_end, sub.u, sub.p, sub.kappa, sub.lam, sub.x0,
                             nthreads=16)
     for f in ("xi", "aw_max", "tol", "status", "iters"):
-        a, b = r[f][::16], o[f]
+        a, b = r[f][::8], o[f]
         same = (a == b) | (np.isnan(a) & np.isnan(b)) if a.dtype.kind == "f" else (a == b)
         assert same.all(), (f, int((~same).sum()))
     # the learning of a strided column: knots bit for bit, Rosenbrock23 steps taken
