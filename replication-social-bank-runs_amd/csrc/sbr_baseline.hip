@@ -65,8 +65,20 @@ __global__ __launch_bounds__(LB) void learn_logistic_kernel(const double* __rest
     // latency-bound (one serial ODE per lane): take issue priority over co-resident
     // equilibrium waves of a previous batch
     __builtin_amdgcn_s_setprio(3);
-    // one column per lane (a knot store or load of the wave touches one row per active lane)
-    const int b = blockIdx.x * LB + threadIdx.x;
+    // one column per lane (a knot store or load of the wave touches one row per active lane).
+    // Heads first (a.wpg, one-wave blocks): the workgroup dispatcher deals consecutive blocks
+    // round-robin over the XCDs and their CUs, so every grid's first wave — block g·32 of a
+    // 2048-column grid — landed on one of only 8 CUs, three heads per CU, and those waves hold
+    // the longest columns of a β-descending grid (config 3: column 22, 4.45k steps against a
+    // 2.9k median).  Dealt first, each head has a CU to itself: a 20-grid launch 4.2-4.7 →
+    // 3.0-3.2 ms (tools/ubench_fill.hip).
+    int blk = blockIdx.x;
+    if (LB == 64 && a.wpg) {
+        const int nh = (a.n_beta / (64 * a.wpg)) * a.head, per = a.wpg - a.head;
+        blk = blk < nh ? (blk / a.head) * a.wpg + blk % a.head
+                       : ((blk - nh) / per) * a.wpg + a.head + (blk - nh) % per;
+    }
+    const int b = blk * LB + threadIdx.x;
     const bool live = b < a.n_beta;
     const double BETA = live ? beta[b] : 1.0, ETA = live ? eta[b] : 1.0, T1 = live ? t_end[b] : 1.0, T0 = 0.0;
     const size_t row = (size_t)(live ? b : 0) * (size_t)L.cap;
@@ -2072,16 +2084,21 @@ hipError_t launch_point_coop(const LearnBufs& L, const double* eta, const double
 hipError_t launch_learn_kernel(const double* beta, const double* eta, const double* t_end, const LearnArgs& a,
                                const LearnBufs& L, hipStream_t s, int mode)
 {
+    const unsigned waves = (unsigned)((a.n_beta + 63) / 64);
+    // heads first: whole grids of one-wave blocks only
+    if (a.wpg && (mode == 0 || a.wpg < 2 || a.head < 1 || a.head >= a.wpg || a.n_beta % (64 * a.wpg) != 0))
+        return hipErrorInvalidValue;
     if (mode == 2) { // LDS-staged rows with the fused hazard (launch_hazard_norm after)
         if (!a.fuse_hazard) return hipErrorInvalidValue;
-        hipLaunchKernelGGL((learn_logistic_kernel<64, true>), dim3((a.n_beta + 63) / 64), dim3(64), kStageLdsPerWave, s,
+        hipLaunchKernelGGL((learn_logistic_kernel<64, true>), dim3(waves), dim3(64), kStageLdsPerWave, s,
                            beta, eta, t_end, a, L);
     } else if (mode == 0) {
         hipLaunchKernelGGL(learn_logistic_kernel<kLearnBlock>, dim3((a.n_beta + kLearnBlock - 1) / kLearnBlock),
                            dim3(kLearnBlock), 0, s, beta, eta, t_end, a, L);
     } else {
-        hipLaunchKernelGGL(learn_logistic_kernel<kLearnBlockLat>, dim3((a.n_beta + kLearnBlockLat - 1) / kLearnBlockLat),
-                           dim3(kLearnBlockLat), 0, s, beta, eta, t_end, a, L);
+        static_assert(kLearnBlockLat == 64, "mode 1 runs one-wave blocks");
+        hipLaunchKernelGGL(learn_logistic_kernel<kLearnBlockLat>, dim3(waves), dim3(kLearnBlockLat), 0, s, beta, eta,
+                           t_end, a, L);
     }
     return hipGetLastError();
 }

@@ -35,6 +35,10 @@ struct LearnArgs {
     // hazard_kernel: the learning pdf's values on the knots (sbr_equilibrium_on_knots_pdf, e.g. the
     // social extension's (1 − G)·β·AW_{n−1}); null: compute_pdf_symbolic_baseline's βG(1 − G)
     const double* pdf = nullptr;
+    // learn_logistic_kernel in one-wave blocks over grids of wpg waves each (n_beta = grids ×
+    // wpg × 64, wpg > head): the first head waves of every grid take the launch's first blocks,
+    // the other waves follow (0: block order = wave order)
+    int32_t head = 0, wpg = 0;
 };
 
 // The equilibrium side of a readiness sweep (eq_ready_kernel): one workgroup per item, each
