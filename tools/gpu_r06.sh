@@ -41,7 +41,7 @@ for s in ${STEPS:-tests smoke bench}; do
     multihost) run multihost 300 python -u bench.py --workload multihost --steps 10 --warmup 2 ;;
     pmcall) for w in ${PMCW:-base hetero interest socbulk soclone}; do
               case $w in
-                base) BA="--steps 4 --warmup 2" ;;
+                base) BA="--steps 20 --warmup 5" ;;
                 hetero) BA="--workload hetero --steps 2 --warmup 1" ;;
                 interest) BA="--workload interest --steps 1 --warmup 1" ;;
                 socbulk) BA="--workload social --steps 1 --warmup 0 --social-max-iter 16" ;;
