@@ -243,12 +243,14 @@ def test_device_info(engine):
     assert info["lds_knot_capacity"] >= 3400  # every config-3 column staged in LDS
 
 
-@pytest.mark.parametrize("ncol,group", [(384, None), (1200, None), (384, 3), (1200, 2)])
+@pytest.mark.parametrize("ncol,group", [(384, None), (1200, None), (1536, None), (384, 3), (1200, 2)])
 def test_pipelined_batches_equal_single_sweeps(engine, ncol, group):
     """sbr_sweep_baseline_batch_dev returns for every batch exactly what a single sweep of that
     grid returns.  By default the 11 grids are learned in one launch (≤ one wave per SIMD) and
     solved by equilibrium launches of ⌈4096 / n_β⌉ grids (384 columns: 11 grids in one launch;
-    1200: three launches of 4, 4, 3).  With a workspace budget of `group` grids per learning
+    1200: three launches of 4, 4, 3).  The learning launch deals every grid's first wave first
+    where grids are whole waves (384: 6 waves per grid, 1536: 24) and stages its rows through LDS
+    from 256 waves on (1536: 264 waves, the wide launch of the config-3 bench).  With a workspace budget of `group` grids per learning
     launch (sbr_set_batch_workspace) the batch runs in groups — 384: four groups of 3, 3, 3, 2;
     1200: six of 2, ..., 1 — learned into two alternating workspaces, each group beside the
     previous group's equilibria, so each workspace is reused behind its readers."""
