@@ -432,7 +432,9 @@ void sbr_apply_early_exit(int64_t n_beta, int64_t n_u, int32_t threshold, sbr_re
  * learning and equilibrium kernels of every baseline sweep call while
  * enabled; sbr_timing_read synchronises `stream` (NULL = the HIP null stream),
  * returns the summed milliseconds per kernel and the number of calls, and
- * resets the accumulators.  This and the other per-device diagnostics below
+ * resets the accumulators.  A pipelined batch times each learning group's equilibrium
+ * launches as one span (first start to last end, the gaps between them included) that counts
+ * as that many calls.  This and the other per-device diagnostics below
  * (sbr_learn_stats, sbr_hetero_learn_stats, sbr_social_prof_read,
  * sbr_social_overflow_stats) return SBR_EARG on an n-device context: call them
  * on sbr_multi_child(ctx, rank). */

@@ -133,6 +133,7 @@ struct sbr_ctx {
     struct TRec {
         int kind; // 0 learning (+ hazard), 1 equilibrium
         hipEvent_t a, b;
+        int count; // launches the span covers (a pipelined batch times its equilibria as one span)
     };
     std::vector<TRec> trec;
     // phases of the last host-pointer baseline sweep while timing is enabled (sbr_host_phases):
@@ -456,23 +457,23 @@ hipEvent_t tstart(sbr_ctx* c, hipStream_t s)
     return e;
 }
 
-void tend(sbr_ctx* c, hipStream_t s, int kind, hipEvent_t a)
+void tend(sbr_ctx* c, hipStream_t s, int kind, hipEvent_t a, int count = 1)
 {
     if (!c->timing || !a) return;
     hipEvent_t e = next_event(c);
     if (!e) return;
     (void)hipEventRecord(e, s);
-    c->trec.push_back({kind, a, e});
+    c->trec.push_back({kind, a, e, count});
 }
 
 int launch_eq(sbr_ctx* c, hipStream_t s, const sbr::LearnBufs& L, const double* eta, const double* t_end,
               const double* u, int64_t n_beta, int64_t n_u, double kappa, const sbr_opts& o,
-              const sbr::ResultSoA& out, double* aw_path, int group = 1)
+              const sbr::ResultSoA& out, double* aw_path, int group = 1, bool timed = true)
 {
     sbr::EqArgs ea{kappa, (int32_t)n_u, o.bisect_max_iters, c->lds_cap_b, aw_path,
                    (o.flags & SBR_FLAG_EXHAUSTIVE) ? 1 : 0, (o.flags >> 8) & 7};
     ea.group = group;
-    hipEvent_t t0 = tstart(c, s);
+    hipEvent_t t0 = timed ? tstart(c, s) : nullptr;
     if (aw_path && n_beta == 1 && n_u == 1) { // single point with its path: the whole workgroup on it
         ea.lds_cap = c->lds_cap;
         HIP_TRY(c, sbr::launch_point_coop(L, eta, t_end, u, ea, out, s), SBR_EDEVICE);
@@ -1041,6 +1042,10 @@ int sbr_sweep_baseline_batch_dev(sbr_ctx* c, void* stream, int64_t n_batch, cons
             // normalisation of its own columns: the normalisations (HBM streams) run ahead on hs,
             // overlapped with the previous equilibrium launch; only the first one is exposed
             const int64_t ne = (gn + P.E - 1) / P.E, Eg = (gn + ne - 1) / ne;
+            // timing (sbr_timing_enable): one span over the group's equilibrium launches, from
+            // the first one's start to the last one's end, counted as ne launches — two timing
+            // events per launch between back-to-back launches cost ≈1 % of the step
+            hipEvent_t te = nullptr;
             for (int64_t e0 = 0; e0 < gn; e0 += Eg) {
                 const int64_t en = (gn - e0) < Eg ? (gn - e0) : Eg;
                 const sbr::LearnBufs We = learn_rows(W, (size_t)(e0 * n_beta));
@@ -1049,17 +1054,19 @@ int sbr_sweep_baseline_batch_dev(sbr_ctx* c, void* stream, int64_t n_batch, cons
                 hipEvent_t eh = c->ev_hn[(size_t)k_hn++];
                 HIP_TRY(c, hipEventRecord(eh, hs), SBR_EDEVICE);
                 HIP_TRY(c, hipStreamWaitEvent(es, eh, 0), SBR_EDEVICE);
+                if (e0 == 0) te = tstart(c, es);
                 // column i·n_beta + j of the launch is grid g0+e0+i's column j: eta / t_end and
                 // every out field are [n_batch × n_beta (× n_u)] contiguous
                 sbr::ResultSoA r{out->xi + gg * np, out->tau_in_unc + gg * np, out->tau_out_unc + gg * np,
                                  out->aw_max + gg * np, out->tol + gg * np, out->status + gg * np,
                                  out->iters ? out->iters + gg * np : nullptr};
                 rc = launch_eq(c, es, We, eta + gg * n_beta, t_end + gg * n_beta, u, en * n_beta, n_u, kappa, o, r,
-                               nullptr, (int)en);
+                               nullptr, (int)en, false);
                 if (rc) return rc;
                 for (int64_t i = 0; i < en; i++) HIP_TRY(c, hipEventRecord(c->ev_grid[gg + i], es), SBR_EDEVICE);
                 c->n_grid = gg + en;
             }
+            tend(c, es, 1, te, (int)ne);
             HIP_TRY(c, hipEventRecord(c->ev_eq[slot], es), SBR_EDEVICE);
             c->last_slot = slot;
             c->last_off = (gn - 1) * n_beta;
@@ -1874,7 +1881,7 @@ int sbr_timing_read(sbr_ctx* c, void* stream, double* learn_ms, double* eq_ms, i
         float t = 0.f;
         HIP_TRY(c, hipEventElapsedTime(&t, r.a, r.b), SBR_EDEVICE);
         if (r.kind == 0) a += t;
-        else { b += t; n++; }
+        else { b += t; n += r.count; }
     }
     if (learn_ms) *learn_ms = a;
     if (eq_ms) *eq_ms = b;
