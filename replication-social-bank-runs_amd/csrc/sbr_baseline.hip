@@ -210,6 +210,7 @@ __global__ __launch_bounds__(LB) void learn_logistic_kernel(const double* __rest
         const LearnBufs* Lp;
         const LearnArgs* ap;
         int b;
+        int ntau_out; // the τ̄ entries of the column, set by finish
         __device__ __forceinline__ void finish(const OdeOut& o)
         {
             if (STAGE) // the entries not flushed yet: knots [fl, n), τ̄ entries [fl, hm)
@@ -236,6 +237,7 @@ __global__ __launch_bounds__(LB) void learn_logistic_kernel(const double* __rest
             Lp->n_knots[b] = n;
             Lp->n_le[b] = n_le;
             if (fuse) Lp->n_tau[b] = n_tau;
+            ntau_out = n_tau;
             Lp->status[b] = st;
             Lp->n_accept[b] = (int)o.naccept;
             Lp->n_reject[b] = (int)o.nreject;
@@ -245,10 +247,33 @@ __global__ __launch_bounds__(LB) void learn_logistic_kernel(const double* __rest
            stage_lds + (size_t)(threadIdx.x >> 6) * (4 * kStageSlots * 64) + (threadIdx.x & 63), 0, 0, 0, 0,
            0, L.lim, -1, 0.0, -INFINITY, ETA,
            0, 0, a.stop_after_eta != 0 ? 1 : 0, st, fuse ? 1 : 0, 0, BETA, a.lam, a.p, 0.0, 0.0, 0.0, 0.0,
-           &L, &a, b};
+           &L, &a, b, 0};
     LogisticSys f{BETA};
     OdeOut o;
     ode_scalar(f, sink, T1, a.x0, a.rtol, a.atol, a.maxiters, o);
+    if (STAGE && a.fuse_hazard == 2 && a.wpg && (blk % a.wpg) >= a.head && sink.ntau_out > 0) {
+        // A tail wave (not a grid's head wave) normalises its columns' hazard rows itself once
+        // every lane has solved — hazard_norm_kernel's operation, the same bits.  The tail waves
+        // end long before the head waves that set the launch's length, so the pass (≈1 ms of
+        // latency-bound loads per lane) is hidden; the head waves' columns are left to a small
+        // hazard_norm_kernel launch after the learning (LearnArgs::part 1).  Eight entries per
+        // round keep eight loads of each row in flight.
+        double* __restrict__ H = L.hr + row;
+        const double* __restrict__ HI = L.hrI + row;
+        const int nt = sink.ntau_out;
+        const double p = a.p, omp = 1.0 - p, ie = HI[nt - 1];
+        for (int i0 = 0; i0 < nt; i0 += 8) {
+            double h[8], q[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                h[k] = i0 + k < nt ? H[i0 + k] : 0.0;
+                q[k] = i0 + k < nt ? HI[i0 + k] : 0.0;
+            }
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+                if (i0 + k < nt) H[i0 + k] = h[k] / ((p * q[k]) + (omp * ie));
+        }
+    }
     }
 }
 
@@ -259,7 +284,10 @@ __global__ __launch_bounds__(LB) void learn_logistic_kernel(const double* __rest
 constexpr int HN_BLOCK = 256, HN_UNROLL = 4;
 __global__ __launch_bounds__(HN_BLOCK) void hazard_norm_kernel(LearnArgs a, LearnBufs L)
 {
-    const int b = blockIdx.x;
+    // a.part == 1: only the columns of each grid's head waves (the rest normalised by their
+    // learning waves, learn_logistic_kernel with fuse_hazard 2): block → grid's head column
+    const int hc = 64 * a.head;
+    const int b = a.part == 1 ? (int)(blockIdx.x / hc) * 64 * a.wpg + (int)(blockIdx.x % hc) : (int)blockIdx.x;
     const int nt = L.n_tau[b];
     if (nt <= 0) return;
     const size_t row = (size_t)b * (size_t)L.cap;

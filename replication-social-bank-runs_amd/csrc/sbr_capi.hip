@@ -1033,14 +1033,26 @@ int sbr_sweep_baseline_batch_dev(sbr_ctx* c, void* stream, int64_t n_batch, cons
                 la.head = 1;
                 la.wpg = (int32_t)(n_beta / 64);
             }
+            // the staged heads-first launch normalises its tail waves' hazard rows itself; one small
+            // hazard_norm_kernel launch takes the head waves' columns (no normalisation launches
+            // beside the first equilibrium launch)
+            const bool norm_in_learn = lmode == 2 && la.wpg;
+            if (norm_in_learn) la.fuse_hazard = 2;
             HIP_TRY(c, sbr::launch_learn_kernel(beta + g0 * n_beta, eta + g0 * n_beta, t_end + g0 * n_beta, la, W, ls,
                                                 lmode), SBR_EDEVICE);
             tend(c, ls, 0, t0);
+            if (norm_in_learn) {
+                sbr::LearnArgs lh = la;
+                lh.part = 1;
+                HIP_TRY(c, sbr::launch_hazard_norm(lh, W, (int)(gn * 64 * la.head), ls), SBR_EDEVICE);
+            }
             HIP_TRY(c, hipEventRecord(c->ev_learned[slot], ls), SBR_EDEVICE);
-            HIP_TRY(c, hipStreamWaitEvent(hs, c->ev_learned[slot], 0), SBR_EDEVICE);
-            // the group's equilibria in launches of E grids (balanced), each after the hazard
-            // normalisation of its own columns: the normalisations (HBM streams) run ahead on hs,
-            // overlapped with the previous equilibrium launch; only the first one is exposed
+            if (norm_in_learn) HIP_TRY(c, hipStreamWaitEvent(es, c->ev_learned[slot], 0), SBR_EDEVICE);
+            else HIP_TRY(c, hipStreamWaitEvent(hs, c->ev_learned[slot], 0), SBR_EDEVICE);
+            // the group's equilibria in launches of E grids (balanced).  Without the learning
+            // kernel's own normalisation each launch follows a hazard_norm_kernel launch for its
+            // columns on hs, run ahead and overlapped with the previous equilibrium launch — all of
+            // them beside the first one, which they slowed from 2.28 to 2.71 ms (20 grids)
             const int64_t ne = (gn + P.E - 1) / P.E, Eg = (gn + ne - 1) / ne;
             // timing (sbr_timing_enable): one span over the group's equilibrium launches, from
             // the first one's start to the last one's end, counted as ne launches — two timing
@@ -1050,10 +1062,12 @@ int sbr_sweep_baseline_batch_dev(sbr_ctx* c, void* stream, int64_t n_batch, cons
                 const int64_t en = (gn - e0) < Eg ? (gn - e0) : Eg;
                 const sbr::LearnBufs We = learn_rows(W, (size_t)(e0 * n_beta));
                 const int64_t gg = g0 + e0;
-                HIP_TRY(c, sbr::launch_hazard_norm(la, We, (int)(en * n_beta), hs), SBR_EDEVICE);
-                hipEvent_t eh = c->ev_hn[(size_t)k_hn++];
-                HIP_TRY(c, hipEventRecord(eh, hs), SBR_EDEVICE);
-                HIP_TRY(c, hipStreamWaitEvent(es, eh, 0), SBR_EDEVICE);
+                if (!norm_in_learn) {
+                    HIP_TRY(c, sbr::launch_hazard_norm(la, We, (int)(en * n_beta), hs), SBR_EDEVICE);
+                    hipEvent_t eh = c->ev_hn[(size_t)k_hn++];
+                    HIP_TRY(c, hipEventRecord(eh, hs), SBR_EDEVICE);
+                    HIP_TRY(c, hipStreamWaitEvent(es, eh, 0), SBR_EDEVICE);
+                }
                 if (e0 == 0) te = tstart(c, es);
                 // column i·n_beta + j of the launch is grid g0+e0+i's column j: eta / t_end and
                 // every out field are [n_batch × n_beta (× n_u)] contiguous

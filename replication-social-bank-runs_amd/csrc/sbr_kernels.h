@@ -27,7 +27,8 @@ struct LearnArgs {
     int64_t maxiters;
     int32_t n_beta;
     int32_t stop_after_eta;
-    int32_t fuse_hazard; // learn_logistic_kernel: stream hazard_rate with the knots (needs hrI)
+    int32_t fuse_hazard; // learn_logistic_kernel: stream hazard_rate with the knots (needs hrI); 2 (the
+                         // staged heads-first launch): the tail waves also normalise their rows
     // per-column readiness (single sweeps, null otherwise): the lane that finishes column b
     // takes slot k = atomicAdd(ready_tail, 1) and release-stores b + 1 into ready_q[k]
     int32_t* ready_tail;
@@ -39,6 +40,7 @@ struct LearnArgs {
     // wpg × 64, wpg > head): the first head waves of every grid take the launch's first blocks,
     // the other waves follow (0: block order = wave order)
     int32_t head = 0, wpg = 0;
+    int32_t part = 0; // hazard_norm_kernel: 1 = only the head waves' columns of each grid
 };
 
 // The equilibrium side of a readiness sweep (eq_ready_kernel): one workgroup per item, each
